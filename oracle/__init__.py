@@ -1,0 +1,99 @@
+"""TEST INFRASTRUCTURE ONLY -- the parity oracle.
+
+Python handle onto the event-replay oracle (oracle/replay.c):
+
+* ``Oracle("own")`` loads ``oracle/liboracle.so`` -- this repo's clean-room CPU
+  restatement of the reference queue layer (``src/xq.c``) and of the server
+  handlers in ``src/adlb.c``.  It is the checker used by ``tests/``,
+  ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg, and it is
+  the timed CPU baseline ("port").
+* ``Oracle("ref")`` loads ``oracle/_ref/libxqref.so`` -- the same replay layer
+  linked against the reference's own ``/root/reference/src/xq.c``.  It exists only
+  in the build container and is used to generate/pin ``tests/golden``.
+
+Nothing in ``adlb_amd/`` may import this package: the product path is the HIP
+library and must fail loudly if it is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBS = {
+    "own": os.path.join(HERE, "liboracle.so"),
+    "ref": os.path.join(HERE, "_ref", "libxqref.so"),
+}
+
+OP_PUT, OP_RESERVE, OP_GET, OP_UNRESERVE, OP_QMROW, OP_SETROW = 1, 2, 3, 4, 5, 6
+OP_CHECKREM, OP_RFRDONE, OP_TQADD, OP_PUSHSEL, OP_INFO, OP_RQDEL, OP_INFOTYPE = 7, 8, 9, 10, 11, 12, 13
+
+
+def build(ref: bool = False) -> None:
+    """Compile the oracle (and, when /root/reference exists, the reference build)."""
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+    if ref and os.path.isdir("/root/reference/src"):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def available(kind: str = "own") -> bool:
+    return os.path.exists(LIBS[kind])
+
+
+class Oracle:
+    """One ADLB server's queue state replayed on the CPU (single instance per
+    process for the "ref" kind, since the reference keeps its queues in globals)."""
+
+    def __init__(self, kind: str = "own"):
+        path = LIBS[kind]
+        if not os.path.exists(path):
+            if kind == "own":
+                build()
+            else:
+                raise FileNotFoundError(f"{path} missing (make -C oracle ref)")
+        self.kind = kind
+        self.lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        self.lib.orc_init.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int]
+        self.lib.orc_replay.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p,
+                                        ctypes.c_long]
+        self.lib.orc_replay.restype = ctypes.c_long
+
+    def init(self, user_types, num_app_ranks: int, num_servers: int = 1, my_server_idx: int = 0):
+        ut = np.ascontiguousarray(np.asarray(user_types, dtype=np.int32))
+        self.ntypes = len(ut)
+        self._ut = ut
+        rc = self.lib.orc_init(len(ut), ut.ctypes.data, num_app_ranks, num_servers, my_server_idx)
+        assert rc == 0
+
+    def replay(self, trace) -> np.ndarray:
+        tr = np.ascontiguousarray(np.asarray(trace, dtype=np.int32))
+        cap = output_bound(tr, self.ntypes)
+        out = np.empty(cap, dtype=np.int32)
+        n = self.lib.orc_replay(tr.ctypes.data, tr.size, out.ctypes.data, cap)
+        if n < 0:
+            raise ValueError(f"oracle: malformed trace or output overflow (rc={n})")
+        return out[:n].copy()
+
+
+def event_nargs(op: int, ntypes: int) -> int:
+    return {OP_PUT: 9, OP_RESERVE: 18, OP_GET: 2, OP_UNRESERVE: 3, OP_QMROW: 0,
+            OP_SETROW: 3 + ntypes, OP_CHECKREM: 0, OP_RFRDONE: 2, OP_TQADD: 3,
+            OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1, OP_INFOTYPE: 1}[op]
+
+
+def output_bound(tr: np.ndarray, ntypes: int) -> int:
+    """Upper bound on replay output ints (the replay mutates state, so the buffer
+    must be big enough the first time)."""
+    ip, n_res, n_chk, n_ev = 0, 0, 0, 0
+    trl = tr.tolist()
+    while ip < len(trl):
+        op = trl[ip]
+        ip += 1 + event_nargs(op, ntypes)
+        n_ev += 1
+        n_res += op == OP_RESERVE
+        n_chk += op in (OP_CHECKREM, OP_TQADD)
+    return 1024 + n_ev * (2 + max(12, ntypes + 1)) + n_chk * (1 + 3 * n_res)

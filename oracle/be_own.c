@@ -1,0 +1,308 @@
+/*
+ * oracle/be_own.c -- TEST INFRASTRUCTURE ONLY.  Clean-room CPU restatement of
+ * the reference's queue layer (src/xq.c) used as the parity oracle and as the
+ * timed CPU baseline ("port") in bench.py.  Not part of the product: the
+ * product path is adlb_amd/csrc (HIP), which must never call into this file.
+ *
+ * Faithfulness notes (what is kept on purpose):
+ *   - storage is a circular doubly-linked list with a sentinel, one list-link
+ *     allocation plus one separately allocated record per entry, so a scan
+ *     chases two dependent pointers per entry like xq.c:17-110 does;
+ *   - every scan walks from the head in append order; the best-so-far is
+ *     replaced only on a strictly greater priority, starting from
+ *     ADLB_LOWEST_PRIO, so ties go to the earliest entry and entries whose
+ *     priority is <= ADLB_LOWEST_PRIO are never returned (xq.c:190-247);
+ *   - a request type of -1 matches every work type, any other value matches
+ *     by equality (so -2 padding never matches a real type)  (xq.c:205,235);
+ *   - count/max_count follow xq_insert_after/xq_delete (xq.c:42-79).
+ */
+#include <stdlib.h>
+#include <string.h>
+#include "be.h"
+
+typedef struct link {
+    struct link *fwd, *back;
+    void *rec;
+} link_t;
+
+typedef struct chain {
+    link_t head; /* sentinel; head.fwd is the oldest entry */
+    int n, n_hwm;
+} chain_t;
+
+typedef struct unit_rec {
+    int target_rank, pin_rank, pinned, work_type, work_prio, work_len;
+    int answer_rank, wqseqno, home_server_rank;
+    int common_len, common_server_rank, common_server_commseqno;
+} unit_rec;
+
+typedef struct park_rec {
+    int world_rank, rqseqno;
+    int types[ORC_REQ_TYPES];
+} park_rec;
+
+typedef struct remote_rec {
+    int app_rank, work_type, remote_server_rank, num_stored;
+} remote_rec;
+
+static chain_t units, parked, remotes;
+
+static void chain_clear(chain_t *c)
+{
+    link_t *l = c->head.fwd;
+    while (l && l != &c->head) {
+        link_t *nx = l->fwd;
+        free(l->rec);
+        free(l);
+        l = nx;
+    }
+    c->head.fwd = c->head.back = &c->head;
+    c->n = c->n_hwm = 0;
+}
+
+static link_t *chain_push_back(chain_t *c, void *rec)
+{
+    link_t *l = (link_t *)malloc(sizeof *l);
+    l->rec = rec;
+    l->back = c->head.back;
+    l->fwd = &c->head;
+    c->head.back->fwd = l;
+    c->head.back = l;
+    if (++c->n > c->n_hwm)
+        c->n_hwm = c->n;
+    return l;
+}
+
+static void chain_unlink(chain_t *c, link_t *l)
+{
+    l->back->fwd = l->fwd;
+    l->fwd->back = l->back;
+    c->n--;
+    free(l->rec);
+    free(l);
+}
+
+#define FOR_EACH(c, l) for (link_t *l = (c).head.fwd; l != &(c).head; l = l->fwd)
+
+static int wants(const int *types16, int work_type)
+{
+    for (int i = 0; i < ORC_REQ_TYPES; i++)
+        if (types16[i] == -1 || types16[i] == work_type)
+            return 1;
+    return 0;
+}
+
+void be_reset(void)
+{
+    static int inited;
+    if (!inited) {
+        units.head.fwd = units.head.back = &units.head;
+        parked.head.fwd = parked.head.back = &parked.head;
+        remotes.head.fwd = remotes.head.back = &remotes.head;
+        inited = 1;
+    }
+    chain_clear(&units);
+    chain_clear(&parked);
+    chain_clear(&remotes);
+}
+
+void *be_wq_add(int type, int prio, int seqno, int answer, int target, int len,
+                int home, int clen, int csrv, int cseq)
+{
+    unit_rec *u = (unit_rec *)malloc(sizeof *u);
+    u->work_type = type;
+    u->work_prio = prio;
+    u->wqseqno = seqno;
+    u->answer_rank = answer;
+    u->target_rank = target;
+    u->work_len = len;
+    u->home_server_rank = home;
+    u->pin_rank = -1;
+    u->pinned = 0;
+    u->common_len = clen;
+    u->common_server_rank = csrv;
+    u->common_server_commseqno = cseq;
+    return chain_push_back(&units, u);
+}
+
+/* best (prio desc, first-in-list) unpinned unit of one target segment:
+ * untargeted != 0 selects units with target_rank < 0 (xq.c:201), otherwise
+ * units whose target_rank equals `target` (xq.c:231) */
+static void *best_in_segment(int untargeted, int target, const int *types16)
+{
+    link_t *best = NULL;
+    int best_prio = ORC_LOWEST_PRIO;
+    FOR_EACH(units, l) {
+        const unit_rec *u = (const unit_rec *)l->rec;
+        if (u->pinned)
+            continue;
+        if (untargeted ? u->target_rank >= 0 : u->target_rank != target)
+            continue;
+        if (u->work_prio > best_prio && wants(types16, u->work_type)) {
+            best_prio = u->work_prio;
+            best = l;
+        }
+    }
+    return best;
+}
+
+void *be_wq_find_pre_targeted_hi_prio(int rank, const int *types16)
+{
+    return best_in_segment(0, rank, types16);
+}
+
+void *be_wq_find_hi_prio(const int *types16)
+{
+    return best_in_segment(1, -1, types16);
+}
+
+void *be_wq_find_pinned_for_rank(int rank, int seqno)
+{
+    FOR_EACH(units, l) {
+        const unit_rec *u = (const unit_rec *)l->rec;
+        if (u->pin_rank == rank && u->wqseqno == seqno)
+            return l;
+    }
+    return NULL;
+}
+
+void *be_wq_find_unpinned(void)
+{
+    FOR_EACH(units, l) {
+        if (!((const unit_rec *)l->rec)->pinned)
+            return l;
+    }
+    return NULL;
+}
+
+int be_wq_num_unpinned_untargeted(void)
+{
+    int n = 0;
+    FOR_EACH(units, l) {
+        const unit_rec *u = (const unit_rec *)l->rec;
+        n += (!u->pinned && u->target_rank < 0);
+    }
+    return n;
+}
+
+int be_wq_avail_hi_prio_of_type(int type)
+{
+    int hi = ORC_LOWEST_PRIO;
+    FOR_EACH(units, l) {
+        const unit_rec *u = (const unit_rec *)l->rec;
+        if (u->pinned || u->target_rank >= 0)
+            continue;
+        if (u->work_type == type && u->work_prio > hi)
+            hi = u->work_prio;
+    }
+    return hi;
+}
+
+void be_wq_view(void *h, be_unit_view *v)
+{
+    const unit_rec *u = (const unit_rec *)((link_t *)h)->rec;
+    v->target_rank = u->target_rank;
+    v->pin_rank = u->pin_rank;
+    v->pinned = u->pinned;
+    v->work_type = u->work_type;
+    v->work_prio = u->work_prio;
+    v->work_len = u->work_len;
+    v->answer_rank = u->answer_rank;
+    v->wqseqno = u->wqseqno;
+    v->home_server_rank = u->home_server_rank;
+    v->common_len = u->common_len;
+    v->common_server_rank = u->common_server_rank;
+    v->common_server_commseqno = u->common_server_commseqno;
+}
+
+void be_wq_set_pin(void *h, int pin_rank, int pinned)
+{
+    unit_rec *u = (unit_rec *)((link_t *)h)->rec;
+    u->pin_rank = pin_rank;
+    u->pinned = pinned;
+}
+
+void be_wq_delete(void *h) { chain_unlink(&units, (link_t *)h); }
+int be_wq_count(void) { return units.n; }
+int be_wq_max_count(void) { return units.n_hwm; }
+void *be_wq_first(void) { return units.head.fwd == &units.head ? NULL : units.head.fwd; }
+void *be_wq_next(void *h)
+{
+    link_t *l = ((link_t *)h)->fwd;
+    return l == &units.head ? NULL : l;
+}
+
+void *be_rq_add(int rank, const int *types16, int rqseqno)
+{
+    park_rec *p = (park_rec *)malloc(sizeof *p);
+    p->world_rank = rank;
+    p->rqseqno = rqseqno;
+    memcpy(p->types, types16, sizeof p->types);
+    return chain_push_back(&parked, p);
+}
+
+void *be_rq_find_rank_queued_for_type(int rank, int type)
+{
+    FOR_EACH(parked, l) {
+        const park_rec *p = (const park_rec *)l->rec;
+        if (rank != -1 && rank != p->world_rank)
+            continue;
+        for (int i = 0; i < ORC_REQ_TYPES; i++)
+            if (type == -1 || p->types[i] == -1 || p->types[i] == type)
+                return l;
+    }
+    return NULL;
+}
+
+void *be_rq_find_seqno(int rqseqno)
+{
+    FOR_EACH(parked, l) {
+        if (((const park_rec *)l->rec)->rqseqno == rqseqno)
+            return l;
+    }
+    return NULL;
+}
+
+void *be_rq_first(void) { return parked.head.fwd == &parked.head ? NULL : parked.head.fwd; }
+void *be_rq_next(void *h)
+{
+    link_t *l = ((link_t *)h)->fwd;
+    return l == &parked.head ? NULL : l;
+}
+
+void be_rq_view(void *h, int *rank, int *rqseqno, int *types16)
+{
+    const park_rec *p = (const park_rec *)((link_t *)h)->rec;
+    *rank = p->world_rank;
+    *rqseqno = p->rqseqno;
+    memcpy(types16, p->types, sizeof p->types);
+}
+
+void be_rq_delete(void *h) { chain_unlink(&parked, (link_t *)h); }
+int be_rq_count(void) { return parked.n; }
+
+int be_tq_find_first_rt(int rank, int type)
+{
+    FOR_EACH(remotes, l) {
+        const remote_rec *r = (const remote_rec *)l->rec;
+        if (r->app_rank == rank && (type == -1 || type == r->work_type))
+            return r->remote_server_rank;
+    }
+    return -1;
+}
+
+int be_tq_bump_or_add(int rank, int type, int server)
+{
+    FOR_EACH(remotes, l) {
+        remote_rec *r = (remote_rec *)l->rec;
+        if (r->app_rank == rank && r->work_type == type && r->remote_server_rank == server)
+            return ++r->num_stored;
+    }
+    remote_rec *r = (remote_rec *)malloc(sizeof *r);
+    r->app_rank = rank;
+    r->work_type = type;
+    r->remote_server_rank = server;
+    r->num_stored = 1;
+    chain_push_back(&remotes, r);
+    return 1;
+}

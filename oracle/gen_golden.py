@@ -1,0 +1,145 @@
+"""TEST INFRASTRUCTURE ONLY -- generate tests/golden/*.npz from the REFERENCE.
+
+Run in the build container (needs /root/reference and MPICH):
+
+    make -C oracle ref && python oracle/gen_golden.py
+
+Every fixture is (server configuration, int32 event trace, expected int32
+output stream) where the expected stream is produced by oracle/_ref/libxqref.so,
+i.e. the replay layer (oracle/replay.c) running on the reference's own
+src/xq.c.  Fixtures are data only: no reference source is stored.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import oracle  # noqa: E402
+from adlb_amd import synth  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+P, R, G, U = synth.OP_PUT, synth.OP_RESERVE, synth.OP_GET, synth.OP_UNRESERVE
+LOW = synth.LOWEST_PRIO
+
+
+def rv(*types):
+    t = list(types) + [-2] * (16 - len(types))
+    return t
+
+
+def put(t, prio, target=-1, answer=0, ln=8):
+    return [P, t, prio, answer, target, ln, -1, 0, -1, -1]
+
+
+def res(rank, types, hang=1):
+    return [R, rank, hang] + rv(*types)
+
+
+def edge_cases():
+    """Known-answer cases T1-T10, each its own small trace."""
+    cases = {}
+    # T1 priority tie -> lower seqno
+    cases["t01_tie_seqno"] = put(0, 5) + put(0, 5) + put(0, 5) + res(0, [0]) + res(1, [0]) + res(2, [0])
+    # T2 wildcard takes highest prio and skips targeted
+    cases["t02_wildcard"] = (put(0, 3) + put(1, 9) + put(2, 100, target=5) + put(2, 7)
+                             + res(0, [-1]) + res(1, [-1]) + res(2, [-1]) + res(3, [-1], hang=0))
+    # T3 pre-targeted unit wins although lower prio
+    cases["t03_pretargeted"] = (put(0, 100) + put(0, 1, target=4) + put(1, 50, target=4)
+                                + res(4, [0]) + res(4, [0, 1]) + res(4, [0]) + res(3, [0]))
+    # T4 multi-type requests
+    cases["t04_multitype"] = (put(0, 1) + put(1, 2) + put(2, 3) + put(3, 4) + put(1, 9)
+                              + res(0, [0, 1]) + res(1, [2, 0]) + res(2, [3, 2, 1]) + res(3, [0, 3])
+                              + res(4, [1, 2, 3, 0]))
+    # T5 pinned units are skipped; unreserve makes them available again
+    cases["t05_pinned"] = (put(0, 10) + put(0, 9) + res(0, [0]) + res(1, [0]) + res(2, [0], 0)
+                           + [U, 0, 1, -1] + res(2, [0]) + [G, 1, 2] + [G, 1, 2])
+    # T6 LOWEST_PRIO-only queue gives no match (but counts in qlen)
+    cases["t06_lowest"] = (put(0, LOW) + put(0, LOW) + put(1, LOW + 1) + res(0, [0], 0)
+                           + res(1, [-1], 0) + [synth.OP_QMROW] + res(2, [1], 0) + [synth.OP_QMROW])
+    # T7 avail-hi-prio and count semantics (pinned and targeted excluded)
+    cases["t07_qmrow"] = (put(0, 5) + put(0, 7, target=2) + put(1, -3) + put(1, 11) + put(2, LOW)
+                          + [synth.OP_QMROW] + res(0, [1]) + [synth.OP_QMROW] + res(2, [0])
+                          + [synth.OP_QMROW] + [synth.OP_INFOTYPE, 0, synth.OP_INFOTYPE, 2,
+                                                synth.OP_INFO])
+    # T8 rq FIFO put-side match
+    cases["t08_rq_fifo"] = (res(0, [1]) + res(1, [0]) + res(2, [0, 1]) + res(3, [0])
+                            + put(0, 1) + put(0, 1) + put(1, 1) + put(0, 1) + [synth.OP_INFO])
+    # T9 wildcard parked request matches any put
+    cases["t09_rq_wild"] = res(5, [-1]) + res(6, [3]) + put(2, 1) + put(3, 1) + put(3, 1)
+    # T10 targeted put matches only that rank's parked entry
+    cases["t10_rq_targeted"] = (res(1, [0]) + res(2, [0]) + put(0, 1, target=2) + put(0, 1, target=7)
+                                + put(0, 1) + res(7, [0]) + [synth.OP_INFO])
+    # T11 Ireserve (hang=0) on empty queue -> NO_CURR_WORK, not parked
+    cases["t11_nohang"] = res(0, [0], 0) + res(1, [-1], 0) + [synth.OP_INFO] + put(0, 1) + res(2, [0], 0)
+    # T12 get failure and removal path
+    cases["t12_get"] = (put(0, 4) + put(1, 4) + res(3, [0, 1]) + [G, 2, 1] + [G, 3, 1] + [G, 3, 1]
+                        + res(3, [-1]) + [G, 3, 2] + [synth.OP_INFO])
+    return {k: np.asarray(v, np.int32) for k, v in cases.items()}
+
+
+def donor_case(T=3):
+    """Donor selection: qmstat rows + tq + rfr_out throttling (adlb.c:3487-3579)."""
+    ev = []
+    # parked requests on an empty local queue
+    ev += res(0, [0]) + res(1, [1, 2]) + res(2, [-1]) + res(3, [2]) + res(4, [0, 1])
+    # remote rows (servers 1..3): qlen, nbytes, hi_prio[T]
+    ev += [synth.OP_SETROW, 1, 3, 1000, 10, 20, LOW]
+    ev += [synth.OP_SETROW, 2, 0, 500, 99, 99, 99]           # qlen 0: never a donor
+    ev += [synth.OP_SETROW, 3, 2, 2000, 10, 25, 30]
+    ev += [synth.OP_CHECKREM]
+    ev += [synth.OP_RFRDONE, 5 + 1, 0, synth.OP_RFRDONE, 5 + 3, 1]
+    ev += [synth.OP_TQADD, 3, 2, 5 + 2]                      # tq: rank 3's type 2 lives on server 2
+    ev += [synth.OP_CHECKREM]
+    ev += [synth.OP_PUSHSEL, 1500, synth.OP_PUSHSEL, 100]
+    ev += put(0, 1) + put(0, 2) + put(0, 3) + put(0, 4) + put(0, 5) + put(0, 6)
+    ev += [synth.OP_PUSHSEL, 1500, synth.OP_PUSHSEL, 100, synth.OP_PUSHSEL, 501, synth.OP_INFO]
+    ev += res(3, [0]) + [synth.OP_CHECKREM] + [synth.OP_SETROW, 2, 4, 10, 1, 1, 1, synth.OP_CHECKREM]
+    return np.asarray(ev, np.int32)
+
+
+def save(name, user_types, num_app_ranks, num_servers, my_idx, trace):
+    o = oracle.Oracle("ref")
+    o.init(user_types, num_app_ranks, num_servers, my_idx)
+    exp = o.replay(trace)
+    np.savez_compressed(os.path.join(OUT, name + ".npz"),
+                        user_types=np.asarray(user_types, np.int32),
+                        cfg=np.asarray([num_app_ranks, num_servers, my_idx], np.int32),
+                        trace=trace.astype(np.int32), expected=exp.astype(np.int32))
+    print(f"{name:28s} events-ints={trace.size:8d} out-ints={exp.size:8d}")
+
+
+def main():
+    oracle.build(ref=True)
+    os.makedirs(OUT, exist_ok=True)
+    for name, tr in edge_cases().items():
+        save(name, [0, 1, 2, 3], 8, 1, 0, tr)
+    save("t13_donor", [0, 1, 2], 5, 4, 0, donor_case())
+    # config 2 at reduced scale, three variants
+    w = synth.config2(n_units=20_000, n_reserves=4096, seed=21)
+    save("c2_n20k_r4k", w.user_types, w.num_app_ranks, 1, 0, synth.workload_trace(w))
+    w = synth.config2(n_units=20_000, n_reserves=4096, seed=22, equal_prio=True)
+    save("c2_eqprio_n20k_r4k", w.user_types, w.num_app_ranks, 1, 0, synth.workload_trace(w))
+    w = synth.config2(n_units=3_000, n_reserves=4096, seed=23, hang=0)
+    save("c2_exhaust_nohang", w.user_types, w.num_app_ranks, 1, 0, synth.workload_trace(w))
+    w = synth.config2(n_units=3_000, n_reserves=4096, seed=24, hang=1, prio_hi=8)
+    tr = np.concatenate([synth.workload_trace(w), synth.put_events(synth.config2(
+        n_units=2000, n_reserves=0, seed=25, prio_hi=8))])
+    save("c2_exhaust_park_then_puts", w.user_types, w.num_app_ranks, 1, 0, tr)
+    # config 4 at reduced scale (32 types, 80% targeted over 64 ranks)
+    w = synth.config4(n_units=30_000, n_reserves=2048, n_ranks=64, seed=41)
+    save("c4_n30k_r2k", w.user_types, w.num_app_ranks, 1, 0, synth.workload_trace(w))
+    # config 5 stream, driven by the reference itself
+    o = oracle.Oracle("ref")
+    o.init([1, 2], 64, 4, 0)
+    tr = synth.config5_stream(lambda ev: synth.split_outputs(o.replay(ev)), n_rounds=300,
+                              n_ranks=64, n_servers=4, seed=51)
+    save("c5_stream", [1, 2], 64, 4, 0, tr)
+
+
+if __name__ == "__main__":
+    main()

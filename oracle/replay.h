@@ -1,0 +1,43 @@
+/*
+ * oracle/replay.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Event-trace replay of one ADLB server's queue handlers.  A trace is a flat
+ * int32 stream of events; each event starts with an opcode followed by a fixed
+ * number of arguments.  Replaying writes, per event, [n, v1 .. vn] to the output
+ * stream.  The same trace/output format is produced by the product's C ABI
+ * replayer (adlb_amd/replay.py), so parity is a byte comparison.
+ *
+ * Event semantics restate the reference server loop (src/adlb.c) handler by
+ * handler; see replay.c for the line citations.
+ */
+#ifndef ADLBQ_ORACLE_REPLAY_H
+#define ADLBQ_ORACLE_REPLAY_H
+
+enum {
+    ORC_OP_PUT = 1,       /* type prio answer target len home clen csrv cseq   -> [wqseqno, matched_rank, matched_rqseqno] */
+    ORC_OP_RESERVE = 2,   /* rank hang t0..t15                                  -> resp[12] */
+    ORC_OP_GET = 3,       /* rank wqseqno                                       -> [rc, len, type, prio, answer] */
+    ORC_OP_UNRESERVE = 4, /* rank wqseqno new_pin_rank                          -> [found] */
+    ORC_OP_QMROW = 5,     /*                                                    -> [qlen_unpin_untarg, hi_prio[T]] */
+    ORC_OP_SETROW = 6,    /* server_idx qlen nbytes hi_prio[T]                  -> [] */
+    ORC_OP_CHECKREM = 7,  /*                                                    -> [k, (rqseqno, rank, cand) * k] */
+    ORC_OP_RFRDONE = 8,   /* from_server_rank for_rank                          -> [] */
+    ORC_OP_TQADD = 9,     /* app_rank type server_rank                          -> like CHECKREM */
+    ORC_OP_PUSHSEL = 10,  /* threshold                                          -> [cand_server_rank, wqseqno] */
+    ORC_OP_INFO = 11,     /*                                                    -> [wq_count, wq_max_count, rq_count] */
+    ORC_OP_RQDEL = 12,    /* rqseqno                                            -> [found] */
+    ORC_OP_INFOTYPE = 13, /* type                                               -> [max_prio, num_max_prio, num_type] */
+};
+
+/* TA_RESERVE_RESP layout (adlb.c:1213-1222), plus two slots this build uses
+ * for the parked case: [10] = rqseqno of the parked request, [11] = server
+ * rank an SS_RFR was sent to (-1 if none). resp[0]: 1 = SUCCESS,
+ * -2 = NO_CURR_WORK, 0 = parked on rq (no reply sent yet). */
+#define ORC_RESP_INTS 12
+
+int  orc_init(int ntypes, const int *user_types, int num_app_ranks, int num_servers,
+              int my_server_idx);
+long orc_replay(const int *trace, long ntrace, int *out, long outcap);
+int  orc_event_nargs(int op, int ntypes);
+
+#endif
