@@ -1,0 +1,176 @@
+// adlbq_impl.h -- internal state and device helpers of the MI355X ADLB queue engine.
+//
+// HBM layout (one handle = one ADLB server's queues):
+//   * Work units live in fixed pages of PAGE slots.  Every page belongs to one
+//     *bucket*: the open bucket (untargeted units, target_rank < 0) or the
+//     bucket of one target app rank.  Within a bucket, pages are chained in
+//     allocation order and slots are filled in order, so bucket order ==
+//     wqseqno order (the reference's append order, xq.c:155-158).
+//   * Per-slot structure of arrays: prio (i32), meta (u32: type index | LIVE |
+//     PINNED), pin_rank (i32), wqseqno (i32), cold fields (2 x int4, read only
+//     for matched units).  The matching scans read prio + meta = 8 B per unit;
+//     type and target are implicit in (meta, bucket).
+//   * Parked Reserves (rq) are indexed by rqseqno-1 (append-only, FIFO order).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+#include <unordered_map>
+
+#include "adlbq.h"
+
+namespace adlbq {
+
+constexpr int PAGE_SHIFT = 12;
+constexpr int PAGE = 1 << PAGE_SHIFT;       // 4096 slots per page
+constexpr int NB = 64;                      // histogram bins per type (distance from anchor)
+constexpr int NBX = 32;                     // bins [0, NBX) are exact (one priority value each)
+constexpr int CHUNK = 16;                   // pages per prefix chunk in the open-bucket scan
+constexpr int LOWEST = ADLBQ_LOWEST_PRIO;
+constexpr uint32_t M_TYPE = 0xffu;
+constexpr uint32_t M_LIVE = 1u << 8;
+constexpr uint32_t M_PINNED = 1u << 9;
+constexpr int NREQ = ADLBQ_REQ_TYPES;
+
+// device-side scalar counters shared by kernels and read back lazily by the host
+struct DevCounters {
+    int rq_n;          // rq slots used (== next_rqseqno - 1)
+    int rq_live;       // parked entries alive
+    int rq_hwm;        // rq->max_count
+    int rq_head;       // lowest rq slot that may be alive
+    int n_parked_last; // parked by the last reserve batch
+    int pad[3];
+};
+
+struct Bucket {
+    std::vector<int> pages;  // page ids in order
+    int tail_fill = PAGE;    // slots used in the last page (PAGE when no page yet)
+};
+
+struct StageTimer {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    double total_ms = 0;
+    long long launches = 0;
+};
+
+}  // namespace adlbq
+
+struct adlbq_server {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+
+    int T = 0;
+    std::vector<int> utypes;
+    std::unordered_map<int, int> tindex;
+    int A = 0, S = 1, my_idx = 0, my_world = 0, master = 0, num_world = 0;
+
+    // ---- unit store
+    int cap_pages = 0;   // allocated pages
+    int n_pages = 0;     // pages handed out
+    int *d_prio = nullptr;
+    uint32_t *d_meta = nullptr;
+    int *d_pin = nullptr;
+    int *d_seq = nullptr;
+    int4 *d_cold0 = nullptr;  // answer_rank, work_len, home_server_rank, common_len
+    int4 *d_cold1 = nullptr;  // common_server_rank, common_seqno, user work_type, target_rank
+    adlbq::Bucket open;
+    std::vector<adlbq::Bucket> rankb;     // per target app rank
+    std::vector<int> bucket_ranks;        // ranks that own a bucket, in creation order
+    std::unordered_map<int, int> rank_index;  // target rank -> index into rankb
+    bool tables_dirty = true;
+    int *d_open_pages = nullptr;  int cap_open_pages = 0;
+    int *d_rank_pages = nullptr;  int cap_rank_pages = 0;   // CSR over bucket_ranks
+    int *d_rank_pstart = nullptr; int cap_rank_pstart = 0;
+    int *d_rank_fill = nullptr;   int cap_rank_fill = 0;
+    int *d_bucket_ranks = nullptr; int cap_bucket_ranks = 0;
+    int *d_all_pages = nullptr;   int cap_all_pages = 0;    // every page, with fills
+    int *d_all_fill = nullptr;    int cap_all_fill = 0;
+
+    // wqseqno -> slot (host mirror for single-event calls, device copy for batches)
+    int next_wqseqno = 1;
+    std::vector<long long> seq2slot;  // index wqseqno
+    long long *d_seq2slot = nullptr; long long cap_seq = 0;
+    long long live_units = 0, max_count = 0, live_targeted = 0;
+    std::vector<long long> anchor;    // per type: max prio ever put (upper bound of live max)
+    long long *d_anchor = nullptr; bool anchor_dirty = true;
+    int *d_utypes = nullptr;
+
+    // ---- parked reserves
+    int rq_cap = 0;
+    int *d_rq_rank = nullptr, *d_rq_types = nullptr, *d_rq_live = nullptr;
+    adlbq::DevCounters *d_ctr = nullptr;
+    adlbq::DevCounters ctr{};      // host copy
+    bool ctr_stale = false;
+    int rq_n_upper = 0;            // upper bound on rq_n while ctr is stale
+
+    // ---- qmstat / donor selection
+    std::vector<int> qm_hi, qm_qlen;
+    std::vector<double> qm_bytes;
+    int *d_qm_hi = nullptr, *d_qm_qlen = nullptr; bool qm_dirty = true;
+    int *d_rfr_out = nullptr, *d_rfr_to_rank = nullptr;
+    std::vector<int> tq;           // 4 ints per entry: app_rank, work_type, server_rank, num_stored
+    int *d_tq = nullptr; int cap_tq = 0; bool tq_dirty = true;
+
+    // ---- reserve-batch scratch
+    int cap_req = 0;
+    unsigned long long *d_mask = nullptr;
+    int *d_tmatch = nullptr, *d_umatch = nullptr;
+    int *d_reqbuf = nullptr, *d_respbuf = nullptr;  // host-API staging
+    int *d_dem = nullptr;              // [T]
+    int *d_theta = nullptr;            // [T] threshold bin (-1 none)
+    int *d_need = nullptr;             // [T]
+    int *d_candoff = nullptr, *d_candlen = nullptr, *d_needsort = nullptr;  // [T]
+    int *d_binoff = nullptr;           // [T*NB]
+    unsigned short *d_gh = nullptr; long long cap_gh = 0;   // [open pages][T*NB]
+    unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] -> exclusive prefix in place
+    unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
+    int *d_cslot = nullptr, *d_cslot2 = nullptr;
+    int *d_result = nullptr;           // small result scratch (16 ints)
+    int *h_result = nullptr;           // pinned host mirror
+    long long last_scan_units = 0;
+
+    bool profiling = false;
+    std::unordered_map<std::string, adlbq::StageTimer> timers;
+};
+
+namespace adlbq {
+
+int fail(int code, const char *msg);
+int hip_fail(hipError_t e, const char *where);
+#define AQ_HIP(call)                                     \
+    do {                                                 \
+        hipError_t _e = (call);                          \
+        if (_e != hipSuccess) return adlbq::hip_fail(_e, #call); \
+    } while (0)
+
+int ensure_req_capacity(adlbq_server *h, int n);
+int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
+int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
+int ensure_rq_capacity(adlbq_server *h, int extra);
+void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
+void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
+int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ unsigned long long make_key(int prio, unsigned int order) {
+    // larger key == better: priority descending, then `order` ascending
+    return ((unsigned long long)((unsigned int)prio ^ 0x80000000u) << 32) |
+           (unsigned long long)(~order);
+}
+
+__device__ __forceinline__ int bin_of(long long d) {
+    if (d < NBX) return (int)d;
+    int o = 63 - __clzll((unsigned long long)d);  // 5 .. 33
+    int b = NBX + (o - 5);
+    return b < NB ? b : NB - 1;
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+    unsigned int lane = __lane_id();
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+}  // namespace adlbq

@@ -1,0 +1,698 @@
+// adlbq_reserve.hip -- batched FA_RESERVE matching (src/adlb.c:1199-1317) on gfx950.
+//
+// A batch of R Reserves is matched with results identical to R sequential
+// calls of wq_find_pre_targeted_hi_prio / wq_find_hi_prio (src/xq.c:190-247)
+// followed by the pin.  Pipeline (all on the handle's stream):
+//
+//   k_req_prep     request type vectors -> 64-bit type masks, per-type demand
+//   k_hist_open    pass 1 over the open (untargeted) bucket: per page and per
+//                  type, histogram of distance-from-anchor bins (8 B/unit read)
+//   k_thresholds   per type: the bin where the demand is reached and how many
+//                  units of it are needed (exact bins: by wqseqno order)
+//   k_select_open  pass 2: order-preserving compaction of the top units of each
+//                  type into per-type candidate lists (prio desc, wqseqno asc)
+//   k_sort_types   only for types whose threshold fell in a multi-priority bin
+//   k_targeted     per target-rank bucket: that rank's Reserves in order against
+//                  its own targeted units (pre-targeted scan, xq.c:219-247)
+//   k_chain        one wavefront replays the untargeted choices in arrival order
+//                  as a T-way merge of the per-type candidate heads
+//   k_finalize     pins, TA_RESERVE_RESP records
+//   k_park         parks unmatched hanging Reserves on rq (FIFO), RFR donor choice
+#include <algorithm>
+#include <climits>
+
+#include "adlbq_donor.h"
+#include "adlbq_impl.h"
+
+using namespace adlbq;
+
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
+    unsigned int lo = __builtin_amdgcn_readlane((unsigned int)v, l);
+    unsigned int hi = __builtin_amdgcn_readlane((unsigned int)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+__global__ __launch_bounds__(256) void k_req_prep(const int *__restrict__ reqs, int R, const int *__restrict__ utypes,
+                                                  int T, unsigned long long *__restrict__ mask, int *dem) {
+    __shared__ int su[ADLBQ_MAX_TYPES], sd[ADLBQ_MAX_TYPES];
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        su[t] = utypes[t];
+        sd[t] = 0;
+    }
+    __syncthreads();
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < R) {
+        const int *rt = reqs + (long long)ADLBQ_RESERVE_INTS * j + 2;
+        unsigned long long m = 0;
+        bool wild = false;
+        for (int i = 0; i < NREQ; i++) {
+            int v = rt[i];
+            if (v == -1) { wild = true; continue; }
+            for (int t = 0; t < T; t++)
+                if (su[t] == v) { m |= 1ull << t; break; }  // get_type_idx: first declared match
+        }
+        if (wild) m = T >= 64 ? ~0ull : ((1ull << T) - 1);
+        mask[j] = m;
+        for (unsigned long long b = m; b; b &= b - 1) atomicAdd(&sd[__ffsll((long long)b) - 1], 1);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+        if (sd[t]) atomicAdd(&dem[t], sd[t]);
+}
+
+// ---------------------------------------------------------------- pass 1
+__global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages, int npages, int tail_fill,
+                                                   const int *__restrict__ prio, const uint32_t *__restrict__ meta,
+                                                   int T, const long long *__restrict__ anchor,
+                                                   const int *__restrict__ dem, unsigned short *__restrict__ gh,
+                                                   unsigned int *__restrict__ csum) {
+    extern __shared__ unsigned int lds[];
+    __shared__ long long sanc[ADLBQ_MAX_TYPES];
+    __shared__ int sdem[ADLBQ_MAX_TYPES];
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        sanc[t] = anchor[t];
+        sdem[t] = dem[t];
+    }
+    unsigned int *hist = lds + w * C;
+    for (int c = lane; c < C; c += 64) hist[c] = 0;
+    __syncthreads();
+    const int p = blockIdx.x * 4 + w;
+    if (p >= npages) return;
+    const long long base = (long long)pages[p] << PAGE_SHIFT;
+    const int fill = (p == npages - 1) ? tail_fill : PAGE;
+    const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
+    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
+    const int nit = (fill + 255) >> 8;
+#pragma unroll 4
+    for (int it = 0; it < nit; it++) {
+        int4 pv = P4[it * 64 + lane];
+        uint4 mv = M4[it * 64 + lane];
+        int pr[4] = {pv.x, pv.y, pv.z, pv.w};
+        uint32_t mm[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if ((mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST) {
+                int t = mm[q] & M_TYPE;
+                if (sdem[t] > 0) atomicAdd(&hist[t * NB + bin_of(sanc[t] - pr[q])], 1u);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    unsigned int *cs = csum + (long long)(p / CHUNK) * C;
+    unsigned short *g = gh + (long long)p * C;
+    for (int c = lane; c < C; c += 64) {
+        unsigned int v = hist[c];
+        g[c] = (unsigned short)v;
+        if (v) atomicAdd(&cs[c], v);
+    }
+}
+
+// ---------------------------------------------------------------- thresholds
+__global__ __launch_bounds__(1024) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
+                                                     int nchunks, int *theta, int *need, int *candoff,
+                                                     int *candlen, int *needsort, int *binoff) {
+    extern __shared__ unsigned int tot[];
+    const int C = T * NB;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        unsigned int run = 0;
+        for (int k = 0; k < nchunks; k++) {
+            unsigned int v = csum[(long long)k * C + c];
+            csum[(long long)k * C + c] = run;  // exclusive prefix over chunks, in place
+            run += v;
+        }
+        tot[c] = run;
+    }
+    __syncthreads();
+    if (threadIdx.x < T) {
+        const int t = threadIdx.x, d = dem[t];
+        int th = -1, nd = 0, len = 0;
+        if (d > 0) {
+            long long cum = 0;
+            for (int b = 0; b < NB; b++) {
+                long long x = tot[t * NB + b];
+                binoff[t * NB + b] = (int)cum;
+                if (cum + x >= d) {
+                    th = b;
+                    if (b < NBX) {          // one priority value: the first (d - cum) by wqseqno
+                        nd = (int)(d - cum);
+                        len = d;
+                    } else {                // several values: take the whole bin, sort later
+                        nd = INT_MAX;
+                        len = (int)(cum + x);
+                    }
+                    break;
+                }
+                cum += x;
+            }
+            if (th < 0) {                   // fewer available units than demand: take all
+                th = NB - 1;
+                nd = INT_MAX;
+                len = (int)cum;
+            }
+        }
+        theta[t] = th;
+        need[t] = nd;
+        candlen[t] = len;
+        needsort[t] = (th >= NBX && len > 1) ? 1 : 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int off = 0;
+        for (int t = 0; t < T; t++) {
+            candoff[t] = off;
+            off += candlen[t];
+        }
+        candoff[T] = off;
+    }
+}
+
+// ---------------------------------------------------------------- pass 2
+__global__ __launch_bounds__(256) void k_select_open(
+    const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
+    const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
+    const int *__restrict__ theta, const int *__restrict__ need, const int *__restrict__ candoff,
+    const int *__restrict__ binoff, const unsigned short *__restrict__ gh, const unsigned int *__restrict__ csum,
+    unsigned long long *__restrict__ ckey, int *__restrict__ cslot) {
+    extern __shared__ unsigned int lds[];
+    __shared__ long long sanc[ADLBQ_MAX_TYPES];
+    __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES];
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        sanc[t] = anchor[t];
+        sth[t] = theta[t];
+        sneed[t] = need[t];
+        soff[t] = candoff[t];
+    }
+    __syncthreads();
+    const int p = blockIdx.x * 4 + w;
+    if (p >= npages) return;
+    // running rank of each (type, bin) column, in wqseqno order over the whole open bucket
+    unsigned int *run = lds + w * C;
+    const int k0 = (p / CHUNK) * CHUNK;
+    for (int c = lane; c < C; c += 64) {
+        const int t = c / NB, b = c - t * NB;
+        if (b > sth[t]) continue;
+        unsigned int r = csum[(long long)(p / CHUNK) * C + c];
+        for (int q = k0; q < p; q++) r += gh[(long long)q * C + c];
+        run[c] = r;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const long long base = (long long)pages[p] << PAGE_SHIFT;
+    const int fill = (p == npages - 1) ? tail_fill : PAGE;
+    const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
+    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
+    const int nit = (fill + 255) >> 8;
+    const unsigned long long lt = lanemask_lt();
+    for (int it = 0; it < nit; it++) {
+        int4 pv = P4[it * 64 + lane];
+        uint4 mv = M4[it * 64 + lane];
+        int pr[4] = {pv.x, pv.y, pv.z, pv.w};
+        uint32_t mm[4] = {mv.x, mv.y, mv.z, mv.w};
+        int key[4];
+        bool pend[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            key[q] = -1;
+            if ((mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST) {
+                int t = mm[q] & M_TYPE;
+                if (sth[t] >= 0) {
+                    int b = bin_of(sanc[t] - pr[q]);
+                    if (b <= sth[t]) key[q] = t * NB + b;
+                }
+            }
+            pend[q] = key[q] >= 0;
+        }
+        // group pending candidates by column; ranks follow (lane, q) == slot order
+        while (true) {
+            unsigned long long any = __ballot(pend[0] || pend[1] || pend[2] || pend[3]);
+            if (!any) break;
+            int fk = pend[0] ? key[0] : pend[1] ? key[1] : pend[2] ? key[2] : pend[3] ? key[3] : -1;
+            const int leader = __ffsll((long long)any) - 1;
+            const int k = __builtin_amdgcn_readlane(fk, leader);
+            unsigned long long m0 = __ballot(pend[0] && key[0] == k), m1 = __ballot(pend[1] && key[1] == k);
+            unsigned long long m2 = __ballot(pend[2] && key[2] == k), m3 = __ballot(pend[3] && key[3] == k);
+            const unsigned int rbase = run[k];
+            const int before = __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+            const int t = k / NB, b = k - t * NB;
+            const unsigned long long ms[4] = {m0, m1, m2, m3};
+            int within = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if ((ms[q] >> lane) & 1ull) {
+                    const unsigned int r = rbase + before + within;
+                    within++;
+                    pend[q] = false;
+                    const bool keep = b < sth[t] || b >= NBX || (int)r < sneed[t];
+                    if (keep) {
+                        const long long pos = (long long)soff[t] + binoff[k] + r;
+                        const long long slot = base + it * 256 + lane * 4 + q;
+                        ckey[pos] = make_key(pr[q], (unsigned int)seqa[slot]);
+                        cslot[pos] = (int)slot;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) run[k] = rbase + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// ---------------------------------------------------------------- per-type sort (multi-priority bins only)
+__device__ inline void bitonic_desc_4096(unsigned long long *sk, int *ss) {
+    for (int k = 2; k <= 4096; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+                int ixj = i ^ j;
+                if (ixj > i) {
+                    unsigned long long a = sk[i], b = sk[ixj];
+                    bool sw = ((i & k) == 0) ? (a < b) : (a > b);
+                    if (sw) {
+                        sk[i] = b;
+                        sk[ixj] = a;
+                        int t = ss[i];
+                        ss[i] = ss[ixj];
+                        ss[ixj] = t;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_sort_types(const int *__restrict__ needsort, const int *__restrict__ candoff,
+                                                     const int *__restrict__ candlen, unsigned long long *key,
+                                                     int *slot, unsigned long long *key2, int *slot2) {
+    const int t = blockIdx.x;
+    if (!needsort[t]) return;
+    const int off = candoff[t], n = candlen[t];
+    if (n <= 1) return;
+    __shared__ unsigned long long sk[4096];
+    __shared__ int ss[4096];
+    for (int c0 = 0; c0 < n; c0 += 4096) {
+        const int m = min(4096, n - c0);
+        for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+            sk[i] = i < m ? key[off + c0 + i] : 0ull;
+            ss[i] = i < m ? slot[off + c0 + i] : -1;
+        }
+        __syncthreads();
+        bitonic_desc_4096(sk, ss);
+        for (int i = threadIdx.x; i < m; i += blockDim.x) {
+            key[off + c0 + i] = sk[i];
+            slot[off + c0 + i] = ss[i];
+        }
+        __syncthreads();
+    }
+    if (n <= 4096) return;
+    __threadfence();
+    __syncthreads();
+    unsigned long long *sK = key + off, *dK = key2 + off;
+    int *sS = slot + off, *dS = slot2 + off;
+    constexpr int ITEMS = 4;
+    for (long long wdt = 4096; wdt < n; wdt *= 2) {
+        for (long long a0 = 0; a0 < n; a0 += 2 * wdt) {
+            const long long na = min((long long)n - a0, wdt);
+            const long long nb = max(0ll, min((long long)n - a0 - wdt, wdt));
+            const unsigned long long *A = sK + a0, *B = sK + a0 + na;
+            const int *AS = sS + a0, *BS = sS + a0 + na;
+            const long long tot = na + nb;
+            for (long long o0 = 0; o0 < tot; o0 += (long long)blockDim.x * ITEMS) {
+                const long long d = o0 + (long long)threadIdx.x * ITEMS;
+                if (d >= tot) continue;
+                long long lo = max(0ll, d - nb), hi = min(d, na);
+                while (lo < hi) {  // number of A elements among the first d outputs
+                    long long mid = (lo + hi) >> 1;
+                    if (A[mid] >= B[d - 1 - mid]) lo = mid + 1;
+                    else hi = mid;
+                }
+                long long i = lo, j = d - lo;
+                for (int e = 0; e < ITEMS && d + e < tot; e++) {
+                    bool takeA = j >= nb || (i < na && A[i] >= B[j]);
+                    if (takeA) {
+                        dK[a0 + d + e] = A[i];
+                        dS[a0 + d + e] = AS[i];
+                        i++;
+                    } else {
+                        dK[a0 + d + e] = B[j];
+                        dS[a0 + d + e] = BS[j];
+                        j++;
+                    }
+                }
+            }
+        }
+        __threadfence();
+        __syncthreads();
+        unsigned long long *tk = sK; sK = dK; dK = tk;
+        int *ts = sS; sS = dS; dS = ts;
+    }
+    if (sK != key + off) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            key[off + i] = sK[i];
+            slot[off + i] = sS[i];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- targeted phase
+__global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket_ranks, const int *__restrict__ pstart,
+                                                  const int *__restrict__ rpages, const int *__restrict__ rfill,
+                                                  const int *__restrict__ prio, uint32_t *meta,
+                                                  const unsigned long long *__restrict__ mask,
+                                                  const int *__restrict__ reqs, int R, int *tmatch) {
+    __shared__ int list[1024];
+    __shared__ int nlist, wcnt[4];
+    __shared__ unsigned long long red[4];
+    const int b = blockIdx.x, r = bucket_ranks[b], p0 = pstart[b], np = pstart[b + 1] - p0;
+    if (np <= 0) return;
+    const long long total = (long long)(np - 1) * PAGE + rfill[b];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) nlist = 0;
+    __syncthreads();
+    for (int j0 = 0; j0 < R; j0 += 256) {
+        const int j = j0 + threadIdx.x;
+        const bool is = j < R && reqs[(long long)ADLBQ_RESERVE_INTS * j] == r;
+        const unsigned long long bal = __ballot(is);
+        if (lane == 0) wcnt[w] = __popcll(bal);
+        __syncthreads();
+        int woff = nlist;
+        for (int q = 0; q < w; q++) woff += wcnt[q];
+        if (is) list[woff + __popcll(bal & lanemask_lt())] = j;
+        __syncthreads();
+        if (threadIdx.x == 0) nlist += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        __syncthreads();
+        if (nlist > 768 || j0 + 256 >= R) {
+            for (int e = 0; e < nlist; e++) {
+                const int jj = list[e];
+                const unsigned long long m = mask[jj];
+                unsigned long long best = 0;
+                for (long long L = threadIdx.x; L < total; L += blockDim.x) {
+                    const long long slot = ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
+                    const uint32_t mt = (uint32_t)ld_agent(reinterpret_cast<const int *>(meta + slot));
+                    if ((mt & (M_LIVE | M_PINNED)) != M_LIVE) continue;
+                    if (!((m >> (mt & M_TYPE)) & 1ull)) continue;
+                    const int pr = prio[slot];
+                    if (pr <= LOWEST) continue;
+                    const unsigned long long k = make_key(pr, (unsigned int)L);
+                    best = k > best ? k : best;
+                }
+                best = wave_max_u64(best);
+                if (lane == 0) red[w] = best;
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    unsigned long long bb = red[0];
+                    for (int q = 1; q < 4; q++) bb = red[q] > bb ? red[q] : bb;
+                    if (bb) {
+                        const long long L = (long long)(~(unsigned int)(bb & 0xffffffffu));
+                        const long long slot =
+                            ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
+                        tmatch[jj] = (int)slot;
+                        // taken for this rank's later Reserves (this block owns the bucket)
+                        st_agent(reinterpret_cast<int *>(meta + slot), (int)(meta[slot] | M_PINNED));
+                    }
+                }
+                __threadfence();
+                __syncthreads();
+            }
+            if (threadIdx.x == 0) nlist = 0;
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------- untargeted choices in arrival order
+template <int WID>
+__global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restrict__ mask,
+                                              const int *__restrict__ tmatch, int R, int T,
+                                              const int *__restrict__ candoff, const int *__restrict__ candlen,
+                                              const unsigned long long *__restrict__ ckey,
+                                              const int *__restrict__ cslot, int *__restrict__ umatch) {
+    const int lane = threadIdx.x;
+    const bool act = lane < T;
+    const int off = act ? candoff[lane] : 0, len = act ? candlen[lane] : 0;
+    int c = 0;
+    unsigned long long cur = len > 0 ? ckey[off] : 0ull, nxt = len > 1 ? ckey[off + 1] : 0ull;
+    int cs = len > 0 ? cslot[off] : -1, ns = len > 1 ? cslot[off + 1] : -1;
+    for (int j0 = 0; j0 < R; j0 += 64) {
+        const int jj = j0 + lane;
+        const unsigned long long mj = jj < R ? mask[jj] : 0ull;
+        const int tj = jj < R ? tmatch[jj] : 0;
+        int res = -1;
+        const int kmax = min(64, R - j0);
+        for (int k = 0; k < kmax; k++) {
+            if (__builtin_amdgcn_readlane(tj, k) >= 0) continue;  // satisfied by its targeted units
+            const unsigned long long mk = readlane64(mj, k);
+            const unsigned long long v = (act && ((mk >> lane) & 1ull)) ? cur : 0ull;
+            unsigned long long bv = v;
+#pragma unroll
+            for (int o = WID / 2; o > 0; o >>= 1) {
+                unsigned long long w2 = __shfl_xor(bv, o, 64);
+                bv = bv > w2 ? bv : w2;
+            }
+            bv = readlane64(bv, 0);
+            if (bv == 0) continue;
+            const int wl = __ffsll((long long)__ballot(v == bv)) - 1;
+            const int s = __builtin_amdgcn_readlane(cs, wl);
+            if (lane == k) res = s;
+            if (lane == wl) {
+                c++;
+                cur = nxt;
+                cs = ns;
+                nxt = c + 1 < len ? ckey[off + c + 1] : 0ull;
+                ns = c + 1 < len ? cslot[off + c + 1] : -1;
+            }
+        }
+        if (jj < R) umatch[jj] = res;
+    }
+}
+
+// ---------------------------------------------------------------- finalize
+__global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, int R, const int *__restrict__ tmatch,
+                                                  const int *__restrict__ umatch, const int *__restrict__ prio,
+                                                  uint32_t *meta, int *pin, const int *__restrict__ seqa,
+                                                  const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
+                                                  int my_world, int *__restrict__ resp) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= R) return;
+    const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
+    const int rank = rq[0], hang = rq[1];
+    const int slot = tmatch[j] >= 0 ? tmatch[j] : umatch[j];
+    int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
+    if (slot >= 0) {
+        pin[slot] = rank;  // adlb.c:1210-1212
+        if (rank >= 0) meta[slot] |= M_PINNED;
+        const int4 c0 = cold0[slot], c1 = cold1[slot];
+        o[0] = 1;
+        o[1] = c1.z;
+        o[2] = prio[slot];
+        o[3] = c0.y;
+        o[4] = c0.x;
+        o[5] = seqa[slot];
+        o[6] = my_world;
+        o[7] = c0.w;
+        o[8] = c1.x;
+        o[9] = c1.y;
+    } else if (!hang) {
+        o[0] = -2;  // NO_CURR_WORK
+    }
+    int *out = resp + (long long)ADLBQ_RESP_INTS * j;
+#pragma unroll
+    for (int i = 0; i < ADLBQ_RESP_INTS; i++) out[i] = o[i];
+}
+
+// ---------------------------------------------------------------- park on rq + RFR donor choice
+__global__ __launch_bounds__(64) void k_park(DonorCtx c, int donors, const int *__restrict__ reqs, int R,
+                                             const int *__restrict__ tmatch, const int *__restrict__ umatch,
+                                             int *rq_rank, int *rq_types, int *rq_live, DevCounters *ctr,
+                                             int *resp) {
+    const int lane = threadIdx.x;
+    int n = ctr->rq_n, live = ctr->rq_live, hwm = ctr->rq_hwm, np = 0;
+    const unsigned long long lt = lanemask_lt();
+    for (int j0 = 0; j0 < R; j0 += 64) {
+        const int j = j0 + lane;
+        const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
+        const bool parked = j < R && tmatch[j] < 0 && umatch[j] < 0 && rq[1] != 0;
+        const unsigned long long b = __ballot(parked);
+        if (!b) continue;
+        if (parked) {
+            const int pos = n + __popcll(b & lt);
+            rq_rank[pos] = rq[0];
+            for (int q = 0; q < NREQ; q++) rq_types[(long long)pos * NREQ + q] = rq[2 + q];
+            st_agent(rq_live + pos, 1);
+            resp[(long long)ADLBQ_RESP_INTS * j + 10] = pos + 1;  // rqseqno (next_rqseqno++, adlb.c:1244)
+        }
+        if (donors) {
+            for (unsigned long long bb = b; bb; bb &= bb - 1) {
+                const int l = __ffsll((long long)bb) - 1, jj = j0 + l;
+                const int *rr = reqs + (long long)ADLBQ_RESERVE_INTS * jj;
+                const int rank = rr[0];
+                int cand = -1;
+                if (rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) < 0)
+                    cand = rfr_select(c, rank, rr + 2);
+                if (lane == 0) resp[(long long)ADLBQ_RESP_INTS * jj + 11] = cand;
+            }
+        }
+        const int cnt = __popcll(b);
+        n += cnt;
+        live += cnt;
+        np += cnt;
+        hwm = live > hwm ? live : hwm;
+    }
+    if (lane == 0) {
+        ctr->rq_n = n;
+        ctr->rq_live = live;
+        ctr->rq_hwm = hwm;
+        ctr->n_parked_last = np;
+    }
+}
+
+// ================================================================ host side
+namespace adlbq {
+
+int ensure_req_capacity(adlbq_server *h, int n) {
+    if (n <= h->cap_req) return ADLBQ_OK;
+    int nc = std::max(n, std::max(1024, h->cap_req * 2));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf};
+    for (void *p : ps)
+        if (p) AQ_HIP(hipFree(p));
+    AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
+    AQ_HIP(hipMalloc((void **)&h->d_tmatch, sizeof(int) * nc));
+    AQ_HIP(hipMalloc((void **)&h->d_umatch, sizeof(int) * nc));
+    AQ_HIP(hipMalloc((void **)&h->d_reqbuf, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)nc));
+    AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
+    h->cap_req = nc;
+    return ADLBQ_OK;
+}
+
+static int ensure_scan_capacity(adlbq_server *h, int npages) {
+    const long long C = (long long)std::max(h->T, 1) * NB;
+    const long long need_gh = (long long)npages * C, nchunks = (npages + CHUNK - 1) / CHUNK;
+    const long long need_cs = std::max(1ll, nchunks) * C, need_cand = (long long)npages * PAGE;
+    if (need_gh > h->cap_gh || need_cs > h->cap_csum || need_cand > h->cap_cand)
+        AQ_HIP(hipStreamSynchronize(h->stream));
+    if (need_gh > h->cap_gh) {
+        if (h->d_gh) AQ_HIP(hipFree(h->d_gh));
+        h->cap_gh = std::max(need_gh, 2 * h->cap_gh);
+        AQ_HIP(hipMalloc((void **)&h->d_gh, sizeof(unsigned short) * h->cap_gh));
+    }
+    if (need_cs > h->cap_csum) {
+        if (h->d_csum) AQ_HIP(hipFree(h->d_csum));
+        h->cap_csum = std::max(need_cs, 2 * h->cap_csum);
+        AQ_HIP(hipMalloc((void **)&h->d_csum, sizeof(unsigned int) * h->cap_csum));
+    }
+    if (need_cand > h->cap_cand) {
+        void *ps[] = {h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2};
+        for (void *p : ps)
+            if (p) AQ_HIP(hipFree(p));
+        h->cap_cand = std::max(need_cand, 2 * h->cap_cand);
+        AQ_HIP(hipMalloc((void **)&h->d_ckey, sizeof(unsigned long long) * h->cap_cand));
+        AQ_HIP(hipMalloc((void **)&h->d_ckey2, sizeof(unsigned long long) * h->cap_cand));
+        AQ_HIP(hipMalloc((void **)&h->d_cslot, sizeof(int) * h->cap_cand));
+        AQ_HIP(hipMalloc((void **)&h->d_cslot2, sizeof(int) * h->cap_cand));
+    }
+    return ADLBQ_OK;
+}
+
+int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
+    int rc;
+    if ((rc = ensure_req_capacity(h, R))) return rc;
+    if ((rc = sync_tables(h))) return rc;
+    if ((rc = ensure_rq_capacity(h, R))) return rc;
+    const int T = h->T, C = T * NB;
+    const int np = (int)h->open.pages.size();
+    if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
+    hipStream_t s = h->stream;
+    hipEvent_t ev;
+
+    AQ_HIP(hipMemsetAsync(h->d_dem, 0, sizeof(int) * std::max(T, 1), s));
+    k_req_prep<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem);
+
+    if (np > 0 && T > 0) {
+        const int nchunks = (np + CHUNK - 1) / CHUNK;
+        AQ_HIP(hipMemsetAsync(h->d_csum, 0, sizeof(unsigned int) * (size_t)nchunks * C, s));
+        stage_begin(h, "hist", &ev);
+        k_hist_open<<<(np + 3) / 4, 256, sizeof(unsigned int) * 4 * C, s>>>(
+            h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_dem, h->d_gh,
+            h->d_csum);
+        stage_end(h, "hist", ev);
+        k_thresholds<<<1, 1024, sizeof(unsigned int) * C, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta,
+                                                               h->d_need, h->d_candoff, h->d_candlen,
+                                                               h->d_needsort, h->d_binoff);
+        stage_begin(h, "select", &ev);
+        k_select_open<<<(np + 3) / 4, 256, sizeof(unsigned int) * 4 * C, s>>>(
+            h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
+            h->d_need, h->d_candoff, h->d_binoff, h->d_gh, h->d_csum, h->d_ckey, h->d_cslot);
+        stage_end(h, "select", ev);
+        stage_begin(h, "sort", &ev);
+        k_sort_types<<<T, 1024, 0, s>>>(h->d_needsort, h->d_candoff, h->d_candlen, h->d_ckey, h->d_cslot,
+                                        h->d_ckey2, h->d_cslot2);
+        stage_end(h, "sort", ev);
+    } else {
+        AQ_HIP(hipMemsetAsync(h->d_candlen, 0, sizeof(int) * std::max(T, 1), s));
+        AQ_HIP(hipMemsetAsync(h->d_candoff, 0, sizeof(int) * (std::max(T, 1) + 1), s));
+    }
+    h->last_scan_units = h->live_units - h->live_targeted;
+
+    AQ_HIP(hipMemsetAsync(h->d_tmatch, 0xff, sizeof(int) * R, s));
+    const int nb = (int)h->bucket_ranks.size();
+    if (h->live_targeted > 0 && nb > 0) {
+        stage_begin(h, "targeted", &ev);
+        k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
+                                      h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch);
+        stage_end(h, "targeted", ev);
+    }
+    stage_begin(h, "chain", &ev);
+    int wid = 1;
+    while (wid < T) wid <<= 1;
+    switch (wid) {
+#define CHAIN(W)                                                                                              \
+    case W:                                                                                                   \
+        k_chain<W><<<1, 64, 0, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey,      \
+                                    h->d_cslot, h->d_umatch);                                                 \
+        break;
+        CHAIN(1) CHAIN(2) CHAIN(4) CHAIN(8) CHAIN(16) CHAIN(32) CHAIN(64)
+#undef CHAIN
+    default: return fail(ADLBQ_ERR_UNSUPPORTED, "too many types");
+    }
+    stage_end(h, "chain", ev);
+    stage_begin(h, "finalize", &ev);
+    k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_prio, h->d_meta, h->d_pin,
+                                               h->d_seq, h->d_cold0, h->d_cold1, h->my_world, d_resp);
+    const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
+    k_park<<<1, 64, 0, s>>>(donor_ctx(h), donors, d_reqs, R, h->d_tmatch, h->d_umatch, h->d_rq_rank,
+                            h->d_rq_types, h->d_rq_live, h->d_ctr, d_resp);
+    stage_end(h, "finalize", ev);
+    AQ_HIP(hipGetLastError());
+    h->ctr_stale = true;
+    h->rq_n_upper += R;
+    return ADLBQ_OK;
+}
+
+}  // namespace adlbq
+
+extern "C" {
+
+int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12) {
+    if (!h || n < 0 || (n && (!reqs18 || !resp12))) return fail(ADLBQ_ERR_ARG, "adlbq_reserve_batch");
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    int rc;
+    if ((rc = ensure_req_capacity(h, n))) return rc;
+    AQ_HIP(hipMemcpyAsync(h->d_reqbuf, reqs18, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)n, hipMemcpyHostToDevice,
+                          h->stream));
+    if ((rc = launch_reserve(h, n, h->d_reqbuf, h->d_respbuf))) return rc;
+    AQ_HIP(hipMemcpyAsync(resp12, h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)n, hipMemcpyDeviceToHost,
+                          h->stream));
+    return refresh_counters(h);
+}
+
+int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int *d_resp12) {
+    if (!h || n < 0 || (n && (!d_reqs18 || !d_resp12))) return fail(ADLBQ_ERR_ARG, "adlbq_reserve_batch_device");
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    return launch_reserve(h, n, d_reqs18, d_resp12);
+}
+
+}  // extern "C"

@@ -1,0 +1,874 @@
+// adlbq_store.hip -- handle lifecycle, HBM unit store, Put / Get / Unreserve,
+// qmstat row, info and donor-selection entry points of the C ABI (include/adlbq.h).
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+
+#include "adlbq_donor.h"
+#include "adlbq_impl.h"
+
+using namespace adlbq;
+
+static thread_local std::string g_err;
+
+namespace adlbq {
+
+int fail(int code, const char *msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *where) {
+    g_err = std::string(where) + ": " + hipGetErrorString(e);
+    return ADLBQ_ERR_HIP;
+}
+
+template <typename T>
+static int grow(T **p, long long old_n, long long new_n, hipStream_t s, int fill_byte = -1) {
+    T *np = nullptr;
+    AQ_HIP(hipMalloc((void **)&np, sizeof(T) * (size_t)new_n));
+    if (*p && old_n > 0) AQ_HIP(hipMemcpyAsync(np, *p, sizeof(T) * (size_t)old_n, hipMemcpyDeviceToDevice, s));
+    if (fill_byte >= 0 && new_n > old_n)
+        AQ_HIP(hipMemsetAsync(np + old_n, fill_byte, sizeof(T) * (size_t)(new_n - old_n), s));
+    if (*p) {
+        AQ_HIP(hipStreamSynchronize(s));
+        AQ_HIP(hipFree(*p));
+    }
+    *p = np;
+    return ADLBQ_OK;
+}
+
+static int grow_pages(adlbq_server *h, int need) {
+    if (need <= h->cap_pages) return ADLBQ_OK;
+    int nc = std::max(need, h->cap_pages * 2);
+    long long o = (long long)h->cap_pages * PAGE, n = (long long)nc * PAGE;
+    int rc;
+    if ((rc = grow(&h->d_prio, o, n, h->stream))) return rc;
+    if ((rc = grow(&h->d_meta, o, n, h->stream, 0))) return rc;
+    if ((rc = grow(&h->d_pin, o, n, h->stream, 0xff))) return rc;
+    if ((rc = grow(&h->d_seq, o, n, h->stream))) return rc;
+    if ((rc = grow(&h->d_cold0, o, n, h->stream))) return rc;
+    if ((rc = grow(&h->d_cold1, o, n, h->stream))) return rc;
+    h->cap_pages = nc;
+    return ADLBQ_OK;
+}
+
+int ensure_rq_capacity(adlbq_server *h, int extra) {
+    long long need = (long long)(h->ctr_stale ? h->rq_n_upper : h->ctr.rq_n) + extra;
+    if (need <= h->rq_cap) return ADLBQ_OK;
+    if (h->ctr_stale) {
+        int rc = refresh_counters(h);
+        if (rc) return rc;
+        need = (long long)h->ctr.rq_n + extra;
+        if (need <= h->rq_cap) return ADLBQ_OK;
+    }
+    long long nc = std::max<long long>(need, (long long)h->rq_cap * 2);
+    nc = std::max<long long>(nc, 1024);
+    int rc;
+    if ((rc = grow(&h->d_rq_rank, h->rq_cap, nc, h->stream))) return rc;
+    if ((rc = grow(&h->d_rq_types, (long long)h->rq_cap * NREQ, nc * NREQ, h->stream))) return rc;
+    if ((rc = grow(&h->d_rq_live, h->rq_cap, nc, h->stream, 0))) return rc;
+    h->rq_cap = (int)nc;
+    return ADLBQ_OK;
+}
+
+int refresh_counters(adlbq_server *h) {
+    AQ_HIP(hipMemcpyAsync(&h->ctr, h->d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    h->ctr_stale = false;
+    h->rq_n_upper = h->ctr.rq_n;
+    return ADLBQ_OK;
+}
+
+template <typename T>
+static int upload(T **dptr, int *cap, const std::vector<T> &v, hipStream_t s) {
+    if ((int)v.size() > *cap) {
+        if (*dptr) {
+            AQ_HIP(hipStreamSynchronize(s));
+            AQ_HIP(hipFree(*dptr));
+        }
+        int nc = std::max<int>((int)v.size(), 2 * *cap);
+        nc = std::max(nc, 64);
+        AQ_HIP(hipMalloc((void **)dptr, sizeof(T) * nc));
+        *cap = nc;
+    }
+    if (!v.empty()) AQ_HIP(hipMemcpyAsync(*dptr, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, s));
+    return ADLBQ_OK;
+}
+
+int sync_tables(adlbq_server *h) {
+    int rc;
+    if (h->tables_dirty) {
+        if ((rc = upload(&h->d_open_pages, &h->cap_open_pages, h->open.pages, h->stream))) return rc;
+        std::vector<int> rp, pstart, fill;
+        pstart.push_back(0);
+        for (size_t k = 0; k < h->bucket_ranks.size(); k++) {
+            const Bucket &b = h->rankb[k];
+            rp.insert(rp.end(), b.pages.begin(), b.pages.end());
+            pstart.push_back((int)rp.size());
+            fill.push_back(b.pages.empty() ? 0 : b.tail_fill);
+        }
+        if ((rc = upload(&h->d_rank_pages, &h->cap_rank_pages, rp, h->stream))) return rc;
+        if ((rc = upload(&h->d_rank_pstart, &h->cap_rank_pstart, pstart, h->stream))) return rc;
+        if ((rc = upload(&h->d_rank_fill, &h->cap_rank_fill, fill, h->stream))) return rc;
+        if ((rc = upload(&h->d_bucket_ranks, &h->cap_bucket_ranks, h->bucket_ranks, h->stream))) return rc;
+        // every page with its fill, for whole-store scans
+        std::vector<int> ap, af;
+        for (size_t i = 0; i < h->open.pages.size(); i++) {
+            ap.push_back(h->open.pages[i]);
+            af.push_back(i + 1 == h->open.pages.size() ? h->open.tail_fill : PAGE);
+        }
+        for (size_t k = 0; k < h->bucket_ranks.size(); k++) {
+            const Bucket &b = h->rankb[k];
+            for (size_t i = 0; i < b.pages.size(); i++) {
+                ap.push_back(b.pages[i]);
+                af.push_back(i + 1 == b.pages.size() ? b.tail_fill : PAGE);
+            }
+        }
+        if ((rc = upload(&h->d_all_pages, &h->cap_all_pages, ap, h->stream))) return rc;
+        if ((rc = upload(&h->d_all_fill, &h->cap_all_fill, af, h->stream))) return rc;
+        h->tables_dirty = false;
+    }
+    if (h->anchor_dirty) {
+        AQ_HIP(hipMemcpyAsync(h->d_anchor, h->anchor.data(), sizeof(long long) * h->T,
+                              hipMemcpyHostToDevice, h->stream));
+        h->anchor_dirty = false;
+    }
+    if (h->qm_dirty) {
+        if (h->S * h->T > 0)
+            AQ_HIP(hipMemcpyAsync(h->d_qm_hi, h->qm_hi.data(), sizeof(int) * h->S * h->T,
+                                  hipMemcpyHostToDevice, h->stream));
+        AQ_HIP(hipMemcpyAsync(h->d_qm_qlen, h->qm_qlen.data(), sizeof(int) * h->S,
+                              hipMemcpyHostToDevice, h->stream));
+        h->qm_dirty = false;
+    }
+    if (h->tq_dirty) {
+        if ((rc = upload(&h->d_tq, &h->cap_tq, h->tq, h->stream))) return rc;
+        h->tq_dirty = false;
+    }
+    return ADLBQ_OK;
+}
+
+DonorCtx donor_ctx(adlbq_server *h) {
+    DonorCtx c;
+    c.qm_hi = h->d_qm_hi;
+    c.qm_qlen = h->d_qm_qlen;
+    c.tq = h->d_tq;
+    c.utypes = h->d_utypes;
+    c.rfr_out = h->d_rfr_out;
+    c.rfr_to_rank = h->d_rfr_to_rank;
+    c.S = h->S;
+    c.T = h->T;
+    c.n_tq = (int)(h->tq.size() / 4);
+    c.master = h->master;
+    c.my_world = h->my_world;
+    c.A = h->A;
+    c.num_world = h->num_world;
+    return c;
+}
+
+void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev) {
+    *ev = nullptr;
+    if (!h->profiling) return;
+    hipEventCreate(ev);
+    hipEventRecord(*ev, h->stream);
+    (void)name;
+}
+
+void stage_end(adlbq_server *h, const char *name, hipEvent_t ev) {
+    if (!h->profiling || !ev) return;
+    hipEvent_t e2;
+    hipEventCreate(&e2);
+    hipEventRecord(e2, h->stream);
+    h->timers[name].pending.push_back({ev, e2});
+}
+
+}  // namespace adlbq
+
+// ============================================================================ kernels
+
+struct PutRec {  // staged by the host per Put
+    int slot, prio, meta, seq;
+    int answer, len, home, clen;
+    int csrv, cseq, utype, target;
+};
+
+__global__ void k_put_scatter(const PutRec *__restrict__ r, int n, int *prio, uint32_t *meta, int *pin,
+                              int *seq, int4 *cold0, int4 *cold1, long long *seq2slot) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    PutRec u = r[i];
+    prio[u.slot] = u.prio;
+    meta[u.slot] = (uint32_t)u.meta;
+    pin[u.slot] = -1;
+    seq[u.slot] = u.seq;
+    cold0[u.slot] = make_int4(u.answer, u.len, u.home, u.clen);
+    cold1[u.slot] = make_int4(u.csrv, u.cseq, u.utype, u.target);
+    seq2slot[u.seq] = u.slot;
+}
+
+// Put-side FIFO match, one wavefront, Puts strictly in order
+// (rq_find_rank_queued_for_type, xq.c:388-405, at adlb.c:988-1042)
+__global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__restrict__ rq_rank,
+                            const int *__restrict__ rq_types, int *rq_live, DevCounters *ctr,
+                            uint32_t *meta, int *pin, int *out3) {
+    const int lane = threadIdx.x;
+    int head = ctr->rq_head, nrq = ctr->rq_n, live = ctr->rq_live;
+    for (int i = 0; i < n; i++) {
+        PutRec u = r[i];
+        int found = -1;
+        if (live > 0) {
+            for (int base = head; base < nrq; base += 64) {
+                int k = base + lane;
+                bool hit = false;
+                if (k < nrq && ld_agent(rq_live + k)) {
+                    int rk = rq_rank[k];
+                    if (u.target == -1 || u.target == rk) {
+                        const int *tv = rq_types + (long long)k * NREQ;
+#pragma unroll
+                        for (int q = 0; q < NREQ; q++) {
+                            int t = tv[q];
+                            hit |= (u.utype == -1 || t == -1 || t == u.utype);
+                        }
+                    }
+                }
+                unsigned long long b = __ballot(hit);
+                if (b) { found = base + __ffsll((long long)b) - 1; break; }
+            }
+        }
+        if (lane == 0) {
+            int *o = out3 + 3 * i;
+            o[0] = u.seq;
+            o[1] = -1;
+            o[2] = -1;
+            if (found >= 0) {
+                int rk = rq_rank[found];
+                st_agent(rq_live + found, 0);
+                o[1] = rk;
+                o[2] = found + 1;  // rqseqno == slot + 1
+                pin[u.slot] = rk;
+                if (rk >= 0) meta[u.slot] = (uint32_t)u.meta | M_PINNED;
+            }
+        }
+        if (found >= 0) {
+            live--;
+            if (found == head)
+                while (head < nrq && !ld_agent(rq_live + head)) head++;
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+    }
+    if (lane == 0) {
+        ctr->rq_live = live;
+        ctr->rq_head = head;
+    }
+}
+
+__global__ void k_get(int slot, int rank, int seq, const int *prio, uint32_t *meta, const int *pin,
+                      const int *seqa, const int4 *cold0, const int4 *cold1, int *res) {
+    uint32_t m = meta[slot];
+    res[0] = -1;
+    res[1] = res[2] = res[3] = res[4] = 0;
+    res[5] = -1;
+    if ((m & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) {
+        int4 c0 = cold0[slot], c1 = cold1[slot];
+        res[0] = 1;
+        res[1] = c0.y;
+        res[2] = c1.z;
+        res[3] = prio[slot];
+        res[4] = c0.x;
+        res[5] = c1.w;
+        meta[slot] = 0;
+    }
+}
+
+__global__ void k_unreserve(int slot, int rank, int seq, int newpin, uint32_t *meta, int *pin,
+                            const int *seqa, int *res) {
+    uint32_t m = meta[slot];
+    res[0] = 0;
+    if ((m & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) {
+        pin[slot] = newpin;
+        meta[slot] = m & ~M_PINNED;
+        res[0] = 1;
+    }
+}
+
+__global__ void k_unreserve_batch(const int *__restrict__ trip, int n, const long long *__restrict__ seq2slot,
+                                  long long nseq, uint32_t *meta, int *pin, const int *seqa) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int rank = trip[3 * i], seq = trip[3 * i + 1], np = trip[3 * i + 2];
+    if (seq <= 0 || seq >= nseq) return;
+    long long slot = seq2slot[seq];
+    if (slot < 0) return;
+    uint32_t m = meta[slot];
+    if ((m & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) {
+        pin[slot] = np;
+        meta[slot] = m & ~M_PINNED;
+    }
+}
+
+// update_local_state over the open bucket: count of live unpinned units and per
+// type max prio (strictly above ADLB_LOWEST_PRIO, else LOWEST)
+__global__ void k_qmrow(const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
+                        const uint32_t *__restrict__ meta, int T, int *res /* [0]=qlen, [1+t]=max */) {
+    __shared__ int smax[ADLBQ_MAX_TYPES];
+    __shared__ int scnt;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) smax[t] = LOWEST;
+    if (threadIdx.x == 0) scnt = 0;
+    __syncthreads();
+    int cnt = 0;
+    long long total = (long long)npages * PAGE;
+    for (long long L = (long long)blockIdx.x * blockDim.x + threadIdx.x; L < total;
+         L += (long long)gridDim.x * blockDim.x) {
+        int p = (int)(L >> PAGE_SHIFT), off = (int)(L & (PAGE - 1));
+        if (p == npages - 1 && off >= tail_fill) continue;
+        long long s = ((long long)pages[p] << PAGE_SHIFT) + off;
+        uint32_t m = meta[s];
+        if ((m & (M_LIVE | M_PINNED)) == M_LIVE) {
+            cnt++;
+            int pr = prio[s];
+            if (pr > LOWEST) atomicMax(&smax[m & M_TYPE], pr);
+        }
+    }
+    atomicAdd(&scnt, cnt);
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+        if (smax[t] > LOWEST) atomicMax(&res[1 + t], smax[t]);
+    if (threadIdx.x == 0) atomicAdd(&res[0], scnt);
+}
+
+// whole-store scan helpers (FA_INFO_NUM_WORK_UNITS, wq_find_unpinned)
+__global__ void k_info_max(const int *__restrict__ pages, const int *__restrict__ fills, int npages,
+                           const int *__restrict__ prio, const uint32_t *__restrict__ meta, int tidx,
+                           int *res /* [0]=max [1]=count */) {
+    int p = blockIdx.x;
+    if (p >= npages) return;
+    long long base = (long long)pages[p] << PAGE_SHIFT;
+    int mx = LOWEST, n = 0;
+    for (int o = threadIdx.x; o < fills[p]; o += blockDim.x) {
+        uint32_t m = meta[base + o];
+        if ((m & M_LIVE) && (int)(m & M_TYPE) == tidx) {
+            n++;
+            int pr = prio[base + o];
+            mx = pr > mx ? pr : mx;
+        }
+    }
+    if (n) {
+        atomicAdd(&res[1], n);
+        if (mx > LOWEST) atomicMax(&res[0], mx);
+    }
+}
+
+__global__ void k_info_cnt(const int *__restrict__ pages, const int *__restrict__ fills, int npages,
+                           const int *__restrict__ prio, const uint32_t *__restrict__ meta, int tidx,
+                           int *res /* [0]=max (in) [2]=count at max */) {
+    int p = blockIdx.x;
+    if (p >= npages) return;
+    long long base = (long long)pages[p] << PAGE_SHIFT;
+    int mx = res[0], n = 0;
+    for (int o = threadIdx.x; o < fills[p]; o += blockDim.x) {
+        uint32_t m = meta[base + o];
+        n += ((m & M_LIVE) && (int)(m & M_TYPE) == tidx && prio[base + o] == mx);
+    }
+    if (n) atomicAdd(&res[2], n);
+}
+
+__global__ void k_first_unpinned(const int *__restrict__ pages, const int *__restrict__ fills, int npages,
+                                 const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int *res) {
+    int p = blockIdx.x;
+    if (p >= npages) return;
+    long long base = (long long)pages[p] << PAGE_SHIFT;
+    int best = INT_MAX;
+    for (int o = threadIdx.x; o < fills[p]; o += blockDim.x) {
+        uint32_t m = meta[base + o];
+        if ((m & (M_LIVE | M_PINNED)) == M_LIVE) {
+            int s = seqa[base + o];
+            best = s < best ? s : best;
+        }
+    }
+    if (best != INT_MAX) atomicMin(res, best);
+}
+
+// check_remote_work_for_queued_apps, one wavefront over rq in FIFO order
+__global__ void k_checkrem(DonorCtx c, const int *__restrict__ rq_rank, const int *__restrict__ rq_types,
+                           const int *rq_live, const DevCounters *ctr, int cap, int *out3, int *count) {
+    int k0 = ctr->rq_head, nrq = ctr->rq_n, n = 0;
+    for (int k = k0; k < nrq; k++) {
+        if (!ld_agent(rq_live + k)) continue;
+        int rank = rq_rank[k];
+        if (rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) >= 0) continue;
+        int cand = rfr_select(c, rank, rq_types + (long long)k * NREQ);
+        if (cand >= 0) {
+            if (threadIdx.x == 0 && n < cap) {
+                out3[3 * n] = k + 1;
+                out3[3 * n + 1] = rank;
+                out3[3 * n + 2] = cand;
+            }
+            n++;
+        }
+    }
+    if (threadIdx.x == 0) *count = n;
+}
+
+__global__ void k_rq_delete(int k, int *rq_live, DevCounters *ctr, int *res) {
+    res[0] = 0;
+    if (k >= 0 && k < ctr->rq_n && rq_live[k]) {
+        rq_live[k] = 0;
+        ctr->rq_live--;
+        res[0] = 1;
+        int head = ctr->rq_head;
+        while (head < ctr->rq_n && !rq_live[head]) head++;
+        ctr->rq_head = head;
+    }
+}
+
+__global__ void k_set_int(int *p, int v) { *p = v; }
+
+// ============================================================================ C ABI
+
+static bool ok_handle(adlbq_server *h) { return h != nullptr; }
+
+extern "C" {
+
+const char *adlbq_last_error(void) { return g_err.c_str(); }
+const char *adlbq_version(void) { return "adlbq 0.1 (gfx950)"; }
+
+int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_app_ranks, int num_servers,
+                 int my_server_idx, long long max_units, int device) {
+    if (!out || ntypes < 0 || (ntypes && !user_types) || num_app_ranks < 0 || num_servers < 1 ||
+        my_server_idx < 0 || my_server_idx >= num_servers)
+        return fail(ADLBQ_ERR_ARG, "adlbq_create: bad argument");
+    if (ntypes > ADLBQ_MAX_TYPES) return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 64 work types");
+    auto *h = new adlbq_server();
+    h->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete h;
+        return hip_fail(e, "hipSetDevice");
+    }
+    if ((e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking)) != hipSuccess) {
+        delete h;
+        return hip_fail(e, "hipStreamCreate");
+    }
+    h->stream = h->own_stream;
+    h->T = ntypes;
+    h->utypes.assign(user_types, user_types + ntypes);
+    for (int i = 0; i < ntypes; i++)
+        if (!h->tindex.count(user_types[i])) h->tindex[user_types[i]] = i;  // get_type_idx: first match
+    h->A = num_app_ranks;
+    h->S = num_servers;
+    h->my_idx = my_server_idx;
+    h->master = num_app_ranks;                    // adlb.c:256
+    h->my_world = num_app_ranks + my_server_idx;
+    h->num_world = num_app_ranks + num_servers;
+    h->anchor.assign(std::max(ntypes, 1), (long long)INT_MIN);
+    h->qm_hi.assign((size_t)num_servers * std::max(ntypes, 1), LOWEST);  // adlb.c:301-316
+    h->qm_qlen.assign(num_servers, 0);
+    h->qm_bytes.assign(num_servers, 0.0);
+    h->seq2slot.assign(1, -1);
+    int rc;
+    auto cleanup = [&](int code) { adlbq_destroy(h); return code; };
+    int T1 = std::max(ntypes, 1);
+    AQ_HIP(hipMalloc((void **)&h->d_anchor, sizeof(long long) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_utypes, sizeof(int) * T1));
+    if (ntypes) AQ_HIP(hipMemcpy(h->d_utypes, user_types, sizeof(int) * ntypes, hipMemcpyHostToDevice));
+    AQ_HIP(hipMalloc((void **)&h->d_qm_hi, sizeof(int) * num_servers * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_qm_qlen, sizeof(int) * num_servers));
+    AQ_HIP(hipMalloc((void **)&h->d_rfr_out, sizeof(int) * std::max(h->num_world, 1)));
+    AQ_HIP(hipMemset(h->d_rfr_out, 0, sizeof(int) * std::max(h->num_world, 1)));  // SURVEY hard part 4
+    AQ_HIP(hipMalloc((void **)&h->d_rfr_to_rank, sizeof(int) * std::max(num_app_ranks, 1)));
+    AQ_HIP(hipMemset(h->d_rfr_to_rank, 0xff, sizeof(int) * std::max(num_app_ranks, 1)));
+    AQ_HIP(hipMalloc((void **)&h->d_ctr, sizeof(DevCounters)));
+    AQ_HIP(hipMemset(h->d_ctr, 0, sizeof(DevCounters)));
+    AQ_HIP(hipMalloc((void **)&h->d_dem, sizeof(int) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_theta, sizeof(int) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_need, sizeof(int) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_candoff, sizeof(int) * (T1 + 1)));
+    AQ_HIP(hipMalloc((void **)&h->d_candlen, sizeof(int) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_needsort, sizeof(int) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_binoff, sizeof(int) * T1 * NB));
+    AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
+    AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
+    long long pages = std::max<long long>(16, (max_units + PAGE - 1) / PAGE + 16);
+    if ((rc = grow_pages(h, (int)std::min<long long>(pages, INT_MAX / PAGE)))) return cleanup(rc);
+    if ((rc = ensure_rq_capacity(h, 1024))) return cleanup(rc);
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *out = h;
+    return ADLBQ_OK;
+}
+
+int adlbq_destroy(adlbq_server *h) {
+    if (!h) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    if (h->own_stream) hipStreamSynchronize(h->own_stream);
+    void *ptrs[] = {h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_open_pages,
+                    h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_all_pages,
+                    h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_utypes, h->d_rq_rank, h->d_rq_types,
+                    h->d_rq_live, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
+                    h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
+                    h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_gh, h->d_csum,
+                    h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_result};
+    for (void *p : ptrs)
+        if (p) hipFree(p);
+    if (h->h_result) hipHostFree(h->h_result);
+    for (auto &kv : h->timers)
+        for (auto &pe : kv.second.pending) {
+            hipEventDestroy(pe.first);
+            hipEventDestroy(pe.second);
+        }
+    if (h->own_stream) hipStreamDestroy(h->own_stream);
+    delete h;
+    return ADLBQ_OK;
+}
+
+static int rank_bucket(adlbq_server *h, int target) {
+    auto it = h->rank_index.find(target);
+    if (it != h->rank_index.end()) return it->second;
+    int k = (int)h->bucket_ranks.size();
+    h->bucket_ranks.push_back(target);
+    h->rankb.emplace_back();
+    h->rank_index[target] = k;
+    return k;
+}
+
+int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
+    if (!ok_handle(h) || n < 0 || (n && (!units9 || !out3))) return fail(ADLBQ_ERR_ARG, "adlbq_put_batch");
+    if (n == 0) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    for (int i = 0; i < n; i++)
+        if (!h->tindex.count(units9[9 * i])) return fail(ADLBQ_ERR_TYPE, "adlbq_put_batch: undeclared work type");
+    std::vector<PutRec> rec(n);
+    int rc;
+    for (int i = 0; i < n; i++) {
+        const int *u = units9 + 9 * i;
+        int tgt = u[3];
+        Bucket *b;
+        if (tgt < 0) {
+            b = &h->open;
+        } else {
+            int k = rank_bucket(h, tgt);
+            b = &h->rankb[k];
+        }
+        if (b->pages.empty() || b->tail_fill == PAGE) {
+            if (h->n_pages == h->cap_pages && (rc = grow_pages(h, h->n_pages + 1))) return rc;
+            b->pages.push_back(h->n_pages++);
+            b->tail_fill = 0;
+        }
+        h->tables_dirty = true;
+        long long slot = ((long long)b->pages.back() << PAGE_SHIFT) + b->tail_fill++;
+        int seq = h->next_wqseqno++;
+        int ti = h->tindex[u[0]];
+        PutRec &r = rec[i];
+        r.slot = (int)slot;
+        r.prio = u[1];
+        r.meta = ti | (int)M_LIVE;
+        r.seq = seq;
+        r.answer = u[2];
+        r.len = u[4];
+        r.home = u[5];
+        r.clen = u[6];
+        r.csrv = u[7];
+        r.cseq = u[8];
+        r.utype = u[0];
+        r.target = tgt;
+        if ((long long)h->seq2slot.size() <= seq) h->seq2slot.resize((size_t)seq * 2 + 16, -1);
+        h->seq2slot[seq] = slot;
+        if (u[1] > h->anchor[ti]) {
+            h->anchor[ti] = u[1];
+            h->anchor_dirty = true;
+        }
+        h->live_units++;
+        if (tgt >= 0) h->live_targeted++;
+        if (h->live_units > h->max_count) h->max_count = h->live_units;
+    }
+    if ((long long)h->next_wqseqno > h->cap_seq) {
+        long long nc = std::max<long long>(h->next_wqseqno + 1024, h->cap_seq * 2);
+        if ((rc = grow(&h->d_seq2slot, h->cap_seq, nc, h->stream, 0xff))) return rc;
+        h->cap_seq = nc;
+    }
+    PutRec *d_rec = nullptr;
+    int *d_out = nullptr;
+    AQ_HIP(hipMalloc((void **)&d_rec, sizeof(PutRec) * n));
+    AQ_HIP(hipMemcpyAsync(d_rec, rec.data(), sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
+    k_put_scatter<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, h->d_prio, h->d_meta, h->d_pin, h->d_seq,
+                                                          h->d_cold0, h->d_cold1, h->d_seq2slot);
+    bool may_match = h->ctr_stale || h->ctr.rq_live > 0;
+    if (may_match) {
+        AQ_HIP(hipMalloc((void **)&d_out, sizeof(int) * 3 * n));
+        k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
+                                             h->d_meta, h->d_pin, d_out);
+        AQ_HIP(hipMemcpyAsync(out3, d_out, sizeof(int) * 3 * n, hipMemcpyDeviceToHost, h->stream));
+        AQ_HIP(hipGetLastError());
+        if ((rc = refresh_counters(h))) return rc;
+        AQ_HIP(hipFree(d_out));
+    } else {
+        for (int i = 0; i < n; i++) {
+            out3[3 * i] = rec[i].seq;
+            out3[3 * i + 1] = -1;
+            out3[3 * i + 2] = -1;
+        }
+        AQ_HIP(hipGetLastError());
+        AQ_HIP(hipStreamSynchronize(h->stream));
+    }
+    AQ_HIP(hipFree(d_rec));
+    return ADLBQ_OK;
+}
+
+static int find_slot(adlbq_server *h, int seq, long long *slot) {
+    if (seq <= 0 || seq >= (long long)h->seq2slot.size() || seq >= h->next_wqseqno) return 0;
+    *slot = h->seq2slot[seq];
+    return *slot >= 0;
+}
+
+int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5) {
+    if (!ok_handle(h) || !out5) return fail(ADLBQ_ERR_ARG, "adlbq_get_reserved");
+    hipSetDevice(h->device);
+    long long slot;
+    out5[0] = -1;
+    out5[1] = out5[2] = out5[3] = out5[4] = 0;
+    if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
+    k_get<<<1, 1, 0, h->stream>>>((int)slot, rank, wqseqno, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0,
+                                  h->d_cold1, h->d_result);
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 6, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    memcpy(out5, h->h_result, sizeof(int) * 5);
+    if (out5[0] == 1) {
+        h->seq2slot[wqseqno] = -1;
+        h->live_units--;
+        if (h->h_result[5] >= 0) h->live_targeted--;
+        // keep the device map consistent for batch unreserves
+        AQ_HIP(hipMemsetAsync(h->d_seq2slot + wqseqno, 0xff, sizeof(long long), h->stream));
+    }
+    return ADLBQ_OK;
+}
+
+int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, int *found) {
+    if (!ok_handle(h) || !found) return fail(ADLBQ_ERR_ARG, "adlbq_unreserve");
+    hipSetDevice(h->device);
+    long long slot;
+    *found = 0;
+    if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
+    k_unreserve<<<1, 1, 0, h->stream>>>((int)slot, rank, wqseqno, new_pin_rank, h->d_meta, h->d_pin, h->d_seq,
+                                        h->d_result);
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *found = h->h_result[0];
+    return ADLBQ_OK;
+}
+
+int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples) {
+    if (!ok_handle(h) || n < 0) return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_batch_device");
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    k_unreserve_batch<<<(n + 255) / 256, 256, 0, h->stream>>>(d_triples, n, h->d_seq2slot, h->next_wqseqno,
+                                                              h->d_meta, h->d_pin, h->d_seq);
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
+int adlbq_qmstat_row(adlbq_server *h, int *qlen, int *type_hi_prio) {
+    if (!ok_handle(h) || !qlen || (h->T && !type_hi_prio)) return fail(ADLBQ_ERR_ARG, "adlbq_qmstat_row");
+    hipSetDevice(h->device);
+    int rc;
+    if ((rc = sync_tables(h))) return rc;
+    std::vector<int> init(1 + h->T, LOWEST);
+    init[0] = 0;
+    AQ_HIP(hipMemcpyAsync(h->d_result, init.data(), sizeof(int) * (1 + h->T), hipMemcpyHostToDevice, h->stream));
+    int np = (int)h->open.pages.size();
+    if (np) {
+        int blocks = std::min(2048, np * (PAGE / 256));
+        k_qmrow<<<blocks, 256, 0, h->stream>>>(h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->T,
+                                               h->d_result);
+    }
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * (1 + h->T), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *qlen = h->h_result[0];
+    for (int t = 0; t < h->T; t++) type_hi_prio[t] = h->h_result[1 + t];
+    // this server's own qmstat row (adlb.c:3586-3591)
+    h->qm_qlen[h->my_idx] = *qlen;
+    for (int t = 0; t < h->T; t++) h->qm_hi[(size_t)h->my_idx * h->T + t] = type_hi_prio[t];
+    h->qm_dirty = true;
+    return ADLBQ_OK;
+}
+
+int adlbq_set_qmstat_row(adlbq_server *h, int server_idx, int qlen, double nbytes_used, const int *type_hi_prio) {
+    if (!ok_handle(h) || server_idx < 0 || server_idx >= h->S || (h->T && !type_hi_prio))
+        return fail(ADLBQ_ERR_ARG, "adlbq_set_qmstat_row");
+    if (server_idx == h->my_idx) return ADLBQ_OK;  // the local row survives the unpack (adlb.c:1724-1728)
+    h->qm_qlen[server_idx] = qlen;
+    h->qm_bytes[server_idx] = nbytes_used;
+    for (int t = 0; t < h->T; t++) h->qm_hi[(size_t)server_idx * h->T + t] = type_hi_prio[t];
+    h->qm_dirty = true;
+    return ADLBQ_OK;
+}
+
+int adlbq_check_remote(adlbq_server *h, int cap, int *out3, int *count) {
+    if (!ok_handle(h) || cap < 0 || !count || (cap && !out3)) return fail(ADLBQ_ERR_ARG, "adlbq_check_remote");
+    hipSetDevice(h->device);
+    int rc;
+    if ((rc = sync_tables(h))) return rc;
+    if (h->ctr_stale && (rc = refresh_counters(h))) return rc;
+    int *d_out = nullptr;
+    int nrq = h->ctr.rq_n;
+    int capd = std::max(1, std::min(cap, nrq));
+    AQ_HIP(hipMalloc((void **)&d_out, sizeof(int) * (3 * capd + 1)));
+    k_checkrem<<<1, 64, 0, h->stream>>>(donor_ctx(h), h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr, capd,
+                                        d_out + 1, d_out);
+    AQ_HIP(hipGetLastError());
+    int k = 0;
+    AQ_HIP(hipMemcpyAsync(&k, d_out, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    int kk = std::min(k, cap);
+    if (kk) AQ_HIP(hipMemcpy(out3, d_out + 1, sizeof(int) * 3 * kk, hipMemcpyDeviceToHost));
+    AQ_HIP(hipFree(d_out));
+    *count = kk;
+    return ADLBQ_OK;
+}
+
+int adlbq_rfr_done(adlbq_server *h, int from_server_rank, int for_rank) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_rfr_done");
+    hipSetDevice(h->device);
+    if (for_rank >= 0 && for_rank < h->A) k_set_int<<<1, 1, 0, h->stream>>>(h->d_rfr_to_rank + for_rank, -1);
+    if (from_server_rank >= 0 && from_server_rank < h->num_world)
+        k_set_int<<<1, 1, 0, h->stream>>>(h->d_rfr_out + from_server_rank, 0);
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
+int adlbq_tq_add(adlbq_server *h, int app_rank, int work_type, int server_rank) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_tq_add");
+    for (size_t i = 0; i + 3 < h->tq.size(); i += 4)
+        if (h->tq[i] == app_rank && h->tq[i + 1] == work_type && h->tq[i + 2] == server_rank) {
+            h->tq[i + 3]++;
+            h->tq_dirty = true;
+            return ADLBQ_OK;
+        }
+    h->tq.insert(h->tq.end(), {app_rank, work_type, server_rank, 1});
+    h->tq_dirty = true;
+    return ADLBQ_OK;
+}
+
+int adlbq_rq_delete(adlbq_server *h, int rqseqno, int *found) {
+    if (!ok_handle(h) || !found) return fail(ADLBQ_ERR_ARG, "adlbq_rq_delete");
+    hipSetDevice(h->device);
+    k_rq_delete<<<1, 1, 0, h->stream>>>(rqseqno - 1, h->d_rq_live, h->d_ctr, h->d_result);
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *found = h->h_result[0];
+    h->ctr_stale = true;
+    return refresh_counters(h);
+}
+
+int adlbq_push_select(adlbq_server *h, double threshold, int *cand_server_rank, int *wqseqno) {
+    if (!ok_handle(h) || !cand_server_rank || !wqseqno) return fail(ADLBQ_ERR_ARG, "adlbq_push_select");
+    hipSetDevice(h->device);
+    int rc;
+    if ((rc = sync_tables(h))) return rc;
+    *cand_server_rank = -1;
+    *wqseqno = -1;
+    int npages = (int)(h->open.pages.size());
+    for (auto &b : h->rankb) npages += (int)b.pages.size();
+    h->h_result[0] = INT_MAX;
+    AQ_HIP(hipMemcpyAsync(h->d_result, h->h_result, sizeof(int), hipMemcpyHostToDevice, h->stream));
+    if (npages)
+        k_first_unpinned<<<npages, 256, 0, h->stream>>>(h->d_all_pages, h->d_all_fill, npages, h->d_meta, h->d_seq,
+                                                        h->d_result);
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    if (h->h_result[0] == INT_MAX) return ADLBQ_OK;
+    // argmin nbytes_used over other servers below the threshold (adlb.c:516-528)
+    double smallest = 999999999999.9;
+    int cand = -1;
+    for (int i = 0; i < h->S; i++) {
+        int srv = h->master + i;
+        if (srv != h->my_world && h->qm_bytes[i] < threshold && h->qm_bytes[i] < smallest) {
+            smallest = h->qm_bytes[i];
+            cand = srv;
+        }
+    }
+    *cand_server_rank = cand;
+    *wqseqno = h->h_result[0];
+    return ADLBQ_OK;
+}
+
+int adlbq_info(adlbq_server *h, int *wq_count, int *wq_max_count, int *rq_count) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_info");
+    hipSetDevice(h->device);
+    int rc;
+    if (h->ctr_stale && (rc = refresh_counters(h))) return rc;
+    if (wq_count) *wq_count = (int)h->live_units;
+    if (wq_max_count) *wq_max_count = (int)h->max_count;
+    if (rq_count) *rq_count = h->ctr.rq_live;
+    return ADLBQ_OK;
+}
+
+int adlbq_info_type(adlbq_server *h, int work_type, int *max_prio, int *num_max_prio, int *num_type) {
+    if (!ok_handle(h) || !max_prio || !num_max_prio || !num_type) return fail(ADLBQ_ERR_ARG, "adlbq_info_type");
+    auto it = h->tindex.find(work_type);
+    if (it == h->tindex.end()) return fail(ADLBQ_ERR_TYPE, "adlbq_info_type: undeclared type");
+    hipSetDevice(h->device);
+    int rc;
+    if ((rc = sync_tables(h))) return rc;
+    int npages = (int)(h->open.pages.size());
+    for (auto &b : h->rankb) npages += (int)b.pages.size();
+    int init[3] = {LOWEST, 0, 0};
+    AQ_HIP(hipMemcpyAsync(h->d_result, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
+    if (npages) {
+        k_info_max<<<npages, 256, 0, h->stream>>>(h->d_all_pages, h->d_all_fill, npages, h->d_prio, h->d_meta,
+                                                  it->second, h->d_result);
+        k_info_cnt<<<npages, 256, 0, h->stream>>>(h->d_all_pages, h->d_all_fill, npages, h->d_prio, h->d_meta,
+                                                  it->second, h->d_result);
+    }
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *max_prio = h->h_result[0];
+    *num_max_prio = h->h_result[2];
+    *num_type = h->h_result[1];
+    return ADLBQ_OK;
+}
+
+int adlbq_set_stream(adlbq_server *h, void *s) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_set_stream");
+    hipStreamSynchronize(h->stream);
+    h->stream = s ? (hipStream_t)s : h->own_stream;
+    return ADLBQ_OK;
+}
+
+void *adlbq_get_stream(adlbq_server *h) { return h ? (void *)h->stream : nullptr; }
+
+int adlbq_sync(adlbq_server *h) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_sync");
+    hipSetDevice(h->device);
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    return ADLBQ_OK;
+}
+
+int adlbq_profile_enable(adlbq_server *h, int on) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_profile_enable");
+    h->profiling = on != 0;
+    return ADLBQ_OK;
+}
+
+int adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, long long *launches) {
+    if (!ok_handle(h) || !stage) return fail(ADLBQ_ERR_ARG, "adlbq_profile_read");
+    hipSetDevice(h->device);
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    auto &t = h->timers[stage];
+    for (auto &pe : t.pending) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, pe.first, pe.second);
+        t.total_ms += ms;
+        t.launches++;
+        hipEventDestroy(pe.first);
+        hipEventDestroy(pe.second);
+    }
+    t.pending.clear();
+    if (total_ms) *total_ms = t.total_ms;
+    if (launches) *launches = t.launches;
+    return ADLBQ_OK;
+}
+
+long long adlbq_last_scan_units(adlbq_server *h) { return h ? h->last_scan_units : 0; }
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+"""Replay an event trace (format of oracle/replay.h) through the C ABI.
+
+Consecutive Puts become one ``adlbq_put_batch`` and consecutive Reserves one
+``adlbq_reserve_batch`` -- the batch entry points guarantee the same results as
+processing the events one at a time, so the output stream must equal the
+oracle's byte for byte.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .server import Server
+from .synth import (OP_CHECKREM, OP_GET, OP_INFO, OP_INFOTYPE, OP_PUSHSEL, OP_PUT, OP_QMROW, OP_RESERVE,
+                    OP_RFRDONE, OP_RQDEL, OP_SETROW, OP_TQADD, OP_UNRESERVE)
+
+
+def nargs(op: int, T: int) -> int:
+    return {OP_PUT: 9, OP_RESERVE: 18, OP_GET: 2, OP_UNRESERVE: 3, OP_QMROW: 0, OP_SETROW: 3 + T,
+            OP_CHECKREM: 0, OP_RFRDONE: 2, OP_TQADD: 3, OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1,
+            OP_INFOTYPE: 1}[op]
+
+
+def _runs(tr: np.ndarray, T: int):
+    """Yield (op, args (k, nargs) array) for maximal runs of identical opcodes
+    (PUT/RESERVE) and single events otherwise."""
+    i, n = 0, tr.size
+    while i < n:
+        op = int(tr[i])
+        w = 1 + nargs(op, T)
+        if op in (OP_PUT, OP_RESERVE):
+            j = i
+            # stride through the run while the opcode repeats
+            while j < n and int(tr[j]) == op:
+                j += w
+            block = tr[i:j].reshape(-1, w)
+            yield op, block[:, 1:]
+            i = j
+        else:
+            yield op, tr[i + 1:i + w].reshape(1, -1)
+            i += w
+
+
+def replay(srv: Server, trace) -> np.ndarray:
+    tr = np.ascontiguousarray(np.asarray(trace, dtype=np.int32))
+    T = srv.T
+    out: list[np.ndarray] = []
+
+    def emit(vals):
+        v = np.asarray(vals, dtype=np.int32).ravel()
+        out.append(np.concatenate([np.asarray([v.size], np.int32), v]))
+
+    for op, a in _runs(tr, T):
+        if op == OP_PUT:
+            r = srv.put_batch(a)
+            blk = np.empty((r.shape[0], 4), np.int32)
+            blk[:, 0] = 3
+            blk[:, 1:] = r
+            out.append(blk.ravel())
+        elif op == OP_RESERVE:
+            r = srv.reserve_batch(a)
+            blk = np.empty((r.shape[0], 13), np.int32)
+            blk[:, 0] = 12
+            blk[:, 1:] = r
+            out.append(blk.ravel())
+        else:
+            x = [int(v) for v in a[0]]
+            if op == OP_GET:
+                emit(srv.get_reserved(x[0], x[1]))
+            elif op == OP_UNRESERVE:
+                emit([srv.unreserve(x[0], x[1], x[2])])
+            elif op == OP_QMROW:
+                q, hi = srv.qmstat_row()
+                emit([q, *hi.tolist()])
+            elif op == OP_SETROW:
+                srv.set_qmstat_row(x[0], x[1], x[2], x[3:3 + T])
+                emit([])
+            elif op == OP_CHECKREM:
+                r = srv.check_remote()
+                emit([r.shape[0], *r.ravel().tolist()])
+            elif op == OP_RFRDONE:
+                srv.rfr_done(x[0], x[1])
+                emit([])
+            elif op == OP_TQADD:
+                srv.tq_add(x[0], x[1], x[2])
+                r = srv.check_remote()  # adlb.c:1179
+                emit([r.shape[0], *r.ravel().tolist()])
+            elif op == OP_PUSHSEL:
+                emit(list(srv.push_select(x[0])))
+            elif op == OP_INFO:
+                emit(list(srv.info()))
+            elif op == OP_RQDEL:
+                emit([srv.rq_delete(x[0])])
+            elif op == OP_INFOTYPE:
+                emit(list(srv.info_type(x[0])))
+            else:
+                raise ValueError(f"unknown opcode {op}")
+    return np.concatenate(out) if out else np.zeros(0, np.int32)

@@ -1,0 +1,180 @@
+"""Host-side mirror of one ADLB server's queue handlers over the C ABI.
+
+Each method corresponds to a handler site of the reference server loop
+(``src/adlb.c``) and to one entry point of ``include/adlbq.h``; the matching
+itself runs in the HIP library (``adlb_amd/libadlbq.so``).  Arguments and
+results keep the reference's meaning: world ranks, user work-type values,
+TA_RESERVE_RESP int[12] records, NULL/-1 for "not found".
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+RESP_INTS = 12
+PUT_INTS = 9
+RESERVE_INTS = 18
+LOWEST_PRIO = -999999999
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Server:
+    """Queue state of one ADLB server rank on one MI355X (ADLBP_Init's per-server
+    setup, adlb.c:295-320)."""
+
+    def __init__(self, user_types, num_app_ranks: int, num_servers: int = 1, my_server_idx: int = 0,
+                 max_units: int = 1 << 16, device: int = 0):
+        self.lib = _lib.load()
+        ut = np.ascontiguousarray(np.asarray(user_types, dtype=np.int32))
+        self.user_types = ut
+        self.T = int(ut.size)
+        self.num_app_ranks = int(num_app_ranks)
+        self.num_servers = int(num_servers)
+        self.my_server_idx = int(my_server_idx)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.adlbq_create(ctypes.byref(h), self.T, _ptr(ut), self.num_app_ranks,
+                                         self.num_servers, self.my_server_idx, int(max_units), int(device)),
+                   "adlbq_create")
+        self.h = h
+
+    # -- lifecycle -------------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.adlbq_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- FA_PUT_HDR (adlb.c:963-1046) -----------------------------------------
+    def put_batch(self, units9) -> np.ndarray:
+        """units9: (n, 9) {type, prio, answer_rank, target_rank, len, home_server,
+        common_len, common_server, common_seqno} -> (n, 3) {wqseqno, matched_rank,
+        matched_rqseqno}."""
+        u = np.ascontiguousarray(np.asarray(units9, dtype=np.int32).reshape(-1, PUT_INTS))
+        out = np.empty((u.shape[0], 3), dtype=np.int32)
+        _lib.check(self.lib.adlbq_put_batch(self.h, u.shape[0], _ptr(u), _ptr(out)), "adlbq_put_batch")
+        return out
+
+    def put(self, work_type, prio, answer_rank=0, target_rank=-1, length=8, home_server=-1,
+            common_len=0, common_server=-1, common_seqno=-1):
+        return self.put_batch([[work_type, prio, answer_rank, target_rank, length, home_server,
+                                common_len, common_server, common_seqno]])[0]
+
+    # -- FA_RESERVE (adlb.c:1199-1317) ----------------------------------------
+    def reserve_batch(self, reqs18) -> np.ndarray:
+        """reqs18: (n, 18) {from_rank, hang, req_types[16]} -> (n, 12) TA_RESERVE_RESP
+        (+ [10] rqseqno if parked, [11] RFR target server rank)."""
+        r = np.ascontiguousarray(np.asarray(reqs18, dtype=np.int32).reshape(-1, RESERVE_INTS))
+        out = np.empty((r.shape[0], RESP_INTS), dtype=np.int32)
+        _lib.check(self.lib.adlbq_reserve_batch(self.h, r.shape[0], _ptr(r), _ptr(out)),
+                   "adlbq_reserve_batch")
+        return out
+
+    def reserve(self, rank, req_types, hang=1):
+        tv = list(req_types)[:16]
+        tv += [-2] * (16 - len(tv))
+        return self.reserve_batch([[rank, hang] + tv])[0]
+
+    def reserve_batch_device(self, n: int, d_reqs: int, d_resp: int) -> None:
+        """Device-pointer variant (HBM-resident requests/responses, stream ordered)."""
+        _lib.check(self.lib.adlbq_reserve_batch_device(self.h, n, d_reqs, d_resp),
+                   "adlbq_reserve_batch_device")
+
+    # -- FA_GET_RESERVED / SS_UNRESERVE ---------------------------------------
+    def get_reserved(self, rank, wqseqno):
+        out = np.empty(5, dtype=np.int32)
+        _lib.check(self.lib.adlbq_get_reserved(self.h, rank, wqseqno, _ptr(out)), "adlbq_get_reserved")
+        return out
+
+    def unreserve(self, rank, wqseqno, new_pin_rank=-1) -> int:
+        f = ctypes.c_int()
+        _lib.check(self.lib.adlbq_unreserve(self.h, rank, wqseqno, new_pin_rank, ctypes.byref(f)),
+                   "adlbq_unreserve")
+        return f.value
+
+    def unreserve_batch_device(self, n: int, d_triples: int) -> None:
+        _lib.check(self.lib.adlbq_unreserve_batch_device(self.h, n, d_triples),
+                   "adlbq_unreserve_batch_device")
+
+    # -- qmstat / donor selection ----------------------------------------------
+    def qmstat_row(self):
+        q = ctypes.c_int()
+        hi = np.empty(max(self.T, 1), dtype=np.int32)
+        _lib.check(self.lib.adlbq_qmstat_row(self.h, ctypes.byref(q), _ptr(hi)), "adlbq_qmstat_row")
+        return q.value, hi[: self.T].copy()
+
+    def set_qmstat_row(self, server_idx, qlen, nbytes_used, type_hi_prio):
+        hi = np.ascontiguousarray(np.asarray(type_hi_prio, dtype=np.int32))
+        _lib.check(self.lib.adlbq_set_qmstat_row(self.h, server_idx, qlen, float(nbytes_used), _ptr(hi)),
+                   "adlbq_set_qmstat_row")
+
+    def check_remote(self) -> np.ndarray:
+        cap = 1 << 16
+        out = np.empty((cap, 3), dtype=np.int32)
+        k = ctypes.c_int()
+        _lib.check(self.lib.adlbq_check_remote(self.h, cap, _ptr(out), ctypes.byref(k)), "adlbq_check_remote")
+        return out[: k.value].copy()
+
+    def rfr_done(self, from_server_rank, for_rank):
+        _lib.check(self.lib.adlbq_rfr_done(self.h, from_server_rank, for_rank), "adlbq_rfr_done")
+
+    def tq_add(self, app_rank, work_type, server_rank):
+        _lib.check(self.lib.adlbq_tq_add(self.h, app_rank, work_type, server_rank), "adlbq_tq_add")
+
+    def rq_delete(self, rqseqno) -> int:
+        f = ctypes.c_int()
+        _lib.check(self.lib.adlbq_rq_delete(self.h, rqseqno, ctypes.byref(f)), "adlbq_rq_delete")
+        return f.value
+
+    def push_select(self, threshold):
+        c, s = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_push_select(self.h, float(threshold), ctypes.byref(c), ctypes.byref(s)),
+                   "adlbq_push_select")
+        return c.value, s.value
+
+    # -- info --------------------------------------------------------------------
+    def info(self):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "adlbq_info")
+        return a.value, b.value, c.value
+
+    def info_type(self, work_type):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_info_type(self.h, work_type, ctypes.byref(a), ctypes.byref(b),
+                                            ctypes.byref(c)), "adlbq_info_type")
+        return a.value, b.value, c.value
+
+    # -- plumbing ------------------------------------------------------------------
+    def set_stream(self, stream_ptr: int | None):
+        _lib.check(self.lib.adlbq_set_stream(self.h, stream_ptr or None), "adlbq_set_stream")
+
+    def sync(self):
+        _lib.check(self.lib.adlbq_sync(self.h), "adlbq_sync")
+
+    def profile(self, on=True):
+        _lib.check(self.lib.adlbq_profile_enable(self.h, 1 if on else 0), "adlbq_profile_enable")
+
+    def profile_read(self, stage: str):
+        ms, n = ctypes.c_double(), ctypes.c_longlong()
+        _lib.check(self.lib.adlbq_profile_read(self.h, stage.encode(), ctypes.byref(ms), ctypes.byref(n)),
+                   "adlbq_profile_read")
+        return ms.value, n.value
+
+    def last_scan_units(self) -> int:
+        return int(self.lib.adlbq_last_scan_units(self.h))

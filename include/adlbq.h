@@ -1,0 +1,146 @@
+/*
+ * adlbq.h -- C ABI of the MI355X-native ADLB server work-queue engine.
+ *
+ * One opaque handle = the queue state of one ADLB server rank: its work queue
+ * (wq), its parked Reserves (rq), its targeted-remote index (tq), its copy of
+ * the qmstat status table and the RFR throttling state.  The matching itself
+ * runs as HIP kernels on gfx950 over a structure-of-arrays store in HBM; the
+ * caller (the C server loop in the reference's src/adlb.c, ADLBP_Server) keeps
+ * the MPI wire protocol and payload buffers and calls these entry points at the
+ * sites listed per function.  See INTEGRATION.md for the call-site patch.
+ *
+ * Conventions
+ *   - return value: ADLBQ_OK (0) or a negative ADLBQ_ERR_* code;
+ *   - no ownership of caller buffers; host pointers unless a name says _device;
+ *   - one caller thread per handle; calls are synchronous on return except
+ *     the _device variants, which are ordered on the handle's HIP stream;
+ *   - ranks are MPI world ranks exactly as in the reference (apps are
+ *     [0, num_app_ranks), servers follow: adlb.c:246-258, no debug server).
+ *
+ * Results are bit-identical to processing the same events one at a time
+ * through the reference handlers (tests/test_gpu_parity.py).
+ */
+#ifndef ADLBQ_H
+#define ADLBQ_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADLBQ_OK                 0
+#define ADLBQ_ERR_ARG           -1   /* bad argument / handle */
+#define ADLBQ_ERR_HIP           -2   /* HIP runtime failure (message via adlbq_last_error) */
+#define ADLBQ_ERR_NOMEM         -3
+#define ADLBQ_ERR_TYPE          -4   /* work type not declared at create (ADLBP_Put aborts: adlb.c:2762) */
+#define ADLBQ_ERR_UNSUPPORTED   -5   /* e.g. more than ADLBQ_MAX_TYPES types */
+
+#define ADLBQ_MAX_TYPES          64  /* request type sets are 64-bit masks on the device */
+#define ADLBQ_REQ_TYPES          16  /* REQ_TYPE_VECT_SZ, src/xq.h:37 */
+#define ADLBQ_RESP_INTS          12  /* TA_RESERVE_RESP int[12], src/adlb.c:1213-1222 */
+#define ADLBQ_PUT_INTS            9
+#define ADLBQ_RESERVE_INTS       18
+#define ADLBQ_LOWEST_PRIO  (-999999999) /* ADLB_LOWEST_PRIO, include/adlb/adlb.h:22 */
+
+typedef struct adlbq_server adlbq_server;
+
+/* Replaces the per-server queue setup of ADLBP_Init (src/adlb.c:295-320:
+ * wq/rq/iq/tq/cq = xq_create(), qmstat_tbl rows = LOWEST, next_wqseqno = 1,
+ * next_rqseqno = 1, rfr_to_rank = -1, rfr_out = 0).  max_units is a sizing hint
+ * for HBM (the store grows on demand).  device = HIP device ordinal. */
+int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_app_ranks,
+                 int num_servers, int my_server_idx, long long max_units, int device);
+int adlbq_destroy(adlbq_server *h);
+
+/* FA_PUT_HDR after the payload arrived, for n Puts in arrival order
+ * (src/adlb.c:963-1046: wq_node_create(next_wqseqno++) + wq_append, then
+ * rq_find_rank_queued_for_type(target_rank, work_type) and pin on a hit).
+ * units9[i] = {work_type, work_prio, answer_rank, target_rank, work_len,
+ *              home_server_rank, common_len, common_server_rank, common_seqno}
+ * (the FA_PUT_HDR info_buf fields, adlb.c:903-970).
+ * out3[i]   = {wqseqno, matched_rank or -1, matched_rqseqno or -1}; on a match
+ * the caller sends TA_RESERVE_RESP to matched_rank (adlb.c:996-1008). */
+int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3);
+
+/* n FA_RESERVE messages in arrival order (src/adlb.c:1199-1317): for each,
+ * wq_find_pre_targeted_hi_prio(rank) then wq_find_hi_prio (xq.c:190-247), pin
+ * on a hit; otherwise park on rq (hang) with the RFR donor choice of
+ * find_cand_rank_with_worktype (adlb.c:1278-1309, 3487-3534), or NO_CURR_WORK.
+ * reqs18[i]  = {from_rank, hang_flag, req_types[16]}  (FA_RESERVE's int[17]
+ *              buffer, adlb.c:2903-2923, prefixed with the sender rank).
+ * resp12[i]  = TA_RESERVE_RESP {rc, type, prio, len, answer_rank, wqseqno,
+ *              server_rank, common_len, common_server, common_seqno} with
+ *              rc = 1 (SUCCESS) / -2 (NO_CURR_WORK) / 0 (parked), and
+ *              [10] = rqseqno if parked, [11] = server rank an SS_RFR goes to
+ *              (-1 if none). */
+int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12);
+
+/* Same, with reqs18/resp12 in device memory, enqueued on the handle's stream
+ * (no host synchronisation).  Used when requests are staged in HBM. */
+int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int *d_resp12);
+
+/* FA_GET_RESERVED (src/adlb.c:1347-1381): wq_find_pinned_for_rank(rank, wqseqno)
+ * (xq.c:249-264) then wq_delete.  out5 = {rc (1 / -1 not found), work_len,
+ * work_type, work_prio, answer_rank}. */
+int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5);
+
+/* SS_UNRESERVE (src/adlb.c:2057-2063): pin_rank = new_pin_rank, pinned = 0. */
+int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, int *found);
+
+/* n SS_UNRESERVEs with device-resident (rank, wqseqno, new_pin) triples. */
+int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples);
+
+/* update_local_state (src/adlb.c:3581-3593): qlen = wq_get_num_unpinned_untargeted
+ * (xq.c:298-311), type_hi_prio[t] = wq_get_avail_hi_prio_of_type(user_types[t])
+ * (xq.c:313-329); also stored as this server's qmstat row. */
+int adlbq_qmstat_row(adlbq_server *h, int *qlen, int *type_hi_prio);
+
+/* The SS_QMSTAT ring hop's unpack of another server's row (adlb.c:1716-1728). */
+int adlbq_set_qmstat_row(adlbq_server *h, int server_idx, int qlen, double nbytes_used,
+                         const int *type_hi_prio);
+
+/* check_remote_work_for_queued_apps (src/adlb.c:3536-3579): for each parked
+ * Reserve in FIFO order without an outstanding RFR, the first type with a donor
+ * (tq_find_first_rt, else qmstat argmax) gets an SS_RFR.  out3[k] = {rqseqno,
+ * for_rank, donor_server_rank}; *count = k (at most cap). */
+int adlbq_check_remote(adlbq_server *h, int cap, int *out3, int *count);
+
+/* SS_RFR_RESP bookkeeping (src/adlb.c:1877-1878). */
+int adlbq_rfr_done(adlbq_server *h, int from_server_rank, int for_rank);
+
+/* FA_DID_PUT_AT_REMOTE's tq update (src/adlb.c:1167-1178); the caller then
+ * runs adlbq_check_remote like adlb.c:1179. */
+int adlbq_tq_add(adlbq_server *h, int app_rank, int work_type, int server_rank);
+
+/* Remove a parked Reserve by rqseqno (rq_find_seqno + rq_delete, adlb.c:1883-1933). */
+int adlbq_rq_delete(adlbq_server *h, int rqseqno, int *found);
+
+/* Memory-pressure push choice (src/adlb.c:513-528): the first unpinned unit
+ * (wq_find_unpinned, xq.c:266-281) and the server with the smallest
+ * nbytes_used below threshold (strict <, lowest index wins).  -1 when none. */
+int adlbq_push_select(adlbq_server *h, double threshold, int *cand_server_rank, int *wqseqno);
+
+/* Counters: wq->count, wq->max_count (ADLB_INFO_MAX_WQ_COUNT, adlb.c:3135), rq->count. */
+int adlbq_info(adlbq_server *h, int *wq_count, int *wq_max_count, int *rq_count);
+
+/* FA_INFO_NUM_WORK_UNITS (src/adlb.c:2466-2496). */
+int adlbq_info_type(adlbq_server *h, int work_type, int *max_prio, int *num_max_prio,
+                    int *num_type);
+
+/* Stream / timing plumbing. */
+int  adlbq_set_stream(adlbq_server *h, void *hip_stream); /* NULL = handle's own stream */
+void *adlbq_get_stream(adlbq_server *h);
+int  adlbq_sync(adlbq_server *h);
+/* Per-stage GPU time (HIP events on the handle's stream) when enabled:
+ * stage names: "hist", "select", "sort", "targeted", "chain", "finalize". */
+int  adlbq_profile_enable(adlbq_server *h, int on);
+int  adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, long long *launches);
+/* Bytes the last reserve batch's open-bucket scan touched algorithmically:
+ * 16 B x live units. */
+long long adlbq_last_scan_units(adlbq_server *h);
+const char *adlbq_last_error(void);
+const char *adlbq_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

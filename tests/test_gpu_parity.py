@@ -1,0 +1,122 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the reference.
+
+* golden fixtures (expected streams generated from the reference's src/xq.c):
+  the ABI replay must reproduce them bit for bit;
+* fresh seeded traces at medium sizes: ABI replay == oracle replay;
+* BASELINE sizes (10M-unit queue, 64K Reserves): the exact stability check of
+  tests/exact_check.py (equivalent to sequential xq matching).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from adlb_amd import replay, synth
+from adlb_amd.server import Server
+from exact_check import check_batch
+
+pytestmark = pytest.mark.gpu
+GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+
+
+def run_abi(ut, cfg, trace, max_units=1 << 16):
+    with Server(ut, int(cfg[0]), int(cfg[1]), int(cfg[2]), max_units=max_units) as s:
+        return replay.replay(s, trace)
+
+
+def run_oracle(ut, cfg, trace):
+    o = oracle.Oracle("own")
+    o.init(ut, int(cfg[0]), int(cfg[1]), int(cfg[2]))
+    return o.replay(trace)
+
+
+def assert_same(got, exp):
+    assert got.size == exp.size, (got.size, exp.size)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"first mismatch at output int {bad[0]}: got {got[bad[0]]} expected {exp[bad[0]]}"
+
+
+@pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p)[:-4] for p in GOLD])
+def test_golden(gpu_available, path):
+    d = np.load(path, allow_pickle=False)
+    assert_same(run_abi(d["user_types"], d["cfg"], d["trace"]), d["expected"])
+
+
+CASES = {
+    "c2_n200k_r16k": lambda: synth.config2(n_units=200_000, n_reserves=16_384, seed=201),
+    "c2_eq_n200k_r16k": lambda: synth.config2(n_units=200_000, n_reserves=16_384, seed=202, equal_prio=True),
+    "c2_t1": lambda: synth.config2(n_units=50_000, n_types=1, n_reserves=8192, seed=203),
+    "c2_t64_wide": lambda: synth.config2(n_units=100_000, n_types=64, n_reserves=8192, seed=204,
+                                         prio_hi=1 << 20),
+    "c2_exhaust": lambda: synth.config2(n_units=5_000, n_reserves=8192, seed=205, prio_hi=16),
+    "c2_exhaust_nohang": lambda: synth.config2(n_units=5_000, n_reserves=8192, seed=206, hang=0),
+    "c4_n200k": lambda: synth.config4(n_units=200_000, n_reserves=8192, n_ranks=256, seed=207),
+    "c4_t8_tied": lambda: synth.config4(n_units=100_000, n_types=8, n_reserves=8192, n_ranks=64, seed=208,
+                                        prio_hi=4),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_fresh_vs_oracle(gpu_available, name):
+    w = CASES[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    assert_same(run_abi(w.user_types, cfg, tr, max_units=w.n_units), run_oracle(w.user_types, cfg, tr))
+
+
+def test_stream_vs_oracle(gpu_available):
+    o = oracle.Oracle("own")
+    o.init([1, 2], 128, 8, 3)
+    tr = synth.config5_stream(lambda ev: synth.split_outputs(o.replay(ev)), n_rounds=400, n_ranks=128,
+                              n_servers=8, my_idx=3, seed=501)
+    cfg = (128, 8, 3)
+    assert_same(run_abi([1, 2], cfg, tr), run_oracle([1, 2], cfg, tr))
+
+
+def _exact_full(w, batches=1):
+    with Server(w.user_types, w.num_app_ranks, max_units=w.n_units) as s:
+        units = np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len,
+                          np.full(w.n_units, -1), np.zeros(w.n_units), np.full(w.n_units, -1),
+                          np.full(w.n_units, -1)], axis=1).astype(np.int32)
+        s.put_batch(units)
+        reqs = np.concatenate([w.r_rank[:, None], w.r_hang[:, None].astype(np.int32), w.r_types],
+                              axis=1).astype(np.int32)
+        seq = np.arange(1, w.n_units + 1)
+        avail = np.ones(w.n_units, bool)
+        first = None
+        for b in range(batches):
+            resp = s.reserve_batch(reqs)
+            check_batch(w.user_types, w.u_type, w.u_prio, w.u_target, seq, avail, w.r_rank, w.r_types,
+                        w.r_hang, resp)
+            if first is None:
+                first = resp.copy()
+            else:
+                assert np.array_equal(first, resp), "same state + same batch must give the same answer"
+            m = np.nonzero(resp[:, 0] == 1)[0]
+            # return the units (SS_UNRESERVE) so the next batch sees the same queue
+            if m.size:
+                import torch
+                trip = torch.tensor(np.stack([w.r_rank[m], resp[m, 5], np.full(m.size, -1)], axis=1)
+                                    .astype(np.int32).ravel(), device="cuda")
+                torch.cuda.synchronize()  # the handle's stream does not order after torch's
+                s.unreserve_batch_device(m.size, trip.data_ptr())
+                s.sync()
+        return first
+
+
+def test_full_size_config2_exact(gpu_available):
+    w = synth.config2(n_units=10_000_000, n_reserves=65_536, seed=7)
+    resp = _exact_full(w, batches=2)
+    assert (resp[:, 0] == 1).all()
+
+
+def test_full_size_config2_equal_prio_exact(gpu_available):
+    w = synth.config2(n_units=10_000_000, n_reserves=65_536, seed=8, equal_prio=True)
+    _exact_full(w)
+
+
+def test_config4_2m_exact(gpu_available):
+    w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
+    _exact_full(w)
