@@ -41,7 +41,8 @@ struct DevCounters {
     int rq_hwm;        // rq->max_count
     int rq_head;       // lowest rq slot that may be alive
     int n_parked_last; // parked by the last reserve batch
-    int pad[3];
+    int chain_rounds;  // Jacobi rounds of the last chain (diagnostic)
+    int pad[2];
 };
 
 struct Bucket {
@@ -100,7 +101,7 @@ struct adlbq_server {
 
     // ---- parked reserves
     int rq_cap = 0;
-    int *d_rq_rank = nullptr, *d_rq_types = nullptr, *d_rq_live = nullptr;
+    int *d_rq_rank = nullptr, *d_rq_types = nullptr, *d_rq_live = nullptr, *d_rq_req = nullptr;
     adlbq::DevCounters *d_ctr = nullptr;
     adlbq::DevCounters ctr{};      // host copy
     bool ctr_stale = false;
@@ -125,6 +126,7 @@ struct adlbq_server {
     int *d_candoff = nullptr, *d_candlen = nullptr, *d_needsort = nullptr;  // [T]
     int *d_binoff = nullptr;           // [T*NB]
     unsigned short *d_gh = nullptr; long long cap_gh = 0;   // [open pages][T*NB]
+    unsigned int *d_pp = nullptr;                           // [open pages][T*NB] column prefix
     unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] -> exclusive prefix in place
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
     int *d_cslot = nullptr, *d_cslot2 = nullptr;

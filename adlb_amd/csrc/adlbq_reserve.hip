@@ -116,10 +116,15 @@ __global__ __launch_bounds__(1024) void k_thresholds(int T, const int *__restric
     const int C = T * NB;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         unsigned int run = 0;
-        for (int k = 0; k < nchunks; k++) {
-            unsigned int v = csum[(long long)k * C + c];
-            csum[(long long)k * C + c] = run;  // exclusive prefix over chunks, in place
-            run += v;
+        for (int k0 = 0; k0 < nchunks; k0 += 16) {
+            unsigned int v[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) v[q] = k0 + q < nchunks ? csum[(long long)(k0 + q) * C + c] : 0u;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                if (k0 + q < nchunks) csum[(long long)(k0 + q) * C + c] = run;  // exclusive prefix, in place
+                run += v[q];
+            }
         }
         tot[c] = run;
     }
@@ -167,12 +172,34 @@ __global__ __launch_bounds__(1024) void k_thresholds(int T, const int *__restric
     }
 }
 
+// ---------------------------------------------------------------- per-page column prefix
+// pp[p][c] = rank, in wqseqno order over the open bucket, of page p's first unit
+// in column c (= type, bin); only the columns a type takes (bin <= theta).
+__global__ __launch_bounds__(256) void k_page_prefix(int npages, int T, const int *__restrict__ theta,
+                                                     const unsigned short *__restrict__ gh,
+                                                     const unsigned int *__restrict__ csum,
+                                                     unsigned int *__restrict__ pp) {
+    const int C = T * NB;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nchunks = (npages + CHUNK - 1) / CHUNK;
+    if (i >= (long long)nchunks * C) return;
+    const int k = (int)(i / C), c = (int)(i - (long long)k * C);
+    const int t = c / NB, b = c - t * NB;
+    if (b > theta[t]) return;
+    unsigned int run = csum[(long long)k * C + c];
+    const int p1 = min(npages, (k + 1) * CHUNK);
+    for (int p = k * CHUNK; p < p1; p++) {
+        pp[(long long)p * C + c] = run;
+        run += gh[(long long)p * C + c];
+    }
+}
+
 // ---------------------------------------------------------------- pass 2
 __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
     const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
     const int *__restrict__ theta, const int *__restrict__ need, const int *__restrict__ candoff,
-    const int *__restrict__ binoff, const unsigned short *__restrict__ gh, const unsigned int *__restrict__ csum,
+    const int *__restrict__ binoff, const unsigned int *__restrict__ pp,
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot) {
     extern __shared__ unsigned int lds[];
     __shared__ long long sanc[ADLBQ_MAX_TYPES];
@@ -189,13 +216,9 @@ __global__ __launch_bounds__(256) void k_select_open(
     if (p >= npages) return;
     // running rank of each (type, bin) column, in wqseqno order over the whole open bucket
     unsigned int *run = lds + w * C;
-    const int k0 = (p / CHUNK) * CHUNK;
     for (int c = lane; c < C; c += 64) {
         const int t = c / NB, b = c - t * NB;
-        if (b > sth[t]) continue;
-        unsigned int r = csum[(long long)(p / CHUNK) * C + c];
-        for (int q = k0; q < p; q++) r += gh[(long long)q * C + c];
-        run[c] = r;
+        if (b <= sth[t]) run[c] = pp[(long long)p * C + c];
     }
     __builtin_amdgcn_wave_barrier();
     const long long base = (long long)pages[p] << PAGE_SHIFT;
@@ -422,54 +445,116 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
 }
 
 // ---------------------------------------------------------------- untargeted choices in arrival order
-template <int WID>
+//
+// One wavefront walks the untargeted Reserves in blocks of 64 (lane = request).
+// At a block start the number of candidates already consumed from every type,
+// c0[t], is exact.  Inside the block each lane's choice depends only on the
+// choices of lower lanes (how many of them took each type), so the block is
+// solved by Jacobi rounds: every lane recomputes its choice from the current
+// choices of lower lanes (ballot + mbcnt per type) until nothing changes.  The
+// fixed point is the sequential result (lane 0 is exact in round 1, lane k by
+// round k+1), and it is reached in ~5 rounds for config 2 (max 65).
+//
+// Candidate keys come from a per-type ring in LDS holding absolute candidate
+// positions [c0[t], c0[t] + 128).  A block consumes at most 64 in total, so the
+// refill for the block after next is one load per lane, issued at a block end
+// and written to LDS at the next block end (global latency hidden by a block).
+constexpr int RING = 128;
+
+__device__ __forceinline__ unsigned int mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned int)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)m, 0u));
+}
+
+__device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+    return v;
+}
+
 __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restrict__ mask,
                                               const int *__restrict__ tmatch, int R, int T,
                                               const int *__restrict__ candoff, const int *__restrict__ candlen,
                                               const unsigned long long *__restrict__ ckey,
-                                              const int *__restrict__ cslot, int *__restrict__ umatch) {
+                                              int *__restrict__ umatch, int *__restrict__ rounds_out) {
+    extern __shared__ unsigned long long ring[];  // [T][RING]
     const int lane = threadIdx.x;
-    const bool act = lane < T;
-    const int off = act ? candoff[lane] : 0, len = act ? candlen[lane] : 0;
-    int c = 0;
-    unsigned long long cur = len > 0 ? ckey[off] : 0ull, nxt = len > 1 ? ckey[off + 1] : 0ull;
-    int cs = len > 0 ? cslot[off] : -1, ns = len > 1 ? cslot[off + 1] : -1;
-    for (int j0 = 0; j0 < R; j0 += 64) {
-        const int jj = j0 + lane;
-        const unsigned long long mj = jj < R ? mask[jj] : 0ull;
-        const int tj = jj < R ? tmatch[jj] : 0;
-        int res = -1;
-        const int kmax = min(64, R - j0);
-        for (int k = 0; k < kmax; k++) {
-            if (__builtin_amdgcn_readlane(tj, k) >= 0) continue;  // satisfied by its targeted units
-            const unsigned long long mk = readlane64(mj, k);
-            const unsigned long long v = (act && ((mk >> lane) & 1ull)) ? cur : 0ull;
-            unsigned long long bv = v;
-#pragma unroll
-            for (int o = WID / 2; o > 0; o >>= 1) {
-                unsigned long long w2 = __shfl_xor(bv, o, 64);
-                bv = bv > w2 ? bv : w2;
-            }
-            bv = readlane64(bv, 0);
-            if (bv == 0) continue;
-            const int wl = __ffsll((long long)__ballot(v == bv)) - 1;
-            const int s = __builtin_amdgcn_readlane(cs, wl);
-            if (lane == k) res = s;
-            if (lane == wl) {
-                c++;
-                cur = nxt;
-                cs = ns;
-                nxt = c + 1 < len ? ckey[off + c + 1] : 0ull;
-                ns = c + 1 < len ? cslot[off + c + 1] : -1;
-            }
-        }
-        if (jj < R) umatch[jj] = res;
+    // lane t keeps type t's state; uniform copies come from readlane
+    const int my_off = lane < T ? candoff[lane] : 0;
+    const int my_len = lane < T ? candlen[lane] : 0;
+    int my_c0 = 0;
+    for (int t = 0; t < T; t++) {
+        const int off = __builtin_amdgcn_readlane(my_off, t), len = __builtin_amdgcn_readlane(my_len, t);
+        for (int i = lane; i < RING; i += 64) ring[t * RING + i] = i < len ? ckey[off + i] : 0ull;
     }
+    __syncthreads();
+    // pending ring refill (issued at the previous block end)
+    unsigned long long pend_key = 0;
+    int pend_addr = -1;
+    int total_rounds = 0;
+    for (int b0 = 0; b0 < R; b0 += 64) {
+        const int j = b0 + lane;
+        const unsigned long long m = (j < R && tmatch[j] < 0) ? mask[j] : 0ull;
+        const unsigned long long U = wave_or_u64(m);
+        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
+        int res = -1;
+        unsigned long long changed;
+        do {
+            int nch = -1, npos = -1;
+            unsigned long long best = 0;
+            for (unsigned long long bb = U; bb; bb &= bb - 1) {
+                const int t = __ffsll((long long)bb) - 1;
+                const unsigned long long Bt = __ballot(ch == t);
+                if ((m >> t) & 1ull) {
+                    const int pos = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(Bt);
+                    if (pos < __builtin_amdgcn_readlane(my_len, t)) {
+                        const unsigned long long k = ring[t * RING + (pos & (RING - 1))];
+                        if (k > best) {
+                            best = k;
+                            nch = t;
+                            npos = pos;
+                        }
+                    }
+                }
+            }
+            changed = __ballot(nch != ch);
+            ch = nch;
+            res = npos;
+            total_rounds++;
+        } while (changed);
+        // results: global candidate index of what each lane took
+        const int choff = __shfl(my_off, ch < 0 ? 0 : ch, 64);  // candoff of the chosen type
+        if (j < R) umatch[j] = ch >= 0 ? choff + res : -1;
+        // block end: write last block's refill, advance c0, issue the next refill
+        __builtin_amdgcn_wave_barrier();
+        if (pend_addr >= 0) ring[pend_addr] = pend_key;
+        int pre = 0, my_t = -1, my_k = 0;
+        for (unsigned long long bb = U; bb; bb &= bb - 1) {
+            const int t = __ffsll((long long)bb) - 1;
+            const int cnt = __popcll(__ballot(ch == t));
+            if (!cnt) continue;
+            const int c0t = __builtin_amdgcn_readlane(my_c0, t);
+            if (lane >= pre && lane < pre + cnt) {
+                my_t = t;
+                my_k = c0t + RING + (lane - pre);  // absolute position entering the ring
+            }
+            pre += cnt;
+            if (lane == t) my_c0 += cnt;
+        }
+        const int tl = my_t < 0 ? 0 : my_t;
+        const int len = __shfl(my_len, tl, 64), off = __shfl(my_off, tl, 64);
+        pend_addr = -1;
+        if (my_t >= 0) {
+            pend_key = my_k < len ? ckey[off + my_k] : 0ull;
+            pend_addr = my_t * RING + (my_k & (RING - 1));
+        }
+    }
+    if (lane == 0 && rounds_out) *rounds_out = total_rounds;
 }
 
 // ---------------------------------------------------------------- finalize
 __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, int R, const int *__restrict__ tmatch,
-                                                  const int *__restrict__ umatch, const int *__restrict__ prio,
+                                                  const int *__restrict__ umatch, const int *__restrict__ cslot,
+                                                  const int *__restrict__ prio,
                                                   uint32_t *meta, int *pin, const int *__restrict__ seqa,
                                                   const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
                                                   int my_world, int *__restrict__ resp) {
@@ -477,7 +562,7 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
     if (j >= R) return;
     const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
     const int rank = rq[0], hang = rq[1];
-    const int slot = tmatch[j] >= 0 ? tmatch[j] : umatch[j];
+    const int slot = tmatch[j] >= 0 ? tmatch[j] : (umatch[j] >= 0 ? cslot[umatch[j]] : -1);
     int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
     if (slot >= 0) {
         pin[slot] = rank;  // adlb.c:1210-1212
@@ -502,47 +587,64 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
 }
 
 // ---------------------------------------------------------------- park on rq + RFR donor choice
-__global__ __launch_bounds__(64) void k_park(DonorCtx c, int donors, const int *__restrict__ reqs, int R,
-                                             const int *__restrict__ tmatch, const int *__restrict__ umatch,
-                                             int *rq_rank, int *rq_types, int *rq_live, DevCounters *ctr,
-                                             int *resp) {
-    const int lane = threadIdx.x;
-    int n = ctr->rq_n, live = ctr->rq_live, hwm = ctr->rq_hwm, np = 0;
-    const unsigned long long lt = lanemask_lt();
-    for (int j0 = 0; j0 < R; j0 += 64) {
-        const int j = j0 + lane;
-        const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
-        const bool parked = j < R && tmatch[j] < 0 && umatch[j] < 0 && rq[1] != 0;
-        const unsigned long long b = __ballot(parked);
-        if (!b) continue;
-        if (parked) {
-            const int pos = n + __popcll(b & lt);
-            rq_rank[pos] = rq[0];
-            for (int q = 0; q < NREQ; q++) rq_types[(long long)pos * NREQ + q] = rq[2 + q];
-            st_agent(rq_live + pos, 1);
-            resp[(long long)ADLBQ_RESP_INTS * j + 10] = pos + 1;  // rqseqno (next_rqseqno++, adlb.c:1244)
-        }
-        if (donors) {
-            for (unsigned long long bb = b; bb; bb &= bb - 1) {
-                const int l = __ffsll((long long)bb) - 1, jj = j0 + l;
-                const int *rr = reqs + (long long)ADLBQ_RESERVE_INTS * jj;
-                const int rank = rr[0];
-                int cand = -1;
-                if (rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) < 0)
-                    cand = rfr_select(c, rank, rr + 2);
-                if (lane == 0) resp[(long long)ADLBQ_RESP_INTS * jj + 11] = cand;
-            }
-        }
-        const int cnt = __popcll(b);
-        n += cnt;
-        live += cnt;
-        np += cnt;
-        hwm = live > hwm ? live : hwm;
+// One workgroup: parked requests are appended to rq in arrival order (block
+// prefix sum over per-thread contiguous chunks); the RFR donor choice, which
+// depends on earlier choices through rfr_out / rfr_to_rank, then walks the
+// newly parked entries in order on wave 0 (only when a donor can exist).
+__global__ __launch_bounds__(1024) void k_park(DonorCtx c, int donors, const int *__restrict__ reqs, int R,
+                                               const int *__restrict__ tmatch, const int *__restrict__ umatch,
+                                               int *rq_rank, int *rq_types, int *rq_live, int *rq_req,
+                                               DevCounters *ctr, int *resp) {
+    __shared__ int wsum[16];
+    __shared__ int s_n0, s_total;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nth = blockDim.x;
+    const int per = (R + nth - 1) / nth, lo = min(R, tid * per), hi = min(R, lo + per);
+    auto parked = [&](int j) {
+        return tmatch[j] < 0 && umatch[j] < 0 && reqs[(long long)ADLBQ_RESERVE_INTS * j + 1] != 0;
+    };
+    int cnt = 0;
+    for (int j = lo; j < hi; j++) cnt += parked(j);
+    // block exclusive scan of cnt
+    int x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    if (lane == 0) {
-        ctr->rq_n = n;
-        ctr->rq_live = live;
-        ctr->rq_hwm = hwm;
+    if (lane == 63) wsum[w] = x;
+    if (tid == 0) s_n0 = ctr->rq_n;
+    __syncthreads();
+    int wpre = 0;
+    for (int q = 0; q < w; q++) wpre += wsum[q];
+    if (tid == nth - 1) s_total = wpre + x;
+    int pos = s_n0 + wpre + x - cnt;
+    for (int j = lo; j < hi; j++) {
+        if (!parked(j)) continue;
+        const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
+        rq_rank[pos] = rq[0];
+        for (int q = 0; q < NREQ; q++) rq_types[(long long)pos * NREQ + q] = rq[2 + q];
+        rq_live[pos] = 1;
+        rq_req[pos] = j;
+        resp[(long long)ADLBQ_RESP_INTS * j + 10] = pos + 1;  // rqseqno (next_rqseqno++, adlb.c:1244)
+        pos++;
+    }
+    __threadfence();
+    __syncthreads();
+    const int n0 = s_n0, np = s_total;
+    if (donors && w == 0) {
+        for (int k = n0; k < n0 + np; k++) {
+            const int j = rq_req[k];
+            const int *rr = reqs + (long long)ADLBQ_RESERVE_INTS * j;
+            const int rank = rr[0];
+            int cand = -1;
+            if (rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) < 0) cand = rfr_select(c, rank, rr + 2);
+            if (lane == 0) resp[(long long)ADLBQ_RESP_INTS * j + 11] = cand;
+        }
+    }
+    if (tid == 0) {
+        ctr->rq_n = n0 + np;
+        ctr->rq_live += np;
+        if (ctr->rq_live > ctr->rq_hwm) ctr->rq_hwm = ctr->rq_live;
         ctr->n_parked_last = np;
     }
 }
@@ -574,8 +676,10 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         AQ_HIP(hipStreamSynchronize(h->stream));
     if (need_gh > h->cap_gh) {
         if (h->d_gh) AQ_HIP(hipFree(h->d_gh));
+        if (h->d_pp) AQ_HIP(hipFree(h->d_pp));
         h->cap_gh = std::max(need_gh, 2 * h->cap_gh);
         AQ_HIP(hipMalloc((void **)&h->d_gh, sizeof(unsigned short) * h->cap_gh));
+        AQ_HIP(hipMalloc((void **)&h->d_pp, sizeof(unsigned int) * h->cap_gh));
     }
     if (need_cs > h->cap_csum) {
         if (h->d_csum) AQ_HIP(hipFree(h->d_csum));
@@ -621,9 +725,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                                                h->d_need, h->d_candoff, h->d_candlen,
                                                                h->d_needsort, h->d_binoff);
         stage_begin(h, "select", &ev);
+        const long long ncol = (long long)nchunks * C;
+        k_page_prefix<<<(int)((ncol + 255) / 256), 256, 0, s>>>(np, T, h->d_theta, h->d_gh, h->d_csum, h->d_pp);
         k_select_open<<<(np + 3) / 4, 256, sizeof(unsigned int) * 4 * C, s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
-            h->d_need, h->d_candoff, h->d_binoff, h->d_gh, h->d_csum, h->d_ckey, h->d_cslot);
+            h->d_need, h->d_candoff, h->d_binoff, h->d_pp, h->d_ckey, h->d_cslot);
         stage_end(h, "select", ev);
         stage_begin(h, "sort", &ev);
         k_sort_types<<<T, 1024, 0, s>>>(h->d_needsort, h->d_candoff, h->d_candlen, h->d_ckey, h->d_cslot,
@@ -644,25 +750,16 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_end(h, "targeted", ev);
     }
     stage_begin(h, "chain", &ev);
-    int wid = 1;
-    while (wid < T) wid <<= 1;
-    switch (wid) {
-#define CHAIN(W)                                                                                              \
-    case W:                                                                                                   \
-        k_chain<W><<<1, 64, 0, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey,      \
-                                    h->d_cslot, h->d_umatch);                                                 \
-        break;
-        CHAIN(1) CHAIN(2) CHAIN(4) CHAIN(8) CHAIN(16) CHAIN(32) CHAIN(64)
-#undef CHAIN
-    default: return fail(ADLBQ_ERR_UNSUPPORTED, "too many types");
-    }
+    k_chain<<<1, 64, sizeof(unsigned long long) * RING * std::max(T, 1), s>>>(
+        h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_umatch, &h->d_ctr->chain_rounds);
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);
-    k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_prio, h->d_meta, h->d_pin,
+    k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
+                                               h->d_meta, h->d_pin,
                                                h->d_seq, h->d_cold0, h->d_cold1, h->my_world, d_resp);
     const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
-    k_park<<<1, 64, 0, s>>>(donor_ctx(h), donors, d_reqs, R, h->d_tmatch, h->d_umatch, h->d_rq_rank,
-                            h->d_rq_types, h->d_rq_live, h->d_ctr, d_resp);
+    k_park<<<1, 1024, 0, s>>>(donor_ctx(h), donors, d_reqs, R, h->d_tmatch, h->d_umatch, h->d_rq_rank,
+                              h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_ctr, d_resp);
     stage_end(h, "finalize", ev);
     AQ_HIP(hipGetLastError());
     h->ctr_stale = true;

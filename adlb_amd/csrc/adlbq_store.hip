@@ -69,6 +69,7 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
     if ((rc = grow(&h->d_rq_rank, h->rq_cap, nc, h->stream))) return rc;
     if ((rc = grow(&h->d_rq_types, (long long)h->rq_cap * NREQ, nc * NREQ, h->stream))) return rc;
     if ((rc = grow(&h->d_rq_live, h->rq_cap, nc, h->stream, 0))) return rc;
+    if ((rc = grow(&h->d_rq_req, h->rq_cap, nc, h->stream))) return rc;
     h->rq_cap = (int)nc;
     return ADLBQ_OK;
 }
@@ -505,9 +506,9 @@ int adlbq_destroy(adlbq_server *h) {
     void *ptrs[] = {h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_open_pages,
                     h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_all_pages,
                     h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_utypes, h->d_rq_rank, h->d_rq_types,
-                    h->d_rq_live, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
+                    h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
-                    h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_gh, h->d_csum,
+                    h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_gh, h->d_pp, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_result};
     for (void *p : ptrs)
         if (p) hipFree(p);

@@ -88,6 +88,9 @@ def event_nargs(op: int, ntypes: int) -> int:
 def output_bound(tr: np.ndarray, ntypes: int) -> int:
     """Upper bound on replay output ints (the replay mutates state, so the buffer
     must be big enough the first time)."""
+    for op, w in ((OP_PUT, 10), (OP_RESERVE, 19)):   # fast path: a pure run of one event kind
+        if tr.size and tr.size % w == 0 and (tr[::w] == op).all():
+            return 1024 + (tr.size // w) * (2 + max(12, ntypes + 1))
     ip, n_res, n_chk, n_ev = 0, 0, 0, 0
     trl = tr.tolist()
     while ip < len(trl):
