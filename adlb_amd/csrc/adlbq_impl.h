@@ -42,7 +42,8 @@ struct DevCounters {
     int rq_head;       // lowest rq slot that may be alive
     int n_parked_last; // parked by the last reserve batch
     int chain_rounds;  // Jacobi rounds of the last chain (diagnostic)
-    int pad[2];
+    int park_pending;  // parked requests counted by k_finalize for k_park
+    int pad[1];
 };
 
 struct Bucket {

@@ -471,6 +471,7 @@ __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) 
     return v;
 }
 
+template <int TB>  // types handled per unrolled group (reads issued together, then compared)
 __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restrict__ mask,
                                               const int *__restrict__ tmatch, int R, int T,
                                               const int *__restrict__ candoff, const int *__restrict__ candlen,
@@ -487,32 +488,50 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
         for (int i = lane; i < RING; i += 64) ring[t * RING + i] = i < len ? ckey[off + i] : 0ull;
     }
     __syncthreads();
-    // pending ring refill (issued at the previous block end)
-    unsigned long long pend_key = 0;
-    int pend_addr = -1;
     int total_rounds = 0;
+    // software pipeline: the next block's inputs are loaded before the refill
+    // load; the prologue issues the same three loads in the same order so the
+    // loop header's wait is vmcnt(1) on both incoming edges
+    unsigned long long m_next = mask[min(lane, R - 1)];
+    int t_next = tmatch[min(lane, R - 1)];
+    unsigned long long pend_key = ckey[0];  // ring refill issued at the previous block end
+    bool pend_zero = true;
+    int pend_addr = -1;
     for (int b0 = 0; b0 < R; b0 += 64) {
         const int j = b0 + lane;
-        const unsigned long long m = (j < R && tmatch[j] < 0) ? mask[j] : 0ull;
-        const unsigned long long U = wave_or_u64(m);
+        const unsigned long long m = (j < R && t_next < 0) ? m_next : 0ull;
+        unsigned long long U = 0;  // types present in the block (T ballots, no LDS traffic)
+        for (int t = 0; t < T; t++) U |= (unsigned long long)(__ballot((m >> t) & 1ull) != 0) << t;
         int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
         int res = -1;
         unsigned long long changed;
         do {
             int nch = -1, npos = -1;
             unsigned long long best = 0;
-            for (unsigned long long bb = U; bb; bb &= bb - 1) {
-                const int t = __ffsll((long long)bb) - 1;
-                const unsigned long long Bt = __ballot(ch == t);
-                if ((m >> t) & 1ull) {
-                    const int pos = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(Bt);
-                    if (pos < __builtin_amdgcn_readlane(my_len, t)) {
-                        const unsigned long long k = ring[t * RING + (pos & (RING - 1))];
-                        if (k > best) {
-                            best = k;
-                            nch = t;
-                            npos = pos;
+            for (int tb = 0; tb < T; tb += TB) {
+                if (!((U >> tb) & ((TB >= 64) ? ~0ull : ((1ull << TB) - 1)))) continue;
+                unsigned long long kk[TB];
+                int pp[TB];
+#pragma unroll
+                for (int q = 0; q < TB; q++) {
+                    const int t = tb + q;
+                    kk[q] = 0;
+                    pp[q] = -1;
+                    if (t < T && ((U >> t) & 1ull)) {
+                        const unsigned long long Bt = __ballot(ch == t);
+                        const int pos = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(Bt);
+                        if (((m >> t) & 1ull) && pos < __builtin_amdgcn_readlane(my_len, t)) {
+                            kk[q] = ring[t * RING + (pos & (RING - 1))];
+                            pp[q] = pos;
                         }
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < TB; q++) {
+                    if (kk[q] > best) {
+                        best = kk[q];
+                        nch = tb + q;
+                        npos = pp[q];
                     }
                 }
             }
@@ -521,12 +540,16 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
             res = npos;
             total_rounds++;
         } while (changed);
-        // results: global candidate index of what each lane took
         const int choff = __shfl(my_off, ch < 0 ? 0 : ch, 64);  // candoff of the chosen type
         if (j < R) umatch[j] = ch >= 0 ? choff + res : -1;
-        // block end: write last block's refill, advance c0, issue the next refill
+        // block end.  Memory-op order matters for vmcnt: the next block's inputs
+        // are loaded before the ring refill, both unconditionally, so the next
+        // block start waits only for its inputs (vmcnt(1)), not for the refill.
+        const int jn = min(j + 64, R - 1);
+        m_next = mask[jn];
+        t_next = tmatch[jn];  // lanes past R are masked by (j < R) at the next block start
         __builtin_amdgcn_wave_barrier();
-        if (pend_addr >= 0) ring[pend_addr] = pend_key;
+        if (pend_addr >= 0) ring[pend_addr] = pend_zero ? 0ull : pend_key;  // refill issued one block ago
         int pre = 0, my_t = -1, my_k = 0;
         for (unsigned long long bb = U; bb; bb &= bb - 1) {
             const int t = __ffsll((long long)bb) - 1;
@@ -542,11 +565,10 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
         }
         const int tl = my_t < 0 ? 0 : my_t;
         const int len = __shfl(my_len, tl, 64), off = __shfl(my_off, tl, 64);
-        pend_addr = -1;
-        if (my_t >= 0) {
-            pend_key = my_k < len ? ckey[off + my_k] : 0ull;
-            pend_addr = my_t * RING + (my_k & (RING - 1));
-        }
+        const bool valid = my_t >= 0 && my_k < len;
+        pend_key = ckey[valid ? off + my_k : 0];  // consumed one block later (no wait here)
+        pend_zero = !valid;
+        pend_addr = my_t >= 0 ? my_t * RING + (my_k & (RING - 1)) : -1;
     }
     if (lane == 0 && rounds_out) *rounds_out = total_rounds;
 }
@@ -557,7 +579,7 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   const int *__restrict__ prio,
                                                   uint32_t *meta, int *pin, const int *__restrict__ seqa,
                                                   const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
-                                                  int my_world, int *__restrict__ resp) {
+                                                  int my_world, int *__restrict__ resp, DevCounters *ctr) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R) return;
     const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
@@ -580,6 +602,8 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
         o[9] = c1.y;
     } else if (!hang) {
         o[0] = -2;  // NO_CURR_WORK
+    } else {
+        atomicAdd(&ctr->park_pending, 1);
     }
     int *out = resp + (long long)ADLBQ_RESP_INTS * j;
 #pragma unroll
@@ -598,6 +622,10 @@ __global__ __launch_bounds__(1024) void k_park(DonorCtx c, int donors, const int
     __shared__ int wsum[16];
     __shared__ int s_n0, s_total;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nth = blockDim.x;
+    if (ctr->park_pending == 0) {  // nothing parked (the common case): skip the scan
+        if (tid == 0) ctr->n_parked_last = 0;
+        return;
+    }
     const int per = (R + nth - 1) / nth, lo = min(R, tid * per), hi = min(R, lo + per);
     auto parked = [&](int j) {
         return tmatch[j] < 0 && umatch[j] < 0 && reqs[(long long)ADLBQ_RESERVE_INTS * j + 1] != 0;
@@ -642,6 +670,7 @@ __global__ __launch_bounds__(1024) void k_park(DonorCtx c, int donors, const int
         }
     }
     if (tid == 0) {
+        ctr->park_pending = 0;
         ctr->rq_n = n0 + np;
         ctr->rq_live += np;
         if (ctr->rq_live > ctr->rq_hwm) ctr->rq_hwm = ctr->rq_live;
@@ -750,13 +779,20 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_end(h, "targeted", ev);
     }
     stage_begin(h, "chain", &ev);
-    k_chain<<<1, 64, sizeof(unsigned long long) * RING * std::max(T, 1), s>>>(
-        h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_umatch, &h->d_ctr->chain_rounds);
+    {
+        const size_t lds = sizeof(unsigned long long) * RING * std::max(T, 1);
+        if (T <= 4)
+            k_chain<4><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey,
+                                          h->d_umatch, &h->d_ctr->chain_rounds);
+        else
+            k_chain<8><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey,
+                                          h->d_umatch, &h->d_ctr->chain_rounds);
+    }
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);
     k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
                                                h->d_meta, h->d_pin,
-                                               h->d_seq, h->d_cold0, h->d_cold1, h->my_world, d_resp);
+                                               h->d_seq, h->d_cold0, h->d_cold1, h->my_world, d_resp, h->d_ctr);
     const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
     k_park<<<1, 1024, 0, s>>>(donor_ctx(h), donors, d_reqs, R, h->d_tmatch, h->d_umatch, h->d_rq_rank,
                               h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_ctr, d_resp);
