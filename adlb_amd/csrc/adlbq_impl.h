@@ -131,6 +131,7 @@ struct adlbq_server {
     unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] -> exclusive prefix in place
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
     int *d_cslot = nullptr, *d_cslot2 = nullptr;
+    unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate
     int *d_result = nullptr;           // small result scratch (16 ints)
     int *h_result = nullptr;           // pinned host mirror
     long long last_scan_units = 0;

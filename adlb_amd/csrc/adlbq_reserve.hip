@@ -471,13 +471,47 @@ __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) 
     return v;
 }
 
-template <int TB>  // types handled per unrolled group (reads issued together, then compared)
+// Packed global rank of every candidate: (rank among all candidates of the
+// batch by (prio desc, wqseqno asc)) << 6 | type.  A smaller packed value is a
+// better unit, so the chain compares heads with one 32-bit min and reads the
+// winning type from the low bits.
+__global__ __launch_bounds__(256) void k_rank(int T, const int *__restrict__ candoff,
+                                              const int *__restrict__ candlen,
+                                              const unsigned long long *__restrict__ ckey,
+                                              unsigned int *__restrict__ crank) {
+    __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES];
+    for (int t = threadIdx.x; t <= T; t += blockDim.x) {
+        soff[t] = candoff[t];
+        if (t < T) slen[t] = candlen[t];
+    }
+    __syncthreads();
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < soff[T]; i += gridDim.x * blockDim.x) {
+        int t = 0;
+        while (t + 1 < T && soff[t + 1] <= i) t++;
+        const unsigned long long key = ckey[i];
+        unsigned int g = (unsigned int)(i - soff[t]);
+        for (int u = 0; u < T; u++) {
+            if (u == t) continue;
+            const unsigned long long *L = ckey + soff[u];
+            int a = 0, b = slen[u];
+            while (a < b) {  // first position whose key is not better than `key` (lists are descending)
+                const int mid = (a + b) >> 1;
+                if (L[mid] > key) a = mid + 1;
+                else b = mid;
+            }
+            g += (unsigned int)a;
+        }
+        crank[i] = (g << 6) | (unsigned int)t;
+    }
+}
+
+template <int TB>  // types handled per unrolled group (reads issued together, then reduced)
 __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restrict__ mask,
                                               const int *__restrict__ tmatch, int R, int T,
                                               const int *__restrict__ candoff, const int *__restrict__ candlen,
-                                              const unsigned long long *__restrict__ ckey,
+                                              const unsigned int *__restrict__ crank,
                                               int *__restrict__ umatch, int *__restrict__ rounds_out) {
-    extern __shared__ unsigned long long ring[];  // [T][RING]
+    extern __shared__ unsigned int ring32[];  // [T][RING] packed ranks
     const int lane = threadIdx.x;
     // lane t keeps type t's state; uniform copies come from readlane
     const int my_off = lane < T ? candoff[lane] : 0;
@@ -485,7 +519,7 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
     int my_c0 = 0;
     for (int t = 0; t < T; t++) {
         const int off = __builtin_amdgcn_readlane(my_off, t), len = __builtin_amdgcn_readlane(my_len, t);
-        for (int i = lane; i < RING; i += 64) ring[t * RING + i] = i < len ? ckey[off + i] : 0ull;
+        for (int i = lane; i < RING; i += 64) ring32[t * RING + i] = i < len ? crank[off + i] : ~0u;
     }
     __syncthreads();
     int total_rounds = 0;
@@ -494,7 +528,7 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
     // loop header's wait is vmcnt(1) on both incoming edges
     unsigned long long m_next = mask[min(lane, R - 1)];
     int t_next = tmatch[min(lane, R - 1)];
-    unsigned long long pend_key = ckey[0];  // ring refill issued at the previous block end
+    unsigned int pend_key = crank[0];  // ring refill issued at the previous block end
     bool pend_zero = true;
     int pend_addr = -1;
     for (int b0 = 0; b0 < R; b0 += 64) {
@@ -503,45 +537,36 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
         unsigned long long U = 0;  // types present in the block (T ballots, no LDS traffic)
         for (int t = 0; t < T; t++) U |= (unsigned long long)(__ballot((m >> t) & 1ull) != 0) << t;
         int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
-        int res = -1;
+        unsigned int best;
         unsigned long long changed;
         do {
-            int nch = -1, npos = -1;
-            unsigned long long best = 0;
+            best = ~0u;
             for (int tb = 0; tb < T; tb += TB) {
                 if (!((U >> tb) & ((TB >= 64) ? ~0ull : ((1ull << TB) - 1)))) continue;
-                unsigned long long kk[TB];
-                int pp[TB];
 #pragma unroll
                 for (int q = 0; q < TB; q++) {
                     const int t = tb + q;
-                    kk[q] = 0;
-                    pp[q] = -1;
                     if (t < T && ((U >> t) & 1ull)) {
-                        const unsigned long long Bt = __ballot(ch == t);
-                        const int pos = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(Bt);
-                        if (((m >> t) & 1ull) && pos < __builtin_amdgcn_readlane(my_len, t)) {
-                            kk[q] = ring[t * RING + (pos & (RING - 1))];
-                            pp[q] = pos;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int q = 0; q < TB; q++) {
-                    if (kk[q] > best) {
-                        best = kk[q];
-                        nch = tb + q;
-                        npos = pp[q];
+                        const int pos = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(__ballot(ch == t));
+                        const bool ok = ((m >> t) & 1ull) && pos < __builtin_amdgcn_readlane(my_len, t);
+                        const unsigned int v = ring32[t * RING + (pos & (RING - 1))];
+                        best = min(best, ok ? v : ~0u);
                     }
                 }
             }
+            const int nch = best == ~0u ? -1 : (int)(best & 63u);
             changed = __ballot(nch != ch);
             ch = nch;
-            res = npos;
             total_rounds++;
         } while (changed);
-        const int choff = __shfl(my_off, ch < 0 ? 0 : ch, 64);  // candoff of the chosen type
-        if (j < R) umatch[j] = ch >= 0 ? choff + res : -1;
+        // position of the chosen type for each lane, from the converged choices
+        int res = 0;
+        for (unsigned long long bb = U; bb; bb &= bb - 1) {
+            const int t = __ffsll((long long)bb) - 1;
+            const unsigned long long Bt = __ballot(ch == t);
+            if (ch == t) res = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(Bt) + __builtin_amdgcn_readlane(my_off, t);
+        }
+        if (j < R) umatch[j] = ch >= 0 ? res : -1;
         // block end.  Memory-op order matters for vmcnt: the next block's inputs
         // are loaded before the ring refill, both unconditionally, so the next
         // block start waits only for its inputs (vmcnt(1)), not for the refill.
@@ -549,7 +574,7 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
         m_next = mask[jn];
         t_next = tmatch[jn];  // lanes past R are masked by (j < R) at the next block start
         __builtin_amdgcn_wave_barrier();
-        if (pend_addr >= 0) ring[pend_addr] = pend_zero ? 0ull : pend_key;  // refill issued one block ago
+        if (pend_addr >= 0) ring32[pend_addr] = pend_zero ? ~0u : pend_key;  // refill issued one block ago
         int pre = 0, my_t = -1, my_k = 0;
         for (unsigned long long bb = U; bb; bb &= bb - 1) {
             const int t = __ffsll((long long)bb) - 1;
@@ -566,7 +591,7 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
         const int tl = my_t < 0 ? 0 : my_t;
         const int len = __shfl(my_len, tl, 64), off = __shfl(my_off, tl, 64);
         const bool valid = my_t >= 0 && my_k < len;
-        pend_key = ckey[valid ? off + my_k : 0];  // consumed one block later (no wait here)
+        pend_key = crank[valid ? off + my_k : 0];  // consumed one block later (no wait here)
         pend_zero = !valid;
         pend_addr = my_t >= 0 ? my_t * RING + (my_k & (RING - 1)) : -1;
     }
@@ -716,7 +741,7 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         AQ_HIP(hipMalloc((void **)&h->d_csum, sizeof(unsigned int) * h->cap_csum));
     }
     if (need_cand > h->cap_cand) {
-        void *ps[] = {h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2};
+        void *ps[] = {h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank};
         for (void *p : ps)
             if (p) AQ_HIP(hipFree(p));
         h->cap_cand = std::max(need_cand, 2 * h->cap_cand);
@@ -724,6 +749,7 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         AQ_HIP(hipMalloc((void **)&h->d_ckey2, sizeof(unsigned long long) * h->cap_cand));
         AQ_HIP(hipMalloc((void **)&h->d_cslot, sizeof(int) * h->cap_cand));
         AQ_HIP(hipMalloc((void **)&h->d_cslot2, sizeof(int) * h->cap_cand));
+        AQ_HIP(hipMalloc((void **)&h->d_crank, sizeof(unsigned int) * h->cap_cand));
     }
     return ADLBQ_OK;
 }
@@ -780,12 +806,14 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     stage_begin(h, "chain", &ev);
     {
-        const size_t lds = sizeof(unsigned long long) * RING * std::max(T, 1);
+        const size_t lds = sizeof(unsigned int) * RING * std::max(T, 1);
+        if (np > 0 && T > 0)
+            k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank);
         if (T <= 4)
-            k_chain<4><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey,
+            k_chain<4><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank,
                                           h->d_umatch, &h->d_ctr->chain_rounds);
         else
-            k_chain<8><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_ckey,
+            k_chain<8><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank,
                                           h->d_umatch, &h->d_ctr->chain_rounds);
     }
     stage_end(h, "chain", ev);
