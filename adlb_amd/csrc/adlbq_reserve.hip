@@ -543,16 +543,21 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
             best = ~0u;
             for (int tb = 0; tb < T; tb += TB) {
                 if (!((U >> tb) & ((TB >= 64) ? ~0ull : ((1ull << TB) - 1)))) continue;
+                // branch-free group: all LDS reads are issued before the first use
+                unsigned int vq[TB];
+                bool okq[TB];
 #pragma unroll
                 for (int q = 0; q < TB; q++) {
                     const int t = tb + q;
-                    if (t < T && ((U >> t) & 1ull)) {
-                        const int pos = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(__ballot(ch == t));
-                        const bool ok = ((m >> t) & 1ull) && pos < __builtin_amdgcn_readlane(my_len, t);
-                        const unsigned int v = ring32[t * RING + (pos & (RING - 1))];
-                        best = min(best, ok ? v : ~0u);
-                    }
+                    const int tt = t < T ? t : 0;
+                    const int c0t = __builtin_amdgcn_readlane(my_c0, tt);
+                    const int lent = t < T ? __builtin_amdgcn_readlane(my_len, tt) : 0;
+                    const int pos = c0t + (int)mbcnt64(__ballot(ch == t));
+                    okq[q] = (((m >> tt) & 1ull) != 0) & (pos < lent);
+                    vq[q] = ring32[tt * RING + (pos & (RING - 1))];
                 }
+#pragma unroll
+                for (int q = 0; q < TB; q++) best = min(best, okq[q] ? vq[q] : ~0u);
             }
             const int nch = best == ~0u ? -1 : (int)(best & 63u);
             changed = __ballot(nch != ch);

@@ -872,4 +872,19 @@ int adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, lon
 
 long long adlbq_last_scan_units(adlbq_server *h) { return h ? h->last_scan_units : 0; }
 
+long long adlbq_stat(adlbq_server *h, const char *name) {
+    if (!h || !name) return -1;
+    hipSetDevice(h->device);
+    if (refresh_counters(h)) return -1;
+    std::string n(name);
+    if (n == "chain_rounds") return h->ctr.chain_rounds;
+    if (n == "parked") return h->ctr.n_parked_last;
+    if (n == "candidates") {
+        int v = 0;
+        if (h->T > 0 && hipMemcpy(&v, h->d_candoff + h->T, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        return v;
+    }
+    return -1;
+}
+
 }  // extern "C"

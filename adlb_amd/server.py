@@ -176,5 +176,8 @@ class Server:
                    "adlbq_profile_read")
         return ms.value, n.value
 
+    def stat(self, name: str) -> int:
+        return int(self.lib.adlbq_stat(self.h, name.encode()))
+
     def last_scan_units(self) -> int:
         return int(self.lib.adlbq_last_scan_units(self.h))

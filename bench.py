@@ -189,6 +189,8 @@ def main():
             "scan_kernels_GBs": round(16 * live / (scan_ms * 1e-3) / 1e9, 1) if scan_ms else None,
         },
         "stages_ms": stages,
+        "chain_rounds_last_batch": srv.stat("chain_rounds"),
+        "candidates_last_batch": srv.stat("candidates"),
         "dominant_stage": dominant,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -137,6 +137,9 @@ int  adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, lo
 /* Bytes the last reserve batch's open-bucket scan touched algorithmically:
  * 16 B x live units. */
 long long adlbq_last_scan_units(adlbq_server *h);
+/* Diagnostics of the last reserve batch: "chain_rounds" (Jacobi rounds of the
+ * ordered-choice kernel), "parked" (Reserves parked), "candidates". -1 if unknown. */
+long long adlbq_stat(adlbq_server *h, const char *name);
 const char *adlbq_last_error(void);
 const char *adlbq_version(void);
 
