@@ -603,6 +603,89 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
     if (lane == 0 && rounds_out) *rounds_out = total_rounds;
 }
 
+// Small-T variant (T <= TB): every per-type quantity of a block is hoisted
+// into registers once per block (uniform values live in SGPRs), rounds are
+// straight-line code, and no cross-lane shuffles are used at block ends.
+template <int TB>
+__global__ __launch_bounds__(64) void k_chain_small(const unsigned long long *__restrict__ mask,
+                                                    const int *__restrict__ tmatch, int R, int T,
+                                                    const int *__restrict__ candoff,
+                                                    const int *__restrict__ candlen,
+                                                    const unsigned int *__restrict__ crank,
+                                                    int *__restrict__ umatch, int *__restrict__ rounds_out) {
+    extern __shared__ unsigned int ring32[];  // [TB][RING] packed ranks
+    const int lane = threadIdx.x;
+    int c0[TB], len[TB], off[TB];
+#pragma unroll
+    for (int q = 0; q < TB; q++) {
+        c0[q] = 0;
+        len[q] = q < T ? candlen[q] : 0;
+        off[q] = q < T ? candoff[q] : 0;
+        for (int i = lane; i < RING; i += 64) ring32[q * RING + i] = i < len[q] ? crank[off[q] + i] : ~0u;
+    }
+    __syncthreads();
+    int total_rounds = 0;
+    // two blocks of inputs in flight; the refill load is the youngest memory op
+    unsigned long long m_next = mask[min(lane, R - 1)];
+    int t_next = tmatch[min(lane, R - 1)];
+    unsigned int pend_key = crank[0];
+    bool pend_zero = true;
+    int pend_addr = -1;
+    for (int b0 = 0; b0 < R; b0 += 64) {
+        const int j = b0 + lane;
+        const unsigned long long m = (j < R && t_next < 0) ? m_next : 0ull;
+        bool have[TB];
+#pragma unroll
+        for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
+        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
+        unsigned long long changed;
+        do {
+            unsigned int v[TB];
+            bool ok[TB];
+#pragma unroll
+            for (int q = 0; q < TB; q++) {
+                const int pos = c0[q] + (int)mbcnt64(__ballot(ch == q));
+                ok[q] = have[q] & (pos < len[q]);
+                v[q] = ring32[q * RING + (pos & (RING - 1))];
+            }
+            unsigned int best = ~0u;
+#pragma unroll
+            for (int q = 0; q < TB; q++) best = min(best, ok[q] ? v[q] : ~0u);
+            const int nch = best == ~0u ? -1 : (int)(best & 63u);
+            changed = __ballot(nch != ch);
+            ch = nch;
+            total_rounds++;
+        } while (changed);
+        // results, c0 advance and refill assignment in one pass over the types
+        int res = -1, pre = 0, my_q = -1, my_k = 0, my_len = 0, my_off = 0;
+#pragma unroll
+        for (int q = 0; q < TB; q++) {
+            const unsigned long long B = __ballot(ch == q);
+            const int cnt = __popcll(B);
+            if (ch == q) res = off[q] + c0[q] + (int)mbcnt64(B);
+            if (lane >= pre && lane < pre + cnt) {
+                my_q = q;
+                my_k = c0[q] + RING + (lane - pre);  // absolute position entering the ring
+                my_len = len[q];
+                my_off = off[q];
+            }
+            pre += cnt;
+            c0[q] += cnt;
+        }
+        if (j < R) umatch[j] = res;
+        const int jn = min(j + 64, R - 1);
+        m_next = mask[jn];
+        t_next = tmatch[jn];  // lanes past R are masked by (j < R) at the next block start
+        __builtin_amdgcn_wave_barrier();
+        if (pend_addr >= 0) ring32[pend_addr] = pend_zero ? ~0u : pend_key;  // refill issued one block ago
+        const bool valid = my_q >= 0 && my_k < my_len;
+        pend_key = crank[valid ? my_off + my_k : 0];  // consumed one block later (no wait here)
+        pend_zero = !valid;
+        pend_addr = my_q >= 0 ? my_q * RING + (my_k & (RING - 1)) : -1;
+    }
+    if (lane == 0 && rounds_out) *rounds_out = total_rounds;
+}
+
 // ---------------------------------------------------------------- finalize
 __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, int R, const int *__restrict__ tmatch,
                                                   const int *__restrict__ umatch, const int *__restrict__ cslot,
@@ -814,9 +897,18 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         const size_t lds = sizeof(unsigned int) * RING * std::max(T, 1);
         if (np > 0 && T > 0)
             k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank);
-        if (T <= 4)
-            k_chain<4><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank,
-                                          h->d_umatch, &h->d_ctr->chain_rounds);
+        if (T <= 2)
+            k_chain_small<2><<<1, 64, sizeof(unsigned int) * RING * 2, s>>>(
+                h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
+                &h->d_ctr->chain_rounds);
+        else if (T <= 4)
+            k_chain_small<4><<<1, 64, sizeof(unsigned int) * RING * 4, s>>>(
+                h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
+                &h->d_ctr->chain_rounds);
+        else if (T <= 8)
+            k_chain_small<8><<<1, 64, sizeof(unsigned int) * RING * 8, s>>>(
+                h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
+                &h->d_ctr->chain_rounds);
         else
             k_chain<8><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank,
                                           h->d_umatch, &h->d_ctr->chain_rounds);

@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--reserves", type=int, default=65_536)
     ap.add_argument("--types", type=int, default=4)
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--equal-prio", action="store_true", help="config-2 variant: all priorities equal")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP event timing")
@@ -89,7 +90,8 @@ def main():
     from adlb_amd.server import Server
 
     R, N = args.reserves, args.units
-    w = synth.config2(n_units=N, n_types=args.types, n_reserves=R, seed=args.seed + 1000 * rank)
+    w = synth.config2(n_units=N, n_types=args.types, n_reserves=R, seed=args.seed + 1000 * rank,
+                      equal_prio=args.equal_prio)
     srv = Server(w.user_types, w.num_app_ranks, max_units=N, device=local)
     # one explicit stream for the library and the torch glue ops (the handle's
     # own stream is non-blocking and would not order against torch's null stream)
