@@ -607,83 +607,120 @@ __global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restri
 // into registers once per block (uniform values live in SGPRs), rounds are
 // straight-line code, and no cross-lane shuffles are used at block ends.
 template <int TB>
+struct SmallChainState {
+    int c0[TB], len[TB], off[TB];
+    unsigned int pend_key;
+    bool pend_zero;
+    int pend_addr;
+    int rounds;
+};
+
+// One 64-request block of the small-T chain.  (m_in, t_in) hold this block's
+// inputs and are overwritten with the inputs of the block two ahead, so the
+// caller alternates two register sets without moves (no wait on a fresh load).
+template <int TB>
+__device__ __forceinline__ void small_chain_block(SmallChainState<TB> &st, unsigned int *ring32, int b0, int R,
+                                                  unsigned long long &m_in, int &t_in,
+                                                  const unsigned long long *__restrict__ mask,
+                                                  const int *__restrict__ tmatch,
+                                                  const unsigned int *__restrict__ crank,
+                                                  int *__restrict__ umatch) {
+    const int lane = threadIdx.x;
+    const int j = b0 + lane;
+    const unsigned long long m = (j < R && t_in < 0) ? m_in : 0ull;
+    bool have[TB];
+#pragma unroll
+    for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
+    int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
+    unsigned long long changed;
+    do {
+        unsigned int v[TB];
+        bool ok[TB];
+#pragma unroll
+        for (int q = 0; q < TB; q++) {
+            const int pos = st.c0[q] + (int)mbcnt64(__ballot(ch == q));
+            ok[q] = have[q] & (pos < st.len[q]);
+            v[q] = ring32[q * RING + (pos & (RING - 1))];
+        }
+        unsigned int best = ~0u;
+#pragma unroll
+        for (int q = 0; q < TB; q++) best = min(best, ok[q] ? v[q] : ~0u);
+        const int nch = best == ~0u ? -1 : (int)(best & 63u);
+        changed = __ballot(nch != ch);
+        ch = nch;
+        st.rounds++;
+    } while (changed);
+    // results, c0 advance and refill assignment in one pass over the types
+    int res = -1, pre = 0, my_q = -1, my_k = 0, my_len = 0, my_off = 0;
+#pragma unroll
+    for (int q = 0; q < TB; q++) {
+        const unsigned long long B = __ballot(ch == q);
+        const int cnt = __popcll(B);
+        if (ch == q) res = st.off[q] + st.c0[q] + (int)mbcnt64(B);
+        if (lane >= pre && lane < pre + cnt) {
+            my_q = q;
+            my_k = st.c0[q] + RING + (lane - pre);  // absolute position entering the ring
+            my_len = st.len[q];
+            my_off = st.off[q];
+        }
+        pre += cnt;
+        st.c0[q] += cnt;
+    }
+    if (j < R) umatch[j] = res;
+    const int jn = min(j + 128, R - 1);
+    m_in = mask[jn];
+    t_in = tmatch[jn];  // lanes past R are masked by (j < R) at their block start
+    __builtin_amdgcn_wave_barrier();
+    // refill of one block ago; lanes without one write the spare slot past the
+    // rings, so the store (and the wait on its load) is unconditional
+    ring32[st.pend_addr] = st.pend_zero ? ~0u : st.pend_key;
+    const bool valid = my_q >= 0 && my_k < my_len;
+    st.pend_key = crank[valid ? my_off + my_k : 0];  // consumed one block later (no wait here)
+    st.pend_zero = !valid;
+    st.pend_addr = my_q >= 0 ? my_q * RING + (my_k & (RING - 1)) : TB * RING;
+}
+
+// Small-T variant (T <= TB): every per-type quantity of a block is hoisted
+// into registers once per block (uniform values live in SGPRs), rounds are
+// straight-line code, and no cross-lane shuffles are used at block ends.
+template <int TB>
 __global__ __launch_bounds__(64) void k_chain_small(const unsigned long long *__restrict__ mask,
                                                     const int *__restrict__ tmatch, int R, int T,
                                                     const int *__restrict__ candoff,
                                                     const int *__restrict__ candlen,
                                                     const unsigned int *__restrict__ crank,
                                                     int *__restrict__ umatch, int *__restrict__ rounds_out) {
-    extern __shared__ unsigned int ring32[];  // [TB][RING] packed ranks
+    extern __shared__ unsigned int ring32[];  // [TB][RING] packed ranks + 1 spare slot
     const int lane = threadIdx.x;
-    int c0[TB], len[TB], off[TB];
+    SmallChainState<TB> st;
 #pragma unroll
     for (int q = 0; q < TB; q++) {
-        c0[q] = 0;
-        len[q] = q < T ? candlen[q] : 0;
-        off[q] = q < T ? candoff[q] : 0;
-        for (int i = lane; i < RING; i += 64) ring32[q * RING + i] = i < len[q] ? crank[off[q] + i] : ~0u;
+        st.c0[q] = 0;
+        st.len[q] = q < T ? candlen[q] : 0;
+        st.off[q] = q < T ? candoff[q] : 0;
+        for (int i = lane; i < RING; i += 64) ring32[q * RING + i] = i < st.len[q] ? crank[st.off[q] + i] : ~0u;
     }
     __syncthreads();
-    int total_rounds = 0;
-    // two blocks of inputs in flight; the refill load is the youngest memory op
-    unsigned long long m_next = mask[min(lane, R - 1)];
-    int t_next = tmatch[min(lane, R - 1)];
-    unsigned int pend_key = crank[0];
-    bool pend_zero = true;
-    int pend_addr = -1;
-    for (int b0 = 0; b0 < R; b0 += 64) {
-        const int j = b0 + lane;
-        const unsigned long long m = (j < R && t_next < 0) ? m_next : 0ull;
-        bool have[TB];
-#pragma unroll
-        for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
-        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
-        unsigned long long changed;
-        do {
-            unsigned int v[TB];
-            bool ok[TB];
-#pragma unroll
-            for (int q = 0; q < TB; q++) {
-                const int pos = c0[q] + (int)mbcnt64(__ballot(ch == q));
-                ok[q] = have[q] & (pos < len[q]);
-                v[q] = ring32[q * RING + (pos & (RING - 1))];
-            }
-            unsigned int best = ~0u;
-#pragma unroll
-            for (int q = 0; q < TB; q++) best = min(best, ok[q] ? v[q] : ~0u);
-            const int nch = best == ~0u ? -1 : (int)(best & 63u);
-            changed = __ballot(nch != ch);
-            ch = nch;
-            total_rounds++;
-        } while (changed);
-        // results, c0 advance and refill assignment in one pass over the types
-        int res = -1, pre = 0, my_q = -1, my_k = 0, my_len = 0, my_off = 0;
-#pragma unroll
-        for (int q = 0; q < TB; q++) {
-            const unsigned long long B = __ballot(ch == q);
-            const int cnt = __popcll(B);
-            if (ch == q) res = off[q] + c0[q] + (int)mbcnt64(B);
-            if (lane >= pre && lane < pre + cnt) {
-                my_q = q;
-                my_k = c0[q] + RING + (lane - pre);  // absolute position entering the ring
-                my_len = len[q];
-                my_off = off[q];
-            }
-            pre += cnt;
-            c0[q] += cnt;
-        }
-        if (j < R) umatch[j] = res;
-        const int jn = min(j + 64, R - 1);
-        m_next = mask[jn];
-        t_next = tmatch[jn];  // lanes past R are masked by (j < R) at the next block start
-        __builtin_amdgcn_wave_barrier();
-        if (pend_addr >= 0) ring32[pend_addr] = pend_zero ? ~0u : pend_key;  // refill issued one block ago
-        const bool valid = my_q >= 0 && my_k < my_len;
-        pend_key = crank[valid ? my_off + my_k : 0];  // consumed one block later (no wait here)
-        pend_zero = !valid;
-        pend_addr = my_q >= 0 ? my_q * RING + (my_k & (RING - 1)) : -1;
+    st.rounds = 0;
+    // two register sets of block inputs, each refilled two blocks ahead
+    unsigned long long mA = mask[min(lane, R - 1)];
+    int tA = tmatch[min(lane, R - 1)];
+    unsigned long long mB = mask[min(lane + 64, R - 1)];
+    int tB = tmatch[min(lane + 64, R - 1)];
+    st.pend_key = 0;
+    st.pend_zero = true;
+    st.pend_addr = TB * RING;
+    // consume the prologue loads here so the loop is entered with no loads in
+    // flight: the waitcnt state at the loop header is then the back-edge one,
+    // where each block's inputs landed a block earlier
+    asm volatile("" : "+v"(mA), "+v"(tA), "+v"(mB), "+v"(tB));
+    int b0 = 0;
+    for (; b0 + 64 < R; b0 += 128) {  // every back edge has run both blocks
+        small_chain_block<TB>(st, ring32, b0, R, mA, tA, mask, tmatch, crank, umatch);
+        small_chain_block<TB>(st, ring32, b0 + 64, R, mB, tB, mask, tmatch, crank, umatch);
     }
-    if (lane == 0 && rounds_out) *rounds_out = total_rounds;
+    if (b0 < R) small_chain_block<TB>(st, ring32, b0, R, mA, tA, mask, tmatch, crank, umatch);
+    if (lane == 0 && rounds_out) *rounds_out = st.rounds;
 }
 
 // ---------------------------------------------------------------- finalize
@@ -898,15 +935,15 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         if (np > 0 && T > 0)
             k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank);
         if (T <= 2)
-            k_chain_small<2><<<1, 64, sizeof(unsigned int) * RING * 2, s>>>(
+            k_chain_small<2><<<1, 64, sizeof(unsigned int) * (RING * 2 + 1), s>>>(
                 h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
                 &h->d_ctr->chain_rounds);
         else if (T <= 4)
-            k_chain_small<4><<<1, 64, sizeof(unsigned int) * RING * 4, s>>>(
+            k_chain_small<4><<<1, 64, sizeof(unsigned int) * (RING * 4 + 1), s>>>(
                 h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
                 &h->d_ctr->chain_rounds);
         else if (T <= 8)
-            k_chain_small<8><<<1, 64, sizeof(unsigned int) * RING * 8, s>>>(
+            k_chain_small<8><<<1, 64, sizeof(unsigned int) * (RING * 8 + 1), s>>>(
                 h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
                 &h->d_ctr->chain_rounds);
         else
