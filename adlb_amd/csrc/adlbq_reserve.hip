@@ -891,7 +891,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipEvent_t ev;
 
     AQ_HIP(hipMemsetAsync(h->d_dem, 0, sizeof(int) * std::max(T, 1), s));
+    stage_begin(h, "prep", &ev);
     k_req_prep<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem);
+    stage_end(h, "prep", ev);
 
     if (np > 0 && T > 0) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
@@ -901,12 +903,16 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_dem, h->d_gh,
             h->d_csum);
         stage_end(h, "hist", ev);
+        stage_begin(h, "thresholds", &ev);
         k_thresholds<<<1, 1024, sizeof(unsigned int) * C, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta,
                                                                h->d_need, h->d_candoff, h->d_candlen,
                                                                h->d_needsort, h->d_binoff);
-        stage_begin(h, "select", &ev);
+        stage_end(h, "thresholds", ev);
+        stage_begin(h, "prefix", &ev);
         const long long ncol = (long long)nchunks * C;
         k_page_prefix<<<(int)((ncol + 255) / 256), 256, 0, s>>>(np, T, h->d_theta, h->d_gh, h->d_csum, h->d_pp);
+        stage_end(h, "prefix", ev);
+        stage_begin(h, "select", &ev);
         k_select_open<<<(np + 3) / 4, 256, sizeof(unsigned int) * 4 * C, s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_candoff, h->d_binoff, h->d_pp, h->d_ckey, h->d_cslot);
@@ -929,11 +935,14 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                       h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch);
         stage_end(h, "targeted", ev);
     }
+    if (np > 0 && T > 0) {
+        stage_begin(h, "rank", &ev);
+        k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank);
+        stage_end(h, "rank", ev);
+    }
     stage_begin(h, "chain", &ev);
     {
         const size_t lds = sizeof(unsigned int) * RING * std::max(T, 1);
-        if (np > 0 && T > 0)
-            k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank);
         if (T <= 2)
             k_chain_small<2><<<1, 64, sizeof(unsigned int) * (RING * 2 + 1), s>>>(
                 h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
@@ -955,10 +964,12 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
                                                h->d_meta, h->d_pin,
                                                h->d_seq, h->d_cold0, h->d_cold1, h->my_world, d_resp, h->d_ctr);
+    stage_end(h, "finalize", ev);
+    stage_begin(h, "park", &ev);
     const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
     k_park<<<1, 1024, 0, s>>>(donor_ctx(h), donors, d_reqs, R, h->d_tmatch, h->d_umatch, h->d_rq_rank,
                               h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_ctr, d_resp);
-    stage_end(h, "finalize", ev);
+    stage_end(h, "park", ev);
     AQ_HIP(hipGetLastError());
     h->ctr_stale = true;
     h->rq_n_upper += R;

@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-STAGES = ["hist", "select", "sort", "targeted", "chain", "finalize"]
+STAGES = ["prep", "hist", "thresholds", "prefix", "select", "sort", "targeted", "rank", "chain", "finalize", "park"]
 
 
 def parse():

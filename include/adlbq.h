@@ -130,8 +130,11 @@ int adlbq_info_type(adlbq_server *h, int work_type, int *max_prio, int *num_max_
 int  adlbq_set_stream(adlbq_server *h, void *hip_stream); /* NULL = handle's own stream */
 void *adlbq_get_stream(adlbq_server *h);
 int  adlbq_sync(adlbq_server *h);
-/* Per-stage GPU time (HIP events on the handle's stream) when enabled:
- * stage names: "hist", "select", "sort", "targeted", "chain", "finalize". */
+/* Per-kernel GPU time (HIP events on the handle's stream around each launch of
+ * a reserve batch) when enabled.  Stage names, one kernel each: "prep"
+ * (k_req_prep), "hist" (k_hist_open), "thresholds", "prefix" (k_page_prefix),
+ * "select" (k_select_open), "sort" (k_sort_types), "targeted", "rank",
+ * "chain" (k_chain_small / k_chain), "finalize", "park". */
 int  adlbq_profile_enable(adlbq_server *h, int on);
 int  adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, long long *launches);
 /* Bytes the last reserve batch's open-bucket scan touched algorithmically:
