@@ -13,16 +13,26 @@ server shard with its own 10M-unit queue and its own Reserve stream (the
 reference shards queues by server); no collective touches the data
 path (weak scaling).  The barrier / max-over-ranks timing is measurement only.
 
-The JSON line carries the roofline of the matching pipeline measured with HIP
-events on the launch stream, and the CPU baseline: the oracle (this repo's
-linked-list restatement of the reference xq scans) timed on a bounded sample.
+The JSON line carries, per kernel of the reserve batch, the average launch
+time measured with HIP events recorded on the launch stream around each launch
+(adlbq_profile_*), the algorithmic bytes of that kernel and the
+HBM traffic from two separate rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; KB,
+FETCH_SIZE doubled per the gfx950 correction) run as child processes before
+this process touches the GPU.  `roofline` is the dominant kernel (largest
+average launch time).  `cpu_baseline` is the oracle (this repo's linked-list
+restatement of the reference xq scans) timed on a bounded sample.
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -47,7 +57,69 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP event timing")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     return ap.parse_args()
+
+
+# stage (adlbq_profile_read name) -> kernel symbol of that launch
+KERNEL_OF = {"prep": "k_req_prep", "hist": "k_hist_open", "thresholds": "k_thresholds",
+             "prefix": "k_page_prefix", "select": "k_select_open", "sort": "k_sort_types",
+             "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain", "finalize": "k_finalize",
+             "park": "k_park"}
+
+
+def _kernel_base(name: str) -> str:
+    n = name.strip().strip('"')
+    if n.startswith("void "):
+        n = n[5:]
+    return n.split("(")[0]
+
+
+def pmc_traffic(args) -> dict | None:
+    """HBM bytes per launch of each kernel from two rocprofv3 PMC passes over a
+    short run of the same workload (child processes; this process has not
+    touched the GPU yet).  FETCH_SIZE/WRITE_SIZE are KB; FETCH_SIZE is doubled
+    (gfx950 reports half of wide streaming reads, MI355X_MICROARCH.md).  The mean
+    over the steady-state launches (the first launch of each kernel dropped)."""
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3")
+                                         else None)
+    if prof is None:
+        return None
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu", "--no-pmc",
+             "--no-profile", "--units", str(args.units), "--reserves", str(args.reserves), "--types",
+             str(args.types), "--seed", str(args.seed)] + (["--equal-prio"] if args.equal_prio else [])
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="adlbq_pmc_")
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            r = subprocess.run([prof, "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--"] + child,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=600,
+                               env=dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp")))
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                return None
+            per = {}
+            for row in csv.DictReader(open(files[0])):
+                per.setdefault(_kernel_base(row["Kernel_Name"]), []).append(float(row["Counter_Value"]))
+            scale = 2048.0 if ctr == "FETCH_SIZE" else 1024.0
+            for k, v in per.items():
+                v = v[1:] if len(v) > 1 else v
+                out.setdefault(k, {})[ctr] = scale * sum(v) / len(v)
+    except (OSError, subprocess.SubprocessError, KeyError, ValueError):
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return {k: v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0) for k, v in out.items()
+            if "FETCH_SIZE" in v and "WRITE_SIZE" in v}
+
+
+def traffic_of(pmc, stage):
+    if not pmc:
+        return None
+    want = KERNEL_OF[stage]
+    hits = [v for k, v in pmc.items() if k == want or k.startswith(want + "_small<") or k.startswith(want + "<")]
+    return round(hits[0]) if len(hits) == 1 else None
 
 
 def cpu_baseline(w, budget_s: float) -> dict:
@@ -75,6 +147,10 @@ def cpu_baseline(w, budget_s: float) -> dict:
 
 def main():
     args = parse()
+    world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    pmc = None
+    if world0 == 1 and not args.no_pmc:
+        pmc = pmc_traffic(args)  # before this process initialises the GPU
     import torch
     import torch.distributed as dist
 
@@ -86,13 +162,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from adlb_amd import synth
+    from adlb_amd import shards, synth
     from adlb_amd.server import Server
 
     R, N = args.reserves, args.units
-    w = synth.config2(n_units=N, n_types=args.types, n_reserves=R, seed=args.seed + 1000 * rank,
+    w = synth.config2(n_units=N, n_types=args.types, n_reserves=R, seed=shards.shard_seed(args.seed, rank),
                       equal_prio=args.equal_prio)
-    srv = Server(w.user_types, w.num_app_ranks, max_units=N, device=local)
+    srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
     # one explicit stream for the library and the torch glue ops (the handle's
     # own stream is non-blocking and would not order against torch's null stream)
     stream = torch.cuda.Stream(dev)
@@ -102,6 +178,8 @@ def main():
                       np.zeros(N), np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32)
     srv.put_batch(units)
     del units
+    if world > 1:
+        shards.exchange_qmstat(srv)  # the qmstat table every shard's donor choice reads (untimed)
     nb = args.steps + args.warmup
     rng = np.random.default_rng(args.seed + 7 + rank)
     reqs = np.empty((nb, R, 18), np.int32)
@@ -143,12 +221,7 @@ def main():
     el = time.perf_counter() - t0
     matched = int((d_resp[args.warmup:, :, 0] == 1).sum().item())
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        m = torch.tensor([matched], dtype=torch.int64, device=dev)
-        dist.all_reduce(m, op=dist.ReduceOp.SUM)
-        matched = int(m.item())
+        el, matched = shards.reduce_step_timing(el, matched)
 
     stages = {}
     if not args.no_profile:
@@ -158,10 +231,35 @@ def main():
             if n - n0:
                 stages[s] = round((ms - ms0) / (n - n0), 4)
     live = srv.last_scan_units()
-    alg_bytes = 16 * live + (72 + 8 + 4) * R          # per matching batch
+    # algorithmic bytes per launch: SURVEY §8(d)'s 16 B per live
+    # unit for the open-bucket scan (hist + select together), 20 B per Reserve
+    # for the ordered-choice chain (8 B type mask + 4 B targeted result read,
+    # 4 B choice written, 4 B candidate rank read), 72+8+4 B per Reserve for the
+    # batch as a whole (request record, assignment output, pin write).
+    alg = {"chain": 20 * R, "scan": 16 * live, "batch": 16 * live + (72 + 8 + 4) * R}
     batch_ms = sum(stages.values()) if stages else el * 1e3 / args.steps
+    kernels = {}
+    for st, ms in stages.items():
+        kernels[st] = {"kernel": KERNEL_OF[st], "ms": ms, "traffic": traffic_of(pmc, st)}
+    dominant = max(stages, key=stages.get) if stages else None
+
+    def roof(bytes_, ms, traffic, kernel):
+        a = bytes_ / (ms * 1e-3) / 1e9 if ms else None
+        return {"bound": "hbm", "kernel": kernel, "achieved": round(a, 2) if a else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(a / HBM_PEAK_GBS, 6) if a else None, "traffic": traffic,
+                "algorithmic_bytes": bytes_, "launch_ms": ms}
+
+    if dominant == "chain":
+        roofline = roof(alg["chain"], stages["chain"], kernels["chain"]["traffic"], KERNEL_OF["chain"])
+    elif dominant in ("hist", "select"):
+        roofline = roof(alg["scan"] / 2, stages[dominant], kernels[dominant]["traffic"], KERNEL_OF[dominant])
+    elif dominant:
+        roofline = roof(alg["batch"] * stages[dominant] / batch_ms, stages[dominant], kernels[dominant]["traffic"],
+                        KERNEL_OF[dominant])
+    else:
+        roofline = roof(alg["batch"], batch_ms, None, "reserve batch (unprofiled)")
     scan_ms = stages.get("hist", 0) + stages.get("select", 0)
-    dominant = max(stages, key=stages.get) if stages else "batch"
+    scan_tr = [kernels[k]["traffic"] for k in ("hist", "select") if k in kernels]
     res = {
         "metric": "matched Reserve assignments/sec at 10M-unit queue",
         "value": matched / el,
@@ -179,21 +277,13 @@ def main():
                                f"{R} hanging Reserves/step (70/20/10 single/pair/wildcard), "
                                f"step = reserve batch + unreserve of matched units",
                    "units_per_shard": N, "reserves_per_step": R, "parallelism": f"shards{world}"},
-        "roofline": {
-            "bound": "hbm",
-            "kernel": "reserve-batch pipeline (all stages of one batch)",
-            "achieved": round(alg_bytes / (batch_ms * 1e-3) / 1e9, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(alg_bytes / (batch_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": None,
-            "algorithmic_bytes": alg_bytes,
-            "scan_kernels_GBs": round(16 * live / (scan_ms * 1e-3) / 1e9, 1) if scan_ms else None,
-        },
-        "stages_ms": stages,
+        "roofline": roofline,
+        "roofline_scan": roof(alg["scan"], scan_ms, sum(scan_tr) if scan_tr and None not in scan_tr else None,
+                              "k_hist_open + k_select_open") if scan_ms else None,
+        "roofline_batch": roof(alg["batch"], batch_ms, None, "all reserve-batch kernels"),
+        "kernels_ms": kernels,
         "chain_rounds_last_batch": srv.stat("chain_rounds"),
         "candidates_last_batch": srv.stat("candidates"),
-        "dominant_stage": dominant,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
