@@ -43,6 +43,7 @@ SIGNATURES = {
     "adlbq_profile_read": (c_int, [P, c_char_p, P, P]),
     "adlbq_last_scan_units": (c_ll, [P]),
     "adlbq_stat": (c_ll, [P, c_char_p]),
+    "adlbq_set_param": (c_int, [P, c_char_p, c_ll]),
     "adlbq_last_error": (c_char_p, []),
     "adlbq_version": (c_char_p, []),
 }

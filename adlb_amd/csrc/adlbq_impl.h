@@ -41,8 +41,11 @@ struct DevCounters {
     int rq_hwm;        // rq->max_count
     int rq_head;       // lowest rq slot that may be alive
     int n_parked_last; // parked by the last reserve batch
-    int chain_rounds;  // Jacobi rounds of the last chain (diagnostic)
+    int chain_rounds;  // Jacobi rounds of the last chain, all wavefronts (diagnostic)
     int park_pending;  // parked requests counted by k_finalize for k_park
+    int chain_passes;      // segment passes of the last chain that recomputed something
+    int chain_recomputed;  // segment solves over those passes
+    int chain_fallback;    // segments k_chain_fix recomputed (0 at a fixed point)
     int pad[1];
 };
 
@@ -132,6 +135,11 @@ struct adlbq_server {
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
     int *d_cslot = nullptr, *d_cslot2 = nullptr;
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate
+    int *d_seg_cnt = nullptr;          // [nseg] chain: untargeted-capable requests per segment
+    int *d_chE = nullptr;              // [2][nseg][T] chain: segment end states
+    int *d_chS = nullptr;              // [nseg][T] chain: segment starts of the last computation
+    int *d_chchg = nullptr;            // [CHAIN_MAX_PASSES + 2] chain: segments recomputed per pass
+    int chain_passes = 8;              // passes before k_chain_fix (adlbq_set_param "chain_passes")
     int *d_result = nullptr;           // small result scratch (16 ints)
     int *h_result = nullptr;           // pinned host mirror
     long long last_scan_units = 0;

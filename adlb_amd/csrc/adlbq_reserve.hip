@@ -26,21 +26,37 @@
 
 using namespace adlbq;
 
+constexpr int SEG = 256;               // chain segment: requests per wavefront (== k_req_prep's block)
+constexpr int SEG_BLOCKS = SEG / 64;
+constexpr int CHAIN_MAX_PASSES = 30;   // bound of the settable pass count (adlbq_set_param)
+
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
     unsigned int lo = __builtin_amdgcn_readlane((unsigned int)v, l);
     unsigned int hi = __builtin_amdgcn_readlane((unsigned int)(v >> 32), l);
     return ((unsigned long long)hi << 32) | lo;
 }
 
-__global__ __launch_bounds__(256) void k_req_prep(const int *__restrict__ reqs, int R, const int *__restrict__ utypes,
-                                                  int T, unsigned long long *__restrict__ mask, int *dem) {
+// One block per chain segment (blockDim == SEG): also the segment's count of
+// requests with a non-empty type set (the chain's level guess, k_chain_pass),
+// and block 0 resets the chain's per-batch counters.
+__global__ __launch_bounds__(SEG) void k_req_prep(const int *__restrict__ reqs, int R, const int *__restrict__ utypes,
+                                                  int T, unsigned long long *__restrict__ mask, int *dem,
+                                                  int *__restrict__ seg_cnt, int *__restrict__ changed,
+                                                  DevCounters *ctr) {
     __shared__ int su[ADLBQ_MAX_TYPES], sd[ADLBQ_MAX_TYPES];
+    __shared__ int scnt;
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         su[t] = utypes[t];
         sd[t] = 0;
     }
+    if (threadIdx.x == 0) scnt = 0;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < CHAIN_MAX_PASSES + 2) changed[threadIdx.x] = 0;
+        if (threadIdx.x == 0) ctr->chain_rounds = 0;
+    }
     __syncthreads();
     int j = blockIdx.x * blockDim.x + threadIdx.x;
+    bool nonempty = false;
     if (j < R) {
         const int *rt = reqs + (long long)ADLBQ_RESERVE_INTS * j + 2;
         unsigned long long m = 0;
@@ -53,9 +69,13 @@ __global__ __launch_bounds__(256) void k_req_prep(const int *__restrict__ reqs, 
         }
         if (wild) m = T >= 64 ? ~0ull : ((1ull << T) - 1);
         mask[j] = m;
+        nonempty = m != 0ull;
         for (unsigned long long b = m; b; b &= b - 1) atomicAdd(&sd[__ffsll((long long)b) - 1], 1);
     }
+    const unsigned long long nz = __ballot(nonempty);
+    if ((threadIdx.x & 63) == 0 && nz) atomicAdd(&scnt, __popcll(nz));
     __syncthreads();
+    if (threadIdx.x == 0) seg_cnt[blockIdx.x] = scnt;
     for (int t = threadIdx.x; t < T; t += blockDim.x)
         if (sd[t]) atomicAdd(&dem[t], sd[t]);
 }
@@ -383,7 +403,8 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
                                                   const int *__restrict__ rpages, const int *__restrict__ rfill,
                                                   const int *__restrict__ prio, uint32_t *meta,
                                                   const unsigned long long *__restrict__ mask,
-                                                  const int *__restrict__ reqs, int R, int *tmatch) {
+                                                  const int *__restrict__ reqs, int R, int *tmatch,
+                                                  int *seg_cnt) {
     __shared__ int list[1024];
     __shared__ int nlist, wcnt[4];
     __shared__ unsigned long long red[4];
@@ -431,6 +452,7 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
                         const long long slot =
                             ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
                         tmatch[jj] = (int)slot;
+                        atomicSub(&seg_cnt[jj / SEG], 1);
                         // taken for this rank's later Reserves (this block owns the bucket)
                         st_agent(reinterpret_cast<int *>(meta + slot), (int)(meta[slot] | M_PINNED));
                     }
@@ -446,20 +468,29 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
 
 // ---------------------------------------------------------------- untargeted choices in arrival order
 //
-// One wavefront walks the untargeted Reserves in blocks of 64 (lane = request).
-// At a block start the number of candidates already consumed from every type,
-// c0[t], is exact.  Inside the block each lane's choice depends only on the
-// choices of lower lanes (how many of them took each type), so the block is
-// solved by Jacobi rounds: every lane recomputes its choice from the current
-// choices of lower lanes (ballot + mbcnt per type) until nothing changes.  The
-// fixed point is the sequential result (lane 0 is exact in round 1, lane k by
-// round k+1), and it is reached in ~5 rounds for config 2 (max 65).
+// After the scan every type t has a candidate list in global preference order
+// (packed ranks ascending, k_rank).  Request j takes the best head among its
+// types: cand_t[pos_t(j)], pos_t(j) = how many earlier requests took type t.
+// The state before request j is the vector pos(j); the sequential order is a
+// chain of T-way merges.  It is solved in parallel by *segments*:
 //
-// Candidate keys come from a per-type ring in LDS holding absolute candidate
-// positions [c0[t], c0[t] + 128).  A block consumes at most 64 in total, so the
-// refill for the block after next is one load per lane, issued at a block end
-// and written to LDS at the next block end (global latency hidden by a block).
-constexpr int RING = 128;
+//   * the batch is cut into segments of SEG requests, one wavefront each; a
+//     wavefront solves its segment exactly from a given start vector (64-lane
+//     blocks, Jacobi rounds inside a block: lane k is exact by round k+1);
+//   * pass 1 starts every segment from a guess: the "level" state
+//     pos_t = #{type-t candidates with global rank < J}, J = requests before the
+//     segment that take an untargeted unit.  The multi-type requests keep the
+//     list heads level, so the guess is close (|error|_1 ~ 10 at config 2);
+//   * pass k > 1 starts segment s from the end state segment s-1 reached in
+//     pass k-1.  Two trajectories of the merge coalesce once the multi-type
+//     requests have levelled the heads (~150 requests), so an end state is exact
+//     as soon as its segment coalesced, whatever its start was.  A segment whose
+//     start did not change is not recomputed;
+//   * a pass in which no start changed is a fixed point, and the fixed point
+//     is the sequential result (segment 0 starts from 0; by induction every
+//     start is exact).  After CHAIN_PASSES passes without one, k_chain_fix
+//     walks the segments in order from the exact prefix and recomputes only
+//     those whose start still differs (adversarial inputs; tests force it).
 
 __device__ __forceinline__ unsigned int mbcnt64(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((unsigned int)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)m, 0u));
@@ -505,222 +536,234 @@ __global__ __launch_bounds__(256) void k_rank(int T, const int *__restrict__ can
     }
 }
 
-template <int TB>  // types handled per unrolled group (reads issued together, then reduced)
-__global__ __launch_bounds__(64) void k_chain(const unsigned long long *__restrict__ mask,
-                                              const int *__restrict__ tmatch, int R, int T,
-                                              const int *__restrict__ candoff, const int *__restrict__ candlen,
-                                              const unsigned int *__restrict__ crank,
-                                              int *__restrict__ umatch, int *__restrict__ rounds_out) {
-    extern __shared__ unsigned int ring32[];  // [T][RING] packed ranks
-    const int lane = threadIdx.x;
-    // lane t keeps type t's state; uniform copies come from readlane
-    const int my_off = lane < T ? candoff[lane] : 0;
-    const int my_len = lane < T ? candlen[lane] : 0;
-    int my_c0 = 0;
-    for (int t = 0; t < T; t++) {
-        const int off = __builtin_amdgcn_readlane(my_off, t), len = __builtin_amdgcn_readlane(my_len, t);
-        for (int i = lane; i < RING; i += 64) ring32[t * RING + i] = i < len ? crank[off + i] : ~0u;
+struct ChainArgs {
+    const unsigned long long *mask;  // [R] type masks (0: no untargeted choice)
+    const int *tmatch;               // [R] slot matched in the targeted phase, or -1
+    int R, T, nseg;
+    const int *candoff, *candlen;    // [T]
+    const unsigned int *crank;       // packed ranks, per type ascending
+    int *umatch;                     // [R] out: candidate index or -1
+    const int *seg_cnt;              // [nseg] requests of the segment that may take an untargeted unit
+    int *E;                          // [2][nseg][T] end state per segment, double-buffered by pass
+    int *Sprev;                      // [nseg][T] start of each segment's last computation
+    int *changed;                    // [CHAIN_MAX_PASSES + 2] segments recomputed per pass
+    DevCounters *ctr;
+};
+
+// One segment, all per-type state uniform (T <= TB <= 8).  win holds, per type,
+// the SEG candidates following the segment's start (~0u past the list end);
+// a segment consumes at most SEG of any type.  Lane t of my_start is type t's
+// start; returns the end state in the same layout.
+template <int TB>
+__device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int my_start, unsigned int *win,
+                                               int &rounds) {
+    const int lane = threadIdx.x, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
+    int st[TB], off[TB], c0[TB];
+    unsigned long long mb[SEG_BLOCKS];
+    int tb[SEG_BLOCKS];
+#pragma unroll
+    for (int b = 0; b < SEG_BLOCKS; b++) {
+        const int j = j0 + b * 64 + lane;
+        mb[b] = j < j1 ? a.mask[j] : 0ull;
+        tb[b] = j < j1 ? a.tmatch[j] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < TB; q++) {
+        st[q] = __builtin_amdgcn_readlane(my_start, q);
+        off[q] = q < a.T ? a.candoff[q] : 0;
+        const int len = q < a.T ? a.candlen[q] : 0;
+        c0[q] = 0;
+#pragma unroll
+        for (int i = lane; i < SEG; i += 64) {
+            const int p = st[q] + i;
+            win[q * SEG + i] = p < len ? a.crank[off[q] + p] : ~0u;
+        }
     }
     __syncthreads();
-    int total_rounds = 0;
-    // software pipeline: the next block's inputs are loaded before the refill
-    // load; the prologue issues the same three loads in the same order so the
-    // loop header's wait is vmcnt(1) on both incoming edges
-    unsigned long long m_next = mask[min(lane, R - 1)];
-    int t_next = tmatch[min(lane, R - 1)];
-    unsigned int pend_key = crank[0];  // ring refill issued at the previous block end
-    bool pend_zero = true;
-    int pend_addr = -1;
-    for (int b0 = 0; b0 < R; b0 += 64) {
-        const int j = b0 + lane;
-        const unsigned long long m = (j < R && t_next < 0) ? m_next : 0ull;
-        unsigned long long U = 0;  // types present in the block (T ballots, no LDS traffic)
-        for (int t = 0; t < T; t++) U |= (unsigned long long)(__ballot((m >> t) & 1ull) != 0) << t;
+#pragma unroll
+    for (int b = 0; b < SEG_BLOCKS; b++) {
+        if (j0 + b * 64 >= j1) break;
+        const int j = j0 + b * 64 + lane;
+        const unsigned long long m = tb[b] < 0 ? mb[b] : 0ull;
+        bool have[TB];
+#pragma unroll
+        for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
         int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
-        unsigned int best;
-        unsigned long long changed;
+        unsigned long long chg;
         do {
-            best = ~0u;
-            for (int tb = 0; tb < T; tb += TB) {
-                if (!((U >> tb) & ((TB >= 64) ? ~0ull : ((1ull << TB) - 1)))) continue;
-                // branch-free group: all LDS reads are issued before the first use
+            unsigned int v[TB];
+#pragma unroll
+            for (int q = 0; q < TB; q++) v[q] = win[q * SEG + c0[q] + (int)mbcnt64(__ballot(ch == q))];
+            unsigned int best = ~0u;
+#pragma unroll
+            for (int q = 0; q < TB; q++) best = min(best, have[q] ? v[q] : ~0u);
+            const int nch = best == ~0u ? -1 : (int)(best & 63u);
+            chg = __ballot(nch != ch);
+            ch = nch;
+            rounds++;
+        } while (chg);
+        int res = -1;
+#pragma unroll
+        for (int q = 0; q < TB; q++) {
+            const unsigned long long B = __ballot(ch == q);
+            if (ch == q) res = off[q] + st[q] + c0[q] + (int)mbcnt64(B);
+            c0[q] += __popcll(B);
+        }
+        if (j < j1) a.umatch[j] = res;
+    }
+    int my_end = my_start;
+#pragma unroll
+    for (int q = 0; q < TB; q++)
+        if (lane == q) my_end = st[q] + c0[q];
+    return my_end;
+}
+
+// Any T <= 64: lane t keeps type t's state, uniform copies come from readlane;
+// rounds touch only the types present in the block, TB LDS reads in flight.
+template <int TB>
+__device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_start, unsigned int *win,
+                                              int &rounds) {
+    const int lane = threadIdx.x, T = a.T, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
+    const int my_off = lane < T ? a.candoff[lane] : 0;
+    const int my_len = lane < T ? a.candlen[lane] : 0;
+    for (int t = 0; t < T; t++) {
+        const int st = __builtin_amdgcn_readlane(my_start, t), off = __builtin_amdgcn_readlane(my_off, t);
+        const int len = __builtin_amdgcn_readlane(my_len, t);
+        for (int i = lane; i < SEG; i += 64) {
+            const int p = st + i;
+            win[t * SEG + i] = p < len ? a.crank[off + p] : ~0u;
+        }
+    }
+    __syncthreads();
+    int my_c0 = 0;
+    for (int b0 = j0; b0 < j1; b0 += 64) {
+        const int j = b0 + lane;
+        const unsigned long long m = (j < j1 && a.tmatch[j] < 0) ? a.mask[j] : 0ull;
+        const unsigned long long U = wave_or_u64(m);  // types present in the block
+        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
+        unsigned long long chg;
+        do {
+            unsigned int best = ~0u;
+            for (int g = 0; g < T; g += TB) {
+                if (!((U >> g) & ((1ull << TB) - 1))) continue;
                 unsigned int vq[TB];
                 bool okq[TB];
 #pragma unroll
                 for (int q = 0; q < TB; q++) {
-                    const int t = tb + q;
-                    const int tt = t < T ? t : 0;
-                    const int c0t = __builtin_amdgcn_readlane(my_c0, tt);
-                    const int lent = t < T ? __builtin_amdgcn_readlane(my_len, tt) : 0;
-                    const int pos = c0t + (int)mbcnt64(__ballot(ch == t));
-                    okq[q] = (((m >> tt) & 1ull) != 0) & (pos < lent);
-                    vq[q] = ring32[tt * RING + (pos & (RING - 1))];
+                    const int t = g + q, tt = t < T ? t : 0;
+                    const int pos = __builtin_amdgcn_readlane(my_c0, tt) + (int)mbcnt64(__ballot(ch == t));
+                    okq[q] = t < T && ((m >> tt) & 1ull);
+                    vq[q] = win[tt * SEG + pos];
                 }
 #pragma unroll
                 for (int q = 0; q < TB; q++) best = min(best, okq[q] ? vq[q] : ~0u);
             }
             const int nch = best == ~0u ? -1 : (int)(best & 63u);
-            changed = __ballot(nch != ch);
+            chg = __ballot(nch != ch);
             ch = nch;
-            total_rounds++;
-        } while (changed);
-        // position of the chosen type for each lane, from the converged choices
-        int res = 0;
+            rounds++;
+        } while (chg);
+        int res = -1;
         for (unsigned long long bb = U; bb; bb &= bb - 1) {
             const int t = __ffsll((long long)bb) - 1;
-            const unsigned long long Bt = __ballot(ch == t);
-            if (ch == t) res = __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(Bt) + __builtin_amdgcn_readlane(my_off, t);
+            const unsigned long long B = __ballot(ch == t);
+            if (ch == t)
+                res = __builtin_amdgcn_readlane(my_off, t) + __builtin_amdgcn_readlane(my_start, t) +
+                      __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(B);
+            if (lane == t) my_c0 += __popcll(B);
         }
-        if (j < R) umatch[j] = ch >= 0 ? res : -1;
-        // block end.  Memory-op order matters for vmcnt: the next block's inputs
-        // are loaded before the ring refill, both unconditionally, so the next
-        // block start waits only for its inputs (vmcnt(1)), not for the refill.
-        const int jn = min(j + 64, R - 1);
-        m_next = mask[jn];
-        t_next = tmatch[jn];  // lanes past R are masked by (j < R) at the next block start
-        __builtin_amdgcn_wave_barrier();
-        if (pend_addr >= 0) ring32[pend_addr] = pend_zero ? ~0u : pend_key;  // refill issued one block ago
-        int pre = 0, my_t = -1, my_k = 0;
-        for (unsigned long long bb = U; bb; bb &= bb - 1) {
-            const int t = __ffsll((long long)bb) - 1;
-            const int cnt = __popcll(__ballot(ch == t));
-            if (!cnt) continue;
-            const int c0t = __builtin_amdgcn_readlane(my_c0, t);
-            if (lane >= pre && lane < pre + cnt) {
-                my_t = t;
-                my_k = c0t + RING + (lane - pre);  // absolute position entering the ring
+        if (j < j1) a.umatch[j] = res;
+    }
+    return my_start + my_c0;
+}
+
+template <int TB>
+__device__ __forceinline__ int seg_solve(const ChainArgs &a, int s, int my_start, unsigned int *win, int &rounds) {
+    if constexpr (TB <= 8) return seg_solve_small<TB>(a, s, my_start, win, rounds);
+    else return seg_solve_wide<8>(a, s, my_start, win, rounds);
+}
+
+// Pass k of the segment iteration (k = 1 .. passes), one wavefront per segment.
+template <int TB>
+__global__ __launch_bounds__(64) void k_chain_pass(ChainArgs a, int k) {
+    extern __shared__ unsigned int win[];
+    const int s = blockIdx.x, lane = threadIdx.x, T = a.T;
+    if (k > 1 && a.changed[k - 1] == 0) return;  // pass k-1 found the fixed point
+    int *Ecur = a.E + (long long)(k & 1) * a.nseg * T;
+    const int *Eprev = a.E + (long long)((k - 1) & 1) * a.nseg * T;
+    int my_start = 0;
+    if (k == 1) {
+        // level guess: J = requests before this segment that take an untargeted unit
+        int J = 0;
+        for (int q = lane; q < s; q += 64) J += a.seg_cnt[q];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
+        if (lane < T && J > 0) {
+            const unsigned int *L = a.crank + a.candoff[lane];
+            int lo = 0, hi = a.candlen[lane];
+            const unsigned int key = (unsigned int)J << 6;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (L[mid] < key) lo = mid + 1;
+                else hi = mid;
             }
-            pre += cnt;
-            if (lane == t) my_c0 += cnt;
+            my_start = lo;
         }
-        const int tl = my_t < 0 ? 0 : my_t;
-        const int len = __shfl(my_len, tl, 64), off = __shfl(my_off, tl, 64);
-        const bool valid = my_t >= 0 && my_k < len;
-        pend_key = crank[valid ? off + my_k : 0];  // consumed one block later (no wait here)
-        pend_zero = !valid;
-        pend_addr = my_t >= 0 ? my_t * RING + (my_k & (RING - 1)) : -1;
+    } else {
+        my_start = (s > 0 && lane < T) ? Eprev[(s - 1) * T + lane] : 0;
+        const bool same = !__ballot(lane < T && my_start != a.Sprev[s * T + lane]);
+        if (same) {  // unchanged start: last computation stands, carry its end state
+            if (lane < T) Ecur[s * T + lane] = Eprev[s * T + lane];
+            return;
+        }
     }
-    if (lane == 0 && rounds_out) *rounds_out = total_rounds;
+    int rounds = 0;
+    const int my_end = seg_solve<TB>(a, s, my_start, win, rounds);
+    if (lane < T) {
+        Ecur[s * T + lane] = my_end;
+        a.Sprev[s * T + lane] = my_start;
+    }
+    if (lane == 0) {
+        atomicAdd(&a.changed[k], 1);
+        atomicAdd(&a.ctr->chain_rounds, rounds);
+    }
 }
 
-// Small-T variant (T <= TB): every per-type quantity of a block is hoisted
-// into registers once per block (uniform values live in SGPRs), rounds are
-// straight-line code, and no cross-lane shuffles are used at block ends.
+// After `passes` passes: nothing to do at a fixed point; otherwise walk the
+// segments in order from the exact start (segment 0 starts at 0) and recompute
+// each one whose start differs from its last computation's.
 template <int TB>
-struct SmallChainState {
-    int c0[TB], len[TB], off[TB];
-    unsigned int pend_key;
-    bool pend_zero;
-    int pend_addr;
-    int rounds;
-};
-
-// One 64-request block of the small-T chain.  (m_in, t_in) hold this block's
-// inputs and are overwritten with the inputs of the block two ahead, so the
-// caller alternates two register sets without moves (no wait on a fresh load).
-template <int TB>
-__device__ __forceinline__ void small_chain_block(SmallChainState<TB> &st, unsigned int *ring32, int b0, int R,
-                                                  unsigned long long &m_in, int &t_in,
-                                                  const unsigned long long *__restrict__ mask,
-                                                  const int *__restrict__ tmatch,
-                                                  const unsigned int *__restrict__ crank,
-                                                  int *__restrict__ umatch) {
-    const int lane = threadIdx.x;
-    const int j = b0 + lane;
-    const unsigned long long m = (j < R && t_in < 0) ? m_in : 0ull;
-    bool have[TB];
-#pragma unroll
-    for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
-    int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
-    unsigned long long changed;
-    do {
-        unsigned int v[TB];
-        bool ok[TB];
-#pragma unroll
-        for (int q = 0; q < TB; q++) {
-            const int pos = st.c0[q] + (int)mbcnt64(__ballot(ch == q));
-            ok[q] = have[q] & (pos < st.len[q]);
-            v[q] = ring32[q * RING + (pos & (RING - 1))];
+__global__ __launch_bounds__(64) void k_chain_fix(ChainArgs a, int passes) {
+    extern __shared__ unsigned int win[];
+    const int lane = threadIdx.x, T = a.T;
+    int used = 0, recomputed = 0;
+    for (int k = 1; k <= passes; k++) {
+        used += a.changed[k] > 0;
+        recomputed += a.changed[k];
+    }
+    const bool fixed = a.changed[passes] == 0;
+    if (lane == 0) {
+        a.ctr->chain_passes = used;
+        a.ctr->chain_recomputed = recomputed;
+        a.ctr->chain_fallback = 0;
+    }
+    if (fixed) return;
+    const int *E = a.E + (long long)(passes & 1) * a.nseg * T;
+    int st = 0, rounds = 0, redo = 0;
+    for (int s = 0; s < a.nseg; s++) {
+        const bool same = !__ballot(lane < T && st != a.Sprev[s * T + lane]);
+        if (same) {
+            st = lane < T ? E[s * T + lane] : 0;
+        } else {
+            st = seg_solve<TB>(a, s, st, win, rounds);
+            __syncthreads();  // win is refilled by the next recomputed segment
+            redo++;
         }
-        unsigned int best = ~0u;
-#pragma unroll
-        for (int q = 0; q < TB; q++) best = min(best, ok[q] ? v[q] : ~0u);
-        const int nch = best == ~0u ? -1 : (int)(best & 63u);
-        changed = __ballot(nch != ch);
-        ch = nch;
-        st.rounds++;
-    } while (changed);
-    // results, c0 advance and refill assignment in one pass over the types
-    int res = -1, pre = 0, my_q = -1, my_k = 0, my_len = 0, my_off = 0;
-#pragma unroll
-    for (int q = 0; q < TB; q++) {
-        const unsigned long long B = __ballot(ch == q);
-        const int cnt = __popcll(B);
-        if (ch == q) res = st.off[q] + st.c0[q] + (int)mbcnt64(B);
-        if (lane >= pre && lane < pre + cnt) {
-            my_q = q;
-            my_k = st.c0[q] + RING + (lane - pre);  // absolute position entering the ring
-            my_len = st.len[q];
-            my_off = st.off[q];
-        }
-        pre += cnt;
-        st.c0[q] += cnt;
     }
-    if (j < R) umatch[j] = res;
-    const int jn = min(j + 128, R - 1);
-    m_in = mask[jn];
-    t_in = tmatch[jn];  // lanes past R are masked by (j < R) at their block start
-    __builtin_amdgcn_wave_barrier();
-    // refill of one block ago; lanes without one write the spare slot past the
-    // rings, so the store (and the wait on its load) is unconditional
-    ring32[st.pend_addr] = st.pend_zero ? ~0u : st.pend_key;
-    const bool valid = my_q >= 0 && my_k < my_len;
-    st.pend_key = crank[valid ? my_off + my_k : 0];  // consumed one block later (no wait here)
-    st.pend_zero = !valid;
-    st.pend_addr = my_q >= 0 ? my_q * RING + (my_k & (RING - 1)) : TB * RING;
-}
-
-// Small-T variant (T <= TB): every per-type quantity of a block is hoisted
-// into registers once per block (uniform values live in SGPRs), rounds are
-// straight-line code, and no cross-lane shuffles are used at block ends.
-template <int TB>
-__global__ __launch_bounds__(64) void k_chain_small(const unsigned long long *__restrict__ mask,
-                                                    const int *__restrict__ tmatch, int R, int T,
-                                                    const int *__restrict__ candoff,
-                                                    const int *__restrict__ candlen,
-                                                    const unsigned int *__restrict__ crank,
-                                                    int *__restrict__ umatch, int *__restrict__ rounds_out) {
-    extern __shared__ unsigned int ring32[];  // [TB][RING] packed ranks + 1 spare slot
-    const int lane = threadIdx.x;
-    SmallChainState<TB> st;
-#pragma unroll
-    for (int q = 0; q < TB; q++) {
-        st.c0[q] = 0;
-        st.len[q] = q < T ? candlen[q] : 0;
-        st.off[q] = q < T ? candoff[q] : 0;
-        for (int i = lane; i < RING; i += 64) ring32[q * RING + i] = i < st.len[q] ? crank[st.off[q] + i] : ~0u;
+    if (lane == 0) {
+        a.ctr->chain_fallback = redo;
+        atomicAdd(&a.ctr->chain_rounds, rounds);
     }
-    __syncthreads();
-    st.rounds = 0;
-    // two register sets of block inputs, each refilled two blocks ahead
-    unsigned long long mA = mask[min(lane, R - 1)];
-    int tA = tmatch[min(lane, R - 1)];
-    unsigned long long mB = mask[min(lane + 64, R - 1)];
-    int tB = tmatch[min(lane + 64, R - 1)];
-    st.pend_key = 0;
-    st.pend_zero = true;
-    st.pend_addr = TB * RING;
-    // consume the prologue loads here so the loop is entered with no loads in
-    // flight: the waitcnt state at the loop header is then the back-edge one,
-    // where each block's inputs landed a block earlier
-    asm volatile("" : "+v"(mA), "+v"(tA), "+v"(mB), "+v"(tB));
-    int b0 = 0;
-    for (; b0 + 64 < R; b0 += 128) {  // every back edge has run both blocks
-        small_chain_block<TB>(st, ring32, b0, R, mA, tA, mask, tmatch, crank, umatch);
-        small_chain_block<TB>(st, ring32, b0 + 64, R, mB, tB, mask, tmatch, crank, umatch);
-    }
-    if (b0 < R) small_chain_block<TB>(st, ring32, b0, R, mA, tA, mask, tmatch, crank, umatch);
-    if (lane == 0 && rounds_out) *rounds_out = st.rounds;
 }
 
 // ---------------------------------------------------------------- finalize
@@ -835,7 +878,8 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     if (n <= h->cap_req) return ADLBQ_OK;
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
-    void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf};
+    void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
+                  h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
@@ -843,6 +887,11 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_umatch, sizeof(int) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_reqbuf, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
+    const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
+    AQ_HIP(hipMalloc((void **)&h->d_seg_cnt, sizeof(int) * nseg));
+    AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * 2 * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chS, sizeof(int) * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chchg, sizeof(int) * (CHAIN_MAX_PASSES + 2)));
     h->cap_req = nc;
     return ADLBQ_OK;
 }
@@ -892,7 +941,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
 
     AQ_HIP(hipMemsetAsync(h->d_dem, 0, sizeof(int) * std::max(T, 1), s));
     stage_begin(h, "prep", &ev);
-    k_req_prep<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem);
+    k_req_prep<<<(R + SEG - 1) / SEG, SEG, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt,
+                                                 h->d_chchg, h->d_ctr);
     stage_end(h, "prep", ev);
 
     if (np > 0 && T > 0) {
@@ -932,7 +982,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if (h->live_targeted > 0 && nb > 0) {
         stage_begin(h, "targeted", &ev);
         k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
-                                      h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch);
+                                      h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);
         stage_end(h, "targeted", ev);
     }
     if (np > 0 && T > 0) {
@@ -942,22 +992,17 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     stage_begin(h, "chain", &ev);
     {
-        const size_t lds = sizeof(unsigned int) * RING * std::max(T, 1);
-        if (T <= 2)
-            k_chain_small<2><<<1, 64, sizeof(unsigned int) * (RING * 2 + 1), s>>>(
-                h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
-                &h->d_ctr->chain_rounds);
-        else if (T <= 4)
-            k_chain_small<4><<<1, 64, sizeof(unsigned int) * (RING * 4 + 1), s>>>(
-                h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
-                &h->d_ctr->chain_rounds);
-        else if (T <= 8)
-            k_chain_small<8><<<1, 64, sizeof(unsigned int) * (RING * 8 + 1), s>>>(
-                h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
-                &h->d_ctr->chain_rounds);
-        else
-            k_chain<8><<<1, 64, lds, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_candoff, h->d_candlen, h->d_crank,
-                                          h->d_umatch, &h->d_ctr->chain_rounds);
+        const int nseg = (R + SEG - 1) / SEG, P = h->chain_passes;
+        ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
+                     h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg, h->d_ctr};
+        auto run = [&](auto kpass, auto kfix, int tw) {
+            const size_t lds = sizeof(unsigned int) * SEG * tw;
+            for (int k = 1; k <= P; k++) kpass<<<nseg, 64, lds, s>>>(ca, k);
+            kfix<<<1, 64, lds, s>>>(ca, P);
+        };
+        if (T <= 4) run(k_chain_pass<4>, k_chain_fix<4>, 4);
+        else if (T <= 8) run(k_chain_pass<8>, k_chain_fix<8>, 8);
+        else run(k_chain_pass<64>, k_chain_fix<64>, T);
     }
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);

@@ -509,7 +509,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_gh, h->d_pp, h->d_csum,
-                    h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result};
+                    h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
+                    h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -872,12 +873,26 @@ int adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, lon
 
 long long adlbq_last_scan_units(adlbq_server *h) { return h ? h->last_scan_units : 0; }
 
+int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
+    if (!h || !name) return fail(ADLBQ_ERR_ARG, "adlbq_set_param");
+    std::string n(name);
+    if (n == "chain_passes") {
+        if (value < 1 || value > 30) return fail(ADLBQ_ERR_ARG, "chain_passes must be in [1, 30]");
+        h->chain_passes = (int)value;
+        return ADLBQ_OK;
+    }
+    return fail(ADLBQ_ERR_ARG, "adlbq_set_param: unknown parameter");
+}
+
 long long adlbq_stat(adlbq_server *h, const char *name) {
     if (!h || !name) return -1;
     hipSetDevice(h->device);
     if (refresh_counters(h)) return -1;
     std::string n(name);
     if (n == "chain_rounds") return h->ctr.chain_rounds;
+    if (n == "chain_passes") return h->ctr.chain_passes;
+    if (n == "chain_recomputed") return h->ctr.chain_recomputed;
+    if (n == "chain_fallback") return h->ctr.chain_fallback;
     if (n == "parked") return h->ctr.n_parked_last;
     if (n == "candidates") {
         int v = 0;

@@ -181,3 +181,7 @@ class Server:
 
     def last_scan_units(self) -> int:
         return int(self.lib.adlbq_last_scan_units(self.h))
+
+    def set_param(self, name: str, value: int) -> None:
+        """Tuning knobs of the engine (adlbq_set_param); results never depend on them."""
+        _lib.check(self.lib.adlbq_set_param(self.h, name.encode(), int(value)), "adlbq_set_param")

@@ -64,7 +64,7 @@ def parse():
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
 KERNEL_OF = {"prep": "k_req_prep", "hist": "k_hist_open", "thresholds": "k_thresholds",
              "prefix": "k_page_prefix", "select": "k_select_open", "sort": "k_sort_types",
-             "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain", "finalize": "k_finalize",
+             "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain_pass", "finalize": "k_finalize",
              "park": "k_park"}
 
 
@@ -282,7 +282,7 @@ def main():
                               "k_hist_open + k_select_open") if scan_ms else None,
         "roofline_batch": roof(alg["batch"], batch_ms, None, "all reserve-batch kernels"),
         "kernels_ms": kernels,
-        "chain_rounds_last_batch": srv.stat("chain_rounds"),
+        "chain_last_batch": {k: srv.stat("chain_" + k) for k in ("rounds", "passes", "recomputed", "fallback")},
         "candidates_last_batch": srv.stat("candidates"),
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -141,8 +141,16 @@ int  adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, lo
  * 16 B x live units. */
 long long adlbq_last_scan_units(adlbq_server *h);
 /* Diagnostics of the last reserve batch: "chain_rounds" (Jacobi rounds of the
- * ordered-choice kernel), "parked" (Reserves parked), "candidates". -1 if unknown. */
+ * ordered-choice kernels, all wavefronts), "chain_passes" (segment passes that
+ * recomputed something), "chain_recomputed" (segment solves in those passes),
+ * "chain_fallback" (segments the in-order fix-up recomputed; 0 when the passes
+ * reached their fixed point), "parked" (Reserves parked), "candidates".
+ * -1 if unknown. */
 long long adlbq_stat(adlbq_server *h, const char *name);
+/* Tuning: "chain_passes" = parallel segment passes of the ordered-choice
+ * kernel before the in-order fix-up (1..30, default 8).  Results never depend
+ * on it; tests lower it to force the fix-up path. */
+int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);
 const char *adlbq_version(void);
 

@@ -2,7 +2,9 @@
 every entry point include/adlbq.h declares, and the Python mirror covers them.
 No compute calls here (no GPU in the build container)."""
 import os
+import shutil
 import subprocess
+import tempfile
 
 import pytest
 
@@ -11,8 +13,11 @@ from adlb_amd import _lib
 
 def test_library_built_for_gfx950():
     assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() first"
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
-                         capture_output=True, text=True)
+    # --offloading extracts the device images next to its input: work on a copy
+    with tempfile.TemporaryDirectory() as d:
+        lib = shutil.copy(_lib.LIB_PATH, d)
+        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
+                             capture_output=True, text=True, cwd=d)
     txt = out.stdout + out.stderr
     assert "gfx950" in txt
 

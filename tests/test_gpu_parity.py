@@ -21,9 +21,14 @@ pytestmark = pytest.mark.gpu
 GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
 
 
-def run_abi(ut, cfg, trace, max_units=1 << 16):
+def run_abi(ut, cfg, trace, max_units=1 << 16, params=None, stats=None):
     with Server(ut, int(cfg[0]), int(cfg[1]), int(cfg[2]), max_units=max_units) as s:
-        return replay.replay(s, trace)
+        for k, v in (params or {}).items():
+            s.set_param(k, v)
+        out = replay.replay(s, trace)
+        if stats is not None:
+            stats.update({k: s.stat(k) for k in ("chain_passes", "chain_recomputed", "chain_fallback")})
+        return out
 
 
 def run_oracle(ut, cfg, trace):
@@ -64,6 +69,21 @@ def test_fresh_vs_oracle(gpu_available, name):
     tr = synth.workload_trace(w)
     cfg = (w.num_app_ranks, 1, 0)
     assert_same(run_abi(w.user_types, cfg, tr, max_units=w.n_units), run_oracle(w.user_types, cfg, tr))
+
+
+@pytest.mark.parametrize("name", ["c2_n200k_r16k", "c2_t64_wide", "c4_n200k", "c4_t8_tied"])
+@pytest.mark.parametrize("passes", [1, 2])
+def test_chain_fixup_path(gpu_available, name, passes):
+    """Few segment passes leave segments off their fixed point, so the in-order
+    fix-up kernel (k_chain_fix) recomputes them: still identical to the oracle."""
+    w = CASES[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    st = {}
+    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units, params={"chain_passes": passes}, stats=st)
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
+    if name == "c2_n200k_r16k" and passes == 1:
+        assert st["chain_fallback"] > 0, st
 
 
 def test_stream_vs_oracle(gpu_available):
