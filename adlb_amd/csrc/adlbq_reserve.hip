@@ -81,48 +81,60 @@ __global__ __launch_bounds__(SEG) void k_req_prep(const int *__restrict__ reqs, 
 }
 
 // ---------------------------------------------------------------- pass 1
+// One workgroup per page: each wave owns a quarter of the page and issues all
+// of its loads (8 x 16 B per lane) before counting.  The histogram is kept in
+// HK lane-interleaved copies so that lanes hitting the same (type, bin) column
+// (most units fall in a few far bins) do not serialise one LDS atomic.
+constexpr int HK = 4;
+
 __global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages, int npages, int tail_fill,
                                                    const int *__restrict__ prio, const uint32_t *__restrict__ meta,
                                                    int T, const long long *__restrict__ anchor,
                                                    const int *__restrict__ dem, unsigned short *__restrict__ gh,
                                                    unsigned int *__restrict__ csum) {
-    extern __shared__ unsigned int lds[];
+    extern __shared__ unsigned int hist[];  // [C][HK]
     __shared__ long long sanc[ADLBQ_MAX_TYPES];
     __shared__ int sdem[ADLBQ_MAX_TYPES];
-    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        sanc[t] = anchor[t];
-        sdem[t] = dem[t];
-    }
-    unsigned int *hist = lds + w * C;
-    for (int c = lane; c < C; c += 64) hist[c] = 0;
-    __syncthreads();
-    const int p = blockIdx.x * 4 + w;
-    if (p >= npages) return;
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = blockIdx.x;
     const long long base = (long long)pages[p] << PAGE_SHIFT;
     const int fill = (p == npages - 1) ? tail_fill : PAGE;
     const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
     const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
-    const int nit = (fill + 255) >> 8;
-#pragma unroll 4
-    for (int it = 0; it < nit; it++) {
-        int4 pv = P4[it * 64 + lane];
-        uint4 mv = M4[it * 64 + lane];
-        int pr[4] = {pv.x, pv.y, pv.z, pv.w};
-        uint32_t mm[4] = {mv.x, mv.y, mv.z, mv.w};
+    int4 pv[4];
+    uint4 mv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = (w * 4 + k) * 64 + lane;
+        const bool ok = idx * 4 < fill;
+        pv[k] = ok ? P4[idx] : make_int4(0, 0, 0, 0);
+        mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
+    }
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        sanc[t] = anchor[t];
+        sdem[t] = dem[t];
+    }
+    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
+    unsigned int *my = hist + (lane % HK);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
+        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if ((mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST) {
-                int t = mm[q] & M_TYPE;
-                if (sdem[t] > 0) atomicAdd(&hist[t * NB + bin_of(sanc[t] - pr[q])], 1u);
+                const int t = mm[q] & M_TYPE;
+                if (sdem[t] > 0) atomicAdd(&my[(t * NB + bin_of(sanc[t] - pr[q])) * HK], 1u);
             }
         }
     }
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
     unsigned int *cs = csum + (long long)(p / CHUNK) * C;
     unsigned short *g = gh + (long long)p * C;
-    for (int c = lane; c < C; c += 64) {
-        unsigned int v = hist[c];
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        unsigned int v = 0;
+#pragma unroll
+        for (int k = 0; k < HK; k++) v += hist[c * HK + k];
         g[c] = (unsigned short)v;
         if (v) atomicAdd(&cs[c], v);
     }
@@ -197,7 +209,7 @@ __global__ __launch_bounds__(1024) void k_thresholds(int T, const int *__restric
 // in column c (= type, bin); only the columns a type takes (bin <= theta).
 __global__ __launch_bounds__(256) void k_page_prefix(int npages, int T, const int *__restrict__ theta,
                                                      const unsigned short *__restrict__ gh,
-                                                     const unsigned int *__restrict__ csum,
+                                                     unsigned int *__restrict__ csum,
                                                      unsigned int *__restrict__ pp) {
     const int C = T * NB;
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -205,8 +217,9 @@ __global__ __launch_bounds__(256) void k_page_prefix(int npages, int T, const in
     if (i >= (long long)nchunks * C) return;
     const int k = (int)(i / C), c = (int)(i - (long long)k * C);
     const int t = c / NB, b = c - t * NB;
-    if (b > theta[t]) return;
     unsigned int run = csum[(long long)k * C + c];
+    csum[(long long)k * C + c] = 0;  // last reader: leave the chunk sums zeroed for the next batch
+    if (b > theta[t]) return;
     const int p1 = min(npages, (k + 1) * CHUNK);
     for (int p = k * CHUNK; p < p1; p++) {
         pp[(long long)p * C + c] = run;
@@ -215,90 +228,128 @@ __global__ __launch_bounds__(256) void k_page_prefix(int npages, int T, const in
 }
 
 // ---------------------------------------------------------------- pass 2
+// Order-preserving compaction of the candidates (the units of each type in the
+// bins up to its threshold) into per-type lists in (prio desc, wqseqno asc)
+// order.  One workgroup per page, each wave a quarter of it:
+//   1. all loads issued up front; a unit is a candidate iff prio >= cut[t]
+//      (equivalent to bin_of(anchor - prio) <= theta[t]);
+//   2. each wave appends its candidates, in slot order, to an LDS list
+//      (key = column << 12 | slot-in-page) and counts them per column;
+//   3. per column: page prefix (k_page_prefix) + counts of the earlier waves;
+//   4. a candidate's rank in its column = that start + the number of equal
+//      columns earlier in the wave's list (64 list entries per step).
 __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
     const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
     const int *__restrict__ theta, const int *__restrict__ need, const int *__restrict__ candoff,
     const int *__restrict__ binoff, const unsigned int *__restrict__ pp,
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot) {
-    extern __shared__ unsigned int lds[];
-    __shared__ long long sanc[ADLBQ_MAX_TYPES];
+    extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
+    __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
     __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES];
-    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        sanc[t] = anchor[t];
-        sth[t] = theta[t];
-        sneed[t] = need[t];
-        soff[t] = candoff[t];
-    }
-    __syncthreads();
-    const int p = blockIdx.x * 4 + w;
-    if (p >= npages) return;
-    // running rank of each (type, bin) column, in wqseqno order over the whole open bucket
-    unsigned int *run = lds + w * C;
-    for (int c = lane; c < C; c += 64) {
-        const int t = c / NB, b = c - t * NB;
-        if (b <= sth[t]) run[c] = pp[(long long)p * C + c];
-    }
-    __builtin_amdgcn_wave_barrier();
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = blockIdx.x;
+    unsigned int *wc = lds;
+    unsigned int *list = lds + 4 * C + w * 1024;
     const long long base = (long long)pages[p] << PAGE_SHIFT;
     const int fill = (p == npages - 1) ? tail_fill : PAGE;
     const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
     const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
-    const int nit = (fill + 255) >> 8;
+    int4 pv[4];
+    uint4 mv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = (w * 4 + k) * 64 + lane;
+        const bool ok = idx * 4 < fill;
+        pv[k] = ok ? P4[idx] : make_int4(0, 0, 0, 0);
+        mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
+    }
+    // page prefix of this thread's columns, loaded early (only columns at or below a threshold are read)
+    constexpr int CPT = (ADLBQ_MAX_TYPES * NB) / 256;  // columns per thread, at most
+    unsigned int ppv[CPT];
+#pragma unroll
+    for (int r = 0; r < CPT; r++) {
+        const int c = threadIdx.x + r * 256;
+        ppv[r] = 0;
+        if (c < C && (c % NB) <= theta[c / NB]) ppv[r] = pp[(long long)p * C + c];
+    }
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        const int th = theta[t];
+        const long long an = anchor[t];
+        sanc[t] = an;
+        sth[t] = th;
+        sneed[t] = need[t];
+        soff[t] = candoff[t];
+        // largest anchor distance of bin th (bin_of: exact below NBX, then powers of two)
+        const long long dmax = th < 0 ? -1 : th < NBX ? th : th >= NB - 1 ? (1ll << 40) : (1ll << (th - NBX + 6)) - 1;
+        scut[t] = th < 0 ? (1ll << 40) : std::max(an - dmax, (long long)LOWEST + 1);
+    }
+    for (int c = threadIdx.x; c < 4 * C; c += blockDim.x) wc[c] = 0;
+    __syncthreads();
+    int n = 0;  // this wave's candidates so far (uniform)
     const unsigned long long lt = lanemask_lt();
-    for (int it = 0; it < nit; it++) {
-        int4 pv = P4[it * 64 + lane];
-        uint4 mv = M4[it * 64 + lane];
-        int pr[4] = {pv.x, pv.y, pv.z, pv.w};
-        uint32_t mm[4] = {mv.x, mv.y, mv.z, mv.w};
-        int key[4];
-        bool pend[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
+        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+        bool cnd[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            cnd[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && (long long)pr[q] >= scut[mm[q] & M_TYPE];
+        const unsigned long long b0 = __ballot(cnd[0]), b1 = __ballot(cnd[1]), b2 = __ballot(cnd[2]),
+                                 b3 = __ballot(cnd[3]);
+        if (!(b0 | b1 | b2 | b3)) continue;
+        int pos = n + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            key[q] = -1;
-            if ((mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST) {
-                int t = mm[q] & M_TYPE;
-                if (sth[t] >= 0) {
-                    int b = bin_of(sanc[t] - pr[q]);
-                    if (b <= sth[t]) key[q] = t * NB + b;
-                }
+            if (cnd[q]) {
+                const int t = mm[q] & M_TYPE;
+                const int col = t * NB + bin_of(sanc[t] - pr[q]);
+                atomicAdd(&wc[w * C + col], 1u);
+                list[pos++] = ((unsigned int)col << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
             }
-            pend[q] = key[q] >= 0;
         }
-        // group pending candidates by column; ranks follow (lane, q) == slot order
-        while (true) {
-            unsigned long long any = __ballot(pend[0] || pend[1] || pend[2] || pend[3]);
-            if (!any) break;
-            int fk = pend[0] ? key[0] : pend[1] ? key[1] : pend[2] ? key[2] : pend[3] ? key[3] : -1;
-            const int leader = __ffsll((long long)any) - 1;
-            const int k = __builtin_amdgcn_readlane(fk, leader);
-            unsigned long long m0 = __ballot(pend[0] && key[0] == k), m1 = __ballot(pend[1] && key[1] == k);
-            unsigned long long m2 = __ballot(pend[2] && key[2] == k), m3 = __ballot(pend[3] && key[3] == k);
-            const unsigned int rbase = run[k];
-            const int before = __popcll(m0 & lt) + __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
-            const int t = k / NB, b = k - t * NB;
-            const unsigned long long ms[4] = {m0, m1, m2, m3};
-            int within = 0;
+        n += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+    }
+    __syncthreads();
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if ((ms[q] >> lane) & 1ull) {
-                    const unsigned int r = rbase + before + within;
-                    within++;
-                    pend[q] = false;
-                    const bool keep = b < sth[t] || b >= NBX || (int)r < sneed[t];
-                    if (keep) {
-                        const long long pos = (long long)soff[t] + binoff[k] + r;
-                        const long long slot = base + it * 256 + lane * 4 + q;
-                        ckey[pos] = make_key(pr[q], (unsigned int)seqa[slot]);
-                        cslot[pos] = (int)slot;
-                    }
-                }
+    for (int r = 0; r < CPT; r++) {
+        const int c = threadIdx.x + r * 256;
+        if (c < C && (c % NB) <= sth[c / NB]) {
+            unsigned int run = ppv[r];
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const unsigned int x = wc[v * C + c];
+                wc[v * C + c] = run;
+                run += x;
             }
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) run[k] = rbase + __popcll(m0) + __popcll(m1) + __popcll(m2) + __popcll(m3);
-            __builtin_amdgcn_wave_barrier();
         }
+    }
+    __syncthreads();
+    unsigned int *run = wc + w * C;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        const unsigned int e = i < n ? list[i] : 0u;
+        const int col = (int)(e >> 12), so = (int)(e & (PAGE - 1));
+        int pr = 0, sq = 0;
+        if (i < n) {
+            pr = prio[base + so];
+            sq = seqa[base + so];
+        }
+        int rank = 0;
+        const int jn = min(n - i0, 64);
+        for (int j = 0; j < jn; j++) rank += (j < lane) & ((int)(list[i0 + j] >> 12) == col);
+        if (i < n) {
+            const unsigned int r = run[col] + rank;
+            const int t = col / NB, b = col - t * NB;
+            if (b < sth[t] || b >= NBX || (int)r < sneed[t]) {  // exact threshold bin: its first `need` only
+                const long long at = (long long)soff[t] + binoff[col] + r;
+                ckey[at] = make_key(pr, (unsigned int)sq);
+                cslot[at] = (int)(base + so);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (i < n) atomicAdd(&run[col], 1u);  // after every lane of the step has read run[]
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -913,6 +964,8 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         if (h->d_csum) AQ_HIP(hipFree(h->d_csum));
         h->cap_csum = std::max(need_cs, 2 * h->cap_csum);
         AQ_HIP(hipMalloc((void **)&h->d_csum, sizeof(unsigned int) * h->cap_csum));
+        // zero once; every batch's k_page_prefix re-zeroes the rows it used
+        AQ_HIP(hipMemsetAsync(h->d_csum, 0, sizeof(unsigned int) * h->cap_csum, h->stream));
     }
     if (need_cand > h->cap_cand) {
         void *ps[] = {h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank};
@@ -947,9 +1000,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
 
     if (np > 0 && T > 0) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
-        AQ_HIP(hipMemsetAsync(h->d_csum, 0, sizeof(unsigned int) * (size_t)nchunks * C, s));
         stage_begin(h, "hist", &ev);
-        k_hist_open<<<(np + 3) / 4, 256, sizeof(unsigned int) * 4 * C, s>>>(
+        k_hist_open<<<np, 256, sizeof(unsigned int) * HK * C, s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_dem, h->d_gh,
             h->d_csum);
         stage_end(h, "hist", ev);
@@ -963,7 +1015,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         k_page_prefix<<<(int)((ncol + 255) / 256), 256, 0, s>>>(np, T, h->d_theta, h->d_gh, h->d_csum, h->d_pp);
         stage_end(h, "prefix", ev);
         stage_begin(h, "select", &ev);
-        k_select_open<<<(np + 3) / 4, 256, sizeof(unsigned int) * 4 * C, s>>>(
+        k_select_open<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_candoff, h->d_binoff, h->d_pp, h->d_ckey, h->d_cslot);
         stage_end(h, "select", ev);
