@@ -41,6 +41,7 @@ SIGNATURES = {
     "adlbq_sync": (c_int, [P]),
     "adlbq_profile_enable": (c_int, [P, c_int]),
     "adlbq_profile_read": (c_int, [P, c_char_p, P, P]),
+    "adlbq_profile_only": (c_int, [P, c_char_p]),
     "adlbq_last_scan_units": (c_ll, [P]),
     "adlbq_stat": (c_ll, [P, c_char_p]),
     "adlbq_set_param": (c_int, [P, c_char_p, c_ll]),

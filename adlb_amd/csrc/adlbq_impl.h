@@ -109,7 +109,15 @@ struct adlbq_server {
     adlbq::DevCounters *d_ctr = nullptr;
     adlbq::DevCounters ctr{};      // host copy
     bool ctr_stale = false;
-    int rq_n_upper = 0;            // upper bound on rq_n while ctr is stale
+    long long rq_n_upper = 0;      // upper bound on rq_n while ctr is stale
+    // rq_n snapshots written by k_park into mapped host memory at the end of
+    // each reserve batch, so the rq capacity bound tightens without a sync
+    static constexpr int NSNAP = 4;
+    adlbq::DevCounters *h_snap = nullptr;   // [NSNAP] pinned, device-visible
+    hipEvent_t snap_ev[NSNAP] = {};
+    long long snap_at[NSNAP] = {};         // reserves launched up to and including that batch
+    int snap_next = 0;
+    long long launched_reserves = 0;
 
     // ---- qmstat / donor selection
     std::vector<int> qm_hi, qm_qlen;
@@ -136,15 +144,19 @@ struct adlbq_server {
     int *d_cslot = nullptr, *d_cslot2 = nullptr;
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate
     int *d_seg_cnt = nullptr;          // [nseg] chain: untargeted-capable requests per segment
-    int *d_chE = nullptr;              // [2][nseg][T] chain: segment end states
+    int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
+    int *d_chcomp = nullptr;           // [passes + 1][nseg] chain: segment computed in pass k
     int *d_chS = nullptr;              // [nseg][T] chain: segment starts of the last computation
     int *d_chchg = nullptr;            // [CHAIN_MAX_PASSES + 2] chain: segments recomputed per pass
-    int chain_passes = 8;              // passes before k_chain_fix (adlbq_set_param "chain_passes")
+    int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
+    int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")
     int *d_result = nullptr;           // small result scratch (16 ints)
     int *h_result = nullptr;           // pinned host mirror
     long long last_scan_units = 0;
 
     bool profiling = false;
+    std::string profile_only;                 // empty: every stage
+    std::vector<hipEvent_t> event_pool;
     std::unordered_map<std::string, adlbq::StageTimer> timers;
 };
 
@@ -161,6 +173,7 @@ int hip_fail(hipError_t e, const char *where);
 int ensure_req_capacity(adlbq_server *h, int n);
 int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
+void tighten_rq_bound(adlbq_server *h);    // newest completed batch snapshot -> rq_n_upper (no sync)
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);

@@ -29,6 +29,7 @@ using namespace adlbq;
 constexpr int SEG = 256;               // chain segment: requests per wavefront (== k_req_prep's block)
 constexpr int SEG_BLOCKS = SEG / 64;
 constexpr int CHAIN_MAX_PASSES = 30;   // bound of the settable pass count (adlbq_set_param)
+constexpr int CHAIN_WARM = 512;        // pass-1 warm-up before each segment (T <= 8), a multiple of SEG
 
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
     unsigned int lo = __builtin_amdgcn_readlane((unsigned int)v, l);
@@ -42,7 +43,8 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 __global__ __launch_bounds__(SEG) void k_req_prep(const int *__restrict__ reqs, int R, const int *__restrict__ utypes,
                                                   int T, unsigned long long *__restrict__ mask, int *dem,
                                                   int *__restrict__ seg_cnt, int *__restrict__ changed,
-                                                  DevCounters *ctr) {
+                                                  DevCounters *ctr, int *__restrict__ tmatch,
+                                                  int *__restrict__ comp, int nseg) {
     __shared__ int su[ADLBQ_MAX_TYPES], sd[ADLBQ_MAX_TYPES];
     __shared__ int scnt;
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
@@ -50,6 +52,7 @@ __global__ __launch_bounds__(SEG) void k_req_prep(const int *__restrict__ reqs, 
         sd[t] = 0;
     }
     if (threadIdx.x == 0) scnt = 0;
+    if (threadIdx.x <= CHAIN_MAX_PASSES) comp[(long long)threadIdx.x * nseg + blockIdx.x] = 0;
     if (blockIdx.x == 0) {
         if (threadIdx.x < CHAIN_MAX_PASSES + 2) changed[threadIdx.x] = 0;
         if (threadIdx.x == 0) ctr->chain_rounds = 0;
@@ -58,6 +61,7 @@ __global__ __launch_bounds__(SEG) void k_req_prep(const int *__restrict__ reqs, 
     int j = blockIdx.x * blockDim.x + threadIdx.x;
     bool nonempty = false;
     if (j < R) {
+        tmatch[j] = -1;
         const int *rt = reqs + (long long)ADLBQ_RESERVE_INTS * j + 2;
         unsigned long long m = 0;
         bool wild = false;
@@ -590,52 +594,103 @@ __global__ __launch_bounds__(256) void k_rank(int T, const int *__restrict__ can
 struct ChainArgs {
     const unsigned long long *mask;  // [R] type masks (0: no untargeted choice)
     const int *tmatch;               // [R] slot matched in the targeted phase, or -1
-    int R, T, nseg;
+    int R, T, nseg, passes, warm;    // warm: requests replayed before a segment in pass 1
     const int *candoff, *candlen;    // [T]
     const unsigned int *crank;       // packed ranks, per type ascending
     int *umatch;                     // [R] out: candidate index or -1
     const int *seg_cnt;              // [nseg] requests of the segment that may take an untargeted unit
-    int *E;                          // [2][nseg][T] end state per segment, double-buffered by pass
+    int *E;                          // [passes + 1][nseg][T] end state of segment s computed in pass k
+    int *comp;                       // [passes + 1][nseg] segment s was computed in pass k
     int *Sprev;                      // [nseg][T] start of each segment's last computation
-    int *changed;                    // [CHAIN_MAX_PASSES + 2] segments recomputed per pass
+    int *changed;                    // [CHAIN_MAX_PASSES + 2] segments computed per pass
     DevCounters *ctr;
 };
 
-// One segment, all per-type state uniform (T <= TB <= 8).  win holds, per type,
-// the SEG candidates following the segment's start (~0u past the list end);
-// a segment consumes at most SEG of any type.  Lane t of my_start is type t's
-// start; returns the end state in the same layout.
+// Level guess for the state after J untargeted choices: pos_t = number of
+// type-t candidates whose global rank is below J (every head at one level).
+// 64-ary search, all TB types at once: three dependent probes per lane.
 template <int TB>
-__device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int my_start, unsigned int *win,
-                                               int &rounds) {
+__device__ __forceinline__ int level_guess(const ChainArgs &a, int J) {
+    const int lane = threadIdx.x;
+    const unsigned int key = (unsigned int)J << 6;
+    int my = 0;
+    for (int g = 0; g < a.T; g += TB) {
+        int lo[TB], hi[TB], off[TB];
+#pragma unroll
+        for (int q = 0; q < TB; q++) {
+            const int t = g + q;
+            off[q] = t < a.T ? a.candoff[t] : 0;
+            lo[q] = 0;
+            hi[q] = (t < a.T && J > 0) ? a.candlen[t] : 0;
+        }
+        while (true) {
+            bool open = false;
+#pragma unroll
+            for (int q = 0; q < TB; q++) open |= hi[q] > lo[q];
+            if (!open) break;
+            unsigned int v[TB];
+            int step[TB];
+#pragma unroll
+            for (int q = 0; q < TB; q++) {
+                step[q] = (hi[q] - lo[q] + 63) >> 6;
+                const int idx = lo[q] + lane * step[q];
+                v[q] = (hi[q] > lo[q] && idx < hi[q]) ? a.crank[off[q] + idx] : ~0u;
+            }
+#pragma unroll
+            for (int q = 0; q < TB; q++) {
+                if (hi[q] <= lo[q]) continue;
+                const int c = __popcll(__ballot(v[q] < key));  // probes below key (a prefix: sorted)
+                const int nlo = c == 0 ? lo[q] : lo[q] + (c - 1) * step[q] + 1;
+                const int nhi = min(hi[q], lo[q] + c * step[q]);
+                lo[q] = nlo;
+                hi[q] = step[q] == 1 ? nlo : nhi;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < TB; q++)
+            if (lane == g + q) my = lo[q];
+    }
+    return my;
+}
+
+// Requests [jb, j1) of segment s (j1 = its end) from the state my_start (lane
+// t = type t) at jb; results are written from j0 = s * SEG on, and my_rec
+// receives the state at j0 (jb < j0 only for pass 1's warm-up).  All
+// per-type state is uniform (T <= TB <= 8).  win holds, per type, the WL
+// candidates following the start (~0u past the list end); a replay of WL
+// requests consumes at most WL of any type.
+template <int TB>
+__device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb, int my_start, unsigned int *win,
+                                               int WL, int &my_rec, int &rounds) {
     const int lane = threadIdx.x, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
     int st[TB], off[TB], c0[TB];
-    unsigned long long mb[SEG_BLOCKS];
-    int tb[SEG_BLOCKS];
-#pragma unroll
-    for (int b = 0; b < SEG_BLOCKS; b++) {
-        const int j = j0 + b * 64 + lane;
-        mb[b] = j < j1 ? a.mask[j] : 0ull;
-        tb[b] = j < j1 ? a.tmatch[j] : 0;
-    }
 #pragma unroll
     for (int q = 0; q < TB; q++) {
         st[q] = __builtin_amdgcn_readlane(my_start, q);
         off[q] = q < a.T ? a.candoff[q] : 0;
         const int len = q < a.T ? a.candlen[q] : 0;
         c0[q] = 0;
-#pragma unroll
-        for (int i = lane; i < SEG; i += 64) {
+        for (int i = lane; i < WL; i += 64) {
             const int p = st[q] + i;
-            win[q * SEG + i] = p < len ? a.crank[off[q] + p] : ~0u;
+            win[q * WL + i] = p < len ? a.crank[off[q] + p] : ~0u;
         }
     }
+    unsigned long long m_nx = jb + lane < j1 ? a.mask[jb + lane] : 0ull;
+    int t_nx = jb + lane < j1 ? a.tmatch[jb + lane] : 0;
     __syncthreads();
+    my_rec = my_start;
+    for (int b0 = jb; b0 < j1; b0 += 64) {
+        if (b0 == j0) {
 #pragma unroll
-    for (int b = 0; b < SEG_BLOCKS; b++) {
-        if (j0 + b * 64 >= j1) break;
-        const int j = j0 + b * 64 + lane;
-        const unsigned long long m = tb[b] < 0 ? mb[b] : 0ull;
+            for (int q = 0; q < TB; q++)
+                if (lane == q) my_rec = st[q] + c0[q];
+        }
+        const int j = b0 + lane;
+        const unsigned long long m = t_nx < 0 ? m_nx : 0ull;
+        if (b0 + 64 < j1) {  // next block's inputs, in flight during this block
+            m_nx = j + 64 < j1 ? a.mask[j + 64] : 0ull;
+            t_nx = j + 64 < j1 ? a.tmatch[j + 64] : 0;
+        }
         bool have[TB];
 #pragma unroll
         for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
@@ -644,7 +699,7 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int my
         do {
             unsigned int v[TB];
 #pragma unroll
-            for (int q = 0; q < TB; q++) v[q] = win[q * SEG + c0[q] + (int)mbcnt64(__ballot(ch == q))];
+            for (int q = 0; q < TB; q++) v[q] = win[q * WL + c0[q] + (int)mbcnt64(__ballot(ch == q))];
             unsigned int best = ~0u;
 #pragma unroll
             for (int q = 0; q < TB; q++) best = min(best, have[q] ? v[q] : ~0u);
@@ -660,7 +715,7 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int my
             if (ch == q) res = off[q] + st[q] + c0[q] + (int)mbcnt64(B);
             c0[q] += __popcll(B);
         }
-        if (j < j1) a.umatch[j] = res;
+        if (b0 >= j0 && j < j1) a.umatch[j] = res;
     }
     int my_end = my_start;
 #pragma unroll
@@ -669,8 +724,8 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int my
     return my_end;
 }
 
-// Any T <= 64: lane t keeps type t's state, uniform copies come from readlane;
-// rounds touch only the types present in the block, TB LDS reads in flight.
+// Any T <= 64, no warm-up: lane t keeps type t's state, uniform copies come
+// from readlane; rounds touch only the types present in the block.
 template <int TB>
 __device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_start, unsigned int *win,
                                               int &rounds) {
@@ -728,10 +783,22 @@ __device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_
     return my_start + my_c0;
 }
 
+// TB <= 8: uniform per-type state (warm-up allowed); TB == 64: wide variant.
 template <int TB>
-__device__ __forceinline__ int seg_solve(const ChainArgs &a, int s, int my_start, unsigned int *win, int &rounds) {
-    if constexpr (TB <= 8) return seg_solve_small<TB>(a, s, my_start, win, rounds);
-    else return seg_solve_wide<8>(a, s, my_start, win, rounds);
+__device__ __forceinline__ int seg_solve(const ChainArgs &a, int s, int jb, int my_start, unsigned int *win,
+                                         int &my_rec, int &rounds) {
+    if constexpr (TB <= 8) {
+        return seg_solve_small<TB>(a, s, jb, my_start, win, s * SEG - jb + SEG, my_rec, rounds);
+    } else {
+        my_rec = my_start;
+        return seg_solve_wide<8>(a, s, my_start, win, rounds);
+    }
+}
+
+// End state of segment s as last computed in a pass <= k.
+__device__ __forceinline__ int latest_end(const ChainArgs &a, int s, int k) {
+    while (k > 1 && !a.comp[(long long)k * a.nseg + s]) k--;
+    return threadIdx.x < a.T ? a.E[((long long)k * a.nseg + s) * a.T + threadIdx.x] : 0;
 }
 
 // Pass k of the segment iteration (k = 1 .. passes), one wavefront per segment.
@@ -740,76 +807,77 @@ __global__ __launch_bounds__(64) void k_chain_pass(ChainArgs a, int k) {
     extern __shared__ unsigned int win[];
     const int s = blockIdx.x, lane = threadIdx.x, T = a.T;
     if (k > 1 && a.changed[k - 1] == 0) return;  // pass k-1 found the fixed point
-    int *Ecur = a.E + (long long)(k & 1) * a.nseg * T;
-    const int *Eprev = a.E + (long long)((k - 1) & 1) * a.nseg * T;
-    int my_start = 0;
+    int my_start = 0, jb = s * SEG;
     if (k == 1) {
-        // level guess: J = requests before this segment that take an untargeted unit
-        int J = 0;
-        for (int q = lane; q < s; q += 64) J += a.seg_cnt[q];
+        jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
+        int J = 0;                      // requests before jb that take an untargeted unit
+        for (int q = lane; q < jb / SEG; q += 64) J += a.seg_cnt[q];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
-        if (lane < T && J > 0) {
-            const unsigned int *L = a.crank + a.candoff[lane];
-            int lo = 0, hi = a.candlen[lane];
-            const unsigned int key = (unsigned int)J << 6;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (L[mid] < key) lo = mid + 1;
-                else hi = mid;
-            }
-            my_start = lo;
-        }
+        my_start = level_guess<(TB <= 8 ? TB : 8)>(a, J);
     } else {
-        my_start = (s > 0 && lane < T) ? Eprev[(s - 1) * T + lane] : 0;
-        const bool same = !__ballot(lane < T && my_start != a.Sprev[s * T + lane]);
-        if (same) {  // unchanged start: last computation stands, carry its end state
-            if (lane < T) Ecur[s * T + lane] = Eprev[s * T + lane];
-            return;
-        }
+        if (s > 0) my_start = latest_end(a, s - 1, k - 1);
+        if (!__ballot(lane < T && my_start != a.Sprev[s * T + lane])) return;  // start unchanged
     }
-    int rounds = 0;
-    const int my_end = seg_solve<TB>(a, s, my_start, win, rounds);
+    int rounds = 0, my_rec;
+    const int my_end = seg_solve<TB>(a, s, jb, my_start, win, my_rec, rounds);
     if (lane < T) {
-        Ecur[s * T + lane] = my_end;
-        a.Sprev[s * T + lane] = my_start;
+        a.E[((long long)k * a.nseg + s) * T + lane] = my_end;
+        a.Sprev[s * T + lane] = my_rec;
     }
     if (lane == 0) {
+        a.comp[(long long)k * a.nseg + s] = 1;
         atomicAdd(&a.changed[k], 1);
         atomicAdd(&a.ctr->chain_rounds, rounds);
     }
 }
 
-// After `passes` passes: nothing to do at a fixed point; otherwise walk the
-// segments in order from the exact start (segment 0 starts at 0) and recompute
-// each one whose start differs from its last computation's.
+// After the passes: nothing to do at a fixed point.  Otherwise walk the
+// segments in order from the exact start (segment 0 starts at 0): a segment
+// whose start equals its last computation's stands, and so does every later
+// one up to the next whose recorded start differs from its predecessor's
+// recorded end (found 64 segments at a time); the others are recomputed.
 template <int TB>
-__global__ __launch_bounds__(64) void k_chain_fix(ChainArgs a, int passes) {
+__global__ __launch_bounds__(64) void k_chain_fix(ChainArgs a) {
     extern __shared__ unsigned int win[];
-    const int lane = threadIdx.x, T = a.T;
+    const int lane = threadIdx.x, T = a.T, P = a.passes;
     int used = 0, recomputed = 0;
-    for (int k = 1; k <= passes; k++) {
+    for (int k = 1; k <= P; k++) {
         used += a.changed[k] > 0;
         recomputed += a.changed[k];
     }
-    const bool fixed = a.changed[passes] == 0;
     if (lane == 0) {
         a.ctr->chain_passes = used;
         a.ctr->chain_recomputed = recomputed;
         a.ctr->chain_fallback = 0;
     }
-    if (fixed) return;
-    const int *E = a.E + (long long)(passes & 1) * a.nseg * T;
-    int st = 0, rounds = 0, redo = 0;
-    for (int s = 0; s < a.nseg; s++) {
-        const bool same = !__ballot(lane < T && st != a.Sprev[s * T + lane]);
-        if (same) {
-            st = lane < T ? E[s * T + lane] : 0;
-        } else {
-            st = seg_solve<TB>(a, s, st, win, rounds);
-            __syncthreads();  // win is refilled by the next recomputed segment
-            redo++;
+    if (a.changed[P] == 0) return;
+    int st = 0, rounds = 0, redo = 0, s = 0;
+    while (s < a.nseg) {
+        if (!__ballot(lane < T && st != a.Sprev[s * T + lane])) {
+            // s stands; find the next segment whose recorded start is not its predecessor's recorded end
+            int nxt = a.nseg;
+            for (int c0 = s + 1; c0 < a.nseg && nxt == a.nseg; c0 += 64) {
+                const int q = c0 + lane;
+                bool bad = false;
+                if (q < a.nseg) {
+                    int k = P;
+                    while (k > 1 && !a.comp[(long long)k * a.nseg + q - 1]) k--;
+                    const int *e = a.E + ((long long)k * a.nseg + q - 1) * T;
+                    for (int t = 0; t < T; t++) bad |= e[t] != a.Sprev[q * T + t];
+                }
+                const unsigned long long bb = __ballot(bad);
+                if (bb) nxt = c0 + __ffsll((long long)bb) - 1;
+            }
+            if (nxt >= a.nseg) break;
+            s = nxt;
+            st = latest_end(a, s - 1, P);
         }
+        int my_rec;
+        st = seg_solve<TB>(a, s, s * SEG, st, win, my_rec, rounds);
+        __syncthreads();  // win is refilled by the next recomputed segment
+        redo++;
+        s++;
     }
     if (lane == 0) {
         a.ctr->chain_fallback = redo;
@@ -862,12 +930,18 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
 __global__ __launch_bounds__(1024) void k_park(DonorCtx c, int donors, const int *__restrict__ reqs, int R,
                                                const int *__restrict__ tmatch, const int *__restrict__ umatch,
                                                int *rq_rank, int *rq_types, int *rq_live, int *rq_req,
-                                               DevCounters *ctr, int *resp) {
+                                               DevCounters *ctr, int *resp, int *dem, int T,
+                                               DevCounters *snap) {
     __shared__ int wsum[16];
     __shared__ int s_n0, s_total;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nth = blockDim.x;
+    if (tid < T) dem[tid] = 0;  // k_req_prep of the next batch accumulates into it
     if (ctr->park_pending == 0) {  // nothing parked (the common case): skip the scan
-        if (tid == 0) ctr->n_parked_last = 0;
+        if (tid == 0) {
+            ctr->n_parked_last = 0;
+            *snap = *ctr;
+            __threadfence_system();
+        }
         return;
     }
     const int per = (R + nth - 1) / nth, lo = min(R, tid * per), hi = min(R, lo + per);
@@ -919,6 +993,8 @@ __global__ __launch_bounds__(1024) void k_park(DonorCtx c, int donors, const int
         ctr->rq_live += np;
         if (ctr->rq_live > ctr->rq_hwm) ctr->rq_hwm = ctr->rq_live;
         ctr->n_parked_last = np;
+        *snap = *ctr;
+        __threadfence_system();
     }
 }
 
@@ -930,7 +1006,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
     void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
-                  h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg};
+                  h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg, h->d_chcomp};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
@@ -940,7 +1016,8 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
     const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
     AQ_HIP(hipMalloc((void **)&h->d_seg_cnt, sizeof(int) * nseg));
-    AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * 2 * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chcomp, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));
     AQ_HIP(hipMalloc((void **)&h->d_chS, sizeof(int) * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chchg, sizeof(int) * (CHAIN_MAX_PASSES + 2)));
     h->cap_req = nc;
@@ -992,10 +1069,10 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipStream_t s = h->stream;
     hipEvent_t ev;
 
-    AQ_HIP(hipMemsetAsync(h->d_dem, 0, sizeof(int) * std::max(T, 1), s));
     stage_begin(h, "prep", &ev);
     k_req_prep<<<(R + SEG - 1) / SEG, SEG, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt,
-                                                 h->d_chchg, h->d_ctr);
+                                                 h->d_chchg, h->d_ctr, h->d_tmatch, h->d_chcomp,
+                                                 (R + SEG - 1) / SEG);
     stage_end(h, "prep", ev);
 
     if (np > 0 && T > 0) {
@@ -1029,7 +1106,6 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     h->last_scan_units = h->live_units - h->live_targeted;
 
-    AQ_HIP(hipMemsetAsync(h->d_tmatch, 0xff, sizeof(int) * R, s));
     const int nb = (int)h->bucket_ranks.size();
     if (h->live_targeted > 0 && nb > 0) {
         stage_begin(h, "targeted", &ev);
@@ -1044,17 +1120,18 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     stage_begin(h, "chain", &ev);
     {
-        const int nseg = (R + SEG - 1) / SEG, P = h->chain_passes;
-        ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, h->d_candoff, h->d_candlen, h->d_crank, h->d_umatch,
-                     h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg, h->d_ctr};
-        auto run = [&](auto kpass, auto kfix, int tw) {
-            const size_t lds = sizeof(unsigned int) * SEG * tw;
+        const int nseg = (R + SEG - 1) / SEG;
+        const int P = h->chain_passes > 0 ? h->chain_passes : (T <= 8 ? 3 : 8);
+        const int warm = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
+        ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, P, warm, h->d_candoff, h->d_candlen, h->d_crank,
+                     h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chcomp, h->d_chS, h->d_chchg, h->d_ctr};
+        auto run = [&](auto kpass, auto kfix, size_t lds) {
             for (int k = 1; k <= P; k++) kpass<<<nseg, 64, lds, s>>>(ca, k);
-            kfix<<<1, 64, lds, s>>>(ca, P);
+            kfix<<<1, 64, lds, s>>>(ca);
         };
-        if (T <= 4) run(k_chain_pass<4>, k_chain_fix<4>, 4);
-        else if (T <= 8) run(k_chain_pass<8>, k_chain_fix<8>, 8);
-        else run(k_chain_pass<64>, k_chain_fix<64>, T);
+        if (T <= 4) run(k_chain_pass<4>, k_chain_fix<4>, sizeof(unsigned int) * 4 * (SEG + std::max(warm, 0)));
+        else if (T <= 8) run(k_chain_pass<8>, k_chain_fix<8>, sizeof(unsigned int) * 8 * (SEG + std::max(warm, 0)));
+        else run(k_chain_pass<64>, k_chain_fix<64>, sizeof(unsigned int) * T * SEG);
     }
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);
@@ -1064,9 +1141,15 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     stage_end(h, "finalize", ev);
     stage_begin(h, "park", &ev);
     const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
+    DevCounters *snap = nullptr;
+    AQ_HIP(hipHostGetDevicePointer((void **)&snap, h->h_snap + h->snap_next, 0));
     k_park<<<1, 1024, 0, s>>>(donor_ctx(h), donors, d_reqs, R, h->d_tmatch, h->d_umatch, h->d_rq_rank,
-                              h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_ctr, d_resp);
+                              h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_ctr, d_resp, h->d_dem, T, snap);
     stage_end(h, "park", ev);
+    h->launched_reserves += R;
+    h->snap_at[h->snap_next] = h->launched_reserves;
+    AQ_HIP(hipEventRecord(h->snap_ev[h->snap_next], s));
+    h->snap_next = (h->snap_next + 1) % adlbq_server::NSNAP;
     AQ_HIP(hipGetLastError());
     h->ctr_stale = true;
     h->rq_n_upper += R;

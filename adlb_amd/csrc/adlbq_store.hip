@@ -54,9 +54,25 @@ static int grow_pages(adlbq_server *h, int need) {
     return ADLBQ_OK;
 }
 
+void tighten_rq_bound(adlbq_server *h) {
+    for (int k = 1; k <= adlbq_server::NSNAP; k++) {
+        const int i = (h->snap_next - k + adlbq_server::NSNAP) % adlbq_server::NSNAP;
+        if (!h->snap_ev[i] || !h->snap_at[i]) continue;
+        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
+        const long long bound = (long long)h->h_snap[i].rq_n + (h->launched_reserves - h->snap_at[i]);
+        if (bound < h->rq_n_upper) h->rq_n_upper = bound;
+        return;
+    }
+}
+
 int ensure_rq_capacity(adlbq_server *h, int extra) {
-    long long need = (long long)(h->ctr_stale ? h->rq_n_upper : h->ctr.rq_n) + extra;
+    long long need = (h->ctr_stale ? h->rq_n_upper : (long long)h->ctr.rq_n) + extra;
     if (need <= h->rq_cap) return ADLBQ_OK;
+    if (h->ctr_stale) {
+        tighten_rq_bound(h);
+        need = h->rq_n_upper + extra;
+        if (need <= h->rq_cap) return ADLBQ_OK;
+    }
     if (h->ctr_stale) {
         int rc = refresh_counters(h);
         if (rc) return rc;
@@ -169,18 +185,31 @@ DonorCtx donor_ctx(adlbq_server *h) {
     return c;
 }
 
+static hipEvent_t pooled_event(adlbq_server *h) {
+    hipEvent_t e = nullptr;
+    if (!h->event_pool.empty()) {
+        e = h->event_pool.back();
+        h->event_pool.pop_back();
+    } else {
+        hipEventCreate(&e);
+    }
+    return e;
+}
+
+static bool stage_on(adlbq_server *h, const char *name) {
+    return h->profiling && (h->profile_only.empty() || h->profile_only == name);
+}
+
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev) {
     *ev = nullptr;
-    if (!h->profiling) return;
-    hipEventCreate(ev);
+    if (!stage_on(h, name)) return;
+    *ev = pooled_event(h);
     hipEventRecord(*ev, h->stream);
-    (void)name;
 }
 
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev) {
-    if (!h->profiling || !ev) return;
-    hipEvent_t e2;
-    hipEventCreate(&e2);
+    if (!ev) return;
+    hipEvent_t e2 = pooled_event(h);
     hipEventRecord(e2, h->stream);
     h->timers[name].pending.push_back({ev, e2});
 }
@@ -482,7 +511,10 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMemset(h->d_rfr_to_rank, 0xff, sizeof(int) * std::max(num_app_ranks, 1)));
     AQ_HIP(hipMalloc((void **)&h->d_ctr, sizeof(DevCounters)));
     AQ_HIP(hipMemset(h->d_ctr, 0, sizeof(DevCounters)));
+    AQ_HIP(hipHostMalloc((void **)&h->h_snap, sizeof(DevCounters) * adlbq_server::NSNAP, hipHostMallocMapped));
+    for (int i = 0; i < adlbq_server::NSNAP; i++) AQ_HIP(hipEventCreateWithFlags(&h->snap_ev[i], hipEventDisableTiming));
     AQ_HIP(hipMalloc((void **)&h->d_dem, sizeof(int) * T1));
+    AQ_HIP(hipMemset(h->d_dem, 0, sizeof(int) * T1));  // k_park re-zeroes it after every batch
     AQ_HIP(hipMalloc((void **)&h->d_theta, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_need, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_candoff, sizeof(int) * (T1 + 1)));
@@ -510,15 +542,19 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_gh, h->d_pp, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
-                    h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg};
+                    h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg, h->d_chcomp};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
+    if (h->h_snap) hipHostFree(h->h_snap);
+    for (int i = 0; i < adlbq_server::NSNAP; i++)
+        if (h->snap_ev[i]) hipEventDestroy(h->snap_ev[i]);
     for (auto &kv : h->timers)
         for (auto &pe : kv.second.pending) {
             hipEventDestroy(pe.first);
             hipEventDestroy(pe.second);
         }
+    for (hipEvent_t e : h->event_pool) hipEventDestroy(e);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return ADLBQ_OK;
@@ -849,6 +885,14 @@ int adlbq_sync(adlbq_server *h) {
 int adlbq_profile_enable(adlbq_server *h, int on) {
     if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_profile_enable");
     h->profiling = on != 0;
+    h->profile_only.clear();
+    return ADLBQ_OK;
+}
+
+int adlbq_profile_only(adlbq_server *h, const char *stage) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_profile_only");
+    h->profiling = true;
+    h->profile_only = stage ? stage : "";
     return ADLBQ_OK;
 }
 
@@ -862,8 +906,8 @@ int adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, lon
         hipEventElapsedTime(&ms, pe.first, pe.second);
         t.total_ms += ms;
         t.launches++;
-        hipEventDestroy(pe.first);
-        hipEventDestroy(pe.second);
+        h->event_pool.push_back(pe.first);
+        h->event_pool.push_back(pe.second);
     }
     t.pending.clear();
     if (total_ms) *total_ms = t.total_ms;
@@ -877,8 +921,13 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (!h || !name) return fail(ADLBQ_ERR_ARG, "adlbq_set_param");
     std::string n(name);
     if (n == "chain_passes") {
-        if (value < 1 || value > 30) return fail(ADLBQ_ERR_ARG, "chain_passes must be in [1, 30]");
+        if (value < 0 || value > 30) return fail(ADLBQ_ERR_ARG, "chain_passes must be in [0, 30] (0 = auto)");
         h->chain_passes = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "chain_warm") {
+        if (value < -1 || value > 4096 || (value > 0 && value % 256)) return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 or a multiple of 256 in [0, 4096]");
+        h->chain_warm = (int)value;
         return ADLBQ_OK;
     }
     return fail(ADLBQ_ERR_ARG, "adlbq_set_param: unknown parameter");

@@ -170,6 +170,9 @@ class Server:
     def profile(self, on=True):
         _lib.check(self.lib.adlbq_profile_enable(self.h, 1 if on else 0), "adlbq_profile_enable")
 
+    def profile_only(self, stage: str | None):
+        _lib.check(self.lib.adlbq_profile_only(self.h, stage.encode() if stage else None), "adlbq_profile_only")
+
     def profile_read(self, stage: str):
         ms, n = ctypes.c_double(), ctypes.c_longlong()
         _lib.check(self.lib.adlbq_profile_read(self.h, stage.encode(), ctypes.byref(ms), ctypes.byref(n)),

@@ -196,19 +196,30 @@ def main():
 
     def step(b):
         srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
-        r = d_resp[b]
-        # SS_UNRESERVE every matched unit (wqseqno <= 0 rows are ignored by the kernel)
-        torch.where(r[:, 0] == 1, r[:, 5], torch.full_like(r[:, 5], -1), out=d_trip[:, 1])
+        # SS_UNRESERVE every matched unit: resp[5] is the wqseqno of a match and 0
+        # otherwise, and rows with wqseqno <= 0 are ignored by the kernel
+        d_trip[:, 1].copy_(d_resp[b][:, 5])
         srv.unreserve_batch_device(R, d_trip.data_ptr())
 
     for b in range(args.warmup):
         step(b)
     torch.cuda.synchronize()
+    stages, dominant, dom_timed = {}, None, None
     if not args.no_profile:
+        # per-stage breakdown, untimed: HIP events around every stage's launches
         srv.profile(True)
-        for s in STAGES:
-            srv.profile_read(s)  # drain warmup
         base = {s: srv.profile_read(s) for s in STAGES}
+        for i in range(min(args.steps, 10)):
+            step(i % max(args.warmup, 1))
+        for s in STAGES:
+            ms, n = srv.profile_read(s)
+            ms0, n0 = base[s]
+            if n - n0:
+                stages[s] = round((ms - ms0) / (n - n0), 4)
+        dominant = max(stages, key=stages.get) if stages else None
+        # the timed region carries events around the dominant stage only
+        srv.profile_only(dominant)
+        base_dom = srv.profile_read(dominant)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -222,14 +233,12 @@ def main():
     matched = int((d_resp[args.warmup:, :, 0] == 1).sum().item())
     if world > 1:
         el, matched = shards.reduce_step_timing(el, matched)
+    if dominant:
+        ms, n = srv.profile_read(dominant)
+        if n - base_dom[1]:
+            dom_timed = round((ms - base_dom[0]) / (n - base_dom[1]), 4)
+            stages[dominant] = dom_timed
 
-    stages = {}
-    if not args.no_profile:
-        for s in STAGES:
-            ms, n = srv.profile_read(s)
-            ms0, n0 = base[s]
-            if n - n0:
-                stages[s] = round((ms - ms0) / (n - n0), 4)
     live = srv.last_scan_units()
     # algorithmic bytes per launch: SURVEY §8(d)'s 16 B per live
     # unit for the open-bucket scan (hist + select together), 20 B per Reserve
@@ -241,7 +250,6 @@ def main():
     kernels = {}
     for st, ms in stages.items():
         kernels[st] = {"kernel": KERNEL_OF[st], "ms": ms, "traffic": traffic_of(pmc, st)}
-    dominant = max(stages, key=stages.get) if stages else None
 
     def roof(bytes_, ms, traffic, kernel):
         a = bytes_ / (ms * 1e-3) / 1e9 if ms else None

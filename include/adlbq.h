@@ -134,8 +134,10 @@ int  adlbq_sync(adlbq_server *h);
  * a reserve batch) when enabled.  Stage names, one kernel each: "prep"
  * (k_req_prep), "hist" (k_hist_open), "thresholds", "prefix" (k_page_prefix),
  * "select" (k_select_open), "sort" (k_sort_types), "targeted", "rank",
- * "chain" (k_chain_small / k_chain), "finalize", "park". */
+ * "chain" (k_chain_pass x passes + k_chain_fix), "finalize", "park". */
 int  adlbq_profile_enable(adlbq_server *h, int on);
+/* Profile one stage only (NULL: every stage); enables profiling. */
+int  adlbq_profile_only(adlbq_server *h, const char *stage);
 int  adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, long long *launches);
 /* Bytes the last reserve batch's open-bucket scan touched algorithmically:
  * 16 B x live units. */
@@ -148,8 +150,10 @@ long long adlbq_last_scan_units(adlbq_server *h);
  * -1 if unknown. */
 long long adlbq_stat(adlbq_server *h, const char *name);
 /* Tuning: "chain_passes" = parallel segment passes of the ordered-choice
- * kernel before the in-order fix-up (1..30, default 8).  Results never depend
- * on it; tests lower it to force the fix-up path. */
+ * kernel before the in-order fix-up (1..30; 0 = auto: 3 for up to 8 types,
+ * else 8); "chain_warm" = requests replayed ahead of each segment in the first
+ * pass (-1 = auto: 512 for up to 8 types; else a multiple of 256 up to 4096).
+ * Results never depend on either; tests lower them to force the fix-up. */
 int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);
 const char *adlbq_version(void);

@@ -72,7 +72,7 @@ def test_fresh_vs_oracle(gpu_available, name):
 
 
 @pytest.mark.parametrize("name", ["c2_n200k_r16k", "c2_t64_wide", "c4_n200k", "c4_t8_tied"])
-@pytest.mark.parametrize("passes", [1, 2])
+@pytest.mark.parametrize("passes", [1, 2, 3])
 def test_chain_fixup_path(gpu_available, name, passes):
     """Few segment passes leave segments off their fixed point, so the in-order
     fix-up kernel (k_chain_fix) recomputes them: still identical to the oracle."""
@@ -80,7 +80,8 @@ def test_chain_fixup_path(gpu_available, name, passes):
     tr = synth.workload_trace(w)
     cfg = (w.num_app_ranks, 1, 0)
     st = {}
-    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units, params={"chain_passes": passes}, stats=st)
+    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units, params={"chain_passes": passes, "chain_warm": 0},
+                  stats=st)
     assert_same(got, run_oracle(w.user_types, cfg, tr))
     if name == "c2_n200k_r16k" and passes == 1:
         assert st["chain_fallback"] > 0, st
