@@ -27,7 +27,7 @@ constexpr int PAGE_SHIFT = 12;
 constexpr int PAGE = 1 << PAGE_SHIFT;       // 4096 slots per page
 constexpr int NB = 64;                      // histogram bins per type (distance from anchor)
 constexpr int NBX = 32;                     // bins [0, NBX) are exact (one priority value each)
-constexpr int CHUNK = 16;                   // pages per prefix chunk in the open-bucket scan
+constexpr int CHUNK = 8;                    // pages per prefix chunk in the open-bucket scan
 constexpr int LOWEST = ADLBQ_LOWEST_PRIO;
 constexpr uint32_t M_TYPE = 0xffu;
 constexpr uint32_t M_LIVE = 1u << 8;
@@ -36,17 +36,16 @@ constexpr int NREQ = ADLBQ_REQ_TYPES;
 
 // device-side scalar counters shared by kernels and read back lazily by the host
 struct DevCounters {
+    unsigned long long fin_ticket;  // k_finalize arrivals: parked << 32 | workgroups (reset by the last)
     int rq_n;          // rq slots used (== next_rqseqno - 1)
     int rq_live;       // parked entries alive
     int rq_hwm;        // rq->max_count
     int rq_head;       // lowest rq slot that may be alive
     int n_parked_last; // parked by the last reserve batch
     int chain_rounds;  // Jacobi rounds of the last chain, all wavefronts (diagnostic)
-    int park_pending;  // parked requests counted by k_finalize for k_park
     int chain_passes;      // segment passes of the last chain that recomputed something
     int chain_recomputed;  // segment solves over those passes
     int chain_fallback;    // segments k_chain_fix recomputed (0 at a fixed point)
-    int pad[1];
 };
 
 struct Bucket {
@@ -110,7 +109,7 @@ struct adlbq_server {
     adlbq::DevCounters ctr{};      // host copy
     bool ctr_stale = false;
     long long rq_n_upper = 0;      // upper bound on rq_n while ctr is stale
-    // rq_n snapshots written by k_park into mapped host memory at the end of
+    // rq_n snapshots written by k_finalize into mapped host memory at the end of
     // each reserve batch, so the rq capacity bound tightens without a sync
     static constexpr int NSNAP = 4;
     adlbq::DevCounters *h_snap = nullptr;   // [NSNAP] pinned, device-visible
@@ -137,9 +136,10 @@ struct adlbq_server {
     int *d_need = nullptr;             // [T]
     int *d_candoff = nullptr, *d_candlen = nullptr, *d_needsort = nullptr;  // [T]
     int *d_binoff = nullptr;           // [T*NB]
+    unsigned int *d_coltot = nullptr;  // [T*NB] column totals (k_thresholds)
+    int *d_type_cnt = nullptr;         // [T] k_thresholds arrival counters (zero between batches)
     unsigned short *d_gh = nullptr; long long cap_gh = 0;   // [open pages][T*NB]
-    unsigned int *d_pp = nullptr;                           // [open pages][T*NB] column prefix
-    unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] -> exclusive prefix in place
+    unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] sums -> exclusive prefix in place
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
     int *d_cslot = nullptr, *d_cslot2 = nullptr;
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate

@@ -4,20 +4,23 @@
 // calls of wq_find_pre_targeted_hi_prio / wq_find_hi_prio (src/xq.c:190-247)
 // followed by the pin.  Pipeline (all on the handle's stream):
 //
-//   k_req_prep     request type vectors -> 64-bit type masks, per-type demand
+//   k_req_prep     request type vectors -> 64-bit type masks, per-type demand,
+//                  per-segment request counts; resets per-batch state
 //   k_hist_open    pass 1 over the open (untargeted) bucket: per page and per
 //                  type, histogram of distance-from-anchor bins (8 B/unit read)
 //   k_thresholds   per type: the bin where the demand is reached and how many
-//                  units of it are needed (exact bins: by wqseqno order)
+//                  units of it are needed (exact bins: by wqseqno order); the
+//                  chunk prefix of every column
 //   k_select_open  pass 2: order-preserving compaction of the top units of each
 //                  type into per-type candidate lists (prio desc, wqseqno asc)
 //   k_sort_types   only for types whose threshold fell in a multi-priority bin
 //   k_targeted     per target-rank bucket: that rank's Reserves in order against
 //                  its own targeted units (pre-targeted scan, xq.c:219-247)
-//   k_chain        one wavefront replays the untargeted choices in arrival order
-//                  as a T-way merge of the per-type candidate heads
-//   k_finalize     pins, TA_RESERVE_RESP records
-//   k_park         parks unmatched hanging Reserves on rq (FIFO), RFR donor choice
+//   k_rank         packed global rank of every candidate
+//   k_chain_pass   the untargeted choices in arrival order, as segment-parallel
+//   k_chain_fix    passes with a fixed-point check (see the chain section)
+//   k_finalize     pins, TA_RESERVE_RESP records; its last workgroup parks the
+//                  unmatched hanging Reserves on rq (FIFO) with their RFR donors
 #include <algorithm>
 #include <climits>
 
@@ -25,6 +28,7 @@
 #include "adlbq_impl.h"
 
 using namespace adlbq;
+
 
 constexpr int SEG = 256;               // chain segment: requests per wavefront (== k_req_prep's block)
 constexpr int SEG_BLOCKS = SEG / 64;
@@ -145,90 +149,75 @@ __global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages
 }
 
 // ---------------------------------------------------------------- thresholds
-__global__ __launch_bounds__(1024) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
-                                                     int nchunks, int *theta, int *need, int *candoff,
-                                                     int *candlen, int *needsort, int *binoff) {
-    extern __shared__ unsigned int tot[];
-    const int C = T * NB;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        unsigned int run = 0;
-        for (int k0 = 0; k0 < nchunks; k0 += 16) {
-            unsigned int v[16];
+// One workgroup per (type, bin) column: block scan of the column's chunk sums
+// (exclusive prefix in place, read by k_select_open) and its total.  The
+// column that arrives last for its type (agent-scope counter; totals published
+// write-through and read back the same way) finds the bin where the type's
+// demand is reached and how many units of it are needed.  Candidate list
+// offsets (the prefix of candlen over types) follow in k_select_open.
+__global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
+                                                     int nchunks, int *theta, int *need, int *candlen,
+                                                     int *needsort, int *binoff, unsigned int *coltot,
+                                                     int *type_cnt) {
+    __shared__ unsigned int wsum[4];
+    __shared__ bool s_last;
+    const int c = blockIdx.x, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned int carry = 0;
+    for (int k0 = 0; k0 < nchunks; k0 += 256) {
+        const int k = k0 + threadIdx.x;
+        const unsigned int v = k < nchunks ? csum[(long long)k * C + c] : 0u;
+        unsigned int x = v;  // block inclusive scan
 #pragma unroll
-            for (int q = 0; q < 16; q++) v[q] = k0 + q < nchunks ? csum[(long long)(k0 + q) * C + c] : 0u;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                if (k0 + q < nchunks) csum[(long long)(k0 + q) * C + c] = run;  // exclusive prefix, in place
-                run += v[q];
-            }
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
-        tot[c] = run;
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        unsigned int pre = carry;
+        for (int q = 0; q < w; q++) pre += wsum[q];
+        if (k < nchunks) csum[(long long)k * C + c] = pre + x - v;
+        carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
     }
-    __syncthreads();
-    if (threadIdx.x < T) {
-        const int t = threadIdx.x, d = dem[t];
-        int th = -1, nd = 0, len = 0;
-        if (d > 0) {
-            long long cum = 0;
-            for (int b = 0; b < NB; b++) {
-                long long x = tot[t * NB + b];
-                binoff[t * NB + b] = (int)cum;
-                if (cum + x >= d) {
-                    th = b;
-                    if (b < NBX) {          // one priority value: the first (d - cum) by wqseqno
-                        nd = (int)(d - cum);
-                        len = d;
-                    } else {                // several values: take the whole bin, sort later
-                        nd = INT_MAX;
-                        len = (int)(cum + x);
-                    }
-                    break;
-                }
-                cum += x;
-            }
-            if (th < 0) {                   // fewer available units than demand: take all
-                th = NB - 1;
-                nd = INT_MAX;
-                len = (int)cum;
-            }
-        }
-        theta[t] = th;
-        need[t] = nd;
-        candlen[t] = len;
-        needsort[t] = (th >= NBX && len > 1) ? 1 : 0;
-    }
-    __syncthreads();
     if (threadIdx.x == 0) {
-        int off = 0;
-        for (int t = 0; t < T; t++) {
-            candoff[t] = off;
-            off += candlen[t];
+        __hip_atomic_store(coltot + c, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = atomicAdd(&type_cnt[t], 1) == NB - 1;
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    type_cnt[t] = 0;  // for the next batch
+    const int d = dem[t];
+    int th = -1, nd = 0, len = 0;
+    if (d > 0) {
+        long long cum = 0;
+        for (int bb = 0; bb < NB; bb++) {
+            const long long x = __hip_atomic_load(coltot + t * NB + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            binoff[t * NB + bb] = (int)cum;
+            if (cum + x >= d) {
+                th = bb;
+                if (bb < NBX) {  // one priority value: the first (d - cum) by wqseqno
+                    nd = (int)(d - cum);
+                    len = d;
+                } else {         // several values: take the whole bin, sort later
+                    nd = INT_MAX;
+                    len = (int)(cum + x);
+                }
+                break;
+            }
+            cum += x;
         }
-        candoff[T] = off;
+        if (th < 0) {            // fewer available units than demand: take all
+            th = NB - 1;
+            nd = INT_MAX;
+            len = (int)cum;
+        }
     }
-}
-
-// ---------------------------------------------------------------- per-page column prefix
-// pp[p][c] = rank, in wqseqno order over the open bucket, of page p's first unit
-// in column c (= type, bin); only the columns a type takes (bin <= theta).
-__global__ __launch_bounds__(256) void k_page_prefix(int npages, int T, const int *__restrict__ theta,
-                                                     const unsigned short *__restrict__ gh,
-                                                     unsigned int *__restrict__ csum,
-                                                     unsigned int *__restrict__ pp) {
-    const int C = T * NB;
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int nchunks = (npages + CHUNK - 1) / CHUNK;
-    if (i >= (long long)nchunks * C) return;
-    const int k = (int)(i / C), c = (int)(i - (long long)k * C);
-    const int t = c / NB, b = c - t * NB;
-    unsigned int run = csum[(long long)k * C + c];
-    csum[(long long)k * C + c] = 0;  // last reader: leave the chunk sums zeroed for the next batch
-    if (b > theta[t]) return;
-    const int p1 = min(npages, (k + 1) * CHUNK);
-    for (int p = k * CHUNK; p < p1; p++) {
-        pp[(long long)p * C + c] = run;
-        run += gh[(long long)p * C + c];
-    }
+    theta[t] = th;
+    need[t] = nd;
+    candlen[t] = len;
+    needsort[t] = (th >= NBX && len > 1) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------- pass 2
@@ -239,14 +228,15 @@ __global__ __launch_bounds__(256) void k_page_prefix(int npages, int T, const in
 //      (equivalent to bin_of(anchor - prio) <= theta[t]);
 //   2. each wave appends its candidates, in slot order, to an LDS list
 //      (key = column << 12 | slot-in-page) and counts them per column;
-//   3. per column: page prefix (k_page_prefix) + counts of the earlier waves;
+//   3. per column: page prefix + counts of the earlier waves;
 //   4. a candidate's rank in its column = that start + the number of equal
 //      columns earlier in the wave's list (64 list entries per step).
 __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
     const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
-    const int *__restrict__ theta, const int *__restrict__ need, const int *__restrict__ candoff,
-    const int *__restrict__ binoff, const unsigned int *__restrict__ pp,
+    const int *__restrict__ theta, const int *__restrict__ need,
+    const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
+    const int *__restrict__ candlen, int *__restrict__ candoff_out,
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot) {
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
@@ -267,14 +257,25 @@ __global__ __launch_bounds__(256) void k_select_open(
         pv[k] = ok ? P4[idx] : make_int4(0, 0, 0, 0);
         mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
     }
-    // page prefix of this thread's columns, loaded early (only columns at or below a threshold are read)
+    // rank of this page's first unit in each of the thread's columns (only
+    // columns at or below a threshold): the chunk's exclusive prefix
+    // (k_thresholds) plus the counts of the chunk's earlier pages (k_hist_open)
     constexpr int CPT = (ADLBQ_MAX_TYPES * NB) / 256;  // columns per thread, at most
     unsigned int ppv[CPT];
+    const int p0 = (p / CHUNK) * CHUNK;
 #pragma unroll
     for (int r = 0; r < CPT; r++) {
         const int c = threadIdx.x + r * 256;
         ppv[r] = 0;
-        if (c < C && (c % NB) <= theta[c / NB]) ppv[r] = pp[(long long)p * C + c];
+        if (c < C && (c % NB) <= theta[c / NB]) {
+            unsigned int v = csum[(long long)(p / CHUNK) * C + c];
+            unsigned short g[CHUNK - 1];
+#pragma unroll
+            for (int q = 0; q < CHUNK - 1; q++) g[q] = p0 + q < p ? gh[(long long)(p0 + q) * C + c] : (unsigned short)0;
+#pragma unroll
+            for (int q = 0; q < CHUNK - 1; q++) v += g[q];
+            ppv[r] = v;
+        }
     }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         const int th = theta[t];
@@ -282,12 +283,23 @@ __global__ __launch_bounds__(256) void k_select_open(
         sanc[t] = an;
         sth[t] = th;
         sneed[t] = need[t];
-        soff[t] = candoff[t];
         // largest anchor distance of bin th (bin_of: exact below NBX, then powers of two)
         const long long dmax = th < 0 ? -1 : th < NBX ? th : th >= NB - 1 ? (1ll << 40) : (1ll << (th - NBX + 6)) - 1;
         scut[t] = th < 0 ? (1ll << 40) : std::max(an - dmax, (long long)LOWEST + 1);
     }
     for (int c = threadIdx.x; c < 4 * C; c += blockDim.x) wc[c] = 0;
+    if (threadIdx.x < 64) {  // candidate list offsets: exclusive prefix of candlen over types
+        const int len = threadIdx.x < T ? candlen[threadIdx.x] : 0;
+        int x = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (threadIdx.x >= o) x += y;
+        }
+        if (threadIdx.x < T) soff[threadIdx.x] = x - len;
+        if (p == 0 && threadIdx.x < T) candoff_out[threadIdx.x] = x - len;
+        if (p == 0 && threadIdx.x == T - 1) candoff_out[T] = x;
+    }
     __syncthreads();
     int n = 0;  // this wave's candidates so far (uniform)
     const unsigned long long lt = lanemask_lt();
@@ -564,8 +576,12 @@ __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) 
 __global__ __launch_bounds__(256) void k_rank(int T, const int *__restrict__ candoff,
                                               const int *__restrict__ candlen,
                                               const unsigned long long *__restrict__ ckey,
-                                              unsigned int *__restrict__ crank) {
+                                              unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
+                                              long long ncsum) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES];
+    // the scan's chunk sums are consumed (k_select_open): leave them zeroed for the next batch
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < ncsum; i += (long long)gridDim.x * blockDim.x)
+        csum[i] = 0;
     for (int t = threadIdx.x; t <= T; t += blockDim.x) {
         soff[t] = candoff[t];
         if (t < T) slen[t] = candlen[t];
@@ -664,20 +680,29 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
                                                int WL, int &my_rec, int &rounds) {
     const int lane = threadIdx.x, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
     int st[TB], off[TB], c0[TB];
+    constexpr int NI = (SEG + CHAIN_WARM) / 64;  // WL <= SEG + CHAIN_WARM
+    unsigned int wv[TB][NI];                      // every window load in flight before the first LDS write
 #pragma unroll
     for (int q = 0; q < TB; q++) {
         st[q] = __builtin_amdgcn_readlane(my_start, q);
         off[q] = q < a.T ? a.candoff[q] : 0;
         const int len = q < a.T ? a.candlen[q] : 0;
         c0[q] = 0;
-        for (int i = lane; i < WL; i += 64) {
-            const int p = st[q] + i;
-            win[q * WL + i] = p < len ? a.crank[off[q] + p] : ~0u;
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const int p = st[q] + i * 64 + lane;
+            wv[q][i] = (i * 64 < WL && p < len) ? a.crank[off[q] + p] : ~0u;
         }
     }
+#pragma unroll
+    for (int q = 0; q < TB; q++)
+#pragma unroll
+        for (int i = 0; i < NI; i++)
+            if (i * 64 < WL) win[q * WL + i * 64 + lane] = wv[q][i];
     unsigned long long m_nx = jb + lane < j1 ? a.mask[jb + lane] : 0ull;
     int t_nx = jb + lane < j1 ? a.tmatch[jb + lane] : 0;
-    __syncthreads();
+    // one wave owns win: its LDS ops complete in order, only the compiler must not reorder
+    __builtin_amdgcn_wave_barrier();
     my_rec = my_start;
     for (int b0 = jb; b0 < j1; b0 += 64) {
         if (b0 == j0) {
@@ -732,15 +757,27 @@ __device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_
     const int lane = threadIdx.x, T = a.T, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
     const int my_off = lane < T ? a.candoff[lane] : 0;
     const int my_len = lane < T ? a.candlen[lane] : 0;
-    for (int t = 0; t < T; t++) {
-        const int st = __builtin_amdgcn_readlane(my_start, t), off = __builtin_amdgcn_readlane(my_off, t);
-        const int len = __builtin_amdgcn_readlane(my_len, t);
-        for (int i = lane; i < SEG; i += 64) {
-            const int p = st + i;
-            win[t * SEG + i] = p < len ? a.crank[off + p] : ~0u;
+    for (int g = 0; g < T; g += 8) {  // 8 types x SEG_BLOCKS loads in flight per lane
+        unsigned int wv[8][SEG_BLOCKS];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int t = g + q < T ? g + q : 0;
+            const int st = __builtin_amdgcn_readlane(my_start, t), off = __builtin_amdgcn_readlane(my_off, t);
+            const int len = g + q < T ? __builtin_amdgcn_readlane(my_len, t) : 0;
+#pragma unroll
+            for (int i = 0; i < SEG_BLOCKS; i++) {
+                const int p = st + i * 64 + lane;
+                wv[q][i] = p < len ? a.crank[off + p] : ~0u;
+            }
         }
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (g + q < T)
+#pragma unroll
+                for (int i = 0; i < SEG_BLOCKS; i++) win[(g + q) * SEG + i * 64 + lane] = wv[q][i];
     }
-    __syncthreads();
+    // one wave owns win: its LDS ops complete in order, only the compiler must not reorder
+    __builtin_amdgcn_wave_barrier();
     int my_c0 = 0;
     for (int b0 = j0; b0 < j1; b0 += 64) {
         const int j = b0 + lane;
@@ -832,15 +869,38 @@ __global__ __launch_bounds__(64) void k_chain_pass(ChainArgs a, int k) {
     }
 }
 
-// After the passes: nothing to do at a fixed point.  Otherwise walk the
-// segments in order from the exact start (segment 0 starts at 0): a segment
-// whose start equals its last computation's stands, and so does every later
-// one up to the next whose recorded start differs from its predecessor's
-// recorded end (found 64 segments at a time); the others are recomputed.
+// After the passes: every segment's recorded start is compared, in parallel,
+// with its predecessor's recorded end (the check of one more pass).  All equal
+// is the fixed point.  Otherwise wave 0 walks the segments in order from the
+// first mismatch, whose start is exact: a segment whose start equals its last
+// computation's stands, and so does every later one up to the next mismatch
+// (found 64 segments at a time); the others are recomputed.
+__device__ __forceinline__ bool seg_mismatch(const ChainArgs &a, int q) {
+    int k = a.passes;
+    while (k > 1 && !a.comp[(long long)k * a.nseg + q - 1]) k--;
+    const int *e = a.E + ((long long)k * a.nseg + q - 1) * a.T;
+    bool bad = false;
+    for (int t = 0; t < a.T; t++) bad |= e[t] != a.Sprev[q * a.T + t];
+    return bad;
+}
+
 template <int TB>
-__global__ __launch_bounds__(64) void k_chain_fix(ChainArgs a) {
+__global__ __launch_bounds__(256) void k_chain_fix(ChainArgs a) {
     extern __shared__ unsigned int win[];
-    const int lane = threadIdx.x, T = a.T, P = a.passes;
+    __shared__ int first_bad;
+    const int lane = threadIdx.x & 63, T = a.T, P = a.passes;
+    if (threadIdx.x == 0) first_bad = a.nseg;
+    __syncthreads();
+    int mine = a.nseg;
+    if (a.changed[P] > 0)  // a pass that recomputed nothing is already the fixed point
+        for (int q = 1 + threadIdx.x; q < a.nseg; q += blockDim.x)
+            if (seg_mismatch(a, q)) {
+                mine = q;
+                break;
+            }
+    if (mine < a.nseg) atomicMin(&first_bad, mine);
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
     int used = 0, recomputed = 0;
     for (int k = 1; k <= P; k++) {
         used += a.changed[k] > 0;
@@ -851,22 +911,16 @@ __global__ __launch_bounds__(64) void k_chain_fix(ChainArgs a) {
         a.ctr->chain_recomputed = recomputed;
         a.ctr->chain_fallback = 0;
     }
-    if (a.changed[P] == 0) return;
-    int st = 0, rounds = 0, redo = 0, s = 0;
+    int s = first_bad;
+    if (s >= a.nseg) return;
+    int st = latest_end(a, s - 1, P), rounds = 0, redo = 0;
     while (s < a.nseg) {
         if (!__ballot(lane < T && st != a.Sprev[s * T + lane])) {
-            // s stands; find the next segment whose recorded start is not its predecessor's recorded end
+            // s stands; jump to the next recorded mismatch
             int nxt = a.nseg;
             for (int c0 = s + 1; c0 < a.nseg && nxt == a.nseg; c0 += 64) {
                 const int q = c0 + lane;
-                bool bad = false;
-                if (q < a.nseg) {
-                    int k = P;
-                    while (k > 1 && !a.comp[(long long)k * a.nseg + q - 1]) k--;
-                    const int *e = a.E + ((long long)k * a.nseg + q - 1) * T;
-                    for (int t = 0; t < T; t++) bad |= e[t] != a.Sprev[q * T + t];
-                }
-                const unsigned long long bb = __ballot(bad);
+                const unsigned long long bb = __ballot(q < a.nseg && seg_mismatch(a, q));
                 if (bb) nxt = c0 + __ffsll((long long)bb) - 1;
             }
             if (nxt >= a.nseg) break;
@@ -875,7 +929,7 @@ __global__ __launch_bounds__(64) void k_chain_fix(ChainArgs a) {
         }
         int my_rec;
         st = seg_solve<TB>(a, s, s * SEG, st, win, my_rec, rounds);
-        __syncthreads();  // win is refilled by the next recomputed segment
+        __builtin_amdgcn_wave_barrier();  // win is refilled by the next recomputed segment
         redo++;
         s++;
     }
@@ -885,73 +939,26 @@ __global__ __launch_bounds__(64) void k_chain_fix(ChainArgs a) {
     }
 }
 
-// ---------------------------------------------------------------- finalize
-__global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, int R, const int *__restrict__ tmatch,
-                                                  const int *__restrict__ umatch, const int *__restrict__ cslot,
-                                                  const int *__restrict__ prio,
-                                                  uint32_t *meta, int *pin, const int *__restrict__ seqa,
-                                                  const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
-                                                  int my_world, int *__restrict__ resp, DevCounters *ctr) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= R) return;
-    const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
-    const int rank = rq[0], hang = rq[1];
-    const int slot = tmatch[j] >= 0 ? tmatch[j] : (umatch[j] >= 0 ? cslot[umatch[j]] : -1);
-    int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
-    if (slot >= 0) {
-        pin[slot] = rank;  // adlb.c:1210-1212
-        if (rank >= 0) meta[slot] |= M_PINNED;
-        const int4 c0 = cold0[slot], c1 = cold1[slot];
-        o[0] = 1;
-        o[1] = c1.z;
-        o[2] = prio[slot];
-        o[3] = c0.y;
-        o[4] = c0.x;
-        o[5] = seqa[slot];
-        o[6] = my_world;
-        o[7] = c0.w;
-        o[8] = c1.x;
-        o[9] = c1.y;
-    } else if (!hang) {
-        o[0] = -2;  // NO_CURR_WORK
-    } else {
-        atomicAdd(&ctr->park_pending, 1);
-    }
-    int *out = resp + (long long)ADLBQ_RESP_INTS * j;
-#pragma unroll
-    for (int i = 0; i < ADLBQ_RESP_INTS; i++) out[i] = o[i];
-}
-
-// ---------------------------------------------------------------- park on rq + RFR donor choice
-// One workgroup: parked requests are appended to rq in arrival order (block
-// prefix sum over per-thread contiguous chunks); the RFR donor choice, which
-// depends on earlier choices through rfr_out / rfr_to_rank, then walks the
-// newly parked entries in order on wave 0 (only when a donor can exist).
-__global__ __launch_bounds__(1024) void k_park(DonorCtx c, int donors, const int *__restrict__ reqs, int R,
-                                               const int *__restrict__ tmatch, const int *__restrict__ umatch,
-                                               int *rq_rank, int *rq_types, int *rq_live, int *rq_req,
-                                               DevCounters *ctr, int *resp, int *dem, int T,
-                                               DevCounters *snap) {
+// ---------------------------------------------------------------- finalize + park
+// Every request: pin its unit and write TA_RESERVE_RESP (adlb.c:1210-1224), or
+// NO_CURR_WORK (1311-1316).  Requests that park are counted into a 64-bit
+// arrival ticket (parked << 32 | 1 per workgroup); the workgroup that arrives
+// last appends them to rq in arrival order and chooses their RFR donors
+// (1238-1310).  Response words [10], [11] of a parked request are written only
+// by that last workgroup, so no two workgroups store the same bytes.
+__device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__ reqs, int R,
+                          const int *__restrict__ tmatch, const int *__restrict__ umatch, int *rq_rank,
+                          int *rq_types, int *rq_live, int *rq_req, DevCounters *ctr, int *resp) {
     __shared__ int wsum[16];
     __shared__ int s_n0, s_total;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nth = blockDim.x;
-    if (tid < T) dem[tid] = 0;  // k_req_prep of the next batch accumulates into it
-    if (ctr->park_pending == 0) {  // nothing parked (the common case): skip the scan
-        if (tid == 0) {
-            ctr->n_parked_last = 0;
-            *snap = *ctr;
-            __threadfence_system();
-        }
-        return;
-    }
     const int per = (R + nth - 1) / nth, lo = min(R, tid * per), hi = min(R, lo + per);
     auto parked = [&](int j) {
         return tmatch[j] < 0 && umatch[j] < 0 && reqs[(long long)ADLBQ_RESERVE_INTS * j + 1] != 0;
     };
     int cnt = 0;
     for (int j = lo; j < hi; j++) cnt += parked(j);
-    // block exclusive scan of cnt
-    int x = cnt;
+    int x = cnt;  // block exclusive scan of cnt
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         int y = __shfl_up(x, o, 64);
@@ -977,22 +984,84 @@ __global__ __launch_bounds__(1024) void k_park(DonorCtx c, int donors, const int
     __threadfence();
     __syncthreads();
     const int n0 = s_n0, np = s_total;
-    if (donors && w == 0) {
+    if (w == 0) {
         for (int k = n0; k < n0 + np; k++) {
             const int j = rq_req[k];
             const int *rr = reqs + (long long)ADLBQ_RESERVE_INTS * j;
             const int rank = rr[0];
             int cand = -1;
-            if (rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) < 0) cand = rfr_select(c, rank, rr + 2);
+            if (donors && rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) < 0)
+                cand = rfr_select(c, rank, rr + 2);
             if (lane == 0) resp[(long long)ADLBQ_RESP_INTS * j + 11] = cand;
         }
     }
     if (tid == 0) {
-        ctr->park_pending = 0;
         ctr->rq_n = n0 + np;
         ctr->rq_live += np;
         if (ctr->rq_live > ctr->rq_hwm) ctr->rq_hwm = ctr->rq_live;
         ctr->n_parked_last = np;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, int R, const int *__restrict__ tmatch,
+                                                  const int *__restrict__ umatch, const int *__restrict__ cslot,
+                                                  const int *__restrict__ prio,
+                                                  uint32_t *meta, int *pin, const int *__restrict__ seqa,
+                                                  const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
+                                                  int my_world, int *__restrict__ resp, DevCounters *ctr,
+                                                  DonorCtx dc, int donors, int *rq_rank, int *rq_types,
+                                                  int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap) {
+    __shared__ int s_parked;
+    __shared__ unsigned long long s_ticket;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (threadIdx.x == 0) s_parked = 0;
+    __syncthreads();
+    if (j < R) {
+        const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
+        const int rank = rq[0], hang = rq[1];
+        const int slot = tmatch[j] >= 0 ? tmatch[j] : (umatch[j] >= 0 ? cslot[umatch[j]] : -1);
+        int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
+        if (slot >= 0) {
+            pin[slot] = rank;  // adlb.c:1210-1212
+            if (rank >= 0) meta[slot] |= M_PINNED;
+            const int4 c0 = cold0[slot], c1 = cold1[slot];
+            o[0] = 1;
+            o[1] = c1.z;
+            o[2] = prio[slot];
+            o[3] = c0.y;
+            o[4] = c0.x;
+            o[5] = seqa[slot];
+            o[6] = my_world;
+            o[7] = c0.w;
+            o[8] = c1.x;
+            o[9] = c1.y;
+        } else if (!hang) {
+            o[0] = -2;  // NO_CURR_WORK
+        }
+        const bool parks = slot < 0 && hang;
+        int *out = resp + (long long)ADLBQ_RESP_INTS * j;
+#pragma unroll
+        for (int i = 0; i < 10; i++) out[i] = o[i];
+        if (!parks) {
+            out[10] = -1;
+            out[11] = -1;
+        }
+        const unsigned long long pb = __ballot(parks);
+        if ((threadIdx.x & 63) == 0 && pb) atomicAdd(&s_parked, __popcll(pb));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_ticket = atomicAdd(&ctr->fin_ticket, ((unsigned long long)s_parked << 32) | 1ull);
+    __syncthreads();
+    if ((unsigned int)s_ticket != gridDim.x - 1) return;
+    // the last workgroup of the batch
+    const int total = (int)(s_ticket >> 32) + s_parked;
+    if (threadIdx.x < T) dem[threadIdx.x] = 0;  // k_req_prep of the next batch accumulates into it
+    if (total > 0) park_tail(dc, donors, reqs, R, tmatch, umatch, rq_rank, rq_types, rq_live, rq_req, ctr, resp);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (total == 0) ctr->n_parked_last = 0;
+        ctr->fin_ticket = 0;
         *snap = *ctr;
         __threadfence_system();
     }
@@ -1032,16 +1101,15 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         AQ_HIP(hipStreamSynchronize(h->stream));
     if (need_gh > h->cap_gh) {
         if (h->d_gh) AQ_HIP(hipFree(h->d_gh));
-        if (h->d_pp) AQ_HIP(hipFree(h->d_pp));
         h->cap_gh = std::max(need_gh, 2 * h->cap_gh);
         AQ_HIP(hipMalloc((void **)&h->d_gh, sizeof(unsigned short) * h->cap_gh));
-        AQ_HIP(hipMalloc((void **)&h->d_pp, sizeof(unsigned int) * h->cap_gh));
+
     }
     if (need_cs > h->cap_csum) {
         if (h->d_csum) AQ_HIP(hipFree(h->d_csum));
         h->cap_csum = std::max(need_cs, 2 * h->cap_csum);
         AQ_HIP(hipMalloc((void **)&h->d_csum, sizeof(unsigned int) * h->cap_csum));
-        // zero once; every batch's k_page_prefix re-zeroes the rows it used
+        // zero once; every batch's k_rank re-zeroes the rows it used
         AQ_HIP(hipMemsetAsync(h->d_csum, 0, sizeof(unsigned int) * h->cap_csum, h->stream));
     }
     if (need_cand > h->cap_cand) {
@@ -1083,18 +1151,13 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             h->d_csum);
         stage_end(h, "hist", ev);
         stage_begin(h, "thresholds", &ev);
-        k_thresholds<<<1, 1024, sizeof(unsigned int) * C, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta,
-                                                               h->d_need, h->d_candoff, h->d_candlen,
-                                                               h->d_needsort, h->d_binoff);
+        k_thresholds<<<C, 256, 0, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
+                                       h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt);
         stage_end(h, "thresholds", ev);
-        stage_begin(h, "prefix", &ev);
-        const long long ncol = (long long)nchunks * C;
-        k_page_prefix<<<(int)((ncol + 255) / 256), 256, 0, s>>>(np, T, h->d_theta, h->d_gh, h->d_csum, h->d_pp);
-        stage_end(h, "prefix", ev);
         stage_begin(h, "select", &ev);
         k_select_open<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
-            h->d_need, h->d_candoff, h->d_binoff, h->d_pp, h->d_ckey, h->d_cslot);
+            h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot);
         stage_end(h, "select", ev);
         stage_begin(h, "sort", &ev);
         k_sort_types<<<T, 1024, 0, s>>>(h->d_needsort, h->d_candoff, h->d_candlen, h->d_ckey, h->d_cslot,
@@ -1115,19 +1178,20 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     if (np > 0 && T > 0) {
         stage_begin(h, "rank", &ev);
-        k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank);
+        k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
+                                    (long long)((np + CHUNK - 1) / CHUNK) * C);
         stage_end(h, "rank", ev);
     }
     stage_begin(h, "chain", &ev);
     {
         const int nseg = (R + SEG - 1) / SEG;
-        const int P = h->chain_passes > 0 ? h->chain_passes : (T <= 8 ? 3 : 8);
+        const int P = h->chain_passes > 0 ? h->chain_passes : (T <= 8 ? 2 : 8);
         const int warm = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, P, warm, h->d_candoff, h->d_candlen, h->d_crank,
                      h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chcomp, h->d_chS, h->d_chchg, h->d_ctr};
         auto run = [&](auto kpass, auto kfix, size_t lds) {
             for (int k = 1; k <= P; k++) kpass<<<nseg, 64, lds, s>>>(ca, k);
-            kfix<<<1, 64, lds, s>>>(ca);
+            kfix<<<1, 256, lds, s>>>(ca);
         };
         if (T <= 4) run(k_chain_pass<4>, k_chain_fix<4>, sizeof(unsigned int) * 4 * (SEG + std::max(warm, 0)));
         else if (T <= 8) run(k_chain_pass<8>, k_chain_fix<8>, sizeof(unsigned int) * 8 * (SEG + std::max(warm, 0)));
@@ -1135,17 +1199,16 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);
-    k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
-                                               h->d_meta, h->d_pin,
-                                               h->d_seq, h->d_cold0, h->d_cold1, h->my_world, d_resp, h->d_ctr);
+    {
+        const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
+        DevCounters *snap = nullptr;
+        AQ_HIP(hipHostGetDevicePointer((void **)&snap, h->h_snap + h->snap_next, 0));
+        k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
+                                                   h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
+                                                   h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
+                                                   h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap);
+    }
     stage_end(h, "finalize", ev);
-    stage_begin(h, "park", &ev);
-    const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
-    DevCounters *snap = nullptr;
-    AQ_HIP(hipHostGetDevicePointer((void **)&snap, h->h_snap + h->snap_next, 0));
-    k_park<<<1, 1024, 0, s>>>(donor_ctx(h), donors, d_reqs, R, h->d_tmatch, h->d_umatch, h->d_rq_rank,
-                              h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_ctr, d_resp, h->d_dem, T, snap);
-    stage_end(h, "park", ev);
     h->launched_reserves += R;
     h->snap_at[h->snap_next] = h->launched_reserves;
     AQ_HIP(hipEventRecord(h->snap_ev[h->snap_next], s));

@@ -514,13 +514,16 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipHostMalloc((void **)&h->h_snap, sizeof(DevCounters) * adlbq_server::NSNAP, hipHostMallocMapped));
     for (int i = 0; i < adlbq_server::NSNAP; i++) AQ_HIP(hipEventCreateWithFlags(&h->snap_ev[i], hipEventDisableTiming));
     AQ_HIP(hipMalloc((void **)&h->d_dem, sizeof(int) * T1));
-    AQ_HIP(hipMemset(h->d_dem, 0, sizeof(int) * T1));  // k_park re-zeroes it after every batch
+    AQ_HIP(hipMemset(h->d_dem, 0, sizeof(int) * T1));  // k_finalize re-zeroes it after every batch
     AQ_HIP(hipMalloc((void **)&h->d_theta, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_need, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_candoff, sizeof(int) * (T1 + 1)));
     AQ_HIP(hipMalloc((void **)&h->d_candlen, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_needsort, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_binoff, sizeof(int) * T1 * NB));
+    AQ_HIP(hipMalloc((void **)&h->d_coltot, sizeof(unsigned int) * T1 * NB));
+    AQ_HIP(hipMalloc((void **)&h->d_type_cnt, sizeof(int) * T1));
+    AQ_HIP(hipMemset(h->d_type_cnt, 0, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     long long pages = std::max<long long>(16, (max_units + PAGE - 1) / PAGE + 16);
@@ -540,7 +543,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
-                    h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_gh, h->d_pp, h->d_csum,
+                    h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
                     h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg, h->d_chcomp};
     for (void *p : ptrs)
@@ -926,7 +929,8 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         return ADLBQ_OK;
     }
     if (n == "chain_warm") {
-        if (value < -1 || value > 4096 || (value > 0 && value % 256)) return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 or a multiple of 256 in [0, 4096]");
+        if (value != -1 && value != 0 && value != 256 && value != 512)
+            return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 (auto), 0, 256 or 512");
         h->chain_warm = (int)value;
         return ADLBQ_OK;
     }

@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-STAGES = ["prep", "hist", "thresholds", "prefix", "select", "sort", "targeted", "rank", "chain", "finalize", "park"]
+STAGES = ["prep", "hist", "thresholds", "select", "sort", "targeted", "rank", "chain", "finalize"]
 
 
 def parse():
@@ -63,9 +63,8 @@ def parse():
 
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
 KERNEL_OF = {"prep": "k_req_prep", "hist": "k_hist_open", "thresholds": "k_thresholds",
-             "prefix": "k_page_prefix", "select": "k_select_open", "sort": "k_sort_types",
-             "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain_pass", "finalize": "k_finalize",
-             "park": "k_park"}
+             "select": "k_select_open", "sort": "k_sort_types",
+             "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain_pass", "finalize": "k_finalize"}
 
 
 def _kernel_base(name: str) -> str:

@@ -131,10 +131,10 @@ int  adlbq_set_stream(adlbq_server *h, void *hip_stream); /* NULL = handle's own
 void *adlbq_get_stream(adlbq_server *h);
 int  adlbq_sync(adlbq_server *h);
 /* Per-kernel GPU time (HIP events on the handle's stream around each launch of
- * a reserve batch) when enabled.  Stage names, one kernel each: "prep"
- * (k_req_prep), "hist" (k_hist_open), "thresholds", "prefix" (k_page_prefix),
- * "select" (k_select_open), "sort" (k_sort_types), "targeted", "rank",
- * "chain" (k_chain_pass x passes + k_chain_fix), "finalize", "park". */
+ * a reserve batch) when enabled.  Stage names: "prep" (k_req_prep), "hist"
+ * (k_hist_open), "thresholds", "select" (k_select_open), "sort"
+ * (k_sort_types), "targeted", "rank", "chain" (k_chain_pass x passes +
+ * k_chain_fix), "finalize" (k_finalize, which also parks). */
 int  adlbq_profile_enable(adlbq_server *h, int on);
 /* Profile one stage only (NULL: every stage); enables profiling. */
 int  adlbq_profile_only(adlbq_server *h, const char *stage);
@@ -152,7 +152,7 @@ long long adlbq_stat(adlbq_server *h, const char *name);
 /* Tuning: "chain_passes" = parallel segment passes of the ordered-choice
  * kernel before the in-order fix-up (1..30; 0 = auto: 3 for up to 8 types,
  * else 8); "chain_warm" = requests replayed ahead of each segment in the first
- * pass (-1 = auto: 512 for up to 8 types; else a multiple of 256 up to 4096).
+ * pass (-1 = auto: 512 for up to 8 types; or 0, 256, 512).
  * Results never depend on either; tests lower them to force the fix-up. */
 int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);
