@@ -111,7 +111,7 @@ struct adlbq_server {
     long long rq_n_upper = 0;      // upper bound on rq_n while ctr is stale
     // rq_n snapshots written by k_finalize into mapped host memory at the end of
     // each reserve batch, so the rq capacity bound tightens without a sync
-    static constexpr int NSNAP = 4;
+    static constexpr int NSNAP = 8;
     adlbq::DevCounters *h_snap = nullptr;   // [NSNAP] pinned, device-visible
     hipEvent_t snap_ev[NSNAP] = {};
     long long snap_at[NSNAP] = {};         // reserves launched up to and including that batch
@@ -173,7 +173,7 @@ int hip_fail(hipError_t e, const char *where);
 int ensure_req_capacity(adlbq_server *h, int n);
 int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
-void tighten_rq_bound(adlbq_server *h);    // newest completed batch snapshot -> rq_n_upper (no sync)
+void tighten_rq_bound(adlbq_server *h, bool wait_oldest);  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);

@@ -54,10 +54,20 @@ static int grow_pages(adlbq_server *h, int need) {
     return ADLBQ_OK;
 }
 
-void tighten_rq_bound(adlbq_server *h) {
-    for (int k = 1; k <= adlbq_server::NSNAP; k++) {
-        const int i = (h->snap_next - k + adlbq_server::NSNAP) % adlbq_server::NSNAP;
-        if (!h->snap_ev[i] || !h->snap_at[i]) continue;
+void tighten_rq_bound(adlbq_server *h, bool wait_oldest) {
+    const int N = adlbq_server::NSNAP;
+    if (wait_oldest) {  // backpressure: let the oldest batch still tracked land
+        for (int k = N; k >= 1; k--) {
+            const int i = (h->snap_next - k + N) % N;
+            if (h->snap_at[i]) {
+                hipEventSynchronize(h->snap_ev[i]);
+                break;
+            }
+        }
+    }
+    for (int k = 1; k <= N; k++) {
+        const int i = (h->snap_next - k + N) % N;
+        if (!h->snap_at[i]) continue;
         if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
         const long long bound = (long long)h->h_snap[i].rq_n + (h->launched_reserves - h->snap_at[i]);
         if (bound < h->rq_n_upper) h->rq_n_upper = bound;
@@ -69,14 +79,14 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
     long long need = (h->ctr_stale ? h->rq_n_upper : (long long)h->ctr.rq_n) + extra;
     if (need <= h->rq_cap) return ADLBQ_OK;
     if (h->ctr_stale) {
-        tighten_rq_bound(h);
+        // the bound is loose by the batches still in flight: use the newest
+        // landed snapshot and, if that is not enough, wait for the oldest
+        // tracked batch (the host then runs at most NSNAP batches ahead)
+        tighten_rq_bound(h, false);
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
-    }
-    if (h->ctr_stale) {
-        int rc = refresh_counters(h);
-        if (rc) return rc;
-        need = (long long)h->ctr.rq_n + extra;
+        tighten_rq_bound(h, true);
+        need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
     }
     long long nc = std::max<long long>(need, (long long)h->rq_cap * 2);

@@ -225,6 +225,7 @@ def main():
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
+    t_submit = time.perf_counter() - t0  # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -275,6 +276,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps,
+        "host_submit_ms_per_step": round(t_submit * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
