@@ -98,8 +98,11 @@ struct adlbq_server {
     std::vector<long long> seq2slot;  // index wqseqno
     long long *d_seq2slot = nullptr; long long cap_seq = 0;
     long long live_units = 0, max_count = 0, live_targeted = 0;
-    std::vector<long long> anchor;    // per type: max prio ever put (upper bound of live max)
-    long long *d_anchor = nullptr; bool anchor_dirty = true;
+    // per type: an upper bound of the prio of every live unpinned unit, kept on
+    // the device (puts and unreserves raise it; a reserve batch lowers it to
+    // the live maximum its histogram saw, applied when the batch ends)
+    long long *d_anchor = nullptr;
+    long long *d_anchor_next = nullptr;   // [T] LLONG_MIN = no update
     int *d_utypes = nullptr;
 
     // ---- parked reserves

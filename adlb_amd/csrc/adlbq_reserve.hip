@@ -158,7 +158,8 @@ __global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages
 __global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
-                                                     int *type_cnt) {
+                                                     int *type_cnt, const long long *__restrict__ anchor,
+                                                     long long *__restrict__ anchor_next) {
     __shared__ unsigned int wsum[4];
     __shared__ bool s_last;
     const int c = blockIdx.x, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -192,9 +193,16 @@ __global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict
     int th = -1, nd = 0, len = 0;
     if (d > 0) {
         long long cum = 0;
+        bool seen = false;
         for (int bb = 0; bb < NB; bb++) {
             const long long x = __hip_atomic_load(coltot + t * NB + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             binoff[t * NB + bb] = (int)cum;
+            if (x > 0 && !seen) {
+                // the live maximum is at most anchor - (smallest distance of this bin):
+                // the next batch's anchor (applied when this batch ends, k_finalize)
+                seen = true;
+                anchor_next[t] = anchor[t] - (bb < NBX ? bb : (1ll << (bb - NBX + 5)));
+            }
             if (cum + x >= d) {
                 th = bb;
                 if (bb < NBX) {  // one priority value: the first (d - cum) by wqseqno
@@ -1010,7 +1018,8 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
                                                   int my_world, int *__restrict__ resp, DevCounters *ctr,
                                                   DonorCtx dc, int donors, int *rq_rank, int *rq_types,
-                                                  int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap) {
+                                                  int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap,
+                                                  long long *anchor, long long *anchor_next) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1056,7 +1065,14 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
     if ((unsigned int)s_ticket != gridDim.x - 1) return;
     // the last workgroup of the batch
     const int total = (int)(s_ticket >> 32) + s_parked;
-    if (threadIdx.x < T) dem[threadIdx.x] = 0;  // k_req_prep of the next batch accumulates into it
+    if (threadIdx.x < T) {
+        dem[threadIdx.x] = 0;  // k_req_prep of the next batch accumulates into it
+        const long long a = anchor_next[threadIdx.x];
+        if (a != LLONG_MIN) {  // lower the anchor to the live maximum k_thresholds saw
+            anchor[threadIdx.x] = a;
+            anchor_next[threadIdx.x] = LLONG_MIN;
+        }
+    }
     if (total > 0) park_tail(dc, donors, reqs, R, tmatch, umatch, rq_rank, rq_types, rq_live, rq_req, ctr, resp);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1152,7 +1168,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_end(h, "hist", ev);
         stage_begin(h, "thresholds", &ev);
         k_thresholds<<<C, 256, 0, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
-                                       h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt);
+                                       h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor,
+                                       h->d_anchor_next);
         stage_end(h, "thresholds", ev);
         stage_begin(h, "select", &ev);
         k_select_open<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
@@ -1206,7 +1223,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
                                                    h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
-                                                   h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap);
+                                                   h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap,
+                                                   h->d_anchor, h->d_anchor_next);
     }
     stage_end(h, "finalize", ev);
     h->launched_reserves += R;

@@ -157,11 +157,6 @@ int sync_tables(adlbq_server *h) {
         if ((rc = upload(&h->d_all_fill, &h->cap_all_fill, af, h->stream))) return rc;
         h->tables_dirty = false;
     }
-    if (h->anchor_dirty) {
-        AQ_HIP(hipMemcpyAsync(h->d_anchor, h->anchor.data(), sizeof(long long) * h->T,
-                              hipMemcpyHostToDevice, h->stream));
-        h->anchor_dirty = false;
-    }
     if (h->qm_dirty) {
         if (h->S * h->T > 0)
             AQ_HIP(hipMemcpyAsync(h->d_qm_hi, h->qm_hi.data(), sizeof(int) * h->S * h->T,
@@ -228,6 +223,25 @@ void stage_end(adlbq_server *h, const char *name, hipEvent_t ev) {
 
 // ============================================================================ kernels
 
+// Keep anchor[t] >= prio.  Most calls do not raise it, so the anchor is read
+// first; the lanes of a wave that do raise it agree on one atomic per type
+// (a single device-scope word per type would otherwise serialise them).
+// Every lane of the wave must call it (INT_MIN: nothing to raise).
+__device__ __forceinline__ void raise_anchor(long long *anchor, int t, int prio) {
+    bool up = __hip_atomic_load(anchor + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (long long)prio;
+    while (true) {
+        const unsigned long long b = __ballot(up);
+        if (!b) break;
+        const int leader = __ffsll((long long)b) - 1;
+        const int lt = __shfl(t, leader, 64);
+        int m = (up && t == lt) ? prio : INT_MIN;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        if (__lane_id() == leader) atomicMax(anchor + lt, (long long)m);
+        if (t == lt) up = false;
+    }
+}
+
 struct PutRec {  // staged by the host per Put
     int slot, prio, meta, seq;
     int answer, len, home, clen;
@@ -235,10 +249,12 @@ struct PutRec {  // staged by the host per Put
 };
 
 __global__ void k_put_scatter(const PutRec *__restrict__ r, int n, int *prio, uint32_t *meta, int *pin,
-                              int *seq, int4 *cold0, int4 *cold1, long long *seq2slot) {
+                              int *seq, int4 *cold0, int4 *cold1, long long *seq2slot, long long *anchor) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    PutRec u = r[i];
+    const bool ok = i < n;
+    PutRec u = r[ok ? i : 0];
+    raise_anchor(anchor, ok ? (u.meta & M_TYPE) : 0, ok ? u.prio : INT_MIN);  // upper bounds of live prios
+    if (!ok) return;
     prio[u.slot] = u.prio;
     meta[u.slot] = (uint32_t)u.meta;
     pin[u.slot] = -1;
@@ -323,29 +339,36 @@ __global__ void k_get(int slot, int rank, int seq, const int *prio, uint32_t *me
 }
 
 __global__ void k_unreserve(int slot, int rank, int seq, int newpin, uint32_t *meta, int *pin,
-                            const int *seqa, int *res) {
+                            const int *seqa, int *res, const int *prio, long long *anchor) {
     uint32_t m = meta[slot];
     res[0] = 0;
     if ((m & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) {
         pin[slot] = newpin;
         meta[slot] = m & ~M_PINNED;
+        atomicMax(&anchor[m & M_TYPE], (long long)prio[slot]);
         res[0] = 1;
     }
 }
 
 __global__ void k_unreserve_batch(const int *__restrict__ trip, int n, const long long *__restrict__ seq2slot,
-                                  long long nseq, uint32_t *meta, int *pin, const int *seqa) {
+                                  long long nseq, uint32_t *meta, int *pin, const int *seqa,
+                                  const int *prio, long long *anchor) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int rank = trip[3 * i], seq = trip[3 * i + 1], np = trip[3 * i + 2];
-    if (seq <= 0 || seq >= nseq) return;
-    long long slot = seq2slot[seq];
-    if (slot < 0) return;
-    uint32_t m = meta[slot];
-    if ((m & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) {
-        pin[slot] = np;
-        meta[slot] = m & ~M_PINNED;
+    int t = 0, up = INT_MIN;
+    if (i < n) {
+        int rank = trip[3 * i], seq = trip[3 * i + 1], np = trip[3 * i + 2];
+        long long slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
+        if (slot >= 0) {
+            uint32_t m = meta[slot];
+            if ((m & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) {
+                pin[slot] = np;
+                meta[slot] = m & ~M_PINNED;
+                t = m & M_TYPE;
+                up = prio[slot];
+            }
+        }
     }
+    raise_anchor(anchor, t, up);  // available again: keep the anchor above it
 }
 
 // update_local_state over the open bucket: count of live unpinned units and per
@@ -502,7 +525,6 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     h->master = num_app_ranks;                    // adlb.c:256
     h->my_world = num_app_ranks + my_server_idx;
     h->num_world = num_app_ranks + num_servers;
-    h->anchor.assign(std::max(ntypes, 1), (long long)INT_MIN);
     h->qm_hi.assign((size_t)num_servers * std::max(ntypes, 1), LOWEST);  // adlb.c:301-316
     h->qm_qlen.assign(num_servers, 0);
     h->qm_bytes.assign(num_servers, 0.0);
@@ -511,6 +533,12 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     auto cleanup = [&](int code) { adlbq_destroy(h); return code; };
     int T1 = std::max(ntypes, 1);
     AQ_HIP(hipMalloc((void **)&h->d_anchor, sizeof(long long) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_anchor_next, sizeof(long long) * T1));
+    {  // anchors start below every prio; the device keeps them (puts / unreserves raise, batches lower)
+        std::vector<long long> lo(T1, (long long)INT_MIN), none(T1, LLONG_MIN);
+        AQ_HIP(hipMemcpy(h->d_anchor, lo.data(), sizeof(long long) * T1, hipMemcpyHostToDevice));
+        AQ_HIP(hipMemcpy(h->d_anchor_next, none.data(), sizeof(long long) * T1, hipMemcpyHostToDevice));
+    }
     AQ_HIP(hipMalloc((void **)&h->d_utypes, sizeof(int) * T1));
     if (ntypes) AQ_HIP(hipMemcpy(h->d_utypes, user_types, sizeof(int) * ntypes, hipMemcpyHostToDevice));
     AQ_HIP(hipMalloc((void **)&h->d_qm_hi, sizeof(int) * num_servers * T1));
@@ -550,7 +578,7 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
     void *ptrs[] = {h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_open_pages,
                     h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_all_pages,
-                    h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_utypes, h->d_rq_rank, h->d_rq_types,
+                    h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_gh, h->d_csum,
@@ -625,10 +653,6 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         r.target = tgt;
         if ((long long)h->seq2slot.size() <= seq) h->seq2slot.resize((size_t)seq * 2 + 16, -1);
         h->seq2slot[seq] = slot;
-        if (u[1] > h->anchor[ti]) {
-            h->anchor[ti] = u[1];
-            h->anchor_dirty = true;
-        }
         h->live_units++;
         if (tgt >= 0) h->live_targeted++;
         if (h->live_units > h->max_count) h->max_count = h->live_units;
@@ -643,7 +667,7 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
     AQ_HIP(hipMalloc((void **)&d_rec, sizeof(PutRec) * n));
     AQ_HIP(hipMemcpyAsync(d_rec, rec.data(), sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
     k_put_scatter<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, h->d_prio, h->d_meta, h->d_pin, h->d_seq,
-                                                          h->d_cold0, h->d_cold1, h->d_seq2slot);
+                                                          h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor);
     bool may_match = h->ctr_stale || h->ctr.rq_live > 0;
     if (may_match) {
         AQ_HIP(hipMalloc((void **)&d_out, sizeof(int) * 3 * n));
@@ -701,7 +725,7 @@ int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, in
     *found = 0;
     if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
     k_unreserve<<<1, 1, 0, h->stream>>>((int)slot, rank, wqseqno, new_pin_rank, h->d_meta, h->d_pin, h->d_seq,
-                                        h->d_result);
+                                        h->d_result, h->d_prio, h->d_anchor);
     AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
     *found = h->h_result[0];
@@ -713,7 +737,8 @@ int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples) {
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
     k_unreserve_batch<<<(n + 255) / 256, 256, 0, h->stream>>>(d_triples, n, h->d_seq2slot, h->next_wqseqno,
-                                                              h->d_meta, h->d_pin, h->d_seq);
+                                                              h->d_meta, h->d_pin, h->d_seq, h->d_prio,
+                                                              h->d_anchor);
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
 }

@@ -87,6 +87,23 @@ def test_chain_fixup_path(gpu_available, name, passes):
         assert st["chain_fallback"] > 0, st
 
 
+@pytest.mark.parametrize("equal_prio", [False, True])
+def test_depletion_batches_vs_oracle(gpu_available, equal_prio):
+    """Reserve batches with nothing given back: each batch pins the best units,
+    so the next one's thresholds sit deeper below the anchor (exact bins, then
+    far bins and the sort path) while the anchor follows the live maximum."""
+    w = synth.config2(n_units=20_000, n_reserves=4096, seed=211, equal_prio=equal_prio)
+    rng = np.random.default_rng(5)
+    parts = [synth.put_events(w)]
+    for _ in range(4):
+        tv = synth.type_vectors(rng, w.user_types, w.n_reserves)
+        parts.append(synth.reserve_events(w.r_rank, tv, w.r_hang))
+        parts.append(synth.simple_events(synth.OP_INFO))  # ends the batch
+    tr = np.concatenate(parts)
+    cfg = (w.num_app_ranks, 1, 0)
+    assert_same(run_abi(w.user_types, cfg, tr, max_units=w.n_units), run_oracle(w.user_types, cfg, tr))
+
+
 def test_stream_vs_oracle(gpu_available):
     o = oracle.Oracle("own")
     o.init([1, 2], 128, 8, 3)
