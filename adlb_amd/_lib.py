@@ -11,7 +11,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libadlbq.so")
+LIB_PATH = os.environ.get("ADLBQ_LIB") or os.path.join(HERE, "libadlbq.so")  # override: experiments only
 HEADER = os.path.join(os.path.dirname(HERE), "include", "adlbq.h")
 
 c_int, c_ll, c_void_p, c_double, c_char_p = (ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p,

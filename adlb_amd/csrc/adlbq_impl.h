@@ -148,9 +148,10 @@ struct adlbq_server {
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate
     int *d_seg_cnt = nullptr;          // [nseg] chain: untargeted-capable requests per segment
     int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
-    int *d_chcomp = nullptr;           // [passes + 1][nseg] chain: segment computed in pass k
-    int *d_chS = nullptr;              // [nseg][T] chain: segment starts of the last computation
-    int *d_chchg = nullptr;            // [CHAIN_MAX_PASSES + 2] chain: segments recomputed per pass
+    int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
+    int *d_chSf = nullptr, *d_chEf = nullptr;  // [nseg][T] chain: final start / end states
+    int *d_chcnt = nullptr;            // [4] chain: ticket, arrivals, recomputes (zero between batches)
+    unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
     int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")
     int *d_result = nullptr;           // small result scratch (16 ints)

@@ -30,10 +30,12 @@
 using namespace adlbq;
 
 
-constexpr int SEG = 256;               // chain segment: requests per wavefront (== k_req_prep's block)
+constexpr int SEG = 256;               // chain segment: requests per wavefront (one k_req_prep block)
 constexpr int SEG_BLOCKS = SEG / 64;
 constexpr int CHAIN_MAX_PASSES = 30;   // bound of the settable pass count (adlbq_set_param)
 constexpr int CHAIN_WARM = 512;        // pass-1 warm-up before each segment (T <= 8), a multiple of SEG
+constexpr int PREP_BLOCK = 256;        // k_req_prep workgroup
+static_assert(SEG % 64 == 0 && CHAIN_WARM % SEG == 0, "chain segments are whole waves of k_req_prep");
 
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
     unsigned int lo = __builtin_amdgcn_readlane((unsigned int)v, l);
@@ -41,39 +43,52 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
     return ((unsigned long long)hi << 32) | lo;
 }
 
-// One block per chain segment (blockDim == SEG): also the segment's count of
-// requests with a non-empty type set (the chain's level guess, k_chain_pass),
+// Request type vectors -> 64-bit type masks (get_type_idx, adlb.c:3476-3485;
+// -1 = any type) and per-type demand.  The workgroup's 256 request records are
+// staged through LDS with coalesced loads (rows padded to 19 words: no bank
+// conflicts).  Each wave also writes its chain segment's count of requests
+// with a non-empty type set (the chain's level guess), tmatch starts at -1,
 // and block 0 resets the chain's per-batch counters.
-__global__ __launch_bounds__(SEG) void k_req_prep(const int *__restrict__ reqs, int R, const int *__restrict__ utypes,
-                                                  int T, unsigned long long *__restrict__ mask, int *dem,
-                                                  int *__restrict__ seg_cnt, int *__restrict__ changed,
-                                                  DevCounters *ctr, int *__restrict__ tmatch,
-                                                  int *__restrict__ comp, int nseg) {
+constexpr int PREP_ROW = ADLBQ_RESERVE_INTS + 1;
+
+__global__ __launch_bounds__(PREP_BLOCK) void k_req_prep(const int *__restrict__ reqs, int R,
+                                                         const int *__restrict__ utypes, int T,
+                                                         unsigned long long *__restrict__ mask, int *dem,
+                                                         int *__restrict__ seg_cnt, DevCounters *ctr,
+                                                         int *__restrict__ tmatch) {
     __shared__ int su[ADLBQ_MAX_TYPES], sd[ADLBQ_MAX_TYPES];
-    __shared__ int scnt;
+    __shared__ int rows[PREP_BLOCK * PREP_ROW];
+    const int j0 = blockIdx.x * PREP_BLOCK, nj = min(PREP_BLOCK, R - j0);
+    const int *src = reqs + (long long)ADLBQ_RESERVE_INTS * j0;
+    for (int i = threadIdx.x; i < nj * ADLBQ_RESERVE_INTS; i += PREP_BLOCK) {
+        const int r = i / ADLBQ_RESERVE_INTS, c = i - r * ADLBQ_RESERVE_INTS;
+        rows[r * PREP_ROW + c] = src[i];
+    }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         su[t] = utypes[t];
         sd[t] = 0;
     }
-    if (threadIdx.x == 0) scnt = 0;
-    if (threadIdx.x <= CHAIN_MAX_PASSES) comp[(long long)threadIdx.x * nseg + blockIdx.x] = 0;
-    if (blockIdx.x == 0) {
-        if (threadIdx.x < CHAIN_MAX_PASSES + 2) changed[threadIdx.x] = 0;
-        if (threadIdx.x == 0) ctr->chain_rounds = 0;
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->chain_rounds = 0;
     __syncthreads();
-    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = j0 + threadIdx.x;
     bool nonempty = false;
-    if (j < R) {
+    if (threadIdx.x < nj) {
         tmatch[j] = -1;
-        const int *rt = reqs + (long long)ADLBQ_RESERVE_INTS * j + 2;
+        const int *rt = rows + threadIdx.x * PREP_ROW + 2;
         unsigned long long m = 0;
         bool wild = false;
+#pragma unroll
         for (int i = 0; i < NREQ; i++) {
-            int v = rt[i];
-            if (v == -1) { wild = true; continue; }
+            const int v = rt[i];
+            if (v == -1) {
+                wild = true;
+                continue;
+            }
             for (int t = 0; t < T; t++)
-                if (su[t] == v) { m |= 1ull << t; break; }  // get_type_idx: first declared match
+                if (su[t] == v) {  // get_type_idx: first declared match
+                    m |= 1ull << t;
+                    break;
+                }
         }
         if (wild) m = T >= 64 ? ~0ull : ((1ull << T) - 1);
         mask[j] = m;
@@ -81,9 +96,8 @@ __global__ __launch_bounds__(SEG) void k_req_prep(const int *__restrict__ reqs, 
         for (unsigned long long b = m; b; b &= b - 1) atomicAdd(&sd[__ffsll((long long)b) - 1], 1);
     }
     const unsigned long long nz = __ballot(nonempty);
-    if ((threadIdx.x & 63) == 0 && nz) atomicAdd(&scnt, __popcll(nz));
+    if ((threadIdx.x & 63) == 0 && j < R) seg_cnt[j >> 6] = __popcll(nz);  // per 64 requests
     __syncthreads();
-    if (threadIdx.x == 0) seg_cnt[blockIdx.x] = scnt;
     for (int t = threadIdx.x; t < T; t += blockDim.x)
         if (sd[t]) atomicAdd(&dem[t], sd[t]);
 }
@@ -527,7 +541,7 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
                         const long long slot =
                             ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
                         tmatch[jj] = (int)slot;
-                        atomicSub(&seg_cnt[jj / SEG], 1);
+                        atomicSub(&seg_cnt[jj >> 6], 1);
                         // taken for this rank's later Reserves (this block owns the bucket)
                         st_agent(reinterpret_cast<int *>(meta + slot), (int)(meta[slot] | M_PINNED));
                     }
@@ -619,14 +633,15 @@ struct ChainArgs {
     const unsigned long long *mask;  // [R] type masks (0: no untargeted choice)
     const int *tmatch;               // [R] slot matched in the targeted phase, or -1
     int R, T, nseg, passes, warm;    // warm: requests replayed before a segment in pass 1
+    unsigned int epoch;              // this batch's flag value (never 0)
     const int *candoff, *candlen;    // [T]
     const unsigned int *crank;       // packed ranks, per type ascending
     int *umatch;                     // [R] out: candidate index or -1
     const int *seg_cnt;              // [nseg] requests of the segment that may take an untargeted unit
-    int *E;                          // [passes + 1][nseg][T] end state of segment s computed in pass k
-    int *comp;                       // [passes + 1][nseg] segment s was computed in pass k
-    int *Sprev;                      // [nseg][T] start of each segment's last computation
-    int *changed;                    // [CHAIN_MAX_PASSES + 2] segments computed per pass
+    int *E;                          // [passes + 1][nseg][T] end state of segment s after pass k
+    int *flags;                      // [passes + 1][nseg] == epoch once E[k][s] is published
+    int *Sf, *Ef;                    // [nseg][T] final start / end of each segment
+    int *counters;                   // [3] segment ticket, arrivals, pass >= 2 recomputes
     DevCounters *ctr;
 };
 
@@ -707,23 +722,29 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
 #pragma unroll
         for (int i = 0; i < NI; i++)
             if (i * 64 < WL) win[q * WL + i * 64 + lane] = wv[q][i];
-    unsigned long long m_nx = jb + lane < j1 ? a.mask[jb + lane] : 0ull;
-    int t_nx = jb + lane < j1 ? a.tmatch[jb + lane] : 0;
+    // every block's inputs up front (one wait, not one per block)
+    constexpr int NRB = (SEG + CHAIN_WARM) / 64;
+    unsigned long long mk[NRB];
+#pragma unroll
+    for (int i = 0; i < NRB; i++) {
+        const int j = jb + i * 64 + lane;
+        mk[i] = 0ull;
+        if (j < j1 && a.tmatch[j] < 0) mk[i] = a.mask[j];
+    }
     // one wave owns win: its LDS ops complete in order, only the compiler must not reorder
     __builtin_amdgcn_wave_barrier();
     my_rec = my_start;
-    for (int b0 = jb; b0 < j1; b0 += 64) {
+#pragma unroll
+    for (int bi = 0; bi < NRB; bi++) {
+        const int b0 = jb + bi * 64;
+        if (b0 >= j1) break;
         if (b0 == j0) {
 #pragma unroll
             for (int q = 0; q < TB; q++)
                 if (lane == q) my_rec = st[q] + c0[q];
         }
         const int j = b0 + lane;
-        const unsigned long long m = t_nx < 0 ? m_nx : 0ull;
-        if (b0 + 64 < j1) {  // next block's inputs, in flight during this block
-            m_nx = j + 64 < j1 ? a.mask[j + 64] : 0ull;
-            t_nx = j + 64 < j1 ? a.tmatch[j + 64] : 0;
-        }
+        const unsigned long long m = mk[bi];
         bool have[TB];
 #pragma unroll
         for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
@@ -840,110 +861,128 @@ __device__ __forceinline__ int seg_solve(const ChainArgs &a, int s, int jb, int 
     }
 }
 
-// End state of segment s as last computed in a pass <= k.
-__device__ __forceinline__ int latest_end(const ChainArgs &a, int s, int k) {
-    while (k > 1 && !a.comp[(long long)k * a.nseg + s]) k--;
-    return threadIdx.x < a.T ? a.E[((long long)k * a.nseg + s) * a.T + threadIdx.x] : 0;
+// Inter-workgroup hand-off of one segment state (T <= 64 ints), following the
+// write-through protocol of MI355X_MICROARCH.md (inter-workgroup visibility):
+// sc1 stores, drained, then an agent-scope flag store by one lane; the reader
+// polls that flag relaxed and reads the payload with sc1 loads.
+__device__ __forceinline__ void publish_state(int *dst, int *flag, unsigned int epoch, int v, int T) {
+    if (threadIdx.x < T) __hip_atomic_store(dst + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) __hip_atomic_store(flag, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Pass k of the segment iteration (k = 1 .. passes), one wavefront per segment.
-template <int TB>
-__global__ __launch_bounds__(64) void k_chain_pass(ChainArgs a, int k) {
-    extern __shared__ unsigned int win[];
-    const int s = blockIdx.x, lane = threadIdx.x, T = a.T;
-    if (k > 1 && a.changed[k - 1] == 0) return;  // pass k-1 found the fixed point
-    int my_start = 0, jb = s * SEG;
-    if (k == 1) {
-        jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
-        int J = 0;                      // requests before jb that take an untargeted unit
-        for (int q = lane; q < jb / SEG; q += 64) J += a.seg_cnt[q];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
-        my_start = level_guess<(TB <= 8 ? TB : 8)>(a, J);
-    } else {
-        if (s > 0) my_start = latest_end(a, s - 1, k - 1);
-        if (!__ballot(lane < T && my_start != a.Sprev[s * T + lane])) return;  // start unchanged
-    }
-    int rounds = 0, my_rec;
-    const int my_end = seg_solve<TB>(a, s, jb, my_start, win, my_rec, rounds);
-    if (lane < T) {
-        a.E[((long long)k * a.nseg + s) * T + lane] = my_end;
-        a.Sprev[s * T + lane] = my_rec;
-    }
-    if (lane == 0) {
-        a.comp[(long long)k * a.nseg + s] = 1;
-        atomicAdd(&a.changed[k], 1);
-        atomicAdd(&a.ctr->chain_rounds, rounds);
-    }
-}
-
-// After the passes: every segment's recorded start is compared, in parallel,
-// with its predecessor's recorded end (the check of one more pass).  All equal
-// is the fixed point.  Otherwise wave 0 walks the segments in order from the
-// first mismatch, whose start is exact: a segment whose start equals its last
-// computation's stands, and so does every later one up to the next mismatch
-// (found 64 segments at a time); the others are recomputed.
-__device__ __forceinline__ bool seg_mismatch(const ChainArgs &a, int q) {
-    int k = a.passes;
-    while (k > 1 && !a.comp[(long long)k * a.nseg + q - 1]) k--;
-    const int *e = a.E + ((long long)k * a.nseg + q - 1) * a.T;
-    bool bad = false;
-    for (int t = 0; t < a.T; t++) bad |= e[t] != a.Sprev[q * a.T + t];
-    return bad;
-}
-
-template <int TB>
-__global__ __launch_bounds__(256) void k_chain_fix(ChainArgs a) {
-    extern __shared__ unsigned int win[];
-    __shared__ int first_bad;
-    const int lane = threadIdx.x & 63, T = a.T, P = a.passes;
-    if (threadIdx.x == 0) first_bad = a.nseg;
-    __syncthreads();
-    int mine = a.nseg;
-    if (a.changed[P] > 0)  // a pass that recomputed nothing is already the fixed point
-        for (int q = 1 + threadIdx.x; q < a.nseg; q += blockDim.x)
-            if (seg_mismatch(a, q)) {
-                mine = q;
+// Wait (bounded) for a flag; false on timeout.  Uniform over the wave.
+__device__ __forceinline__ bool wait_flag(const int *flag, unsigned int epoch) {
+    int ok = 0;
+    if (threadIdx.x == 0) {
+        for (int spin = 0; spin < (1 << 22); spin++) {
+            if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)epoch) {
+                ok = 1;
                 break;
             }
-    if (mine < a.nseg) atomicMin(&first_bad, mine);
-    __syncthreads();
-    if (threadIdx.x >= 64) return;
-    int used = 0, recomputed = 0;
-    for (int k = 1; k <= P; k++) {
-        used += a.changed[k] > 0;
-        recomputed += a.changed[k];
-    }
-    if (lane == 0) {
-        a.ctr->chain_passes = used;
-        a.ctr->chain_recomputed = recomputed;
-        a.ctr->chain_fallback = 0;
-    }
-    int s = first_bad;
-    if (s >= a.nseg) return;
-    int st = latest_end(a, s - 1, P), rounds = 0, redo = 0;
-    while (s < a.nseg) {
-        if (!__ballot(lane < T && st != a.Sprev[s * T + lane])) {
-            // s stands; jump to the next recorded mismatch
-            int nxt = a.nseg;
-            for (int c0 = s + 1; c0 < a.nseg && nxt == a.nseg; c0 += 64) {
-                const int q = c0 + lane;
-                const unsigned long long bb = __ballot(q < a.nseg && seg_mismatch(a, q));
-                if (bb) nxt = c0 + __ffsll((long long)bb) - 1;
-            }
-            if (nxt >= a.nseg) break;
-            s = nxt;
-            st = latest_end(a, s - 1, P);
+            __builtin_amdgcn_s_sleep(1);
         }
-        int my_rec;
-        st = seg_solve<TB>(a, s, s * SEG, st, win, my_rec, rounds);
-        __builtin_amdgcn_wave_barrier();  // win is refilled by the next recomputed segment
-        redo++;
-        s++;
+    }
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+__device__ __forceinline__ int load_state(const int *src, int T) {
+    return threadIdx.x < T ? __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+}
+
+// The whole ordered choice in one launch, one wavefront per segment.
+//   pass 1: every segment from its level guess, after a warm-up replay;
+//   pass k = 2 .. passes: segment s waits for segment s-1's pass k-1 end state
+//     and recomputes only if it differs from its own start (segments are taken
+//     in order from a ticket, so the predecessor is always held by a running
+//     wavefront and the wait cannot deadlock; a timed-out wait skips the pass);
+//   the last wavefront to finish checks every segment's final start against
+//     its predecessor's final end.  All equal is the fixed point, i.e. the
+//     sequential result (segment 0 starts from 0; induction).  Otherwise it
+//     walks from the first mismatch, whose start is exact, recomputing the
+//     segments whose start differs and skipping the runs that stand.
+template <int TB>
+__global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
+    extern __shared__ unsigned int win[];
+    const int lane = threadIdx.x, T = a.T, K = a.passes, nseg = a.nseg;
+    int tk = 0;
+    if (lane == 0) tk = atomicAdd(&a.counters[0], 1);
+    const int s = __builtin_amdgcn_readfirstlane(tk);
+    int rounds = 0, recomputed = 0;
+    // pass 1
+    const int jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
+    int J = 0;                                // requests before jb that take an untargeted unit
+    for (int q = lane; q < (jb >> 6); q += 64) J += a.seg_cnt[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
+    int cur_start, cur_end = seg_solve<TB>(a, s, jb, level_guess<(TB <= 8 ? TB : 8)>(a, J), win, cur_start, rounds);
+    publish_state(a.E + ((long long)1 * nseg + s) * T, a.flags + (long long)1 * nseg + s, a.epoch, cur_end, T);
+    for (int k = 2; k <= K; k++) {
+        if (s > 0 && wait_flag(a.flags + (long long)(k - 1) * nseg + s - 1, a.epoch)) {
+            const int pe = load_state(a.E + ((long long)(k - 1) * nseg + s - 1) * T, T);
+            if (__ballot(lane < T && pe != cur_start)) {
+                int rec;
+                __builtin_amdgcn_wave_barrier();  // win is refilled
+                cur_end = seg_solve<TB>(a, s, s * SEG, pe, win, rec, rounds);
+                cur_start = pe;
+                recomputed++;
+            }
+        }
+        publish_state(a.E + ((long long)k * nseg + s) * T, a.flags + (long long)k * nseg + s, a.epoch, cur_end, T);
+    }
+    // final states, then arrive
+    if (lane < T) {
+        __hip_atomic_store(a.Sf + s * T + lane, cur_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.Ef + s * T + lane, cur_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) {
+        if (recomputed) atomicAdd(&a.counters[2], recomputed);
+        atomicAdd(&a.ctr->chain_rounds, rounds);
+        last = atomicAdd(&a.counters[1], 1) == nseg - 1;
+    }
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    // ---- the last wavefront: global fixed-point check, then the walk if needed
+    auto bad = [&](int q) {  // segment q's final start differs from segment q-1's final end
+        bool b = false;
+        for (int t = 0; t < T; t++)
+            b |= __hip_atomic_load(a.Sf + q * T + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                 __hip_atomic_load(a.Ef + (q - 1) * T + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return b;
+    };
+    auto next_bad = [&](int from) {
+        for (int c0 = from; c0 < nseg; c0 += 64) {
+            const int q = c0 + lane;
+            const unsigned long long bb = __ballot(q >= 1 && q < nseg && bad(q));
+            if (bb) return c0 + __ffsll((long long)bb) - 1;
+        }
+        return nseg;
+    };
+    int redo = 0, q = next_bad(1);
+    if (q < nseg) {
+        int st = load_state(a.Ef + (q - 1) * T, T);
+        while (q < nseg) {
+            if (__ballot(lane < T && st != load_state(a.Sf + q * T, T))) {
+                int rec;
+                __builtin_amdgcn_wave_barrier();
+                st = seg_solve<TB>(a, q, q * SEG, st, win, rec, rounds);
+                redo++;
+                q++;
+            } else {  // q stands, and so does every segment up to the next recorded mismatch
+                q = next_bad(q + 1);
+                if (q < nseg) st = load_state(a.Ef + (q - 1) * T, T);
+            }
+        }
     }
     if (lane == 0) {
+        a.ctr->chain_passes = K;
+        a.ctr->chain_recomputed = __hip_atomic_load(a.counters + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         a.ctr->chain_fallback = redo;
         atomicAdd(&a.ctr->chain_rounds, rounds);
+        a.counters[0] = 0;  // for the next batch (kernel boundary in between)
+        a.counters[1] = 0;
+        a.counters[2] = 0;
     }
 }
 
@@ -1091,7 +1130,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
     void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
-                  h->d_seg_cnt, h->d_chE, h->d_chS, h->d_chchg, h->d_chcomp};
+                  h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
@@ -1100,11 +1139,14 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_reqbuf, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
     const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
-    AQ_HIP(hipMalloc((void **)&h->d_seg_cnt, sizeof(int) * nseg));
+    AQ_HIP(hipMalloc((void **)&h->d_seg_cnt, sizeof(int) * ((nc + 63) / 64)));
     AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chcomp, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));
-    AQ_HIP(hipMalloc((void **)&h->d_chS, sizeof(int) * nseg * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chchg, sizeof(int) * (CHAIN_MAX_PASSES + 2)));
+    AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));
+    AQ_HIP(hipMemset(h->d_chflag, 0, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));  // epochs start at 1
+    AQ_HIP(hipMalloc((void **)&h->d_chSf, sizeof(int) * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chEf, sizeof(int) * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(int) * 4));
+    AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(int) * 4));  // the chain's last wavefront re-zeroes them
     h->cap_req = nc;
     return ADLBQ_OK;
 }
@@ -1154,9 +1196,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipEvent_t ev;
 
     stage_begin(h, "prep", &ev);
-    k_req_prep<<<(R + SEG - 1) / SEG, SEG, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt,
-                                                 h->d_chchg, h->d_ctr, h->d_tmatch, h->d_chcomp,
-                                                 (R + SEG - 1) / SEG);
+    k_req_prep<<<(R + PREP_BLOCK - 1) / PREP_BLOCK, PREP_BLOCK, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask,
+                                                                   h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch);
     stage_end(h, "prep", ev);
 
     if (np > 0 && T > 0) {
@@ -1202,17 +1243,15 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     stage_begin(h, "chain", &ev);
     {
         const int nseg = (R + SEG - 1) / SEG;
-        const int P = h->chain_passes > 0 ? h->chain_passes : (T <= 8 ? 2 : 8);
+        const int K = h->chain_passes > 0 ? h->chain_passes : (T <= 8 ? 3 : 8);
         const int warm = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
-        ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, P, warm, h->d_candoff, h->d_candlen, h->d_crank,
-                     h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chcomp, h->d_chS, h->d_chchg, h->d_ctr};
-        auto run = [&](auto kpass, auto kfix, size_t lds) {
-            for (int k = 1; k <= P; k++) kpass<<<nseg, 64, lds, s>>>(ca, k);
-            kfix<<<1, 256, lds, s>>>(ca);
-        };
-        if (T <= 4) run(k_chain_pass<4>, k_chain_fix<4>, sizeof(unsigned int) * 4 * (SEG + std::max(warm, 0)));
-        else if (T <= 8) run(k_chain_pass<8>, k_chain_fix<8>, sizeof(unsigned int) * 8 * (SEG + std::max(warm, 0)));
-        else run(k_chain_pass<64>, k_chain_fix<64>, sizeof(unsigned int) * T * SEG);
+        if (++h->chain_epoch == 0) h->chain_epoch = 1;
+        ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, K, warm, h->chain_epoch, h->d_candoff, h->d_candlen,
+                     h->d_crank, h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf,
+                     h->d_chcnt, h->d_ctr};
+        if (T <= 4) k_chain<4><<<nseg, 64, sizeof(unsigned int) * 4 * (SEG + warm), s>>>(ca);
+        else if (T <= 8) k_chain<8><<<nseg, 64, sizeof(unsigned int) * 8 * (SEG + warm), s>>>(ca);
+        else k_chain<64><<<nseg, 64, sizeof(unsigned int) * T * SEG, s>>>(ca);
     }
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);
