@@ -368,11 +368,12 @@ __global__ __launch_bounds__(256) void k_select_open(
         const int i = i0 + lane;
         const unsigned int e = i < n ? list[i] : 0u;
         const int col = (int)(e >> 12), so = (int)(e & (PAGE - 1));
-        int pr = 0, sq = 0;
-        if (i < n) {
-            pr = prio[base + so];
-            sq = seqa[base + so];
-        }
+        // key order = (prio desc, position in the open bucket asc): the bucket
+        // holds its units in wqseqno order, so this is the reference's order.
+        // An exact bin fixes the prio (anchor - bin); only a multi-prio bin reads it.
+        const int ct = col / NB, cb = col - ct * NB;
+        const int pr = i >= n ? 0 : cb < NBX ? (int)(sanc[ct] - cb) : prio[base + so];
+        const unsigned int bpos = ((unsigned int)p << PAGE_SHIFT) | (unsigned int)so;
         int rank = 0;
         const int jn = min(n - i0, 64);
         for (int j = 0; j < jn; j++) rank += (j < lane) & ((int)(list[i0 + j] >> 12) == col);
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(256) void k_select_open(
             const int t = col / NB, b = col - t * NB;
             if (b < sth[t] || b >= NBX || (int)r < sneed[t]) {  // exact threshold bin: its first `need` only
                 const long long at = (long long)soff[t] + binoff[col] + r;
-                ckey[at] = make_key(pr, (unsigned int)sq);
+                ckey[at] = make_key(pr, bpos);
                 cslot[at] = (int)(base + so);
             }
         }

@@ -64,7 +64,7 @@ def parse():
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
 KERNEL_OF = {"prep": "k_req_prep", "hist": "k_hist_open", "thresholds": "k_thresholds",
              "select": "k_select_open", "sort": "k_sort_types",
-             "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain_pass", "finalize": "k_finalize"}
+             "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain", "finalize": "k_finalize"}
 
 
 def _kernel_base(name: str) -> str:
