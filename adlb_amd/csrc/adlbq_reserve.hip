@@ -595,38 +595,110 @@ __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) 
 // Packed global rank of every candidate: (rank among all candidates of the
 // batch by (prio desc, wqseqno asc)) << 6 | type.  A smaller packed value is a
 // better unit, so the chain compares heads with one 32-bit min and reads the
-// winning type from the low bits.
-__global__ __launch_bounds__(256) void k_rank(int T, const int *__restrict__ candoff,
-                                              const int *__restrict__ candlen,
-                                              const unsigned long long *__restrict__ ckey,
-                                              unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
-                                              long long ncsum) {
-    __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES];
+// winning type from the low bits.  rank = position in its own list + for every
+// other type u the number of u's candidates with a better key (a lower bound).
+// The lists are sorted, so for a tile of 256 consecutive candidates of one
+// type the lower bounds in list u lie between those of the tile's first and
+// last keys: one wave finds both (32-ary searches, three probe rounds), loads
+// that stretch of list u into LDS and the tile's threads search it there.
+// The waves of a workgroup take the other types in turn.
+constexpr int RANK_TILE = 256, RANK_SPAN = 2048;
+
+__device__ __forceinline__ int lower_bound_key(const unsigned long long *L, int n, unsigned long long key) {
+    int lo = 0, hi = n;  // first position whose key is not better than `key` (L descending)
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (L[mid] > key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict__ candoff,
+                                                    const int *__restrict__ candlen,
+                                                    const unsigned long long *__restrict__ ckey,
+                                                    unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
+                                                    long long ncsum) {
+    __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
+    __shared__ unsigned long long span[4][RANK_SPAN];
+    __shared__ unsigned long long s_first, s_last;
+    __shared__ int s_a0[4], s_len[4];
     // the scan's chunk sums are consumed (k_select_open): leave them zeroed for the next batch
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < ncsum; i += (long long)gridDim.x * blockDim.x)
         csum[i] = 0;
-    for (int t = threadIdx.x; t <= T; t += blockDim.x) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int t = tid; t <= T; t += blockDim.x) {
         soff[t] = candoff[t];
         if (t < T) slen[t] = candlen[t];
     }
     __syncthreads();
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < soff[T]; i += gridDim.x * blockDim.x) {
-        int t = 0;
-        while (t + 1 < T && soff[t + 1] <= i) t++;
-        const unsigned long long key = ckey[i];
-        unsigned int g = (unsigned int)(i - soff[t]);
-        for (int u = 0; u < T; u++) {
-            if (u == t) continue;
-            const unsigned long long *L = ckey + soff[u];
-            int a = 0, b = slen[u];
-            while (a < b) {  // first position whose key is not better than `key` (lists are descending)
-                const int mid = (a + b) >> 1;
-                if (L[mid] > key) a = mid + 1;
-                else b = mid;
-            }
-            g += (unsigned int)a;
+    if (tid == 0) {
+        int acc = 0;
+        for (int t = 0; t < T; t++) {
+            stile[t] = acc;
+            acc += (slen[t] + RANK_TILE - 1) / RANK_TILE;
         }
-        crank[i] = (g << 6) | (unsigned int)t;
+        stile[T] = acc;
+    }
+    __syncthreads();
+    for (int tile = blockIdx.x; tile < stile[T]; tile += gridDim.x) {
+        int t = 0;
+        while (t + 1 < T && stile[t + 1] <= tile) t++;
+        const int i0 = (tile - stile[t]) * RANK_TILE, n = min(RANK_TILE, slen[t] - i0);
+        const unsigned long long *Lt = ckey + soff[t];
+        const unsigned long long key = tid < n ? Lt[i0 + tid] : 0ull;
+        if (tid == 0) s_first = key;
+        if (tid == n - 1) s_last = key;
+        __syncthreads();
+        const unsigned long long kf = s_first, kl = s_last;
+        unsigned int g = (unsigned int)(i0 + tid);
+        for (int r0 = 0; r0 < T; r0 += 4) {  // wave w takes type r0 + w; every wave meets every barrier
+            const int u = r0 + w;
+            int a0 = 0, len = -1;
+            if (u < T && u != t && slen[u] > 0) {
+                const unsigned long long *L = ckey + soff[u];
+                // lanes 0-31 search kf, lanes 32-63 search kl (32-ary, all probes of a round in flight)
+                const unsigned long long kk = lane < 32 ? kf : kl;
+                const int sl = lane & 31;
+                int lo = 0, hi = slen[u];
+                while (true) {
+                    const int lo_f = __builtin_amdgcn_readlane(lo, 0), hi_f = __builtin_amdgcn_readlane(hi, 0);
+                    const int lo_l = __builtin_amdgcn_readlane(lo, 32), hi_l = __builtin_amdgcn_readlane(hi, 32);
+                    if (hi_f <= lo_f && hi_l <= lo_l) break;
+                    const int step = (hi - lo + 31) >> 5;
+                    const int idx = lo + sl * step;
+                    const bool better = hi > lo && idx < hi && L[idx] > kk;
+                    const unsigned long long bal = __ballot(better);
+                    const int c = __popcll(lane < 32 ? (bal & 0xffffffffull) : (bal >> 32));
+                    if (hi > lo) {
+                        const int nlo = c == 0 ? lo : lo + (c - 1) * step + 1;
+                        const int nhi = min(hi, lo + c * step);
+                        lo = nlo;
+                        hi = step == 1 ? nlo : nhi;
+                    }
+                }
+                a0 = __builtin_amdgcn_readlane(lo, 0);
+                len = __builtin_amdgcn_readlane(lo, 32) - a0;  // the tile's lower bounds lie in [a0, a0 + len]
+                if (len <= RANK_SPAN)
+                    for (int q = lane; q < len; q += 64) span[w][q] = L[a0 + q];
+            }
+            if (lane == 0) {
+                s_a0[w] = a0;
+                s_len[w] = len;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int lq = s_len[q], aq = s_a0[q];
+                if (lq < 0 || tid >= n) continue;
+                const int lb = lq <= RANK_SPAN ? lower_bound_key(span[q], lq, key)
+                                               : lower_bound_key(ckey + soff[r0 + q] + aq, lq, key);
+                g += (unsigned int)(aq + lb);
+            }
+            __syncthreads();
+        }
+        if (tid < n) crank[soff[t] + i0 + tid] = (g << 6) | (unsigned int)t;
+        __syncthreads();
     }
 }
 
@@ -1237,7 +1309,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     if (np > 0 && T > 0) {
         stage_begin(h, "rank", &ev);
-        k_rank<<<1024, 256, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
+        k_rank<<<512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
                                     (long long)((np + CHUNK - 1) / CHUNK) * C);
         stage_end(h, "rank", ev);
     }
