@@ -36,7 +36,8 @@ constexpr int NREQ = ADLBQ_REQ_TYPES;
 
 // device-side scalar counters shared by kernels and read back lazily by the host
 struct DevCounters {
-    unsigned long long fin_ticket;  // k_finalize arrivals: parked << 32 | workgroups (reset by the last)
+    unsigned long long fin_group[8];  // k_finalize arrivals per group: parked << 32 | workgroups
+    unsigned long long fin_top;       // groups done: parked << 32 | groups (all reset by the last)
     int rq_n;          // rq slots used (== next_rqseqno - 1)
     int rq_live;       // parked entries alive
     int rq_hwm;        // rq->max_count

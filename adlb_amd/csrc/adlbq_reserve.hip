@@ -51,6 +51,7 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 // and block 0 resets the chain's per-batch counters.
 constexpr int PREP_ROW = ADLBQ_RESERVE_INTS + 1;
 
+template <int TB>  // TB >= T; TB <= 8: the user types are compared in registers
 __global__ __launch_bounds__(PREP_BLOCK) void k_req_prep(const int *__restrict__ reqs, int R,
                                                          const int *__restrict__ utypes, int T,
                                                          unsigned long long *__restrict__ mask, int *dem,
@@ -69,34 +70,56 @@ __global__ __launch_bounds__(PREP_BLOCK) void k_req_prep(const int *__restrict__
         sd[t] = 0;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) ctr->chain_rounds = 0;
+    // small T: user types in registers; a type equal to an earlier one never matches
+    // (get_type_idx returns the first declared match)
+    int ur[TB <= 8 ? TB : 1];
+    bool uok[TB <= 8 ? TB : 1];
+    if constexpr (TB <= 8) {
+#pragma unroll
+        for (int t = 0; t < TB; t++) {
+            ur[t] = t < T ? utypes[t] : 0;
+            uok[t] = t < T;
+#pragma unroll
+            for (int t2 = 0; t2 < t; t2++) uok[t] = uok[t] && ur[t2] != ur[t];
+        }
+    }
     __syncthreads();
     const int j = j0 + threadIdx.x;
-    bool nonempty = false;
+    unsigned long long m = 0;
     if (threadIdx.x < nj) {
         tmatch[j] = -1;
         const int *rt = rows + threadIdx.x * PREP_ROW + 2;
-        unsigned long long m = 0;
         bool wild = false;
 #pragma unroll
         for (int i = 0; i < NREQ; i++) {
             const int v = rt[i];
-            if (v == -1) {
-                wild = true;
-                continue;
+            wild |= v == -1;
+            if constexpr (TB <= 8) {
+#pragma unroll
+                for (int t = 0; t < TB; t++) m |= (uok[t] && v == ur[t]) ? (1ull << t) : 0ull;
+            } else {
+                if (v == -1) continue;
+                for (int t = 0; t < T; t++)
+                    if (su[t] == v) {  // get_type_idx: first declared match
+                        m |= 1ull << t;
+                        break;
+                    }
             }
-            for (int t = 0; t < T; t++)
-                if (su[t] == v) {  // get_type_idx: first declared match
-                    m |= 1ull << t;
-                    break;
-                }
         }
         if (wild) m = T >= 64 ? ~0ull : ((1ull << T) - 1);
         mask[j] = m;
-        nonempty = m != 0ull;
+    }
+    const unsigned long long nz = __ballot(m != 0ull);
+    if ((threadIdx.x & 63) == 0 && j < R) seg_cnt[j >> 6] = __popcll(nz);  // per 64 requests
+    if constexpr (TB <= 8) {  // per-type demand: one LDS add per wave and type
+#pragma unroll
+        for (int t = 0; t < TB; t++) {
+            const int c = __popcll(__ballot((m >> t) & 1ull));
+            if ((threadIdx.x & 63) == 0 && c) atomicAdd(&sd[t], c);
+        }
+    } else {
         for (unsigned long long b = m; b; b &= b - 1) atomicAdd(&sd[__ffsll((long long)b) - 1], 1);
     }
-    const unsigned long long nz = __ballot(nonempty);
-    if ((threadIdx.x & 63) == 0 && j < R) seg_cnt[j >> 6] = __popcll(nz);  // per 64 requests
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += blockDim.x)
         if (sd[t]) atomicAdd(&dem[t], sd[t]);
@@ -1171,12 +1194,22 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
         if ((threadIdx.x & 63) == 0 && pb) atomicAdd(&s_parked, __popcll(pb));
     }
     __syncthreads();
-    if (threadIdx.x == 0)
-        s_ticket = atomicAdd(&ctr->fin_ticket, ((unsigned long long)s_parked << 32) | 1ull);
+    // two-level arrival (8 groups, then one top counter) keeps every counter's
+    // atomics to about gridDim / 8; a count rides in the high half
+    if (threadIdx.x == 0) {
+        const unsigned int nb = gridDim.x, g = blockIdx.x & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
+        unsigned long long v = atomicAdd(&ctr->fin_group[g], ((unsigned long long)s_parked << 32) | 1ull);
+        s_ticket = 0;  // not last
+        if ((unsigned int)v == ng - 1u) {
+            const unsigned long long tg = (v >> 32) + (unsigned long long)s_parked;
+            const unsigned long long top = atomicAdd(&ctr->fin_top, (tg << 32) | 1ull);
+            if ((unsigned int)top == ngroups - 1u) s_ticket = (((top >> 32) + tg) << 32) | 1ull;
+        }
+    }
     __syncthreads();
-    if ((unsigned int)s_ticket != gridDim.x - 1) return;
+    if (!(s_ticket & 1ull)) return;
     // the last workgroup of the batch
-    const int total = (int)(s_ticket >> 32) + s_parked;
+    const int total = (int)(s_ticket >> 32);
     if (threadIdx.x < T) {
         dem[threadIdx.x] = 0;  // k_req_prep of the next batch accumulates into it
         const long long a = anchor_next[threadIdx.x];
@@ -1189,9 +1222,9 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
     __syncthreads();
     if (threadIdx.x == 0) {
         if (total == 0) ctr->n_parked_last = 0;
-        ctr->fin_ticket = 0;
-        *snap = *ctr;
-        __threadfence_system();
+        for (int g = 0; g < 8; g++) ctr->fin_group[g] = 0;
+        ctr->fin_top = 0;
+        *snap = *ctr;  // mapped host memory; visible to the host once the kernel has completed
     }
 }
 
@@ -1269,8 +1302,16 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipEvent_t ev;
 
     stage_begin(h, "prep", &ev);
-    k_req_prep<<<(R + PREP_BLOCK - 1) / PREP_BLOCK, PREP_BLOCK, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask,
-                                                                   h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch);
+    {
+        const int nb = (R + PREP_BLOCK - 1) / PREP_BLOCK;
+        auto prep = [&](auto kern) {
+            kern<<<nb, PREP_BLOCK, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr,
+                                           h->d_tmatch);
+        };
+        if (T <= 4) prep(k_req_prep<4>);
+        else if (T <= 8) prep(k_req_prep<8>);
+        else prep(k_req_prep<64>);
+    }
     stage_end(h, "prep", ev);
 
     if (np > 0 && T > 0) {
