@@ -1,0 +1,33 @@
+"""Per-step kernel timeline from a rocprofv3 --kernel-trace CSV directory.
+
+usage: python tools/step_timeline.py <rocprofv3 output dir>
+
+A step starts at each k_req_prep launch (the first kernel of a reserve batch);
+the last five complete steps are averaged per kernel position.  'span' is the
+first kernel start to the last kernel end of a step, 'busy' the sum of the
+kernel durations (the difference is the idle time between kernels).
+"""
+import csv
+import glob
+import sys
+
+
+def main(d):
+    f = glob.glob(d + "/**/*kernel_trace.csv", recursive=True)[0]
+    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "k_req_prep" in r["Kernel_Name"]]
+    steps = [rows[a:b] for a, b in zip(idx[-6:-1], idx[-5:])]
+    agg = {}
+    for st in steps:
+        for n, r in enumerate(st):
+            agg.setdefault((n, r["Kernel_Name"][:60]), []).append(
+                (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
+    for (n, name), v in sorted(agg.items()):
+        print(f"{n:2d} {name:60s} {sum(v) / len(v):8.2f} us")
+    spans = [(int(st[-1]["End_Timestamp"]) - int(st[0]["Start_Timestamp"])) / 1000 for st in steps]
+    busy = [sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in st) / 1000 for st in steps]
+    print(f"step span {sum(spans) / len(spans):.1f} us, busy {sum(busy) / len(busy):.1f} us")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
