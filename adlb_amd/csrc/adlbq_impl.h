@@ -130,6 +130,9 @@ struct adlbq_server {
     std::vector<int> tq;           // 4 ints per entry: app_rank, work_type, server_rank, num_stored
     int *d_tq = nullptr; int cap_tq = 0; bool tq_dirty = true;
 
+    // ---- put staging
+    void *d_putrec = nullptr; int *d_putout = nullptr; int cap_put = 0;
+
     // ---- reserve-batch scratch
     int cap_req = 0;
     unsigned long long *d_mask = nullptr;
@@ -178,7 +181,8 @@ int hip_fail(hipError_t e, const char *where);
 int ensure_req_capacity(adlbq_server *h, int n);
 int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
-void tighten_rq_bound(adlbq_server *h, bool wait_oldest);  // newest landed batch snapshot -> rq_n_upper
+void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
+long long rq_live_upper(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);

@@ -75,6 +75,20 @@ void tighten_rq_bound(adlbq_server *h, bool wait_oldest) {
     }
 }
 
+// Upper bound of the parked Reserves alive now, from the newest landed batch
+// snapshot plus every Reserve launched after it (no synchronisation).
+long long rq_live_upper(adlbq_server *h) {
+    const int N = adlbq_server::NSNAP;
+    for (int k = 1; k <= N; k++) {
+        const int i = (h->snap_next - k + N) % N;
+        if (!h->snap_at[i]) continue;
+        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
+        if (h->snap_at[i] != h->launched_reserves) return (long long)h->h_snap[i].rq_live + (h->launched_reserves - h->snap_at[i]);
+        return h->h_snap[i].rq_live;
+    }
+    return LLONG_MAX;  // nothing landed yet: assume a match is possible
+}
+
 int ensure_rq_capacity(adlbq_server *h, int extra) {
     long long need = (h->ctr_stale ? h->rq_n_upper : (long long)h->ctr.rq_n) + extra;
     if (need <= h->rq_cap) return ADLBQ_OK;
@@ -583,7 +597,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
-                    h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt};
+                    h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -662,21 +676,29 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         if ((rc = grow(&h->d_seq2slot, h->cap_seq, nc, h->stream, 0xff))) return rc;
         h->cap_seq = nc;
     }
-    PutRec *d_rec = nullptr;
-    int *d_out = nullptr;
-    AQ_HIP(hipMalloc((void **)&d_rec, sizeof(PutRec) * n));
+    // persistent staging: the records go through a pageable copy (consumed
+    // before the call returns), so only a possible rq match synchronises
+    if (n > h->cap_put) {
+        AQ_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_putrec) AQ_HIP(hipFree(h->d_putrec));
+        if (h->d_putout) AQ_HIP(hipFree(h->d_putout));
+        h->cap_put = std::max(n, 2 * h->cap_put);
+        AQ_HIP(hipMalloc((void **)&h->d_putrec, sizeof(PutRec) * (size_t)h->cap_put));
+        AQ_HIP(hipMalloc((void **)&h->d_putout, sizeof(int) * 3 * (size_t)h->cap_put));
+    }
+    PutRec *d_rec = reinterpret_cast<PutRec *>(h->d_putrec);
     AQ_HIP(hipMemcpyAsync(d_rec, rec.data(), sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
     k_put_scatter<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, h->d_prio, h->d_meta, h->d_pin, h->d_seq,
                                                           h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor);
-    bool may_match = h->ctr_stale || h->ctr.rq_live > 0;
+    // a parked Reserve can only exist if the last known count, plus every
+    // Reserve launched since, is positive
+    bool may_match = h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0);
     if (may_match) {
-        AQ_HIP(hipMalloc((void **)&d_out, sizeof(int) * 3 * n));
         k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
-                                             h->d_meta, h->d_pin, d_out);
-        AQ_HIP(hipMemcpyAsync(out3, d_out, sizeof(int) * 3 * n, hipMemcpyDeviceToHost, h->stream));
+                                             h->d_meta, h->d_pin, h->d_putout);
+        AQ_HIP(hipMemcpyAsync(out3, h->d_putout, sizeof(int) * 3 * n, hipMemcpyDeviceToHost, h->stream));
         AQ_HIP(hipGetLastError());
         if ((rc = refresh_counters(h))) return rc;
-        AQ_HIP(hipFree(d_out));
     } else {
         for (int i = 0; i < n; i++) {
             out3[3 * i] = rec[i].seq;
@@ -684,9 +706,7 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
             out3[3 * i + 2] = -1;
         }
         AQ_HIP(hipGetLastError());
-        AQ_HIP(hipStreamSynchronize(h->stream));
     }
-    AQ_HIP(hipFree(d_rec));
     return ADLBQ_OK;
 }
 
