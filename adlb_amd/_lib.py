@@ -33,6 +33,11 @@ SIGNATURES = {
     "adlbq_rfr_done": (c_int, [P, c_int, c_int]),
     "adlbq_tq_add": (c_int, [P, c_int, c_int, c_int]),
     "adlbq_rq_delete": (c_int, [P, c_int, P]),
+    "adlbq_steal_export": (c_int, [P, c_int, P, P, P]),
+    "adlbq_rq_export": (c_int, [P, c_int, P, P]),
+    "adlbq_steal_merge": (c_int, [c_int, c_int, P, c_int, P, P, P, c_int, P, P, P]),
+    "adlbq_grant_batch": (c_int, [P, c_int, P, P]),
+    "adlbq_rq_delete_batch": (c_int, [P, c_int, P, P]),
     "adlbq_push_select": (c_int, [P, c_double, P, P]),
     "adlbq_info": (c_int, [P, P, P, P]),
     "adlbq_info_type": (c_int, [P, c_int, P, P, P]),

@@ -158,6 +158,7 @@ struct adlbq_server {
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
     int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")
+    int *d_export = nullptr; long long cap_export = 0;  // adlbq_steal_export records
     int *d_result = nullptr;           // small result scratch (16 ints)
     int *h_result = nullptr;           // pinned host mirror
     long long last_scan_units = 0;

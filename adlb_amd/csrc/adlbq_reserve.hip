@@ -1228,6 +1228,50 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
     }
 }
 
+// ---------------------------------------------------------------- steal export
+// The k best available units of every type for the cross-shard merge
+// (SURVEY §8(e)): the two passes above with demand k for every type, then the
+// first min(k, candlen) entries of each candidate list (preference order) as
+// records {prio, wqseqno, work_type, len, answer_rank, common_len,
+// common_server, common_seqno} -- the fields SS_RFR_RESP carries
+// (adlb.c:1828-1840).  Block t gathers type t; the blocks also do what k_rank
+// and k_finalize do after a batch's scan: zero the chunk sums, reset the
+// demand, apply the anchors the thresholds found.
+__global__ void k_export_begin(int *dem, int T, int k) {
+    if ((int)threadIdx.x < T) dem[threadIdx.x] = k;
+}
+
+__global__ __launch_bounds__(256) void k_export_gather(int T, int k, const int *__restrict__ candoff,
+                                                       const int *__restrict__ candlen, const int *__restrict__ cslot,
+                                                       const int *__restrict__ prio, const int *__restrict__ seqa,
+                                                       const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
+                                                       int *__restrict__ recs, int *__restrict__ nrec,
+                                                       unsigned int *csum, long long ncsum, int *dem,
+                                                       long long *anchor, long long *anchor_next) {
+    const int t = blockIdx.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < ncsum;
+         i += (long long)gridDim.x * blockDim.x)
+        csum[i] = 0;
+    const int n = min(k, candlen[t]), off = candoff[t];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int slot = cslot[off + i];
+        const int4 c0 = cold0[slot], c1 = cold1[slot];
+        int4 *r = reinterpret_cast<int4 *>(recs + ((long long)t * k + i) * 8);
+        r[0] = make_int4(prio[slot], seqa[slot], c1.z, c0.y);
+        r[1] = make_int4(c0.x, c0.w, c1.x, c1.y);
+    }
+    if (threadIdx.x == 0) nrec[t] = n;
+    if (t == 0)
+        for (int u = threadIdx.x; u < T; u += blockDim.x) {
+            dem[u] = 0;
+            const long long a = anchor_next[u];
+            if (a != LLONG_MIN) {
+                anchor[u] = a;
+                anchor_next[u] = LLONG_MIN;
+            }
+        }
+}
+
 // ================================================================ host side
 namespace adlbq {
 
@@ -1290,30 +1334,13 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
     return ADLBQ_OK;
 }
 
-int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
-    int rc;
-    if ((rc = ensure_req_capacity(h, R))) return rc;
-    if ((rc = sync_tables(h))) return rc;
-    if ((rc = ensure_rq_capacity(h, R))) return rc;
+// Both passes over the open bucket for the current demand (d_dem): per-type
+// candidate lists in preference order at d_candoff / d_candlen / d_cslot.
+static int launch_scan(adlbq_server *h) {
     const int T = h->T, C = T * NB;
     const int np = (int)h->open.pages.size();
-    if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
     hipStream_t s = h->stream;
     hipEvent_t ev;
-
-    stage_begin(h, "prep", &ev);
-    {
-        const int nb = (R + PREP_BLOCK - 1) / PREP_BLOCK;
-        auto prep = [&](auto kern) {
-            kern<<<nb, PREP_BLOCK, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr,
-                                           h->d_tmatch);
-        };
-        if (T <= 4) prep(k_req_prep<4>);
-        else if (T <= 8) prep(k_req_prep<8>);
-        else prep(k_req_prep<64>);
-    }
-    stage_end(h, "prep", ev);
-
     if (np > 0 && T > 0) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
         stage_begin(h, "hist", &ev);
@@ -1339,6 +1366,34 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         AQ_HIP(hipMemsetAsync(h->d_candlen, 0, sizeof(int) * std::max(T, 1), s));
         AQ_HIP(hipMemsetAsync(h->d_candoff, 0, sizeof(int) * (std::max(T, 1) + 1), s));
     }
+    return ADLBQ_OK;
+}
+
+int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
+    int rc;
+    if ((rc = ensure_req_capacity(h, R))) return rc;
+    if ((rc = sync_tables(h))) return rc;
+    if ((rc = ensure_rq_capacity(h, R))) return rc;
+    const int T = h->T, C = T * NB;
+    const int np = (int)h->open.pages.size();
+    if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
+    hipStream_t s = h->stream;
+    hipEvent_t ev;
+
+    stage_begin(h, "prep", &ev);
+    {
+        const int nb = (R + PREP_BLOCK - 1) / PREP_BLOCK;
+        auto prep = [&](auto kern) {
+            kern<<<nb, PREP_BLOCK, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr,
+                                           h->d_tmatch);
+        };
+        if (T <= 4) prep(k_req_prep<4>);
+        else if (T <= 8) prep(k_req_prep<8>);
+        else prep(k_req_prep<64>);
+    }
+    stage_end(h, "prep", ev);
+
+    if ((rc = launch_scan(h))) return rc;
     h->last_scan_units = h->live_units - h->live_targeted;
 
     const int nb = (int)h->bucket_ranks.size();
@@ -1390,6 +1445,23 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     return ADLBQ_OK;
 }
 
+// recs8 [T][k][8] and nrec [T] land in d_out (device); navail from the column totals
+static int launch_export(adlbq_server *h, int k, int *d_out) {
+    int rc;
+    if ((rc = sync_tables(h))) return rc;
+    const int T = h->T, C = T * NB;
+    const int np = (int)h->open.pages.size();
+    if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
+    k_export_begin<<<1, 64, 0, h->stream>>>(h->d_dem, T, k);
+    if ((rc = launch_scan(h))) return rc;
+    const long long ncsum = np > 0 ? (long long)((np + CHUNK - 1) / CHUNK) * C : 0;
+    k_export_gather<<<T, 256, 0, h->stream>>>(T, k, h->d_candoff, h->d_candlen, h->d_cslot, h->d_prio, h->d_seq,
+                                              h->d_cold0, h->d_cold1, d_out, d_out + (size_t)T * k * 8, h->d_csum,
+                                              ncsum, h->d_dem, h->d_anchor, h->d_anchor_next);
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
 }  // namespace adlbq
 
 extern "C" {
@@ -1413,6 +1485,36 @@ int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int 
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
     return launch_reserve(h, n, d_reqs18, d_resp12);
+}
+
+int adlbq_steal_export(adlbq_server *h, int k, int *recs8, int *nrec, long long *navail) {
+    if (!h || k < 0 || (h->T && (!nrec || !navail || (k && !recs8)))) return fail(ADLBQ_ERR_ARG, "adlbq_steal_export");
+    if (!h->T) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    const int T = h->T;
+    const size_t n_out = (size_t)T * k * 8 + T;
+    if ((long long)n_out > h->cap_export) {
+        AQ_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_export) AQ_HIP(hipFree(h->d_export));
+        AQ_HIP(hipMalloc((void **)&h->d_export, sizeof(int) * n_out));
+        h->cap_export = (long long)n_out;
+    }
+    int rc;
+    if ((rc = launch_export(h, k, h->d_export))) return rc;
+    if (k) AQ_HIP(hipMemcpyAsync(recs8, h->d_export, sizeof(int) * (size_t)T * k * 8, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipMemcpyAsync(nrec, h->d_export + (size_t)T * k * 8, sizeof(int) * T, hipMemcpyDeviceToHost, h->stream));
+    std::vector<unsigned int> tot((size_t)T * NB, 0);
+    const bool scanned = !h->open.pages.empty();
+    if (scanned)
+        AQ_HIP(hipMemcpyAsync(tot.data(), h->d_coltot, sizeof(unsigned int) * tot.size(), hipMemcpyDeviceToHost,
+                              h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    for (int t = 0; t < T; t++) {
+        long long a = 0;
+        for (int b = 0; scanned && b < NB; b++) a += tot[(size_t)t * NB + b];
+        navail[t] = a;
+    }
+    return ADLBQ_OK;
 }
 
 }  // extern "C"

@@ -148,6 +148,42 @@ class Server:
                    "adlbq_push_select")
         return c.value, s.value
 
+    # -- steal round (adlb_amd/shards.py) ----------------------------
+    def steal_export(self, k: int):
+        """Per type, the k best available units (SS_RFR donor side for every request
+        at once): (recs [T, k, 8] {prio, wqseqno, type, len, answer, common_len,
+        common_server, common_seqno}, nrec [T], navail [T] int64)."""
+        recs = np.empty((max(self.T, 1), int(k), 8), dtype=np.int32)
+        nrec = np.empty(max(self.T, 1), dtype=np.int32)
+        navail = np.empty(max(self.T, 1), dtype=np.int64)
+        _lib.check(self.lib.adlbq_steal_export(self.h, int(k), _ptr(recs), _ptr(nrec), _ptr(navail)),
+                   "adlbq_steal_export")
+        return recs[: self.T], nrec[: self.T], navail[: self.T]
+
+    def rq_export(self) -> np.ndarray:
+        """Live parked Reserves in rqseqno order: (n, 18) {rqseqno, world_rank, req_types[16]}."""
+        cap = 1024
+        while True:
+            out = np.empty((cap, 18), dtype=np.int32)
+            c = ctypes.c_int()
+            _lib.check(self.lib.adlbq_rq_export(self.h, cap, _ptr(out), ctypes.byref(c)), "adlbq_rq_export")
+            if c.value <= cap:
+                return out[: c.value].copy()
+            cap = c.value
+
+    def grant_batch(self, pairs2) -> np.ndarray:
+        """Pin (rank, wqseqno) pairs the merge granted (adlb.c:1820-1824) -> found[n]."""
+        p = np.ascontiguousarray(np.asarray(pairs2, dtype=np.int32).reshape(-1, 2))
+        found = np.empty(p.shape[0], dtype=np.int32)
+        _lib.check(self.lib.adlbq_grant_batch(self.h, p.shape[0], _ptr(p), _ptr(found)), "adlbq_grant_batch")
+        return found
+
+    def rq_delete_batch(self, rqseqnos) -> np.ndarray:
+        q = np.ascontiguousarray(np.asarray(rqseqnos, dtype=np.int32).ravel())
+        found = np.empty(q.size, dtype=np.int32)
+        _lib.check(self.lib.adlbq_rq_delete_batch(self.h, q.size, _ptr(q), _ptr(found)), "adlbq_rq_delete_batch")
+        return found
+
     # -- info --------------------------------------------------------------------
     def info(self):
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

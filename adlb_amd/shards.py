@@ -12,11 +12,24 @@ output (adlb.c:3581-3593).  Donor selection (find_cand_rank_with_worktype,
 adlb.c:3487-3534) then runs on each shard against that table
 (Server.check_remote).
 
+The steal round (`steal_round`) replaces the SS_RFR /
+SS_RFR_RESP round trips (adlb.c:1280-1308, 1802-1933): every shard exports its
+top-k available units per type and its parked Reserves, one all-gather moves
+them to every process, and every process runs the same deterministic merge
+(adlbq_steal_merge in the library: the round trips serialised in (shard,
+rqseqno) order against the donors' current heads).  Donors then pin what the
+merge granted and requesters answer their apps and drop the rq entries -- no
+further exchange, since every process computed the same grants.
+
 `reduce_step_timing` is the bench's max-over-ranks / sum-over-ranks reduction.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
+
+from . import _lib
 
 
 def shard_seed(base: int, rank: int) -> int:
@@ -67,3 +80,145 @@ def reduce_step_timing(elapsed_s: float, matched: int, group=None):
     m = torch.tensor([int(matched)], dtype=torch.int64, device=dev)
     dist.all_reduce(m, op=dist.ReduceOp.SUM, group=group)
     return float(t.item()), int(m.item())
+
+
+# ------------------------------------------------------------------ steal round
+def steal_merge(user_types, k: int, recs, nrec, navail, reqs19):
+    """The merge over S shards (adlbq_steal_merge): recs [S, T, k, 8], nrec [S, T],
+    navail [S, T], reqs19 (n, 19) {shard, rqseqno, rank, types[16]} in (shard,
+    rqseqno) order -> (out (n, 3) {donor shard, type index, record index} or -1,
+    number of requests decided)."""
+    lib = _lib.load()
+    ut = np.ascontiguousarray(np.asarray(user_types, dtype=np.int32))
+    recs = np.ascontiguousarray(np.asarray(recs, dtype=np.int32))
+    S, T = recs.shape[0], ut.size
+    nrec = np.ascontiguousarray(np.asarray(nrec, dtype=np.int32).reshape(S, T))
+    navail = np.ascontiguousarray(np.asarray(navail, dtype=np.int64).reshape(S, T))
+    q = np.ascontiguousarray(np.asarray(reqs19, dtype=np.int32).reshape(-1, 19))
+    out = np.empty((q.shape[0], 3), dtype=np.int32)
+    nd = ctypes.c_int()
+    _lib.check(lib.adlbq_steal_merge(S, T, ut.ctypes.data, int(k), recs.ctypes.data, nrec.ctypes.data,
+                                     navail.ctypes.data, q.shape[0], q.ctypes.data, out.ctypes.data,
+                                     ctypes.byref(nd)), "adlbq_steal_merge")
+    return out, nd.value
+
+
+def _sort_reqs(reqs19: np.ndarray) -> np.ndarray:
+    if reqs19.shape[0] == 0:
+        return reqs19
+    return reqs19[np.lexsort((reqs19[:, 1], reqs19[:, 0]))]
+
+
+def settle(local, num_app_ranks: int, user_types, k: int, recs, nrec, navail, reqs19):
+    """Run the merge on the gathered exports and apply this process's side of it.
+
+    local: {shard index: server} for the shards this process owns (objects with
+    grant_batch and rq_delete_batch, e.g. adlb_amd.server.Server).
+    Returns (responses (m, 15) {shard, rqseqno, rank, TA_RESERVE_RESP[12]} for
+    the Reserves of local shards that were settled -- the reply
+    SS_RFR_RESP sends the app, adlb.c:1885-1898, with the donor's world rank --,
+    the number of Reserves the merge decided and the number it settled, both
+    over all shards: the same on every process)."""
+    reqs19 = _sort_reqs(np.asarray(reqs19, dtype=np.int32).reshape(-1, 19))
+    out, nd = steal_merge(user_types, k, recs, nrec, navail, reqs19)
+    won = np.nonzero(out[:nd, 0] >= 0)[0]
+    d, t, i = out[won, 0], out[won, 1], out[won, 2]
+    r = recs[d, t, i]                                  # [m, 8] records of the granted units
+    q = reqs19[won]
+    for s, srv in local.items():
+        g = np.nonzero(d == s)[0]
+        if g.size:
+            found = srv.grant_batch(np.stack([q[g, 2], r[g, 1]], axis=1))
+            if not found.all():
+                raise RuntimeError(f"shard {s}: {int((found == 0).sum())} granted units were no longer available")
+    mine = np.isin(q[:, 0], np.fromiter(local.keys(), dtype=np.int32, count=len(local)))
+    resp = np.empty((int(mine.sum()), 15), dtype=np.int32)
+    qm, rm, dm = q[mine], r[mine], d[mine]
+    resp[:, 0:3] = qm[:, 0:3]
+    resp[:, 3] = 1                                     # SUCCESS
+    resp[:, 4] = rm[:, 2]                              # work_type
+    resp[:, 5] = rm[:, 0]                              # work_prio
+    resp[:, 6] = rm[:, 3]                              # work_len
+    resp[:, 7] = rm[:, 4]                              # answer_rank
+    resp[:, 8] = rm[:, 1]                              # wqseqno
+    resp[:, 9] = num_app_ranks + dm                    # donor server's world rank
+    resp[:, 10:13] = rm[:, 5:8]                        # common_len, common_server, common_seqno
+    resp[:, 13:15] = -1
+    for s, srv in local.items():
+        g = np.nonzero(resp[:, 0] == s)[0]
+        if g.size:
+            found = srv.rq_delete_batch(resp[g, 1])
+            if not found.all():
+                raise RuntimeError(f"shard {s}: settled Reserves were no longer parked")
+    return resp, nd, int(won.size)
+
+
+def _export(srv, k: int):
+    recs, nrec, navail = srv.steal_export(k)
+    rq = srv.rq_export()
+    reqs = np.empty((rq.shape[0], 19), dtype=np.int32)
+    reqs[:, 0] = srv.my_server_idx
+    reqs[:, 1:] = rq
+    return recs, nrec, navail, reqs
+
+
+def steal_round_local(servers, k: int):
+    """The steal round among shards held by one process (no collective)."""
+    S = servers[0].num_servers
+    T = servers[0].T
+    recs = np.zeros((S, T, k, 8), np.int32)
+    nrec = np.zeros((S, T), np.int32)
+    navail = np.zeros((S, T), np.int64)
+    reqs = []
+    for srv in servers:
+        a, b, c, q = _export(srv, k)
+        recs[srv.my_server_idx], nrec[srv.my_server_idx], navail[srv.my_server_idx] = a, b, c
+        reqs.append(q)
+    local = {srv.my_server_idx: srv for srv in servers}
+    return settle(local, servers[0].num_app_ranks, servers[0].user_types, k, recs, nrec, navail,
+                  np.concatenate(reqs) if reqs else np.zeros((0, 19), np.int32))
+
+
+def steal_round(servers, k: int, group=None):
+    """The steal round across processes: each process holds `servers` (its
+    shards); one all-gather of sizes and one of the padded exports (RCCL over
+    xGMI on GPU ranks, gloo on CPU), then the same merge everywhere."""
+    import torch
+    import torch.distributed as dist
+    S, T = servers[0].num_servers, servers[0].T
+    dev = _dev_of(dist.get_backend(group))
+    world = dist.get_world_size(group)
+    # one int32 blob per process: per shard [idx, nrec[T], navail lo/hi [2T], recs[T*k*8]], then reqs
+    per = 1 + 3 * T + T * k * 8
+    parts, reqs = [], []
+    for srv in servers:
+        a, b, c, q = _export(srv, k)
+        nav = np.ascontiguousarray(c.astype(np.int64)).view(np.int32)
+        parts.append(np.concatenate([[srv.my_server_idx], b, nav, a.ravel()]).astype(np.int32))
+        reqs.append(q.ravel())
+    blob = np.concatenate([[len(servers)], *parts, *reqs]).astype(np.int32)
+    n = torch.tensor([blob.size], dtype=torch.int64, device=dev)
+    sizes = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    cap = int(max(int(x.item()) for x in sizes))
+    mine = torch.zeros(cap, dtype=torch.int32, device=dev)
+    mine[: blob.size] = torch.from_numpy(blob).to(dev)
+    got = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine, group=group)
+    recs = np.zeros((S, T, k, 8), np.int32)
+    nrec = np.zeros((S, T), np.int32)
+    navail = np.zeros((S, T), np.int64)
+    allreqs = []
+    for g, sz in zip(got, sizes):
+        b = g.cpu().numpy()[: int(sz.item())]
+        ns, off = int(b[0]), 1
+        for _ in range(ns):
+            idx = int(b[off])
+            nrec[idx] = b[off + 1: off + 1 + T]
+            navail[idx] = b[off + 1 + T: off + 1 + 3 * T].copy().view(np.int64)
+            recs[idx] = b[off + 1 + 3 * T: off + per].reshape(T, k, 8)
+            off += per
+        allreqs.append(b[off:].reshape(-1, 19))
+    local = {srv.my_server_idx: srv for srv in servers}
+    return settle(local, servers[0].num_app_ranks, servers[0].user_types, k, recs, nrec, navail,
+                  np.concatenate(allreqs))

@@ -172,6 +172,36 @@ def config4(n_units=10_000_000, n_types=32, n_reserves=65_536, n_ranks=1024, see
                     name="config4", meta=dict(seed=seed))
 
 
+def config3_shard(shard, n_shards=64, n_units=1_562_500, n_types=4, n_reserves=8192, seed=3, prio_hi=1024,
+                  p_remote=0.1, hang=1) -> Workload:
+    """Config 3: one server shard of a queue sharded over n_shards servers
+    (per-server seqnos).  Type popularity is skewed per shard: shard s holds no
+    unit of type s % T, and a fraction p_remote of its Reserves ask for just
+    that type -- no local match, so they park and go to the cross-shard steal
+    round.  The other Reserves draw from the local types like config 2 (70% one
+    type, 20% two, 10% wildcard).  Reserve j of shard s comes from app rank
+    j * n_shards + s, so ranks are distinct across shards."""
+    rng = np.random.default_rng(seed + 7919 * shard)
+    ut = np.arange(n_types, dtype=np.int32)
+    miss = shard % n_types
+    local = np.delete(ut, miss) if n_types > 1 else ut
+    u_type = local[rng.integers(0, local.size, size=n_units)]
+    u_prio = rng.integers(0, prio_hi, size=n_units).astype(np.int32)
+    R = n_reserves
+    r_types = type_vectors(rng, local, R)
+    remote = rng.random(R) < p_remote
+    r_types[remote] = -2
+    r_types[remote, 0] = miss
+    A = R * n_shards
+    return Workload(user_types=ut, num_app_ranks=A, u_type=u_type, u_prio=u_prio,
+                    u_target=np.full(n_units, -1, np.int32),
+                    u_answer=(np.arange(n_units) % A).astype(np.int32),
+                    u_len=(8 + (np.arange(n_units) % 57)).astype(np.int32),
+                    r_rank=(np.arange(R) * n_shards + shard).astype(np.int32),
+                    r_types=r_types, r_hang=np.full(R, hang, np.uint8),
+                    name="config3", meta=dict(seed=seed, shard=shard, n_shards=n_shards, missing_type=int(miss)))
+
+
 # ----------------------------------------------------------------------------- config 5: stream
 def split_outputs(out: np.ndarray):
     """Split a replay output stream into per-event int arrays."""

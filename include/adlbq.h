@@ -114,6 +114,46 @@ int adlbq_tq_add(adlbq_server *h, int app_rank, int work_type, int server_rank);
 /* Remove a parked Reserve by rqseqno (rq_find_seqno + rq_delete, adlb.c:1883-1933). */
 int adlbq_rq_delete(adlbq_server *h, int rqseqno, int *found);
 
+/* ---- steal round: replaces the SS_RFR / SS_RFR_RESP round
+ * trips (adlb.c:1280-1308, 1802-1933, 3536-3579) between co-resident servers
+ * by one export + all-gather + deterministic merge (adlb_amd/shards.py). */
+
+/* The donor side of SS_RFR for every possible request at once: per work type
+ * (user_types order), the k >= 1 best available units -- unpinned,
+ * untargeted, prio > ADLB_LOWEST_PRIO -- in wq_find_hi_prio preference order
+ * (prio desc, wqseqno asc; xq.c:190-217).  recs8[t][i] = {work_prio, wqseqno,
+ * work_type, work_len, answer_rank, common_len, common_server_rank,
+ * common_seqno} (the SS_RFR_RESP fields, adlb.c:1828-1840); nrec[t] = records
+ * written (<= k); navail[t] = available units of type t in all. */
+int adlbq_steal_export(adlbq_server *h, int k, int *recs8, int *nrec, long long *navail);
+
+/* The live rq in FIFO (rqseqno) order: out18[i] = {rqseqno, world_rank,
+ * req_types[16]} (rq_struct_t, xq.h:79-86).  *count = live entries (only
+ * min(count, cap) are written). */
+int adlbq_rq_export(adlbq_server *h, int cap, int *out18, int *count);
+
+/* The serialised steal round over S shards (pure host function, same result
+ * on every caller).  recs8 [S][T][k][8], nrec [S][T], navail [S][T]: every
+ * shard's adlbq_steal_export.  reqs19[r] = {shard_idx, rqseqno, world_rank,
+ * req_types[16]} in (shard_idx, rqseqno) order.  For each request in that
+ * order: donor = find_cand_rank_with_worktype over the current heads
+ * (adlb.c:1280-1308, 3487-3534), unit = the donor's wq_find_hi_prio over the
+ * request's types (adlb.c:1816-1818).  out3[r] = {donor shard_idx, type
+ * index, record index} or {-1, -1, -1}.  *n_decided = requests settled
+ * before the first one that needs a unit past some shard's exported k; it
+ * and all later requests get -1 (they stay parked). */
+int adlbq_steal_merge(int S, int T, const int *user_types, int k, const int *recs8, const int *nrec,
+                      const long long *navail, int nreq, const int *reqs19, int *out3, int *n_decided);
+
+/* Donor side of a granted steal (adlb.c:1820-1824): pin_rank = rank,
+ * pinned = (rank >= 0).  pairs2[i] = {rank, wqseqno}; found[i] = 0 if that
+ * unit is no longer live, unpinned and untargeted. */
+int adlbq_grant_batch(adlbq_server *h, int n, const int *pairs2, int *found);
+
+/* Requester side: rq_find_seqno + rq_delete for each rqseqno (adlb.c:1883,
+ * 1933); found[i] = 1 if it was parked. */
+int adlbq_rq_delete_batch(adlbq_server *h, int n, const int *rqseqnos, int *found);
+
 /* Memory-pressure push choice (src/adlb.c:513-528): the first unpinned unit
  * (wq_find_unpinned, xq.c:266-281) and the server with the smallest
  * nbytes_used below threshold (strict <, lowest index wins).  -1 when none. */

@@ -18,11 +18,14 @@ from __future__ import annotations
 
 import ctypes
 import os
+import shutil
 import subprocess
+import tempfile
 
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+LOWEST = -999999999
 LIBS = {
     "own": os.path.join(HERE, "liboracle.so"),
     "ref": os.path.join(HERE, "_ref", "libxqref.so"),
@@ -30,6 +33,7 @@ LIBS = {
 
 OP_PUT, OP_RESERVE, OP_GET, OP_UNRESERVE, OP_QMROW, OP_SETROW = 1, 2, 3, 4, 5, 6
 OP_CHECKREM, OP_RFRDONE, OP_TQADD, OP_PUSHSEL, OP_INFO, OP_RQDEL, OP_INFOTYPE = 7, 8, 9, 10, 11, 12, 13
+OP_RFR, OP_RQLIST = 14, 15
 
 
 def build(ref: bool = False) -> None:
@@ -47,7 +51,9 @@ class Oracle:
     """One ADLB server's queue state replayed on the CPU (single instance per
     process for the "ref" kind, since the reference keeps its queues in globals)."""
 
-    def __init__(self, kind: str = "own"):
+    def __init__(self, kind: str = "own", private: bool = False):
+        """private=True loads a copy of the library, so that several servers
+        (shards) can live in one process -- the replay state is global."""
         path = LIBS[kind]
         if not os.path.exists(path):
             if kind == "own":
@@ -55,7 +61,14 @@ class Oracle:
             else:
                 raise FileNotFoundError(f"{path} missing (make -C oracle ref)")
         self.kind = kind
-        self.lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        if private:
+            tmp = tempfile.mkdtemp(prefix="oracle_")
+            dst = os.path.join(tmp, os.path.basename(path))
+            shutil.copy(path, dst)
+            self.lib = ctypes.CDLL(dst, mode=ctypes.RTLD_LOCAL)
+            shutil.rmtree(tmp, ignore_errors=True)   # the mapping stays valid
+        else:
+            self.lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         self.lib.orc_init.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int]
         self.lib.orc_replay.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p,
@@ -78,11 +91,85 @@ class Oracle:
             raise ValueError(f"oracle: malformed trace or output overflow (rc={n})")
         return out[:n].copy()
 
+    def _one(self, op: int, *args, cap: int = 4096) -> np.ndarray:
+        tr = np.asarray([op, *args], dtype=np.int32)
+        out = np.empty(cap, dtype=np.int32)
+        n = self.lib.orc_replay(tr.ctypes.data, tr.size, out.ctypes.data, cap)
+        if n < 0:
+            raise ValueError(f"oracle: event {op} failed (rc={n})")
+        return out[1:1 + out[0]].copy()
+
+    def qmrow(self):
+        r = self._one(OP_QMROW)
+        return int(r[0]), r[1:1 + self.ntypes]
+
+    def rq_list(self) -> np.ndarray:
+        """(n, 18) {rqseqno, rank, types[16]} in FIFO order."""
+        nrq = int(self._one(OP_INFO)[2])
+        r = self._one(OP_RQLIST, cap=64 + 18 * nrq)
+        return r[1:].reshape(-1, 18)
+
+    def rfr(self, rqseqno: int, for_rank: int, types16) -> np.ndarray:
+        return self._one(OP_RFR, rqseqno, for_rank, *[int(x) for x in types16])
+
+    def rqdel(self, rqseqno: int) -> int:
+        return int(self._one(OP_RQDEL, rqseqno)[0])
+
+
+def _find_cand_serial(me: int, types16, rows, user_types) -> int:
+    """find_cand_rank_with_worktype (adlb.c:3487-3534) walked over the request's
+    types in order (adlb.c:1280-1308) on a fresh table, no RFR outstanding and
+    no tq entries.  Returns a shard index or -1."""
+    for v in types16:
+        v = int(v)
+        if v < -1:
+            break
+        best, hi = -1, LOWEST
+        for j, (qlen, row) in enumerate(rows):
+            if j == me or qlen <= 0:
+                continue
+            if v < 0:
+                for x in row:
+                    if x > hi:
+                        hi, best = int(x), j
+            elif v in user_types:
+                x = row[user_types.index(v)]
+                if x > hi:
+                    hi, best = int(x), j
+        if best >= 0:
+            return best
+    return -1
+
+
+def serial_steal_round(orcs, num_app_ranks: int) -> np.ndarray:
+    """The steal round adlbq_steal_merge replaces, one RFR exchange at a time:
+    the parked Reserves of shard 0, 1, ... in rqseqno order; each picks its
+    donor on the current qmstat rows of every shard (update_local_state,
+    adlb.c:3581-3593), the donor runs SS_RFR (adlb.c:1802-1866) and the
+    requester SS_RFR_RESP (adlb.c:1868-1933: TA_RESERVE_RESP with the donor's
+    world rank, rq_delete) before the next Reserve starts.
+    Returns (n, 15) {shard, rqseqno, rank, TA_RESERVE_RESP[12]} per steal."""
+    user_types = [int(x) for x in orcs[0]._ut]
+    out = []
+    for i, o in enumerate(orcs):
+        for e in o.rq_list():
+            rqseqno, rank, types = int(e[0]), int(e[1]), e[2:]
+            rows = [x.qmrow() for x in orcs]
+            d = _find_cand_serial(i, types, rows, user_types)
+            if d < 0:
+                continue
+            r = orcs[d].rfr(rqseqno, rank, types)
+            assert r[0] == 1, "a donor chosen on a fresh table must have a unit"
+            assert o.rqdel(rqseqno) == 1
+            out.append([i, rqseqno, rank, 1, r[3], r[4], r[5], r[6], r[7], num_app_ranks + d, r[9], r[10], r[11],
+                        -1, -1])
+    return np.asarray(out, dtype=np.int32).reshape(-1, 15)
+
 
 def event_nargs(op: int, ntypes: int) -> int:
     return {OP_PUT: 9, OP_RESERVE: 18, OP_GET: 2, OP_UNRESERVE: 3, OP_QMROW: 0,
             OP_SETROW: 3 + ntypes, OP_CHECKREM: 0, OP_RFRDONE: 2, OP_TQADD: 3,
-            OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1, OP_INFOTYPE: 1}[op]
+            OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1, OP_INFOTYPE: 1, OP_RFR: 18, OP_RQLIST: 0}[op]
 
 
 def output_bound(tr: np.ndarray, ntypes: int) -> int:

@@ -147,6 +147,8 @@ int orc_event_nargs(int op, int ntypes)
     case ORC_OP_INFO: return 0;
     case ORC_OP_RQDEL: return 1;
     case ORC_OP_INFOTYPE: return 1;
+    case ORC_OP_RFR: return 2 + ORC_REQ_TYPES;
+    case ORC_OP_RQLIST: return 0;
     default: return -1;
     }
 }
@@ -331,6 +333,62 @@ long orc_replay(const int *tr, long ntrace, int *out, long outcap)
                 o[0] = 1;
             }
             n = 1;
+            break;
+        }
+        case ORC_OP_RFR: {
+            /* SS_RFR at the donor, adlb.c:1802-1866: the pre-targeted scan for
+             * for_rank, then the untargeted scan; pin and answer SS_RFR_RESP */
+            int for_rank = a[1];
+            const int *types = a + 2;
+            void *u = be_wq_find_pre_targeted_hi_prio(for_rank, types);
+            if (!u)
+                u = be_wq_find_hi_prio(types);
+            if (u) {
+                be_unit_view v;
+                be_wq_view(u, &v);
+                be_wq_set_pin(u, for_rank, for_rank >= 0 ? 1 : v.pinned); /* 1820-1824 */
+                o[0] = 1;
+                o[1] = a[0];
+                o[2] = for_rank;
+                o[3] = v.work_type;
+                o[4] = v.work_prio;
+                o[5] = v.work_len;
+                o[6] = v.answer_rank;
+                o[7] = v.wqseqno;
+                o[8] = v.target_rank; /* prev_target */
+                o[9] = v.common_len;
+                o[10] = v.common_server_rank;
+                o[11] = v.common_server_commseqno;
+                n = 12;
+            } else {
+                /* NO_CURR_WORK; the donor refreshes its own qmstat row (1858) */
+                int q = be_wq_num_unpinned_untargeted();
+                S.qm_qlen[S.my_idx] = q;
+                for (int i = 0; i < T; i++)
+                    S.qm_hi[(long)S.my_idx * T + i] = be_wq_avail_hi_prio_of_type(S.user_types[i]);
+                o[0] = -2;
+                o[1] = a[0];
+                o[2] = for_rank;
+                n = 3;
+            }
+            break;
+        }
+        case ORC_OP_RQLIST: {
+            /* the rq in FIFO order (xq_first / xq_next over rq) */
+            long k = 0;
+            int rank, rqseqno, types[ORC_REQ_TYPES];
+            for (void *r = be_rq_first(); r; r = be_rq_next(r)) {
+                if (op + 2 + 18 * (k + 1) > outcap)
+                    return -1;
+                be_rq_view(r, &rank, &rqseqno, types);
+                int *e = o + 1 + 18 * k;
+                e[0] = rqseqno;
+                e[1] = rank;
+                memcpy(e + 2, types, sizeof(types));
+                k++;
+            }
+            o[0] = (int)k;
+            n = 1 + 18 * k;
             break;
         }
         case ORC_OP_INFOTYPE: {

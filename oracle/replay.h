@@ -27,6 +27,8 @@ enum {
     ORC_OP_INFO = 11,     /*                                                    -> [wq_count, wq_max_count, rq_count] */
     ORC_OP_RQDEL = 12,    /* rqseqno                                            -> [found] */
     ORC_OP_INFOTYPE = 13, /* type                                               -> [max_prio, num_max_prio, num_type] */
+    ORC_OP_RFR = 14,      /* rqseqno for_rank t0..t15 (SS_RFR rfr_buf)          -> SS_RFR_RESP [12] or [-2, rqseqno, for_rank] */
+    ORC_OP_RQLIST = 15,   /*                                                    -> [k, (rqseqno, rank, t0..t15) * k] */
 };
 
 /* TA_RESERVE_RESP layout (adlb.c:1213-1222), plus two slots this build uses
