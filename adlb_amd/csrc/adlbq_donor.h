@@ -90,6 +90,26 @@ __device__ inline int find_cand(const DonorCtx &c, int for_rank, int work_type) 
     return c.master + (int)(0xffffffffu - (unsigned int)(best & 0xffffffffu));
 }
 
+// Could find_cand return a server at all (tq aside)?  Some server i != self
+// without an outstanding RFR, qlen > 0 and a type above LOWEST.  Once none is
+// left, every later parked request of the batch gets no donor.  Wave-uniform.
+__device__ inline bool any_donor(const DonorCtx &c) {
+    const int lane = __lane_id();
+    for (int base = 0; base < c.S; base += 64) {
+        const int i = base + lane;
+        bool ok = false;
+        if (i < c.S) {
+            const int srv = c.master + i;
+            if (srv != c.my_world && !ld_agent(c.rfr_out + srv) && c.qm_qlen[i] > 0) {
+                const int *row = c.qm_hi + (long long)i * c.T;
+                for (int j = 0; j < c.T && !ok; j++) ok = row[j] > LOWEST;
+            }
+        }
+        if (__ballot(ok)) return true;
+    }
+    return false;
+}
+
 DonorCtx donor_ctx(adlbq_server *h);  // host: snapshot of the device pointers / sizes
 
 // the RFR part of FA_RESERVE / check_remote (adlb.c:1280-1308, 3549-3577)

@@ -1093,7 +1093,7 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
                           const int *__restrict__ tmatch, const int *__restrict__ umatch, int *rq_rank,
                           int *rq_types, int *rq_live, int *rq_req, DevCounters *ctr, int *resp) {
     __shared__ int wsum[16];
-    __shared__ int s_n0, s_total;
+    __shared__ int s_n0, s_total, s_stop;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nth = blockDim.x;
     const int per = (R + nth - 1) / nth, lo = min(R, tid * per), hi = min(R, lo + per);
     auto parked = [&](int j) {
@@ -1127,17 +1127,26 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     __threadfence();
     __syncthreads();
     const int n0 = s_n0, np = s_total;
+    // the RFR donors in FIFO order (rfr_out / rfr_to_rank chain them); once no
+    // server can be a donor any more (each RFR sets rfr_out), the rest get -1
+    // in parallel
     if (w == 0) {
-        for (int k = n0; k < n0 + np; k++) {
+        bool open = donors && (c.n_tq > 0 || any_donor(c));
+        int k = n0;
+        for (; k < n0 + np && open; k++) {
             const int j = rq_req[k];
             const int *rr = reqs + (long long)ADLBQ_RESERVE_INTS * j;
             const int rank = rr[0];
             int cand = -1;
-            if (donors && rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) < 0)
+            if (rank >= 0 && rank < c.A && ld_agent(c.rfr_to_rank + rank) < 0)
                 cand = rfr_select(c, rank, rr + 2);
             if (lane == 0) resp[(long long)ADLBQ_RESP_INTS * j + 11] = cand;
+            if (cand >= 0 && c.n_tq == 0) open = any_donor(c);
         }
+        if (lane == 0) s_stop = k;
     }
+    __syncthreads();
+    for (int k = s_stop + tid; k < n0 + np; k += nth) resp[(long long)ADLBQ_RESP_INTS * rq_req[k] + 11] = -1;
     if (tid == 0) {
         ctr->rq_n = n0 + np;
         ctr->rq_live += np;

@@ -26,6 +26,8 @@ further exchange, since every process computed the same grants.
 from __future__ import annotations
 
 import ctypes
+import time
+from typing import NamedTuple
 
 import numpy as np
 
@@ -83,6 +85,13 @@ def reduce_step_timing(elapsed_s: float, matched: int, group=None):
 
 
 # ------------------------------------------------------------------ steal round
+class StealResult(NamedTuple):
+    resp: np.ndarray   # (m, 15) {shard, rqseqno, rank, TA_RESERVE_RESP[12]} for local requesters
+    decided: int       # Reserves the merge decided, all shards
+    settled: int       # Reserves it settled (a donor granted a unit), all shards
+    grants: dict       # local donor shard -> (n, 2) {rank, wqseqno} it pinned
+
+
 def steal_merge(user_types, k: int, recs, nrec, navail, reqs19):
     """The merge over S shards (adlbq_steal_merge): recs [S, T, k, 8], nrec [S, T],
     navail [S, T], reqs19 (n, 19) {shard, rqseqno, rank, types[16]} in (shard,
@@ -109,28 +118,41 @@ def _sort_reqs(reqs19: np.ndarray) -> np.ndarray:
     return reqs19[np.lexsort((reqs19[:, 1], reqs19[:, 0]))]
 
 
-def settle(local, num_app_ranks: int, user_types, k: int, recs, nrec, navail, reqs19):
+def _tick(timing, key, t0):
+    if timing is not None:
+        t = time.perf_counter()
+        timing[key] = timing.get(key, 0.0) + (t - t0)
+        return t
+    return t0
+
+
+def settle(local, num_app_ranks: int, user_types, k: int, recs, nrec, navail, reqs19, timing=None):
     """Run the merge on the gathered exports and apply this process's side of it.
 
     local: {shard index: server} for the shards this process owns (objects with
     grant_batch and rq_delete_batch, e.g. adlb_amd.server.Server).
-    Returns (responses (m, 15) {shard, rqseqno, rank, TA_RESERVE_RESP[12]} for
-    the Reserves of local shards that were settled -- the reply
-    SS_RFR_RESP sends the app, adlb.c:1885-1898, with the donor's world rank --,
-    the number of Reserves the merge decided and the number it settled, both
-    over all shards: the same on every process)."""
+    Returns a StealResult: the responses for the Reserves of local shards that
+    were settled (the reply SS_RFR_RESP sends the app, adlb.c:1885-1898, with
+    the donor's world rank), the numbers of Reserves the merge decided and
+    settled over all shards (the same on every process), and the units each
+    local donor pinned."""
+    t0 = time.perf_counter()
     reqs19 = _sort_reqs(np.asarray(reqs19, dtype=np.int32).reshape(-1, 19))
     out, nd = steal_merge(user_types, k, recs, nrec, navail, reqs19)
+    t0 = _tick(timing, "merge", t0)
     won = np.nonzero(out[:nd, 0] >= 0)[0]
     d, t, i = out[won, 0], out[won, 1], out[won, 2]
     r = recs[d, t, i]                                  # [m, 8] records of the granted units
     q = reqs19[won]
+    grants = {}
     for s, srv in local.items():
         g = np.nonzero(d == s)[0]
         if g.size:
-            found = srv.grant_batch(np.stack([q[g, 2], r[g, 1]], axis=1))
+            grants[s] = np.stack([q[g, 2], r[g, 1]], axis=1).astype(np.int32)
+            found = srv.grant_batch(grants[s])
             if not found.all():
                 raise RuntimeError(f"shard {s}: {int((found == 0).sum())} granted units were no longer available")
+    t0 = _tick(timing, "grant", t0)
     mine = np.isin(q[:, 0], np.fromiter(local.keys(), dtype=np.int32, count=len(local)))
     resp = np.empty((int(mine.sum()), 15), dtype=np.int32)
     qm, rm, dm = q[mine], r[mine], d[mine]
@@ -150,7 +172,8 @@ def settle(local, num_app_ranks: int, user_types, k: int, recs, nrec, navail, re
             found = srv.rq_delete_batch(resp[g, 1])
             if not found.all():
                 raise RuntimeError(f"shard {s}: settled Reserves were no longer parked")
-    return resp, nd, int(won.size)
+    _tick(timing, "rq_delete", t0)
+    return StealResult(resp, nd, int(won.size), grants)
 
 
 def _export(srv, k: int):
@@ -162,8 +185,9 @@ def _export(srv, k: int):
     return recs, nrec, navail, reqs
 
 
-def steal_round_local(servers, k: int):
+def steal_round_local(servers, k: int, timing=None):
     """The steal round among shards held by one process (no collective)."""
+    t0 = time.perf_counter()
     S = servers[0].num_servers
     T = servers[0].T
     recs = np.zeros((S, T, k, 8), np.int32)
@@ -174,12 +198,13 @@ def steal_round_local(servers, k: int):
         a, b, c, q = _export(srv, k)
         recs[srv.my_server_idx], nrec[srv.my_server_idx], navail[srv.my_server_idx] = a, b, c
         reqs.append(q)
+    _tick(timing, "export", t0)
     local = {srv.my_server_idx: srv for srv in servers}
     return settle(local, servers[0].num_app_ranks, servers[0].user_types, k, recs, nrec, navail,
-                  np.concatenate(reqs) if reqs else np.zeros((0, 19), np.int32))
+                  np.concatenate(reqs) if reqs else np.zeros((0, 19), np.int32), timing)
 
 
-def steal_round(servers, k: int, group=None):
+def steal_round(servers, k: int, group=None, timing=None):
     """The steal round across processes: each process holds `servers` (its
     shards); one all-gather of sizes and one of the padded exports (RCCL over
     xGMI on GPU ranks, gloo on CPU), then the same merge everywhere."""
@@ -190,6 +215,7 @@ def steal_round(servers, k: int, group=None):
     world = dist.get_world_size(group)
     # one int32 blob per process: per shard [idx, nrec[T], navail lo/hi [2T], recs[T*k*8]], then reqs
     per = 1 + 3 * T + T * k * 8
+    t0 = time.perf_counter()
     parts, reqs = [], []
     for srv in servers:
         a, b, c, q = _export(srv, k)
@@ -197,6 +223,7 @@ def steal_round(servers, k: int, group=None):
         parts.append(np.concatenate([[srv.my_server_idx], b, nav, a.ravel()]).astype(np.int32))
         reqs.append(q.ravel())
     blob = np.concatenate([[len(servers)], *parts, *reqs]).astype(np.int32)
+    t0 = _tick(timing, "export", t0)
     n = torch.tensor([blob.size], dtype=torch.int64, device=dev)
     sizes = [torch.empty_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
@@ -219,6 +246,7 @@ def steal_round(servers, k: int, group=None):
             recs[idx] = b[off + 1 + 3 * T: off + per].reshape(T, k, 8)
             off += per
         allreqs.append(b[off:].reshape(-1, 19))
+    _tick(timing, "allgather", t0)
     local = {srv.my_server_idx: srv for srv in servers}
     return settle(local, servers[0].num_app_ranks, servers[0].user_types, k, recs, nrec, navail,
-                  np.concatenate(allreqs))
+                  np.concatenate(allreqs), timing)

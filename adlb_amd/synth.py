@@ -172,6 +172,20 @@ def config4(n_units=10_000_000, n_types=32, n_reserves=65_536, n_ranks=1024, see
                     name="config4", meta=dict(seed=seed))
 
 
+def config3_types(rng, n_types, shard, R, p_remote=0.1) -> np.ndarray:
+    """Config 3 Reserve type vectors of one shard: a fraction p_remote ask for
+    just the shard's missing type (shard % T), the rest draw from its local
+    types like config 2."""
+    ut = np.arange(n_types, dtype=np.int32)
+    miss = shard % n_types
+    local = np.delete(ut, miss) if n_types > 1 else ut
+    r_types = type_vectors(rng, local, R)
+    remote = rng.random(R) < p_remote
+    r_types[remote] = -2
+    r_types[remote, 0] = miss
+    return r_types
+
+
 def config3_shard(shard, n_shards=64, n_units=1_562_500, n_types=4, n_reserves=8192, seed=3, prio_hi=1024,
                   p_remote=0.1, hang=1) -> Workload:
     """Config 3: one server shard of a queue sharded over n_shards servers
@@ -188,10 +202,7 @@ def config3_shard(shard, n_shards=64, n_units=1_562_500, n_types=4, n_reserves=8
     u_type = local[rng.integers(0, local.size, size=n_units)]
     u_prio = rng.integers(0, prio_hi, size=n_units).astype(np.int32)
     R = n_reserves
-    r_types = type_vectors(rng, local, R)
-    remote = rng.random(R) < p_remote
-    r_types[remote] = -2
-    r_types[remote, 0] = miss
+    r_types = config3_types(rng, n_types, shard, R, p_remote)
     A = R * n_shards
     return Workload(user_types=ut, num_app_ranks=A, u_type=u_type, u_prio=u_prio,
                     u_target=np.full(n_units, -1, np.int32),

@@ -58,6 +58,13 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP event timing")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-config3", action="store_true", help="skip the config-3 steal-round measurement")
+    ap.add_argument("--c3-servers", type=int, default=8, help="config 3: server shards per GPU")
+    ap.add_argument("--c3-units", type=int, default=1_562_500, help="config 3: units per server shard")
+    ap.add_argument("--c3-reserves", type=int, default=8192, help="config 3: Reserves per shard per step")
+    ap.add_argument("--c3-k", type=int, default=1024, help="config 3: exported units per type per shard")
+    ap.add_argument("--c3-steps", type=int, default=5)
+    ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     return ap.parse_args()
 
 
@@ -85,6 +92,7 @@ def pmc_traffic(args) -> dict | None:
     if prof is None:
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu", "--no-pmc",
+             "--no-config3",
              "--no-profile", "--units", str(args.units), "--reserves", str(args.reserves), "--types",
              str(args.types), "--seed", str(args.seed)] + (["--equal-prio"] if args.equal_prio else [])
     out = {}
@@ -142,6 +150,121 @@ def cpu_baseline(w, budget_s: float) -> dict:
     return {"value": done / el, "unit": "assignments/s", "cores": 1, "kind": "port",
             "sample": f"first {done} Reserves of the step-0 batch on a {w.n_units}-unit queue "
                       f"({el:.1f} s, oracle/liboracle.so: linked-list restatement of xq.c scans)"}
+
+
+def bench_config3(args, torch, dist, world, rank, local, dev):
+    """Config 3: c3_servers server shards per GPU (64 over 8
+    GPUs), c3_units units each, per-shard type skew so ~10% of the Reserves
+    have no local match.  One step = every shard's Reserve batch (concurrent
+    streams), then one steal round over all shards (device top-k export, one
+    all-gather over RCCL, the merge, grants), then SS_UNRESERVE of every
+    matched and stolen unit so each step sees the same queues.  Reports
+    (local + stolen assignments) / s and the steal round's share."""
+    from adlb_amd import shards, synth
+    from adlb_amd.server import Server
+
+    SL, N, R, k = args.c3_servers, args.c3_units, args.c3_reserves, args.c3_k
+    S, T = SL * world, 4
+    nb = args.c3_steps + 1
+    srvs, streams, d_reqs, d_resp, d_trip = [], [], [], [], []
+    for j in range(SL):
+        idx = rank * SL + j
+        w = synth.config3_shard(idx, S, N, T, R, seed=args.seed)
+        srv = Server(w.user_types, w.num_app_ranks, S, idx, max_units=N, device=local)
+        st = torch.cuda.Stream(dev)
+        srv.set_stream(st.cuda_stream)
+        srv.put_batch(np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1),
+                                np.zeros(N), np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32))
+        rng = np.random.default_rng(args.seed + 31 * idx)
+        reqs = np.empty((nb, R, 18), np.int32)
+        for b in range(nb):
+            reqs[b, :, 0] = w.r_rank
+            reqs[b, :, 1] = 1
+            reqs[b, :, 2:] = synth.config3_types(rng, T, idx, R) if b else w.r_types
+        with torch.cuda.stream(st):
+            d_reqs.append(torch.from_numpy(reqs).to(dev))
+            d_resp.append(torch.empty((nb, R, 12), dtype=torch.int32, device=dev))
+            tr = torch.empty((R, 3), dtype=torch.int32, device=dev)
+            tr[:, 0] = torch.from_numpy(w.r_rank).to(dev)
+            tr[:, 2] = -1
+            d_trip.append(tr)
+        srvs.append(srv)
+        streams.append(st)
+    torch.cuda.synchronize()
+    keep, parts, sparts = [], {"batches": 0.0, "steal": 0.0, "unreserve": 0.0}, {}
+
+    def step(b, timed_parts=False):
+        t0 = time.perf_counter()
+        for j, srv in enumerate(srvs):
+            srv.reserve_batch_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
+        if timed_parts:
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        tm = sparts if timed_parts else None
+        res = shards.steal_round(srvs, k, timing=tm) if world > 1 else shards.steal_round_local(srvs, k, timing=tm)
+        t2 = time.perf_counter()
+        for j, srv in enumerate(srvs):
+            with torch.cuda.stream(streams[j]):
+                d_trip[j][:, 1].copy_(d_resp[j][b][:, 5])
+            srv.unreserve_batch_device(R, d_trip[j].data_ptr())
+            g = res.grants.get(srv.my_server_idx)
+            if g is not None and g.size:
+                trip = np.concatenate([g, np.full((g.shape[0], 1), -1, np.int32)], axis=1)
+                with torch.cuda.stream(streams[j]):
+                    t = torch.from_numpy(trip).to(dev, non_blocking=False)
+                keep.append(t)
+                srv.unreserve_batch_device(g.shape[0], t.data_ptr())
+        if timed_parts:
+            torch.cuda.synchronize()
+            parts["batches"] += t1 - t0
+            parts["steal"] += t2 - t1
+            parts["unreserve"] += time.perf_counter() - t2
+        return res
+
+    step(0)                              # warm-up
+    torch.cuda.synchronize()
+    keep.clear()
+    if args.c3_parts:                    # per-part timing, synchronised (untimed)
+        for b in range(1, nb):
+            step(b, timed_parts=True)
+        torch.cuda.synchronize()
+        keep.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    settled = decided = 0
+    for b in range(1, nb):
+        r = step(b)
+        settled += r.settled
+        decided += r.decided
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    local_matched = int(sum(int((d[1:, :, 0] == 1).sum().item()) for d in d_resp))
+    parked = int(sum(int((d[1:, :, 0] == 0).sum().item()) for d in d_resp))
+    if world > 1:
+        el, local_matched = shards.reduce_step_timing(el, local_matched)
+        _, parked = shards.reduce_step_timing(0.0, parked)
+    steps = nb - 1
+    out = {
+        "workload": f"config3: {S} server shards ({SL}/GPU) x {N} units, {T} types with one type missing per "
+                    f"shard, {R} Reserves/shard/step (~10% only the missing type), steal round k={k}",
+        "value": (local_matched + settled) / el,
+        "unit": "assignments/s",
+        "ms_per_step": el * 1e3 / steps,
+        "local_matched_per_step": local_matched / steps,
+        "parked_per_step": parked / steps,
+        "stolen_per_step": settled / steps,
+        "decided_per_step": decided / steps,
+        "parts_ms_per_step": ({kk: round(v * 1e3 / (nb - 1), 3) for kk, v in {**parts, **sparts}.items()}
+                              if args.c3_parts else None),
+        "scaling": "weak",
+    }
+    for srv in srvs:
+        srv.close()
+    return out
 
 
 def main():
@@ -294,11 +417,17 @@ def main():
         "chain_last_batch": {k: srv.stat("chain_" + k) for k in ("rounds", "passes", "recomputed", "fallback")},
         "candidates_last_batch": srv.stat("candidates"),
     }
+    srv.close()
+    del d_reqs, d_resp
+    if not args.no_config3:
+        try:
+            res["config3"] = bench_config3(args, torch, dist, world, rank, local, dev)
+        except Exception as e:  # reported, not fatal: the metric line above stands
+            res["config3"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(res), flush=True)
-    srv.close()
     if world > 1:
         dist.destroy_process_group()
 

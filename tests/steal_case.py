@@ -101,8 +101,8 @@ def rounds(round_fn, max_rounds=10_000):
     stops early always makes progress); concatenated responses."""
     got = []
     for _ in range(max_rounds):
-        resp, _nd, settled = round_fn()
-        got.append(resp)
-        if settled == 0:
+        r = round_fn()
+        got.append(r.resp)
+        if r.settled == 0:
             break
     return np.concatenate(got) if got else np.zeros((0, 15), np.int32)

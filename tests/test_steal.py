@@ -30,7 +30,7 @@ def test_merge_equals_serial_round(S, seed):
     ls = list_shards(ws, orcs, resps)
     nreq = sum(x.rq.shape[0] for x in ls)
     assert nreq > 0
-    got, nd, settled = shards.steal_round_local(ls, k=4096)
+    got, nd, settled, _ = shards.steal_round_local(ls, k=4096)
     assert nd == nreq
     exp = oracle.serial_steal_round(orcs, ws[0].num_app_ranks)
     assert exp.shape[0] > 0 and settled == exp.shape[0]
