@@ -35,6 +35,10 @@ SIGNATURES = {
     "adlbq_rq_delete": (c_int, [P, c_int, P]),
     "adlbq_steal_export": (c_int, [P, c_int, P, P, P]),
     "adlbq_rq_export": (c_int, [P, c_int, P, P]),
+    "adlbq_steal_begin": (c_int, [P, c_int]),
+    "adlbq_steal_collect": (c_int, [P, P, P, P, c_int, P, P]),
+    "adlbq_steal_apply": (c_int, [P, c_int, P, c_int, P]),
+    "adlbq_steal_check": (c_int, [P, P, P]),
     "adlbq_steal_merge": (c_int, [c_int, c_int, P, c_int, P, P, P, c_int, P, P, P]),
     "adlbq_grant_batch": (c_int, [P, c_int, P, P]),
     "adlbq_rq_delete_batch": (c_int, [P, c_int, P, P]),

@@ -150,7 +150,8 @@ struct adlbq_server {
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
     int *d_cslot = nullptr, *d_cslot2 = nullptr;
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate
-    int *d_seg_cnt = nullptr;          // [nseg] chain: untargeted-capable requests per segment
+    int *d_seg_cnt = nullptr;          // [R/64] chain: untargeted-capable requests per 64 requests
+    unsigned long long *d_pmask = nullptr;  // [R/64] k_finalize: ballots of the requests that park
     int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
     int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
     int *d_chSf = nullptr, *d_chEf = nullptr;  // [nseg][T] chain: final start / end states
@@ -158,7 +159,17 @@ struct adlbq_server {
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
     int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")
-    int *d_export = nullptr; long long cap_export = 0;  // adlbq_steal_export records
+    // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
+    int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]
+    long long *d_navail = nullptr;                       // [T]
+    int *d_rqx = nullptr; long long cap_rqx = 0;         // [1 count | cap*18 rq entries]
+    int *h_steal = nullptr; long long cap_hsteal = 0;    // pinned: recs | nrec | navail (2T) | count | rq
+    int steal_k = -1, steal_rqcap = 0;                   // shape of the export in flight (-1: none)
+    hipEvent_t steal_ev = nullptr;
+    int *h_apply = nullptr; long long cap_happly = 0;    // pinned staging of grants / deletions
+    int *d_apply = nullptr; long long cap_dapply = 0;
+    int *d_apply_bad = nullptr;                          // [2] grants not available, deletions not parked
+    hipEvent_t apply_ev = nullptr;
     int *d_result = nullptr;           // small result scratch (16 ints)
     int *h_result = nullptr;           // pinned host mirror
     long long last_scan_units = 0;
@@ -188,6 +199,7 @@ int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
 int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
+int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail);
 
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ unsigned long long make_key(int prio, unsigned int order) {

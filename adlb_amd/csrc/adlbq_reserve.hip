@@ -641,7 +641,8 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
                                                     const int *__restrict__ candlen,
                                                     const unsigned long long *__restrict__ ckey,
                                                     unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
-                                                    long long ncsum) {
+                                                    long long ncsum, const unsigned long long *__restrict__ mask,
+                                                    const int *__restrict__ tmatch, int R, int *seg_cnt) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
     __shared__ unsigned long long span[4][RANK_SPAN];
     __shared__ unsigned long long s_first, s_last;
@@ -655,6 +656,27 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         if (t < T) slen[t] = candlen[t];
     }
     __syncthreads();
+    {
+        // the chain's level guess counts the requests that take an untargeted
+        // unit: drop those whose types have no candidate at all (k_req_prep
+        // counted every non-empty type set, k_targeted the targeted matches)
+        unsigned long long cm = 0;
+        for (int t = 0; t < T; t++) cm |= slen[t] > 0 ? (1ull << t) : 0ull;
+        const unsigned long long all = T >= 64 ? ~0ull : ((1ull << T) - 1);
+        if (cm != all) {
+            const int waves = gridDim.x * (RANK_TILE / 64);
+            for (int g = blockIdx.x * (RANK_TILE / 64) + w; g * 64 < R; g += waves) {
+                const int j = g * 64 + lane;
+                bool drop = false;
+                if (j < R) {
+                    const unsigned long long m = mask[j];
+                    drop = m != 0ull && !(m & cm) && tmatch[j] < 0;
+                }
+                const unsigned long long b = __ballot(drop);
+                if (lane == 0 && b) atomicSub(&seg_cnt[g], __popcll(b));
+            }
+        }
+    }
     if (tid == 0) {
         int acc = 0;
         for (int t = 0; t < T; t++) {
@@ -1090,17 +1112,25 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
 // (1238-1310).  Response words [10], [11] of a parked request are written only
 // by that last workgroup, so no two workgroups store the same bytes.
 __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__ reqs, int R,
-                          const int *__restrict__ tmatch, const int *__restrict__ umatch, int *rq_rank,
-                          int *rq_types, int *rq_live, int *rq_req, DevCounters *ctr, int *resp) {
+                          const unsigned long long *pmask, int *rq_rank, int *rq_types, int *rq_live, int *rq_req,
+                          DevCounters *ctr, int *resp) {
     __shared__ int wsum[16];
     __shared__ int s_n0, s_total, s_stop;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nth = blockDim.x;
-    const int per = (R + nth - 1) / nth, lo = min(R, tid * per), hi = min(R, lo + per);
-    auto parked = [&](int j) {
-        return tmatch[j] < 0 && umatch[j] < 0 && reqs[(long long)ADLBQ_RESERVE_INTS * j + 1] != 0;
-    };
+    // the parked requests are the set bits of the per-wave ballots every
+    // workgroup published (pmask[j >> 6]); thread tid takes a contiguous run
+    // of words so that rq order is request order
+    const int nw = (R + 63) / 64, per = (nw + nth - 1) / nth, w0 = min(nw, tid * per), w1 = min(nw, w0 + per);
+    constexpr int MAXW = 8;  // per <= 8 words held in registers (R <= 131072 at 256 threads)
+    unsigned long long bits[MAXW];
     int cnt = 0;
-    for (int j = lo; j < hi; j++) cnt += parked(j);
+#pragma unroll
+    for (int q = 0; q < MAXW; q++) {
+        bits[q] = w0 + q < w1 ? __hip_atomic_load(pmask + w0 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        cnt += __popcll(bits[q]);
+    }
+    for (int q = w0 + MAXW; q < w1; q++)  // larger batches: the rest straight from memory
+        cnt += __popcll(__hip_atomic_load(pmask + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     int x = cnt;  // block exclusive scan of cnt
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1114,15 +1144,19 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     for (int q = 0; q < w; q++) wpre += wsum[q];
     if (tid == nth - 1) s_total = wpre + x;
     int pos = s_n0 + wpre + x - cnt;
-    for (int j = lo; j < hi; j++) {
-        if (!parked(j)) continue;
-        const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
-        rq_rank[pos] = rq[0];
-        for (int q = 0; q < NREQ; q++) rq_types[(long long)pos * NREQ + q] = rq[2 + q];
-        rq_live[pos] = 1;
-        rq_req[pos] = j;
-        resp[(long long)ADLBQ_RESP_INTS * j + 10] = pos + 1;  // rqseqno (next_rqseqno++, adlb.c:1244)
-        pos++;
+    for (int q = w0; q < w1; q++) {
+        unsigned long long b = q - w0 < MAXW ? bits[q - w0]
+                                             : __hip_atomic_load(pmask + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (; b; b &= b - 1) {
+            const int jj = q * 64 + __ffsll((long long)b) - 1;
+            const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * jj;
+            rq_rank[pos] = rq[0];
+            for (int k = 0; k < NREQ; k++) rq_types[(long long)pos * NREQ + k] = rq[2 + k];
+            rq_live[pos] = 1;
+            rq_req[pos] = jj;
+            resp[(long long)ADLBQ_RESP_INTS * jj + 10] = pos + 1;  // rqseqno (next_rqseqno++, adlb.c:1244)
+            pos++;
+        }
     }
     __threadfence();
     __syncthreads();
@@ -1163,7 +1197,8 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   int my_world, int *__restrict__ resp, DevCounters *ctr,
                                                   DonorCtx dc, int donors, int *rq_rank, int *rq_types,
                                                   int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap,
-                                                  long long *anchor, long long *anchor_next) {
+                                                  long long *anchor, long long *anchor_next,
+                                                  unsigned long long *pmask) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1200,7 +1235,12 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
             out[11] = -1;
         }
         const unsigned long long pb = __ballot(parks);
-        if ((threadIdx.x & 63) == 0 && pb) atomicAdd(&s_parked, __popcll(pb));
+        if ((threadIdx.x & 63) == 0) {
+            // published for the last workgroup's park (write-through, drained before the arrival below)
+            __hip_atomic_store(pmask + (j >> 6), pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (pb) atomicAdd(&s_parked, __popcll(pb));
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's store has landed before the block arrives
+        }
     }
     __syncthreads();
     // two-level arrival (8 groups, then one top counter) keeps every counter's
@@ -1227,7 +1267,7 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
             anchor_next[threadIdx.x] = LLONG_MIN;
         }
     }
-    if (total > 0) park_tail(dc, donors, reqs, R, tmatch, umatch, rq_rank, rq_types, rq_live, rq_req, ctr, resp);
+    if (total > 0) park_tail(dc, donors, reqs, R, pmask, rq_rank, rq_types, rq_live, rq_req, ctr, resp);
     __syncthreads();
     if (threadIdx.x == 0) {
         if (total == 0) ctr->n_parked_last = 0;
@@ -1255,9 +1295,17 @@ __global__ __launch_bounds__(256) void k_export_gather(int T, int k, const int *
                                                        const int *__restrict__ prio, const int *__restrict__ seqa,
                                                        const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
                                                        int *__restrict__ recs, int *__restrict__ nrec,
+                                                       long long *__restrict__ navail,
+                                                       const unsigned int *__restrict__ coltot, int scanned,
                                                        unsigned int *csum, long long ncsum, int *dem,
                                                        long long *anchor, long long *anchor_next) {
     const int t = blockIdx.x;
+    if (threadIdx.x < 64) {  // available units of type t: its column totals (k_thresholds)
+        unsigned long long a = scanned ? coltot[t * NB + threadIdx.x] : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        if (threadIdx.x == 0) navail[t] = (long long)a;
+    }
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < ncsum;
          i += (long long)gridDim.x * blockDim.x)
         csum[i] = 0;
@@ -1289,7 +1337,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
     void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
-                  h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt};
+                  h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_pmask};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
@@ -1299,6 +1347,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
     const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
     AQ_HIP(hipMalloc((void **)&h->d_seg_cnt, sizeof(int) * ((nc + 63) / 64)));
+    AQ_HIP(hipMalloc((void **)&h->d_pmask, sizeof(unsigned long long) * ((nc + 63) / 64)));
     AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));
     AQ_HIP(hipMemset(h->d_chflag, 0, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));  // epochs start at 1
@@ -1415,7 +1464,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if (np > 0 && T > 0) {
         stage_begin(h, "rank", &ev);
         k_rank<<<512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
-                                    (long long)((np + CHUNK - 1) / CHUNK) * C);
+                                    (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
+                                    h->d_seg_cnt);
         stage_end(h, "rank", ev);
     }
     stage_begin(h, "chain", &ev);
@@ -1441,7 +1491,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                                    h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
                                                    h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap,
-                                                   h->d_anchor, h->d_anchor_next);
+                                                   h->d_anchor, h->d_anchor_next, h->d_pmask);
     }
     stage_end(h, "finalize", ev);
     h->launched_reserves += R;
@@ -1454,8 +1504,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     return ADLBQ_OK;
 }
 
-// recs8 [T][k][8] and nrec [T] land in d_out (device); navail from the column totals
-static int launch_export(adlbq_server *h, int k, int *d_out) {
+// recs8 [T][k][8] then nrec [T] land in d_out, navail [T] in d_navail (device)
+int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
     int rc;
     if ((rc = sync_tables(h))) return rc;
     const int T = h->T, C = T * NB;
@@ -1465,8 +1515,9 @@ static int launch_export(adlbq_server *h, int k, int *d_out) {
     if ((rc = launch_scan(h))) return rc;
     const long long ncsum = np > 0 ? (long long)((np + CHUNK - 1) / CHUNK) * C : 0;
     k_export_gather<<<T, 256, 0, h->stream>>>(T, k, h->d_candoff, h->d_candlen, h->d_cslot, h->d_prio, h->d_seq,
-                                              h->d_cold0, h->d_cold1, d_out, d_out + (size_t)T * k * 8, h->d_csum,
-                                              ncsum, h->d_dem, h->d_anchor, h->d_anchor_next);
+                                              h->d_cold0, h->d_cold1, d_out, d_out + (size_t)T * k * 8, d_navail,
+                                              h->d_coltot, np > 0 ? 1 : 0, h->d_csum, ncsum, h->d_dem, h->d_anchor,
+                                              h->d_anchor_next);
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
 }
@@ -1496,34 +1547,5 @@ int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int 
     return launch_reserve(h, n, d_reqs18, d_resp12);
 }
 
-int adlbq_steal_export(adlbq_server *h, int k, int *recs8, int *nrec, long long *navail) {
-    if (!h || k < 0 || (h->T && (!nrec || !navail || (k && !recs8)))) return fail(ADLBQ_ERR_ARG, "adlbq_steal_export");
-    if (!h->T) return ADLBQ_OK;
-    hipSetDevice(h->device);
-    const int T = h->T;
-    const size_t n_out = (size_t)T * k * 8 + T;
-    if ((long long)n_out > h->cap_export) {
-        AQ_HIP(hipStreamSynchronize(h->stream));
-        if (h->d_export) AQ_HIP(hipFree(h->d_export));
-        AQ_HIP(hipMalloc((void **)&h->d_export, sizeof(int) * n_out));
-        h->cap_export = (long long)n_out;
-    }
-    int rc;
-    if ((rc = launch_export(h, k, h->d_export))) return rc;
-    if (k) AQ_HIP(hipMemcpyAsync(recs8, h->d_export, sizeof(int) * (size_t)T * k * 8, hipMemcpyDeviceToHost, h->stream));
-    AQ_HIP(hipMemcpyAsync(nrec, h->d_export + (size_t)T * k * 8, sizeof(int) * T, hipMemcpyDeviceToHost, h->stream));
-    std::vector<unsigned int> tot((size_t)T * NB, 0);
-    const bool scanned = !h->open.pages.empty();
-    if (scanned)
-        AQ_HIP(hipMemcpyAsync(tot.data(), h->d_coltot, sizeof(unsigned int) * tot.size(), hipMemcpyDeviceToHost,
-                              h->stream));
-    AQ_HIP(hipStreamSynchronize(h->stream));
-    for (int t = 0; t < T; t++) {
-        long long a = 0;
-        for (int b = 0; scanned && b < NB; b++) a += tot[(size_t)t * NB + b];
-        navail[t] = a;
-    }
-    return ADLBQ_OK;
-}
 
 }  // extern "C"

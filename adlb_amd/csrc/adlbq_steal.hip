@@ -46,46 +46,107 @@ using namespace adlbq;
 namespace {
 
 // donor side of SS_RFR: pin_rank = for_rank, pinned = (for_rank >= 0)
-// (adlb.c:1820-1824) for units still live, unpinned and untargeted
+// (adlb.c:1820-1824) for units still live, unpinned and untargeted.
+// found (optional) per pair; bad (optional) counts the pairs that were not.
 __global__ void k_grant(const int *__restrict__ pairs, int n, const long long *__restrict__ seq2slot,
                         long long nseq, uint32_t *meta, int *pin, const int *__restrict__ seqa,
-                        const int4 *__restrict__ cold1, int *__restrict__ found) {
+                        const int4 *__restrict__ cold1, int *__restrict__ found, int *bad) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int rank = pairs[2 * i], seq = pairs[2 * i + 1];
-    const long long slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
     int ok = 0;
-    if (slot >= 0) {
-        const uint32_t m = meta[slot];
-        if ((m & (M_LIVE | M_PINNED)) == M_LIVE && seqa[slot] == seq && cold1[slot].w < 0) {
-            pin[slot] = rank;
-            if (rank >= 0) meta[slot] = m | M_PINNED;
-            ok = 1;
+    if (i < n) {
+        const int rank = pairs[2 * i], seq = pairs[2 * i + 1];
+        const long long slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
+        if (slot >= 0) {
+            const uint32_t m = meta[slot];
+            if ((m & (M_LIVE | M_PINNED)) == M_LIVE && seqa[slot] == seq && cold1[slot].w < 0) {
+                // the pin is claimed atomically: of two grants of one unit the first to land wins
+                ok = rank < 0 || !(atomicOr(&meta[slot], M_PINNED) & M_PINNED);
+                if (ok) pin[slot] = rank;
+            }
         }
+        if (found) found[i] = ok;
     }
-    found[i] = ok;
+    const unsigned long long b = __ballot(i < n && !ok);
+    if (bad && (threadIdx.x & 63) == 0 && b) atomicAdd(bad, __popcll(b));
 }
 
 // rq_find_seqno + rq_delete for many rqseqnos (adlb.c:1883, 1933)
 __global__ void k_rq_delete_batch(const int *__restrict__ rqseqnos, int n, int *rq_live, const DevCounters *ctr,
-                                  int *found, int *ndel) {
+                                  int *found, int *ndel, int *bad) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     int hit = 0;
     if (i < n) {
         const int k = rqseqnos[i] - 1;
         if (k >= 0 && k < ctr->rq_n && atomicExch(&rq_live[k], 0)) hit = 1;
-        found[i] = hit;
+        if (found) found[i] = hit;
     }
-    const unsigned long long b = __ballot(hit);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(ndel, __popcll(b));
+    const unsigned long long b = __ballot(hit), m = __ballot(i < n && !hit);
+    if ((threadIdx.x & 63) == 0) {
+        if (b) atomicAdd(ndel, __popcll(b));
+        if (bad && m) atomicAdd(bad, __popcll(m));
+    }
 }
 
-__global__ void k_rq_delete_fix(int *rq_live, DevCounters *ctr, int *ndel) {
-    ctr->rq_live -= *ndel;
-    *ndel = 0;
-    int head = ctr->rq_head;
-    while (head < ctr->rq_n && !rq_live[head]) head++;
-    ctr->rq_head = head;
+// rq->count bookkeeping and the new FIFO head (first live entry), 1024 slots per step
+__global__ __launch_bounds__(1024) void k_rq_delete_fix(const int *rq_live, DevCounters *ctr, int *ndel) {
+    __shared__ int s_first;
+    const int head = ctr->rq_head, n = ctr->rq_n;
+    if (threadIdx.x == 0) {
+        ctr->rq_live -= *ndel;
+        *ndel = 0;
+        s_first = n;
+    }
+    __syncthreads();
+    for (int base = head; base < n; base += 1024) {
+        const int k = base + threadIdx.x;
+        if (k < n && rq_live[k]) atomicMin(&s_first, k);
+        __syncthreads();
+        const int f = s_first;
+        __syncthreads();  // every thread has read it before the next step may lower it
+        if (f < n) break;
+    }
+    if (threadIdx.x == 0) ctr->rq_head = s_first;
+}
+
+// The live rq entries in FIFO order, compacted: out[0] = count, then up to cap
+// entries {rqseqno, world_rank, req_types[16]}.  One workgroup of 1024.
+__global__ __launch_bounds__(1024) void k_rq_compact(const int *__restrict__ rq_live, const int *__restrict__ rq_rank,
+                                                     const int *__restrict__ rq_types, const DevCounters *ctr,
+                                                     int cap, int *__restrict__ out) {
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int head = ctr->rq_head, n = ctr->rq_n;
+    int base = 0;
+    for (int c0 = head; c0 < n; c0 += 1024) {
+        const int k = c0 + tid;
+        const bool live = k < n && rq_live[k];
+        const unsigned long long b = __ballot(live);
+        if (lane == 0) wsum[w] = __popcll(b);
+        __syncthreads();
+        int pre = base, tot = 0;
+        for (int q = 0; q < 16; q++) {
+            pre += q < w ? wsum[q] : 0;
+            tot += wsum[q];
+        }
+        const int pos = pre + __popcll(b & lanemask_lt());
+        if (live && pos < cap) {
+            int *o = out + 1 + (long long)pos * 18;
+            o[0] = k + 1;
+            o[1] = rq_rank[k];
+            const int4 *src = reinterpret_cast<const int4 *>(rq_types + (long long)k * NREQ);
+#pragma unroll
+            for (int q = 0; q < NREQ / 4; q++) {
+                const int4 v = src[q];
+                o[2 + 4 * q] = v.x;
+                o[3 + 4 * q] = v.y;
+                o[4 + 4 * q] = v.z;
+                o[5 + 4 * q] = v.w;
+            }
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) out[0] = base;
 }
 
 // ---------------------------------------------------------------- merge (host)
@@ -122,7 +183,150 @@ inline int key_shard(unsigned long long k) { return (int)(0xffffffffu - (unsigne
 
 }  // namespace
 
+static int ensure_steal_buffers(adlbq_server *h, int k, int rqcap) {
+    const int T = h->T;
+    const long long n_out = (long long)T * k * 8 + T, n_rq = 1 + (long long)rqcap * 18;
+    const long long n_host = n_out + 2ll * T + n_rq;
+    if (n_out > h->cap_export || n_rq > h->cap_rqx || n_host > h->cap_hsteal) AQ_HIP(hipStreamSynchronize(h->stream));
+    if (n_out > h->cap_export) {
+        if (h->d_export) AQ_HIP(hipFree(h->d_export));
+        AQ_HIP(hipMalloc((void **)&h->d_export, sizeof(int) * n_out));
+        h->cap_export = n_out;
+    }
+    if (!h->d_navail) AQ_HIP(hipMalloc((void **)&h->d_navail, sizeof(long long) * std::max(T, 1)));
+    if (n_rq > h->cap_rqx) {
+        if (h->d_rqx) AQ_HIP(hipFree(h->d_rqx));
+        const long long nc = std::max(n_rq, 2 * h->cap_rqx);
+        AQ_HIP(hipMalloc((void **)&h->d_rqx, sizeof(int) * nc));
+        h->cap_rqx = nc;
+    }
+    if (n_host > h->cap_hsteal) {
+        if (h->h_steal) AQ_HIP(hipHostFree(h->h_steal));
+        const long long nc = std::max(n_host, 2 * h->cap_hsteal);
+        AQ_HIP(hipHostMalloc((void **)&h->h_steal, sizeof(int) * nc, hipHostMallocDefault));
+        h->cap_hsteal = nc;
+    }
+    if (!h->steal_ev) AQ_HIP(hipEventCreateWithFlags(&h->steal_ev, hipEventDisableTiming));
+    return ADLBQ_OK;
+}
+
 extern "C" {
+
+int adlbq_steal_begin(adlbq_server *h, int k) {
+    if (!h || k < 1) return fail(ADLBQ_ERR_ARG, "adlbq_steal_begin");
+    hipSetDevice(h->device);
+    const int T = h->T;
+    // every live rq entry fits: the landed-snapshot bound, else the whole capacity
+    const long long up = rq_live_upper(h);
+    const int rqcap = (int)std::max(0ll, std::min<long long>(up, h->rq_cap));
+    int rc;
+    if ((rc = ensure_steal_buffers(h, k, rqcap))) return rc;
+    if (T && (rc = launch_export(h, k, h->d_export, h->d_navail))) return rc;
+    if (h->rq_cap > 0) {
+        k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, rqcap, h->d_rqx);
+    } else {
+        AQ_HIP(hipMemsetAsync(h->d_rqx, 0, sizeof(int), h->stream));
+    }
+    AQ_HIP(hipGetLastError());
+    const long long n_out = (long long)T * k * 8 + T;
+    int *hs = h->h_steal;
+    if (T) {
+        AQ_HIP(hipMemcpyAsync(hs, h->d_export, sizeof(int) * n_out, hipMemcpyDeviceToHost, h->stream));
+        AQ_HIP(hipMemcpyAsync(hs + n_out, h->d_navail, sizeof(long long) * T, hipMemcpyDeviceToHost, h->stream));
+    }
+    AQ_HIP(hipMemcpyAsync(hs + n_out + 2 * T, h->d_rqx, sizeof(int) * (1 + (size_t)rqcap * 18), hipMemcpyDeviceToHost,
+                          h->stream));
+    AQ_HIP(hipEventRecord(h->steal_ev, h->stream));
+    h->steal_k = k;
+    h->steal_rqcap = rqcap;
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_collect(adlbq_server *h, int *recs8, int *nrec, long long *navail, int cap, int *out18,
+                        int *count) {
+    if (!h || cap < 0 || (cap && !out18)) return fail(ADLBQ_ERR_ARG, "adlbq_steal_collect");
+    if (h->steal_k < 0) return fail(ADLBQ_ERR_ARG, "adlbq_steal_collect: no adlbq_steal_begin in flight");
+    hipSetDevice(h->device);
+    AQ_HIP(hipEventSynchronize(h->steal_ev));
+    const int T = h->T, k = h->steal_k;
+    const long long n_out = (long long)T * k * 8 + T;
+    const int *hs = h->h_steal;
+    if (recs8) std::memcpy(recs8, hs, sizeof(int) * (size_t)T * k * 8);
+    if (nrec) std::memcpy(nrec, hs + (size_t)T * k * 8, sizeof(int) * T);
+    if (navail) std::memcpy(navail, hs + n_out, sizeof(long long) * T);
+    const int *rq = hs + n_out + 2 * T;
+    const int c = rq[0];
+    if (c > h->steal_rqcap) return fail(ADLBQ_ERR_ARG, "adlbq_steal_collect: rq bound violated");
+    if (out18) std::memcpy(out18, rq + 1, sizeof(int) * 18 * (size_t)std::min(c, cap));
+    if (count) *count = c;
+    h->steal_k = -1;
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_export(adlbq_server *h, int k, int *recs8, int *nrec, long long *navail) {
+    if (!h || k < 1 || (h->T && (!nrec || !navail || !recs8))) return fail(ADLBQ_ERR_ARG, "adlbq_steal_export");
+    int rc;
+    if ((rc = adlbq_steal_begin(h, k))) return rc;
+    return adlbq_steal_collect(h, recs8, nrec, navail, 0, nullptr, nullptr);
+}
+
+int adlbq_steal_apply(adlbq_server *h, int ngrant, const int *pairs2, int ndel, const int *rqseqnos) {
+    if (!h || ngrant < 0 || ndel < 0 || (ngrant && !pairs2) || (ndel && !rqseqnos))
+        return fail(ADLBQ_ERR_ARG, "adlbq_steal_apply");
+    if (!ngrant && !ndel) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    const long long need = 2ll * ngrant + ndel;
+    if (h->apply_ev) AQ_HIP(hipEventSynchronize(h->apply_ev));  // the staging of the previous apply is free
+    else AQ_HIP(hipEventCreateWithFlags(&h->apply_ev, hipEventDisableTiming));
+    if (need > h->cap_happly) {
+        if (h->h_apply) AQ_HIP(hipHostFree(h->h_apply));
+        const long long nc = std::max(need, 2 * h->cap_happly);
+        AQ_HIP(hipHostMalloc((void **)&h->h_apply, sizeof(int) * nc, hipHostMallocDefault));
+        h->cap_happly = nc;
+    }
+    if (need > h->cap_dapply) {
+        AQ_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_apply) AQ_HIP(hipFree(h->d_apply));
+        const long long nc = std::max(need, 2 * h->cap_dapply);
+        AQ_HIP(hipMalloc((void **)&h->d_apply, sizeof(int) * nc));
+        h->cap_dapply = nc;
+    }
+    if (!h->d_apply_bad) {
+        AQ_HIP(hipMalloc((void **)&h->d_apply_bad, sizeof(int) * 3));
+        AQ_HIP(hipMemsetAsync(h->d_apply_bad, 0, sizeof(int) * 3, h->stream));
+    }
+    if (ngrant) std::memcpy(h->h_apply, pairs2, sizeof(int) * 2 * (size_t)ngrant);
+    if (ndel) std::memcpy(h->h_apply + 2 * (size_t)ngrant, rqseqnos, sizeof(int) * (size_t)ndel);
+    AQ_HIP(hipMemcpyAsync(h->d_apply, h->h_apply, sizeof(int) * need, hipMemcpyHostToDevice, h->stream));
+    AQ_HIP(hipEventRecord(h->apply_ev, h->stream));
+    if (ngrant)
+        k_grant<<<(ngrant + 255) / 256, 256, 0, h->stream>>>(h->d_apply, ngrant, h->d_seq2slot, h->next_wqseqno,
+                                                            h->d_meta, h->d_pin, h->d_seq, h->d_cold1, nullptr,
+                                                            h->d_apply_bad);
+    if (ndel) {
+        k_rq_delete_batch<<<(ndel + 255) / 256, 256, 0, h->stream>>>(h->d_apply + 2 * (size_t)ngrant, ndel,
+                                                                    h->d_rq_live, h->d_ctr, nullptr,
+                                                                    h->d_apply_bad + 2, h->d_apply_bad + 1);
+        k_rq_delete_fix<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_ctr, h->d_apply_bad + 2);
+        h->ctr_stale = true;
+    }
+    AQ_HIP(hipGetLastError());
+    h->qm_dirty = true;
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_check(adlbq_server *h, int *bad_grants, int *bad_deletes) {
+    if (!h || !bad_grants || !bad_deletes) return fail(ADLBQ_ERR_ARG, "adlbq_steal_check");
+    hipSetDevice(h->device);
+    *bad_grants = *bad_deletes = 0;
+    if (!h->d_apply_bad) return ADLBQ_OK;
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_apply_bad, sizeof(int) * 2, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipMemsetAsync(h->d_apply_bad, 0, sizeof(int) * 2, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *bad_grants = h->h_result[0];
+    *bad_deletes = h->h_result[1];
+    return ADLBQ_OK;
+}
 
 int adlbq_rq_export(adlbq_server *h, int cap, int *out18, int *count) {
     if (!h || cap < 0 || !count || (cap && !out18)) return fail(ADLBQ_ERR_ARG, "adlbq_rq_export");
@@ -161,7 +365,7 @@ int adlbq_grant_batch(adlbq_server *h, int n, const int *pairs2, int *found) {
     AQ_HIP(hipMallocAsync((void **)&d, sizeof(int) * 3 * (size_t)n, h->stream));
     AQ_HIP(hipMemcpyAsync(d, pairs2, sizeof(int) * 2 * (size_t)n, hipMemcpyHostToDevice, h->stream));
     k_grant<<<(n + 255) / 256, 256, 0, h->stream>>>(d, n, h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_pin,
-                                                   h->d_seq, h->d_cold1, d + 2 * (size_t)n);
+                                                   h->d_seq, h->d_cold1, d + 2 * (size_t)n, nullptr);
     AQ_HIP(hipGetLastError());
     AQ_HIP(hipMemcpyAsync(found, d + 2 * (size_t)n, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipFreeAsync(d, h->stream));
@@ -178,8 +382,9 @@ int adlbq_rq_delete_batch(adlbq_server *h, int n, const int *rqseqnos, int *foun
     AQ_HIP(hipMallocAsync((void **)&d, sizeof(int) * (2 * (size_t)n + 1), h->stream));
     AQ_HIP(hipMemcpyAsync(d, rqseqnos, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
     AQ_HIP(hipMemsetAsync(d + 2 * (size_t)n, 0, sizeof(int), h->stream));
-    k_rq_delete_batch<<<(n + 255) / 256, 256, 0, h->stream>>>(d, n, h->d_rq_live, h->d_ctr, d + n, d + 2 * (size_t)n);
-    k_rq_delete_fix<<<1, 1, 0, h->stream>>>(h->d_rq_live, h->d_ctr, d + 2 * (size_t)n);
+    k_rq_delete_batch<<<(n + 255) / 256, 256, 0, h->stream>>>(d, n, h->d_rq_live, h->d_ctr, d + n, d + 2 * (size_t)n,
+                                                              nullptr);
+    k_rq_delete_fix<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_ctr, d + 2 * (size_t)n);
     AQ_HIP(hipGetLastError());
     AQ_HIP(hipMemcpyAsync(found, d + n, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipFreeAsync(d, h->stream));

@@ -597,11 +597,16 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
-                    h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export};
+                    h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export,
+                    h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
     if (h->h_snap) hipHostFree(h->h_snap);
+    if (h->h_steal) hipHostFree(h->h_steal);
+    if (h->h_apply) hipHostFree(h->h_apply);
+    if (h->steal_ev) hipEventDestroy(h->steal_ev);
+    if (h->apply_ev) hipEventDestroy(h->apply_ev);
     for (int i = 0; i < adlbq_server::NSNAP; i++)
         if (h->snap_ev[i]) hipEventDestroy(h->snap_ev[i]);
     for (auto &kv : h->timers)

@@ -160,6 +160,42 @@ class Server:
                    "adlbq_steal_export")
         return recs[: self.T], nrec[: self.T], navail[: self.T]
 
+    def steal_begin(self, k: int) -> None:
+        """Enqueue the export (top-k per type + live rq entries); steal_collect() waits."""
+        _lib.check(self.lib.adlbq_steal_begin(self.h, int(k)), "adlbq_steal_begin")
+        self._steal_k = int(k)
+
+    def steal_collect(self):
+        """-> (recs [T, k, 8], nrec [T], navail [T], rq (n, 18)) of the export in flight."""
+        k = self._steal_k
+        recs = np.empty((max(self.T, 1), k, 8), dtype=np.int32)
+        nrec = np.empty(max(self.T, 1), dtype=np.int32)
+        navail = np.empty(max(self.T, 1), dtype=np.int64)
+        cap = getattr(self, "_rq_cap_hint", 1024)
+        rq = np.empty((cap, 18), dtype=np.int32)
+        c = ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_collect(self.h, _ptr(recs), _ptr(nrec), _ptr(navail), cap, _ptr(rq),
+                                                ctypes.byref(c)), "adlbq_steal_collect")
+        if c.value > cap:   # only the first cap entries were copied: take the rest the slow way
+            self._rq_cap_hint = 2 * c.value
+            rq = self.rq_export()
+        else:
+            rq = rq[: c.value].copy()
+        return recs[: self.T], nrec[: self.T], navail[: self.T], rq
+
+    def steal_apply(self, pairs2, rqseqnos) -> None:
+        """Enqueue this shard's side of a settled round: pin the granted (rank,
+        wqseqno) pairs, drop the settled rq entries (no host synchronisation)."""
+        p = np.ascontiguousarray(np.asarray(pairs2, dtype=np.int32).reshape(-1, 2))
+        q = np.ascontiguousarray(np.asarray(rqseqnos, dtype=np.int32).ravel())
+        _lib.check(self.lib.adlbq_steal_apply(self.h, p.shape[0], _ptr(p), q.size, _ptr(q)), "adlbq_steal_apply")
+
+    def steal_check(self):
+        """Synchronise; (grants whose unit was gone, rqseqnos no longer parked) since the last check."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_check(self.h, ctypes.byref(a), ctypes.byref(b)), "adlbq_steal_check")
+        return a.value, b.value
+
     def rq_export(self) -> np.ndarray:
         """Live parked Reserves in rqseqno order: (n, 18) {rqseqno, world_rank, req_types[16]}."""
         cap = 1024

@@ -130,7 +130,7 @@ def settle(local, num_app_ranks: int, user_types, k: int, recs, nrec, navail, re
     """Run the merge on the gathered exports and apply this process's side of it.
 
     local: {shard index: server} for the shards this process owns (objects with
-    grant_batch and rq_delete_batch, e.g. adlb_amd.server.Server).
+    steal_apply and steal_check, e.g. adlb_amd.server.Server).
     Returns a StealResult: the responses for the Reserves of local shards that
     were settled (the reply SS_RFR_RESP sends the app, adlb.c:1885-1898, with
     the donor's world rank), the numbers of Reserves the merge decided and
@@ -144,15 +144,8 @@ def settle(local, num_app_ranks: int, user_types, k: int, recs, nrec, navail, re
     d, t, i = out[won, 0], out[won, 1], out[won, 2]
     r = recs[d, t, i]                                  # [m, 8] records of the granted units
     q = reqs19[won]
-    grants = {}
-    for s, srv in local.items():
-        g = np.nonzero(d == s)[0]
-        if g.size:
-            grants[s] = np.stack([q[g, 2], r[g, 1]], axis=1).astype(np.int32)
-            found = srv.grant_batch(grants[s])
-            if not found.all():
-                raise RuntimeError(f"shard {s}: {int((found == 0).sum())} granted units were no longer available")
-    t0 = _tick(timing, "grant", t0)
+    grants = {s: np.stack([q[g, 2], r[g, 1]], axis=1).astype(np.int32)
+              for s in local for g in [np.nonzero(d == s)[0]] if g.size}
     mine = np.isin(q[:, 0], np.fromiter(local.keys(), dtype=np.int32, count=len(local)))
     resp = np.empty((int(mine.sum()), 15), dtype=np.int32)
     qm, rm, dm = q[mine], r[mine], d[mine]
@@ -166,23 +159,31 @@ def settle(local, num_app_ranks: int, user_types, k: int, recs, nrec, navail, re
     resp[:, 9] = num_app_ranks + dm                    # donor server's world rank
     resp[:, 10:13] = rm[:, 5:8]                        # common_len, common_server, common_seqno
     resp[:, 13:15] = -1
+    empty = np.zeros((0, 2), np.int32)
+    for s, srv in local.items():                       # enqueue every shard's side, then check
+        srv.steal_apply(grants.get(s, empty), resp[resp[:, 0] == s, 1])
     for s, srv in local.items():
-        g = np.nonzero(resp[:, 0] == s)[0]
-        if g.size:
-            found = srv.rq_delete_batch(resp[g, 1])
-            if not found.all():
-                raise RuntimeError(f"shard {s}: settled Reserves were no longer parked")
-    _tick(timing, "rq_delete", t0)
+        bg, bd = srv.steal_check()
+        if bg or bd:
+            raise RuntimeError(f"shard {s}: {bg} granted units no longer available, "
+                               f"{bd} settled Reserves no longer parked")
+    _tick(timing, "apply", t0)
     return StealResult(resp, nd, int(won.size), grants)
 
 
-def _export(srv, k: int):
-    recs, nrec, navail = srv.steal_export(k)
-    rq = srv.rq_export()
-    reqs = np.empty((rq.shape[0], 19), dtype=np.int32)
-    reqs[:, 0] = srv.my_server_idx
-    reqs[:, 1:] = rq
-    return recs, nrec, navail, reqs
+def _export_all(servers, k: int):
+    """Every local shard's export: all scans enqueued first (one stream each),
+    then collected -> list of (recs, nrec, navail, reqs19)."""
+    for srv in servers:
+        srv.steal_begin(k)
+    out = []
+    for srv in servers:
+        recs, nrec, navail, rq = srv.steal_collect()
+        reqs = np.empty((rq.shape[0], 19), dtype=np.int32)
+        reqs[:, 0] = srv.my_server_idx
+        reqs[:, 1:] = rq
+        out.append((recs, nrec, navail, reqs))
+    return out
 
 
 def steal_round_local(servers, k: int, timing=None):
@@ -194,8 +195,7 @@ def steal_round_local(servers, k: int, timing=None):
     nrec = np.zeros((S, T), np.int32)
     navail = np.zeros((S, T), np.int64)
     reqs = []
-    for srv in servers:
-        a, b, c, q = _export(srv, k)
+    for srv, (a, b, c, q) in zip(servers, _export_all(servers, k)):
         recs[srv.my_server_idx], nrec[srv.my_server_idx], navail[srv.my_server_idx] = a, b, c
         reqs.append(q)
     _tick(timing, "export", t0)
@@ -217,8 +217,7 @@ def steal_round(servers, k: int, group=None, timing=None):
     per = 1 + 3 * T + T * k * 8
     t0 = time.perf_counter()
     parts, reqs = [], []
-    for srv in servers:
-        a, b, c, q = _export(srv, k)
+    for srv, (a, b, c, q) in zip(servers, _export_all(servers, k)):
         nav = np.ascontiguousarray(c.astype(np.int64)).view(np.int32)
         parts.append(np.concatenate([[srv.my_server_idx], b, nav, a.ravel()]).astype(np.int32))
         reqs.append(q.ravel())

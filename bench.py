@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--c3-k", type=int, default=1024, help="config 3: exported units per type per shard")
     ap.add_argument("--c3-steps", type=int, default=5)
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
+    ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
     return ap.parse_args()
 
 
@@ -287,6 +288,13 @@ def main():
     from adlb_amd import shards, synth
     from adlb_amd.server import Server
 
+    if args.config3_only:
+        out = bench_config3(args, torch, dist, world, rank, local, dev)
+        if rank == 0:
+            print(json.dumps({"config3": out}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     R, N = args.reserves, args.units
     w = synth.config2(n_units=N, n_types=args.types, n_reserves=R, seed=shards.shard_seed(args.seed, rank),
                       equal_prio=args.equal_prio)

@@ -127,6 +127,15 @@ int adlbq_rq_delete(adlbq_server *h, int rqseqno, int *found);
  * written (<= k); navail[t] = available units of type t in all. */
 int adlbq_steal_export(adlbq_server *h, int k, int *recs8, int *nrec, long long *navail);
 
+/* The same export split in two so that many handles (shards on one GPU) scan
+ * concurrently: _begin enqueues the scan, the rq compaction and the copies to
+ * pinned host memory on the handle's stream; _collect waits and hands out the
+ * top-k records (any of recs8 / nrec / navail may be NULL) and the live rq
+ * entries as adlbq_rq_export does (out18 up to cap, *count = all live). */
+int adlbq_steal_begin(adlbq_server *h, int k);
+int adlbq_steal_collect(adlbq_server *h, int *recs8, int *nrec, long long *navail, int cap, int *out18,
+                        int *count);
+
 /* The live rq in FIFO (rqseqno) order: out18[i] = {rqseqno, world_rank,
  * req_types[16]} (rq_struct_t, xq.h:79-86).  *count = live entries (only
  * min(count, cap) are written). */
@@ -153,6 +162,15 @@ int adlbq_grant_batch(adlbq_server *h, int n, const int *pairs2, int *found);
 /* Requester side: rq_find_seqno + rq_delete for each rqseqno (adlb.c:1883,
  * 1933); found[i] = 1 if it was parked. */
 int adlbq_rq_delete_batch(adlbq_server *h, int n, const int *rqseqnos, int *found);
+
+/* Both sides of a settled steal round for one shard, enqueued without a host
+ * synchronisation (inputs are staged; the buffers may be reused on return):
+ * the grants it donates and the rqseqnos it settled.  adlbq_steal_check
+ * synchronises and returns how many grants found their unit no longer
+ * available and how many rqseqnos were no longer parked since the last check
+ * (both 0 when every shard applied the same merge). */
+int adlbq_steal_apply(adlbq_server *h, int ngrant, const int *pairs2, int ndel, const int *rqseqnos);
+int adlbq_steal_check(adlbq_server *h, int *bad_grants, int *bad_deletes);
 
 /* Memory-pressure push choice (src/adlb.c:513-528): the first unpinned unit
  * (wq_find_unpinned, xq.c:266-281) and the server with the smallest

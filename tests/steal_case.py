@@ -76,6 +76,19 @@ class ListShard:
     def rq_export(self):
         return self.rq.copy()
 
+    def steal_begin(self, k):
+        self._k = k
+
+    def steal_collect(self):
+        return (*self.steal_export(self._k), self.rq_export())
+
+    def steal_apply(self, pairs, rqseqnos):
+        self._bad = (int((self.grant_batch(pairs) == 0).sum()), int((self.rq_delete_batch(rqseqnos) == 0).sum()))
+
+    def steal_check(self):
+        bad, self._bad = getattr(self, "_bad", (0, 0)), (0, 0)
+        return bad
+
     def grant_batch(self, pairs):
         found = np.zeros(len(pairs), np.int32)
         for i, (rank, seq) in enumerate(np.asarray(pairs).reshape(-1, 2)):

@@ -81,3 +81,20 @@ def test_steal_export_matches_scan(gpu_available):
         o.replay(synth.put_events(w))
         tr = synth.reserve_events(w.r_rank, w.r_types, w.r_hang)
         np.testing.assert_array_equal(replay.replay(srv, tr), o.replay(tr))
+
+
+def test_grant_and_rq_delete_batches(gpu_available):
+    """The synchronous donor / requester entry points: a granted unit is pinned
+    (a Reserve no longer sees it, SS_UNRESERVE by the grantee frees it), a
+    second grant of it fails; deleting a parked rqseqno twice finds it once."""
+    with Server([0, 1], 16, 2, 0, max_units=64) as srv:
+        srv.put(0, 10)                                   # wqseqno 1
+        srv.put(1, 20)                                   # wqseqno 2
+        assert srv.grant_batch([[5, 2], [6, 2], [7, 99]]).tolist() == [1, 0, 0]
+        r = srv.reserve(3, [1])                          # type 1: only wqseqno 2, pinned for rank 5
+        assert r[0] == 0 and r[10] == 1                  # parked, rqseqno 1
+        assert srv.rq_export()[:, :2].tolist() == [[1, 3]]
+        assert srv.rq_delete_batch([1, 1, 7]).tolist() == [1, 0, 0]
+        assert srv.info()[2] == 0
+        assert srv.unreserve(5, 2) == 1
+        assert srv.reserve(4, [1])[5] == 2
