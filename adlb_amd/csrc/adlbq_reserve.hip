@@ -224,45 +224,51 @@ __global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict
         s_last = atomicAdd(&type_cnt[t], 1) == NB - 1;
     }
     __syncthreads();
-    if (!s_last || threadIdx.x != 0) return;
-    type_cnt[t] = 0;  // for the next batch
+    if (!s_last || threadIdx.x >= 64) return;
+    // the last column of type t: wave 0, lane b = bin b (NB == 64), all totals loaded at once
+    static_assert(NB == 64, "one lane per bin");
+    if (lane == 0) type_cnt[t] = 0;  // for the next batch
     const int d = dem[t];
+    const long long x = __hip_atomic_load(coltot + t * NB + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long incl = x;  // inclusive prefix over bins
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const long long cum = incl - x;
     int th = -1, nd = 0, len = 0;
     if (d > 0) {
-        long long cum = 0;
-        bool seen = false;
-        for (int bb = 0; bb < NB; bb++) {
-            const long long x = __hip_atomic_load(coltot + t * NB + bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            binoff[t * NB + bb] = (int)cum;
-            if (x > 0 && !seen) {
-                // the live maximum is at most anchor - (smallest distance of this bin):
-                // the next batch's anchor (applied when this batch ends, k_finalize)
-                seen = true;
-                anchor_next[t] = anchor[t] - (bb < NBX ? bb : (1ll << (bb - NBX + 5)));
-            }
-            if (cum + x >= d) {
-                th = bb;
-                if (bb < NBX) {  // one priority value: the first (d - cum) by wqseqno
-                    nd = (int)(d - cum);
-                    len = d;
-                } else {         // several values: take the whole bin, sort later
-                    nd = INT_MAX;
-                    len = (int)(cum + x);
-                }
-                break;
-            }
-            cum += x;
+        binoff[t * NB + lane] = (int)cum;
+        const unsigned long long nz = __ballot(x > 0), hit = __ballot(incl >= d);
+        if (nz && lane == 0) {
+            // the live maximum is at most anchor - (smallest distance of the first
+            // non-empty bin): the next batch's anchor (applied when this batch ends)
+            const int bb = __ffsll((long long)nz) - 1;
+            anchor_next[t] = anchor[t] - (bb < NBX ? bb : (1ll << (bb - NBX + 5)));
         }
-        if (th < 0) {            // fewer available units than demand: take all
+        if (hit) {
+            th = __ffsll((long long)hit) - 1;
+            const long long cth = __shfl(cum, th, 64), ith = __shfl(incl, th, 64);
+            if (th < NBX) {  // one priority value: the first (d - cum) by wqseqno
+                nd = (int)(d - cth);
+                len = d;
+            } else {         // several values: take the whole bin, sort later
+                nd = INT_MAX;
+                len = (int)ith;
+            }
+        } else {             // fewer available units than demand: take all
             th = NB - 1;
             nd = INT_MAX;
-            len = (int)cum;
+            len = (int)__shfl(incl, 63, 64);
         }
     }
-    theta[t] = th;
-    need[t] = nd;
-    candlen[t] = len;
-    needsort[t] = (th >= NBX && len > 1) ? 1 : 0;
+    if (lane == 0) {
+        theta[t] = th;
+        need[t] = nd;
+        candlen[t] = len;
+        needsort[t] = (th >= NBX && len > 1) ? 1 : 0;
+    }
 }
 
 // ---------------------------------------------------------------- pass 2
