@@ -4,10 +4,11 @@
 // calls of wq_find_pre_targeted_hi_prio / wq_find_hi_prio (src/xq.c:190-247)
 // followed by the pin.  Pipeline (all on the handle's stream):
 //
-//   k_req_prep     request type vectors -> 64-bit type masks, per-type demand,
-//                  per-segment request counts; resets per-batch state
-//   k_hist_open    pass 1 over the open (untargeted) bucket: per page and per
-//                  type, histogram of distance-from-anchor bins (8 B/unit read)
+//   k_prep_hist    one launch, two roles: request type vectors -> 64-bit type
+//                  masks, per-type demand, per-segment request counts, per-batch
+//                  resets (prep_block); and pass 1 over the open (untargeted)
+//                  bucket: per page and per type, histogram of
+//                  distance-from-anchor bins, 8 B/unit read (hist_page)
 //   k_thresholds   per type: the bin where the demand is reached and how many
 //                  units of it are needed (exact bins: by wqseqno order); the
 //                  chunk prefix of every column
@@ -30,12 +31,12 @@
 using namespace adlbq;
 
 
-constexpr int SEG = 256;               // chain segment: requests per wavefront (one k_req_prep block)
+constexpr int SEG = 256;               // chain segment: requests per wavefront (one prep_block)
 constexpr int SEG_BLOCKS = SEG / 64;
 constexpr int CHAIN_MAX_PASSES = 30;   // bound of the settable pass count (adlbq_set_param)
 constexpr int CHAIN_WARM = 512;        // pass-1 warm-up before each segment (T <= 8), a multiple of SEG
-constexpr int PREP_BLOCK = 256;        // k_req_prep workgroup
-static_assert(SEG % 64 == 0 && CHAIN_WARM % SEG == 0, "chain segments are whole waves of k_req_prep");
+constexpr int PREP_BLOCK = 256;        // prep_block workgroup
+static_assert(SEG % 64 == 0 && CHAIN_WARM % SEG == 0, "chain segments are whole waves of prep_block");
 
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
     unsigned int lo = __builtin_amdgcn_readlane((unsigned int)v, l);
@@ -51,15 +52,27 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 // and block 0 resets the chain's per-batch counters.
 constexpr int PREP_ROW = ADLBQ_RESERVE_INTS + 1;
 
+struct PrepArgs {
+    const int *reqs;
+    int R;
+    const int *utypes;
+    int T;
+    unsigned long long *mask;
+    int *dem;
+    int *seg_cnt;
+    DevCounters *ctr;
+    int *tmatch;
+};
+
 template <int TB>  // TB >= T; TB <= 8: the user types are compared in registers
-__global__ __launch_bounds__(PREP_BLOCK) void k_req_prep(const int *__restrict__ reqs, int R,
-                                                         const int *__restrict__ utypes, int T,
-                                                         unsigned long long *__restrict__ mask, int *dem,
-                                                         int *__restrict__ seg_cnt, DevCounters *ctr,
-                                                         int *__restrict__ tmatch) {
+__device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int *__restrict__ rows) {
     __shared__ int su[ADLBQ_MAX_TYPES], sd[ADLBQ_MAX_TYPES];
-    __shared__ int rows[PREP_BLOCK * PREP_ROW];
-    const int j0 = blockIdx.x * PREP_BLOCK, nj = min(PREP_BLOCK, R - j0);
+    const int *__restrict__ reqs = a.reqs, *__restrict__ utypes = a.utypes;
+    const int R = a.R, T = a.T;
+    unsigned long long *__restrict__ mask = a.mask;
+    int *dem = a.dem, *__restrict__ seg_cnt = a.seg_cnt, *__restrict__ tmatch = a.tmatch;
+    DevCounters *ctr = a.ctr;
+    const int j0 = blk * PREP_BLOCK, nj = min(PREP_BLOCK, R - j0);
     const int *src = reqs + (long long)ADLBQ_RESERVE_INTS * j0;
     for (int i = threadIdx.x; i < nj * ADLBQ_RESERVE_INTS; i += PREP_BLOCK) {
         const int r = i / ADLBQ_RESERVE_INTS, c = i - r * ADLBQ_RESERVE_INTS;
@@ -69,7 +82,7 @@ __global__ __launch_bounds__(PREP_BLOCK) void k_req_prep(const int *__restrict__
         su[t] = utypes[t];
         sd[t] = 0;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->chain_rounds = 0;
+    if (blk == 0 && threadIdx.x == 0) ctr->chain_rounds = 0;
     // small T: user types in registers; a type equal to an earlier one never matches
     // (get_type_idx returns the first declared match)
     int ur[TB <= 8 ? TB : 1];
@@ -132,16 +145,29 @@ __global__ __launch_bounds__(PREP_BLOCK) void k_req_prep(const int *__restrict__
 // (most units fall in a few far bins) do not serialise one LDS atomic.
 constexpr int HK = 4;
 
-__global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages, int npages, int tail_fill,
-                                                   const int *__restrict__ prio, const uint32_t *__restrict__ meta,
-                                                   int T, const long long *__restrict__ anchor,
-                                                   const int *__restrict__ dem, unsigned short *__restrict__ gh,
-                                                   unsigned int *__restrict__ csum) {
-    extern __shared__ unsigned int hist[];  // [C][HK]
+struct HistArgs {
+    const int *pages;
+    int npages, tail_fill;
+    const int *prio;
+    const uint32_t *meta;
+    int T;
+    const long long *anchor;
+    unsigned short *gh;
+    unsigned int *csum;
+};
+
+// Every type is counted, demand or not: k_thresholds ignores the columns of a
+// type without demand, and k_rank re-zeroes every chunk sum.
+__device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist /* [C][HK] */) {
     __shared__ long long sanc[ADLBQ_MAX_TYPES];
-    __shared__ int sdem[ADLBQ_MAX_TYPES];
-    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = blockIdx.x;
-    const long long base = (long long)pages[p] << PAGE_SHIFT;
+    const int *__restrict__ prio = a.prio;
+    const uint32_t *__restrict__ meta = a.meta;
+    const int T = a.T, npages = a.npages, tail_fill = a.tail_fill;
+    const long long *__restrict__ anchor = a.anchor;
+    unsigned short *__restrict__ gh = a.gh;
+    unsigned int *__restrict__ csum = a.csum;
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long base = (long long)a.pages[p] << PAGE_SHIFT;
     const int fill = (p == npages - 1) ? tail_fill : PAGE;
     const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
     const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
@@ -156,7 +182,6 @@ __global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages
     }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         sanc[t] = anchor[t];
-        sdem[t] = dem[t];
     }
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
     __syncthreads();
@@ -169,7 +194,7 @@ __global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages
         for (int q = 0; q < 4; q++) {
             if ((mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST) {
                 const int t = mm[q] & M_TYPE;
-                if (sdem[t] > 0) atomicAdd(&my[(t * NB + bin_of(sanc[t] - pr[q])) * HK], 1u);
+                atomicAdd(&my[(t * NB + bin_of(sanc[t] - pr[q])) * HK], 1u);
             }
         }
     }
@@ -183,6 +208,18 @@ __global__ __launch_bounds__(256) void k_hist_open(const int *__restrict__ pages
         g[c] = (unsigned short)v;
         if (v) atomicAdd(&cs[c], v);
     }
+}
+
+// Pass 1 and the request preparation in one launch (they are independent):
+// workgroups [0, nprep) prepare 256 requests each, the rest count one page.
+constexpr int PREP_LDS = (int)sizeof(int) * PREP_BLOCK * PREP_ROW;
+
+template <int TB>
+__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha) {
+    static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
+    extern __shared__ unsigned int lds[];
+    if ((int)blockIdx.x < nprep) prep_block<TB>(pa, blockIdx.x, reinterpret_cast<int *>(lds));
+    else hist_page(ha, blockIdx.x - nprep, lds);
 }
 
 // ---------------------------------------------------------------- thresholds
@@ -310,7 +347,7 @@ __global__ __launch_bounds__(256) void k_select_open(
     }
     // rank of this page's first unit in each of the thread's columns (only
     // columns at or below a threshold): the chunk's exclusive prefix
-    // (k_thresholds) plus the counts of the chunk's earlier pages (k_hist_open)
+    // (k_thresholds) plus the counts of the chunk's earlier pages (hist_page)
     constexpr int CPT = (ADLBQ_MAX_TYPES * NB) / 256;  // columns per thread, at most
     unsigned int ppv[CPT];
     const int p0 = (p / CHUNK) * CHUNK;
@@ -664,7 +701,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     __syncthreads();
     {
         // the chain's level guess counts the requests that take an untargeted
-        // unit: drop those whose types have no candidate at all (k_req_prep
+        // unit: drop those whose types have no candidate at all (prep_block
         // counted every non-empty type set, k_targeted the targeted matches)
         unsigned long long cm = 0;
         for (int t = 0; t < T; t++) cm |= slen[t] > 0 ? (1ull << t) : 0ull;
@@ -1266,7 +1303,7 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
     // the last workgroup of the batch
     const int total = (int)(s_ticket >> 32);
     if (threadIdx.x < T) {
-        dem[threadIdx.x] = 0;  // k_req_prep of the next batch accumulates into it
+        dem[threadIdx.x] = 0;  // prep_block of the next batch accumulates into it
         const long long a = anchor_next[threadIdx.x];
         if (a != LLONG_MIN) {  // lower the anchor to the live maximum k_thresholds saw
             anchor[threadIdx.x] = a;
@@ -1400,18 +1437,26 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
 
 // Both passes over the open bucket for the current demand (d_dem): per-type
 // candidate lists in preference order at d_candoff / d_candlen / d_cslot.
-static int launch_scan(adlbq_server *h) {
+// A reserve batch's request preparation (pa, nprep workgroups) rides in the
+// first launch.
+static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep) {
     const int T = h->T, C = T * NB;
     const int np = (int)h->open.pages.size();
     hipStream_t s = h->stream;
     hipEvent_t ev;
-    if (np > 0 && T > 0) {
-        const int nchunks = (np + CHUNK - 1) / CHUNK;
+    const bool scan = np > 0 && T > 0;
+    const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, h->d_csum};
+    const int grid = nprep + (scan ? np : 0);
+    if (grid > 0) {
+        const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0, scan ? sizeof(unsigned int) * HK * C : 0);
         stage_begin(h, "hist", &ev);
-        k_hist_open<<<np, 256, sizeof(unsigned int) * HK * C, s>>>(
-            h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_dem, h->d_gh,
-            h->d_csum);
+        if (T <= 4) k_prep_hist<4><<<grid, 256, lds, s>>>(pa, nprep, ha);
+        else if (T <= 8) k_prep_hist<8><<<grid, 256, lds, s>>>(pa, nprep, ha);
+        else k_prep_hist<64><<<grid, 256, lds, s>>>(pa, nprep, ha);
         stage_end(h, "hist", ev);
+    }
+    if (scan) {
+        const int nchunks = (np + CHUNK - 1) / CHUNK;
         stage_begin(h, "thresholds", &ev);
         k_thresholds<<<C, 256, 0, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                        h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor,
@@ -1444,20 +1489,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipStream_t s = h->stream;
     hipEvent_t ev;
 
-    stage_begin(h, "prep", &ev);
-    {
-        const int nb = (R + PREP_BLOCK - 1) / PREP_BLOCK;
-        auto prep = [&](auto kern) {
-            kern<<<nb, PREP_BLOCK, 0, s>>>(d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr,
-                                           h->d_tmatch);
-        };
-        if (T <= 4) prep(k_req_prep<4>);
-        else if (T <= 8) prep(k_req_prep<8>);
-        else prep(k_req_prep<64>);
-    }
-    stage_end(h, "prep", ev);
-
-    if ((rc = launch_scan(h))) return rc;
+    const PrepArgs pa{d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch};
+    if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK))) return rc;
     h->last_scan_units = h->live_units - h->live_targeted;
 
     const int nb = (int)h->bucket_ranks.size();
@@ -1518,7 +1551,7 @@ int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
     const int np = (int)h->open.pages.size();
     if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
     k_export_begin<<<1, 64, 0, h->stream>>>(h->d_dem, T, k);
-    if ((rc = launch_scan(h))) return rc;
+    if ((rc = launch_scan(h, PrepArgs{}, 0))) return rc;
     const long long ncsum = np > 0 ? (long long)((np + CHUNK - 1) / CHUNK) * C : 0;
     k_export_gather<<<T, 256, 0, h->stream>>>(T, k, h->d_candoff, h->d_candlen, h->d_cslot, h->d_prio, h->d_seq,
                                               h->d_cold0, h->d_cold1, d_out, d_out + (size_t)T * k * 8, d_navail,

@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-STAGES = ["prep", "hist", "thresholds", "select", "sort", "targeted", "rank", "chain", "finalize"]
+STAGES = ["hist", "thresholds", "select", "sort", "targeted", "rank", "chain", "finalize"]
 
 
 def parse():
@@ -70,7 +70,7 @@ def parse():
 
 
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
-KERNEL_OF = {"prep": "k_req_prep", "hist": "k_hist_open", "thresholds": "k_thresholds",
+KERNEL_OF = {"hist": "k_prep_hist", "thresholds": "k_thresholds",
              "select": "k_select_open", "sort": "k_sort_types",
              "targeted": "k_targeted", "rank": "k_rank", "chain": "k_chain", "finalize": "k_finalize"}
 
@@ -419,7 +419,7 @@ def main():
                    "units_per_shard": N, "reserves_per_step": R, "parallelism": f"shards{world}"},
         "roofline": roofline,
         "roofline_scan": roof(alg["scan"], scan_ms, sum(scan_tr) if scan_tr and None not in scan_tr else None,
-                              "k_hist_open + k_select_open") if scan_ms else None,
+                              "k_prep_hist + k_select_open (time includes the request preparation)") if scan_ms else None,
         "roofline_batch": roof(alg["batch"], batch_ms, None, "all reserve-batch kernels"),
         "kernels_ms": kernels,
         "chain_last_batch": {k: srv.stat("chain_" + k) for k in ("rounds", "passes", "recomputed", "fallback")},

@@ -2,7 +2,7 @@
 
 usage: python tools/step_timeline.py <rocprofv3 output dir>
 
-A step starts at each k_req_prep launch (the first kernel of a reserve batch);
+A step starts at each k_prep_hist launch (the first kernel of a reserve batch);
 the last five complete steps are averaged per kernel position.  'span' is the
 first kernel start to the last kernel end of a step, 'busy' the sum of the
 kernel durations (the difference is the idle time between kernels).
@@ -15,7 +15,7 @@ import sys
 def main(d):
     f = glob.glob(d + "/**/*kernel_trace.csv", recursive=True)[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "k_req_prep" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "k_prep_hist" in r["Kernel_Name"]]
     steps = [rows[a:b] for a, b in zip(idx[-6:-1], idx[-5:])]
     agg = {}
     for st in steps:
