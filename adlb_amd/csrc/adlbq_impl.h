@@ -145,6 +145,8 @@ struct adlbq_server {
     int *d_binoff = nullptr;           // [T*NB]
     unsigned int *d_coltot = nullptr;  // [T*NB] column totals (k_thresholds)
     int *d_type_cnt = nullptr;         // [T] k_thresholds arrival counters (zero between batches)
+    int *d_rank_sync = nullptr;        // [ADLBQ_MAX_TYPES + 2] k_rank's in-launch sort: epochs, ticket, timeouts
+    unsigned int rank_epoch = 0;       // per reserve batch, never 0 once used
     unsigned short *d_gh = nullptr; long long cap_gh = 0;   // [open pages][T*NB]
     unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] sums -> exclusive prefix in place
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;

@@ -481,15 +481,10 @@ __device__ inline void bitonic_desc_4096(unsigned long long *sk, int *ss) {
     }
 }
 
-__global__ __launch_bounds__(1024) void k_sort_types(const int *__restrict__ needsort, const int *__restrict__ candoff,
-                                                     const int *__restrict__ candlen, unsigned long long *key,
-                                                     int *slot, unsigned long long *key2, int *slot2) {
-    const int t = blockIdx.x;
-    if (!needsort[t]) return;
-    const int off = candoff[t], n = candlen[t];
-    if (n <= 1) return;
-    __shared__ unsigned long long sk[4096];
-    __shared__ int ss[4096];
+// Type t's candidate list by key, descending: 4096-entry bitonic blocks in
+// LDS (sk, ss), then pairwise merges through key2/slot2.  Any block size.
+__device__ void sort_type(const int off, const int n, unsigned long long *key, int *slot, unsigned long long *key2,
+                          int *slot2, unsigned long long *sk, int *ss) {
     for (int c0 = 0; c0 < n; c0 += 4096) {
         const int m = min(4096, n - c0);
         for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
@@ -552,6 +547,17 @@ __global__ __launch_bounds__(1024) void k_sort_types(const int *__restrict__ nee
             slot[off + i] = sS[i];
         }
     }
+}
+
+// Export path only (a reserve batch sorts inside k_rank).
+__global__ __launch_bounds__(1024) void k_sort_types(const int *__restrict__ needsort, const int *__restrict__ candoff,
+                                                     const int *__restrict__ candlen, unsigned long long *key,
+                                                     int *slot, unsigned long long *key2, int *slot2) {
+    const int t = blockIdx.x;
+    if (!needsort[t] || candlen[t] <= 1) return;
+    __shared__ unsigned long long sk[4096];
+    __shared__ int ss[4096];
+    sort_type(candoff[t], candlen[t], key, slot, key2, slot2, sk, ss);
 }
 
 // ---------------------------------------------------------------- targeted phase
@@ -680,20 +686,86 @@ __device__ __forceinline__ int lower_bound_key(const unsigned long long *L, int 
     return lo;
 }
 
+// Types whose threshold fell in a multi-priority bin (needsort) are sorted
+// first, inside this launch: the first workgroups to draw a ticket each sort
+// one such type (sort_type), release it and raise its flag; every workgroup
+// waits for those flags (relaxed poll, agent acquire).  Sorters are running
+// before anyone waits for them, so the waits cannot deadlock.  Without such a
+// type (the usual case) nobody draws a ticket or waits.
+struct RankSort {
+    const int *needsort;
+    unsigned long long *ckey2;
+    int *cslot, *cslot2;
+    int *sync;  // [t] sorted epochs, [ADLBQ_MAX_TYPES] ticket, [ADLBQ_MAX_TYPES + 1] timed-out waits
+    unsigned int epoch;
+};
+
 __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict__ candoff,
                                                     const int *__restrict__ candlen,
-                                                    const unsigned long long *__restrict__ ckey,
+                                                    unsigned long long *ckey,  // sorted in this launch: not restrict
                                                     unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
                                                     long long ncsum, const unsigned long long *__restrict__ mask,
-                                                    const int *__restrict__ tmatch, int R, int *seg_cnt) {
+                                                    const int *__restrict__ tmatch, int R, int *seg_cnt, RankSort rs) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
-    __shared__ unsigned long long span[4][RANK_SPAN];
-    __shared__ unsigned long long s_first, s_last;
-    __shared__ int s_a0[4], s_len[4];
+    __shared__ unsigned long long span[4][RANK_SPAN];  // also the sort's LDS blocks
+    static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * 4096,
+                  "sort_type's LDS fits in span");
+    __shared__ unsigned long long s_first, s_last, s_sortmask;
+    __shared__ int s_a0[4], s_len[4], s_tk;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid < 64) {
+        const bool ns = tid < T && rs.needsort[tid] && candlen[tid] > 1;
+        const unsigned long long m = __ballot(ns);
+        if (tid == 0) s_sortmask = m;
+    }
     // the scan's chunk sums are consumed (k_select_open): leave them zeroed for the next batch
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < ncsum; i += (long long)gridDim.x * blockDim.x)
         csum[i] = 0;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    __syncthreads();
+    const unsigned long long sortmask = s_sortmask;
+    if (sortmask) {
+        const int nsort = __popcll(sortmask);
+        if (tid == 0) {
+            const int tk = __hip_atomic_fetch_add(rs.sync + ADLBQ_MAX_TYPES, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tk == (int)gridDim.x - 1)  // every ticket drawn: reset for the next batch
+                __hip_atomic_store(rs.sync + ADLBQ_MAX_TYPES, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_tk = tk;
+        }
+        __syncthreads();
+        const int tk = s_tk;
+        if (tk < nsort) {
+            unsigned long long mm = sortmask;  // the tk-th type that needs sorting
+            for (int q = 0; q < tk; q++) mm &= mm - 1;
+            const int t = __ffsll((long long)mm) - 1;
+            unsigned long long *sk = &span[0][0];
+            int *ss = reinterpret_cast<int *>(sk + 4096);
+            sort_type(candoff[t], candlen[t], ckey, rs.cslot, rs.ckey2, rs.cslot2, sk, ss);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(rs.sync + t, (int)rs.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (tid < 64) {
+            bool ok = true;
+            if ((sortmask >> lane) & 1ull) {
+                for (int spin = 0; __hip_atomic_load(rs.sync + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                                   (int)rs.epoch; spin++) {
+                    if (spin >= (1 << 22)) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            if (!ok) atomicAdd(rs.sync + ADLBQ_MAX_TYPES + 1, 1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
     for (int t = tid; t <= T; t += blockDim.x) {
         soff[t] = candoff[t];
         if (t < T) slen[t] = candlen[t];
@@ -1439,7 +1511,7 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
 // candidate lists in preference order at d_candoff / d_candlen / d_cslot.
 // A reserve batch's request preparation (pa, nprep workgroups) rides in the
 // first launch.
-static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep) {
+static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort) {
     const int T = h->T, C = T * NB;
     const int np = (int)h->open.pages.size();
     hipStream_t s = h->stream;
@@ -1467,10 +1539,12 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep) {
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot);
         stage_end(h, "select", ev);
-        stage_begin(h, "sort", &ev);
-        k_sort_types<<<T, 1024, 0, s>>>(h->d_needsort, h->d_candoff, h->d_candlen, h->d_ckey, h->d_cslot,
-                                        h->d_ckey2, h->d_cslot2);
-        stage_end(h, "sort", ev);
+        if (sort) {  // a reserve batch sorts inside k_rank
+            stage_begin(h, "sort", &ev);
+            k_sort_types<<<T, 1024, 0, s>>>(h->d_needsort, h->d_candoff, h->d_candlen, h->d_ckey, h->d_cslot,
+                                            h->d_ckey2, h->d_cslot2);
+            stage_end(h, "sort", ev);
+        }
     } else {
         AQ_HIP(hipMemsetAsync(h->d_candlen, 0, sizeof(int) * std::max(T, 1), s));
         AQ_HIP(hipMemsetAsync(h->d_candoff, 0, sizeof(int) * (std::max(T, 1) + 1), s));
@@ -1490,7 +1564,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipEvent_t ev;
 
     const PrepArgs pa{d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch};
-    if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK))) return rc;
+    if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false))) return rc;
     h->last_scan_units = h->live_units - h->live_targeted;
 
     const int nb = (int)h->bucket_ranks.size();
@@ -1502,9 +1576,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     if (np > 0 && T > 0) {
         stage_begin(h, "rank", &ev);
+        if (++h->rank_epoch == 0) h->rank_epoch = 1;
+        const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch};
         k_rank<<<512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
                                     (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
-                                    h->d_seg_cnt);
+                                    h->d_seg_cnt, rs);
         stage_end(h, "rank", ev);
     }
     stage_begin(h, "chain", &ev);
@@ -1551,7 +1627,7 @@ int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
     const int np = (int)h->open.pages.size();
     if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
     k_export_begin<<<1, 64, 0, h->stream>>>(h->d_dem, T, k);
-    if ((rc = launch_scan(h, PrepArgs{}, 0))) return rc;
+    if ((rc = launch_scan(h, PrepArgs{}, 0, true))) return rc;
     const long long ncsum = np > 0 ? (long long)((np + CHUNK - 1) / CHUNK) * C : 0;
     k_export_gather<<<T, 256, 0, h->stream>>>(T, k, h->d_candoff, h->d_candlen, h->d_cslot, h->d_prio, h->d_seq,
                                               h->d_cold0, h->d_cold1, d_out, d_out + (size_t)T * k * 8, d_navail,

@@ -576,6 +576,8 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMalloc((void **)&h->d_coltot, sizeof(unsigned int) * T1 * NB));
     AQ_HIP(hipMalloc((void **)&h->d_type_cnt, sizeof(int) * T1));
     AQ_HIP(hipMemset(h->d_type_cnt, 0, sizeof(int) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_rank_sync, sizeof(int) * (ADLBQ_MAX_TYPES + 2)));
+    AQ_HIP(hipMemset(h->d_rank_sync, 0, sizeof(int) * (ADLBQ_MAX_TYPES + 2)));
     AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     long long pages = std::max<long long>(16, (max_units + PAGE - 1) / PAGE + 16);
@@ -595,7 +597,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
-                    h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_gh, h->d_csum,
+                    h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask};
@@ -1010,6 +1012,11 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n == "candidates") {
         int v = 0;
         if (h->T > 0 && hipMemcpy(&v, h->d_candoff + h->T, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        return v;
+    }
+    if (n == "sort_timeouts") {  // k_rank waits for an in-launch sort that gave up (cumulative; 0 unless broken)
+        int v = 0;
+        if (hipMemcpy(&v, h->d_rank_sync + ADLBQ_MAX_TYPES + 1, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
         return v;
     }
     return -1;

@@ -204,7 +204,9 @@ long long adlbq_last_scan_units(adlbq_server *h);
  * ordered-choice kernels, all wavefronts), "chain_passes" (segment passes that
  * recomputed something), "chain_recomputed" (segment solves in those passes),
  * "chain_fallback" (segments the in-order fix-up recomputed; 0 when the passes
- * reached their fixed point), "parked" (Reserves parked), "candidates".
+ * reached their fixed point), "parked" (Reserves parked), "candidates",
+ * "sort_timeouts" (waits of the rank pass for an in-launch sort that gave up,
+ * cumulative; 0 unless something is broken).
  * -1 if unknown. */
 long long adlbq_stat(adlbq_server *h, const char *name);
 /* Tuning: "chain_passes" = parallel segment passes of the ordered-choice

@@ -26,6 +26,7 @@ def run_abi(ut, cfg, trace, max_units=1 << 16, params=None, stats=None):
         for k, v in (params or {}).items():
             s.set_param(k, v)
         out = replay.replay(s, trace)
+        assert s.stat("sort_timeouts") == 0, "k_rank timed out waiting for an in-launch sort"
         if stats is not None:
             stats.update({k: s.stat(k) for k in ("chain_passes", "chain_recomputed", "chain_fallback")})
         return out
