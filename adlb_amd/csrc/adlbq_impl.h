@@ -157,7 +157,7 @@ struct adlbq_server {
     int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
     int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
     int *d_chSf = nullptr, *d_chEf = nullptr;  // [nseg][T] chain: final start / end states
-    int *d_chcnt = nullptr;            // [4] chain: ticket, arrivals, recomputes (zero between batches)
+    unsigned long long *d_chcnt = nullptr;  // [9] chain: two-level arrival counters (zero between batches)
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
     int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")

@@ -874,7 +874,7 @@ struct ChainArgs {
     int *E;                          // [passes + 1][nseg][T] end state of segment s after pass k
     int *flags;                      // [passes + 1][nseg] == epoch once E[k][s] is published
     int *Sf, *Ef;                    // [nseg][T] final start / end of each segment
-    int *counters;                   // [3] segment ticket, arrivals, pass >= 2 recomputes
+    unsigned long long *counters;    // [9] two-level arrival counters (zero between batches)
     DevCounters *ctr;
 };
 
@@ -1104,15 +1104,20 @@ __device__ __forceinline__ void publish_state(int *dst, int *flag, unsigned int 
     if (threadIdx.x == 0) __hip_atomic_store(flag, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wait (bounded) for a flag; false on timeout.  Uniform over the wave.
+// Wait (bounded: CHAIN_WAIT_US of wall clock) for a flag; false on timeout.
+// Uniform over the wave.  A timeout costs time, never correctness: the pass is
+// skipped and the last wavefront's walk repairs what it left.
+constexpr long long CHAIN_WAIT_US = 500;
 __device__ __forceinline__ bool wait_flag(const int *flag, unsigned int epoch) {
     int ok = 0;
     if (threadIdx.x == 0) {
-        for (int spin = 0; spin < (1 << 22); spin++) {
+        const long long t0 = wall_clock64(), limit = CHAIN_WAIT_US * 100;  // 100 MHz constant clock
+        while (true) {
             if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)epoch) {
                 ok = 1;
                 break;
             }
+            if (wall_clock64() - t0 > limit) break;
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -1125,22 +1130,22 @@ __device__ __forceinline__ int load_state(const int *src, int T) {
 
 // The whole ordered choice in one launch, one wavefront per segment.
 //   pass 1: every segment from its level guess, after a warm-up replay;
-//   pass k = 2 .. passes: segment s waits for segment s-1's pass k-1 end state
-//     and recomputes only if it differs from its own start (segments are taken
-//     in order from a ticket, so the predecessor is always held by a running
-//     wavefront and the wait cannot deadlock; a timed-out wait skips the pass);
-//   the last wavefront to finish checks every segment's final start against
-//     its predecessor's final end.  All equal is the fixed point, i.e. the
-//     sequential result (segment 0 starts from 0; induction).  Otherwise it
-//     walks from the first mismatch, whose start is exact, recomputing the
-//     segments whose start differs and skipping the runs that stand.
+//   pass k = 2 .. passes: segment s (= workgroup s) waits for segment s-1's
+//     pass k-1 end state and recomputes only if it differs from its own start
+//     (every wait is bounded in wall-clock time: a timed-out wait skips the
+//     pass, and a predecessor that is not running cannot deadlock anyone);
+//   each segment then compares its final start with its predecessor's final
+//     end (published in the last pass) and reports a mismatch in its arrival
+//     (two-level counter).  No mismatch anywhere is the fixed point, i.e. the
+//     sequential result (segment 0 starts from 0; induction).  Otherwise the
+//     last wavefront to arrive walks from the first mismatch, whose start is
+//     exact, recomputing the segments whose start differs and skipping the
+//     runs that stand.
 template <int TB>
 __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
     extern __shared__ unsigned int win[];
     const int lane = threadIdx.x, T = a.T, K = a.passes, nseg = a.nseg;
-    int tk = 0;
-    if (lane == 0) tk = atomicAdd(&a.counters[0], 1);
-    const int s = __builtin_amdgcn_readfirstlane(tk);
+    const int s = blockIdx.x;
     int rounds = 0, recomputed = 0;
     // pass 1
     const int jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
@@ -1163,20 +1168,48 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
         }
         publish_state(a.E + ((long long)k * nseg + s) * T, a.flags + (long long)k * nseg + s, a.epoch, cur_end, T);
     }
-    // final states, then arrive
+    // own check: does the final start equal the predecessor's final end?
+    int mybad = 0;
+    if (s > 0) {
+        if (wait_flag(a.flags + (long long)K * nseg + s - 1, a.epoch)) {
+            const int pe = load_state(a.E + ((long long)K * nseg + s - 1) * T, T);
+            mybad = __ballot(lane < T && pe != cur_start) ? 1 : 0;
+        } else {
+            mybad = 1;  // unknown: the last wavefront looks
+        }
+    }
+    // final states (for the walk), then arrive
     if (lane < T) {
         __hip_atomic_store(a.Sf + s * T + lane, cur_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(a.Ef + s * T + lane, cur_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // two-level arrival (8 groups, then the top counter), fields packed in one
+    // 64-bit add: arrivals (bits 0-19), mismatches (20-39), recomputes (40-63)
+    constexpr unsigned long long CNT = (1ull << 20) - 1;
     int last = 0;
+    unsigned long long tot = 0;
     if (lane == 0) {
-        if (recomputed) atomicAdd(&a.counters[2], recomputed);
-        atomicAdd(&a.ctr->chain_rounds, rounds);
-        last = atomicAdd(&a.counters[1], 1) == nseg - 1;
+        atomicAdd(&a.ctr->chain_rounds, rounds);  // diagnostic, no return
+        const unsigned long long mine =
+            ((unsigned long long)recomputed << 40) | ((unsigned long long)mybad << 20) | 1ull;
+        const unsigned int g = (unsigned int)s & 7u, ng = ((unsigned int)nseg - g + 7u) / 8u,
+                           ngroups = min((unsigned int)nseg, 8u);
+        const unsigned long long v = atomicAdd(&a.counters[g], mine);
+        if ((v & CNT) == ng - 1u) {
+            const unsigned long long up = ((v + mine) & ~CNT) | 1ull;
+            const unsigned long long tv = atomicAdd(&a.counters[8], up);
+            if ((tv & CNT) == ngroups - 1u) {
+                last = 1;
+                tot = tv + up;
+            }
+        }
     }
     if (!__builtin_amdgcn_readfirstlane(last)) return;
-    // ---- the last wavefront: global fixed-point check, then the walk if needed
+    // ---- the last wavefront: walk from the first mismatch, if any segment saw one
+    const unsigned long long totu = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned int)(tot >> 32)) << 32) |
+                                    __builtin_amdgcn_readfirstlane((unsigned int)tot);
+    const int nbad = (int)((totu >> 20) & CNT);
     auto bad = [&](int q) {  // segment q's final start differs from segment q-1's final end
         bool b = false;
         for (int t = 0; t < T; t++)
@@ -1192,7 +1225,7 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
         }
         return nseg;
     };
-    int redo = 0, q = next_bad(1);
+    int redo = 0, q = nbad ? next_bad(1) : nseg;
     if (q < nseg) {
         int st = load_state(a.Ef + (q - 1) * T, T);
         while (q < nseg) {
@@ -1210,12 +1243,10 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
     }
     if (lane == 0) {
         a.ctr->chain_passes = K;
-        a.ctr->chain_recomputed = __hip_atomic_load(a.counters + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.ctr->chain_recomputed = (int)(totu >> 40);
         a.ctr->chain_fallback = redo;
-        atomicAdd(&a.ctr->chain_rounds, rounds);
-        a.counters[0] = 0;  // for the next batch (kernel boundary in between)
-        a.counters[1] = 0;
-        a.counters[2] = 0;
+        atomicAdd(&a.ctr->chain_rounds, rounds);  // the walk's
+        for (int g = 0; g < 9; g++) a.counters[g] = 0;  // for the next batch (kernel boundary in between)
     }
 }
 
@@ -1468,8 +1499,8 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMemset(h->d_chflag, 0, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));  // epochs start at 1
     AQ_HIP(hipMalloc((void **)&h->d_chSf, sizeof(int) * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chEf, sizeof(int) * nseg * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(int) * 4));
-    AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(int) * 4));  // the chain's last wavefront re-zeroes them
+    AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * 9));
+    AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(unsigned long long) * 9));  // the chain's last wavefront re-zeroes them
     h->cap_req = nc;
     return ADLBQ_OK;
 }
