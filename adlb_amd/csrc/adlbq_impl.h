@@ -25,6 +25,7 @@ namespace adlbq {
 
 constexpr int PAGE_SHIFT = 12;
 constexpr int PAGE = 1 << PAGE_SHIFT;       // 4096 slots per page
+constexpr int SPEC_CAP = 128;              // pass-1 speculative candidates per wave quarter of a page
 constexpr int NB = 64;                      // histogram bins per type (distance from anchor)
 constexpr int NBX = 32;                     // bins [0, NBX) are exact (one priority value each)
 constexpr int CHUNK = 8;                    // pages per prefix chunk in the open-bucket scan
@@ -104,6 +105,10 @@ struct adlbq_server {
     // the live maximum its histogram saw, applied when the batch ends)
     long long *d_anchor = nullptr;
     long long *d_anchor_next = nullptr;   // [T] LLONG_MIN = no update
+    // per type: the prio cut guessed for the next scan (the last reserve
+    // batch's cut less a margin); pass 1 lists the units at or above it
+    long long *d_gcut = nullptr;          // [T] LLONG_MAX = no guess
+    long long *d_gcut_next = nullptr;     // [T] LLONG_MIN = no update
     int *d_utypes = nullptr;
 
     // ---- parked reserves
@@ -148,6 +153,7 @@ struct adlbq_server {
     int *d_rank_sync = nullptr;        // [ADLBQ_MAX_TYPES + 2] k_rank's in-launch sort: epochs, ticket, timeouts
     unsigned int rank_epoch = 0;       // per reserve batch, never 0 once used
     unsigned short *d_gh = nullptr; long long cap_gh = 0;   // [open pages][T*NB]
+    unsigned int *d_spec = nullptr; int *d_specn = nullptr; long long cap_spec = 0;  // [open pages][4][SPEC_CAP], [open pages][4]
     unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] sums -> exclusive prefix in place
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
     int *d_cslot = nullptr, *d_cslot2 = nullptr;

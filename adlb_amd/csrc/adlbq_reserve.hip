@@ -154,12 +154,16 @@ struct HistArgs {
     const long long *anchor;
     unsigned short *gh;
     unsigned int *csum;
+    const long long *gcut;   // [T] guessed cut (LLONG_MAX: none)
+    unsigned int *spec;      // [npages][4][SPEC_CAP] per wave: (column << 12 | slot-in-page), slot order
+    int *specn;              // [npages][4] entries found (> SPEC_CAP: overflowed, not usable)
 };
 
 // Every type is counted, demand or not: k_thresholds ignores the columns of a
 // type without demand, and k_rank re-zeroes every chunk sum.
 __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist /* [C][HK] */) {
     __shared__ long long sanc[ADLBQ_MAX_TYPES];
+    __shared__ int sgc[ADLBQ_MAX_TYPES];
     const int *__restrict__ prio = a.prio;
     const uint32_t *__restrict__ meta = a.meta;
     const int T = a.T, npages = a.npages, tail_fill = a.tail_fill;
@@ -182,22 +186,47 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
     }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         sanc[t] = anchor[t];
+        // 32-bit copy of the guess, rounded down: a looser guess only lists more units
+        sgc[t] = (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN);
     }
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
     __syncthreads();
     unsigned int *my = hist + (lane % HK);
+    // units at or above the guessed cut go to this wave's speculative list, in
+    // slot order: k_select_open reads the list instead of the page when the
+    // guess holds (every real cut at or above it) and the list did not overflow
+    unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
+    const unsigned long long lt = lanemask_lt();
+    int sn = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
         const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+        int col[4];
+        bool in[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            if ((mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST) {
-                const int t = mm[q] & M_TYPE;
-                atomicAdd(&my[(t * NB + bin_of(sanc[t] - pr[q])) * HK], 1u);
+            const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
+            const int t = mm[q] & M_TYPE;
+            col[q] = t * NB + bin_of(sanc[t] - pr[q]);
+            in[q] = av && pr[q] >= sgc[t];
+            if (av) atomicAdd(&my[col[q] * HK], 1u);
+        }
+        const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
+                                 b3 = __ballot(in[3]);
+        if (!(b0 | b1 | b2 | b3)) continue;
+        int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (in[q]) {
+                if (pos < SPEC_CAP)
+                    sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+                pos++;
             }
         }
+        sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
     }
+    if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
     unsigned int *cs = csum + (long long)(p / CHUNK) * C;
     unsigned short *g = gh + (long long)p * C;
@@ -222,6 +251,14 @@ __global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistA
     else hist_page(ha, blockIdx.x - nprep, lds);
 }
 
+// The lowest prio in bins 0..th of a type with anchor an (bin_of: exact bins
+// below NBX, then powers of two); no bin (th < 0) cuts above every prio.
+__device__ __forceinline__ long long cut_of(int th, long long an) {
+    if (th < 0) return 1ll << 40;
+    const long long dmax = th < NBX ? th : th >= NB - 1 ? (1ll << 40) : (1ll << (th - NBX + 6)) - 1;
+    return std::max(an - dmax, (long long)LOWEST + 1);
+}
+
 // ---------------------------------------------------------------- thresholds
 // One workgroup per (type, bin) column: block scan of the column's chunk sums
 // (exclusive prefix in place, read by k_select_open) and its total.  The
@@ -233,7 +270,8 @@ __global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
                                                      int *type_cnt, const long long *__restrict__ anchor,
-                                                     long long *__restrict__ anchor_next) {
+                                                     long long *__restrict__ anchor_next,
+                                                     long long *__restrict__ gcut_next, int guess) {
     __shared__ unsigned int wsum[4];
     __shared__ bool s_last;
     const int c = blockIdx.x, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -301,6 +339,10 @@ __global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict
         }
     }
     if (lane == 0) {
+        if (guess && d > 0) {  // next batch's pass-1 guess: this cut less a margin of half its depth
+            const long long an = anchor[t], cut = cut_of(th, an);
+            gcut_next[t] = cut - std::max(2ll, (an - cut) / 2);
+        }
         theta[t] = th;
         need[t] = nd;
         candlen[t] = len;
@@ -325,7 +367,8 @@ __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ theta, const int *__restrict__ need,
     const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
     const int *__restrict__ candlen, int *__restrict__ candoff_out,
-    unsigned long long *__restrict__ ckey, int *__restrict__ cslot) {
+    unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
+    const unsigned int *__restrict__ spec, const int *__restrict__ specn) {
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
     __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES];
@@ -334,16 +377,35 @@ __global__ __launch_bounds__(256) void k_select_open(
     unsigned int *list = lds + 4 * C + w * 1024;
     const long long base = (long long)pages[p] << PAGE_SHIFT;
     const int fill = (p == npages - 1) ? tail_fill : PAGE;
+    // Pass 1's speculative list of this wave's quarter is usable when it did
+    // not overflow and, for every type with demand, the guessed cut is at or
+    // below the real one (lane t checks type t; T <= 64): then the list holds
+    // every candidate and the page's columns are not read again.
+    // All of the prologue's loads are issued together: lane t's type-t
+    // parameters, the list (read whether or not it is used) and, below, the
+    // page prefix rows.
+    const bool tl = lane < T;
+    const int th_l = tl ? theta[lane] : -1, nd_l = tl ? need[lane] : 0, len_l = tl ? candlen[lane] : 0;
+    const long long an_l = tl ? anchor[lane] : 0, gc_l = tl ? gcut[lane] : 0;
+    const int sn = specn[(long long)p * 4 + w];
+    const unsigned int *__restrict__ sp = spec + ((long long)p * 4 + w) * SPEC_CAP;
+    unsigned int se[SPEC_CAP / 64];
+#pragma unroll
+    for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
+    const long long cut_l = cut_of(th_l, an_l);
+    const bool use_spec = __ballot(th_l >= 0 && gc_l > cut_l) == 0 && sn <= SPEC_CAP;  // wave-uniform
     const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
     const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
     int4 pv[4];
     uint4 mv[4];
+    if (!use_spec) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int idx = (w * 4 + k) * 64 + lane;
-        const bool ok = idx * 4 < fill;
-        pv[k] = ok ? P4[idx] : make_int4(0, 0, 0, 0);
-        mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < 4; k++) {
+            const int idx = (w * 4 + k) * 64 + lane;
+            const bool ok = idx * 4 < fill;
+            pv[k] = ok ? P4[idx] : make_int4(0, 0, 0, 0);
+            mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
+        }
     }
     // rank of this page's first unit in each of the thread's columns (only
     // columns at or below a threshold): the chunk's exclusive prefix
@@ -355,7 +417,9 @@ __global__ __launch_bounds__(256) void k_select_open(
     for (int r = 0; r < CPT; r++) {
         const int c = threadIdx.x + r * 256;
         ppv[r] = 0;
-        if (c < C && (c % NB) <= theta[c / NB]) {
+        if (r * 256 >= C) break;
+        const int thc = __shfl(th_l, (c / NB) & 63, 64);
+        if (c < C && (c % NB) <= thc) {
             unsigned int v = csum[(long long)(p / CHUNK) * C + c];
             unsigned short g[CHUNK - 1];
 #pragma unroll
@@ -365,19 +429,15 @@ __global__ __launch_bounds__(256) void k_select_open(
             ppv[r] = v;
         }
     }
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        const int th = theta[t];
-        const long long an = anchor[t];
-        sanc[t] = an;
-        sth[t] = th;
-        sneed[t] = need[t];
-        // largest anchor distance of bin th (bin_of: exact below NBX, then powers of two)
-        const long long dmax = th < 0 ? -1 : th < NBX ? th : th >= NB - 1 ? (1ll << 40) : (1ll << (th - NBX + 6)) - 1;
-        scut[t] = th < 0 ? (1ll << 40) : std::max(an - dmax, (long long)LOWEST + 1);
+    if (w == 0 && tl) {
+        sanc[lane] = an_l;
+        sth[lane] = th_l;
+        sneed[lane] = nd_l;
+        scut[lane] = cut_l;
     }
     for (int c = threadIdx.x; c < 4 * C; c += blockDim.x) wc[c] = 0;
     if (threadIdx.x < 64) {  // candidate list offsets: exclusive prefix of candlen over types
-        const int len = threadIdx.x < T ? candlen[threadIdx.x] : 0;
+        const int len = len_l;
         int x = len;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -391,6 +451,21 @@ __global__ __launch_bounds__(256) void k_select_open(
     __syncthreads();
     int n = 0;  // this wave's candidates so far (uniform)
     const unsigned long long lt = lanemask_lt();
+    if (use_spec) {  // filter the list: entries in bins up to the type's threshold
+#pragma unroll
+        for (int k = 0; k < SPEC_CAP / 64; k++) {
+            if (k * 64 >= sn) break;
+            const unsigned int e = se[k];
+            const int col = (int)(e >> 12), ct = col / NB;
+            const bool c = k * 64 + lane < sn && col - ct * NB <= sth[ct];
+            const unsigned long long b = __ballot(c);
+            if (c) {
+                list[n + __popcll(b & lt)] = e;
+                atomicAdd(&wc[w * C + col], 1u);
+            }
+            n += __popcll(b);
+        }
+    } else
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
@@ -1344,7 +1419,7 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   DonorCtx dc, int donors, int *rq_rank, int *rq_types,
                                                   int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap,
                                                   long long *anchor, long long *anchor_next,
-                                                  unsigned long long *pmask) {
+                                                  unsigned long long *pmask, long long *gcut, long long *gcut_next) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1411,6 +1486,11 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
         if (a != LLONG_MIN) {  // lower the anchor to the live maximum k_thresholds saw
             anchor[threadIdx.x] = a;
             anchor_next[threadIdx.x] = LLONG_MIN;
+        }
+        const long long g = gcut_next[threadIdx.x];
+        if (g != LLONG_MIN) {  // the next scan's pass-1 guess
+            gcut[threadIdx.x] = g;
+            gcut_next[threadIdx.x] = LLONG_MIN;
         }
     }
     if (total > 0) park_tail(dc, donors, reqs, R, pmask, rq_rank, rq_types, rq_live, rq_req, ctr, resp);
@@ -1509,7 +1589,7 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
     const long long C = (long long)std::max(h->T, 1) * NB;
     const long long need_gh = (long long)npages * C, nchunks = (npages + CHUNK - 1) / CHUNK;
     const long long need_cs = std::max(1ll, nchunks) * C, need_cand = (long long)npages * PAGE;
-    if (need_gh > h->cap_gh || need_cs > h->cap_csum || need_cand > h->cap_cand)
+    if (need_gh > h->cap_gh || need_cs > h->cap_csum || need_cand > h->cap_cand || (long long)npages * 4 > h->cap_spec)
         AQ_HIP(hipStreamSynchronize(h->stream));
     if (need_gh > h->cap_gh) {
         if (h->d_gh) AQ_HIP(hipFree(h->d_gh));
@@ -1523,6 +1603,13 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         AQ_HIP(hipMalloc((void **)&h->d_csum, sizeof(unsigned int) * h->cap_csum));
         // zero once; every batch's k_rank re-zeroes the rows it used
         AQ_HIP(hipMemsetAsync(h->d_csum, 0, sizeof(unsigned int) * h->cap_csum, h->stream));
+    }
+    if ((long long)npages * 4 > h->cap_spec) {
+        if (h->d_spec) AQ_HIP(hipFree(h->d_spec));
+        if (h->d_specn) AQ_HIP(hipFree(h->d_specn));
+        h->cap_spec = std::max((long long)npages * 4, 2 * h->cap_spec);
+        AQ_HIP(hipMalloc((void **)&h->d_spec, sizeof(unsigned int) * SPEC_CAP * h->cap_spec));
+        AQ_HIP(hipMalloc((void **)&h->d_specn, sizeof(int) * h->cap_spec));
     }
     if (need_cand > h->cap_cand) {
         void *ps[] = {h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank};
@@ -1548,7 +1635,8 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     hipStream_t s = h->stream;
     hipEvent_t ev;
     const bool scan = np > 0 && T > 0;
-    const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, h->d_csum};
+    const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, h->d_csum,
+                      h->d_gcut, h->d_spec, h->d_specn};
     const int grid = nprep + (scan ? np : 0);
     if (grid > 0) {
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0, scan ? sizeof(unsigned int) * HK * C : 0);
@@ -1563,12 +1651,13 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         stage_begin(h, "thresholds", &ev);
         k_thresholds<<<C, 256, 0, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                        h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor,
-                                       h->d_anchor_next);
+                                       h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0);
         stage_end(h, "thresholds", ev);
         stage_begin(h, "select", &ev);
         k_select_open<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
-            h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot);
+            h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
+            h->d_gcut, h->d_spec, h->d_specn);
         stage_end(h, "select", ev);
         if (sort) {  // a reserve batch sorts inside k_rank
             stage_begin(h, "sort", &ev);
@@ -1637,7 +1726,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                                    h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
                                                    h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap,
-                                                   h->d_anchor, h->d_anchor_next, h->d_pmask);
+                                                   h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut,
+                                                   h->d_gcut_next);
     }
     stage_end(h, "finalize", ev);
     h->launched_reserves += R;

@@ -548,10 +548,15 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     int T1 = std::max(ntypes, 1);
     AQ_HIP(hipMalloc((void **)&h->d_anchor, sizeof(long long) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_anchor_next, sizeof(long long) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_gcut, sizeof(long long) * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_gcut_next, sizeof(long long) * T1));
     {  // anchors start below every prio; the device keeps them (puts / unreserves raise, batches lower)
         std::vector<long long> lo(T1, (long long)INT_MIN), none(T1, LLONG_MIN);
         AQ_HIP(hipMemcpy(h->d_anchor, lo.data(), sizeof(long long) * T1, hipMemcpyHostToDevice));
         AQ_HIP(hipMemcpy(h->d_anchor_next, none.data(), sizeof(long long) * T1, hipMemcpyHostToDevice));
+        AQ_HIP(hipMemcpy(h->d_gcut_next, none.data(), sizeof(long long) * T1, hipMemcpyHostToDevice));
+        std::vector<long long> noguess(T1, LLONG_MAX);
+        AQ_HIP(hipMemcpy(h->d_gcut, noguess.data(), sizeof(long long) * T1, hipMemcpyHostToDevice));
     }
     AQ_HIP(hipMalloc((void **)&h->d_utypes, sizeof(int) * T1));
     if (ntypes) AQ_HIP(hipMemcpy(h->d_utypes, user_types, sizeof(int) * ntypes, hipMemcpyHostToDevice));
@@ -594,7 +599,7 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
     void *ptrs[] = {h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_open_pages,
                     h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_all_pages,
-                    h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_utypes, h->d_rq_rank, h->d_rq_types,
+                    h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_gcut, h->d_gcut_next, h->d_spec, h->d_specn, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
