@@ -82,6 +82,10 @@ struct adlbq_server {
     int *d_seq = nullptr;
     int4 *d_cold0 = nullptr;  // answer_rank, work_len, home_server_rank, common_len
     int4 *d_cold1 = nullptr;  // common_server_rank, common_seqno, user work_type, target_rank
+    // [2 per slot] the fields a matched Reserve's response carries, in one 32 B
+    // record: {answer_rank, work_len, wqseqno, common_len}, {common_server_rank,
+    // common_seqno, user work_type, prio} (immutable after the Put)
+    int4 *d_rrec = nullptr;
     adlbq::Bucket open;
     std::vector<adlbq::Bucket> rankb;     // per target app rank
     std::vector<int> bucket_ranks;        // ranks that own a bucket, in creation order
@@ -220,6 +224,13 @@ __device__ __forceinline__ int bin_of(long long d) {
     if (d < NBX) return (int)d;
     int o = 63 - __clzll((unsigned long long)d);  // 5 .. 33
     int b = NBX + (o - 5);
+    return b < NB ? b : NB - 1;
+}
+
+// bin_of for a distance known to fit 32 bits (an int anchor less an int prio)
+__device__ __forceinline__ int bin_of32(unsigned int d) {
+    if (d < (unsigned int)NBX) return (int)d;
+    const int b = NBX + (31 - __clz((int)d)) - 5;
     return b < NB ? b : NB - 1;
 }
 

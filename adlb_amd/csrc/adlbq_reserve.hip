@@ -162,8 +162,9 @@ struct HistArgs {
 // Every type is counted, demand or not: k_thresholds ignores the columns of a
 // type without demand, and k_rank re-zeroes every chunk sum.
 __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist /* [C][HK] */) {
-    __shared__ long long sanc[ADLBQ_MAX_TYPES];
-    __shared__ int sgc[ADLBQ_MAX_TYPES];
+    // per type: the anchor (an int: it bounds live prios, which are ints) and
+    // the guessed cut, rounded down to an int (a looser guess only lists more units)
+    __shared__ int2 sag[ADLBQ_MAX_TYPES];
     const int *__restrict__ prio = a.prio;
     const uint32_t *__restrict__ meta = a.meta;
     const int T = a.T, npages = a.npages, tail_fill = a.tail_fill;
@@ -185,9 +186,7 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
         mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
     }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        sanc[t] = anchor[t];
-        // 32-bit copy of the guess, rounded down: a looser guess only lists more units
-        sgc[t] = (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN);
+        sag[t] = make_int2((int)anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
     }
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
     __syncthreads();
@@ -208,8 +207,9 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
         for (int q = 0; q < 4; q++) {
             const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
             const int t = mm[q] & M_TYPE;
-            col[q] = t * NB + bin_of(sanc[t] - pr[q]);
-            in[q] = av && pr[q] >= sgc[t];
+            const int2 ag = sag[t];
+            col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
+            in[q] = av && pr[q] >= ag.y;
             if (av) atomicAdd(&my[col[q] * HK], 1u);
         }
         const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
@@ -1419,7 +1419,8 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   DonorCtx dc, int donors, int *rq_rank, int *rq_types,
                                                   int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap,
                                                   long long *anchor, long long *anchor_next,
-                                                  unsigned long long *pmask, long long *gcut, long long *gcut_next) {
+                                                  unsigned long long *pmask, long long *gcut, long long *gcut_next,
+                                                  const int4 *__restrict__ rrec) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1432,14 +1433,14 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
         int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
         if (slot >= 0) {
             pin[slot] = rank;  // adlb.c:1210-1212
-            if (rank >= 0) meta[slot] |= M_PINNED;
-            const int4 c0 = cold0[slot], c1 = cold1[slot];
+            if (rank >= 0) __hip_atomic_fetch_or(meta + slot, M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int4 c0 = rrec[2ll * slot], c1 = rrec[2ll * slot + 1];  // one 32 B record
             o[0] = 1;
             o[1] = c1.z;
-            o[2] = prio[slot];
+            o[2] = c1.w;
             o[3] = c0.y;
             o[4] = c0.x;
-            o[5] = seqa[slot];
+            o[5] = c0.z;
             o[6] = my_world;
             o[7] = c0.w;
             o[8] = c1.x;
@@ -1727,7 +1728,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
                                                    h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap,
                                                    h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut,
-                                                   h->d_gcut_next);
+                                                   h->d_gcut_next, h->d_rrec);
     }
     stage_end(h, "finalize", ev);
     h->launched_reserves += R;

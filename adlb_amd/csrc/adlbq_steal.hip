@@ -311,7 +311,6 @@ int adlbq_steal_apply(adlbq_server *h, int ngrant, const int *pairs2, int ndel, 
         h->ctr_stale = true;
     }
     AQ_HIP(hipGetLastError());
-    h->qm_dirty = true;
     return ADLBQ_OK;
 }
 
@@ -370,7 +369,6 @@ int adlbq_grant_batch(adlbq_server *h, int n, const int *pairs2, int *found) {
     AQ_HIP(hipMemcpyAsync(found, d + 2 * (size_t)n, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipFreeAsync(d, h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
-    h->qm_dirty = true;
     return ADLBQ_OK;
 }
 

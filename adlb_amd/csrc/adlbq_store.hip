@@ -50,6 +50,7 @@ static int grow_pages(adlbq_server *h, int need) {
     if ((rc = grow(&h->d_seq, o, n, h->stream))) return rc;
     if ((rc = grow(&h->d_cold0, o, n, h->stream))) return rc;
     if ((rc = grow(&h->d_cold1, o, n, h->stream))) return rc;
+    if ((rc = grow(&h->d_rrec, 2 * o, 2 * n, h->stream))) return rc;
     h->cap_pages = nc;
     return ADLBQ_OK;
 }
@@ -263,7 +264,8 @@ struct PutRec {  // staged by the host per Put
 };
 
 __global__ void k_put_scatter(const PutRec *__restrict__ r, int n, int *prio, uint32_t *meta, int *pin,
-                              int *seq, int4 *cold0, int4 *cold1, long long *seq2slot, long long *anchor) {
+                              int *seq, int4 *cold0, int4 *cold1, long long *seq2slot, long long *anchor,
+                              int4 *rrec) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool ok = i < n;
     PutRec u = r[ok ? i : 0];
@@ -275,6 +277,8 @@ __global__ void k_put_scatter(const PutRec *__restrict__ r, int n, int *prio, ui
     seq[u.slot] = u.seq;
     cold0[u.slot] = make_int4(u.answer, u.len, u.home, u.clen);
     cold1[u.slot] = make_int4(u.csrv, u.cseq, u.utype, u.target);
+    rrec[2ll * u.slot] = make_int4(u.answer, u.len, u.seq, u.clen);
+    rrec[2ll * u.slot + 1] = make_int4(u.csrv, u.cseq, u.utype, u.prio);
     seq2slot[u.seq] = u.slot;
 }
 
@@ -597,7 +601,7 @@ int adlbq_destroy(adlbq_server *h) {
     if (!h) return ADLBQ_OK;
     hipSetDevice(h->device);
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
-    void *ptrs[] = {h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_open_pages,
+    void *ptrs[] = {h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_rrec, h->d_open_pages,
                     h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_all_pages,
                     h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_gcut, h->d_gcut_next, h->d_spec, h->d_specn, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
@@ -701,7 +705,8 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
     PutRec *d_rec = reinterpret_cast<PutRec *>(h->d_putrec);
     AQ_HIP(hipMemcpyAsync(d_rec, rec.data(), sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
     k_put_scatter<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, h->d_prio, h->d_meta, h->d_pin, h->d_seq,
-                                                          h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor);
+                                                          h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor,
+                                                          h->d_rrec);
     // a parked Reserve can only exist if the last known count, plus every
     // Reserve launched since, is positive
     bool may_match = h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0);

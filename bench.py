@@ -63,7 +63,8 @@ def parse():
     ap.add_argument("--c3-units", type=int, default=1_562_500, help="config 3: units per server shard")
     ap.add_argument("--c3-reserves", type=int, default=8192, help="config 3: Reserves per shard per step")
     ap.add_argument("--c3-k", type=int, default=1024, help="config 3: exported units per type per shard")
-    ap.add_argument("--c3-steps", type=int, default=5)
+    ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--c3-warmup", type=int, default=3, help="config 3: untimed steps (rq and export buffers grow)")
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
     return ap.parse_args()
@@ -166,8 +167,9 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
 
     SL, N, R, k = args.c3_servers, args.c3_units, args.c3_reserves, args.c3_k
     S, T = SL * world, 4
-    nb = args.c3_steps + 1
-    srvs, streams, d_reqs, d_resp, d_trip = [], [], [], [], []
+    W3 = max(1, args.c3_warmup)
+    nb = args.c3_steps + W3
+    srvs, streams, d_reqs, d_resp, d_trip, g_host, g_dev = [], [], [], [], [], [], []
     for j in range(SL):
         idx = rank * SL + j
         w = synth.config3_shard(idx, S, N, T, R, seed=args.seed)
@@ -189,6 +191,8 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
             tr[:, 0] = torch.from_numpy(w.r_rank).to(dev)
             tr[:, 2] = -1
             d_trip.append(tr)
+            g_host.append(torch.empty((R, 3), dtype=torch.int32).pin_memory())
+            g_dev.append(torch.empty((R, 3), dtype=torch.int32, device=dev))
         srvs.append(srv)
         streams.append(st)
     torch.cuda.synchronize()
@@ -210,11 +214,14 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
             srv.unreserve_batch_device(R, d_trip[j].data_ptr())
             g = res.grants.get(srv.my_server_idx)
             if g is not None and g.size:
-                trip = np.concatenate([g, np.full((g.shape[0], 1), -1, np.int32)], axis=1)
+                # pinned staging, free again: the last round's steal_check synchronised this stream
+                m = g.shape[0]
+                hb = g_host[j].numpy()
+                hb[:m, :2] = g
+                hb[:m, 2] = -1
                 with torch.cuda.stream(streams[j]):
-                    t = torch.from_numpy(trip).to(dev, non_blocking=False)
-                keep.append(t)
-                srv.unreserve_batch_device(g.shape[0], t.data_ptr())
+                    g_dev[j][:m].copy_(g_host[j][:m], non_blocking=True)
+                srv.unreserve_batch_device(m, g_dev[j].data_ptr())
         if timed_parts:
             torch.cuda.synchronize()
             parts["batches"] += t1 - t0
@@ -222,11 +229,12 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
             parts["unreserve"] += time.perf_counter() - t2
         return res
 
-    step(0)                              # warm-up
+    for b in range(W3):                  # warm-up
+        step(b)
     torch.cuda.synchronize()
     keep.clear()
     if args.c3_parts:                    # per-part timing, synchronised (untimed)
-        for b in range(1, nb):
+        for b in range(W3, nb):
             step(b, timed_parts=True)
         torch.cuda.synchronize()
         keep.clear()
@@ -235,7 +243,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     settled = decided = 0
-    for b in range(1, nb):
+    for b in range(W3, nb):
         r = step(b)
         settled += r.settled
         decided += r.decided
@@ -243,12 +251,12 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    local_matched = int(sum(int((d[1:, :, 0] == 1).sum().item()) for d in d_resp))
-    parked = int(sum(int((d[1:, :, 0] == 0).sum().item()) for d in d_resp))
+    local_matched = int(sum(int((d[W3:, :, 0] == 1).sum().item()) for d in d_resp))
+    parked = int(sum(int((d[W3:, :, 0] == 0).sum().item()) for d in d_resp))
     if world > 1:
         el, local_matched = shards.reduce_step_timing(el, local_matched)
         _, parked = shards.reduce_step_timing(0.0, parked)
-    steps = nb - 1
+    steps = nb - W3
     out = {
         "workload": f"config3: {S} server shards ({SL}/GPU) x {N} units, {T} types with one type missing per "
                     f"shard, {R} Reserves/shard/step (~10% only the missing type), steal round k={k}",
@@ -259,7 +267,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         "parked_per_step": parked / steps,
         "stolen_per_step": settled / steps,
         "decided_per_step": decided / steps,
-        "parts_ms_per_step": ({kk: round(v * 1e3 / (nb - 1), 3) for kk, v in {**parts, **sparts}.items()}
+        "parts_ms_per_step": ({kk: round(v * 1e3 / (nb - W3), 3) for kk, v in {**parts, **sparts}.items()}
                               if args.c3_parts else None),
         "scaling": "weak",
     }
