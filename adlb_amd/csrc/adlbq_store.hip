@@ -369,20 +369,23 @@ __global__ void k_unreserve(int slot, int rank, int seq, int newpin, uint32_t *m
 }
 
 __global__ void k_unreserve_batch(const int *__restrict__ trip, int n, const long long *__restrict__ seq2slot,
-                                  long long nseq, uint32_t *meta, int *pin, const int *seqa,
-                                  const int *prio, long long *anchor) {
+                                  long long nseq, uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
+                                  long long *anchor) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     int t = 0, up = INT_MIN;
     if (i < n) {
         int rank = trip[3 * i], seq = trip[3 * i + 1], np = trip[3 * i + 2];
         long long slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
         if (slot >= 0) {
-            uint32_t m = meta[slot];
-            if ((m & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) {
+            // meta, pin and the slot's response record (wqseqno, prio) in one round trip
+            const uint32_t m = meta[slot];
+            const int pn = pin[slot];
+            const int4 r0 = rrec[2 * slot], r1 = rrec[2 * slot + 1];
+            if ((m & M_LIVE) && pn == rank && r0.z == seq) {
                 pin[slot] = np;
                 meta[slot] = m & ~M_PINNED;
                 t = m & M_TYPE;
-                up = prio[slot];
+                up = r1.w;
             }
         }
     }
@@ -774,8 +777,7 @@ int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples) {
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
     k_unreserve_batch<<<(n + 255) / 256, 256, 0, h->stream>>>(d_triples, n, h->d_seq2slot, h->next_wqseqno,
-                                                              h->d_meta, h->d_pin, h->d_seq, h->d_prio,
-                                                              h->d_anchor);
+                                                              h->d_meta, h->d_pin, h->d_rrec, h->d_anchor);
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
 }
