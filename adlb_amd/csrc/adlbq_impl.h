@@ -33,6 +33,10 @@ constexpr int LOWEST = ADLBQ_LOWEST_PRIO;
 constexpr uint32_t M_TYPE = 0xffu;
 constexpr uint32_t M_LIVE = 1u << 8;
 constexpr uint32_t M_PINNED = 1u << 9;
+// bits 10..31: prio - page base, when the page is narrow (every unit's prio
+// within 2^22 of the base): the scans then read 4 B per unit, not 8
+constexpr int M_OFF_SHIFT = 10;
+constexpr long long M_OFF_RANGE = 1ll << 22;
 constexpr int NREQ = ADLBQ_REQ_TYPES;
 
 // device-side scalar counters shared by kernels and read back lazily by the host
@@ -48,6 +52,7 @@ struct DevCounters {
     int chain_passes;      // segment passes of the last chain that recomputed something
     int chain_recomputed;  // segment solves over those passes
     int chain_fallback;    // segments k_chain_fix recomputed (0 at a fixed point)
+    int spec_page0;        // the last scan's page 0, wave 0 read pass 1's list (diagnostic)
 };
 
 struct Bucket {
@@ -91,6 +96,9 @@ struct adlbq_server {
     std::vector<int> bucket_ranks;        // ranks that own a bucket, in creation order
     std::unordered_map<int, int> rank_index;  // target rank -> index into rankb
     bool tables_dirty = true;
+    // per page id: base prio of the packed offsets, and whether some unit did not fit (wide)
+    std::vector<int> page_base, page_wide;
+    int *d_pbase = nullptr, *d_pwide = nullptr; int cap_pbase = 0, cap_pwide = 0; bool pinfo_dirty = true;
     int *d_open_pages = nullptr;  int cap_open_pages = 0;
     int *d_rank_pages = nullptr;  int cap_rank_pages = 0;   // CSR over bucket_ranks
     int *d_rank_pstart = nullptr; int cap_rank_pstart = 0;

@@ -157,7 +157,38 @@ struct HistArgs {
     const long long *gcut;   // [T] guessed cut (LLONG_MAX: none)
     unsigned int *spec;      // [npages][4][SPEC_CAP] per wave: (column << 12 | slot-in-page), slot order
     int *specn;              // [npages][4] entries found (> SPEC_CAP: overflowed, not usable)
+    const int *pbase, *pwide;  // per page id: packed-offset base, wide flag
 };
+
+// A quarter page (16 units per lane) of the scan columns.  A narrow page's
+// prios come from the offsets packed into meta (4 B per unit); only a wide
+// page reads the prio column as well.
+__device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const uint32_t *__restrict__ meta,
+                                             const int *__restrict__ pbase, const int *__restrict__ pwide,
+                                             int pg, int fill, int w, int4 (&pv)[4], uint4 (&mv)[4]) {
+    const int lane = threadIdx.x & 63;
+    const long long base = (long long)pg << PAGE_SHIFT;
+    const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
+    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
+    const int wide = pwide[pg], pb = pbase[pg];  // in flight with the meta loads
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = (w * 4 + k) * 64 + lane;
+        mv[k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+    }
+    if (wide) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int idx = (w * 4 + k) * 64 + lane;
+            pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            pv[k] = make_int4(pb + (int)(mv[k].x >> M_OFF_SHIFT), pb + (int)(mv[k].y >> M_OFF_SHIFT),
+                              pb + (int)(mv[k].z >> M_OFF_SHIFT), pb + (int)(mv[k].w >> M_OFF_SHIFT));
+    }
+}
 
 // Every type is counted, demand or not: k_thresholds ignores the columns of a
 // type without demand, and k_rank re-zeroes every chunk sum.
@@ -172,19 +203,10 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
     unsigned short *__restrict__ gh = a.gh;
     unsigned int *__restrict__ csum = a.csum;
     const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const long long base = (long long)a.pages[p] << PAGE_SHIFT;
     const int fill = (p == npages - 1) ? tail_fill : PAGE;
-    const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
-    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
     int4 pv[4];
     uint4 mv[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int idx = (w * 4 + k) * 64 + lane;
-        const bool ok = idx * 4 < fill;
-        pv[k] = ok ? P4[idx] : make_int4(0, 0, 0, 0);
-        mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
-    }
+    load_quarter(prio, meta, a.pbase, a.pwide, a.pages[p], fill, w, pv, mv);
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         sag[t] = make_int2((int)anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
     }
@@ -368,7 +390,8 @@ __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
     const int *__restrict__ candlen, int *__restrict__ candoff_out,
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
-    const unsigned int *__restrict__ spec, const int *__restrict__ specn) {
+    const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
+    const int *__restrict__ pwide, DevCounters *ctr) {
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
     __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES];
@@ -394,19 +417,10 @@ __global__ __launch_bounds__(256) void k_select_open(
     for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
     const long long cut_l = cut_of(th_l, an_l);
     const bool use_spec = __ballot(th_l >= 0 && gc_l > cut_l) == 0 && sn <= SPEC_CAP;  // wave-uniform
-    const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
-    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
     int4 pv[4];
     uint4 mv[4];
-    if (!use_spec) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int idx = (w * 4 + k) * 64 + lane;
-            const bool ok = idx * 4 < fill;
-            pv[k] = ok ? P4[idx] : make_int4(0, 0, 0, 0);
-            mv[k] = ok ? M4[idx] : make_uint4(0, 0, 0, 0);
-        }
-    }
+    if (!use_spec) load_quarter(prio, meta, pbase, pwide, pages[p], fill, w, pv, mv);
+    if (p == 0 && threadIdx.x == 0) ctr->spec_page0 = use_spec ? 1 : 0;
     // rank of this page's first unit in each of the thread's columns (only
     // columns at or below a threshold): the chunk's exclusive prefix
     // (k_thresholds) plus the counts of the chunk's earlier pages (hist_page)
@@ -1637,7 +1651,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     hipEvent_t ev;
     const bool scan = np > 0 && T > 0;
     const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, h->d_csum,
-                      h->d_gcut, h->d_spec, h->d_specn};
+                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide};
     const int grid = nprep + (scan ? np : 0);
     if (grid > 0) {
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0, scan ? sizeof(unsigned int) * HK * C : 0);
@@ -1658,7 +1672,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         k_select_open<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
-            h->d_gcut, h->d_spec, h->d_specn);
+            h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr);
         stage_end(h, "select", ev);
         if (sort) {  // a reserve batch sorts inside k_rank
             stage_begin(h, "sort", &ev);

@@ -172,6 +172,11 @@ int sync_tables(adlbq_server *h) {
         if ((rc = upload(&h->d_all_fill, &h->cap_all_fill, af, h->stream))) return rc;
         h->tables_dirty = false;
     }
+    if (h->pinfo_dirty) {
+        if ((rc = upload(&h->d_pbase, &h->cap_pbase, h->page_base, h->stream))) return rc;
+        if ((rc = upload(&h->d_pwide, &h->cap_pwide, h->page_wide, h->stream))) return rc;
+        h->pinfo_dirty = false;
+    }
     if (h->qm_dirty) {
         if (h->S * h->T > 0)
             AQ_HIP(hipMemcpyAsync(h->d_qm_hi, h->qm_hi.data(), sizeof(int) * h->S * h->T,
@@ -604,7 +609,7 @@ int adlbq_destroy(adlbq_server *h) {
     if (!h) return ADLBQ_OK;
     hipSetDevice(h->device);
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
-    void *ptrs[] = {h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_rrec, h->d_open_pages,
+    void *ptrs[] = {h->d_pbase, h->d_pwide, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_rrec, h->d_open_pages,
                     h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_all_pages,
                     h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_gcut, h->d_gcut_next, h->d_spec, h->d_specn, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
@@ -666,6 +671,10 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
             if (h->n_pages == h->cap_pages && (rc = grow_pages(h, h->n_pages + 1))) return rc;
             b->pages.push_back(h->n_pages++);
             b->tail_fill = 0;
+            // the page's packed-offset base: its first prio less half the range
+            h->page_base.push_back((int)std::max((long long)u[1] - M_OFF_RANGE / 2, (long long)INT_MIN));
+            h->page_wide.push_back(0);
+            h->pinfo_dirty = true;
         }
         h->tables_dirty = true;
         long long slot = ((long long)b->pages.back() << PAGE_SHIFT) + b->tail_fill++;
@@ -675,6 +684,15 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         r.slot = (int)slot;
         r.prio = u[1];
         r.meta = ti | (int)M_LIVE;
+        {
+            const int pg = b->pages.back();
+            const long long off = (long long)u[1] - h->page_base[pg];
+            if (off >= 0 && off < M_OFF_RANGE) r.meta |= (int)((unsigned int)off << M_OFF_SHIFT);
+            else if (!h->page_wide[pg]) {
+                h->page_wide[pg] = 1;
+                h->pinfo_dirty = true;
+            }
+        }
         r.seq = seq;
         r.answer = u[2];
         r.len = u[4];
@@ -1021,6 +1039,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n == "chain_recomputed") return h->ctr.chain_recomputed;
     if (n == "chain_fallback") return h->ctr.chain_fallback;
     if (n == "parked") return h->ctr.n_parked_last;
+    if (n == "spec_lists") return h->ctr.spec_page0;
     if (n == "candidates") {
         int v = 0;
         if (h->T > 0 && hipMemcpy(&v, h->d_candoff + h->T, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;

@@ -127,14 +127,19 @@ def zipf_weights(T: int, s: float = 1.1) -> np.ndarray:
 
 # ----------------------------------------------------------------------------- configs
 def config2(n_units=1_000_000, n_types=4, n_reserves=65_536, seed=2, prio_hi=1024,
-            equal_prio=False, hang=1) -> Workload:
+            equal_prio=False, hang=1, wide_frac=0.0, wide_range=(-(1 << 30), 1 << 30)) -> Workload:
     """Config 2 / metric: untargeted units, uniform types, prio ~ U[0,prio_hi),
-    R hanging Reserves from ranks 0..R-1 (70% one type, 20% two, 10% wildcard)."""
+    R hanging Reserves from ranks 0..R-1 (70% one type, 20% two, 10% wildcard).
+    wide_frac: that fraction of the units instead draws prio ~ U[wide_range)
+    (pages whose prios span more than the packed-offset range)."""
     rng = np.random.default_rng(seed)
     ut = np.arange(n_types, dtype=np.int32)
     u_type = ut[rng.integers(0, n_types, size=n_units)]
     u_prio = (np.zeros(n_units, np.int32) if equal_prio
               else rng.integers(0, prio_hi, size=n_units).astype(np.int32))
+    if wide_frac > 0:
+        far = rng.random(n_units) < wide_frac
+        u_prio[far] = rng.integers(wide_range[0], wide_range[1], size=int(far.sum())).astype(np.int32)
     R = n_reserves
     w = Workload(user_types=ut, num_app_ranks=max(R, 1),
                  u_type=u_type, u_prio=u_prio,

@@ -28,7 +28,8 @@ def run_abi(ut, cfg, trace, max_units=1 << 16, params=None, stats=None):
         out = replay.replay(s, trace)
         assert s.stat("sort_timeouts") == 0, "k_rank timed out waiting for an in-launch sort"
         if stats is not None:
-            stats.update({k: s.stat(k) for k in ("chain_passes", "chain_recomputed", "chain_fallback")})
+            stats.update({k: s.stat(k) for k in ("chain_passes", "chain_recomputed", "chain_fallback",
+                                                 "spec_lists")})
         return out
 
 
@@ -56,6 +57,9 @@ CASES = {
     "c2_t1": lambda: synth.config2(n_units=50_000, n_types=1, n_reserves=8192, seed=203),
     "c2_t64_wide": lambda: synth.config2(n_units=100_000, n_types=64, n_reserves=8192, seed=204,
                                          prio_hi=1 << 20),
+    # some open pages wide (prio column read), the rest narrow (packed offsets)
+    "c2_mixed_wide_pages": lambda: synth.config2(n_units=200_000, n_reserves=16_384, seed=209, wide_frac=1e-4),
+    "c2_all_wide_pages": lambda: synth.config2(n_units=100_000, n_reserves=8192, seed=210, wide_frac=0.5),
     "c2_exhaust": lambda: synth.config2(n_units=5_000, n_reserves=8192, seed=205, prio_hi=16),
     "c2_exhaust_nohang": lambda: synth.config2(n_units=5_000, n_reserves=8192, seed=206, hang=0),
     "c4_n200k": lambda: synth.config4(n_units=200_000, n_reserves=8192, n_ranks=256, seed=207),
@@ -159,3 +163,50 @@ def test_full_size_config2_equal_prio_exact(gpu_available):
 def test_config4_2m_exact(gpu_available):
     w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
     _exact_full(w)
+
+
+REPEAT = {
+    "c2": lambda: synth.config2(n_units=50_000, n_reserves=4096, seed=221),
+    "c2_eq": lambda: synth.config2(n_units=50_000, n_reserves=4096, seed=222, equal_prio=True),
+    # far prios below the bulk: wide pages, while the cuts stay in the exact bins
+    "c2_mixed_wide_pages": lambda: synth.config2(n_units=50_000, n_reserves=4096, seed=223, wide_frac=3e-4,
+                                                 wide_range=(-(1 << 30), -(1 << 29))),
+    "c2_all_wide_pages": lambda: synth.config2(n_units=50_000, n_reserves=4096, seed=224, wide_frac=0.5),
+    "c2_t64": lambda: synth.config2(n_units=50_000, n_types=64, n_reserves=4096, seed=225, prio_hi=1 << 20),
+    "c4": lambda: synth.config4(n_units=50_000, n_reserves=4096, n_ranks=128, seed=226),
+}
+
+
+@pytest.mark.parametrize("name", sorted(REPEAT))
+def test_repeated_batches_vs_oracle(gpu_available, name):
+    """Four Reserve batches against one queue, each batch's matches given back
+    (SS_UNRESERVE) before the next, as in the bench: from the second batch on
+    the pass-1 guess (last cut less a margin) holds, so k_select_open reads the
+    speculative lists; wide pages read the prio column, narrow ones the packed
+    offsets.  Identical to the oracle, event for event."""
+    w = REPEAT[name]()
+    cfg = (w.num_app_ranks, 1, 0)
+    o = oracle.Oracle("own")
+    o.init(w.user_types, *cfg)
+    trace, exp = [], []
+
+    def step(ev):
+        ev = np.asarray(ev, dtype=np.int32).ravel()
+        out = o.replay(ev)
+        trace.append(ev)
+        exp.append(out)
+        return synth.split_outputs(out)
+
+    step(synth.put_events(w))
+    R, nb = len(w.r_rank), 4
+    for b in range(nb):
+        lo, hi = b * R // nb, (b + 1) * R // nb
+        outs = step(synth.reserve_events(w.r_rank[lo:hi], w.r_types[lo:hi], w.r_hang[lo:hi]))
+        back = [[synth.OP_UNRESERVE, int(r), int(x[5]), -1] for r, x in zip(w.r_rank[lo:hi], outs) if x[0] == 1]
+        assert back, "the batch matched nothing"
+        step(back)
+    st = {}
+    got = run_abi(w.user_types, cfg, np.concatenate(trace), max_units=w.n_units, stats=st)
+    assert_same(got, np.concatenate(exp))
+    if name in ("c2", "c2_mixed_wide_pages"):  # exact-bin cuts: the last batch's guess held
+        assert st["spec_lists"] == 1, st
