@@ -1020,6 +1020,8 @@ __device__ __forceinline__ int level_guess(const ChainArgs &a, int J) {
 // per-type state is uniform (T <= TB <= 8).  win holds, per type, the WL
 // candidates following the start (~0u past the list end); a replay of WL
 // requests consumes at most WL of any type.
+constexpr int CH_NONE = 63;  // no choice (T <= 8: never a type index)
+
 template <int TB>
 __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb, int my_start, unsigned int *win,
                                                int WL, int &my_rec, int &rounds) {
@@ -1053,6 +1055,7 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
         mk[i] = 0ull;
         if (j < j1 && a.tmatch[j] < 0) mk[i] = a.mask[j];
     }
+    const int sent = TB * (SEG + a.warm);  // 64 words of ~0u after the windows (k_chain's prologue)
     // one wave owns win: its LDS ops complete in order, only the compiler must not reorder
     __builtin_amdgcn_wave_barrier();
     my_rec = my_start;
@@ -1067,19 +1070,20 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
         }
         const int j = b0 + lane;
         const unsigned long long m = mk[bi];
-        bool have[TB];
+        // a type the request lacks reads the sentinel row (~0u): no select in the round
+        int base[TB];
 #pragma unroll
-        for (int q = 0; q < TB; q++) have[q] = (m >> q) & 1ull;
-        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
+        for (int q = 0; q < TB; q++) base[q] = ((m >> q) & 1ull) ? q * WL + c0[q] : sent;
+        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : CH_NONE;
         unsigned long long chg;
         do {
             unsigned int v[TB];
 #pragma unroll
-            for (int q = 0; q < TB; q++) v[q] = win[q * WL + c0[q] + (int)mbcnt64(__ballot(ch == q))];
-            unsigned int best = ~0u;
+            for (int q = 0; q < TB; q++) v[q] = win[base[q] + (int)mbcnt64(__ballot(ch == q))];
+            unsigned int best = v[0];
 #pragma unroll
-            for (int q = 0; q < TB; q++) best = min(best, have[q] ? v[q] : ~0u);
-            const int nch = best == ~0u ? -1 : (int)(best & 63u);
+            for (int q = 1; q < TB; q++) best = min(best, v[q]);
+            const int nch = (int)(best & 63u);  // packed rank's type; ~0u (no head) gives CH_NONE
             chg = __ballot(nch != ch);
             ch = nch;
             rounds++;
@@ -1235,6 +1239,7 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
     extern __shared__ unsigned int win[];
     const int lane = threadIdx.x, T = a.T, K = a.passes, nseg = a.nseg;
     const int s = blockIdx.x;
+    if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
     int rounds = 0, recomputed = 0;
     // pass 1
     const int jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
@@ -1727,8 +1732,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, K, warm, h->chain_epoch, h->d_candoff, h->d_candlen,
                      h->d_crank, h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf,
                      h->d_chcnt, h->d_ctr};
-        if (T <= 4) k_chain<4><<<nseg, 64, sizeof(unsigned int) * 4 * (SEG + warm), s>>>(ca);
-        else if (T <= 8) k_chain<8><<<nseg, 64, sizeof(unsigned int) * 8 * (SEG + warm), s>>>(ca);
+        if (T <= 4) k_chain<4><<<nseg, 64, sizeof(unsigned int) * (4 * (SEG + warm) + 64), s>>>(ca);
+        else if (T <= 8) k_chain<8><<<nseg, 64, sizeof(unsigned int) * (8 * (SEG + warm) + 64), s>>>(ca);
         else k_chain<64><<<nseg, 64, sizeof(unsigned int) * T * SEG, s>>>(ca);
     }
     stage_end(h, "chain", ev);

@@ -60,6 +60,9 @@ CASES = {
     # some open pages wide (prio column read), the rest narrow (packed offsets)
     "c2_mixed_wide_pages": lambda: synth.config2(n_units=200_000, n_reserves=16_384, seed=209, wide_frac=1e-4),
     "c2_all_wide_pages": lambda: synth.config2(n_units=100_000, n_reserves=8192, seed=210, wide_frac=0.5),
+    # the whole int32 range: INT_MAX next to ADLB_LOWEST_PRIO and below it (never matched)
+    "c2_extreme_prios": lambda: synth.config2(n_units=60_000, n_reserves=8192, seed=212, wide_frac=0.05,
+                                              wide_range=(-(1 << 31), (1 << 31) - 1)),
     "c2_exhaust": lambda: synth.config2(n_units=5_000, n_reserves=8192, seed=205, prio_hi=16),
     "c2_exhaust_nohang": lambda: synth.config2(n_units=5_000, n_reserves=8192, seed=206, hang=0),
     "c4_n200k": lambda: synth.config4(n_units=200_000, n_reserves=8192, n_ranks=256, seed=207),
