@@ -172,6 +172,7 @@ struct adlbq_server {
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate
     int *d_seg_cnt = nullptr;          // [R/64] chain: untargeted-capable requests per 64 requests
     unsigned long long *d_pmask = nullptr;  // [R/64] k_finalize: ballots of the requests that park
+    int *d_lv = nullptr;               // [R][T] k_rank: level rows for the chain's guess (T <= 8)
     int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
     int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
     int *d_chSf = nullptr, *d_chEf = nullptr;  // [nseg][T] chain: final start / end states

@@ -781,6 +781,15 @@ __device__ __forceinline__ int lower_bound_key(const unsigned long long *L, int 
 // waits for those flags (relaxed poll, agent acquire).  Sorters are running
 // before anyone waits for them, so the waits cannot deadlock.  Without such a
 // type (the usual case) nobody draws a ticket or waits.
+// The chain's level guess for T <= 8: row g (g < R) holds, for the candidate
+// at global rank g, the number of candidates of each type ranked before it --
+// the lower bounds k_rank computes anyway -- i.e. the state in which the first
+// g candidates in preference order are taken.
+struct LevelRows {
+    int *lv;  // [R][T], or nullptr (T > 8)
+    int R;
+};
+
 struct RankSort {
     const int *needsort;
     unsigned long long *ckey2;
@@ -794,7 +803,8 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
                                                     unsigned long long *ckey,  // sorted in this launch: not restrict
                                                     unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
                                                     long long ncsum, const unsigned long long *__restrict__ mask,
-                                                    const int *__restrict__ tmatch, int R, int *seg_cnt, RankSort rs) {
+                                                    const int *__restrict__ tmatch, int R, int *seg_cnt, RankSort rs,
+                                                    LevelRows lr) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
     __shared__ unsigned long long span[4][RANK_SPAN];  // also the sort's LDS blocks
     static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * 4096,
@@ -901,6 +911,9 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         __syncthreads();
         const unsigned long long kf = s_first, kl = s_last;
         unsigned int g = (unsigned int)(i0 + tid);
+        int lbv[8];  // per type: candidates ranked before this one (level rows, T <= 8)
+#pragma unroll
+        for (int u = 0; u < 8; u++) lbv[u] = u == t ? i0 + tid : 0;
         for (int r0 = 0; r0 < T; r0 += 4) {  // wave w takes type r0 + w; every wave meets every barrier
             const int u = r0 + w;
             int a0 = 0, len = -1;
@@ -943,10 +956,18 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
                 const int lb = lq <= RANK_SPAN ? lower_bound_key(span[q], lq, key)
                                                : lower_bound_key(ckey + soff[r0 + q] + aq, lq, key);
                 g += (unsigned int)(aq + lb);
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (u == r0 + q) lbv[u] = aq + lb;
             }
             __syncthreads();
         }
         if (tid < n) crank[soff[t] + i0 + tid] = (g << 6) | (unsigned int)t;
+        if (lr.lv != nullptr && tid < n && (int)g < lr.R) {
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (u < T) lr.lv[(long long)g * T + u] = lbv[u];
+        }
         __syncthreads();
     }
 }
@@ -965,6 +986,7 @@ struct ChainArgs {
     int *Sf, *Ef;                    // [nseg][T] final start / end of each segment
     unsigned long long *counters;    // [9] two-level arrival counters (zero between batches)
     DevCounters *ctr;
+    const int *lv;                   // [R][T] k_rank's level rows (T <= 8), else nullptr
 };
 
 // Level guess for the state after J untargeted choices: pos_t = number of
@@ -1247,7 +1269,14 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
     for (int q = lane; q < (jb >> 6); q += 64) J += a.seg_cnt[q];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
-    int cur_start, cur_end = seg_solve<TB>(a, s, jb, level_guess<(TB <= 8 ? TB : 8)>(a, J), win, cur_start, rounds);
+    int guess;
+    if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
+        const int G = a.candoff[T], len = lane < T ? a.candlen[lane] : 0;
+        guess = lane >= T || J == 0 ? 0 : J >= G ? len : a.lv[(long long)J * T + lane];
+    } else {
+        guess = level_guess<(TB <= 8 ? TB : 8)>(a, J);
+    }
+    int cur_start, cur_end = seg_solve<TB>(a, s, jb, guess, win, cur_start, rounds);
     publish_state(a.E + ((long long)1 * nseg + s) * T, a.flags + (long long)1 * nseg + s, a.epoch, cur_end, T);
     for (int k = 2; k <= K; k++) {
         if (s > 0 && wait_flag(a.flags + (long long)(k - 1) * nseg + s - 1, a.epoch)) {
@@ -1583,7 +1612,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
     void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
-                  h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_pmask};
+                  h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_pmask, h->d_lv};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
@@ -1601,6 +1630,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_chEf, sizeof(int) * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * 9));
     AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(unsigned long long) * 9));  // the chain's last wavefront re-zeroes them
+    AQ_HIP(hipMalloc((void **)&h->d_lv, sizeof(int) * 8 * (size_t)nc));
     h->cap_req = nc;
     return ADLBQ_OK;
 }
@@ -1720,7 +1750,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch};
         k_rank<<<512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
                                     (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
-                                    h->d_seg_cnt, rs);
+                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R});
         stage_end(h, "rank", ev);
     }
     stage_begin(h, "chain", &ev);
@@ -1731,7 +1761,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         if (++h->chain_epoch == 0) h->chain_epoch = 1;
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, K, warm, h->chain_epoch, h->d_candoff, h->d_candlen,
                      h->d_crank, h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf,
-                     h->d_chcnt, h->d_ctr};
+                     h->d_chcnt, h->d_ctr, (T <= 8 && np > 0) ? h->d_lv : nullptr};
         if (T <= 4) k_chain<4><<<nseg, 64, sizeof(unsigned int) * (4 * (SEG + warm) + 64), s>>>(ca);
         else if (T <= 8) k_chain<8><<<nseg, 64, sizeof(unsigned int) * (8 * (SEG + warm) + 64), s>>>(ca);
         else k_chain<64><<<nseg, 64, sizeof(unsigned int) * T * SEG, s>>>(ca);
