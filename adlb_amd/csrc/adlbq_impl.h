@@ -173,6 +173,13 @@ struct adlbq_server {
     int *d_seg_cnt = nullptr;          // [R/64] chain: untargeted-capable requests per 64 requests
     unsigned long long *d_pmask = nullptr;  // [R/64] k_finalize: ballots of the requests that park
     int *d_lv = nullptr;               // [R][T] k_rank: level rows for the chain's guess (T <= 8)
+    // targeted units' sorted index (k_targeted_idx): keys/vals double buffers,
+    // per (bucket, type) ranges, radix-sort scratch; rebuilt after targeted Puts
+    unsigned long long *d_tkeys = nullptr, *d_tkeys2 = nullptr;
+    int *d_tvals = nullptr, *d_tvals2 = nullptr; long long cap_tidx = 0;
+    int *d_tstart = nullptr, *d_tend = nullptr; long long cap_trange = 0;
+    void *d_tsort = nullptr; size_t cap_tsort = 0;
+    bool tindex_dirty = true;
     int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
     int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
     int *d_chSf = nullptr, *d_chEf = nullptr;  // [nseg][T] chain: final start / end states

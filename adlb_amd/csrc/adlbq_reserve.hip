@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <climits>
 
+#include <hipcub/hipcub.hpp>
+
 #include "adlbq_donor.h"
 #include "adlbq_impl.h"
 
@@ -711,6 +713,135 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
                 __threadfence();
                 __syncthreads();
             }
+            if (threadIdx.x == 0) nlist = 0;
+            __syncthreads();
+        }
+    }
+}
+
+// ---------------------------------------------------------------- targeted phase over a sorted index
+// The pre-targeted match (wq_find_pre_targeted_hi_prio, xq.c:219-247) of a
+// rank's Reserves, in order, against that rank's bucket.  Instead of one scan
+// of the bucket per Reserve, the bucket's units are kept in an index sorted
+// by (bucket, type, prio desc, bucket position asc) -- one stable radix sort,
+// rebuilt only after targeted Puts (k_tindex_keys, hipcub) -- with the range
+// of every (bucket, type) (k_tindex_ranges).  A Reserve's best unit is then
+// the best head among its types' ranges: lane t of wave 0 keeps type t's
+// head, skips units no longer available (pinned, deleted, prio <= LOWEST),
+// and the wave takes the minimum of (prio desc, position asc).
+constexpr int TIDX_TYPE_BITS = 6, TIDX_PRIO_BITS = 32;
+constexpr int TIDX_BUCKET_SHIFT = TIDX_TYPE_BITS + TIDX_PRIO_BITS;  // bucket index above type and prio
+constexpr int TIDX_KEY_BITS = TIDX_BUCKET_SHIFT + 20;               // buckets < 2^20
+
+__global__ __launch_bounds__(256) void k_tindex_keys(const int *__restrict__ pstart, const int *__restrict__ rpages,
+                                                     const int *__restrict__ rfill, int nb,
+                                                     const int *__restrict__ prio, const uint32_t *__restrict__ meta,
+                                                     unsigned long long *keys, int *vals) {
+    // block = one page of the concatenated rank-bucket page list
+    const int gp = blockIdx.x;
+    int lo = 0, hi = nb;  // bucket b with pstart[b] <= gp < pstart[b+1]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pstart[mid] <= gp) lo = mid; else hi = mid;
+    }
+    const int b = lo, pi = gp - pstart[b], last = pstart[b + 1] - 1;
+    const int fill = gp == last ? rfill[b] : PAGE;
+    const long long base = (long long)rpages[gp] << PAGE_SHIFT;
+    for (int q = threadIdx.x; q < PAGE; q += blockDim.x) {
+        const long long o = (long long)gp * PAGE + q;
+        if (q < fill) {
+            const unsigned int t = meta[base + q] & M_TYPE;
+            const unsigned int inv = ~((unsigned int)prio[base + q] ^ 0x80000000u);  // prio descending
+            keys[o] = ((unsigned long long)b << TIDX_BUCKET_SHIFT) | ((unsigned long long)t << TIDX_PRIO_BITS) | inv;
+            vals[o] = pi * PAGE + q;  // position in the bucket (wqseqno order)
+        } else {
+            keys[o] = ~0ull;  // holes sort last
+            vals[o] = -1;
+        }
+    }
+}
+
+__global__ void k_tindex_ranges(const unsigned long long *__restrict__ keys, long long n, int *tstart, int *tend) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = keys[i];
+    if (k >> TIDX_KEY_BITS) return;  // a hole
+    const unsigned int g = (unsigned int)(k >> TIDX_PRIO_BITS);  // bucket << 6 | type
+    if (i == 0 || (unsigned int)(keys[i - 1] >> TIDX_PRIO_BITS) != g) tstart[g] = (int)i;
+    if (i == n - 1 || (keys[i + 1] >> TIDX_KEY_BITS) || (unsigned int)(keys[i + 1] >> TIDX_PRIO_BITS) != g)
+        tend[g] = (int)(i + 1);
+}
+
+__global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bucket_ranks,
+                                                      const int *__restrict__ pstart, const int *__restrict__ rpages,
+                                                      const unsigned long long *__restrict__ tkeys,
+                                                      const int *__restrict__ tvals, const int *__restrict__ tstart,
+                                                      const int *__restrict__ tend, int T, uint32_t *meta,
+                                                      const unsigned long long *__restrict__ mask,
+                                                      const int *__restrict__ reqs, int R, int *tmatch, int *seg_cnt) {
+    __shared__ int list[1024];
+    __shared__ int nlist, wcnt[4];
+    const int b = blockIdx.x, r = bucket_ranks[b], p0 = pstart[b];
+    if (pstart[b + 1] - p0 <= 0) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // lane t of wave 0: type t's range and head
+    const bool tl = w == 0 && lane < T;
+    int hd = tl ? tstart[b * 64 + lane] : 0;
+    const int end = tl ? tend[b * 64 + lane] : 0;
+    if (threadIdx.x == 0) nlist = 0;
+    __syncthreads();
+    for (int j0 = 0; j0 < R; j0 += 256) {
+        const int j = j0 + threadIdx.x;
+        const bool is = j < R && reqs[(long long)ADLBQ_RESERVE_INTS * j] == r;
+        const unsigned long long bal = __ballot(is);
+        if (lane == 0) wcnt[w] = __popcll(bal);
+        __syncthreads();
+        int woff = nlist;
+        for (int q = 0; q < w; q++) woff += wcnt[q];
+        if (is) list[woff + __popcll(bal & lanemask_lt())] = j;
+        __syncthreads();
+        if (threadIdx.x == 0) nlist += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        __syncthreads();
+        if (nlist > 768 || j0 + 256 >= R) {
+            if (w == 0) {
+                for (int e = 0; e < nlist; e++) {
+                    const int jj = list[e];
+                    const unsigned long long m = mask[jj];
+                    unsigned long long best = ~0ull;
+                    int slot = -1;
+                    if (tl && ((m >> lane) & 1ull)) {
+                        for (; hd < end; hd++) {  // skip units no longer available
+                            const unsigned int low = (unsigned int)tkeys[hd];
+                            const int pr = (int)(~low ^ 0x80000000u);
+                            if (pr <= LOWEST) {  // prio descending: nothing after it matches either
+                                hd = end;
+                                break;
+                            }
+                            const int L = tvals[hd];
+                            const long long sl = ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
+                            const uint32_t mt = (uint32_t)ld_agent(reinterpret_cast<const int *>(meta + sl));
+                            if ((mt & (M_LIVE | M_PINNED)) == M_LIVE) {
+                                best = ((unsigned long long)low << 32) | (unsigned int)L;
+                                slot = (int)sl;
+                                break;
+                            }
+                        }
+                    }
+                    unsigned long long bb = best;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) {
+                        const unsigned long long y = __shfl_xor(bb, o, 64);
+                        bb = y < bb ? y : bb;
+                    }
+                    if (bb != ~0ull && best == bb) {  // the one lane holding the best head (positions are unique)
+                        tmatch[jj] = slot;
+                        atomicSub(&seg_cnt[jj >> 6], 1);
+                        st_agent(reinterpret_cast<int *>(meta + slot), (int)(meta[slot] | M_PINNED));
+                        hd++;
+                    }
+                }
+            }
+            __syncthreads();
             if (threadIdx.x == 0) nlist = 0;
             __syncthreads();
         }
@@ -1722,6 +1853,63 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     return ADLBQ_OK;
 }
 
+// The targeted units' sorted index (k_targeted_idx), rebuilt after targeted
+// Puts: keys/vals over every slot of every rank-bucket page (holes sort last),
+// one stable radix sort, then the (bucket, type) ranges.
+static int ensure_tindex(adlbq_server *h) {
+    if (!h->tindex_dirty) return ADLBQ_OK;
+    hipStream_t s = h->stream;
+    const int nb = (int)h->bucket_ranks.size();
+    int npg = 0;
+    for (int k = 0; k < nb; k++) npg += (int)h->rankb[k].pages.size();
+    const long long n = (long long)npg * PAGE;
+    if (n > h->cap_tidx) {
+        AQ_HIP(hipStreamSynchronize(s));
+        void *ps[] = {h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2};
+        for (void *p : ps)
+            if (p) AQ_HIP(hipFree(p));
+        h->cap_tidx = std::max(n, 2 * h->cap_tidx);
+        AQ_HIP(hipMalloc((void **)&h->d_tkeys, sizeof(unsigned long long) * h->cap_tidx));
+        AQ_HIP(hipMalloc((void **)&h->d_tkeys2, sizeof(unsigned long long) * h->cap_tidx));
+        AQ_HIP(hipMalloc((void **)&h->d_tvals, sizeof(int) * h->cap_tidx));
+        AQ_HIP(hipMalloc((void **)&h->d_tvals2, sizeof(int) * h->cap_tidx));
+    }
+    if ((long long)nb * 64 > h->cap_trange) {
+        AQ_HIP(hipStreamSynchronize(s));
+        if (h->d_tstart) AQ_HIP(hipFree(h->d_tstart));
+        if (h->d_tend) AQ_HIP(hipFree(h->d_tend));
+        h->cap_trange = std::max((long long)nb * 64, 2 * h->cap_trange);
+        AQ_HIP(hipMalloc((void **)&h->d_tstart, sizeof(int) * h->cap_trange));
+        AQ_HIP(hipMalloc((void **)&h->d_tend, sizeof(int) * h->cap_trange));
+    }
+    size_t tmp = 0;
+    hipcub::DoubleBuffer<unsigned long long> dk(h->d_tkeys, h->d_tkeys2);
+    hipcub::DoubleBuffer<int> dv(h->d_tvals, h->d_tvals2);
+    AQ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, dk, dv, (int)n, 0, TIDX_KEY_BITS, s));
+    if (tmp > h->cap_tsort) {
+        AQ_HIP(hipStreamSynchronize(s));
+        if (h->d_tsort) AQ_HIP(hipFree(h->d_tsort));
+        h->cap_tsort = std::max(tmp, 2 * h->cap_tsort);
+        AQ_HIP(hipMalloc(&h->d_tsort, h->cap_tsort));
+    }
+    if (npg > 0) {
+        k_tindex_keys<<<npg, 256, 0, s>>>(h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill, nb, h->d_prio, h->d_meta,
+                                          h->d_tkeys, h->d_tvals);
+        size_t t2 = h->cap_tsort;
+        AQ_HIP(hipcub::DeviceRadixSort::SortPairs(h->d_tsort, t2, dk, dv, (int)n, 0, TIDX_KEY_BITS, s));
+        if (dk.Current() != h->d_tkeys) {  // keep the sorted arrays in d_tkeys / d_tvals
+            std::swap(h->d_tkeys, h->d_tkeys2);
+            std::swap(h->d_tvals, h->d_tvals2);
+        }
+    }
+    AQ_HIP(hipMemsetAsync(h->d_tstart, 0, sizeof(int) * (size_t)nb * 64, s));
+    AQ_HIP(hipMemsetAsync(h->d_tend, 0, sizeof(int) * (size_t)nb * 64, s));
+    if (n > 0) k_tindex_ranges<<<(int)((n + 255) / 256), 256, 0, s>>>(h->d_tkeys, n, h->d_tstart, h->d_tend);
+    AQ_HIP(hipGetLastError());
+    h->tindex_dirty = false;
+    return ADLBQ_OK;
+}
+
 int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
     if ((rc = ensure_req_capacity(h, R))) return rc;
@@ -1739,9 +1927,15 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
 
     const int nb = (int)h->bucket_ranks.size();
     if (h->live_targeted > 0 && nb > 0) {
+        if (nb < (1 << 20) && (rc = ensure_tindex(h))) return rc;
         stage_begin(h, "targeted", &ev);
-        k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
-                                      h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);
+        if (nb < (1 << 20))
+            k_targeted_idx<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_tkeys,
+                                              h->d_tvals, h->d_tstart, h->d_tend, T, h->d_meta, h->d_mask, d_reqs, R,
+                                              h->d_tmatch, h->d_seg_cnt);
+        else
+            k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
+                                          h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);
         stage_end(h, "targeted", ev);
     }
     if (np > 0 && T > 0) {

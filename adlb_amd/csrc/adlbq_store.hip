@@ -617,7 +617,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export,
-                    h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv};
+                    h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv,
+                    h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -705,7 +706,10 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         if ((long long)h->seq2slot.size() <= seq) h->seq2slot.resize((size_t)seq * 2 + 16, -1);
         h->seq2slot[seq] = slot;
         h->live_units++;
-        if (tgt >= 0) h->live_targeted++;
+        if (tgt >= 0) {
+            h->live_targeted++;
+            h->tindex_dirty = true;
+        }
         if (h->live_units > h->max_count) h->max_count = h->live_units;
     }
     if ((long long)h->next_wqseqno > h->cap_seq) {

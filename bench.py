@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--c3-warmup", type=int, default=3, help="config 3: untimed steps (rq and export buffers grow)")
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
+    ap.add_argument("--config4-only", action="store_true", help="only the config-4 leg (profiling)")
+    ap.add_argument("--c4-units", type=int, default=10_000_000, help="config 4: units (80%% targeted)")
+    ap.add_argument("--c4-steps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -94,7 +98,7 @@ def pmc_traffic(args) -> dict | None:
     if prof is None:
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu", "--no-pmc",
-             "--no-config3",
+             "--no-config3", "--no-config4",
              "--no-profile", "--units", str(args.units), "--reserves", str(args.reserves), "--types",
              str(args.types), "--seed", str(args.seed)] + (["--equal-prio"] if args.equal_prio else [])
     out = {}
@@ -276,6 +280,101 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     return out
 
 
+def zipf_type_sets(rng, n_types, R, lo=1, hi=4):
+    """(R, 16) request vectors of lo..hi distinct types drawn without replacement
+    with Zipf(1.1) weights (Gumbel top-k: the same law as synth.type_vectors with
+    ntypes_range, vectorised), padded with -2."""
+    from adlb_amd import synth
+    w = synth.zipf_weights(n_types)
+    keys = np.log(w)[None, :] + rng.gumbel(size=(R, n_types))
+    order = np.argsort(-keys, axis=1)[:, :hi].astype(np.int32)
+    k = rng.integers(lo, hi + 1, size=R)
+    out = np.full((R, 16), -2, np.int32)
+    for c in range(hi):
+        sel = k > c
+        out[sel, c] = order[sel, c]
+    return out
+
+
+def bench_config4(args, torch, dist, world, rank, local, dev):
+    """Config 4: c4_units units with 80% targeted (target ~
+    Zipf(1.1) over 1,024 app ranks), 32 types with Zipf(1.1) popularity, prio ~
+    U[0, 2^16); 65,536 hanging Reserves per step from ranks U[0, 1024) with 1-4
+    Zipf types each, a different pre-staged batch per step.  A step = the
+    reserve batch (pre-targeted scan per rank bucket, then the untargeted
+    scan, wide-T chain) + SS_UNRESERVE of every match, so each step sees the
+    same queue.  Reports matched assignments/s and the per-stage times."""
+    from adlb_amd import shards, synth
+    from adlb_amd.server import Server
+
+    R, N, W4 = args.reserves, args.c4_units, 2
+    nb = args.c4_steps + W4
+    w = synth.config4(n_units=N, n_reserves=R, seed=shards.shard_seed(args.seed + 40, rank))
+    srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
+    stream = torch.cuda.Stream(dev)
+    srv.set_stream(stream.cuda_stream)
+    srv.put_batch(np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1),
+                            np.zeros(N), np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32))
+    rng = np.random.default_rng(args.seed + 41 + rank)
+    reqs = np.empty((nb, R, 18), np.int32)
+    for b in range(nb):
+        reqs[b, :, 0] = rng.integers(0, w.num_app_ranks, size=R)
+        reqs[b, :, 1] = 1
+        reqs[b, :, 2:] = zipf_type_sets(rng, len(w.user_types), R) if b else w.r_types
+    with torch.cuda.stream(stream):
+        d_reqs = torch.from_numpy(reqs).to(dev)
+        d_resp = torch.empty((nb, R, 12), dtype=torch.int32, device=dev)
+        d_trip = torch.empty((nb, R, 3), dtype=torch.int32, device=dev)
+        d_trip[:, :, 0] = d_reqs[:, :, 0]
+        d_trip[:, :, 2] = -1
+    torch.cuda.synchronize()
+
+    def step(b):
+        srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        with torch.cuda.stream(stream):
+            d_trip[b, :, 1].copy_(d_resp[b][:, 5])
+        srv.unreserve_batch_device(R, d_trip[b].data_ptr())
+
+    for b in range(W4):
+        step(b)
+    torch.cuda.synchronize()
+    srv.profile(True)
+    base = {st: srv.profile_read(st) for st in STAGES}
+    step(W4 - 1)
+    stages = {}
+    for st in STAGES:
+        ms, n = srv.profile_read(st)
+        if n - base[st][1]:
+            stages[st] = round((ms - base[st][0]) / (n - base[st][1]), 4)
+    srv.profile(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(W4, nb):
+        step(b)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    matched = int((d_resp[W4:, :, 0] == 1).sum().item())
+    if world > 1:
+        el, matched = shards.reduce_step_timing(el, matched)
+    steps = nb - W4
+    out = {
+        "workload": f"config4: {N} units/shard (80% targeted, Zipf(1.1) over 1024 ranks), 32 Zipf types, "
+                    f"prio U[0,2^16), {R} hanging Reserves/step with 1-4 types",
+        "value": matched / el,
+        "unit": "assignments/s",
+        "ms_per_step": el * 1e3 / steps,
+        "matched_per_step": matched / steps,
+        "stages_ms": stages,
+        "scaling": "weak",
+    }
+    srv.close()
+    return out
+
+
 def main():
     args = parse()
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -296,6 +395,13 @@ def main():
     from adlb_amd import shards, synth
     from adlb_amd.server import Server
 
+    if args.config4_only:
+        out = bench_config4(args, torch, dist, world, rank, local, dev)
+        if rank == 0:
+            print(json.dumps({"config4": out}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if args.config3_only:
         out = bench_config3(args, torch, dist, world, rank, local, dev)
         if rank == 0:
@@ -440,6 +546,11 @@ def main():
             res["config3"] = bench_config3(args, torch, dist, world, rank, local, dev)
         except Exception as e:  # reported, not fatal: the metric line above stands
             res["config3"] = {"error": f"{type(e).__name__}: {e}"}
+    if not args.no_config4:
+        try:
+            res["config4"] = bench_config4(args, torch, dist, world, rank, local, dev)
+        except Exception as e:  # reported, not fatal
+            res["config4"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     if rank == 0:
