@@ -53,6 +53,7 @@ struct DevCounters {
     int chain_recomputed;  // segment solves over those passes
     int chain_fallback;    // segments k_chain_fix recomputed (0 at a fixed point)
     int spec_page0;        // the last scan's page 0, wave 0 read pass 1's list (diagnostic)
+    int needsort_last;     // the last reserve batch had a type whose threshold fell in a multi-prio bin
 };
 
 struct Bucket {
@@ -180,6 +181,10 @@ struct adlbq_server {
     int *d_tstart = nullptr, *d_tend = nullptr; long long cap_trange = 0;
     void *d_tsort = nullptr; size_t cap_tsort = 0;
     bool tindex_dirty = true;
+    // segmented radix sort of the multi-prio-bin candidate lists (launched
+    // when the newest landed batch needed one; k_rank sorts otherwise)
+    int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;
+    long long ssort_items = 0;
     int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
     int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
     int *d_chSf = nullptr, *d_chEf = nullptr;  // [nseg][T] chain: final start / end states
@@ -222,7 +227,8 @@ int ensure_req_capacity(adlbq_server *h, int n);
 int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
-long long rq_live_upper(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
+long long rq_live_upper(adlbq_server *h);
+bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);

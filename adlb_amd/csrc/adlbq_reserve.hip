@@ -944,7 +944,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     __shared__ int s_a0[4], s_len[4], s_tk;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid < 64) {
-        const bool ns = tid < T && rs.needsort[tid] && candlen[tid] > 1;
+        const bool ns = tid < T && rs.needsort[tid] == 1 && candlen[tid] > 1;  // 2: already sorted
         const unsigned long long m = __ballot(ns);
         if (tid == 0) s_sortmask = m;
     }
@@ -1599,7 +1599,7 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap,
                                                   long long *anchor, long long *anchor_next,
                                                   unsigned long long *pmask, long long *gcut, long long *gcut_next,
-                                                  const int4 *__restrict__ rrec) {
+                                                  const int4 *__restrict__ rrec, const int *__restrict__ needsort) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1677,6 +1677,9 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
     __syncthreads();
     if (threadIdx.x == 0) {
         if (total == 0) ctr->n_parked_last = 0;
+        int ns = 0;
+        for (int t = 0; t < T; t++) ns |= needsort[t];
+        ctr->needsort_last = ns;  // the host launches the segmented sort while this holds
         for (int g = 0; g < 8; g++) ctr->fin_group[g] = 0;
         ctr->fin_top = 0;
         *snap = *ctr;  // mapped host memory; visible to the host once the kernel has completed
@@ -1910,6 +1913,60 @@ static int ensure_tindex(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
+__global__ void k_segsort_prep(int T, const int *__restrict__ candoff, const int *__restrict__ candlen,
+                               const int *__restrict__ needsort, int *sbeg, int *send) {
+    const int t = threadIdx.x;
+    if (t >= T) return;
+    sbeg[t] = candoff[t];
+    send[t] = (needsort[t] == 1 && candlen[t] > 1) ? candoff[t] + candlen[t] : candoff[t];
+}
+
+// the sorted segments back into the candidate lists; needsort 2 = sorted
+__global__ __launch_bounds__(256) void k_segsort_back(const int *__restrict__ sbeg, const int *__restrict__ send,
+                                                      const unsigned long long *__restrict__ k2,
+                                                      const int *__restrict__ s2, unsigned long long *key, int *slot,
+                                                      int *needsort) {
+    const int t = blockIdx.x, b = sbeg[t], e = send[t];
+    if (e <= b) return;
+    for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+        key[i] = k2[i];
+        slot[i] = s2[i];
+    }
+    if (threadIdx.x == 0) needsort[t] = 2;
+}
+
+// Multi-prio-bin candidate lists sorted by one segmented radix sort (64-bit
+// keys, descending) over every type at once, instead of one k_rank workgroup
+// per type.  Types that do not need it get empty segments.
+static int launch_segsort(adlbq_server *h) {
+    const int T = h->T;
+    hipStream_t s = h->stream;
+    if (!h->d_sbeg) {
+        AQ_HIP(hipMalloc((void **)&h->d_sbeg, sizeof(int) * ADLBQ_MAX_TYPES));
+        AQ_HIP(hipMalloc((void **)&h->d_send, sizeof(int) * ADLBQ_MAX_TYPES));
+    }
+    const long long n = h->cap_cand;  // bound of every list's end
+    size_t tmp = 0;
+    AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey, h->d_ckey2, h->d_cslot,
+                                                                 h->d_cslot2, (int)n, T, h->d_sbeg, h->d_send, 0, 64,
+                                                                 s));
+    if (tmp > h->cap_ssort) {
+        AQ_HIP(hipStreamSynchronize(s));
+        if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
+        h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
+        AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
+    }
+    k_segsort_prep<<<1, 64, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_needsort, h->d_sbeg, h->d_send);
+    size_t t2 = h->cap_ssort;
+    AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey, h->d_ckey2, h->d_cslot,
+                                                                 h->d_cslot2, (int)n, T, h->d_sbeg, h->d_send, 0, 64,
+                                                                 s));
+    k_segsort_back<<<T, 256, 0, s>>>(h->d_sbeg, h->d_send, h->d_ckey2, h->d_cslot2, h->d_ckey, h->d_cslot,
+                                     h->d_needsort);
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
 int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
     if ((rc = ensure_req_capacity(h, R))) return rc;
@@ -1937,6 +1994,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
                                           h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);
         stage_end(h, "targeted", ev);
+    }
+    if (np > 0 && T > 0 && sort_hint(h)) {
+        stage_begin(h, "sort", &ev);
+        if ((rc = launch_segsort(h))) return rc;
+        stage_end(h, "sort", ev);
     }
     if (np > 0 && T > 0) {
         stage_begin(h, "rank", &ev);
@@ -1971,7 +2033,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
                                                    h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap,
                                                    h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut,
-                                                   h->d_gcut_next, h->d_rrec);
+                                                   h->d_gcut_next, h->d_rrec, h->d_needsort);
     }
     stage_end(h, "finalize", ev);
     h->launched_reserves += R;

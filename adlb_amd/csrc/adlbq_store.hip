@@ -90,6 +90,18 @@ long long rq_live_upper(adlbq_server *h) {
     return LLONG_MAX;  // nothing landed yet: assume a match is possible
 }
 
+// Whether the newest landed reserve batch needed a multi-prio-bin sort.
+bool sort_hint(adlbq_server *h) {
+    const int N = adlbq_server::NSNAP;
+    for (int k = 1; k <= N; k++) {
+        const int i = (h->snap_next - k + N) % N;
+        if (!h->snap_at[i]) continue;
+        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
+        return h->h_snap[i].needsort_last != 0;
+    }
+    return false;
+}
+
 int ensure_rq_capacity(adlbq_server *h, int extra) {
     long long need = (h->ctr_stale ? h->rq_n_upper : (long long)h->ctr.rq_n) + extra;
     if (need <= h->rq_cap) return ADLBQ_OK;
@@ -618,7 +630,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv,
-                    h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort};
+                    h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
+                    h->d_sbeg, h->d_send, h->d_ssort};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);

@@ -76,7 +76,7 @@ def parse():
 
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
 KERNEL_OF = {"hist": "k_prep_hist", "thresholds": "k_thresholds",
-             "select": "k_select_open", "sort": "k_sort_types",
+             "select": "k_select_open", "sort": "hipcub segmented radix sort",
              "targeted": "k_targeted_idx", "rank": "k_rank", "chain": "k_chain", "finalize": "k_finalize"}
 
 
