@@ -183,7 +183,8 @@ struct adlbq_server {
     bool tindex_dirty = true;
     // segmented radix sort of the multi-prio-bin candidate lists (launched
     // when the newest landed batch needed one; k_rank sorts otherwise)
-    int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;
+    int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort
+    long long n_segsort = 0;                          // lists given a device-wide sort (cumulative)
     long long ssort_items = 0;
     int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
     int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
@@ -192,6 +193,9 @@ struct adlbq_server {
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
     int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")
+    int segsort_merged = 1;            // one merged sort of every list when the keys allow ("segsort_merged")
+    unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
+    int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]
     long long *d_navail = nullptr;                       // [T]

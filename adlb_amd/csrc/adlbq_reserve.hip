@@ -1913,56 +1913,203 @@ static int ensure_tindex(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
-__global__ void k_segsort_prep(int T, const int *__restrict__ candoff, const int *__restrict__ candlen,
-                               const int *__restrict__ needsort, int *sbeg, int *send) {
-    const int t = threadIdx.x;
-    if (t >= T) return;
-    sbeg[t] = candoff[t];
-    send[t] = (needsort[t] == 1 && candlen[t] > 1) ? candoff[t] + candlen[t] : candoff[t];
-}
+// The ranges sorted by launch_segsort, passed by value.
+struct SegList {
+    int n;
+    int type[ADLBQ_MAX_TYPES], beg[ADLBQ_MAX_TYPES], end[ADLBQ_MAX_TYPES];
+};
 
-// the sorted segments back into the candidate lists; needsort 2 = sorted
-__global__ __launch_bounds__(256) void k_segsort_back(const int *__restrict__ sbeg, const int *__restrict__ send,
-                                                      const unsigned long long *__restrict__ k2,
+// the sorted ranges back into the candidate lists; needsort 2 = sorted
+__global__ __launch_bounds__(256) void k_segsort_back(SegList sl, const unsigned long long *__restrict__ k2,
                                                       const int *__restrict__ s2, unsigned long long *key, int *slot,
                                                       int *needsort) {
-    const int t = blockIdx.x, b = sbeg[t], e = send[t];
-    if (e <= b) return;
-    for (int i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int q = blockIdx.y;
+    if (q >= sl.n) return;
+    const int b = sl.beg[q], e = sl.end[q];
+    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x) {
         key[i] = k2[i];
         slot[i] = s2[i];
     }
-    if (threadIdx.x == 0) needsort[t] = 2;
+    if (blockIdx.x == 0 && threadIdx.x == 0) needsort[sl.type[q]] = 2;
 }
 
-// Multi-prio-bin candidate lists sorted by one segmented radix sort (64-bit
-// keys, descending) over every type at once, instead of one k_rank workgroup
-// per type.  Types that do not need it get empty segments.
+__global__ void k_segsort_bounds(SegList sl, int from, int *sbeg, int *send) {
+    const int q = from + threadIdx.x;
+    if (q >= sl.n) return;
+    sbeg[q - from] = sl.beg[q];
+    send[q - from] = sl.end[q];
+}
+
+// Multi-prio-bin candidate lists sorted before k_rank (64-bit keys,
+// descending).  The list bounds are read back first (one stream sync).  When
+// no list's keys differ in their top 6 bits (k_keybits), every list is sorted
+// by ONE device-wide radix sort over all candidates, the type index in those
+// bits and only the bits some list varies in sorted ("segsort_merged", the
+// default).  Otherwise lists
+// of at least segsort_wide entries get a device-wide radix sort each, spread
+// over every CU, the shorter ones share one segmented sort (a block per
+// list).  One segmented sort over every list ran the few large ones in one
+// block each: 2.8 ms of a config-4 step.
+// Per-type OR / AND of the candidate keys (kb[t] = OR, kb[64 + t] = AND):
+// the bits a list's keys differ in, so launch_segsort can sort every list in
+// one device-wide radix sort with the list index in constant top bits.
+__global__ __launch_bounds__(256) void k_keybits(const int *__restrict__ candoff, const int *__restrict__ candlen,
+                                                 const unsigned long long *__restrict__ key,
+                                                 unsigned long long *kb) {
+    const int t = blockIdx.y, b = candoff[t], e = b + candlen[t];
+    unsigned long long o = 0, a = ~0ull;
+    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x) {
+        const unsigned long long k = key[i];
+        o |= k;
+        a &= k;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        o |= __shfl_xor(o, d, 64);
+        a &= __shfl_xor(a, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && a != ~0ull) {
+        atomicOr(&kb[t], o);
+        atomicAnd(&kb[ADLBQ_MAX_TYPES + t], a);
+    }
+}
+
+constexpr int LIST_SHIFT = 58;  // list index bits of a merged sort key (T <= 64)
+constexpr unsigned long long LIST_LOW = (1ull << LIST_SHIFT) - 1;
+
+// key -> (63 - t) << 58 | low bits: a descending sort keeps type t's list at
+// its own offsets, in preference order
+__global__ __launch_bounds__(256) void k_merge_keys(const int *__restrict__ candoff, const int *__restrict__ candlen,
+                                                    const unsigned long long *__restrict__ key,
+                                                    unsigned long long *mkey) {
+    const int t = blockIdx.y, b = candoff[t], e = b + candlen[t];
+    const unsigned long long top = (unsigned long long)(63 - t) << LIST_SHIFT;
+    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x)
+        mkey[i] = top | (key[i] & LIST_LOW);
+}
+
+// sorted merged keys back, with each list's constant top bits; needsort 2
+__global__ __launch_bounds__(256) void k_unmerge_keys(const int *__restrict__ candoff,
+                                                      const int *__restrict__ candlen,
+                                                      const unsigned long long *__restrict__ kb,
+                                                      const unsigned long long *mkey,  // may be `key`
+                                                      const int *__restrict__ s2, unsigned long long *key, int *slot,
+                                                      int *needsort) {
+    const int t = blockIdx.y, b = candoff[t], e = b + candlen[t];
+    const unsigned long long top = kb[ADLBQ_MAX_TYPES + t] & ~LIST_LOW;
+    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x) {
+        key[i] = top | (mkey[i] & LIST_LOW);
+        slot[i] = s2[i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && needsort[t] == 1) needsort[t] = 2;
+}
+
 static int launch_segsort(adlbq_server *h) {
     const int T = h->T;
     hipStream_t s = h->stream;
+    if (!h->d_kb) AQ_HIP(hipMalloc((void **)&h->d_kb, sizeof(unsigned long long) * 2 * ADLBQ_MAX_TYPES));
+    const int kgx = 16;  // blocks per list of the key passes
+    if (h->segsort_merged) {
+        AQ_HIP(hipMemsetAsync(h->d_kb, 0, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
+        AQ_HIP(hipMemsetAsync(h->d_kb + ADLBQ_MAX_TYPES, 0xff, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
+        k_keybits<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_kb);
+        AQ_HIP(hipGetLastError());
+    }
+    std::vector<int> hb(3 * (size_t)T + 1);
+    std::vector<unsigned long long> kb(2 * ADLBQ_MAX_TYPES);
+    AQ_HIP(hipMemcpyAsync(hb.data(), h->d_candoff, sizeof(int) * (T + 1), hipMemcpyDeviceToHost, s));
+    AQ_HIP(hipMemcpyAsync(hb.data() + T + 1, h->d_candlen, sizeof(int) * T, hipMemcpyDeviceToHost, s));
+    AQ_HIP(hipMemcpyAsync(hb.data() + 2 * T + 1, h->d_needsort, sizeof(int) * T, hipMemcpyDeviceToHost, s));
+    if (h->segsort_merged)
+        AQ_HIP(hipMemcpyAsync(kb.data(), h->d_kb, sizeof(unsigned long long) * 2 * ADLBQ_MAX_TYPES,
+                              hipMemcpyDeviceToHost, s));
+    AQ_HIP(hipStreamSynchronize(s));
+    if (h->segsort_merged) {
+        // one sort of every list when no list's keys differ in the top bits
+        const int G = hb[T];
+        int nsort = 0, lo = 64;
+        bool ok = G > 1;
+        for (int t = 0; t < T && ok; t++) {
+            if (hb[T + 1 + t] == 0) continue;
+            const unsigned long long diff = kb[t] ^ kb[ADLBQ_MAX_TYPES + t];
+            ok = (diff >> LIST_SHIFT) == 0;
+            if (diff) lo = std::min(lo, __builtin_ctzll(diff));
+            nsort += hb[2 * T + 1 + t] == 1 && hb[T + 1 + t] > 1;
+        }
+        if (nsort == 0) return ADLBQ_OK;
+        if (ok) {
+            if (lo >= LIST_SHIFT) lo = LIST_SHIFT;  // every list is constant: the sort only keeps lists apart
+            size_t tmp = 0;
+            AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey2, h->d_ckey, h->d_cslot,
+                                                                h->d_cslot2, G, lo, 64, s));
+            if (tmp > h->cap_ssort) {
+                if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
+                h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
+                AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
+            }
+            k_merge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_ckey2);
+            size_t t2 = h->cap_ssort;
+            AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey2, h->d_ckey, h->d_cslot,
+                                                                h->d_cslot2, G, lo, 64, s));
+            k_unmerge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_kb, h->d_ckey, h->d_cslot2,
+                                                        h->d_ckey, h->d_cslot, h->d_needsort);
+            AQ_HIP(hipGetLastError());
+            h->n_segsort += nsort;
+            return ADLBQ_OK;
+        }
+    }
+    // wide lists first, then the short ones
+    SegList sl{};
+    int maxlen = 0, nwide = 0;
+    for (int pass = 0; pass < 2; pass++)
+        for (int t = 0; t < T; t++) {
+            const int off = hb[t], len = hb[T + 1 + t], ns = hb[2 * T + 1 + t];
+            if (ns != 1 || len < 2 || (len >= h->segsort_wide) != (pass == 0)) continue;
+            sl.type[sl.n] = t;
+            sl.beg[sl.n] = off;
+            sl.end[sl.n] = off + len;
+            sl.n++;
+            nwide += pass == 0;
+            maxlen = std::max(maxlen, len);
+        }
+    if (sl.n == 0) return ADLBQ_OK;
+    h->n_segsort += nwide;
     if (!h->d_sbeg) {
         AQ_HIP(hipMalloc((void **)&h->d_sbeg, sizeof(int) * ADLBQ_MAX_TYPES));
         AQ_HIP(hipMalloc((void **)&h->d_send, sizeof(int) * ADLBQ_MAX_TYPES));
     }
-    const long long n = h->cap_cand;  // bound of every list's end
-    size_t tmp = 0;
-    AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey, h->d_ckey2, h->d_cslot,
-                                                                 h->d_cslot2, (int)n, T, h->d_sbeg, h->d_send, 0, 64,
-                                                                 s));
+    const int nshort = sl.n - nwide;
+    const int span = nshort > 0 ? sl.end[sl.n - 1] : 0;  // short lists lie below this bound (candoff ascends)
+    size_t tmp = 0, t1 = 0;
+    if (nwide > 0)
+        AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey, h->d_ckey2, h->d_cslot,
+                                                            h->d_cslot2, maxlen, 0, 64, s));
+    if (nshort > 0) {
+        AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(nullptr, t1, h->d_ckey, h->d_ckey2, h->d_cslot,
+                                                                     h->d_cslot2, span, nshort, h->d_sbeg,
+                                                                     h->d_send, 0, 64, s));
+        tmp = std::max(tmp, t1);
+    }
     if (tmp > h->cap_ssort) {
-        AQ_HIP(hipStreamSynchronize(s));
         if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
         h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
         AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
     }
-    k_segsort_prep<<<1, 64, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_needsort, h->d_sbeg, h->d_send);
-    size_t t2 = h->cap_ssort;
-    AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey, h->d_ckey2, h->d_cslot,
-                                                                 h->d_cslot2, (int)n, T, h->d_sbeg, h->d_send, 0, 64,
-                                                                 s));
-    k_segsort_back<<<T, 256, 0, s>>>(h->d_sbeg, h->d_send, h->d_ckey2, h->d_cslot2, h->d_ckey, h->d_cslot,
-                                     h->d_needsort);
+    for (int q = 0; q < nwide; q++) {
+        const int b = sl.beg[q], len = sl.end[q] - b;
+        size_t t2 = h->cap_ssort;
+        AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey + b, h->d_ckey2 + b,
+                                                            h->d_cslot + b, h->d_cslot2 + b, len, 0, 64, s));
+    }
+    if (nshort > 0) {
+        k_segsort_bounds<<<1, 64, 0, s>>>(sl, nwide, h->d_sbeg, h->d_send);
+        size_t t2 = h->cap_ssort;
+        AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey, h->d_ckey2,
+                                                                     h->d_cslot, h->d_cslot2, span, nshort,
+                                                                     h->d_sbeg, h->d_send, 0, 64, s));
+    }
+    const int gx = std::min((maxlen + 255) / 256, 256);
+    k_segsort_back<<<dim3(gx, sl.n), 256, 0, s>>>(sl, h->d_ckey2, h->d_cslot2, h->d_ckey, h->d_cslot, h->d_needsort);
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
 }

@@ -631,7 +631,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
-                    h->d_sbeg, h->d_send, h->d_ssort};
+                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1043,6 +1043,16 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_warm = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "segsort_merged") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "segsort_merged must be 0 or 1");
+        h->segsort_merged = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "segsort_wide") {
+        if (value < 2 || value > (1ll << 30)) return fail(ADLBQ_ERR_ARG, "segsort_wide must be in [2, 2^30]");
+        h->segsort_wide = (int)value;
+        return ADLBQ_OK;
+    }
     return fail(ADLBQ_ERR_ARG, "adlbq_set_param: unknown parameter");
 }
 
@@ -1062,6 +1072,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         if (h->T > 0 && hipMemcpy(&v, h->d_candoff + h->T, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
         return v;
     }
+    if (n == "device_sorted_lists") return h->n_segsort;  // candidate lists given a device-wide sort (cumulative)
     if (n == "sort_timeouts") {  // k_rank waits for an in-launch sort that gave up (cumulative; 0 unless broken)
         int v = 0;
         if (hipMemcpy(&v, h->d_rank_sync + ADLBQ_MAX_TYPES + 1, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;

@@ -71,12 +71,17 @@ def parse():
     ap.add_argument("--config4-only", action="store_true", help="only the config-4 leg (profiling)")
     ap.add_argument("--c4-units", type=int, default=10_000_000, help="config 4: units (80%% targeted)")
     ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-chain-passes", type=int, default=None,
+                    help="config 4: parallel chain passes before the in-order fix-up (adlbq 'chain_passes')")
+    ap.add_argument("--c4-segsort-wide", type=int, default=None,
+                    help="config 4: sort list by list (no merged sort); length from which a list gets a device-wide "
+                         "sort (adlbq 'segsort_wide')")
     return ap.parse_args()
 
 
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
 KERNEL_OF = {"hist": "k_prep_hist", "thresholds": "k_thresholds",
-             "select": "k_select_open", "sort": "hipcub segmented radix sort",
+             "select": "k_select_open", "sort": "k_keybits + merged hipcub radix sort",
              "targeted": "k_targeted_idx", "rank": "k_rank", "chain": "k_chain", "finalize": "k_finalize"}
 
 
@@ -313,6 +318,11 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
     stream = torch.cuda.Stream(dev)
     srv.set_stream(stream.cuda_stream)
+    if args.c4_chain_passes is not None:
+        srv.set_param("chain_passes", args.c4_chain_passes)
+    if args.c4_segsort_wide is not None:
+        srv.set_param("segsort_merged", 0)
+        srv.set_param("segsort_wide", args.c4_segsort_wide)
     srv.put_batch(np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1),
                             np.zeros(N), np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32))
     rng = np.random.default_rng(args.seed + 41 + rank)

@@ -206,14 +206,20 @@ long long adlbq_last_scan_units(adlbq_server *h);
  * "chain_fallback" (segments the in-order fix-up recomputed; 0 when the passes
  * reached their fixed point), "parked" (Reserves parked), "candidates",
  * "sort_timeouts" (waits of the rank pass for an in-launch sort that gave up,
- * cumulative; 0 unless something is broken).
+ * cumulative; 0 unless something is broken), "device_sorted_lists" (candidate
+ * lists long enough for a device-wide radix sort of their own, cumulative).
  * -1 if unknown. */
 long long adlbq_stat(adlbq_server *h, const char *name);
 /* Tuning: "chain_passes" = parallel segment passes of the ordered-choice
  * kernel before the in-order fix-up (1..30; 0 = auto: 3 for up to 8 types,
  * else 8); "chain_warm" = requests replayed ahead of each segment in the first
- * pass (-1 = auto: 512 for up to 8 types; or 0, 256, 512).
- * Results never depend on either; tests lower them to force the fix-up. */
+ * pass (-1 = auto: 512 for up to 8 types; or 0, 256, 512); "segsort_wide" =
+ * candidate-list length from which a multi-priority list is sorted by a
+ * device-wide radix sort of its own rather than a shared segmented sort
+ * (default 16384) when the lists are not sorted together; "segsort_merged" =
+ * 1 (default) sorts every list in one device-wide radix sort when no list's
+ * keys differ in their top 6 bits, 0 always sorts list by list.
+ * Results never depend on them; tests lower them to force the other paths. */
 int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);
 const char *adlbq_version(void);

@@ -121,8 +121,10 @@ def test_stream_vs_oracle(gpu_available):
     assert_same(run_abi([1, 2], cfg, tr), run_oracle([1, 2], cfg, tr))
 
 
-def _exact_full(w, batches=1):
+def _exact_full(w, batches=1, stats=None, params=()):
     with Server(w.user_types, w.num_app_ranks, max_units=w.n_units) as s:
+        for k, v in params:
+            s.set_param(k, v)
         units = np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len,
                           np.full(w.n_units, -1), np.zeros(w.n_units), np.full(w.n_units, -1),
                           np.full(w.n_units, -1)], axis=1).astype(np.int32)
@@ -149,6 +151,9 @@ def _exact_full(w, batches=1):
                 torch.cuda.synchronize()  # the handle's stream does not order after torch's
                 s.unreserve_batch_device(m.size, trip.data_ptr())
                 s.sync()
+        if stats is not None:
+            for k in ("device_sorted_lists", "sort_timeouts"):
+                stats[k] = s.stat(k)
         return first
 
 
@@ -163,9 +168,19 @@ def test_full_size_config2_equal_prio_exact(gpu_available):
     _exact_full(w)
 
 
-def test_config4_2m_exact(gpu_available):
+@pytest.mark.parametrize("merged,wide", [(1, 16384), (0, 16384), (0, 256)])
+def test_config4_2m_exact(gpu_available, merged, wide):
+    """Three batches: from the second on the multi-prio-bin candidate lists are
+    sorted before the rank pass (launch_segsort): all lists in one merged
+    device-wide radix sort (merged=1), or list by list, lists of `wide`
+    entries or more by a device-wide sort each and shorter ones by a shared
+    segmented sort (256 forces the device-wide path)."""
     w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
-    _exact_full(w)
+    stats = {}
+    _exact_full(w, batches=3, stats=stats, params=[("segsort_merged", merged), ("segsort_wide", wide)])
+    if merged or wide == 256:
+        assert stats["device_sorted_lists"] > 0, "the device-wide list sort did not run"
+    assert stats["sort_timeouts"] == 0
 
 
 REPEAT = {
