@@ -37,6 +37,7 @@ constexpr int SEG = 256;               // chain segment: requests per wavefront 
 constexpr int SEG_BLOCKS = SEG / 64;
 constexpr int CHAIN_MAX_PASSES = 30;   // bound of the settable pass count (adlbq_set_param)
 constexpr int CHAIN_WARM = 512;        // pass-1 warm-up before each segment (T <= 8), a multiple of SEG
+constexpr int CHAIN_WARM_WIDE = 0;     // the same for T > 8
 constexpr int PREP_BLOCK = 256;        // prep_block workgroup
 static_assert(SEG % 64 == 0 && CHAIN_WARM % SEG == 0, "chain segments are whole waves of prep_block");
 
@@ -1257,11 +1258,12 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
     return my_end;
 }
 
-// Any T <= 64, no warm-up: lane t keeps type t's state, uniform copies come
-// from readlane; rounds touch only the types present in the block.
+// Any T <= 64: lane t keeps type t's state, uniform copies come from
+// readlane; rounds touch only the types present in the block.  `write` false
+// = a warm-up replay of an earlier segment (end state only).
 template <int TB>
 __device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_start, unsigned int *win,
-                                              int &rounds) {
+                                              int &rounds, bool write = true) {
     const int lane = threadIdx.x, T = a.T, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
     const int my_off = lane < T ? a.candoff[lane] : 0;
     const int my_len = lane < T ? a.candlen[lane] : 0;
@@ -1323,18 +1325,23 @@ __device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_
                       __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(B);
             if (lane == t) my_c0 += __popcll(B);
         }
-        if (j < j1) a.umatch[j] = res;
+        if (write && j < j1) a.umatch[j] = res;
     }
     return my_start + my_c0;
 }
 
-// TB <= 8: uniform per-type state (warm-up allowed); TB == 64: wide variant.
+// TB <= 8: uniform per-type state; TB == 64: wide variant (warm-up replayed
+// segment by segment).
 template <int TB>
 __device__ __forceinline__ int seg_solve(const ChainArgs &a, int s, int jb, int my_start, unsigned int *win,
                                          int &my_rec, int &rounds) {
     if constexpr (TB <= 8) {
         return seg_solve_small<TB>(a, s, jb, my_start, win, s * SEG - jb + SEG, my_rec, rounds);
     } else {
+        for (int q = jb / SEG; q < s; q++) {  // pass 1's warm-up: replay the segments before s
+            my_start = seg_solve_wide<8>(a, q, my_start, win, rounds, false);
+            __builtin_amdgcn_wave_barrier();  // win is refilled
+        }
         my_rec = my_start;
         return seg_solve_wide<8>(a, s, my_start, win, rounds);
     }
@@ -2160,7 +2167,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     {
         const int nseg = (R + SEG - 1) / SEG;
         const int K = h->chain_passes > 0 ? h->chain_passes : (T <= 8 ? 3 : 8);
-        const int warm = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
+        const int warm = h->chain_warm >= 0 ? h->chain_warm : (T <= 8 ? CHAIN_WARM : CHAIN_WARM_WIDE);
         if (++h->chain_epoch == 0) h->chain_epoch = 1;
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, K, warm, h->chain_epoch, h->d_candoff, h->d_candlen,
                      h->d_crank, h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf,

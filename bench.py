@@ -73,6 +73,10 @@ def parse():
     ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--c4-chain-passes", type=int, default=None,
                     help="config 4: parallel chain passes before the in-order fix-up (adlbq 'chain_passes')")
+    ap.add_argument("--c4-chain-warm", type=int, default=None,
+                    help="config 4: requests replayed before each chain segment in pass 1 (adlbq 'chain_warm')")
+    ap.add_argument("--c4-chain-stats", action="store_true",
+                    help="config 4: after the timed region, replay each batch alone and report its chain counters")
     ap.add_argument("--c4-segsort-wide", type=int, default=None,
                     help="config 4: sort list by list (no merged sort); length from which a list gets a device-wide "
                          "sort (adlbq 'segsort_wide')")
@@ -318,6 +322,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
     stream = torch.cuda.Stream(dev)
     srv.set_stream(stream.cuda_stream)
+    if args.c4_chain_warm is not None:
+        srv.set_param("chain_warm", args.c4_chain_warm)
     if args.c4_chain_passes is not None:
         srv.set_param("chain_passes", args.c4_chain_passes)
     if args.c4_segsort_wide is not None:
@@ -371,6 +377,16 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     if world > 1:
         el, matched = shards.reduce_step_timing(el, matched)
     steps = nb - W4
+    per_batch = []
+    if args.c4_chain_stats:
+        for b in range(W4, nb):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            step(b)
+            torch.cuda.synchronize()
+            per_batch.append({"ms": round((time.perf_counter() - t1) * 1e3, 3),
+                              **{k: srv.stat(k) for k in ("chain_rounds", "chain_passes", "chain_recomputed",
+                                                          "chain_fallback")}})
     out = {
         "workload": f"config4: {N} units/shard (80% targeted, Zipf(1.1) over 1024 ranks), 32 Zipf types, "
                     f"prio U[0,2^16), {R} hanging Reserves/step with 1-4 types",
@@ -381,6 +397,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "stages_ms": stages,
         "scaling": "weak",
     }
+    if per_batch:
+        out["chain_per_batch"] = per_batch
     srv.close()
     return out
 
