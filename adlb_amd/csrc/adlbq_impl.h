@@ -193,6 +193,8 @@ struct adlbq_server {
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
     int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")
+    int chain_guess = 0;               // T > 8 pass-1 guess: 0 level, 1 demand-capped level ("chain_guess")
+    int *d_segdem = nullptr; long long cap_segdem = 0;  // [nseg][T] k_seg_demand
     int segsort_merged = 1;            // one merged sort of every list when the keys allow ("segsort_merged")
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")

@@ -1119,6 +1119,7 @@ struct ChainArgs {
     unsigned long long *counters;    // [9] two-level arrival counters (zero between batches)
     DevCounters *ctr;
     const int *lv;                   // [R][T] k_rank's level rows (T <= 8), else nullptr
+    const int *dem;                  // [nseg][T] requests of segment s that include type t, or nullptr
 };
 
 // Level guess for the state after J untargeted choices: pos_t = number of
@@ -1381,6 +1382,23 @@ __device__ __forceinline__ int load_state(const int *src, int T) {
     return threadIdx.x < T ? __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
 }
 
+// Per segment and type: requests that may take an untargeted unit of that
+// type (k_chain's demand-capped level guess, T > 8).  One wave per segment.
+__global__ __launch_bounds__(64) void k_seg_demand(const unsigned long long *__restrict__ mask,
+                                                   const int *__restrict__ tmatch, int R, int T, int *dem) {
+    const int lane = threadIdx.x, s = blockIdx.x;
+    int my = 0;
+    for (int b0 = s * SEG; b0 < min(R, s * SEG + SEG); b0 += 64) {
+        const int j = b0 + lane;
+        const unsigned long long m = (j < R && tmatch[j] < 0) ? mask[j] : 0ull;
+        for (int t = 0; t < T; t++) {
+            const int c = __popcll(__ballot((m >> t) & 1ull));
+            if (lane == t) my += c;
+        }
+    }
+    if (lane < T) dem[s * T + lane] = my;
+}
+
 // The whole ordered choice in one launch, one wavefront per segment.
 //   pass 1: every segment from its level guess, after a warm-up replay;
 //   pass k = 2 .. passes: segment s (= workgroup s) waits for segment s-1's
@@ -1411,6 +1429,24 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
     if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
         const int G = a.candoff[T], len = lane < T ? a.candlen[lane] : 0;
         guess = lane >= T || J == 0 ? 0 : J >= G ? len : a.lv[(long long)J * T + lane];
+    } else if (a.dem != nullptr) {
+        // demand-capped level: type t's head is at most the requests before
+        // jb that include t; the level L rises until the capped heads sum to J
+        // (slope <= 1: the iteration approaches the fixed point from below)
+        int D = 0;
+        if (lane < T)
+            for (int q = 0; q < jb / SEG; q++) D += a.dem[q * T + lane];
+        const int G = a.candoff[T];
+        int L = min(J, G);
+        guess = 0;
+        for (int it = 0; it < 4; it++) {
+            guess = min(level_guess<8>(a, L), D);
+            int f = guess;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
+            if (f >= J || L >= G) break;
+            L = min(G, L + (J - f));
+        }
     } else {
         guess = level_guess<(TB <= 8 ? TB : 8)>(a, J);
     }
@@ -2171,7 +2207,17 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         if (++h->chain_epoch == 0) h->chain_epoch = 1;
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, K, warm, h->chain_epoch, h->d_candoff, h->d_candlen,
                      h->d_crank, h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf,
-                     h->d_chcnt, h->d_ctr, (T <= 8 && np > 0) ? h->d_lv : nullptr};
+                     h->d_chcnt, h->d_ctr, (T <= 8 && np > 0) ? h->d_lv : nullptr, nullptr};
+        if (T > 8 && h->chain_guess == 1) {
+            if ((long long)nseg * T > h->cap_segdem) {
+                AQ_HIP(hipStreamSynchronize(s));
+                if (h->d_segdem) AQ_HIP(hipFree(h->d_segdem));
+                h->cap_segdem = std::max((long long)nseg * T, 2 * h->cap_segdem);
+                AQ_HIP(hipMalloc((void **)&h->d_segdem, sizeof(int) * h->cap_segdem));
+            }
+            k_seg_demand<<<nseg, 64, 0, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_segdem);
+            ca.dem = h->d_segdem;
+        }
         if (T <= 4) k_chain<4><<<nseg, 64, sizeof(unsigned int) * (4 * (SEG + warm) + 64), s>>>(ca);
         else if (T <= 8) k_chain<8><<<nseg, 64, sizeof(unsigned int) * (8 * (SEG + warm) + 64), s>>>(ca);
         else k_chain<64><<<nseg, 64, sizeof(unsigned int) * T * SEG, s>>>(ca);

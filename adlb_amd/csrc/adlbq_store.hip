@@ -631,7 +631,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
-                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb};
+                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_segdem};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1041,6 +1041,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         if (value != -1 && value != 0 && value != 256 && value != 512)
             return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 (auto), 0, 256 or 512");
         h->chain_warm = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "chain_guess") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "chain_guess must be 0 or 1");
+        h->chain_guess = (int)value;
         return ADLBQ_OK;
     }
     if (n == "segsort_merged") {

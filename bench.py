@@ -75,6 +75,8 @@ def parse():
                     help="config 4: parallel chain passes before the in-order fix-up (adlbq 'chain_passes')")
     ap.add_argument("--c4-chain-warm", type=int, default=None,
                     help="config 4: requests replayed before each chain segment in pass 1 (adlbq 'chain_warm')")
+    ap.add_argument("--c4-chain-guess", type=int, default=None,
+                    help="config 4: chain pass-1 guess, 0 level (default), 1 demand-capped level (adlbq 'chain_guess')")
     ap.add_argument("--c4-chain-stats", action="store_true",
                     help="config 4: after the timed region, replay each batch alone and report its chain counters")
     ap.add_argument("--c4-segsort-wide", type=int, default=None,
@@ -322,6 +324,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
     stream = torch.cuda.Stream(dev)
     srv.set_stream(stream.cuda_stream)
+    if args.c4_chain_guess is not None:
+        srv.set_param("chain_guess", args.c4_chain_guess)
     if args.c4_chain_warm is not None:
         srv.set_param("chain_warm", args.c4_chain_warm)
     if args.c4_chain_passes is not None:

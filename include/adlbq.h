@@ -218,7 +218,10 @@ long long adlbq_stat(adlbq_server *h, const char *name);
  * device-wide radix sort of its own rather than a shared segmented sort
  * (default 16384) when the lists are not sorted together; "segsort_merged" =
  * 1 (default) sorts every list in one device-wide radix sort when no list's
- * keys differ in their top 6 bits, 0 always sorts list by list.
+ * keys differ in their top 6 bits, 0 always sorts list by list; "chain_guess"
+ * = the ordered-choice kernel's first-pass state guess for more than 8 types:
+ * 0 (default) the plain level guess, 1 caps each type's level head by the
+ * requests before the segment that include the type.
  * Results never depend on them; tests lower them to force the other paths. */
 int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);

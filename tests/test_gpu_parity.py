@@ -168,18 +168,20 @@ def test_full_size_config2_equal_prio_exact(gpu_available):
     _exact_full(w)
 
 
-@pytest.mark.parametrize("merged,wide,warm", [(1, 16384, -1), (0, 16384, -1), (0, 256, -1), (1, 16384, 512)])
-def test_config4_2m_exact(gpu_available, merged, wide, warm):
+@pytest.mark.parametrize("merged,wide,warm,guess",
+                         [(1, 16384, -1, 1), (0, 16384, -1, 1), (0, 256, -1, 1), (1, 16384, 512, 1), (1, 16384, -1, 0)])
+def test_config4_2m_exact(gpu_available, merged, wide, warm, guess):
     """Three batches: from the second on the multi-prio-bin candidate lists are
     sorted before the rank pass (launch_segsort): all lists in one merged
     device-wide radix sort (merged=1), or list by list, lists of `wide`
     entries or more by a device-wide sort each and shorter ones by a shared
     segmented sort (256 forces the device-wide path).  warm=512: the 32-type
-    chain replays two segments before its own in pass 1."""
+    chain replays two segments before its own in pass 1.  guess: the 32-type
+    chain's pass-1 state guess (1 demand-capped level, 0 plain level)."""
     w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
     stats = {}
     _exact_full(w, batches=3, stats=stats, params=[("segsort_merged", merged), ("segsort_wide", wide),
-                                                       ("chain_warm", warm)])
+                                                       ("chain_warm", warm), ("chain_guess", guess)])
     if merged or wide == 256:
         assert stats["device_sorted_lists"] > 0, "the device-wide list sort did not run"
     assert stats["sort_timeouts"] == 0
