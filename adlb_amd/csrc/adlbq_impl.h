@@ -51,7 +51,8 @@ struct DevCounters {
     int chain_rounds;  // Jacobi rounds of the last chain, all wavefronts (diagnostic)
     int chain_passes;      // segment passes of the last chain that recomputed something
     int chain_recomputed;  // segment solves over those passes
-    int chain_fallback;    // segments k_chain_fix recomputed (0 at a fixed point)
+    int chain_fallback;    // segments the last chain launch's walk re-solved (0 at a fixed point)
+    int chain_timeouts;    // bounded hand-off waits of round 0's neighbour passes that gave up (cumulative)
     int spec_page0;        // the last scan's page 0, wave 0 read pass 1's list (diagnostic)
     int needsort_last;     // the last reserve batch had a type whose threshold fell in a multi-prio bin
 };
@@ -186,15 +187,23 @@ struct adlbq_server {
     int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort
     long long n_segsort = 0;                          // lists given a device-wide sort (cumulative)
     long long ssort_items = 0;
-    int *d_chE = nullptr;              // [passes + 1][nseg][T] chain: segment end states per pass
-    int *d_chflag = nullptr;           // [passes + 1][nseg] chain: epoch once published
-    int *d_chSf = nullptr, *d_chEf = nullptr;  // [nseg][T] chain: final start / end states
-    unsigned long long *d_chcnt = nullptr;  // [9] chain: two-level arrival counters (zero between batches)
+    // ordered choice (k_chain0 / k_chainr): per segment start used and delta, the
+    // delta prefix within its arrival group, group totals / offsets, the
+    // per-request choice (next round's seed), the clean flag, arrival counters
+    int *d_chS = nullptr, *d_chD = nullptr;                     // [2][nseg][T] (launch parity)
+    int *d_chLP = nullptr;                                      // [nseg][T]
+    int *d_chGT = nullptr, *d_chGO = nullptr;                   // [8][T]
+    int *d_chclean = nullptr;
+    unsigned char *d_cht = nullptr;                             // [R]
+    unsigned long long *d_chcnt = nullptr;                      // [9]
+    int *d_chE = nullptr, *d_chflag = nullptr;                  // round 0's hand-offs: [P][nseg][T], [P][nseg]
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
-    int chain_passes = 0;              // passes before k_chain_fix, 0 = auto (adlbq_set_param "chain_passes")
-    int chain_warm = -1;               // pass-1 warm-up requests, -1 = auto (adlbq_set_param "chain_warm")
-    int chain_guess = 0;               // T > 8 pass-1 guess: 0 level, 1 demand-capped level ("chain_guess")
-    int *d_segdem = nullptr; long long cap_segdem = 0;  // [nseg][T] k_seg_demand
+    int chain_passes = 0;              // round 0's in-launch passes, 0 = auto (adlbq_set_param "chain_passes")
+    int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
+    int chain_stamps = 0;              // diagnostic: phase stamps of the first chain launch ("chain_stamps")
+    unsigned long long *d_stamps = nullptr; int cap_stamps = 0, n_stamps = 0;
+    int chain_warm = -1;               // round-0 warm-up requests (T <= 8), -1 = auto ("chain_warm")
+    long long chain_modes = -1;        // bit k-1: round k uses prefix starts, -1 = auto ("chain_modes")
     int segsort_merged = 1;            // one merged sort of every list when the keys allow ("segsort_merged")
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")

@@ -35,9 +35,7 @@ using namespace adlbq;
 
 constexpr int SEG = 256;               // chain segment: requests per wavefront (one prep_block)
 constexpr int SEG_BLOCKS = SEG / 64;
-constexpr int CHAIN_MAX_PASSES = 30;   // bound of the settable pass count (adlbq_set_param)
-constexpr int CHAIN_WARM = 512;        // pass-1 warm-up before each segment (T <= 8), a multiple of SEG
-constexpr int CHAIN_WARM_WIDE = 0;     // the same for T > 8
+constexpr int CHAIN_WARM = 512;        // largest round-0 warm-up before a segment (T <= 8), a multiple of SEG
 constexpr int PREP_BLOCK = 256;        // prep_block workgroup
 static_assert(SEG % 64 == 0 && CHAIN_WARM % SEG == 0, "chain segments are whole waves of prep_block");
 
@@ -1104,29 +1102,80 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     }
 }
 
+// ---------------------------------------------------------------- ordered choice: rounds over segment prefixes
+//
+// Segment s (SEG requests, one wavefront) turns a start state (lane t = head
+// position of type t) into its choices and a per-type delta D_s = end - start.
+// The sequential chain is start_0 = 0, start_s = sum_{q<s} D_q.  Launches:
+//
+//   k_chain0      round 0: every segment from a guessed start (the level
+//                 state, optionally after a warm-up replay for T <= 8);
+//   k_chainr x K  round k: every segment compares its start S_s with
+//                 P_s = sum_{q<s} D_q (the deltas of the previous round) and
+//                 re-solves from P_s when they differ, seeded with its previous
+//                 choices (a Jacobi iteration converges from any seed; the
+//                 seed makes an unchanged segment cost one round per block).
+//
+// After every round the deltas are summed by the arrivals themselves: the
+// last arriver of each group of contiguous segments writes the group's local
+// exclusive prefix LP and total GT, the last group writes the group offsets
+// GO, so P_s = GO[g(s)] + LP[s] for the next launch.  A round in which no
+// delta changed leaves every S_s == P_s: the fixed point, which is the
+// sequential result (P_0 = 0; induction on s); the `clean` flag then turns the
+// remaining round launches into no-ops.  A start error that no choice in a
+// segment depends on passes through as a constant shift, so one round repairs
+// it everywhere at once (in place of one segment per pass).  If the last round
+// is still not clean, its last arriver walks the segments in order from the
+// exact prefix, re-solving only those whose start differs.  No wavefront ever
+// waits for another: only arrival counters and kernel boundaries order them.
+
+constexpr int CH_GROUPS = 8;
+constexpr unsigned char CHT_NONE = 255;
+
 struct ChainArgs {
     const unsigned long long *mask;  // [R] type masks (0: no untargeted choice)
     const int *tmatch;               // [R] slot matched in the targeted phase, or -1
-    int R, T, nseg, passes, warm;    // warm: requests replayed before a segment in pass 1
-    unsigned int epoch;              // this batch's flag value (never 0)
+    int R, T, nseg, warm;            // warm: requests replayed before a segment in round 0 (T <= 8)
+    int gs;                          // segments per arrival group (contiguous)
     const int *candoff, *candlen;    // [T]
     const unsigned int *crank;       // packed ranks, per type ascending
     int *umatch;                     // [R] out: candidate index or -1
-    const int *seg_cnt;              // [nseg] requests of the segment that may take an untargeted unit
-    int *E;                          // [passes + 1][nseg][T] end state of segment s after pass k
-    int *flags;                      // [passes + 1][nseg] == epoch once E[k][s] is published
-    int *Sf, *Ef;                    // [nseg][T] final start / end of each segment
-    unsigned long long *counters;    // [9] two-level arrival counters (zero between batches)
+    unsigned char *cht;              // [R] the choice's type index (CHT_NONE: none), the next round's seed
+    const int *seg_cnt;              // [R/64] requests of each 64 that may take an untargeted unit
+    int *S, *D;                      // [nseg][T] start used and delta, written by this launch
+    const int *Sp, *Dp;              // [nseg][T] the same from the previous launch (double-buffered)
+    int *LP;                         // [nseg][T] exclusive prefix of D in the group
+    int *GT, *GO;                    // [CH_GROUPS][T] group totals, exclusive prefix over groups
+    int *clean;                      // [1] set by a round that changed no delta
+    unsigned long long *counters;    // [CH_GROUPS + 1] two-level arrival counters (zero between launches)
     DevCounters *ctr;
     const int *lv;                   // [R][T] k_rank's level rows (T <= 8), else nullptr
-    const int *dem;                  // [nseg][T] requests of segment s that include type t, or nullptr
+    unsigned long long *stamps;      // [nseg][8] s_memrealtime per phase (diagnostic build of the run), or nullptr
 };
+
+// diagnostic phase stamps (100 MHz constant clock), lane 0 of a segment
+__device__ __forceinline__ void chain_stamp(const ChainArgs &a, int s, int ph) {
+    if (a.stamps != nullptr) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) {
+            a.stamps[s * 8 + ph] = __builtin_amdgcn_s_memrealtime();
+            a.stamps[(a.nseg + s) * 8 + ph] = __builtin_amdgcn_s_memtime();  // shader clock
+        }
+    }
+}
+
+__device__ __forceinline__ void st_sc1(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Level guess for the state after J untargeted choices: pos_t = number of
 // type-t candidates whose global rank is below J (every head at one level).
 // 64-ary search, all TB types at once: three dependent probes per lane.
 template <int TB>
-__device__ __forceinline__ int level_guess(const ChainArgs &a, int J) {
+__device__ __forceinline__ int level_guess(const ChainArgs a, int J) {
     const int lane = threadIdx.x;
     const unsigned int key = (unsigned int)J << 6;
     int my = 0;
@@ -1171,19 +1220,52 @@ __device__ __forceinline__ int level_guess(const ChainArgs &a, int J) {
 
 // Requests [jb, j1) of segment s (j1 = its end) from the state my_start (lane
 // t = type t) at jb; results are written from j0 = s * SEG on, and my_rec
-// receives the state at j0 (jb < j0 only for pass 1's warm-up).  All
+// receives the state at j0 (jb < j0 only for round 0's warm-up).  All
 // per-type state is uniform (T <= TB <= 8).  win holds, per type, the WL
 // candidates following the start (~0u past the list end); a replay of WL
-// requests consumes at most WL of any type.
+// requests consumes at most WL of any type.  seeded: the Jacobi rounds start
+// from the choices of the previous solve (cht) instead of the single-type ones.
 constexpr int CH_NONE = 63;  // no choice (T <= 8: never a type index)
 
+// LDS after the windows and the sentinel row: the staged type masks of the
+// segment's requests from pass 1's first request on (8 B each; so the block
+// loop is not unrolled and one copy of the Jacobi loop stays in the
+// instruction cache), then the segment's own choices (1 B each, the seed of
+// the next solve).
 template <int TB>
-__device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb, int my_start, unsigned int *win,
-                                               int WL, int &my_rec, int &rounds) {
+__device__ __forceinline__ unsigned long long *staged_masks(const ChainArgs a, unsigned int *win) {
+    return reinterpret_cast<unsigned long long *>(win + TB * (SEG + a.warm) + 64);
+}
+template <int TB>
+__device__ __forceinline__ unsigned char *staged_seeds(const ChainArgs a, unsigned int *win) {
+    return reinterpret_cast<unsigned char *>(staged_masks<TB>(a, win) + (SEG + a.warm));
+}
+
+// load: masks of [jb, jb + WL) and (seeded) the segment's choices come from
+// global memory into the staged area; otherwise they are staged already, the
+// mask of request jb at index mk0.
+template <int TB>
+__device__ __forceinline__ int seg_solve_small(const ChainArgs a, int s, int jb, int my_start, unsigned int *win,
+                                               int WL, bool seeded, bool load, int mk0, int &my_rec, int &rounds) {
     const int lane = threadIdx.x, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
     int st[TB], off[TB], c0[TB];
     constexpr int NI = (SEG + CHAIN_WARM) / 64;  // WL <= SEG + CHAIN_WARM
     unsigned int wv[TB][NI];                      // every window load in flight before the first LDS write
+    unsigned long long *smk = staged_masks<TB>(a, win);
+    unsigned char *ssd = staged_seeds<TB>(a, win);
+    unsigned long long mk[SEG_BLOCKS];
+    int tm[SEG_BLOCKS];
+    unsigned char sd[SEG_BLOCKS];
+    if (load) {  // a re-solve of one segment (jb == j0): its masks, results of the targeted phase, seeds
+#pragma unroll
+        for (int i = 0; i < SEG_BLOCKS; i++) {
+            const int j = jb + i * 64 + lane;
+            const bool ok = j < j1;
+            mk[i] = ok ? a.mask[j] : 0ull;
+            tm[i] = ok ? a.tmatch[j] : 0;
+            sd[i] = (seeded && ok) ? a.cht[j] : CHT_NONE;
+        }
+    }
 #pragma unroll
     for (int q = 0; q < TB; q++) {
         st[q] = __builtin_amdgcn_readlane(my_start, q);
@@ -1201,35 +1283,41 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
 #pragma unroll
         for (int i = 0; i < NI; i++)
             if (i * 64 < WL) win[q * WL + i * 64 + lane] = wv[q][i];
-    // every block's inputs up front (one wait, not one per block)
-    constexpr int NRB = (SEG + CHAIN_WARM) / 64;
-    unsigned long long mk[NRB];
+    if (load) {
 #pragma unroll
-    for (int i = 0; i < NRB; i++) {
-        const int j = jb + i * 64 + lane;
-        mk[i] = 0ull;
-        if (j < j1 && a.tmatch[j] < 0) mk[i] = a.mask[j];
+        for (int i = 0; i < SEG_BLOCKS; i++) {
+            smk[i * 64 + lane] = tm[i] < 0 ? mk[i] : 0ull;
+            ssd[i * 64 + lane] = sd[i];
+        }
+        mk0 = 0;
     }
-    const int sent = TB * (SEG + a.warm);  // 64 words of ~0u after the windows (k_chain's prologue)
+    const int sent = TB * (SEG + a.warm);  // 64 words of ~0u after the windows (the kernels' prologue)
     // one wave owns win: its LDS ops complete in order, only the compiler must not reorder
     __builtin_amdgcn_wave_barrier();
+    if (!seeded) chain_stamp(a, s, 6);
     my_rec = my_start;
-#pragma unroll
-    for (int bi = 0; bi < NRB; bi++) {
+    const int nblk = (min(j1, jb + WL) - jb + 63) / 64;
+#pragma unroll 1
+    for (int bi = 0; bi < nblk; bi++) {
         const int b0 = jb + bi * 64;
-        if (b0 >= j1) break;
         if (b0 == j0) {
 #pragma unroll
             for (int q = 0; q < TB; q++)
                 if (lane == q) my_rec = st[q] + c0[q];
         }
         const int j = b0 + lane;
-        const unsigned long long m = mk[bi];
+        const unsigned long long m = smk[mk0 + bi * 64 + lane];
         // a type the request lacks reads the sentinel row (~0u): no select in the round
         int base[TB];
 #pragma unroll
         for (int q = 0; q < TB; q++) base[q] = ((m >> q) & 1ull) ? q * WL + c0[q] : sent;
-        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : CH_NONE;
+        int ch;
+        if (seeded) {  // jb == j0
+            const unsigned char sv = ssd[bi * 64 + lane];
+            ch = sv == CHT_NONE ? CH_NONE : (int)sv;
+        } else {
+            ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : CH_NONE;
+        }
         unsigned long long chg;
         do {
             unsigned int v[TB];
@@ -1250,7 +1338,14 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
             if (ch == q) res = off[q] + st[q] + c0[q] + (int)mbcnt64(B);
             c0[q] += __popcll(B);
         }
-        if (b0 >= j0 && j < j1) a.umatch[j] = res;
+        if (b0 >= j0) {
+            const unsigned char c = ch == CH_NONE ? CHT_NONE : (unsigned char)ch;
+            ssd[(b0 - j0) + lane] = c;
+            if (j < j1) {
+                a.umatch[j] = res;
+                a.cht[j] = c;
+            }
+        }
     }
     int my_end = my_start;
 #pragma unroll
@@ -1259,12 +1354,25 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs &a, int s, int jb
     return my_end;
 }
 
-// Any T <= 64: lane t keeps type t's state, uniform copies come from
-// readlane; rounds touch only the types present in the block.  `write` false
-// = a warm-up replay of an earlier segment (end state only).
-template <int TB>
-__device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_start, unsigned int *win,
-                                              int &rounds, bool write = true) {
+// Any T <= 64 (the wide variant).  Per type t an LDS record {lanes of the
+// block choosing t (64-bit), choices of t in earlier blocks, list offset +
+// start}.  A Jacobi round costs the same for any T: every lane clears the
+// ballot word of its previous choice and ORs its bit into the one of its new
+// choice (one wave's LDS operations complete in order), then reads the
+// records of its own types (up to four in registers; more walk the mask) and
+// the window entry each points at.
+struct TypeRec {
+    unsigned long long bal;
+    int c0, offst;
+};
+
+__device__ __forceinline__ unsigned int head_of(const TypeRec *rec, const unsigned int *win, int t) {
+    const TypeRec r = rec[t];
+    return win[t * SEG + r.c0 + (int)mbcnt64(r.bal)];
+}
+
+__device__ __forceinline__ int seg_solve_wide(const ChainArgs a, int s, int my_start, unsigned int *win,
+                                              TypeRec *rec, bool seeded, int &rounds) {
     const int lane = threadIdx.x, T = a.T, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
     const int my_off = lane < T ? a.candoff[lane] : 0;
     const int my_len = lane < T ? a.candlen[lane] : 0;
@@ -1287,87 +1395,248 @@ __device__ __forceinline__ int seg_solve_wide(const ChainArgs &a, int s, int my_
 #pragma unroll
                 for (int i = 0; i < SEG_BLOCKS; i++) win[(g + q) * SEG + i * 64 + lane] = wv[q][i];
     }
-    // one wave owns win: its LDS ops complete in order, only the compiler must not reorder
+    if (lane < T) {
+        rec[lane].bal = 0ull;
+        rec[lane].c0 = 0;
+        rec[lane].offst = my_off + my_start;
+    }
+    unsigned long long mk[SEG_BLOCKS];
+    unsigned char sd[SEG_BLOCKS];
+#pragma unroll
+    for (int i = 0; i < SEG_BLOCKS; i++) {
+        const int j = j0 + i * 64 + lane;
+        mk[i] = (j < j1 && a.tmatch[j] < 0) ? a.mask[j] : 0ull;
+        sd[i] = (seeded && j < j1) ? a.cht[j] : CHT_NONE;
+    }
+    // one wave owns win and rec: its LDS ops complete in order, only the compiler must not reorder
     __builtin_amdgcn_wave_barrier();
-    int my_c0 = 0;
-    for (int b0 = j0; b0 < j1; b0 += 64) {
+    for (int bi = 0; bi < SEG_BLOCKS; bi++) {
+        const int b0 = j0 + bi * 64;
+        if (b0 >= j1) break;
         const int j = b0 + lane;
-        const unsigned long long m = (j < j1 && a.tmatch[j] < 0) ? a.mask[j] : 0ull;
-        const unsigned long long U = wave_or_u64(m);  // types present in the block
-        int ch = (m && !(m & (m - 1))) ? (__ffsll((long long)m) - 1) : -1;
+        const unsigned long long m = mk[bi];
+        // the lane's first four types in registers, the rest (rare) by a walk over the mask
+        int ty[4];
+        unsigned long long rest = m;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            ty[q] = rest ? __ffsll((long long)rest) - 1 : -1;
+            rest &= rest - 1;
+        }
+        int ch = seeded ? (sd[bi] == CHT_NONE ? -1 : (int)sd[bi])
+                        : ((m && !(m & (m - 1))) ? ty[0] : -1);
+        int prev = -1;
         unsigned long long chg;
         do {
+            if (prev >= 0) rec[prev].bal = 0ull;
+            __builtin_amdgcn_wave_barrier();
+            if (ch >= 0) atomicOr(&rec[ch].bal, 1ull << lane);
+            __builtin_amdgcn_wave_barrier();
             unsigned int best = ~0u;
-            for (int g = 0; g < T; g += TB) {
-                if (!((U >> g) & ((1ull << TB) - 1))) continue;
-                unsigned int vq[TB];
-                bool okq[TB];
 #pragma unroll
-                for (int q = 0; q < TB; q++) {
-                    const int t = g + q, tt = t < T ? t : 0;
-                    const int pos = __builtin_amdgcn_readlane(my_c0, tt) + (int)mbcnt64(__ballot(ch == t));
-                    okq[q] = t < T && ((m >> tt) & 1ull);
-                    vq[q] = win[tt * SEG + pos];
-                }
-#pragma unroll
-                for (int q = 0; q < TB; q++) best = min(best, okq[q] ? vq[q] : ~0u);
-            }
+            for (int q = 0; q < 4; q++)
+                if (ty[q] >= 0) best = min(best, head_of(rec, win, ty[q]));
+            for (unsigned long long r = rest; r; r &= r - 1) best = min(best, head_of(rec, win, __ffsll((long long)r) - 1));
             const int nch = best == ~0u ? -1 : (int)(best & 63u);
             chg = __ballot(nch != ch);
+            prev = ch;
             ch = nch;
             rounds++;
+            __builtin_amdgcn_wave_barrier();
         } while (chg);
+        // converged: the ballot words hold the final choices; results, then the block's counts
         int res = -1;
-        for (unsigned long long bb = U; bb; bb &= bb - 1) {
-            const int t = __ffsll((long long)bb) - 1;
-            const unsigned long long B = __ballot(ch == t);
-            if (ch == t)
-                res = __builtin_amdgcn_readlane(my_off, t) + __builtin_amdgcn_readlane(my_start, t) +
-                      __builtin_amdgcn_readlane(my_c0, t) + (int)mbcnt64(B);
-            if (lane == t) my_c0 += __popcll(B);
+        if (ch >= 0) {
+            const TypeRec r = rec[ch];
+            res = r.offst + r.c0 + (int)mbcnt64(r.bal);
         }
-        if (write && j < j1) a.umatch[j] = res;
+        __builtin_amdgcn_wave_barrier();
+        if (ch >= 0) {
+            rec[ch].bal = 0ull;
+            atomicAdd(&rec[ch].c0, 1);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (j < j1) {
+            a.umatch[j] = res;
+            a.cht[j] = ch < 0 ? CHT_NONE : (unsigned char)ch;
+        }
     }
-    return my_start + my_c0;
+    __builtin_amdgcn_wave_barrier();
+    return my_start + (lane < T ? rec[lane].c0 : 0);
 }
 
-// TB <= 8: uniform per-type state; TB == 64: wide variant (warm-up replayed
-// segment by segment).
+// load: the segment's inputs come from global memory (a new launch, or the
+// walk over other segments); otherwise round 0 staged them (T <= 8) and the
+// masks of request jb sit at mk0.
 template <int TB>
-__device__ __forceinline__ int seg_solve(const ChainArgs &a, int s, int jb, int my_start, unsigned int *win,
-                                         int &my_rec, int &rounds) {
+__device__ __forceinline__ int seg_solve(const ChainArgs a, int s, int jb, int my_start, unsigned int *win,
+                                         bool seeded, bool load, int mk0, int &my_rec, int &rounds) {
     if constexpr (TB <= 8) {
-        return seg_solve_small<TB>(a, s, jb, my_start, win, s * SEG - jb + SEG, my_rec, rounds);
+        return seg_solve_small<TB>(a, s, jb, my_start, win, s * SEG - jb + SEG, seeded, load, mk0, my_rec, rounds);
     } else {
-        for (int q = jb / SEG; q < s; q++) {  // pass 1's warm-up: replay the segments before s
-            my_start = seg_solve_wide<8>(a, q, my_start, win, rounds, false);
-            __builtin_amdgcn_wave_barrier();  // win is refilled
-        }
         my_rec = my_start;
-        return seg_solve_wide<8>(a, s, my_start, win, rounds);
+        TypeRec *rec = reinterpret_cast<TypeRec *>(win + a.T * SEG);
+        return seg_solve_wide(a, s, my_start, win, rec, seeded, rounds);
     }
 }
 
-// Inter-workgroup hand-off of one segment state (T <= 64 ints), following the
-// write-through protocol of MI355X_MICROARCH.md (inter-workgroup visibility):
-// sc1 stores, drained, then an agent-scope flag store by one lane; the reader
-// polls that flag relaxed and reads the payload with sc1 loads.
-__device__ __forceinline__ void publish_state(int *dst, int *flag, unsigned int epoch, int v, int T) {
-    if (threadIdx.x < T) __hip_atomic_store(dst + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// After a round: segment s publishes its start and delta (sc1 stores, drained
+// before the arrival), then arrives at its group, and the group at the top
+// counter.  When the next launch takes prefix starts, the last arriver of each
+// group also sums the group's deltas (LP, GT) and the last group the group
+// offsets (GO).  The very last arriver of the launch records the round, sets
+// `clean` when nothing was re-solved (never in round 0) and, in the final round
+// launch, walks what is still inconsistent.
+constexpr unsigned long long CNT20 = (1ull << 20) - 1;
+
+template <int TB>
+__device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, int dv, int solved, int bad, int rounds,
+                                             int round, int passes, bool final, bool prefix, unsigned int *win) {
+    const int lane = threadIdx.x, T = a.T, nseg = a.nseg;
+    if (lane < T) {
+        st_sc1(a.S + s * T + lane, sv);
+        st_sc1(a.D + s * T + lane, dv);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) __hip_atomic_store(flag, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int g = s / a.gs, g0 = g * a.gs, gn = min(nseg, g0 + a.gs) - g0, ng = (nseg + a.gs - 1) / a.gs;
+    // fields packed in one 64-bit add: arrivals (bits 0-19), possibly inconsistent
+    // segments (20-39), segment re-solves (40-63)
+    const unsigned long long mine = ((unsigned long long)solved << 40) | ((unsigned long long)bad << 20) | 1ull;
+    int last = 0;
+    unsigned long long v = 0;
+    if (lane == 0) {
+        if (rounds) atomicAdd(&a.ctr->chain_rounds, rounds);  // diagnostic, no return
+        v = atomicAdd(&a.counters[g], mine) + mine;
+        last = (int)(v & CNT20) == gn;
+    }
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    chain_stamp(a, s, 6);
+    // the group's last arriver: local exclusive prefix of the deltas, and the group total
+    if (prefix && lane < T) {
+        int acc = 0;
+        for (int q0 = 0; q0 < gn; q0 += 16) {
+            int d[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) d[i] = q0 + i < gn ? ld_sc1(a.D + (g0 + q0 + i) * T + lane) : 0;
+#pragma unroll
+            for (int i = 0; i < 16; i++)
+                if (q0 + i < gn) {
+                    st_sc1(a.LP + (g0 + q0 + i) * T + lane, acc);
+                    acc += d[i];
+                }
+        }
+        st_sc1(a.GT + g * T + lane, acc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    unsigned long long tot = 0;
+    if (lane == 0) {
+        const unsigned long long up = (v & ~CNT20) | 1ull;  // the group's counts, one arrival
+        tot = atomicAdd(&a.counters[CH_GROUPS], up) + up;
+        last = (int)(tot & CNT20) == ng;
+    }
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    chain_stamp(a, s, 7);
+    // ---- the last arriver of the launch
+    if (prefix && lane < T) {
+        int x[CH_GROUPS];
+#pragma unroll
+        for (int q = 0; q < CH_GROUPS; q++) x[q] = q < ng ? ld_sc1(a.GT + q * T + lane) : 0;
+        int acc = 0;
+#pragma unroll
+        for (int q = 0; q < CH_GROUPS; q++)
+            if (q < ng) {
+                a.GO[q * T + lane] = acc;
+                acc += x[q];
+            }
+    }
+    const unsigned long long totu =
+        ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned int)(tot >> 32)) << 32) |
+        __builtin_amdgcn_readfirstlane((unsigned int)tot);
+    const int nbad = (int)((totu >> 20) & CNT20), nsolved = (int)(totu >> 40);
+    const bool clean = nbad == 0;  // every start equals its predecessor's end
+    if (lane == 0) {
+        for (int q = 0; q <= CH_GROUPS; q++) a.counters[q] = 0;  // for the next launch (kernel boundary in between)
+        *a.clean = clean ? 1 : 0;
+        if (round == 0) {
+            a.ctr->chain_passes = passes;
+            a.ctr->chain_recomputed = nsolved;
+            a.ctr->chain_fallback = 0;
+        } else {
+            a.ctr->chain_passes += 1;
+            a.ctr->chain_recomputed += nsolved;
+        }
+    }
+    if (!final || clean) return;
+    // ---- walk: every segment before the first inconsistent one (start !=
+    // predecessor's end) is exact; from there on, in order, re-solve each
+    // segment whose start differs from the running exact start
+    int redo = 0, rounds_w = 0;
+    int first = nseg;
+    for (int c0 = 0; c0 < nseg && first == nseg; c0 += 64) {
+        const int q = c0 + lane;
+        bool bad = false;
+        if (q < nseg)
+            for (int t = 0; t < T; t++)
+                bad |= ld_sc1(a.S + q * T + t) !=
+                       (q ? ld_sc1(a.S + (q - 1) * T + t) + ld_sc1(a.D + (q - 1) * T + t) : 0);
+        const unsigned long long bb = __ballot(bad);
+        if (bb) first = c0 + __ffsll((long long)bb) - 1;
+    }
+    if (first < nseg) {
+        int st = (lane < T && first > 0) ? ld_sc1(a.S + (first - 1) * T + lane) + ld_sc1(a.D + (first - 1) * T + lane)
+                                         : 0;
+        constexpr int AHEAD = 8;  // S and D of the next segments in flight
+        for (int q0 = first; q0 < nseg; q0 += AHEAD) {
+            int sq[AHEAD], dq[AHEAD];
+#pragma unroll
+            for (int i = 0; i < AHEAD; i++) {
+                const bool ok = lane < T && q0 + i < nseg;
+                sq[i] = ok ? ld_sc1(a.S + (q0 + i) * T + lane) : 0;
+                dq[i] = ok ? ld_sc1(a.D + (q0 + i) * T + lane) : 0;
+            }
+#pragma unroll
+            for (int i = 0; i < AHEAD; i++) {
+                const int q = q0 + i;
+                if (q >= nseg) break;
+                if (__ballot(lane < T && sq[i] != st)) {
+                    int rec;
+                    __builtin_amdgcn_wave_barrier();  // win is refilled
+                    st = seg_solve<TB>(a, q, q * SEG, st, win, true, true, 0, rec, rounds_w);
+                    redo++;
+                } else {
+                    st += dq[i];
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        a.ctr->chain_fallback = redo;
+        atomicAdd(&a.ctr->chain_rounds, rounds_w);
+    }
 }
 
-// Wait (bounded: CHAIN_WAIT_US of wall clock) for a flag; false on timeout.
-// Uniform over the wave.  A timeout costs time, never correctness: the pass is
-// skipped and the last wavefront's walk repairs what it left.
+// In-launch neighbour passes of round 0 (T <= 64 ints per hand-off), following
+// the write-through protocol of MI355X_MICROARCH.md (inter-workgroup
+// visibility): sc1 stores, drained, then an sc1 flag store by one lane; the
+// reader polls the flag (relaxed, agent scope) and reads the state with sc1
+// loads.  Waits are bounded (CHAIN_WAIT_US of wall clock): a timed-out wait
+// skips that pass and is counted (chain_timeouts); it costs time, never
+// correctness, since the segment then reports itself unchecked.
 constexpr long long CHAIN_WAIT_US = 500;
+constexpr int CHAIN_MAX_PASSES = 8;
+
+__device__ __forceinline__ void publish_state(int *dst, int *flag, unsigned int epoch, int v, int T) {
+    if (threadIdx.x < T) st_sc1(dst + threadIdx.x, v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) st_sc1(flag, (int)epoch);
+}
+
 __device__ __forceinline__ bool wait_flag(const int *flag, unsigned int epoch) {
     int ok = 0;
     if (threadIdx.x == 0) {
         const long long t0 = wall_clock64(), limit = CHAIN_WAIT_US * 100;  // 100 MHz constant clock
         while (true) {
-            if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)epoch) {
+            if (ld_sc1(flag) == (int)epoch) {
                 ok = 1;
                 break;
             }
@@ -1378,49 +1647,41 @@ __device__ __forceinline__ bool wait_flag(const int *flag, unsigned int epoch) {
     return __builtin_amdgcn_readfirstlane(ok) != 0;
 }
 
-__device__ __forceinline__ int load_state(const int *src, int T) {
-    return threadIdx.x < T ? __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-}
+struct ChainPass {
+    int *E;              // [CHAIN_MAX_PASSES][nseg][T] end state of segment s after pass k
+    int *flags;          // [CHAIN_MAX_PASSES][nseg] == epoch once E[k][s] is published
+    unsigned int epoch;  // per batch, never 0
+    int passes;          // in-launch passes, 1 .. CHAIN_MAX_PASSES (1: round 0 alone)
+};
 
-// Per segment and type: requests that may take an untargeted unit of that
-// type (k_chain's demand-capped level guess, T > 8).  One wave per segment.
-__global__ __launch_bounds__(64) void k_seg_demand(const unsigned long long *__restrict__ mask,
-                                                   const int *__restrict__ tmatch, int R, int T, int *dem) {
-    const int lane = threadIdx.x, s = blockIdx.x;
-    int my = 0;
-    for (int b0 = s * SEG; b0 < min(R, s * SEG + SEG); b0 += 64) {
-        const int j = b0 + lane;
-        const unsigned long long m = (j < R && tmatch[j] < 0) ? mask[j] : 0ull;
-        for (int t = 0; t < T; t++) {
-            const int c = __popcll(__ballot((m >> t) & 1ull));
-            if (lane == t) my += c;
+// Round 0: every segment from its level guess (lane t = type t's head), then
+// passes 2 .. P in the same launch: segment s waits for segment s-1's end of
+// the previous pass and re-solves (seeded) only if it differs from its own
+// start; finally each segment checks its start against its predecessor's last
+// end.  A launch in which every check holds is the fixed point.
+template <int TB>
+__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final) {
+    extern __shared__ unsigned int win[];
+    const int lane = threadIdx.x, T = a.T, s = blockIdx.x, nseg = a.nseg, P = cp.passes;
+    chain_stamp(a, s, 0);
+    if (s == 0 && lane == 0) *a.clean = 0;
+    if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
+    int rounds = 0;
+    const int jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
+    // the type masks of [jb, segment end) in flight with the guess's loads (T <= 8: staged in LDS)
+    constexpr int NRB = TB <= 8 ? (SEG + CHAIN_WARM) / 64 : 1;
+    unsigned long long mk[NRB];
+    int tm[NRB];
+    const int j1 = min(a.R, s * SEG + SEG);
+    if constexpr (TB <= 8) {
+#pragma unroll
+        for (int i = 0; i < NRB; i++) {
+            const int j = jb + i * 64 + lane;
+            const bool ok = j < j1;
+            mk[i] = ok ? a.mask[j] : 0ull;
+            tm[i] = ok ? a.tmatch[j] : 0;
         }
     }
-    if (lane < T) dem[s * T + lane] = my;
-}
-
-// The whole ordered choice in one launch, one wavefront per segment.
-//   pass 1: every segment from its level guess, after a warm-up replay;
-//   pass k = 2 .. passes: segment s (= workgroup s) waits for segment s-1's
-//     pass k-1 end state and recomputes only if it differs from its own start
-//     (every wait is bounded in wall-clock time: a timed-out wait skips the
-//     pass, and a predecessor that is not running cannot deadlock anyone);
-//   each segment then compares its final start with its predecessor's final
-//     end (published in the last pass) and reports a mismatch in its arrival
-//     (two-level counter).  No mismatch anywhere is the fixed point, i.e. the
-//     sequential result (segment 0 starts from 0; induction).  Otherwise the
-//     last wavefront to arrive walks from the first mismatch, whose start is
-//     exact, recomputing the segments whose start differs and skipping the
-//     runs that stand.
-template <int TB>
-__global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
-    extern __shared__ unsigned int win[];
-    const int lane = threadIdx.x, T = a.T, K = a.passes, nseg = a.nseg;
-    const int s = blockIdx.x;
-    if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
-    int rounds = 0, recomputed = 0;
-    // pass 1
-    const int jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
     int J = 0;                                // requests before jb that take an untargeted unit
     for (int q = lane; q < (jb >> 6); q += 64) J += a.seg_cnt[q];
 #pragma unroll
@@ -1429,122 +1690,88 @@ __global__ __launch_bounds__(64) void k_chain(ChainArgs a) {
     if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
         const int G = a.candoff[T], len = lane < T ? a.candlen[lane] : 0;
         guess = lane >= T || J == 0 ? 0 : J >= G ? len : a.lv[(long long)J * T + lane];
-    } else if (a.dem != nullptr) {
-        // demand-capped level: type t's head is at most the requests before
-        // jb that include t; the level L rises until the capped heads sum to J
-        // (slope <= 1: the iteration approaches the fixed point from below)
-        int D = 0;
-        if (lane < T)
-            for (int q = 0; q < jb / SEG; q++) D += a.dem[q * T + lane];
-        const int G = a.candoff[T];
-        int L = min(J, G);
-        guess = 0;
-        for (int it = 0; it < 4; it++) {
-            guess = min(level_guess<8>(a, L), D);
-            int f = guess;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
-            if (f >= J || L >= G) break;
-            L = min(G, L + (J - f));
-        }
     } else {
         guess = level_guess<(TB <= 8 ? TB : 8)>(a, J);
     }
-    int cur_start, cur_end = seg_solve<TB>(a, s, jb, guess, win, cur_start, rounds);
-    publish_state(a.E + ((long long)1 * nseg + s) * T, a.flags + (long long)1 * nseg + s, a.epoch, cur_end, T);
-    for (int k = 2; k <= K; k++) {
-        if (s > 0 && wait_flag(a.flags + (long long)(k - 1) * nseg + s - 1, a.epoch)) {
-            const int pe = load_state(a.E + ((long long)(k - 1) * nseg + s - 1) * T, T);
-            if (__ballot(lane < T && pe != cur_start)) {
-                int rec;
-                __builtin_amdgcn_wave_barrier();  // win is refilled
-                cur_end = seg_solve<TB>(a, s, s * SEG, pe, win, rec, rounds);
-                cur_start = pe;
-                recomputed++;
+    if constexpr (TB <= 8) {
+        unsigned long long *smk = staged_masks<TB>(a, win);
+#pragma unroll
+        for (int i = 0; i < NRB; i++)
+            if (jb + i * 64 < j1) smk[i * 64 + lane] = tm[i] < 0 ? mk[i] : 0ull;
+    }
+    chain_stamp(a, s, 1);
+    int start;
+    int end = seg_solve<TB>(a, s, jb, guess, win, false, TB > 8, 0, start, rounds);
+    chain_stamp(a, s, 2);
+    int solves = 0, timeouts = 0;
+    auto E = [&](int k, int q) { return cp.E + ((long long)k * nseg + q) * T; };
+    auto F = [&](int k, int q) { return cp.flags + (long long)k * nseg + q; };
+    publish_state(E(0, s), F(0, s), cp.epoch, end, T);
+    for (int k = 1; k < P; k++) {
+        if (s > 0) {
+            if (wait_flag(F(k - 1, s - 1), cp.epoch)) {
+                const int pe = lane < T ? ld_sc1(E(k - 1, s - 1) + lane) : 0;
+                if (__ballot(lane < T && pe != start)) {
+                    int rec;
+                    __builtin_amdgcn_wave_barrier();  // win is refilled
+                    end = seg_solve<TB>(a, s, s * SEG, pe, win, true, TB > 8, s * SEG - jb, rec, rounds);
+                    start = pe;
+                    solves++;
+                }
+            } else {
+                timeouts++;
             }
         }
-        publish_state(a.E + ((long long)k * nseg + s) * T, a.flags + (long long)k * nseg + s, a.epoch, cur_end, T);
+        publish_state(E(k, s), F(k, s), cp.epoch, end, T);
     }
-    // own check: does the final start equal the predecessor's final end?
-    int mybad = 0;
+    chain_stamp(a, s, 3);
+    // own check: the final start against the predecessor's final end
+    int bad = 0;
     if (s > 0) {
-        if (wait_flag(a.flags + (long long)K * nseg + s - 1, a.epoch)) {
-            const int pe = load_state(a.E + ((long long)K * nseg + s - 1) * T, T);
-            mybad = __ballot(lane < T && pe != cur_start) ? 1 : 0;
+        if (wait_flag(F(P - 1, s - 1), cp.epoch)) {
+            const int pe = lane < T ? ld_sc1(E(P - 1, s - 1) + lane) : 0;
+            bad = __ballot(lane < T && pe != start) ? 1 : 0;
         } else {
-            mybad = 1;  // unknown: the last wavefront looks
+            timeouts++;
+            bad = 1;  // unknown: a later round or the walk looks
         }
     }
-    // final states (for the walk), then arrive
-    if (lane < T) {
-        __hip_atomic_store(a.Sf + s * T + lane, cur_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.Ef + s * T + lane, cur_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (timeouts && lane == 0) atomicAdd(&a.ctr->chain_timeouts, timeouts);
+    chain_stamp(a, s, 4);
+    chain_arrive<TB>(a, s, start, end - start, solves, bad, rounds, 0, P, final != 0, prefix_next != 0, win);
+    chain_stamp(a, s, 5);
+}
+
+// Round k >= 1: a segment re-solves when its start differs from the estimate
+// of its exact start, seeded with its previous choices.  mode 0 (neighbour):
+// the estimate is the predecessor's end from the previous launch -- right as
+// soon as the predecessor was, and absorbing start errors where multi-type
+// requests level the list heads (few types); mode 1 (prefix): the sum of all
+// earlier deltas -- passes a start error that no choice depends on straight
+// through (many types, rare multi-type competition).  A launch that re-solved
+// nothing proves every start equal to its predecessor's end: the fixed point.
+template <int TB>
+__global__ __launch_bounds__(64) void k_chainr(ChainArgs a, int round, int final, int mode, int prefix_next) {
+    if (*a.clean) return;
+    extern __shared__ unsigned int win[];
+    const int lane = threadIdx.x, T = a.T, s = blockIdx.x, g = s / a.gs;
+    if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
+    const bool tl = lane < T;
+    int sv = tl ? a.Sp[s * T + lane] : 0;
+    int dv = tl ? a.Dp[s * T + lane] : 0;
+    int xv = 0;
+    if (mode == 0) xv = (tl && s > 0) ? a.Sp[(s - 1) * T + lane] + a.Dp[(s - 1) * T + lane] : 0;
+    else xv = tl ? a.GO[g * T + lane] + a.LP[s * T + lane] : 0;
+    int rounds = 0, solved = 0;
+    if (__ballot(tl && xv != sv)) {
+        int rec;
+        const int end = seg_solve<TB>(a, s, s * SEG, xv, win, true, true, 0, rec, rounds);
+        solved = 1;
+        sv = xv;
+        dv = end - xv;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // two-level arrival (8 groups, then the top counter), fields packed in one
-    // 64-bit add: arrivals (bits 0-19), mismatches (20-39), recomputes (40-63)
-    constexpr unsigned long long CNT = (1ull << 20) - 1;
-    int last = 0;
-    unsigned long long tot = 0;
-    if (lane == 0) {
-        atomicAdd(&a.ctr->chain_rounds, rounds);  // diagnostic, no return
-        const unsigned long long mine =
-            ((unsigned long long)recomputed << 40) | ((unsigned long long)mybad << 20) | 1ull;
-        const unsigned int g = (unsigned int)s & 7u, ng = ((unsigned int)nseg - g + 7u) / 8u,
-                           ngroups = min((unsigned int)nseg, 8u);
-        const unsigned long long v = atomicAdd(&a.counters[g], mine);
-        if ((v & CNT) == ng - 1u) {
-            const unsigned long long up = ((v + mine) & ~CNT) | 1ull;
-            const unsigned long long tv = atomicAdd(&a.counters[8], up);
-            if ((tv & CNT) == ngroups - 1u) {
-                last = 1;
-                tot = tv + up;
-            }
-        }
-    }
-    if (!__builtin_amdgcn_readfirstlane(last)) return;
-    // ---- the last wavefront: walk from the first mismatch, if any segment saw one
-    const unsigned long long totu = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned int)(tot >> 32)) << 32) |
-                                    __builtin_amdgcn_readfirstlane((unsigned int)tot);
-    const int nbad = (int)((totu >> 20) & CNT);
-    auto bad = [&](int q) {  // segment q's final start differs from segment q-1's final end
-        bool b = false;
-        for (int t = 0; t < T; t++)
-            b |= __hip_atomic_load(a.Sf + q * T + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                 __hip_atomic_load(a.Ef + (q - 1) * T + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return b;
-    };
-    auto next_bad = [&](int from) {
-        for (int c0 = from; c0 < nseg; c0 += 64) {
-            const int q = c0 + lane;
-            const unsigned long long bb = __ballot(q >= 1 && q < nseg && bad(q));
-            if (bb) return c0 + __ffsll((long long)bb) - 1;
-        }
-        return nseg;
-    };
-    int redo = 0, q = nbad ? next_bad(1) : nseg;
-    if (q < nseg) {
-        int st = load_state(a.Ef + (q - 1) * T, T);
-        while (q < nseg) {
-            if (__ballot(lane < T && st != load_state(a.Sf + q * T, T))) {
-                int rec;
-                __builtin_amdgcn_wave_barrier();
-                st = seg_solve<TB>(a, q, q * SEG, st, win, rec, rounds);
-                redo++;
-                q++;
-            } else {  // q stands, and so does every segment up to the next recorded mismatch
-                q = next_bad(q + 1);
-                if (q < nseg) st = load_state(a.Ef + (q - 1) * T, T);
-            }
-        }
-    }
-    if (lane == 0) {
-        a.ctr->chain_passes = K;
-        a.ctr->chain_recomputed = (int)(totu >> 40);
-        a.ctr->chain_fallback = redo;
-        atomicAdd(&a.ctr->chain_rounds, rounds);  // the walk's
-        for (int g = 0; g < 9; g++) a.counters[g] = 0;  // for the next batch (kernel boundary in between)
-    }
+    // a re-solved segment may now be inconsistent with a predecessor re-solved alongside it
+    chain_arrive<TB>(a, s, sv, dv, solved, solved, rounds, round, 0, final != 0, prefix_next != 0, win);
 }
 
 // ---------------------------------------------------------------- finalize + park
@@ -1789,7 +2016,8 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
     void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
-                  h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_pmask, h->d_lv};
+                  h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht,
+                  h->d_chcnt, h->d_chE, h->d_chflag, h->d_pmask, h->d_lv};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
@@ -1800,13 +2028,19 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
     AQ_HIP(hipMalloc((void **)&h->d_seg_cnt, sizeof(int) * ((nc + 63) / 64)));
     AQ_HIP(hipMalloc((void **)&h->d_pmask, sizeof(unsigned long long) * ((nc + 63) / 64)));
-    AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));
-    AQ_HIP(hipMemset(h->d_chflag, 0, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));  // epochs start at 1
-    AQ_HIP(hipMalloc((void **)&h->d_chSf, sizeof(int) * nseg * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chEf, sizeof(int) * nseg * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * 9));
-    AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(unsigned long long) * 9));  // the chain's last wavefront re-zeroes them
+    AQ_HIP(hipMalloc((void **)&h->d_chS, sizeof(int) * 2 * nseg * T1));  // two buffers: launch parity
+    AQ_HIP(hipMalloc((void **)&h->d_chD, sizeof(int) * 2 * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chLP, sizeof(int) * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * CHAIN_MAX_PASSES * nseg * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * CHAIN_MAX_PASSES * nseg));
+    AQ_HIP(hipMemset(h->d_chflag, 0, sizeof(int) * CHAIN_MAX_PASSES * nseg));  // epochs start at 1
+    AQ_HIP(hipMalloc((void **)&h->d_chGT, sizeof(int) * CH_GROUPS * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chGO, sizeof(int) * CH_GROUPS * T1));
+    AQ_HIP(hipMalloc((void **)&h->d_chclean, sizeof(int)));
+    AQ_HIP(hipMalloc((void **)&h->d_cht, (size_t)nc));
+    AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * (CH_GROUPS + 1)));
+    // the last arriver of every chain launch re-zeroes them
+    AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 1)));
     AQ_HIP(hipMalloc((void **)&h->d_lv, sizeof(int) * 8 * (size_t)nc));
     h->cap_req = nc;
     return ADLBQ_OK;
@@ -2202,25 +2436,56 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     stage_begin(h, "chain", &ev);
     {
         const int nseg = (R + SEG - 1) / SEG;
-        const int K = h->chain_passes > 0 ? h->chain_passes : (T <= 8 ? 3 : 8);
-        const int warm = h->chain_warm >= 0 ? h->chain_warm : (T <= 8 ? CHAIN_WARM : CHAIN_WARM_WIDE);
+        // in-launch neighbour passes of round 0, then round launches (the last
+        // launch walks in order whatever is still off the fixed point)
+        const int P = h->chain_passes > 0 ? std::min(h->chain_passes, CHAIN_MAX_PASSES) : (T <= 8 ? 3 : 2);
+        const int K = h->chain_rounds >= 0 ? h->chain_rounds : (T <= 8 ? 0 : 2);
+        const int warm = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
+        const int gs = (nseg + CH_GROUPS - 1) / CH_GROUPS;
+        const long long nsT = (long long)nseg * std::max(T, 1);
+        // round k's mode: bit k-1 of chain_modes (1 = prefix starts); default
+        // prefix rounds (the neighbour passes already ran inside round 0)
+        const long long modes = h->chain_modes != -1 ? h->chain_modes : ~0ll;
         if (++h->chain_epoch == 0) h->chain_epoch = 1;
-        ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, K, warm, h->chain_epoch, h->d_candoff, h->d_candlen,
-                     h->d_crank, h->d_umatch, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf,
-                     h->d_chcnt, h->d_ctr, (T <= 8 && np > 0) ? h->d_lv : nullptr, nullptr};
-        if (T > 8 && h->chain_guess == 1) {
-            if ((long long)nseg * T > h->cap_segdem) {
+        const ChainPass cp{h->d_chE, h->d_chflag, h->chain_epoch, P};
+        ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, warm, gs, h->d_candoff, h->d_candlen, h->d_crank,
+                     h->d_umatch, h->d_cht, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chS + nsT, h->d_chD + nsT,
+                     h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_chcnt, h->d_ctr,
+                     (T <= 8 && np > 0) ? h->d_lv : nullptr, nullptr};
+        if (h->chain_stamps) {
+            if (nseg > h->cap_stamps) {
                 AQ_HIP(hipStreamSynchronize(s));
-                if (h->d_segdem) AQ_HIP(hipFree(h->d_segdem));
-                h->cap_segdem = std::max((long long)nseg * T, 2 * h->cap_segdem);
-                AQ_HIP(hipMalloc((void **)&h->d_segdem, sizeof(int) * h->cap_segdem));
+                if (h->d_stamps) AQ_HIP(hipFree(h->d_stamps));
+                h->cap_stamps = nseg;
+                AQ_HIP(hipMalloc((void **)&h->d_stamps, sizeof(unsigned long long) * 16 * nseg));
             }
-            k_seg_demand<<<nseg, 64, 0, s>>>(h->d_mask, h->d_tmatch, R, T, h->d_segdem);
-            ca.dem = h->d_segdem;
+            AQ_HIP(hipMemsetAsync(h->d_stamps, 0, sizeof(unsigned long long) * 16 * nseg, s));
+            ca.stamps = h->d_stamps;
+            h->n_stamps = nseg;
         }
-        if (T <= 4) k_chain<4><<<nseg, 64, sizeof(unsigned int) * (4 * (SEG + warm) + 64), s>>>(ca);
-        else if (T <= 8) k_chain<8><<<nseg, 64, sizeof(unsigned int) * (8 * (SEG + warm) + 64), s>>>(ca);
-        else k_chain<64><<<nseg, 64, sizeof(unsigned int) * T * SEG, s>>>(ca);
+        auto flip = [&](int k) {  // launch k writes buffer k & 1 and reads the other
+            ca.S = h->d_chS + (k & 1) * nsT;
+            ca.D = h->d_chD + (k & 1) * nsT;
+            ca.Sp = h->d_chS + ((k + 1) & 1) * nsT;
+            ca.Dp = h->d_chD + ((k + 1) & 1) * nsT;
+        };
+        flip(0);
+        size_t lds;
+        // small variants: windows, sentinel row, staged masks (8 B) and seeds (1 B) per request
+        if (T <= 4) lds = sizeof(unsigned int) * (4 * (SEG + warm) + 64) + 9 * (SEG + warm);
+        else if (T <= 8) lds = sizeof(unsigned int) * (8 * (SEG + warm) + 64) + 9 * (SEG + warm);
+        else lds = sizeof(unsigned int) * T * SEG + sizeof(TypeRec) * ADLBQ_MAX_TYPES;
+        auto mode_of = [&](int k) { return (k >= 1 && k <= K) ? (int)(((unsigned long long)modes >> (k - 1)) & 1ull) : 0; };
+        if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
+        else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
+        else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
+        for (int k = 1; k <= K; k++) {
+            flip(k);
+            const int mode = mode_of(k), pn = mode_of(k + 1);
+            if (T <= 4) k_chainr<4><<<nseg, 64, lds, s>>>(ca, k, k == K, mode, pn);
+            else if (T <= 8) k_chainr<8><<<nseg, 64, lds, s>>>(ca, k, k == K, mode, pn);
+            else k_chainr<64><<<nseg, 64, lds, s>>>(ca, k, k == K, mode, pn);
+        }
     }
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);

@@ -628,10 +628,10 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
-                    h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chE, h->d_chflag, h->d_chSf, h->d_chEf, h->d_chcnt, h->d_export,
+                    h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
-                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_segdem};
+                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1033,8 +1033,17 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (!h || !name) return fail(ADLBQ_ERR_ARG, "adlbq_set_param");
     std::string n(name);
     if (n == "chain_passes") {
-        if (value < 0 || value > 30) return fail(ADLBQ_ERR_ARG, "chain_passes must be in [0, 30] (0 = auto)");
+        if (value < 0 || value > 8) return fail(ADLBQ_ERR_ARG, "chain_passes must be in [0, 8] (0 = auto)");
         h->chain_passes = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "chain_stamps") {
+        h->chain_stamps = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
+    if (n == "chain_rounds") {
+        if (value < -1 || value > 30) return fail(ADLBQ_ERR_ARG, "chain_rounds must be in [-1, 30] (-1 = auto)");
+        h->chain_rounds = (int)value;
         return ADLBQ_OK;
     }
     if (n == "chain_warm") {
@@ -1043,9 +1052,8 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_warm = (int)value;
         return ADLBQ_OK;
     }
-    if (n == "chain_guess") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "chain_guess must be 0 or 1");
-        h->chain_guess = (int)value;
+    if (n == "chain_modes") {
+        h->chain_modes = value;
         return ADLBQ_OK;
     }
     if (n == "segsort_merged") {
@@ -1070,6 +1078,37 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n == "chain_passes") return h->ctr.chain_passes;
     if (n == "chain_recomputed") return h->ctr.chain_recomputed;
     if (n == "chain_fallback") return h->ctr.chain_fallback;
+    if (n == "chain_timeouts") return h->ctr.chain_timeouts;
+    if (n.rfind("chain_phase", 0) == 0 && h->d_stamps && h->n_stamps > 0) {
+        // diagnostic: "chain_phaseK" = median over segments of (stamp K - stamp 0)
+        // in ns; "chain_phaseK_max" = the largest; K = 1..7 (0 where unstamped)
+        const bool mx = n.size() > 4 && n.substr(n.size() - 4) == "_max";
+        const bool clk = n.size() > 4 && n.substr(n.size() - 4) == "_mhz";  // shader clock over phases 1-2
+        const int k = n[11] - '0';
+        if (k < 1 || k > 7) return -1;
+        std::vector<unsigned long long> st(16 * (size_t)h->n_stamps);
+        if (clk) {
+            if (hipMemcpy(st.data(), h->d_stamps, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost) != hipSuccess)
+                return -1;
+            std::vector<long long> f;
+            for (int q = 0; q < h->n_stamps; q++) {
+                const unsigned long long *r = &st[8 * q], *c = &st[8 * ((size_t)h->n_stamps + q)];
+                if (r[k] > r[1] && r[1]) f.push_back((long long)((c[k] - c[1]) * 100 / (r[k] - r[1])));
+            }
+            if (f.empty()) return 0;
+            std::sort(f.begin(), f.end());
+            return f[f.size() / 2];
+        }
+        st.resize(8 * (size_t)h->n_stamps);
+        if (hipMemcpy(st.data(), h->d_stamps, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+        std::vector<long long> d;
+        for (int q = 0; q < h->n_stamps; q++)
+            if (st[8 * q + k] && st[8 * q]) d.push_back((long long)(st[8 * q + k] - st[8 * q]) * 10);
+        if (d.empty()) return 0;
+        std::sort(d.begin(), d.end());
+        return mx ? d.back() : d[d.size() / 2];
+    }
     if (n == "parked") return h->ctr.n_parked_last;
     if (n == "spec_lists") return h->ctr.spec_page0;
     if (n == "candidates") {

@@ -72,11 +72,16 @@ def parse():
     ap.add_argument("--c4-units", type=int, default=10_000_000, help="config 4: units (80%% targeted)")
     ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--c4-chain-passes", type=int, default=None,
-                    help="config 4: parallel chain passes before the in-order fix-up (adlbq 'chain_passes')")
-    ap.add_argument("--c4-chain-warm", type=int, default=None,
-                    help="config 4: requests replayed before each chain segment in pass 1 (adlbq 'chain_warm')")
-    ap.add_argument("--c4-chain-guess", type=int, default=None,
-                    help="config 4: chain pass-1 guess, 0 level (default), 1 demand-capped level (adlbq 'chain_guess')")
+                    help="config 4: in-launch neighbour passes of the ordered choice's round 0 (adlbq 'chain_passes')")
+    ap.add_argument("--c4-chain-rounds", type=int, default=None,
+                    help="config 4: ordered-choice round launches after round 0 (adlbq 'chain_rounds')")
+    ap.add_argument("--chain-rounds", type=int, default=None, help="metric leg: adlbq 'chain_rounds'")
+    ap.add_argument("--chain-stamps", action="store_true",
+                    help="metric leg: after the timed region, one batch with the chain's phase stamps (diagnostic)")
+    ap.add_argument("--c4-chain-modes", type=int, default=None, help="config 4: adlbq 'chain_modes'")
+    ap.add_argument("--chain-passes", type=int, default=None, help="metric leg: adlbq 'chain_passes'")
+    ap.add_argument("--chain-modes", type=int, default=None, help="metric leg: adlbq 'chain_modes'")
+    ap.add_argument("--chain-warm", type=int, default=None, help="metric leg: adlbq 'chain_warm' (0, 256, 512)")
     ap.add_argument("--c4-chain-stats", action="store_true",
                     help="config 4: after the timed region, replay each batch alone and report its chain counters")
     ap.add_argument("--c4-segsort-wide", type=int, default=None,
@@ -324,12 +329,12 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
     stream = torch.cuda.Stream(dev)
     srv.set_stream(stream.cuda_stream)
-    if args.c4_chain_guess is not None:
-        srv.set_param("chain_guess", args.c4_chain_guess)
-    if args.c4_chain_warm is not None:
-        srv.set_param("chain_warm", args.c4_chain_warm)
     if args.c4_chain_passes is not None:
         srv.set_param("chain_passes", args.c4_chain_passes)
+    if args.c4_chain_modes is not None:
+        srv.set_param("chain_modes", args.c4_chain_modes)
+    if args.c4_chain_rounds is not None:
+        srv.set_param("chain_rounds", args.c4_chain_rounds)
     if args.c4_segsort_wide is not None:
         srv.set_param("segsort_merged", 0)
         srv.set_param("segsort_wide", args.c4_segsort_wide)
@@ -390,7 +395,7 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
             torch.cuda.synchronize()
             per_batch.append({"ms": round((time.perf_counter() - t1) * 1e3, 3),
                               **{k: srv.stat(k) for k in ("chain_rounds", "chain_passes", "chain_recomputed",
-                                                          "chain_fallback")}})
+                                                          "chain_fallback", "chain_timeouts")}})
     out = {
         "workload": f"config4: {N} units/shard (80% targeted, Zipf(1.1) over 1024 ranks), 32 Zipf types, "
                     f"prio U[0,2^16), {R} hanging Reserves/step with 1-4 types",
@@ -445,6 +450,14 @@ def main():
     w = synth.config2(n_units=N, n_types=args.types, n_reserves=R, seed=shards.shard_seed(args.seed, rank),
                       equal_prio=args.equal_prio)
     srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
+    if args.chain_passes is not None:
+        srv.set_param("chain_passes", args.chain_passes)
+    if args.chain_warm is not None:
+        srv.set_param("chain_warm", args.chain_warm)
+    if args.chain_modes is not None:
+        srv.set_param("chain_modes", args.chain_modes)
+    if args.chain_rounds is not None:
+        srv.set_param("chain_rounds", args.chain_rounds)
     # one explicit stream for the library and the torch glue ops (the handle's
     # own stream is non-blocking and would not order against torch's null stream)
     stream = torch.cuda.Stream(dev)
@@ -516,6 +529,14 @@ def main():
             dom_timed = round((ms - base_dom[0]) / (n - base_dom[1]), 4)
             stages[dominant] = dom_timed
 
+    phases = None
+    if args.chain_stamps:
+        srv.set_param("chain_stamps", 1)
+        step(args.warmup)
+        torch.cuda.synchronize()
+        phases = {f"phase{k}": (srv.stat(f"chain_phase{k}"), srv.stat(f"chain_phase{k}_max")) for k in range(1, 8)}
+        phases["clock_mhz_pass1"] = srv.stat("chain_phase2_mhz")
+        srv.set_param("chain_stamps", 0)
     live = srv.last_scan_units()
     # algorithmic bytes per launch: SURVEY §8(d)'s 16 B per live
     # unit for the open-bucket scan (hist + select together), 20 B per Reserve
@@ -568,9 +589,12 @@ def main():
                               "k_prep_hist + k_select_open (time includes the request preparation)") if scan_ms else None,
         "roofline_batch": roof(alg["batch"], batch_ms, None, "all reserve-batch kernels"),
         "kernels_ms": kernels,
-        "chain_last_batch": {k: srv.stat("chain_" + k) for k in ("rounds", "passes", "recomputed", "fallback")},
+        "chain_last_batch": {k: srv.stat("chain_" + k) for k in ("rounds", "passes", "recomputed", "fallback",
+                                                                  "timeouts")},
         "candidates_last_batch": srv.stat("candidates"),
     }
+    if phases:
+        res["chain_phases_ns"] = phases
     srv.close()
     del d_reqs, d_resp
     if not args.no_config3:

@@ -191,8 +191,8 @@ int  adlbq_sync(adlbq_server *h);
 /* Per-kernel GPU time (HIP events on the handle's stream around each launch of
  * a reserve batch) when enabled.  Stage names: "prep" (k_req_prep), "hist"
  * (k_hist_open), "thresholds", "select" (k_select_open), "sort"
- * (k_sort_types), "targeted", "rank", "chain" (k_chain_pass x passes +
- * k_chain_fix), "finalize" (k_finalize, which also parks). */
+ * (k_sort_types), "targeted", "rank", "chain" (k_chain0 + the k_chainr
+ * round launches), "finalize" (k_finalize, which also parks). */
 int  adlbq_profile_enable(adlbq_server *h, int on);
 /* Profile one stage only (NULL: every stage); enables profiling. */
 int  adlbq_profile_only(adlbq_server *h, const char *stage);
@@ -201,27 +201,32 @@ int  adlbq_profile_read(adlbq_server *h, const char *stage, double *total_ms, lo
  * 16 B x live units. */
 long long adlbq_last_scan_units(adlbq_server *h);
 /* Diagnostics of the last reserve batch: "chain_rounds" (Jacobi rounds of the
- * ordered-choice kernels, all wavefronts), "chain_passes" (segment passes that
- * recomputed something), "chain_recomputed" (segment solves in those passes),
- * "chain_fallback" (segments the in-order fix-up recomputed; 0 when the passes
- * reached their fixed point), "parked" (Reserves parked), "candidates",
+ * ordered-choice kernels, all wavefronts), "chain_passes" (passes of the
+ * first launch plus the round launches that were not no-ops),
+ * "chain_recomputed" (segment re-solves after pass 1), "chain_fallback"
+ * (segments the last launch's in-order walk re-solved; 0 once a pass or round
+ * reached the fixed point), "chain_timeouts" (bounded hand-off waits between
+ * passes that gave up, cumulative; they cost time only), "parked" (Reserves parked), "candidates",
  * "sort_timeouts" (waits of the rank pass for an in-launch sort that gave up,
  * cumulative; 0 unless something is broken), "device_sorted_lists" (candidate
  * lists long enough for a device-wide radix sort of their own, cumulative).
  * -1 if unknown. */
 long long adlbq_stat(adlbq_server *h, const char *name);
-/* Tuning: "chain_passes" = parallel segment passes of the ordered-choice
- * kernel before the in-order fix-up (1..30; 0 = auto: 3 for up to 8 types,
- * else 8); "chain_warm" = requests replayed ahead of each segment in the first
- * pass (-1 = auto: 512 for up to 8 types; or 0, 256, 512); "segsort_wide" =
- * candidate-list length from which a multi-priority list is sorted by a
- * device-wide radix sort of its own rather than a shared segmented sort
- * (default 16384) when the lists are not sorted together; "segsort_merged" =
- * 1 (default) sorts every list in one device-wide radix sort when no list's
- * keys differ in their top 6 bits, 0 always sorts list by list; "chain_guess"
- * = the ordered-choice kernel's first-pass state guess for more than 8 types:
- * 0 (default) the plain level guess, 1 caps each type's level head by the
- * requests before the segment that include the type.
+/* Tuning: "chain_passes" = passes of the ordered choice's first launch (1..8;
+ * 0 = auto: 3 for up to 8 types, else 2): pass 1 solves every segment from a
+ * guess, each later pass re-solves a segment whose start differs from its
+ * predecessor's end of the pass before; "chain_rounds" = further launches
+ * (0..30; -1 = auto: 0 for up to 8 types, else 2), the last of which walks in
+ * order whatever is still off the fixed point; "chain_modes" = bit k-1 set:
+ * round launch k starts each segment from the prefix sum of the earlier
+ * segments' deltas, clear: from its predecessor's end (-1 = auto: prefix);
+ * "chain_warm" = requests replayed ahead of each segment in pass 1 for up to 8
+ * types (-1 = auto (512); or 0, 256, 512); "segsort_wide" = candidate-list
+ * length from which a multi-priority list is sorted by a device-wide radix
+ * sort of its own rather than a shared segmented sort (default 16384) when the
+ * lists are not sorted together; "segsort_merged" = 1 (default) sorts every
+ * list in one device-wide radix sort when no list's keys differ in their top
+ * 6 bits, 0 always sorts list by list.
  * Results never depend on them; tests lower them to force the other paths. */
 int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);

@@ -29,7 +29,7 @@ def run_abi(ut, cfg, trace, max_units=1 << 16, params=None, stats=None):
         assert s.stat("sort_timeouts") == 0, "k_rank timed out waiting for an in-launch sort"
         if stats is not None:
             stats.update({k: s.stat(k) for k in ("chain_passes", "chain_recomputed", "chain_fallback",
-                                                 "spec_lists")})
+                                                 "chain_timeouts", "spec_lists")})
         return out
 
 
@@ -82,8 +82,8 @@ def test_fresh_vs_oracle(gpu_available, name):
 @pytest.mark.parametrize("name", ["c2_n200k_r16k", "c2_t64_wide", "c4_n200k", "c4_t8_tied"])
 @pytest.mark.parametrize("passes", [1, 2, 3])
 def test_chain_fixup_path(gpu_available, name, passes):
-    """Few segment passes leave segments off their fixed point, so the in-order
-    fix-up kernel (k_chain_fix) recomputes them: still identical to the oracle."""
+    """Few round launches (no warm-up) leave segments off their fixed point, so
+    the last round's in-order walk re-solves them: still identical to the oracle."""
     w = CASES[name]()
     tr = synth.workload_trace(w)
     cfg = (w.num_app_ranks, 1, 0)
@@ -168,20 +168,20 @@ def test_full_size_config2_equal_prio_exact(gpu_available):
     _exact_full(w)
 
 
-@pytest.mark.parametrize("merged,wide,warm,guess",
-                         [(1, 16384, -1, 1), (0, 16384, -1, 1), (0, 256, -1, 1), (1, 16384, 512, 1), (1, 16384, -1, 0)])
-def test_config4_2m_exact(gpu_available, merged, wide, warm, guess):
+@pytest.mark.parametrize("merged,wide,rounds",
+                         [(1, 16384, -1), (0, 16384, -1), (0, 256, -1), (1, 16384, 0), (1, 16384, 1)])
+def test_config4_2m_exact(gpu_available, merged, wide, rounds):
     """Three batches: from the second on the multi-prio-bin candidate lists are
     sorted before the rank pass (launch_segsort): all lists in one merged
     device-wide radix sort (merged=1), or list by list, lists of `wide`
     entries or more by a device-wide sort each and shorter ones by a shared
-    segmented sort (256 forces the device-wide path).  warm=512: the 32-type
-    chain replays two segments before its own in pass 1.  guess: the 32-type
-    chain's pass-1 state guess (1 demand-capped level, 0 plain level)."""
+    segmented sort (256 forces the device-wide path).  rounds: prefix-round
+    launches of the 32-type ordered choice after round 0 (-1 = auto; 0 and 1
+    leave the in-order walk more to do)."""
     w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
     stats = {}
     _exact_full(w, batches=3, stats=stats, params=[("segsort_merged", merged), ("segsort_wide", wide),
-                                                       ("chain_warm", warm), ("chain_guess", guess)])
+                                                       ("chain_rounds", rounds)])
     if merged or wide == 256:
         assert stats["device_sorted_lists"] > 0, "the device-wide list sort did not run"
     assert stats["sort_timeouts"] == 0
