@@ -27,6 +27,7 @@ SIGNATURES = {
     "adlbq_get_reserved": (c_int, [P, c_int, c_int, P]),
     "adlbq_unreserve": (c_int, [P, c_int, c_int, c_int, P]),
     "adlbq_unreserve_batch_device": (c_int, [P, c_int, P]),
+    "adlbq_unreserve_resp_device": (c_int, [P, c_int, P, P]),
     "adlbq_qmstat_row": (c_int, [P, P, P]),
     "adlbq_set_qmstat_row": (c_int, [P, c_int, c_int, c_double, P]),
     "adlbq_check_remote": (c_int, [P, c_int, P, P]),

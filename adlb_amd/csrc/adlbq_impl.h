@@ -55,6 +55,7 @@ struct DevCounters {
     int chain_timeouts;    // bounded hand-off waits of round 0's neighbour passes that gave up (cumulative)
     int spec_page0;        // the last scan's page 0, wave 0 read pass 1's list (diagnostic)
     int needsort_last;     // the last reserve batch had a type whose threshold fell in a multi-prio bin
+    int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
 };
 
 struct Bucket {
@@ -200,6 +201,7 @@ struct adlbq_server {
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // round 0's in-launch passes, 0 = auto (adlbq_set_param "chain_passes")
     int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
+    int rank_in_select = 1;            // k_select_open ranks the candidates when it can ("rank_in_select")
     int chain_stamps = 0;              // diagnostic: phase stamps of the first chain launch ("chain_stamps")
     unsigned long long *d_stamps = nullptr; int cap_stamps = 0, n_stamps = 0;
     int chain_warm = -1;               // round-0 warm-up requests (T <= 8), -1 = auto ("chain_warm")
@@ -243,6 +245,7 @@ int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
+bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
 bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);

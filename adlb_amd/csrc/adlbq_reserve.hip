@@ -37,6 +37,8 @@ constexpr int SEG = 256;               // chain segment: requests per wavefront 
 constexpr int SEG_BLOCKS = SEG / 64;
 constexpr int CHAIN_WARM = 512;        // largest round-0 warm-up before a segment (T <= 8), a multiple of SEG
 constexpr int PREP_BLOCK = 256;        // prep_block workgroup
+constexpr int RANK_FAST_T = 8;         // k_select_open ranks the candidates itself for up to this many types
+constexpr int LV_STEP = 64;            // the chain's level rows are kept for every LV_STEP-th global rank
 static_assert(SEG % 64 == 0 && CHAIN_WARM % SEG == 0, "chain segments are whole waves of prep_block");
 
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, int l) {
@@ -384,6 +386,7 @@ __global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict
 //   3. per column: page prefix + counts of the earlier waves;
 //   4. a candidate's rank in its column = that start + the number of equal
 //      columns earlier in the wave's list (64 list entries per step).
+template <int TB>  // TB >= T; the candidates are ranked here only for TB <= RT
 __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
     const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
@@ -392,10 +395,12 @@ __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ candlen, int *__restrict__ candoff_out,
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
     const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
-    const int *__restrict__ pwide, DevCounters *ctr) {
+    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv, int R) {
+    constexpr int RT = TB <= RANK_FAST_T ? TB : 1;  // types of the fast ranking
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
-    __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES];
+    __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES], slen[RT];
+    __shared__ int sbo[RT * NB];  // binoff (fast ranking)
     const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = blockIdx.x;
     unsigned int *wc = lds;
     unsigned int *list = lds + 4 * C + w * 1024;
@@ -412,6 +417,13 @@ __global__ __launch_bounds__(256) void k_select_open(
     const int th_l = tl ? theta[lane] : -1, nd_l = tl ? need[lane] : 0, len_l = tl ? candlen[lane] : 0;
     const long long an_l = tl ? anchor[lane] : 0, gc_l = tl ? gcut[lane] : 0;
     const int sn = specn[(long long)p * 4 + w];
+    // binoff for the fast ranking (T <= 8: at most two columns per thread), in flight with the rest
+    int bo_r[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int c = threadIdx.x + q * 256;
+        bo_r[q] = (TB <= RANK_FAST_T && crank != nullptr && c < C) ? binoff[c] : 0;
+    }
     const unsigned int *__restrict__ sp = spec + ((long long)p * 4 + w) * SPEC_CAP;
     unsigned int se[SPEC_CAP / 64];
 #pragma unroll
@@ -449,7 +461,17 @@ __global__ __launch_bounds__(256) void k_select_open(
         sth[lane] = th_l;
         sneed[lane] = nd_l;
         scut[lane] = cut_l;
+        if (lane < RT) slen[lane] = len_l;
     }
+    // ranks computed here (k_rank then skips its tiles) when every threshold
+    // lies in an exact bin: every candidate list is then in (prio desc,
+    // position asc) order by construction, and a unit of another type u with
+    // the same prio precedes this one iff it lies earlier in the open bucket
+    const bool fast = TB <= RANK_FAST_T && crank != nullptr && __ballot(tl && th_l >= NBX) == 0;
+    if (fast)  // binoff (only read for the types with demand, the ones k_thresholds wrote it for)
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            if (threadIdx.x + q * 256 < C) sbo[threadIdx.x + q * 256] = bo_r[q];
     for (int c = threadIdx.x; c < 4 * C; c += blockDim.x) wc[c] = 0;
     if (threadIdx.x < 64) {  // candidate list offsets: exclusive prefix of candlen over types
         const int len = len_l;
@@ -520,6 +542,19 @@ __global__ __launch_bounds__(256) void k_select_open(
     }
     __syncthreads();
     unsigned int *run = wc + w * C;
+    // the fast ranking's per-type constants, uniform over the wave (from LDS once)
+    long long an_u[RT];
+    int th_u[RT], nd_u[RT], len_u[RT];
+    if (fast) {
+#pragma unroll
+        for (int u = 0; u < RT; u++) {
+            const bool ok = u < T;
+            an_u[u] = ok ? sanc[u] : 0;
+            th_u[u] = ok ? sth[u] : -1;
+            nd_u[u] = ok ? sneed[u] : 0;
+            len_u[u] = ok ? slen[u] : 0;
+        }
+    }
     for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
         const unsigned int e = i < n ? list[i] : 0u;
@@ -530,9 +565,29 @@ __global__ __launch_bounds__(256) void k_select_open(
         const int ct = col / NB, cb = col - ct * NB;
         const int pr = i >= n ? 0 : cb < NBX ? (int)(sanc[ct] - cb) : prio[base + so];
         const unsigned int bpos = ((unsigned int)p << PAGE_SHIFT) | (unsigned int)so;
+        // fast ranking: per type u, the column holding prio pr (exact bins at
+        // or below u's threshold), else -1 (u has no unit of prio pr among its
+        // candidates: all of them are better, or none)
+        int tcol[RT], cnt[RT];
+        if (fast) {
+#pragma unroll
+            for (int u = 0; u < RT; u++) {
+                const long long bu = an_u[u] - (long long)pr;
+                tcol[u] = (bu >= 0 && bu <= th_u[u]) ? u * NB + (int)bu : -1;
+                cnt[u] = 0;
+            }
+        }
         int rank = 0;
         const int jn = min(n - i0, 64);
-        for (int j = 0; j < jn; j++) rank += (j < lane) & ((int)(list[i0 + j] >> 12) == col);
+        for (int j = 0; j < jn; j++) {
+            const int cj = (int)(list[i0 + j] >> 12);
+            const int before = j < lane;
+            rank += before & (cj == col);
+            if (fast) {
+#pragma unroll
+                for (int u = 0; u < RT; u++) cnt[u] += before & (cj == tcol[u]);
+            }
+        }
         if (i < n) {
             const unsigned int r = run[col] + rank;
             const int t = col / NB, b = col - t * NB;
@@ -540,12 +595,36 @@ __global__ __launch_bounds__(256) void k_select_open(
                 const long long at = (long long)soff[t] + binoff[col] + r;
                 ckey[at] = make_key(pr, bpos);
                 cslot[at] = (int)(base + so);
+                if (fast) {
+                    // global rank: per type u, its candidates better than this one
+                    int lb[RT], g = 0;
+#pragma unroll
+                    for (int u = 0; u < RT; u++) {
+                        lb[u] = 0;
+                        if (tcol[u] >= 0) {
+                            int c = (int)run[tcol[u]] + cnt[u];  // units of prio pr earlier in the bucket
+                            if (tcol[u] - u * NB == th_u[u]) c = min(c, nd_u[u]);  // the threshold bin's first `need`
+                            lb[u] = sbo[tcol[u]] + c;
+                        } else if (an_u[u] >= (long long)pr) {
+                            lb[u] = len_u[u];  // every candidate of u is better
+                        }
+                        g += lb[u];
+                    }
+                    crank[at] = ((unsigned int)g << 6) | (unsigned int)t;
+                    // level rows, sampled every LV_STEP ranks (the chain's guess interpolates)
+                    if (lv != nullptr && (g & (LV_STEP - 1)) == 0 && g < R)
+#pragma unroll
+                        for (int u = 0; u < RT; u++)
+                            if (u < T) lv[(long long)(g / LV_STEP) * T + u] = lb[u];
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
         if (i < n) atomicAdd(&run[col], 1u);  // after every lane of the step has read run[]
         __builtin_amdgcn_wave_barrier();
     }
+    if (fast && p == 0 && threadIdx.x == 0) ctr->rank_fast = 1;
+    if (!fast && crank != nullptr && p == 0 && threadIdx.x == 0) ctr->rank_fast = 0;
 }
 
 // ---------------------------------------------------------------- per-type sort (multi-priority bins only)
@@ -911,10 +990,10 @@ __device__ __forceinline__ int lower_bound_key(const unsigned long long *L, int 
 // waits for those flags (relaxed poll, agent acquire).  Sorters are running
 // before anyone waits for them, so the waits cannot deadlock.  Without such a
 // type (the usual case) nobody draws a ticket or waits.
-// The chain's level guess for T <= 8: row g (g < R) holds, for the candidate
-// at global rank g, the number of candidates of each type ranked before it --
-// the lower bounds k_rank computes anyway -- i.e. the state in which the first
-// g candidates in preference order are taken.
+// The chain's level guess for T <= 8: row g / LV_STEP (g < R, g a multiple of
+// LV_STEP) holds, for the candidate at global rank g, the number of candidates
+// of each type ranked before it -- the lower bounds k_rank computes anyway --
+// i.e. the state in which the first g candidates in preference order are taken.
 struct LevelRows {
     int *lv;  // [R][T], or nullptr (T > 8)
     int R;
@@ -934,7 +1013,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
                                                     unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
                                                     long long ncsum, const unsigned long long *__restrict__ mask,
                                                     const int *__restrict__ tmatch, int R, int *seg_cnt, RankSort rs,
-                                                    LevelRows lr) {
+                                                    LevelRows lr, const DevCounters *ctr) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
     __shared__ unsigned long long span[4][RANK_SPAN];  // also the sort's LDS blocks
     static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * 4096,
@@ -1030,6 +1109,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         stile[T] = acc;
     }
     __syncthreads();
+    if (ctr->rank_fast) return;  // k_select_open ranked the candidates and wrote the level rows
     for (int tile = blockIdx.x; tile < stile[T]; tile += gridDim.x) {
         int t = 0;
         while (t + 1 < T && stile[t + 1] <= tile) t++;
@@ -1093,10 +1173,10 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
             __syncthreads();
         }
         if (tid < n) crank[soff[t] + i0 + tid] = (g << 6) | (unsigned int)t;
-        if (lr.lv != nullptr && tid < n && (int)g < lr.R) {
+        if (lr.lv != nullptr && tid < n && (int)g < lr.R && (g & (LV_STEP - 1)) == 0) {
 #pragma unroll
             for (int u = 0; u < 8; u++)
-                if (u < T) lr.lv[(long long)g * T + u] = lbv[u];
+                if (u < T) lr.lv[(long long)(g / LV_STEP) * T + u] = lbv[u];
         }
         __syncthreads();
     }
@@ -1246,7 +1326,8 @@ __device__ __forceinline__ unsigned char *staged_seeds(const ChainArgs a, unsign
 // mask of request jb at index mk0.
 template <int TB>
 __device__ __forceinline__ int seg_solve_small(const ChainArgs a, int s, int jb, int my_start, unsigned int *win,
-                                               int WL, bool seeded, bool load, int mk0, int &my_rec, int &rounds) {
+                                               int WL, bool seeded, bool load, int mk0, int my_off, int my_len,
+                                               int &my_rec, int &rounds) {
     const int lane = threadIdx.x, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
     int st[TB], off[TB], c0[TB];
     constexpr int NI = (SEG + CHAIN_WARM) / 64;  // WL <= SEG + CHAIN_WARM
@@ -1269,8 +1350,8 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs a, int s, int jb,
 #pragma unroll
     for (int q = 0; q < TB; q++) {
         st[q] = __builtin_amdgcn_readlane(my_start, q);
-        off[q] = q < a.T ? a.candoff[q] : 0;
-        const int len = q < a.T ? a.candlen[q] : 0;
+        off[q] = __builtin_amdgcn_readlane(my_off, q);  // lane t holds type t's list offset and length
+        const int len = __builtin_amdgcn_readlane(my_len, q);
         c0[q] = 0;
 #pragma unroll
         for (int i = 0; i < NI; i++) {
@@ -1372,10 +1453,8 @@ __device__ __forceinline__ unsigned int head_of(const TypeRec *rec, const unsign
 }
 
 __device__ __forceinline__ int seg_solve_wide(const ChainArgs a, int s, int my_start, unsigned int *win,
-                                              TypeRec *rec, bool seeded, int &rounds) {
+                                              TypeRec *rec, bool seeded, int my_off, int my_len, int &rounds) {
     const int lane = threadIdx.x, T = a.T, j0 = s * SEG, j1 = min(a.R, j0 + SEG);
-    const int my_off = lane < T ? a.candoff[lane] : 0;
-    const int my_len = lane < T ? a.candlen[lane] : 0;
     for (int g = 0; g < T; g += 8) {  // 8 types x SEG_BLOCKS loads in flight per lane
         unsigned int wv[8][SEG_BLOCKS];
 #pragma unroll
@@ -1470,13 +1549,15 @@ __device__ __forceinline__ int seg_solve_wide(const ChainArgs a, int s, int my_s
 // masks of request jb sit at mk0.
 template <int TB>
 __device__ __forceinline__ int seg_solve(const ChainArgs a, int s, int jb, int my_start, unsigned int *win,
-                                         bool seeded, bool load, int mk0, int &my_rec, int &rounds) {
+                                         bool seeded, bool load, int mk0, int my_off, int my_len, int &my_rec,
+                                         int &rounds) {
     if constexpr (TB <= 8) {
-        return seg_solve_small<TB>(a, s, jb, my_start, win, s * SEG - jb + SEG, seeded, load, mk0, my_rec, rounds);
+        return seg_solve_small<TB>(a, s, jb, my_start, win, s * SEG - jb + SEG, seeded, load, mk0, my_off, my_len,
+                                   my_rec, rounds);
     } else {
         my_rec = my_start;
         TypeRec *rec = reinterpret_cast<TypeRec *>(win + a.T * SEG);
-        return seg_solve_wide(a, s, my_start, win, rec, seeded, rounds);
+        return seg_solve_wide(a, s, my_start, win, rec, seeded, my_off, my_len, rounds);
     }
 }
 
@@ -1567,6 +1648,7 @@ __device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, i
         }
     }
     if (!final || clean) return;
+    const int my_off = lane <= T ? ld_sc1(a.candoff + lane) : 0, my_len = lane < T ? ld_sc1(a.candlen + lane) : 0;
     // ---- walk: every segment before the first inconsistent one (start !=
     // predecessor's end) is exact; from there on, in order, re-solve each
     // segment whose start differs from the running exact start
@@ -1601,7 +1683,7 @@ __device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, i
                 if (__ballot(lane < T && sq[i] != st)) {
                     int rec;
                     __builtin_amdgcn_wave_barrier();  // win is refilled
-                    st = seg_solve<TB>(a, q, q * SEG, st, win, true, true, 0, rec, rounds_w);
+                    st = seg_solve<TB>(a, q, q * SEG, st, win, true, true, 0, my_off, my_len, rec, rounds_w);
                     redo++;
                 } else {
                     st += dq[i];
@@ -1682,14 +1764,29 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
             tm[i] = ok ? a.tmatch[j] : 0;
         }
     }
-    int J = 0;                                // requests before jb that take an untargeted unit
-    for (int q = lane; q < (jb >> 6); q += 64) J += a.seg_cnt[q];
+    // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
+    const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
+    int J = 0;  // requests before jb that take an untargeted unit
+    {
+        const int nq = jb >> 6;
+        int cv[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) cv[u] = u * 64 + lane < nq ? a.seg_cnt[u * 64 + lane] : 0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) J += cv[u];
+        for (int q = 1024 + lane; q < nq; q += 64) J += a.seg_cnt[q];  // batches above 65,536 Reserves
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
     int guess;
     if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
-        const int G = a.candoff[T], len = lane < T ? a.candlen[lane] : 0;
-        guess = lane >= T || J == 0 ? 0 : J >= G ? len : a.lv[(long long)J * T + lane];
+        const int G = __builtin_amdgcn_readlane(my_off, T);
+        // the row at the sampled rank below J, the rest spread in proportion to the list lengths
+        const int Js = J & ~(LV_STEP - 1);
+        guess = lane >= T || J == 0 ? 0
+                : J >= G            ? my_len
+                                    : min(my_len, (Js ? a.lv[(long long)(Js / LV_STEP) * T + lane] : 0) +
+                                                      (int)((long long)(J - Js) * my_len / max(G, 1)));
     } else {
         guess = level_guess<(TB <= 8 ? TB : 8)>(a, J);
     }
@@ -1701,7 +1798,7 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
     }
     chain_stamp(a, s, 1);
     int start;
-    int end = seg_solve<TB>(a, s, jb, guess, win, false, TB > 8, 0, start, rounds);
+    int end = seg_solve<TB>(a, s, jb, guess, win, false, TB > 8, 0, my_off, my_len, start, rounds);
     chain_stamp(a, s, 2);
     int solves = 0, timeouts = 0;
     auto E = [&](int k, int q) { return cp.E + ((long long)k * nseg + q) * T; };
@@ -1714,7 +1811,7 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
                 if (__ballot(lane < T && pe != start)) {
                     int rec;
                     __builtin_amdgcn_wave_barrier();  // win is refilled
-                    end = seg_solve<TB>(a, s, s * SEG, pe, win, true, TB > 8, s * SEG - jb, rec, rounds);
+                    end = seg_solve<TB>(a, s, s * SEG, pe, win, true, TB > 8, s * SEG - jb, my_off, my_len, rec, rounds);
                     start = pe;
                     solves++;
                 }
@@ -1757,6 +1854,7 @@ __global__ __launch_bounds__(64) void k_chainr(ChainArgs a, int round, int final
     const int lane = threadIdx.x, T = a.T, s = blockIdx.x, g = s / a.gs;
     if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
     const bool tl = lane < T;
+    const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = tl ? a.candlen[lane] : 0;
     int sv = tl ? a.Sp[s * T + lane] : 0;
     int dv = tl ? a.Dp[s * T + lane] : 0;
     int xv = 0;
@@ -1765,7 +1863,7 @@ __global__ __launch_bounds__(64) void k_chainr(ChainArgs a, int round, int final
     int rounds = 0, solved = 0;
     if (__ballot(tl && xv != sv)) {
         int rec;
-        const int end = seg_solve<TB>(a, s, s * SEG, xv, win, true, true, 0, rec, rounds);
+        const int end = seg_solve<TB>(a, s, s * SEG, xv, win, true, true, 0, my_off, my_len, rec, rounds);
         solved = 1;
         sv = xv;
         dv = end - xv;
@@ -2090,7 +2188,7 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
 // candidate lists in preference order at d_candoff / d_candlen / d_cslot.
 // A reserve batch's request preparation (pa, nprep workgroups) rides in the
 // first launch.
-static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort) {
+static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort, int R) {
     const int T = h->T, C = T * NB;
     const int np = (int)h->open.pages.size();
     hipStream_t s = h->stream;
@@ -2115,10 +2213,12 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                                        h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0);
         stage_end(h, "thresholds", ev);
         stage_begin(h, "select", &ev);
-        k_select_open<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
+        auto sel = T <= 4 ? k_select_open<4> : T <= 8 ? k_select_open<8> : k_select_open<64>;
+        sel<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
-            h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr);
+            h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr,
+            (sort || !h->rank_in_select) ? nullptr : h->d_crank, (!sort && T <= 8) ? h->d_lv : nullptr, R);
         stage_end(h, "select", ev);
         if (sort) {  // a reserve batch sorts inside k_rank
             stage_begin(h, "sort", &ev);
@@ -2403,7 +2503,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipEvent_t ev;
 
     const PrepArgs pa{d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch};
-    if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false))) return rc;
+    if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) return rc;
     h->last_scan_units = h->live_units - h->live_targeted;
 
     const int nb = (int)h->bucket_ranks.size();
@@ -2428,9 +2528,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_begin(h, "rank", &ev);
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
         const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch};
-        k_rank<<<512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
+        // a small grid when the last landed batch was ranked in k_select_open
+        // (every loop is grid-strided: any grid is correct, the hint only sizes it)
+        k_rank<<<rank_hint(h) ? 64 : 512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
                                     (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
-                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R});
+                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R}, h->d_ctr);
         stage_end(h, "rank", ev);
     }
     stage_begin(h, "chain", &ev);
@@ -2519,7 +2621,7 @@ int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
     const int np = (int)h->open.pages.size();
     if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
     k_export_begin<<<1, 64, 0, h->stream>>>(h->d_dem, T, k);
-    if ((rc = launch_scan(h, PrepArgs{}, 0, true))) return rc;
+    if ((rc = launch_scan(h, PrepArgs{}, 0, true, 0))) return rc;
     const long long ncsum = np > 0 ? (long long)((np + CHUNK - 1) / CHUNK) * C : 0;
     k_export_gather<<<T, 256, 0, h->stream>>>(T, k, h->d_candoff, h->d_candlen, h->d_cslot, h->d_prio, h->d_seq,
                                               h->d_cold0, h->d_cold1, d_out, d_out + (size_t)T * k * 8, d_navail,

@@ -91,6 +91,17 @@ long long rq_live_upper(adlbq_server *h) {
 }
 
 // Whether the newest landed reserve batch needed a multi-prio-bin sort.
+bool rank_hint(adlbq_server *h) {  // the newest landed batch ranked its candidates in k_select_open
+    const int N = adlbq_server::NSNAP;
+    for (int k = 1; k <= N; k++) {
+        const int i = (h->snap_next - k + N) % N;
+        if (!h->snap_at[i]) continue;
+        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
+        return h->h_snap[i].rank_fast != 0;
+    }
+    return false;
+}
+
 bool sort_hint(adlbq_server *h) {
     const int N = adlbq_server::NSNAP;
     for (int k = 1; k <= N; k++) {
@@ -400,6 +411,33 @@ __global__ void k_unreserve_batch(const int *__restrict__ trip, int n, const lon
             const int4 r0 = rrec[2 * slot], r1 = rrec[2 * slot + 1];
             if ((m & M_LIVE) && pn == rank && r0.z == seq) {
                 pin[slot] = np;
+                meta[slot] = m & ~M_PINNED;
+                t = m & M_TYPE;
+                up = r1.w;
+            }
+        }
+    }
+    raise_anchor(anchor, t, up);  // available again: keep the anchor above it
+}
+
+// SS_UNRESERVE of every unit a reserve batch handed out, read straight from the
+// batch's requests and TA_RESERVE_RESP records (rc 1 = matched, [5] = wqseqno;
+// the new pin is -1, i.e. the unit is available again)
+__global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
+                                 const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta, int *pin,
+                                 const int4 *__restrict__ rrec, long long *anchor) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int t = 0, up = INT_MIN;
+    if (i < n) {
+        const int rc = resp[(long long)ADLBQ_RESP_INTS * i], seq = resp[(long long)ADLBQ_RESP_INTS * i + 5];
+        const int rank = reqs[(long long)ADLBQ_RESERVE_INTS * i];
+        long long slot = (rc == 1 && seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
+        if (slot >= 0) {
+            const uint32_t m = meta[slot];
+            const int pn = pin[slot];
+            const int4 r0 = rrec[2 * slot], r1 = rrec[2 * slot + 1];
+            if ((m & M_LIVE) && pn == rank && r0.z == seq) {
+                pin[slot] = -1;
                 meta[slot] = m & ~M_PINNED;
                 t = m & M_TYPE;
                 up = r1.w;
@@ -807,6 +845,17 @@ int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, in
     return ADLBQ_OK;
 }
 
+int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12) {
+    if (!ok_handle(h) || n < 0 || (n && (!d_reqs18 || !d_resp12)))
+        return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_device");
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    k_unreserve_resp<<<(n + 255) / 256, 256, 0, h->stream>>>(d_reqs18, d_resp12, n, h->d_seq2slot, h->next_wqseqno,
+                                                             h->d_meta, h->d_pin, h->d_rrec, h->d_anchor);
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
 int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples) {
     if (!ok_handle(h) || n < 0) return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_batch_device");
     if (!n) return ADLBQ_OK;
@@ -1037,6 +1086,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_passes = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "rank_in_select") {
+        h->rank_in_select = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "chain_stamps") {
         h->chain_stamps = value ? 1 : 0;
         return ADLBQ_OK;
@@ -1111,6 +1164,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     }
     if (n == "parked") return h->ctr.n_parked_last;
     if (n == "spec_lists") return h->ctr.spec_page0;
+    if (n == "rank_fast") return h->ctr.rank_fast;
     if (n == "candidates") {
         int v = 0;
         if (h->T > 0 && hipMemcpy(&v, h->d_candoff + h->T, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;

@@ -112,6 +112,11 @@ class Server:
         _lib.check(self.lib.adlbq_unreserve_batch_device(self.h, n, d_triples),
                    "adlbq_unreserve_batch_device")
 
+    def unreserve_resp_device(self, n: int, d_reqs18: int, d_resp12: int) -> None:
+        """SS_UNRESERVE every unit the reserve batch (d_reqs18, d_resp12) matched."""
+        _lib.check(self.lib.adlbq_unreserve_resp_device(self.h, n, d_reqs18, d_resp12),
+                   "adlbq_unreserve_resp_device")
+
     # -- qmstat / donor selection ----------------------------------------------
     def qmstat_row(self):
         q = ctypes.c_int()

@@ -81,6 +81,7 @@ def parse():
     ap.add_argument("--c4-chain-modes", type=int, default=None, help="config 4: adlbq 'chain_modes'")
     ap.add_argument("--chain-passes", type=int, default=None, help="metric leg: adlbq 'chain_passes'")
     ap.add_argument("--chain-modes", type=int, default=None, help="metric leg: adlbq 'chain_modes'")
+    ap.add_argument("--rank-in-select", type=int, default=None, help="metric leg: adlbq 'rank_in_select'")
     ap.add_argument("--chain-warm", type=int, default=None, help="metric leg: adlbq 'chain_warm' (0, 256, 512)")
     ap.add_argument("--c4-chain-stats", action="store_true",
                     help="config 4: after the timed region, replay each batch alone and report its chain counters")
@@ -349,16 +350,11 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     with torch.cuda.stream(stream):
         d_reqs = torch.from_numpy(reqs).to(dev)
         d_resp = torch.empty((nb, R, 12), dtype=torch.int32, device=dev)
-        d_trip = torch.empty((nb, R, 3), dtype=torch.int32, device=dev)
-        d_trip[:, :, 0] = d_reqs[:, :, 0]
-        d_trip[:, :, 2] = -1
     torch.cuda.synchronize()
 
     def step(b):
         srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
-        with torch.cuda.stream(stream):
-            d_trip[b, :, 1].copy_(d_resp[b][:, 5])
-        srv.unreserve_batch_device(R, d_trip[b].data_ptr())
+        srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
 
     for b in range(W4):
         step(b)
@@ -458,6 +454,8 @@ def main():
         srv.set_param("chain_modes", args.chain_modes)
     if args.chain_rounds is not None:
         srv.set_param("chain_rounds", args.chain_rounds)
+    if args.rank_in_select is not None:
+        srv.set_param("rank_in_select", args.rank_in_select)
     # one explicit stream for the library and the torch glue ops (the handle's
     # own stream is non-blocking and would not order against torch's null stream)
     stream = torch.cuda.Stream(dev)
@@ -478,17 +476,12 @@ def main():
         reqs[b, :, 2:] = synth.type_vectors(rng, w.user_types, R) if b else w.r_types
     d_reqs = torch.from_numpy(reqs).to(dev)
     d_resp = torch.empty((nb, R, 12), dtype=torch.int32, device=dev)
-    d_trip = torch.empty((R, 3), dtype=torch.int32, device=dev)
-    d_trip[:, 0] = torch.arange(R, dtype=torch.int32, device=dev)
-    d_trip[:, 2] = -1
     torch.cuda.synchronize()
 
     def step(b):
         srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
-        # SS_UNRESERVE every matched unit: resp[5] is the wqseqno of a match and 0
-        # otherwise, and rows with wqseqno <= 0 are ignored by the kernel
-        d_trip[:, 1].copy_(d_resp[b][:, 5])
-        srv.unreserve_batch_device(R, d_trip.data_ptr())
+        # SS_UNRESERVE every matched unit, straight from the batch's responses
+        srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
 
     for b in range(args.warmup):
         step(b)
@@ -592,6 +585,7 @@ def main():
         "chain_last_batch": {k: srv.stat("chain_" + k) for k in ("rounds", "passes", "recomputed", "fallback",
                                                                   "timeouts")},
         "candidates_last_batch": srv.stat("candidates"),
+        "rank_in_select_last_batch": srv.stat("rank_fast"),
     }
     if phases:
         res["chain_phases_ns"] = phases

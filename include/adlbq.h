@@ -89,6 +89,11 @@ int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, in
 /* n SS_UNRESERVEs with device-resident (rank, wqseqno, new_pin) triples. */
 int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples);
 
+/* SS_UNRESERVE (src/adlb.c:2051-2070) of every unit a reserve batch handed
+ * out, taken straight from that batch's device-resident reqs18 / resp12 (rows
+ * with rc 1): pin_rank = -1, pinned = 0.  Enqueued on the handle's stream. */
+int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12);
+
 /* update_local_state (src/adlb.c:3581-3593): qlen = wq_get_num_unpinned_untargeted
  * (xq.c:298-311), type_hi_prio[t] = wq_get_avail_hi_prio_of_type(user_types[t])
  * (xq.c:313-329); also stored as this server's qmstat row. */

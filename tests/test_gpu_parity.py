@@ -29,7 +29,7 @@ def run_abi(ut, cfg, trace, max_units=1 << 16, params=None, stats=None):
         assert s.stat("sort_timeouts") == 0, "k_rank timed out waiting for an in-launch sort"
         if stats is not None:
             stats.update({k: s.stat(k) for k in ("chain_passes", "chain_recomputed", "chain_fallback",
-                                                 "chain_timeouts", "spec_lists")})
+                                                 "chain_timeouts", "spec_lists", "rank_fast")})
         return out
 
 
@@ -232,3 +232,35 @@ def test_repeated_batches_vs_oracle(gpu_available, name):
     assert_same(got, np.concatenate(exp))
     if name in ("c2", "c2_mixed_wide_pages"):  # exact-bin cuts: the last batch's guess held
         assert st["spec_lists"] == 1, st
+
+
+def test_unreserve_resp_restores_queue(gpu_available):
+    """adlbq_unreserve_resp_device (SS_UNRESERVE of every unit a batch matched,
+    read from the batch's own responses) leaves the queue as it was: the same
+    batch then gets the same answers, which equal the oracle's."""
+    import torch
+    w = synth.config2(n_units=100_000, n_reserves=8192, seed=231)
+    reqs = np.concatenate([w.r_rank[:, None], w.r_hang[:, None].astype(np.int32), w.r_types],
+                          axis=1).astype(np.int32)
+    exp = run_oracle(w.user_types, (w.num_app_ranks, 1, 0), np.concatenate(
+        [synth.put_events(w), synth.reserve_events(w.r_rank, w.r_types, w.r_hang)]))
+    exp = synth.split_outputs(exp)[-len(reqs):]
+    with Server(w.user_types, w.num_app_ranks, max_units=w.n_units) as s:
+        units = np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(w.n_units, -1),
+                          np.zeros(w.n_units), np.full(w.n_units, -1), np.full(w.n_units, -1)],
+                         axis=1).astype(np.int32)
+        s.put_batch(units)
+        d_req = torch.from_numpy(reqs).cuda()
+        d_resp = torch.empty((len(reqs), 12), dtype=torch.int32, device="cuda")
+        outs = []
+        torch.cuda.synchronize()
+        for _ in range(3):
+            s.reserve_batch_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
+            s.sync()
+            outs.append(d_resp.cpu().numpy().copy())
+            s.unreserve_resp_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
+            s.sync()
+        assert (outs[0][:, 0] == 1).all()
+        for o in outs[1:]:
+            assert np.array_equal(o, outs[0])
+        assert np.array_equal(outs[0][:, :10], np.asarray(exp)[:, :10])
