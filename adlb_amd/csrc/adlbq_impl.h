@@ -107,6 +107,11 @@ struct adlbq_server {
     int *d_rank_pstart = nullptr; int cap_rank_pstart = 0;
     int *d_rank_fill = nullptr;   int cap_rank_fill = 0;
     int *d_bucket_ranks = nullptr; int cap_bucket_ranks = 0;
+    int *d_rank2b = nullptr; int cap_rank2b = 0;            // [A] app rank -> bucket index or -1
+    // per-bucket Reserve lists of a batch (prep_block appends, k_targeted_idx reads and resets)
+    int *d_tcnt = nullptr; long long cap_tcnt = 0;
+    int *d_tlist = nullptr; long long cap_tlist = 0;
+    int tcap = 0;
     int *d_all_pages = nullptr;   int cap_all_pages = 0;    // every page, with fills
     int *d_all_fill = nullptr;    int cap_all_fill = 0;
 

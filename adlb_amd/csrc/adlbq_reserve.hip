@@ -65,6 +65,12 @@ struct PrepArgs {
     int *seg_cnt;
     DevCounters *ctr;
     int *tmatch;
+    // per target-rank bucket lists of the batch's Reserves (k_targeted_idx), or tlist == nullptr
+    const int *rank2b;  // [A] app rank -> bucket index or -1
+    int A;
+    int *tcnt;          // [buckets] appended entries (k_targeted_idx resets its own)
+    int *tlist;         // [buckets][tcap] request indices, any order
+    int tcap;
 };
 
 template <int TB>  // TB >= T; TB <= 8: the user types are compared in registers
@@ -124,6 +130,14 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
         }
         if (wild) m = T >= 64 ? ~0ull : ((1ull << T) - 1);
         mask[j] = m;
+        if (a.tlist != nullptr && m) {  // the Reserve's rank owns targeted units: list it under that bucket
+            const int r = rows[threadIdx.x * PREP_ROW];
+            const int b = (r >= 0 && r < a.A) ? a.rank2b[r] : -1;
+            if (b >= 0) {
+                const int k = atomicAdd(&a.tcnt[b], 1);
+                if (k < a.tcap) a.tlist[(long long)b * a.tcap + k] = j;
+            }
+        }
     }
     const unsigned long long nz = __ballot(m != 0ull);
     if ((threadIdx.x & 63) == 0 && j < R) seg_cnt[j >> 6] = __popcll(nz);  // per 64 requests
@@ -850,79 +864,281 @@ __global__ void k_tindex_ranges(const unsigned long long *__restrict__ keys, lon
         tend[g] = (int)(i + 1);
 }
 
+// One block per target-rank bucket: that rank's Reserves in arrival order
+// against its targeted units (wq_find_pre_targeted_hi_prio, xq.c:219-247).  The
+// Reserves come from the list prep_block built (sorted here into arrival
+// order), or -- when more Reserves named the rank than the list holds -- from a
+// scan of the batch, TGT_REQ at a time.  Per batch, every type's head of the
+// bucket's sorted index is prefetched into an LDS cache: about twice the
+// Reserves that can take the type, all loads in flight together, unavailable
+// units (pinned, deleted, prio <= LOWEST) dropped.  Wave 0 then serves the
+// Reserves in order from LDS: lane t offers type t's head, the wave takes the
+// minimum of (prio desc, position asc), the winner advances.  A type whose
+// cache runs dry walks its range in global memory (a deep run of pinned
+// units).  The pins are k_finalize's.
+constexpr int TGT_REQ = 1024;    // Reserves per batch of the block
+constexpr int TGT_CACHE = 2048;  // cached index entries per block
+constexpr int TGT_PER = TGT_CACHE / 256;
+
+__device__ __forceinline__ long long tidx_slot(const int *__restrict__ rpages, int p0, int L) {
+    return ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
+}
+
 __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bucket_ranks,
                                                       const int *__restrict__ pstart, const int *__restrict__ rpages,
                                                       const unsigned long long *__restrict__ tkeys,
                                                       const int *__restrict__ tvals, const int *__restrict__ tstart,
-                                                      const int *__restrict__ tend, int T, uint32_t *meta,
+                                                      const int *__restrict__ tend, int T, const uint32_t *meta,
                                                       const unsigned long long *__restrict__ mask,
-                                                      const int *__restrict__ reqs, int R, int *tmatch, int *seg_cnt) {
-    __shared__ int list[1024];
-    __shared__ int nlist, wcnt[4];
+                                                      const int *__restrict__ reqs, int R, int *tmatch, int *seg_cnt,
+                                                      int *tcnt, const int *__restrict__ tlist, int tcap) {
+    __shared__ int sreq[TGT_REQ];                   // the batch's Reserves in arrival order
+    __shared__ unsigned long long smk[TGT_REQ];     // their type masks
+    __shared__ unsigned long long ckey[TGT_CACHE];  // cached heads: inverted prio << 32 | position in the bucket
+    __shared__ int cslot[TGT_CACHE], cgi[TGT_CACHE], cex[TGT_CACHE + 1];
+    __shared__ int dem[64], coff[65], gbase[64], gend[64], ccnt[64];
+    __shared__ int nlist, wcnt[4], wsum[4], s_over;
     const int b = blockIdx.x, r = bucket_ranks[b], p0 = pstart[b];
-    if (pstart[b + 1] - p0 <= 0) return;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // lane t of wave 0: type t's range and head
-    const bool tl = w == 0 && lane < T;
-    int hd = tl ? tstart[b * 64 + lane] : 0;
-    const int end = tl ? tend[b * 64 + lane] : 0;
-    if (threadIdx.x == 0) nlist = 0;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if (pstart[b + 1] - p0 <= 0) {
+        if (tid == 0) tcnt[b] = 0;
+        return;
+    }
+    if (tid < 64) {
+        gbase[tid] = tid < T ? tstart[b * 64 + tid] : 0;
+        gend[tid] = tid < T ? tend[b * 64 + tid] : 0;
+    }
+    if (tid == 0) {
+        const int n = tcnt[b];
+        s_over = n > tcap;
+        nlist = s_over ? 0 : n;
+        tcnt[b] = 0;  // for the next batch (prep_block appends again)
+    }
     __syncthreads();
-    for (int j0 = 0; j0 < R; j0 += 256) {
-        const int j = j0 + threadIdx.x;
-        const bool is = j < R && reqs[(long long)ADLBQ_RESERVE_INTS * j] == r;
-        const unsigned long long bal = __ballot(is);
-        if (lane == 0) wcnt[w] = __popcll(bal);
+    const bool over = s_over;
+    int j0 = 0;  // scan position (overflow)
+    while (true) {
+        // ---- the next batch of this rank's Reserves, in arrival order
+        int n;
+        if (!over) {
+            n = nlist;
+            for (int k = tid; k < n; k += blockDim.x) sreq[k] = tlist[(long long)b * tcap + k];
+            __syncthreads();
+            int v[TGT_REQ / 256], pos[TGT_REQ / 256];  // rank of each among the distinct request indices
+#pragma unroll
+            for (int q = 0; q < TGT_REQ / 256; q++) {
+                const int k = tid + q * 256;
+                v[q] = k < n ? sreq[k] : INT_MAX;
+                pos[q] = 0;
+            }
+            for (int k = 0; k < n; k++) {
+                const int x = sreq[k];
+#pragma unroll
+                for (int q = 0; q < TGT_REQ / 256; q++) pos[q] += x < v[q];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < TGT_REQ / 256; q++)
+                if (tid + q * 256 < n) sreq[pos[q]] = v[q];
+        } else {
+            if (tid == 0) nlist = 0;
+            __syncthreads();
+            for (; j0 < R; j0 += 256) {
+                const int j = j0 + tid;
+                const bool is = j < R && reqs[(long long)ADLBQ_RESERVE_INTS * j] == r;
+                const unsigned long long bal = __ballot(is);
+                if (lane == 0) wcnt[w] = __popcll(bal);
+                __syncthreads();
+                int woff = nlist;
+                for (int q = 0; q < w; q++) woff += wcnt[q];
+                if (is) sreq[woff + __popcll(bal & lanemask_lt())] = j;
+                __syncthreads();
+                if (tid == 0) nlist += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+                __syncthreads();
+                if (nlist > TGT_REQ - 256) {
+                    j0 += 256;
+                    break;
+                }
+            }
+            n = nlist;
+        }
         __syncthreads();
-        int woff = nlist;
-        for (int q = 0; q < w; q++) woff += wcnt[q];
-        if (is) list[woff + __popcll(bal & lanemask_lt())] = j;
+        if (n == 0) break;
+        for (int k = tid; k < n; k += blockDim.x) smk[k] = mask[sreq[k]];
+        if (tid < 64) dem[tid] = 0;
         __syncthreads();
-        if (threadIdx.x == 0) nlist += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        // ---- per type: the Reserves that can take it (each takes at most one unit)
+        for (int k = tid; k < n; k += blockDim.x)
+            for (unsigned long long m = smk[k]; m; m &= m - 1) atomicAdd(&dem[__ffsll((long long)m) - 1], 1);
         __syncthreads();
-        if (nlist > 768 || j0 + 256 >= R) {
-            if (w == 0) {
-                for (int e = 0; e < nlist; e++) {
-                    const int jj = list[e];
-                    const unsigned long long m = mask[jj];
+        // ---- cache regions: twice the demand + 8 per type (less when the cache is short)
+        if (tid == 0) {
+            int tot = 0;
+            for (int t = 0; t < T; t++) tot += min(2 * dem[t] + 8, gend[t] - gbase[t]);
+            const bool big = tot > TGT_CACHE;
+            int acc = 0;
+            for (int t = 0; t < T; t++) {
+                int want = min(big ? dem[t] : 2 * dem[t] + 8, gend[t] - gbase[t]);
+                want = max(0, min(want, TGT_CACHE - acc));
+                coff[t] = acc;
+                acc += want;
+            }
+            coff[T] = acc;
+        }
+        __syncthreads();
+        const int F = coff[T];
+        // ---- fetch: thread tid takes flat entries [tid * TGT_PER, +TGT_PER), three dependent rounds of loads
+        unsigned long long kv[TGT_PER];
+        long long sl[TGT_PER];
+        int gi[TGT_PER];
+        bool av[TGT_PER];
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) {
+            const int f = tid * TGT_PER + q;
+            gi[q] = -1;
+            kv[q] = ~0ull;
+            if (f < F) {
+                int lo = 0, hi = T;  // type of flat entry f: coff[t] <= f < coff[t+1]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (coff[mid] <= f) lo = mid; else hi = mid;
+                }
+                gi[q] = gbase[lo] + (f - coff[lo]);
+                kv[q] = tkeys[gi[q]];
+            }
+        }
+        int L[TGT_PER];
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) L[q] = gi[q] >= 0 ? tvals[gi[q]] : 0;
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) sl[q] = gi[q] >= 0 ? tidx_slot(rpages, p0, L[q]) : 0;
+        int cnt = 0;
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) {
+            av[q] = false;
+            if (gi[q] >= 0) {
+                const uint32_t mt = meta[sl[q]];
+                const int pr = (int)(~(unsigned int)kv[q] ^ 0x80000000u);
+                av[q] = (mt & (M_LIVE | M_PINNED)) == M_LIVE && pr > LOWEST;
+            }
+            cnt += av[q];
+        }
+        // block exclusive scan of the availability flags over the flat order
+        int x = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int pre = x - cnt;
+        for (int q = 0; q < w; q++) pre += wsum[q];
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) {
+            const int f = tid * TGT_PER + q;
+            if (f < F) cex[f] = pre;
+            pre += av[q];
+        }
+        if (tid == 255) cex[F] = pre;
+        __syncthreads();
+        // compacted in order into each type's region
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) {
+            const int f = tid * TGT_PER + q;
+            if (f < F && av[q]) {
+                int lo = 0, hi = T;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (coff[mid] <= f) lo = mid; else hi = mid;
+                }
+                const int at = coff[lo] + (cex[f] - cex[coff[lo]]);
+                ckey[at] = ((kv[q] & 0xffffffffull) << 32) | (unsigned int)L[q];
+                cslot[at] = (int)sl[q];
+                cgi[at] = gi[q];
+            }
+        }
+        if (tid < T) ccnt[tid] = cex[coff[tid + 1]] - cex[coff[tid]];
+        __syncthreads();
+        // ---- serve the Reserves in order (wave 0): lane t holds type t's head
+        // (and the one after it) in registers; per Reserve a scalar loop over
+        // its types compares the heads (readlane), the winner's lane advances
+        if (w == 0) {
+            const bool tl = lane < T;
+            const int co = tl ? coff[lane] : 0, cn = tl ? ccnt[lane] : 0, ge = tl ? gend[lane] : 0;
+            int hd = 0;                                                     // cached heads consumed
+            int gn = tl ? gbase[lane] + (coff[lane + 1] - coff[lane]) : 0;  // next index past the fetch
+            int pg = -1;  // global index of a head found by the walk (cache dry), -1: from the cache
+            unsigned long long hk = ~0ull, nk = ~0ull;  // head key and the next cached one
+            int hs = -1, ns = -1;
+            auto walk = [&](unsigned long long &k, int &sl) {  // next available unit past the fetch (slow path)
+                k = ~0ull;
+                sl = -1;
+                for (; gn < ge; gn++) {
+                    const unsigned long long kk = tkeys[gn];
+                    const int pr = (int)(~(unsigned int)kk ^ 0x80000000u);
+                    if (pr <= LOWEST) {  // prio descending: nothing after it matches either
+                        gn = ge;
+                        break;
+                    }
+                    const int LL = tvals[gn];
+                    const long long ss = tidx_slot(rpages, p0, LL);
+                    if ((meta[ss] & (M_LIVE | M_PINNED)) == M_LIVE) {
+                        k = ((kk & 0xffffffffull) << 32) | (unsigned int)LL;
+                        sl = (int)ss;
+                        pg = gn++;
+                        break;
+                    }
+                }
+            };
+            if (tl) {
+                if (cn > 0) { hk = ckey[co]; hs = cslot[co]; }
+                if (cn > 1) { nk = ckey[co + 1]; ns = cslot[co + 1]; }
+            }
+            for (int k0 = 0; k0 < n; k0 += 64) {
+                const unsigned long long mv = k0 + lane < n ? smk[k0 + lane] : 0ull;
+                const int jv = k0 + lane < n ? sreq[k0 + lane] : 0;
+                const int kn = min(64, n - k0);
+                for (int kk = 0; kk < kn; kk++) {
+                    const unsigned long long m = readlane64(mv, kk);
+                    // a type whose cache ran dry walks before it competes (uniform loop over such types)
+                    const unsigned long long dry = __ballot(tl && hk == ~0ull && hd >= cn && gn < ge) & m;
+                    if (dry && ((dry >> lane) & 1ull)) walk(hk, hs);
                     unsigned long long best = ~0ull;
-                    int slot = -1;
-                    if (tl && ((m >> lane) & 1ull)) {
-                        for (; hd < end; hd++) {  // skip units no longer available
-                            const unsigned int low = (unsigned int)tkeys[hd];
-                            const int pr = (int)(~low ^ 0x80000000u);
-                            if (pr <= LOWEST) {  // prio descending: nothing after it matches either
-                                hd = end;
-                                break;
-                            }
-                            const int L = tvals[hd];
-                            const long long sl = ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
-                            const uint32_t mt = (uint32_t)ld_agent(reinterpret_cast<const int *>(meta + sl));
-                            if ((mt & (M_LIVE | M_PINNED)) == M_LIVE) {
-                                best = ((unsigned long long)low << 32) | (unsigned int)L;
-                                slot = (int)sl;
-                                break;
-                            }
+                    int bt = -1;
+                    for (unsigned long long mm = m; mm; mm &= mm - 1) {
+                        const int t = __ffsll((long long)mm) - 1;
+                        const unsigned long long kt = readlane64(hk, t);
+                        if (kt < best) {
+                            best = kt;
+                            bt = t;
                         }
                     }
-                    unsigned long long bb = best;
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) {
-                        const unsigned long long y = __shfl_xor(bb, o, 64);
-                        bb = y < bb ? y : bb;
+                    if (bt < 0 || best == ~0ull) continue;
+                    if (lane == 0) {
+                        const int j = __builtin_amdgcn_readlane(jv, kk);
+                        tmatch[j] = __builtin_amdgcn_readlane(hs, bt);
+                        atomicSub(&seg_cnt[j >> 6], 1);
                     }
-                    if (bb != ~0ull && best == bb) {  // the one lane holding the best head (positions are unique)
-                        tmatch[jj] = slot;
-                        atomicSub(&seg_cnt[jj >> 6], 1);
-                        st_agent(reinterpret_cast<int *>(meta + slot), (int)(meta[slot] | M_PINNED));
-                        hd++;
+                    if (lane == bt) {  // advance: the next cached head, else the walk later
+                        if (hd < cn) hd++;
+                        if (pg >= 0 && hd >= cn) pg = -1;
+                        if (hd < cn) {
+                            hk = nk;
+                            hs = ns;
+                            if (hd + 1 < cn) { nk = ckey[co + hd + 1]; ns = cslot[co + hd + 1]; }
+                        } else {
+                            hk = ~0ull;
+                            hs = -1;
+                        }
                     }
                 }
             }
-            __syncthreads();
-            if (threadIdx.x == 0) nlist = 0;
-            __syncthreads();
+            // the first unconsumed index of each type, for the next batch (overflow only)
+            if (tl) gbase[lane] = (hd >= cn && hk != ~0ull && pg >= 0) ? pg : hd < cn ? cgi[co + hd] : gn;
         }
+        __syncthreads();
+        if (!over || j0 >= R) break;
     }
 }
 
@@ -2502,18 +2718,43 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipStream_t s = h->stream;
     hipEvent_t ev;
 
-    const PrepArgs pa{d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch};
+    PrepArgs pa{d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch,
+                nullptr, 0, nullptr, nullptr, 0};
+    const int nb = (int)h->bucket_ranks.size();
+    const bool targeted = h->live_targeted > 0 && nb > 0;
+    if (targeted && nb < (1 << 20)) {  // per-bucket Reserve lists for k_targeted_idx
+        const int tcap = std::min(TGT_REQ, std::max(64, 2 * ((R + nb - 1) / nb) + 64));
+        if ((long long)nb > h->cap_tcnt || (long long)nb * tcap > h->cap_tlist) {
+            AQ_HIP(hipStreamSynchronize(s));
+            if ((long long)nb > h->cap_tcnt) {
+                if (h->d_tcnt) AQ_HIP(hipFree(h->d_tcnt));
+                h->cap_tcnt = std::max<long long>(nb, 2 * h->cap_tcnt);
+                AQ_HIP(hipMalloc((void **)&h->d_tcnt, sizeof(int) * h->cap_tcnt));
+                AQ_HIP(hipMemset(h->d_tcnt, 0, sizeof(int) * h->cap_tcnt));  // k_targeted_idx re-zeroes its own
+            }
+            if ((long long)nb * tcap > h->cap_tlist) {
+                if (h->d_tlist) AQ_HIP(hipFree(h->d_tlist));
+                h->cap_tlist = std::max<long long>((long long)nb * tcap, 2 * h->cap_tlist);
+                AQ_HIP(hipMalloc((void **)&h->d_tlist, sizeof(int) * h->cap_tlist));
+            }
+        }
+        h->tcap = tcap;
+        pa.rank2b = h->d_rank2b;
+        pa.A = h->A;
+        pa.tcnt = h->d_tcnt;
+        pa.tlist = h->d_tlist;
+        pa.tcap = tcap;
+    }
     if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) return rc;
     h->last_scan_units = h->live_units - h->live_targeted;
 
-    const int nb = (int)h->bucket_ranks.size();
-    if (h->live_targeted > 0 && nb > 0) {
+    if (targeted) {
         if (nb < (1 << 20) && (rc = ensure_tindex(h))) return rc;
         stage_begin(h, "targeted", &ev);
         if (nb < (1 << 20))
             k_targeted_idx<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_tkeys,
                                               h->d_tvals, h->d_tstart, h->d_tend, T, h->d_meta, h->d_mask, d_reqs, R,
-                                              h->d_tmatch, h->d_seg_cnt);
+                                              h->d_tmatch, h->d_seg_cnt, h->d_tcnt, h->d_tlist, h->tcap);
         else
             k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
                                           h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);

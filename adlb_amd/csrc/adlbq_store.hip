@@ -178,6 +178,10 @@ int sync_tables(adlbq_server *h) {
         if ((rc = upload(&h->d_rank_pstart, &h->cap_rank_pstart, pstart, h->stream))) return rc;
         if ((rc = upload(&h->d_rank_fill, &h->cap_rank_fill, fill, h->stream))) return rc;
         if ((rc = upload(&h->d_bucket_ranks, &h->cap_bucket_ranks, h->bucket_ranks, h->stream))) return rc;
+        std::vector<int> r2b(std::max(h->A, 1), -1);
+        for (size_t k = 0; k < h->bucket_ranks.size(); k++)
+            if (h->bucket_ranks[k] >= 0 && h->bucket_ranks[k] < h->A) r2b[h->bucket_ranks[k]] = (int)k;
+        if ((rc = upload(&h->d_rank2b, &h->cap_rank2b, r2b, h->stream))) return rc;
         // every page with its fill, for whole-store scans
         std::vector<int> ap, af;
         for (size_t i = 0; i < h->open.pages.size(); i++) {
@@ -660,7 +664,7 @@ int adlbq_destroy(adlbq_server *h) {
     hipSetDevice(h->device);
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
     void *ptrs[] = {h->d_pbase, h->d_pwide, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_rrec, h->d_open_pages,
-                    h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_all_pages,
+                    h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_rank2b, h->d_tcnt, h->d_tlist, h->d_all_pages,
                     h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_gcut, h->d_gcut_next, h->d_spec, h->d_specn, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
