@@ -25,6 +25,8 @@ SIGNATURES = {
     "adlbq_reserve_batch": (c_int, [P, c_int, P, P]),
     "adlbq_reserve_batch_device": (c_int, [P, c_int, P, P]),
     "adlbq_get_reserved": (c_int, [P, c_int, c_int, P]),
+    "adlbq_get_reserved_batch": (c_int, [P, c_int, P, P]),
+    "adlbq_get_reserved_batch_device": (c_int, [P, c_int, P, P]),
     "adlbq_unreserve": (c_int, [P, c_int, c_int, c_int, P]),
     "adlbq_unreserve_batch_device": (c_int, [P, c_int, P]),
     "adlbq_unreserve_resp_device": (c_int, [P, c_int, P, P]),
@@ -45,6 +47,9 @@ SIGNATURES = {
     "adlbq_rq_delete_batch": (c_int, [P, c_int, P, P]),
     "adlbq_push_select": (c_int, [P, c_double, P, P]),
     "adlbq_info": (c_int, [P, P, P, P]),
+    "adlbq_bytes": (c_int, [P, P, P]),
+    "adlbq_bytes_adjust": (c_int, [P, c_double]),
+    "adlbq_put_check": (c_int, [P, c_int, c_double, P, P]),
     "adlbq_info_type": (c_int, [P, c_int, P, P, P]),
     "adlbq_set_stream": (c_int, [P, P]),
     "adlbq_get_stream": (c_void_p, [P]),

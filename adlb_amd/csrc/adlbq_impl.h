@@ -38,6 +38,10 @@ constexpr uint32_t M_PINNED = 1u << 9;
 constexpr int M_OFF_SHIFT = 10;
 constexpr long long M_OFF_RANGE = 1ll << 22;
 constexpr int NREQ = ADLBQ_REQ_TYPES;
+// the reference's allocation sizes on LP64 (xq.h:8-79): xq_node_t 24 B + wq_struct_t 72 B per
+// unit (plus its payload), + rq_struct_t 80 B per parked Reserve, + tq_struct_t 16 B per tq entry
+constexpr long long BYTES_WQ = 24 + 72, BYTES_RQ = 24 + 80, BYTES_TQ = 24 + 16;
+
 
 // device-side scalar counters shared by kernels and read back lazily by the host
 struct DevCounters {
@@ -56,7 +60,16 @@ struct DevCounters {
     int spec_page0;        // the last scan's page 0, wave 0 read pass 1's list (diagnostic)
     int needsort_last;     // the last reserve batch had a type whose threshold fell in a multi-prio bin
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
+    // the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced (adlb.c:3419-3474) over the
+    // structures this handle replaces, plus what the caller adds (adlbq_bytes_adjust)
+    long long bytes, bytes_hwm;
+    long long got, got_targeted;  // units removed by device-side Get batches (folded into the host counts)
 };
+
+__device__ __forceinline__ void bytes_add(DevCounters *c, long long d) {  // one thread, in event order
+    c->bytes += d;
+    if (c->bytes > c->bytes_hwm) c->bytes_hwm = c->bytes;
+}
 
 struct Bucket {
     std::vector<int> pages;  // page ids in order
@@ -226,6 +239,10 @@ struct adlbq_server {
     int *d_apply_bad = nullptr;                          // [2] grants not available, deletions not parked
     hipEvent_t apply_ev = nullptr;
     int *d_result = nullptr;           // small result scratch (16 ints)
+    int *d_getclaim = nullptr; long long cap_getclaim = 0;  // [wqseqno] lowest claiming Get of a batch (INT_MAX: none)
+    int *d_getbuf = nullptr; long long cap_getbuf = 0;      // host-buffer Get batches: pairs, then results
+    long long got_seen = 0, got_t_seen = 0;                 // the device Get counters already folded in
+    int *d_info = nullptr;                                  // fused info reduction: per-block partials + counter
     int *h_result = nullptr;           // pinned host mirror
     long long last_scan_units = 0;
 

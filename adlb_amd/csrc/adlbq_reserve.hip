@@ -2168,6 +2168,7 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     if (tid == 0) {
         ctr->rq_n = n0 + np;
         ctr->rq_live += np;
+        bytes_add(ctr, BYTES_RQ * np);  // rq_node_create per parked Reserve (adlb.c:1244-1276)
         if (ctr->rq_live > ctr->rq_hwm) ctr->rq_hwm = ctr->rq_live;
         ctr->n_parked_last = np;
     }

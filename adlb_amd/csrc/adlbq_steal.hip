@@ -93,6 +93,7 @@ __global__ __launch_bounds__(1024) void k_rq_delete_fix(const int *rq_live, DevC
     const int head = ctr->rq_head, n = ctr->rq_n;
     if (threadIdx.x == 0) {
         ctr->rq_live -= *ndel;
+        bytes_add(ctr, -BYTES_RQ * *ndel);  // rq_delete per settled Reserve (adlb.c:1933)
         *ndel = 0;
         s_first = n;
     }

@@ -143,6 +143,11 @@ int refresh_counters(adlbq_server *h) {
     AQ_HIP(hipStreamSynchronize(h->stream));
     h->ctr_stale = false;
     h->rq_n_upper = h->ctr.rq_n;
+    // units the device-side Get batches removed since the last look
+    h->live_units -= h->ctr.got - h->got_seen;
+    h->live_targeted -= h->ctr.got_targeted - h->got_t_seen;
+    h->got_seen = h->ctr.got;
+    h->got_t_seen = h->ctr.got_targeted;
     return ADLBQ_OK;
 }
 
@@ -297,8 +302,9 @@ struct PutRec {  // staged by the host per Put
 
 __global__ void k_put_scatter(const PutRec *__restrict__ r, int n, int *prio, uint32_t *meta, int *pin,
                               int *seq, int4 *cold0, int4 *cold1, long long *seq2slot, long long *anchor,
-                              int4 *rrec) {
+                              int4 *rrec, DevCounters *ctr, long long add_bytes) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 && add_bytes) bytes_add(ctr, add_bytes);  // the batch's puts, when no rq match interleaves
     const bool ok = i < n;
     PutRec u = r[ok ? i : 0];
     raise_anchor(anchor, ok ? (u.meta & M_TYPE) : 0, ok ? u.prio : INT_MIN);  // upper bounds of live prios
@@ -323,6 +329,7 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
     int head = ctr->rq_head, nrq = ctr->rq_n, live = ctr->rq_live;
     for (int i = 0; i < n; i++) {
         PutRec u = r[i];
+        if (lane == 0) bytes_add(ctr, BYTES_WQ + u.len);  // pmalloc + wq_node_create (adlb.c:933, 963)
         int found = -1;
         if (live > 0) {
             for (int base = head; base < nrq; base += 64) {
@@ -353,6 +360,7 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
                 st_agent(rq_live + found, 0);
                 o[1] = rk;
                 o[2] = found + 1;  // rqseqno == slot + 1
+                bytes_add(ctr, -BYTES_RQ);  // rq_delete (adlb.c:1040)
                 pin[u.slot] = rk;
                 if (rk >= 0) meta[u.slot] = (uint32_t)u.meta | M_PINNED;
             }
@@ -371,7 +379,7 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
 }
 
 __global__ void k_get(int slot, int rank, int seq, const int *prio, uint32_t *meta, const int *pin,
-                      const int *seqa, const int4 *cold0, const int4 *cold1, int *res) {
+                      const int *seqa, const int4 *cold0, const int4 *cold1, int *res, DevCounters *ctr) {
     uint32_t m = meta[slot];
     res[0] = -1;
     res[1] = res[2] = res[3] = res[4] = 0;
@@ -385,6 +393,7 @@ __global__ void k_get(int slot, int rank, int seq, const int *prio, uint32_t *me
         res[4] = c0.x;
         res[5] = c1.w;
         meta[slot] = 0;
+        bytes_add(ctr, -(BYTES_WQ + c0.y));  // wq_delete frees the record, node and payload (xq.c:160-174)
     }
 }
 
@@ -422,6 +431,127 @@ __global__ void k_unreserve_batch(const int *__restrict__ trip, int n, const lon
         }
     }
     raise_anchor(anchor, t, up);  // available again: keep the anchor above it
+}
+
+// FA_GET_RESERVED for a batch of (rank, wqseqno) pairs (adlb.c:1347-1381:
+// wq_find_pinned_for_rank, then wq_delete).  Sequentially a unit can be got
+// once: of several valid Gets of one wqseqno in a batch the lowest index wins
+// (claimed with atomicMin in k_get_claim), the others find it gone.
+__global__ void k_get_claim(const int *__restrict__ pairs, int n, const long long *__restrict__ seq2slot,
+                            long long nseq, const uint32_t *__restrict__ meta, const int *__restrict__ pin,
+                            const int *__restrict__ seqa, int *claim) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int rank = pairs[2 * i], seq = pairs[2 * i + 1];
+    const long long slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
+    if (slot < 0) return;
+    if ((meta[slot] & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) atomicMin(&claim[seq], i);
+}
+
+__global__ void k_get_apply(const int *__restrict__ pairs, int n, long long *seq2slot, long long nseq,
+                            uint32_t *meta, const int *__restrict__ prio, const int4 *__restrict__ cold0,
+                            const int4 *__restrict__ cold1, int *claim, int *out5, DevCounters *ctr) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int ok = 0, tgt = 0;
+    long long freed = 0;
+    if (i < n) {
+        const int seq = pairs[2 * i + 1];
+        int o[5] = {-1, 0, 0, 0, 0};
+        if (seq > 0 && seq < nseq && claim[seq] == i) {
+            const long long slot = seq2slot[seq];
+            const int4 c0 = cold0[slot], c1 = cold1[slot];
+            o[0] = 1;
+            o[1] = c0.y;
+            o[2] = c1.z;
+            o[3] = prio[slot];
+            o[4] = c0.x;
+            meta[slot] = 0;
+            seq2slot[seq] = -1;
+            claim[seq] = INT_MAX;  // for the next batch
+            ok = 1;
+            tgt = c1.w >= 0;
+            freed = BYTES_WQ + c0.y;
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) out5[5 * i + k] = o[k];
+    }
+    // wave totals: removed units, targeted ones, freed bytes (deletions only lower the count: no mark)
+    const unsigned long long b = __ballot(ok), bt = __ballot(tgt);
+    for (int o = 32; o > 0; o >>= 1) freed += __shfl_xor(freed, o, 64);
+    if ((threadIdx.x & 63) == 0 && b) {
+        atomicAdd((unsigned long long *)&ctr->got, (unsigned long long)__popcll(b));
+        if (bt) atomicAdd((unsigned long long *)&ctr->got_targeted, (unsigned long long)__popcll(bt));
+        atomicAdd((unsigned long long *)&ctr->bytes, (unsigned long long)(-freed));
+    }
+}
+
+// FA_INFO_NUM_WORK_UNITS (adlb.c:2466-2496) in one pass over every page:
+// max prio of the type (strict >, from LOWEST), units at that max, units of
+// the type.  Blocks publish partials; the last to arrive combines them.
+__global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ pages, const int *__restrict__ fills,
+                                                    int npages, const int *__restrict__ prio,
+                                                    const uint32_t *__restrict__ meta, int tidx, int *part,
+                                                    int *res) {
+    __shared__ int smx[4], scm[4], scn[4];
+    __shared__ bool s_last;
+    int mx = LOWEST, cm = 0, cn = 0;
+    for (int p = blockIdx.x; p < npages; p += gridDim.x) {
+        const long long base = (long long)pages[p] << PAGE_SHIFT;
+        for (int o = threadIdx.x; o < fills[p]; o += blockDim.x) {
+            const uint32_t m = meta[base + o];
+            if ((m & M_LIVE) && (int)(m & M_TYPE) == tidx) {
+                const int pr = prio[base + o];
+                cn++;
+                if (pr > mx) {
+                    mx = pr;
+                    cm = 1;
+                } else if (pr == mx) {
+                    cm++;
+                }
+            }
+        }
+    }
+    // combine (max, count at max, count) over the block
+    for (int o = 32; o > 0; o >>= 1) {
+        const int m2 = __shfl_xor(mx, o, 64), c2 = __shfl_xor(cm, o, 64), n2 = __shfl_xor(cn, o, 64);
+        cm = m2 > mx ? c2 : m2 == mx ? cm + c2 : cm;
+        mx = max(mx, m2);
+        cn += n2;
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        smx[w] = mx;
+        scm[w] = cm;
+        scn[w] = cn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < 4; q++) {
+            cm = smx[q] > mx ? scm[q] : smx[q] == mx ? cm + scm[q] : cm;
+            mx = max(mx, smx[q]);
+            cn += scn[q];
+        }
+        __hip_atomic_store(part + 3 * blockIdx.x, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part + 3 * blockIdx.x + 1, cm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part + 3 * blockIdx.x + 2, cn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = atomicAdd(part + 3 * gridDim.x, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    mx = LOWEST;
+    cm = cn = 0;
+    for (int b = 0; b < (int)gridDim.x; b++) {
+        const int m2 = __hip_atomic_load(part + 3 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int c2 = __hip_atomic_load(part + 3 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cm = m2 > mx ? c2 : m2 == mx ? cm + c2 : cm;
+        mx = max(mx, m2);
+        cn += __hip_atomic_load(part + 3 * b + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    part[3 * gridDim.x] = 0;  // for the next call
+    res[0] = mx;
+    res[1] = cm;
+    res[2] = cn;
 }
 
 // SS_UNRESERVE of every unit a reserve batch handed out, read straight from the
@@ -481,42 +611,7 @@ __global__ void k_qmrow(const int *__restrict__ pages, int npages, int tail_fill
     if (threadIdx.x == 0) atomicAdd(&res[0], scnt);
 }
 
-// whole-store scan helpers (FA_INFO_NUM_WORK_UNITS, wq_find_unpinned)
-__global__ void k_info_max(const int *__restrict__ pages, const int *__restrict__ fills, int npages,
-                           const int *__restrict__ prio, const uint32_t *__restrict__ meta, int tidx,
-                           int *res /* [0]=max [1]=count */) {
-    int p = blockIdx.x;
-    if (p >= npages) return;
-    long long base = (long long)pages[p] << PAGE_SHIFT;
-    int mx = LOWEST, n = 0;
-    for (int o = threadIdx.x; o < fills[p]; o += blockDim.x) {
-        uint32_t m = meta[base + o];
-        if ((m & M_LIVE) && (int)(m & M_TYPE) == tidx) {
-            n++;
-            int pr = prio[base + o];
-            mx = pr > mx ? pr : mx;
-        }
-    }
-    if (n) {
-        atomicAdd(&res[1], n);
-        if (mx > LOWEST) atomicMax(&res[0], mx);
-    }
-}
-
-__global__ void k_info_cnt(const int *__restrict__ pages, const int *__restrict__ fills, int npages,
-                           const int *__restrict__ prio, const uint32_t *__restrict__ meta, int tidx,
-                           int *res /* [0]=max (in) [2]=count at max */) {
-    int p = blockIdx.x;
-    if (p >= npages) return;
-    long long base = (long long)pages[p] << PAGE_SHIFT;
-    int mx = res[0], n = 0;
-    for (int o = threadIdx.x; o < fills[p]; o += blockDim.x) {
-        uint32_t m = meta[base + o];
-        n += ((m & M_LIVE) && (int)(m & M_TYPE) == tidx && prio[base + o] == mx);
-    }
-    if (n) atomicAdd(&res[2], n);
-}
-
+// whole-store scan helper (wq_find_unpinned)
 __global__ void k_first_unpinned(const int *__restrict__ pages, const int *__restrict__ fills, int npages,
                                  const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int *res) {
     int p = blockIdx.x;
@@ -559,6 +654,7 @@ __global__ void k_rq_delete(int k, int *rq_live, DevCounters *ctr, int *res) {
     if (k >= 0 && k < ctr->rq_n && rq_live[k]) {
         rq_live[k] = 0;
         ctr->rq_live--;
+        bytes_add(ctr, -BYTES_RQ);
         res[0] = 1;
         int head = ctr->rq_head;
         while (head < ctr->rq_n && !rq_live[head]) head++;
@@ -567,6 +663,8 @@ __global__ void k_rq_delete(int k, int *rq_live, DevCounters *ctr, int *res) {
 }
 
 __global__ void k_set_int(int *p, int v) { *p = v; }
+
+__global__ void k_add_bytes(DevCounters *ctr, long long d) { bytes_add(ctr, d); }
 
 // ============================================================================ C ABI
 
@@ -673,7 +771,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
-                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb};
+                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -784,12 +882,15 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
     }
     PutRec *d_rec = reinterpret_cast<PutRec *>(h->d_putrec);
     AQ_HIP(hipMemcpyAsync(d_rec, rec.data(), sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
-    k_put_scatter<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, h->d_prio, h->d_meta, h->d_pin, h->d_seq,
-                                                          h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor,
-                                                          h->d_rrec);
     // a parked Reserve can only exist if the last known count, plus every
     // Reserve launched since, is positive
     bool may_match = h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0);
+    long long add_bytes = 0;  // bytes of the batch's units (k_put_match adds them one Put at a time)
+    if (!may_match)
+        for (int i = 0; i < n; i++) add_bytes += BYTES_WQ + rec[i].len;
+    k_put_scatter<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, h->d_prio, h->d_meta, h->d_pin, h->d_seq,
+                                                          h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor,
+                                                          h->d_rrec, h->d_ctr, add_bytes);
     if (may_match) {
         k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
                                              h->d_meta, h->d_pin, h->d_putout);
@@ -821,7 +922,7 @@ int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5) {
     out5[1] = out5[2] = out5[3] = out5[4] = 0;
     if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
     k_get<<<1, 1, 0, h->stream>>>((int)slot, rank, wqseqno, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0,
-                                  h->d_cold1, h->d_result);
+                                  h->d_cold1, h->d_result, h->d_ctr);
     AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 6, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
     memcpy(out5, h->h_result, sizeof(int) * 5);
@@ -832,6 +933,56 @@ int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5) {
         // keep the device map consistent for batch unreserves
         AQ_HIP(hipMemsetAsync(h->d_seq2slot + wqseqno, 0xff, sizeof(long long), h->stream));
     }
+    return ADLBQ_OK;
+}
+
+static int launch_get_batch(adlbq_server *h, int n, const int *d_pairs, int *d_out5) {
+    if ((long long)h->next_wqseqno > h->cap_getclaim) {
+        AQ_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_getclaim) AQ_HIP(hipFree(h->d_getclaim));
+        h->cap_getclaim = std::max<long long>(h->cap_seq, h->next_wqseqno);
+        AQ_HIP(hipMalloc((void **)&h->d_getclaim, sizeof(int) * h->cap_getclaim));
+        AQ_HIP(hipMemsetAsync(h->d_getclaim, 0x7f, sizeof(int) * h->cap_getclaim, h->stream));  // "none"
+    }
+    const int g = (n + 255) / 256;
+    k_get_claim<<<g, 256, 0, h->stream>>>(d_pairs, n, h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_pin, h->d_seq,
+                                         h->d_getclaim);
+    k_get_apply<<<g, 256, 0, h->stream>>>(d_pairs, n, h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_prio,
+                                         h->d_cold0, h->d_cold1, h->d_getclaim, d_out5, h->d_ctr);
+    AQ_HIP(hipGetLastError());
+    h->ctr_stale = true;
+    return ADLBQ_OK;
+}
+
+int adlbq_get_reserved_batch_device(adlbq_server *h, int n, const int *d_pairs2, int *d_out5) {
+    if (!ok_handle(h) || n < 0 || (n && (!d_pairs2 || !d_out5)))
+        return fail(ADLBQ_ERR_ARG, "adlbq_get_reserved_batch_device");
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    return launch_get_batch(h, n, d_pairs2, d_out5);
+}
+
+int adlbq_get_reserved_batch(adlbq_server *h, int n, const int *pairs2, int *out5) {
+    if (!ok_handle(h) || n < 0 || (n && (!pairs2 || !out5))) return fail(ADLBQ_ERR_ARG, "adlbq_get_reserved_batch");
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    if ((long long)n * 7 > h->cap_getbuf) {
+        AQ_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_getbuf) AQ_HIP(hipFree(h->d_getbuf));
+        h->cap_getbuf = std::max<long long>((long long)n * 7, 2 * h->cap_getbuf);
+        AQ_HIP(hipMalloc((void **)&h->d_getbuf, sizeof(int) * h->cap_getbuf));
+    }
+    AQ_HIP(hipMemcpyAsync(h->d_getbuf, pairs2, sizeof(int) * 2 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+    int rc;
+    if ((rc = launch_get_batch(h, n, h->d_getbuf, h->d_getbuf + 2 * (size_t)n))) return rc;
+    AQ_HIP(hipMemcpyAsync(out5, h->d_getbuf + 2 * (size_t)n, sizeof(int) * 5 * (size_t)n, hipMemcpyDeviceToHost,
+                          h->stream));
+    if ((rc = refresh_counters(h))) return rc;  // synchronises; folds the removed units into the host counts
+    for (int i = 0; i < n; i++)
+        if (out5[5 * i] == 1) {
+            const int seq = pairs2[2 * i + 1];
+            if (seq > 0 && seq < (long long)h->seq2slot.size()) h->seq2slot[seq] = -1;
+        }
     return ADLBQ_OK;
 }
 
@@ -888,7 +1039,10 @@ int adlbq_qmstat_row(adlbq_server *h, int *qlen, int *type_hi_prio) {
     AQ_HIP(hipStreamSynchronize(h->stream));
     *qlen = h->h_result[0];
     for (int t = 0; t < h->T; t++) type_hi_prio[t] = h->h_result[1 + t];
-    // this server's own qmstat row (adlb.c:3586-3591)
+    // this server's own qmstat row (adlb.c:3586-3591), nbytes_used included
+    h->ctr_stale = true;
+    if ((rc = refresh_counters(h))) return rc;
+    h->qm_bytes[h->my_idx] = (double)h->ctr.bytes;
     h->qm_qlen[h->my_idx] = *qlen;
     for (int t = 0; t < h->T; t++) h->qm_hi[(size_t)h->my_idx * h->T + t] = type_hi_prio[t];
     h->qm_dirty = true;
@@ -949,6 +1103,55 @@ int adlbq_tq_add(adlbq_server *h, int app_rank, int work_type, int server_rank) 
         }
     h->tq.insert(h->tq.end(), {app_rank, work_type, server_rank, 1});
     h->tq_dirty = true;
+    hipSetDevice(h->device);
+    k_add_bytes<<<1, 1, 0, h->stream>>>(h->d_ctr, BYTES_TQ);  // tq_node_create (adlb.c:1176)
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
+int adlbq_bytes(adlbq_server *h, double *curr, double *hwm) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_bytes");
+    hipSetDevice(h->device);
+    int rc;
+    h->ctr_stale = true;
+    if ((rc = refresh_counters(h))) return rc;
+    if (curr) *curr = (double)h->ctr.bytes;
+    if (hwm) *hwm = (double)h->ctr.bytes_hwm;
+    return ADLBQ_OK;
+}
+
+int adlbq_bytes_adjust(adlbq_server *h, double delta) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_bytes_adjust");
+    if (delta == 0) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    k_add_bytes<<<1, 1, 0, h->stream>>>(h->d_ctr, (long long)delta);
+    AQ_HIP(hipGetLastError());
+    h->ctr_stale = true;
+    return ADLBQ_OK;
+}
+
+// argmin nbytes_used over the other servers below THRESHOLD_TO_START_PUSH
+// (strict <, lowest index wins): adlb.c:912-928, 516-528
+static int reject_hint(const adlbq_server *h, double threshold) {
+    double smallest = 999999999999.9;
+    int cand = -1;
+    for (int i = 0; i < h->S; i++) {
+        const int srv = h->master + i;
+        if (srv != h->my_world && h->qm_bytes[i] < threshold && h->qm_bytes[i] < smallest) {
+            smallest = h->qm_bytes[i];
+            cand = srv;
+        }
+    }
+    return cand;
+}
+
+int adlbq_put_check(adlbq_server *h, int work_len, double max_malloc, int *rejected, int *hint_server_rank) {
+    if (!ok_handle(h) || !rejected || !hint_server_rank) return fail(ADLBQ_ERR_ARG, "adlbq_put_check");
+    double curr = 0;
+    int rc;
+    if ((rc = adlbq_bytes(h, &curr, nullptr))) return rc;
+    *rejected = (curr + work_len) > max_malloc ? 1 : 0;
+    *hint_server_rank = *rejected ? reject_hint(h, 0.95 * max_malloc) : -1;
     return ADLBQ_OK;
 }
 
@@ -980,17 +1183,7 @@ int adlbq_push_select(adlbq_server *h, double threshold, int *cand_server_rank, 
     AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
     if (h->h_result[0] == INT_MAX) return ADLBQ_OK;
-    // argmin nbytes_used over other servers below the threshold (adlb.c:516-528)
-    double smallest = 999999999999.9;
-    int cand = -1;
-    for (int i = 0; i < h->S; i++) {
-        int srv = h->master + i;
-        if (srv != h->my_world && h->qm_bytes[i] < threshold && h->qm_bytes[i] < smallest) {
-            smallest = h->qm_bytes[i];
-            cand = srv;
-        }
-    }
-    *cand_server_rank = cand;
+    *cand_server_rank = reject_hint(h, threshold);  // argmin nbytes_used (adlb.c:516-528)
     *wqseqno = h->h_result[0];
     return ADLBQ_OK;
 }
@@ -1015,19 +1208,23 @@ int adlbq_info_type(adlbq_server *h, int work_type, int *max_prio, int *num_max_
     if ((rc = sync_tables(h))) return rc;
     int npages = (int)(h->open.pages.size());
     for (auto &b : h->rankb) npages += (int)b.pages.size();
-    int init[3] = {LOWEST, 0, 0};
-    AQ_HIP(hipMemcpyAsync(h->d_result, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
+    constexpr int IB = 1024;  // blocks of the fused reduction
+    if (!h->d_info) {
+        AQ_HIP(hipMalloc((void **)&h->d_info, sizeof(int) * (3 * IB + 1)));
+        AQ_HIP(hipMemsetAsync(h->d_info, 0, sizeof(int) * (3 * IB + 1), h->stream));
+    }
     if (npages) {
-        k_info_max<<<npages, 256, 0, h->stream>>>(h->d_all_pages, h->d_all_fill, npages, h->d_prio, h->d_meta,
-                                                  it->second, h->d_result);
-        k_info_cnt<<<npages, 256, 0, h->stream>>>(h->d_all_pages, h->d_all_fill, npages, h->d_prio, h->d_meta,
-                                                  it->second, h->d_result);
+        k_info_fused<<<std::min(npages, IB), 256, 0, h->stream>>>(h->d_all_pages, h->d_all_fill, npages, h->d_prio,
+                                                                  h->d_meta, it->second, h->d_info, h->d_result);
+    } else {
+        int init[3] = {LOWEST, 0, 0};
+        AQ_HIP(hipMemcpyAsync(h->d_result, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
     }
     AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
     *max_prio = h->h_result[0];
-    *num_max_prio = h->h_result[2];
-    *num_type = h->h_result[1];
+    *num_max_prio = h->h_result[1];
+    *num_type = h->h_result[2];
     return ADLBQ_OK;
 }
 

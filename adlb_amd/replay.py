@@ -1,7 +1,8 @@
 """Replay an event trace (format of oracle/replay.h) through the C ABI.
 
-Consecutive Puts become one ``adlbq_put_batch`` and consecutive Reserves one
-``adlbq_reserve_batch`` -- the batch entry points guarantee the same results as
+Consecutive Puts become one ``adlbq_put_batch``, consecutive Reserves one
+``adlbq_reserve_batch`` and consecutive Gets one ``adlbq_get_reserved_batch``
+-- the batch entry points guarantee the same results as
 processing the events one at a time, so the output stream must equal the
 oracle's byte for byte.
 """
@@ -10,14 +11,14 @@ from __future__ import annotations
 import numpy as np
 
 from .server import Server
-from .synth import (OP_CHECKREM, OP_GET, OP_INFO, OP_INFOTYPE, OP_PUSHSEL, OP_PUT, OP_QMROW, OP_RESERVE,
-                    OP_RFRDONE, OP_RQDEL, OP_SETROW, OP_TQADD, OP_UNRESERVE)
+from .synth import (OP_BYTES, OP_CHECKREM, OP_GET, OP_HWM, OP_INFO, OP_INFOTYPE, OP_PUSHSEL, OP_PUT,
+                    OP_PUTCHECK, OP_QMROW, OP_RESERVE, OP_RFRDONE, OP_RQDEL, OP_SETROW, OP_TQADD, OP_UNRESERVE)
 
 
 def nargs(op: int, T: int) -> int:
     return {OP_PUT: 9, OP_RESERVE: 18, OP_GET: 2, OP_UNRESERVE: 3, OP_QMROW: 0, OP_SETROW: 3 + T,
             OP_CHECKREM: 0, OP_RFRDONE: 2, OP_TQADD: 3, OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1,
-            OP_INFOTYPE: 1}[op]
+            OP_INFOTYPE: 1, OP_BYTES: 0, OP_PUTCHECK: 2, OP_HWM: 0}[op]
 
 
 def _runs(tr: np.ndarray, T: int):
@@ -27,7 +28,7 @@ def _runs(tr: np.ndarray, T: int):
     while i < n:
         op = int(tr[i])
         w = 1 + nargs(op, T)
-        if op in (OP_PUT, OP_RESERVE):
+        if op in (OP_PUT, OP_RESERVE, OP_GET):
             j = i
             # stride through the run while the opcode repeats
             while j < n and int(tr[j]) == op:
@@ -62,11 +63,15 @@ def replay(srv: Server, trace) -> np.ndarray:
             blk[:, 0] = 12
             blk[:, 1:] = r
             out.append(blk.ravel())
+        elif op == OP_GET:
+            r = srv.get_reserved_batch(a)
+            blk = np.empty((r.shape[0], 6), np.int32)
+            blk[:, 0] = 5
+            blk[:, 1:] = r
+            out.append(blk.ravel())
         else:
             x = [int(v) for v in a[0]]
-            if op == OP_GET:
-                emit(srv.get_reserved(x[0], x[1]))
-            elif op == OP_UNRESERVE:
+            if op == OP_UNRESERVE:
                 emit([srv.unreserve(x[0], x[1], x[2])])
             elif op == OP_QMROW:
                 q, hi = srv.qmstat_row()
@@ -92,6 +97,12 @@ def replay(srv: Server, trace) -> np.ndarray:
                 emit([srv.rq_delete(x[0])])
             elif op == OP_INFOTYPE:
                 emit(list(srv.info_type(x[0])))
+            elif op == OP_BYTES:
+                emit([int(srv.bytes()[0])])
+            elif op == OP_HWM:
+                emit([int(srv.bytes()[1])])
+            elif op == OP_PUTCHECK:
+                emit(list(srv.put_check(x[0], x[1])))
             else:
                 raise ValueError(f"unknown opcode {op}")
     return np.concatenate(out) if out else np.zeros(0, np.int32)

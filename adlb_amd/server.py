@@ -102,6 +102,18 @@ class Server:
         _lib.check(self.lib.adlbq_get_reserved(self.h, rank, wqseqno, _ptr(out)), "adlbq_get_reserved")
         return out
 
+    def get_reserved_batch(self, pairs) -> np.ndarray:
+        """FA_GET_RESERVED for (n, 2) {rank, wqseqno} pairs in arrival order -> (n, 5)."""
+        p = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1, 2))
+        out = np.empty((p.shape[0], 5), dtype=np.int32)
+        _lib.check(self.lib.adlbq_get_reserved_batch(self.h, p.shape[0], _ptr(p), _ptr(out)),
+                   "adlbq_get_reserved_batch")
+        return out
+
+    def get_reserved_batch_device(self, n: int, d_pairs2: int, d_out5: int) -> None:
+        _lib.check(self.lib.adlbq_get_reserved_batch_device(self.h, n, d_pairs2, d_out5),
+                   "adlbq_get_reserved_batch_device")
+
     def unreserve(self, rank, wqseqno, new_pin_rank=-1) -> int:
         f = ctypes.c_int()
         _lib.check(self.lib.adlbq_unreserve(self.h, rank, wqseqno, new_pin_rank, ctypes.byref(f)),
@@ -230,6 +242,22 @@ class Server:
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.adlbq_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "adlbq_info")
         return a.value, b.value, c.value
+
+    def bytes(self):
+        """(curr, hwm): the handle's share of curr_bytes_dmalloced / hwm_bytes_dmalloced."""
+        c, h = ctypes.c_double(), ctypes.c_double()
+        _lib.check(self.lib.adlbq_bytes(self.h, ctypes.byref(c), ctypes.byref(h)), "adlbq_bytes")
+        return c.value, h.value
+
+    def bytes_adjust(self, delta: float) -> None:
+        _lib.check(self.lib.adlbq_bytes_adjust(self.h, float(delta)), "adlbq_bytes_adjust")
+
+    def put_check(self, work_len: int, max_malloc: float):
+        """FA_PUT_HDR's memory check: (rejected, hint_server_rank)."""
+        r, hnt = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_put_check(self.h, int(work_len), float(max_malloc), ctypes.byref(r),
+                                            ctypes.byref(hnt)), "adlbq_put_check")
+        return r.value, hnt.value
 
     def info_type(self, work_type):
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

@@ -83,6 +83,15 @@ int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int 
  * work_type, work_prio, answer_rank}. */
 int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5);
 
+/* n FA_GET_RESERVEDs in arrival order (one kernel pair, one synchronisation):
+ * pairs2[i] = {rank, wqseqno}; out5[i] as adlbq_get_reserved.  A unit can be
+ * got once: of several valid Gets of one wqseqno the first wins, as in the
+ * sequential server loop. */
+int adlbq_get_reserved_batch(adlbq_server *h, int n, const int *pairs2, int *out5);
+/* The same with device-resident pairs2 / out5, enqueued without a host
+ * synchronisation (the host's unit counts catch up at the next counter read). */
+int adlbq_get_reserved_batch_device(adlbq_server *h, int n, const int *d_pairs2, int *d_out5);
+
 /* SS_UNRESERVE (src/adlb.c:2057-2063): pin_rank = new_pin_rank, pinned = 0. */
 int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, int *found);
 
@@ -182,10 +191,27 @@ int adlbq_steal_check(adlbq_server *h, int *bad_grants, int *bad_deletes);
  * nbytes_used below threshold (strict <, lowest index wins).  -1 when none. */
 int adlbq_push_select(adlbq_server *h, double threshold, int *cand_server_rank, int *wqseqno);
 
+/* ---- byte accounting (SURVEY hard part 5; adlb.c:3419-3474).  The handle
+ * keeps the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced for the
+ * structures it replaces: 24 + 72 B plus the payload per wq unit (pmalloc +
+ * wq_node_create, adlb.c:933, 963), 24 + 80 B per parked Reserve
+ * (rq_node_create), 24 + 16 B per tq entry; the caller adds its own
+ * allocations (init tables, Isend buffers, common prefixes) with
+ * adlbq_bytes_adjust, so the count is the server's.  adlbq_qmstat_row stores
+ * it as this server's nbytes_used (adlb.c:3586). */
+int adlbq_bytes(adlbq_server *h, double *curr, double *hwm);  /* synchronises */
+int adlbq_bytes_adjust(adlbq_server *h, double delta);        /* enqueued in order */
+/* FA_PUT_HDR's memory check (adlb.c:908-931): rejected = curr + work_len >
+ * max_malloc; then hint = the server with the smallest nbytes_used below
+ * 0.95 * max_malloc (THRESHOLD_TO_START_PUSH, adlb.c:93), excluding this one,
+ * lowest index on ties, or -1 -- ack_buf[1] of the ADLB_PUT_REJECTED reply. */
+int adlbq_put_check(adlbq_server *h, int work_len, double max_malloc, int *rejected, int *hint_server_rank);
+
 /* Counters: wq->count, wq->max_count (ADLB_INFO_MAX_WQ_COUNT, adlb.c:3135), rq->count. */
 int adlbq_info(adlbq_server *h, int *wq_count, int *wq_max_count, int *rq_count);
 
-/* FA_INFO_NUM_WORK_UNITS (src/adlb.c:2466-2496). */
+/* FA_INFO_NUM_WORK_UNITS (src/adlb.c:2466-2496): the reference's two wq
+ * passes as one fused reduction over every page. */
 int adlbq_info_type(adlbq_server *h, int work_type, int *max_prio, int *num_max_prio,
                     int *num_type);
 

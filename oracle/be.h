@@ -56,6 +56,14 @@ void  be_rq_view(void *r, int *rank, int *rqseqno, int *types16);
 void  be_rq_delete(void *r);
 int   be_rq_count(void);
 
+/* The reference server's byte accounting (dmalloc/pmalloc/dfree,
+ * adlb.c:3419-3474) over the queue structures: node + record per wq unit
+ * (24 + 72 B) plus its payload, per rq entry (24 + 80 B), per tq entry
+ * (24 + 16 B).  *curr = bytes held now, *hwm = the high-water mark (-1 where
+ * the backend cannot tell); both include whatever the backend allocated at
+ * init (the caller subtracts the value it saw after be_reset). */
+void  be_bytes(double *curr, double *hwm);
+
 /* tq (xq.c:505-585) */
 int   be_tq_find_first_rt(int rank, int type); /* remote server rank or -1 */
 int   be_tq_bump_or_add(int rank, int type, int server); /* FA_DID_PUT_AT_REMOTE */

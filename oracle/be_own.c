@@ -47,6 +47,23 @@ typedef struct remote_rec {
 
 static chain_t units, parked, remotes;
 
+/* the reference's allocation sizes on LP64 (xq.h:8-79): xq_node_t 24 B,
+ * wq_struct_t 72 B, rq_struct_t 80 B, tq_struct_t 16 B */
+enum { NODE_B = 24, WQ_B = 72, RQ_B = 80, TQ_B = 16 };
+static double bytes_curr, bytes_hwm;
+static void bytes_add(double d)
+{
+    bytes_curr += d;
+    if (bytes_curr > bytes_hwm)
+        bytes_hwm = bytes_curr;
+}
+
+void be_bytes(double *curr, double *hwm)
+{
+    *curr = bytes_curr;
+    *hwm = bytes_hwm;
+}
+
 static void chain_clear(chain_t *c)
 {
     link_t *l = c->head.fwd;
@@ -104,12 +121,15 @@ void be_reset(void)
     chain_clear(&units);
     chain_clear(&parked);
     chain_clear(&remotes);
+    bytes_curr = bytes_hwm = 0.0;
 }
 
 void *be_wq_add(int type, int prio, int seqno, int answer, int target, int len,
                 int home, int clen, int csrv, int cseq)
 {
     unit_rec *u = (unit_rec *)malloc(sizeof *u);
+    bytes_add((double)len);           /* pmalloc(work_len), adlb.c:933 */
+    bytes_add((double)(WQ_B + NODE_B)); /* wq_node_create, xq.c:126 + 62 */
     u->work_type = type;
     u->work_prio = prio;
     u->wqseqno = seqno;
@@ -222,7 +242,12 @@ void be_wq_set_pin(void *h, int pin_rank, int pinned)
     u->pinned = pinned;
 }
 
-void be_wq_delete(void *h) { chain_unlink(&units, (link_t *)h); }
+void be_wq_delete(void *h)
+{
+    const unit_rec *u = (const unit_rec *)((link_t *)h)->rec;
+    bytes_add(-(double)(u->work_len + WQ_B + NODE_B)); /* wq_delete, xq.c:160-174 */
+    chain_unlink(&units, (link_t *)h);
+}
 int be_wq_count(void) { return units.n; }
 int be_wq_max_count(void) { return units.n_hwm; }
 void *be_wq_first(void) { return units.head.fwd == &units.head ? NULL : units.head.fwd; }
@@ -235,6 +260,7 @@ void *be_wq_next(void *h)
 void *be_rq_add(int rank, const int *types16, int rqseqno)
 {
     park_rec *p = (park_rec *)malloc(sizeof *p);
+    bytes_add((double)(RQ_B + NODE_B)); /* rq_node_create, xq.c:358 + 62 */
     p->world_rank = rank;
     p->rqseqno = rqseqno;
     memcpy(p->types, types16, sizeof p->types);
@@ -278,7 +304,11 @@ void be_rq_view(void *h, int *rank, int *rqseqno, int *types16)
     memcpy(types16, p->types, sizeof p->types);
 }
 
-void be_rq_delete(void *h) { chain_unlink(&parked, (link_t *)h); }
+void be_rq_delete(void *h)
+{
+    bytes_add(-(double)(RQ_B + NODE_B)); /* rq_delete, xq.c:378-385 */
+    chain_unlink(&parked, (link_t *)h);
+}
 int be_rq_count(void) { return parked.n; }
 
 int be_tq_find_first_rt(int rank, int type)
@@ -299,6 +329,7 @@ int be_tq_bump_or_add(int rank, int type, int server)
             return ++r->num_stored;
     }
     remote_rec *r = (remote_rec *)malloc(sizeof *r);
+    bytes_add((double)(TQ_B + NODE_B)); /* tq_node_create, xq.c:512 + 62 */
     r->app_rank = rank;
     r->work_type = type;
     r->remote_server_rank = server;

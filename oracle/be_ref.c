@@ -13,6 +13,10 @@
 #include "xq.h"        /* /root/reference/src/xq.h */
 #include "be.h"
 
+/* adlb.c's allocators (global functions of the reference, adlb.c:3419-3474) */
+void *pmalloc(int nbytes, const char *funcname, int linenum);
+void dfree(void *ptr, int nbytes, const char *funcname, int linenum);
+
 static void drain(xq_t *q, void (*del)(xq_node_t *))
 {
     xq_node_t *n;
@@ -46,9 +50,11 @@ void be_reset(void)
 void *be_wq_add(int type, int prio, int seqno, int answer, int target, int len,
                 int home, int clen, int csrv, int cseq)
 {
-    /* adlb.c:963-973: wq_node_create + field fill + wq_append; payload NULL so
-     * wq_delete's afree(work_buf) is skipped (xq.c:167) */
-    xq_node_t *n = wq_node_create(type, prio, seqno, answer, target, len, NULL);
+    /* adlb.c:933 + 963-973: the payload through the reference's pmalloc (so
+     * its accounting holds it, and wq_delete's afree releases it, xq.c:167),
+     * then wq_node_create + field fill + wq_append */
+    void *buf = len > 0 ? pmalloc(len, __FUNCTION__, __LINE__) : NULL;
+    xq_node_t *n = wq_node_create(type, prio, seqno, answer, target, len, buf);
     wq_struct_t *ws = (wq_struct_t *)n->data;
     ws->home_server_rank = home;
     ws->common_len = clen;
@@ -118,6 +124,25 @@ void be_rq_view(void *h, int *rank, int *rqseqno, int *t)
 
 void be_rq_delete(void *h) { rq_delete((xq_node_t *)h); }
 int be_rq_count(void) { return rq->count; }
+
+/* The reference keeps curr_bytes_dmalloced static (adlb.c:121); only its
+ * high-water mark is readable (ADLBP_Info_get(ADLB_INFO_MALLOC_HWM),
+ * adlb.c:3074-3078).  curr is read by a probe: pmalloc(X) raises the mark to
+ * curr + X when X exceeds the mark's lead over curr, and dfree returns it.
+ * Each probe uses a larger X (by 1 MiB), so it reads curr exactly while curr
+ * never drops by a MiB between probes (fixture traces are far smaller); the
+ * mark itself is then unusable (*hwm = -1). */
+void be_bytes(double *curr, double *hwm)
+{
+    static int probes;
+    const int x = (1 << 30) + (++probes << 20);
+    void *p = pmalloc(x, __FUNCTION__, __LINE__);
+    double m = 0;
+    ADLBP_Info_get(ADLB_INFO_MALLOC_HWM, &m);
+    dfree(p, x, __FUNCTION__, __LINE__);
+    *curr = m - (double)x;
+    *hwm = -1;
+}
 
 int be_tq_find_first_rt(int rank, int type)
 {

@@ -2,7 +2,7 @@
 
 Run in the build container (needs /root/reference and MPICH):
 
-    make -C oracle ref && python oracle/gen_golden.py
+    make -C oracle ref && python oracle/gen_golden.py [fixture names]
 
 Every fixture is (server configuration, int32 event trace, expected int32
 output stream) where the expected stream is produced by oracle/_ref/libxqref.so,
@@ -102,6 +102,76 @@ def donor_case(T=3):
     return np.asarray(ev, np.int32)
 
 
+def bytes_case():
+    """Byte accounting (adlb.c:3419-3474) and FA_PUT_HDR's reject check with its
+    hint (adlb.c:908-931): curr after puts with payloads, matches, parks, put-side
+    rq matches, rq deletes, tq entries and gets, on 4 servers (6 app ranks)."""
+    B, PC = [synth.OP_BYTES], synth.OP_PUTCHECK
+    ev = list(B)
+    ev += [synth.OP_SETROW, 1, 3, 1000, 1, 1, 1]
+    ev += [synth.OP_SETROW, 2, 0, 500, LOW, LOW, LOW]
+    ev += [synth.OP_SETROW, 3, 2, 2000, 2, 2, 2]
+    ev += put(0, 5, ln=100) + B + put(1, 7, ln=0) + B + put(2, 9, target=3, ln=40) + B
+    ev += [PC, 10, 400, PC, 10, 1000, PC, 700, 1000, PC, 0, 428, PC, 1, 428]
+    ev += res(0, [0]) + B + res(1, [2]) + B + res(2, [1], 0) + B + res(3, [2]) + B
+    ev += [G, 0, 1] + B + [G, 0, 1] + B
+    ev += put(2, 4, ln=16) + B
+    ev += res(4, [0]) + res(5, [0]) + B + [synth.OP_RQDEL, 2] + B + [synth.OP_RQDEL, 2] + B
+    ev += [synth.OP_TQADD, 4, 0, 9] + B + [synth.OP_TQADD, 4, 0, 9] + B + [synth.OP_TQADD, 4, 1, 9] + B
+    ev += [G, 3, 3] + B + put(0, 1, ln=7) + B + [PC, 2000, 2300, PC, 5, 100]
+    ev += [synth.OP_SETROW, 2, 0, 3000, LOW, LOW, LOW, PC, 5, 100, synth.OP_INFO]
+    return np.asarray(ev, np.int32)
+
+
+def bytes_stream(seed=61, n_events=600, kind="ref", hwm=False):
+    """A random mix of puts (payloads 0-200 B), Reserves (hanging or not, some
+    parking), gets of matched units and rq deletes, with the byte count after
+    every few events and reject checks against limits near it; the reference
+    itself decides every outcome the next event depends on (kind "own": the
+    restatement, for traces that also read the high-water mark, hwm=True)."""
+    rng = np.random.default_rng(seed)
+    o = oracle.Oracle(kind)
+    o.init([0, 1, 2], 16, 3, 1)
+    ev, matched, parked, nextrq = [], [], [], 1
+    curr = 0
+
+    def step(e):
+        ev.extend(e)
+        return synth.split_outputs(o.replay(np.asarray(e, np.int32)))[0]
+
+    step([synth.OP_SETROW, 0, 5, 700, 3, 3, 3])
+    step([synth.OP_SETROW, 2, 1, 300, 9, 9, 9])
+    for i in range(n_events):
+        k = rng.random()
+        if k < 0.4:
+            out = step(put(int(rng.integers(0, 3)), int(rng.integers(0, 8)), target=int(rng.integers(-1, 16))
+                           if rng.random() < 0.2 else -1, ln=int(rng.integers(0, 201))))
+            if out[1] >= 0:
+                parked = [p for p in parked if p[1] != out[2]]
+                matched.append((out[1], out[0]))
+        elif k < 0.75:
+            rank = int(rng.integers(0, 16))
+            types = [int(x) for x in rng.choice(3, size=int(rng.integers(1, 3)), replace=False)]
+            out = step(res(rank, types, int(rng.random() < 0.7)))
+            if out[0] == 1:
+                matched.append((rank, out[5]))
+            elif out[0] == 0:
+                parked.append((rank, out[10]))
+        elif k < 0.9 and matched:
+            rank, seq = matched.pop(int(rng.integers(0, len(matched))))
+            step([G, rank, seq])
+        elif parked:
+            rank, rqs = parked.pop(int(rng.integers(0, len(parked))))
+            step([synth.OP_RQDEL, rqs])
+        if i % 4 == 0:
+            curr = step([synth.OP_BYTES])[0]
+            if hwm:
+                step([synth.OP_HWM])
+        if i % 15 == 0:
+            step([synth.OP_PUTCHECK, int(rng.integers(0, 300)), max(1, curr + int(rng.integers(-200, 200)))])
+    return np.asarray(ev, np.int32)
+
+
 def save(name, user_types, num_app_ranks, num_servers, my_idx, trace):
     o = oracle.Oracle("ref")
     o.init(user_types, num_app_ranks, num_servers, my_idx)
@@ -116,6 +186,15 @@ def save(name, user_types, num_app_ranks, num_servers, my_idx, trace):
 def main():
     oracle.build(ref=True)
     os.makedirs(OUT, exist_ok=True)
+    only = set(sys.argv[1:])  # fixture names to (re)generate; none = all
+    if only:
+        if "t14_bytes" in only:
+            save("t14_bytes", [0, 1, 2], 6, 4, 0, bytes_case())
+        if "t15_bytes_stream" in only:
+            save("t15_bytes_stream", [0, 1, 2], 16, 3, 1, bytes_stream())
+        return
+    save("t14_bytes", [0, 1, 2], 6, 4, 0, bytes_case())
+    save("t15_bytes_stream", [0, 1, 2], 16, 3, 1, bytes_stream())
     for name, tr in edge_cases().items():
         save(name, [0, 1, 2, 3], 8, 1, 0, tr)
     save("t13_donor", [0, 1, 2], 5, 4, 0, donor_case())

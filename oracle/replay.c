@@ -21,6 +21,7 @@ static struct {
     double *qm_bytes; /* [num_servers]          qmstat_tbl[i].nbytes_used */
     int *rfr_out;     /* [num_world]  (adlb.c:112, zeroed: SURVEY hard part 4) */
     int *rfr_to_rank; /* [num_app_ranks] */
+    double bytes0;    /* the backend's byte count after init (queue bytes are relative to it) */
 } S;
 
 int orc_init(int ntypes, const int *user_types, int num_app_ranks, int num_servers,
@@ -50,6 +51,8 @@ int orc_init(int ntypes, const int *user_types, int num_app_ranks, int num_serve
     for (int i = 0; i < num_app_ranks; i++)
         S.rfr_to_rank[i] = -1;
     be_reset();
+    double h;
+    be_bytes(&S.bytes0, &h);
     return 0;
 }
 
@@ -149,6 +152,9 @@ int orc_event_nargs(int op, int ntypes)
     case ORC_OP_INFOTYPE: return 1;
     case ORC_OP_RFR: return 2 + ORC_REQ_TYPES;
     case ORC_OP_RQLIST: return 0;
+    case ORC_OP_BYTES: return 0;
+    case ORC_OP_PUTCHECK: return 2;
+    case ORC_OP_HWM: return 0;
     default: return -1;
     }
 }
@@ -315,6 +321,40 @@ long orc_replay(const int *tr, long ntrace, int *out, long outcap)
                 }
                 o[0] = cand;
                 o[1] = v.wqseqno;
+            }
+            n = 2;
+            break;
+        }
+        case ORC_OP_BYTES: {
+            double c, h;
+            be_bytes(&c, &h);
+            o[0] = (int)(c - S.bytes0);
+            n = 1;
+            break;
+        }
+        case ORC_OP_HWM: {
+            double c, h;
+            be_bytes(&c, &h);
+            o[0] = h < 0 ? -1 : (int)(h - S.bytes0);
+            n = 1;
+            break;
+        }
+        case ORC_OP_PUTCHECK: {
+            /* FA_PUT_HDR's memory check and reject hint, adlb.c:908-931 */
+            double c, h;
+            be_bytes(&c, &h);
+            o[0] = (c - S.bytes0) + (double)a[0] > (double)a[1];
+            o[1] = -1;
+            if (o[0]) {
+                const double thr = 0.95 * (double)a[1]; /* THRESHOLD_TO_START_PUSH, adlb.c:93 */
+                double smallest = 999999999999.9;
+                for (int i = 0; i < S.num_servers; i++) {
+                    int srv = S.master_server_rank + i;
+                    if (srv != S.my_world_rank && S.qm_bytes[i] < thr && S.qm_bytes[i] < smallest) {
+                        smallest = S.qm_bytes[i];
+                        o[1] = srv;
+                    }
+                }
             }
             n = 2;
             break;

@@ -29,6 +29,9 @@ enum {
     ORC_OP_INFOTYPE = 13, /* type                                               -> [max_prio, num_max_prio, num_type] */
     ORC_OP_RFR = 14,      /* rqseqno for_rank t0..t15 (SS_RFR rfr_buf)          -> SS_RFR_RESP [12] or [-2, rqseqno, for_rank] */
     ORC_OP_RQLIST = 15,   /*                                                    -> [k, (rqseqno, rank, t0..t15) * k] */
+    ORC_OP_BYTES = 16,    /*                                                    -> [curr] bytes the queues hold beyond init (adlb.c:3419-3474) */
+    ORC_OP_PUTCHECK = 17, /* work_len max_malloc                               -> [rejected, hint_server_rank] (adlb.c:908-931) */
+    ORC_OP_HWM = 18,      /*                                                    -> [hwm] their high-water mark beyond init (-1: backend cannot tell) */
 };
 
 /* TA_RESERVE_RESP layout (adlb.c:1213-1222), plus two slots this build uses

@@ -8,6 +8,7 @@
 """
 import glob
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -16,6 +17,8 @@ import oracle
 from adlb_amd import replay, synth
 from adlb_amd.server import Server
 from exact_check import check_batch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
 
 pytestmark = pytest.mark.gpu
 GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
@@ -264,3 +267,14 @@ def test_unreserve_resp_restores_queue(gpu_available):
         for o in outs[1:]:
             assert np.array_equal(o, outs[0])
         assert np.array_equal(outs[0][:, :10], np.asarray(exp)[:, :10])
+
+
+@pytest.mark.parametrize("seed", [62, 63])
+def test_bytes_hwm_vs_oracle(gpu_available, seed):
+    """The handle's byte accounting (adlbq_bytes, adlbq_put_check) over a random
+    put / Reserve / get / rq-delete stream, high-water mark included: identical
+    to the restatement (whose current count the reference pins: t14, t15)."""
+    import gen_golden
+    tr = gen_golden.bytes_stream(seed=seed, n_events=500, kind="own", hwm=True)
+    cfg = (16, 3, 1)
+    assert_same(run_abi([0, 1, 2], cfg, tr), run_oracle([0, 1, 2], cfg, tr))
