@@ -243,6 +243,7 @@ struct adlbq_server {
     int *d_getbuf = nullptr; long long cap_getbuf = 0;      // host-buffer Get batches: pairs, then results
     long long got_seen = 0, got_t_seen = 0;                 // the device Get counters already folded in
     int *d_info = nullptr;                                  // fused info reduction: per-block partials + counter
+    int *d_crem = nullptr, *h_crem = nullptr; long long cap_crem = 0;  // check_remote results (device, pinned)
     int *h_result = nullptr;           // pinned host mirror
     long long last_scan_units = 0;
 

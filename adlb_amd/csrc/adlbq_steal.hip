@@ -70,6 +70,12 @@ __global__ void k_grant(const int *__restrict__ pairs, int n, const long long *_
     if (bad && (threadIdx.x & 63) == 0 && b) atomicAdd(bad, __popcll(b));
 }
 
+__global__ void k_rfr_reset(int *rfr_to_rank, int A, int *rfr_out, int nworld) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < A) rfr_to_rank[i] = -1;
+    if (i < nworld) rfr_out[i] = 0;
+}
+
 // rq_find_seqno + rq_delete for many rqseqnos (adlb.c:1883, 1933)
 __global__ void k_rq_delete_batch(const int *__restrict__ rqseqnos, int n, int *rq_live, const DevCounters *ctr,
                                   int *found, int *ndel, int *bad) {
@@ -217,6 +223,11 @@ int adlbq_steal_begin(adlbq_server *h, int k) {
     if (!h || k < 1) return fail(ADLBQ_ERR_ARG, "adlbq_steal_begin");
     hipSetDevice(h->device);
     const int T = h->T;
+    // the round answers every SS_RFR the parks of this shard sent (resp[11]):
+    // as each SS_RFR_RESP would (adlb.c:1877-1878), rfr_to_rank = -1 and
+    // rfr_out = 0, so later parks and check_remote see no RFR outstanding
+    k_rfr_reset<<<(std::max(h->A, h->num_world) + 255) / 256, 256, 0, h->stream>>>(h->d_rfr_to_rank, h->A,
+                                                                                   h->d_rfr_out, h->num_world);
     // every live rq entry fits: the landed-snapshot bound, else the whole capacity
     const long long up = rq_live_upper(h);
     const int rqcap = (int)std::max(0ll, std::min<long long>(up, h->rq_cap));

@@ -771,13 +771,14 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
-                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info};
+                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
     if (h->h_snap) hipHostFree(h->h_snap);
     if (h->h_steal) hipHostFree(h->h_steal);
     if (h->h_apply) hipHostFree(h->h_apply);
+    if (h->h_crem) hipHostFree(h->h_crem);
     if (h->steal_ev) hipEventDestroy(h->steal_ev);
     if (h->apply_ev) hipEventDestroy(h->apply_ev);
     for (int i = 0; i < adlbq_server::NSNAP; i++)
@@ -1066,19 +1067,24 @@ int adlbq_check_remote(adlbq_server *h, int cap, int *out3, int *count) {
     int rc;
     if ((rc = sync_tables(h))) return rc;
     if (h->ctr_stale && (rc = refresh_counters(h))) return rc;
-    int *d_out = nullptr;
-    int nrq = h->ctr.rq_n;
-    int capd = std::max(1, std::min(cap, nrq));
-    AQ_HIP(hipMalloc((void **)&d_out, sizeof(int) * (3 * capd + 1)));
+    const int nrq = h->ctr.rq_n;
+    const int capd = std::max(1, std::min(cap, nrq));
+    // persistent device buffer and pinned staging (no allocation, one synchronisation)
+    if (3ll * capd + 1 > h->cap_crem) {
+        if (h->d_crem) AQ_HIP(hipFree(h->d_crem));
+        if (h->h_crem) AQ_HIP(hipHostFree(h->h_crem));
+        h->cap_crem = std::max(3ll * capd + 1, 2 * h->cap_crem);
+        AQ_HIP(hipMalloc((void **)&h->d_crem, sizeof(int) * h->cap_crem));
+        AQ_HIP(hipHostMalloc((void **)&h->h_crem, sizeof(int) * h->cap_crem, hipHostMallocDefault));
+    }
     k_checkrem<<<1, 64, 0, h->stream>>>(donor_ctx(h), h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr, capd,
-                                        d_out + 1, d_out);
+                                        h->d_crem + 1, h->d_crem);
     AQ_HIP(hipGetLastError());
-    int k = 0;
-    AQ_HIP(hipMemcpyAsync(&k, d_out, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipMemcpyAsync(h->h_crem, h->d_crem, sizeof(int) * (3 * (size_t)capd + 1), hipMemcpyDeviceToHost,
+                          h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
-    int kk = std::min(k, cap);
-    if (kk) AQ_HIP(hipMemcpy(out3, d_out + 1, sizeof(int) * 3 * kk, hipMemcpyDeviceToHost));
-    AQ_HIP(hipFree(d_out));
+    const int kk = std::min(h->h_crem[0], cap);
+    if (kk) memcpy(out3, h->h_crem + 1, sizeof(int) * 3 * (size_t)kk);
     *count = kk;
     return ADLBQ_OK;
 }

@@ -190,7 +190,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     S, T = SL * world, 4
     W3 = max(1, args.c3_warmup)
     nb = args.c3_steps + W3
-    srvs, streams, d_reqs, d_resp, d_trip, g_host, g_dev = [], [], [], [], [], [], []
+    srvs, streams, d_reqs, d_resp, g_host, g_dev = [], [], [], [], [], []
     for j in range(SL):
         idx = rank * SL + j
         w = synth.config3_shard(idx, S, N, T, R, seed=args.seed)
@@ -208,10 +208,6 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         with torch.cuda.stream(st):
             d_reqs.append(torch.from_numpy(reqs).to(dev))
             d_resp.append(torch.empty((nb, R, 12), dtype=torch.int32, device=dev))
-            tr = torch.empty((R, 3), dtype=torch.int32, device=dev)
-            tr[:, 0] = torch.from_numpy(w.r_rank).to(dev)
-            tr[:, 2] = -1
-            d_trip.append(tr)
             g_host.append(torch.empty((R, 3), dtype=torch.int32).pin_memory())
             g_dev.append(torch.empty((R, 3), dtype=torch.int32, device=dev))
         srvs.append(srv)
@@ -230,9 +226,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         res = shards.steal_round(srvs, k, timing=tm) if world > 1 else shards.steal_round_local(srvs, k, timing=tm)
         t2 = time.perf_counter()
         for j, srv in enumerate(srvs):
-            with torch.cuda.stream(streams[j]):
-                d_trip[j][:, 1].copy_(d_resp[j][b][:, 5])
-            srv.unreserve_batch_device(R, d_trip[j].data_ptr())
+            srv.unreserve_resp_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
             g = res.grants.get(srv.my_server_idx)
             if g is not None and g.size:
                 # pinned staging, free again: the last round's steal_check synchronised this stream

@@ -141,7 +141,10 @@ int adlbq_rq_delete(adlbq_server *h, int rqseqno, int *found);
  * written (<= k); navail[t] = available units of type t in all. */
 int adlbq_steal_export(adlbq_server *h, int k, int *recs8, int *nrec, long long *navail);
 
-/* The same export split in two so that many handles (shards on one GPU) scan
+/* A steal round answers every SS_RFR this shard's parks sent (resp[11]):
+ * _begin clears rfr_to_rank / rfr_out as each SS_RFR_RESP would
+ * (adlb.c:1877-1878).
+ * The same export split in two so that many handles (shards on one GPU) scan
  * concurrently: _begin enqueues the scan, the rq compaction and the copies to
  * pinned host memory on the handle's stream; _collect waits and hands out the
  * top-k records (any of recs8 / nrec / navail may be NULL) and the live rq

@@ -34,10 +34,22 @@ def _run(S, n_units, R, seed, k, **kw):
             q, hi = srv.qmstat_row()
             oq, ohi = orcs[s].qmrow()
             assert q == oq and hi.tolist() == ohi.tolist()
+            # the round answered every SS_RFR the parks sent: the serial model
+            # receives each SS_RFR_RESP (adlb.c:1877-1878) as RFRDONE
+            rfr = [[synth.OP_RFRDONE, int(r[11]), int(rk)] for r, rk in zip(resps[s], w.r_rank)
+                   if r[0] == 0 and r[11] >= 0]
+            if rfr:
+                orcs[s].replay(np.asarray(rfr, np.int32).ravel())
             tv = synth.type_vectors(rng, w.user_types, 256)
             tr = np.concatenate([synth.simple_events(synth.OP_INFO),
                                  synth.reserve_events(np.arange(256) * S + s, tv, np.zeros(256, np.uint8)),
                                  synth.simple_events(synth.OP_INFO)])
+            np.testing.assert_array_equal(replay.replay(srv, tr), orcs[s].replay(tr))
+            # parks after the round: their RFR donors (resp[11]) and check_remote
+            # see no RFR outstanding from before the round
+            tv = synth.type_vectors(rng, w.user_types, 64)
+            tr = np.concatenate([synth.reserve_events(np.arange(64) * S + s, tv, np.ones(64, np.uint8)),
+                                 synth.simple_events(synth.OP_CHECKREM), synth.simple_events(synth.OP_INFO)])
             np.testing.assert_array_equal(replay.replay(srv, tr), orcs[s].replay(tr))
     finally:
         for srv in srvs:
