@@ -36,6 +36,10 @@ SIGNATURES = {
     "adlbq_rfr_done": (c_int, [P, c_int, c_int]),
     "adlbq_tq_add": (c_int, [P, c_int, c_int, c_int]),
     "adlbq_rq_delete": (c_int, [P, c_int, P]),
+    "adlbq_tq_dec": (c_int, [P, c_int, c_int, c_int]),
+    "adlbq_rfr_failed": (c_int, [P, c_int, c_int, P]),
+    "adlbq_rfr_retry": (c_int, [P, c_int, P, P]),
+    "adlbq_unit_target": (c_int, [P, c_int, P]),
     "adlbq_steal_export": (c_int, [P, c_int, P, P, P]),
     "adlbq_rq_export": (c_int, [P, c_int, P, P]),
     "adlbq_steal_begin": (c_int, [P, c_int]),

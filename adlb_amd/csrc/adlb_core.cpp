@@ -1,0 +1,474 @@
+// adlb_core.cpp -- the ADLB server's message handlers over the adlbq engine.
+//
+// Each handler restates one branch of the reference server loop
+// (ADLBP_Server, src/adlb.c:382-2500) with the queue work replaced by adlbq
+// calls (GPU) and the replies emitted in the reference's order.  Host-side
+// state: unit payloads and put timestamps (wqseqno -> bytes), common prefixes
+// (cq), the parked Reserves' type vectors (for the SS_RFR buffers), and the
+// counters behind ADLB_Info_get.
+#include "adlb_core.h"
+
+#include <chrono>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "adlb_wire.h"
+#include "adlbq.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string &m) {
+    g_err = m;
+    return -1;
+}
+
+double now() {
+    using namespace std::chrono;
+    return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+struct Unit {
+    std::vector<char> buf;
+    double t = 0.0;  // ws->time_stamp (adlb.c:972)
+};
+
+struct Common {
+    std::vector<char> buf;
+    int refcnt = -1;  // unknown until FA_PUT_BATCH_DONE (adlb.c:1144)
+    int ngets = 0;
+};
+
+struct Parked {
+    int rank = -1;
+    int types[WIRE_REQ];
+    double t = 0.0;
+};
+
+}  // namespace
+
+struct adlbsrv {
+    adlbq_server *q = nullptr;
+    int T = 0, A = 0, S = 1, me = 0, master = 0;
+    double max_malloc = 0.0;
+    adlbsrv_emit_fn emit = nullptr;
+    void *ctx = nullptr;
+    bool nmw = false;
+    std::unordered_map<int, Unit> units;
+    std::unordered_map<int, Common> cq;
+    int next_cq = 1;
+    std::unordered_map<int, Parked> parked;  // rqseqno -> parked Reserve
+    int rfr_out = 0;
+    long long activity = 0;
+    // ADLB_Info_get counters (adlb.c:3072-3141)
+    long long num_reserves = 0, num_put_on_rq = 0, num_rejected = 0, n_rq_timed = 0;
+    double time_on_rq = 0.0;
+    std::vector<char> first_time_on_rq;
+    std::vector<int> reqs, resp, pairs, out5, crem, rqx;
+
+    int rc(int r, const char *what) {
+        if (r) g_err = std::string(what) + ": " + adlbq_last_error();
+        return r ? -1 : 0;
+    }
+    void send(int dest, int tag, const void *b, int n) { emit(ctx, dest, tag, b, n); }
+    void send_ints(int dest, int tag, const int *v, int n) { send(dest, tag, v, (int)sizeof(int) * n); }
+    void send_rc(int dest, int tag, int code) {
+        int b[WIRE_IBUF] = {code};
+        send_ints(dest, tag, b, WIRE_IBUF);
+    }
+    void send_rfr(int donor, int rqseqno, const Parked &p) {
+        int b[WIRE_RFR] = {rqseqno, p.rank};
+        std::memcpy(b + 2, p.types, sizeof(p.types));
+        send_ints(donor, TAG_SS_RFR, b, WIRE_RFR);
+        rfr_out++;
+    }
+    void served(int rqseqno) {  // a parked Reserve got its answer (time_on_rq, adlb.c:1015-1021)
+        auto it = parked.find(rqseqno);
+        if (it == parked.end()) return;
+        const int r = it->second.rank;
+        if (r >= 0 && r < A && first_time_on_rq[r]) first_time_on_rq[r] = 0;
+        else {
+            time_on_rq += now() - it->second.t;
+            n_rq_timed++;
+        }
+        parked.erase(it);
+    }
+    // check_remote_work_for_queued_apps (adlb.c:3536-3579)
+    int check_remote() {
+        int cnt = 0;
+        const int cap = (int)parked.size();
+        if (!cap) return 0;
+        crem.resize(3 * (size_t)cap);
+        if (rc(adlbq_check_remote(q, cap, crem.data(), &cnt), "adlbq_check_remote")) return -1;
+        for (int i = 0; i < cnt; i++) {
+            auto it = parked.find(crem[3 * i]);
+            if (it != parked.end()) send_rfr(crem[3 * i + 2], crem[3 * i], it->second);
+        }
+        return 0;
+    }
+    // answer every parked Reserve with code, FIFO order (adlb.c:1412-1442, 1639-1649)
+    int drain_rq(int code) {
+        if (parked.empty()) return 0;
+        int count = 0;
+        rqx.resize(18 * parked.size());
+        if (rc(adlbq_rq_export(q, (int)parked.size(), rqx.data(), &count), "adlbq_rq_export")) return -1;
+        count = std::min<int>(count, (int)parked.size());
+        std::vector<int> seqs((size_t)count), found((size_t)count);
+        for (int i = 0; i < count; i++) {
+            send_rc(rqx[18 * (size_t)i + 1], TAG_RESERVE_RESP, code);
+            seqs[(size_t)i] = rqx[18 * (size_t)i];
+            parked.erase(seqs[(size_t)i]);
+        }
+        if (count && rc(adlbq_rq_delete_batch(q, count, seqs.data(), found.data()), "adlbq_rq_delete_batch"))
+            return -1;
+        parked.clear();
+        return 0;
+    }
+};
+
+extern "C" {
+
+const char *adlbsrv_last_error(void) { return g_err.c_str(); }
+
+int adlbsrv_create(adlbsrv **out, int ntypes, const int *user_types, int num_app_ranks, int num_servers,
+                   int my_world_rank, double max_malloc, int device, adlbsrv_emit_fn emit, void *ctx) {
+    if (!out || !emit || num_servers < 1 || my_world_rank < num_app_ranks ||
+        my_world_rank >= num_app_ranks + num_servers)
+        return fail("adlbsrv_create: bad argument");
+    auto *s = new adlbsrv();
+    s->T = ntypes;
+    s->A = num_app_ranks;
+    s->S = num_servers;
+    s->me = my_world_rank;
+    s->master = num_app_ranks;
+    s->max_malloc = max_malloc;
+    s->emit = emit;
+    s->ctx = ctx;
+    s->first_time_on_rq.assign((size_t)std::max(num_app_ranks, 1), 1);
+    if (adlbq_create(&s->q, ntypes, user_types, num_app_ranks, num_servers, my_world_rank - num_app_ranks,
+                     1 << 16, device)) {
+        g_err = std::string("adlbq_create: ") + adlbq_last_error();
+        delete s;
+        return -1;
+    }
+    *out = s;
+    return 0;
+}
+
+int adlbsrv_destroy(adlbsrv *s) {
+    if (!s) return 0;
+    if (s->q) adlbq_destroy(s->q);
+    delete s;
+    return 0;
+}
+
+int adlbsrv_put_hdr(adlbsrv *s, int src, const int *hdr, int *need_payload) {
+    *need_payload = 0;
+    if (s->nmw) {  // adlb.c:894-901
+        s->send_rc(src, TAG_ACK_AND_RC, WIRE_NO_MORE_WORK);
+        return 0;
+    }
+    int rej = 0, hint = -1;
+    if (s->rc(adlbq_put_check(s->q, hdr[4], s->max_malloc, &rej, &hint), "adlbq_put_check")) return -1;
+    if (rej) {  // adlb.c:908-931
+        s->num_rejected++;
+        int b[WIRE_IBUF] = {WIRE_PUT_REJECTED, hint, 1};
+        s->send_ints(src, TAG_ACK_AND_RC, b, WIRE_IBUF);
+        return 0;
+    }
+    s->send_rc(src, TAG_ACK_AND_RC, WIRE_SUCCESS);  // adlb.c:960-961
+    *need_payload = 1;
+    return 0;
+}
+
+int adlbsrv_put_payload(adlbsrv *s, int src, const int *hdr, const void *buf, int len) {
+    // wq_node_create + wq_append, then rq_find_rank_queued_for_type (adlb.c:963-988)
+    const int u[ADLBQ_PUT_INTS] = {hdr[0], hdr[1], hdr[2], hdr[3], hdr[4], hdr[5], hdr[7], hdr[8], hdr[9]};
+    int o[3];
+    if (s->rc(adlbq_put_batch(s->q, 1, u, o), "adlbq_put_batch")) return -1;
+    Unit &unit = s->units[o[0]];
+    unit.buf.assign((const char *)buf, (const char *)buf + (len > 0 ? len : 0));
+    unit.t = now();
+    s->activity++;
+    if (o[1] >= 0) {  // the parked Reserve gets this unit (adlb.c:989-1042)
+        int b[WIRE_IBUF] = {WIRE_SUCCESS, hdr[0], hdr[1], hdr[4], hdr[2], o[0], s->me, hdr[7], hdr[8], hdr[9]};
+        s->send_ints(o[1], TAG_RESERVE_RESP, b, WIRE_IBUF);
+        s->served(o[2]);
+    }
+    s->send_rc(src, TAG_ACK_AND_RC, WIRE_SUCCESS);  // adlb.c:1048-1049
+    return 0;
+}
+
+int adlbsrv_put_common_hdr(adlbsrv *s, int src, int common_len, int *need_payload) {
+    *need_payload = 0;
+    if (s->nmw) {
+        s->send_rc(src, TAG_ACK_AND_RC, WIRE_NO_MORE_WORK);
+        return 0;
+    }
+    int rej = 0, hint = -1;
+    if (s->rc(adlbq_put_check(s->q, common_len, s->max_malloc, &rej, &hint), "adlbq_put_check")) return -1;
+    if (rej) {  // adlb.c:1068-1093
+        s->num_rejected++;
+        int b[WIRE_IBUF] = {WIRE_PUT_REJECTED, hint, 1};
+        s->send_ints(src, TAG_ACK_AND_RC, b, WIRE_IBUF);
+        return 0;
+    }
+    s->send_rc(src, TAG_ACK_AND_RC, WIRE_SUCCESS);
+    *need_payload = 1;
+    return 0;
+}
+
+int adlbsrv_put_common_payload(adlbsrv *s, int src, const void *buf, int len) {
+    // cq_node_create + cq_append (adlb.c:1127-1132); its bytes count like a put's
+    Common &c = s->cq[s->next_cq];
+    c.buf.assign((const char *)buf, (const char *)buf + (len > 0 ? len : 0));
+    adlbq_bytes_adjust(s->q, (double)len);
+    int b[WIRE_IBUF] = {WIRE_SUCCESS, s->next_cq};
+    s->next_cq++;
+    s->send_ints(src, TAG_ACK_AND_RC, b, WIRE_IBUF);
+    return 0;
+}
+
+static void cq_maybe_free(adlbsrv *s, int cqseqno) {
+    auto it = s->cq.find(cqseqno);
+    if (it != s->cq.end() && it->second.refcnt == it->second.ngets) {  // cq_delete (adlb.c:1145, 1330)
+        adlbq_bytes_adjust(s->q, -(double)it->second.buf.size());
+        s->cq.erase(it);
+    }
+}
+
+int adlbsrv_batch_done(adlbsrv *s, int src, int cqseqno, int refcnt) {
+    if (cqseqno > 0) {
+        auto it = s->cq.find(cqseqno);
+        if (it != s->cq.end()) {
+            it->second.refcnt = refcnt;
+            cq_maybe_free(s, cqseqno);
+        }
+    }
+    s->send_rc(src, TAG_ACK_AND_RC, s->nmw ? WIRE_NO_MORE_WORK : WIRE_SUCCESS);
+    return 0;
+}
+
+int adlbsrv_get_common(adlbsrv *s, int src, int cqseqno) {
+    auto it = s->cq.find(cqseqno);
+    if (it == s->cq.end()) return fail("FA_GET_COMMON: unknown common seqno " + std::to_string(cqseqno));
+    s->send(src, TAG_GET_COMMON_RESP, it->second.buf.data(), (int)it->second.buf.size());
+    it->second.ngets++;
+    cq_maybe_free(s, cqseqno);
+    return 0;
+}
+
+int adlbsrv_did_put_at_remote(adlbsrv *s, int type, int target, int server_rank) {
+    if (s->rc(adlbq_tq_add(s->q, target, type, server_rank), "adlbq_tq_add")) return -1;
+    return s->check_remote();  // adlb.c:1179
+}
+
+int adlbsrv_reserve_batch(adlbsrv *s, int n, const int *src, const int *bufs17) {
+    s->num_reserves += n;
+    if (s->nmw) {  // adlb.c:1192-1198
+        for (int i = 0; i < n; i++) s->send_rc(src[i], TAG_RESERVE_RESP, WIRE_NO_MORE_WORK);
+        return 0;
+    }
+    s->reqs.resize((size_t)n * ADLBQ_RESERVE_INTS);
+    s->resp.resize((size_t)n * ADLBQ_RESP_INTS);
+    for (int i = 0; i < n; i++) {
+        int *r = s->reqs.data() + (size_t)i * ADLBQ_RESERVE_INTS;
+        r[0] = src[i];
+        std::memcpy(r + 1, bufs17 + (size_t)i * 17, sizeof(int) * 17);
+    }
+    if (s->rc(adlbq_reserve_batch(s->q, n, s->reqs.data(), s->resp.data()), "adlbq_reserve_batch")) return -1;
+    const double t = now();
+    for (int i = 0; i < n; i++) {
+        int *r = s->resp.data() + (size_t)i * ADLBQ_RESP_INTS;
+        if (r[0] == 1) {  // adlb.c:1207-1224
+            int b[WIRE_IBUF];
+            std::memcpy(b, r, sizeof(int) * 10);
+            b[10] = b[11] = 0;
+            s->send_ints(src[i], TAG_RESERVE_RESP, b, WIRE_IBUF);
+            s->activity++;
+        } else if (r[0] == -2) {  // adlb.c:1311-1316
+            s->send_rc(src[i], TAG_RESERVE_RESP, WIRE_NO_CURR_WORK);
+        } else {  // parked (adlb.c:1240-1309)
+            Parked &p = s->parked[r[10]];
+            p.rank = src[i];
+            std::memcpy(p.types, s->reqs.data() + (size_t)i * ADLBQ_RESERVE_INTS + 2, sizeof(p.types));
+            p.t = t;
+            s->num_put_on_rq++;
+            if (r[11] >= 0) s->send_rfr(r[11], r[10], p);
+        }
+    }
+    return 0;
+}
+
+int adlbsrv_get_batch(adlbsrv *s, int n, const int *src, const int *wqseqno) {
+    if (s->nmw) {  // adlb.c:1340-1346
+        for (int i = 0; i < n; i++) {
+            double d[WIRE_IBUF] = {(double)WIRE_NO_MORE_WORK};
+            s->send(src[i], TAG_ACK_AND_RC, d, (int)sizeof d);
+        }
+        return 0;
+    }
+    s->pairs.resize(2 * (size_t)n);
+    s->out5.resize(5 * (size_t)n);
+    for (int i = 0; i < n; i++) {
+        s->pairs[2 * (size_t)i] = src[i];
+        s->pairs[2 * (size_t)i + 1] = wqseqno[i];
+    }
+    if (s->rc(adlbq_get_reserved_batch(s->q, n, s->pairs.data(), s->out5.data()), "adlbq_get_reserved_batch"))
+        return -1;
+    const double t = now();
+    int bad = 0;
+    for (int i = 0; i < n; i++) {
+        const int *o = s->out5.data() + 5 * (size_t)i;
+        auto it = o[0] == 1 ? s->units.find(wqseqno[i]) : s->units.end();
+        if (it == s->units.end()) {  // adlb.c:1349-1358
+            double d[WIRE_IBUF] = {(double)WIRE_ERROR};
+            s->send(src[i], TAG_ACK_AND_RC, d, (int)sizeof d);
+            bad++;
+            continue;
+        }
+        double d[WIRE_IBUF] = {(double)WIRE_SUCCESS, (double)o[1], t - it->second.t};
+        s->send(src[i], TAG_ACK_AND_RC, d, (int)sizeof d);  // adlb.c:1360-1366
+        s->send(src[i], TAG_GET_RESERVED_RESP, it->second.buf.data(), (int)it->second.buf.size());
+        s->units.erase(it);
+        s->activity++;
+    }
+    if (bad) return fail("FA_GET_RESERVED: " + std::to_string(bad) + " unit(s) not reserved for the rank");
+    return 0;
+}
+
+int adlbsrv_info_num(adlbsrv *s, int src, int work_type) {
+    int b[WIRE_IBUF] = {ADLBQ_LOWEST_PRIO, 0, 0, s->nmw ? WIRE_NO_MORE_WORK : 0};
+    if (s->rc(adlbq_info_type(s->q, work_type, &b[0], &b[1], &b[2]), "adlbq_info_type")) return -1;
+    s->send_ints(src, TAG_ACK_AND_RC, b, WIRE_IBUF);
+    return 0;
+}
+
+int adlbsrv_no_more_work(adlbsrv *s) {
+    const int fresh = !s->nmw;
+    s->nmw = true;
+    if (s->drain_rq(WIRE_NO_MORE_WORK)) return -1;
+    return fresh;
+}
+
+int adlbsrv_exhausted(adlbsrv *s) { return s->drain_rq(WIRE_DONE_BY_EXHAUSTION); }
+
+int adlbsrv_qmstat(adlbsrv *s, const int *qlen, const double *nbytes, const int *hi) {
+    const int mine = s->me - s->master;
+    for (int i = 0; i < s->S; i++)
+        if (i != mine &&
+            s->rc(adlbq_set_qmstat_row(s->q, i, qlen[i], nbytes[i], hi + (size_t)i * s->T), "adlbq_set_qmstat_row"))
+            return -1;
+    return s->check_remote();  // adlb.c:1755
+}
+
+int adlbsrv_my_row(adlbsrv *s, int *qlen, double *nbytes, int *hi) {
+    if (s->rc(adlbq_qmstat_row(s->q, qlen, hi), "adlbq_qmstat_row")) return -1;
+    double hwm;
+    return s->rc(adlbq_bytes(s->q, nbytes, &hwm), "adlbq_bytes");
+}
+
+int adlbsrv_rfr(adlbsrv *s, int src, const int *b) {
+    // the donor side: wq_find_pre_targeted_hi_prio(for_rank) then wq_find_hi_prio, pin (adlb.c:1807-1827)
+    int req[ADLBQ_RESERVE_INTS] = {b[1], 0};
+    std::memcpy(req + 2, b + 2, sizeof(int) * WIRE_REQ);
+    int r[ADLBQ_RESP_INTS];
+    if (s->rc(adlbq_reserve_batch(s->q, 1, req, r), "adlbq_reserve_batch")) return -1;
+    int o[WIRE_RFR] = {0};
+    if (r[0] == 1) {  // adlb.c:1821-1846
+        int prev_target = -1;
+        if (s->rc(adlbq_unit_target(s->q, r[5], &prev_target), "adlbq_unit_target")) return -1;
+        const int v[12] = {WIRE_SUCCESS, b[0], b[1], r[1], r[2], r[3], r[4], r[5], prev_target, r[7], r[8], r[9]};
+        std::memcpy(o, v, sizeof v);
+        s->activity++;
+    } else {  // adlb.c:1848-1863
+        o[0] = WIRE_NO_CURR_WORK;
+        o[1] = b[0];
+        o[2] = b[1];
+        std::memcpy(o + 3, b + 2, sizeof(int) * WIRE_REQ);
+    }
+    s->send_ints(src, TAG_SS_RFR_RESP, o, WIRE_RFR);
+    return 0;
+}
+
+int adlbsrv_rfr_resp(adlbsrv *s, int src, const int *b) {
+    const int code = b[0], rqseqno = b[1], for_rank = b[2];
+    if (s->rc(adlbq_rfr_done(s->q, src, for_rank), "adlbq_rfr_done")) return -1;  // adlb.c:1877-1878
+    if (s->rfr_out > 0) s->rfr_out--;
+    if (code == WIRE_SUCCESS) {
+        int found = 0;
+        if (s->rc(adlbq_rq_delete(s->q, rqseqno, &found), "adlbq_rq_delete")) return -1;
+        if (found) {  // adlb.c:1884-1947
+            auto it = s->parked.find(rqseqno);
+            const int rank = it != s->parked.end() ? it->second.rank : for_rank;
+            int r[WIRE_IBUF] = {WIRE_SUCCESS, b[3], b[4], b[5], b[6], b[7], src, b[9], b[10], b[11]};
+            s->send_ints(rank, TAG_RESERVE_RESP, r, WIRE_IBUF);
+            s->served(rqseqno);
+            s->activity++;
+            if (for_rank == b[8] && s->rc(adlbq_tq_dec(s->q, for_rank, b[3], src), "adlbq_tq_dec")) return -1;
+        } else {  // a Put answered it meanwhile: give the unit back (adlb.c:1949-1963)
+            int u[WIRE_IBUF] = {for_rank, b[7], b[8]};
+            s->send_ints(src, TAG_SS_UNRESERVE, u, WIRE_IBUF);
+        }
+        return s->check_remote();  // adlb.c:1964
+    }
+    // failure: patch the donor's row and tq, retry this Reserve, then everyone (adlb.c:1966-2047)
+    if (s->rc(adlbq_rfr_failed(s->q, src, for_rank, b + 3), "adlbq_rfr_failed")) return -1;
+    int found = 0, donor = -1;
+    if (s->rc(adlbq_rfr_retry(s->q, rqseqno, &found, &donor), "adlbq_rfr_retry")) return -1;
+    if (found && donor >= 0) {
+        auto it = s->parked.find(rqseqno);
+        if (it != s->parked.end()) s->send_rfr(donor, rqseqno, it->second);
+    }
+    return s->check_remote();
+}
+
+int adlbsrv_unreserve(adlbsrv *s, int src, const int *b) {
+    (void)src;
+    int found = 0;
+    if (s->rc(adlbq_unreserve(s->q, b[0], b[1], b[2], &found), "adlbq_unreserve")) return -1;
+    s->activity++;
+    return 0;
+}
+
+int adlbsrv_num_parked(adlbsrv *s) { return (int)s->parked.size(); }
+long long adlbsrv_activity(adlbsrv *s) { return s->activity; }
+int adlbsrv_rfr_outstanding(adlbsrv *s) { return s->rfr_out; }
+int adlbsrv_nmw(adlbsrv *s) { return s->nmw ? 1 : 0; }
+
+int adlbsrv_info_get(adlbsrv *s, int key, double *val) {
+    double curr = 0, hwm = 0;
+    int wq = 0, wqmax = 0, rq = 0;
+    switch (key) {
+    case 1:  // ADLB_INFO_MALLOC_HWM
+        if (s->rc(adlbq_bytes(s->q, &curr, &hwm), "adlbq_bytes")) return -1;
+        *val = hwm;
+        return 0;
+    case 2:  // ADLB_INFO_AVG_TIME_ON_RQ
+        *val = s->n_rq_timed ? s->time_on_rq / (double)s->n_rq_timed : 0.0;
+        return 0;
+    case 3: case 4: case 6: case 7: case 8: case 9:  // push / qmstat-ring timings: no push, no ring here
+        *val = 0.0;
+        return 0;
+    case 5:  // ADLB_INFO_NREJECTED_PUTS
+        *val = (double)s->num_rejected;
+        return 0;
+    case 10:  // ADLB_INFO_NUM_RESERVES
+        *val = (double)s->num_reserves;
+        return 0;
+    case 11:  // ADLB_INFO_NUM_RESERVES_PUT_ON_RQ
+        *val = (double)s->num_put_on_rq;
+        return 0;
+    case 12:  // ADLB_INFO_MAX_WQ_COUNT
+        if (s->rc(adlbq_info(s->q, &wq, &wqmax, &rq), "adlbq_info")) return -1;
+        *val = (double)wqmax;
+        return 0;
+    default:
+        return fail("adlbsrv_info_get: unknown key");
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+/* adlb_core.h -- the ADLB server's message handlers, without MPI.
+ *
+ * One adlbsrv object = one server rank.  Each function is the handler of one
+ * inbound message kind of the reference server loop (ADLBP_Server,
+ * src/adlb.c:382-2500) and emits its replies through the callback given at
+ * create, in the order the reference sends them.  The queue work runs on the
+ * GPU through the adlbq engine (include/adlbq.h); payloads, common prefixes
+ * and timestamps stay in host memory here.
+ *
+ * Two drivers use it: the MPI server loop (adlb_mpi.cpp, libadlb.so) and the
+ * replay of recorded reference event streams (tests/test_gpu_server.py).
+ */
+#ifndef ADLB_CORE_H
+#define ADLB_CORE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct adlbsrv adlbsrv;
+/* dest = world rank; buf/nbytes are only valid during the call */
+typedef void (*adlbsrv_emit_fn)(void *ctx, int dest, int tag, const void *buf, int nbytes);
+
+int adlbsrv_create(adlbsrv **out, int ntypes, const int *user_types, int num_app_ranks, int num_servers,
+                   int my_world_rank, double max_malloc, int device, adlbsrv_emit_fn emit, void *ctx);
+int adlbsrv_destroy(adlbsrv *s);
+const char *adlbsrv_last_error(void);
+
+/* FA_PUT_HDR (adlb.c:891-962): acks (or rejects / answers NO_MORE_WORK);
+ * *need_payload = 1 when the sender will now send the payload, which goes to
+ * adlbsrv_put_payload (adlb.c:963-1049). */
+int adlbsrv_put_hdr(adlbsrv *s, int src, const int *hdr12, int *need_payload);
+int adlbsrv_put_payload(adlbsrv *s, int src, const int *hdr12, const void *buf, int len);
+/* FA_PUT_COMMON_HDR / _MSG (adlb.c:1054-1134), FA_PUT_BATCH_DONE (1135-1160),
+ * FA_GET_COMMON (1321-1332) */
+int adlbsrv_put_common_hdr(adlbsrv *s, int src, int common_len, int *need_payload);
+int adlbsrv_put_common_payload(adlbsrv *s, int src, const void *buf, int len);
+int adlbsrv_batch_done(adlbsrv *s, int src, int cqseqno, int refcnt);
+int adlbsrv_get_common(adlbsrv *s, int src, int cqseqno);
+/* FA_DID_PUT_AT_REMOTE (adlb.c:1161-1180) */
+int adlbsrv_did_put_at_remote(adlbsrv *s, int type, int target, int server_rank);
+/* n FA_RESERVEs in arrival order (adlb.c:1181-1320): one adlbq_reserve_batch */
+int adlbsrv_reserve_batch(adlbsrv *s, int n, const int *src, const int *bufs17);
+/* n FA_GET_RESERVEDs in arrival order (adlb.c:1333-1384): one adlbq_get_reserved_batch */
+int adlbsrv_get_batch(adlbsrv *s, int n, const int *src, const int *wqseqno);
+/* FA_INFO_NUM_WORK_UNITS (adlb.c:2466-2496) */
+int adlbsrv_info_num(adlbsrv *s, int src, int work_type);
+/* FA_NO_MORE_WORK / SS_NO_MORE_WORK (adlb.c:1385-1492): set the flag and
+ * answer every parked Reserve; returns 1 if the flag was newly set */
+int adlbsrv_no_more_work(adlbsrv *s);
+/* SS_DONE_BY_EXHAUSTION (adlb.c:1627-1650, 757-772): answer every parked Reserve */
+int adlbsrv_exhausted(adlbsrv *s);
+/* SS_QMSTAT (adlb.c:1705-1757): install the other servers' rows, then
+ * check_remote_work_for_queued_apps (3536-3579).  qlen[S], nbytes[S], hi[S*T]. */
+int adlbsrv_qmstat(adlbsrv *s, const int *qlen, const double *nbytes, const int *hi);
+/* update_local_state (adlb.c:3581-3593): this server's row */
+int adlbsrv_my_row(adlbsrv *s, int *qlen, double *nbytes, int *hi);
+/* SS_RFR (adlb.c:1802-1866), SS_RFR_RESP (1867-2050), SS_UNRESERVE (2051-2070) */
+int adlbsrv_rfr(adlbsrv *s, int src, const int *buf28);
+int adlbsrv_rfr_resp(adlbsrv *s, int src, const int *buf28);
+int adlbsrv_unreserve(adlbsrv *s, int src, const int *buf12);
+
+/* state for the driver */
+int adlbsrv_num_parked(adlbsrv *s);     /* rq->count */
+long long adlbsrv_activity(adlbsrv *s); /* events that changed a queue (exhaustion check) */
+int adlbsrv_rfr_outstanding(adlbsrv *s);
+int adlbsrv_nmw(adlbsrv *s);
+/* ADLB_Info_get keys (adlb.h ADLB_INFO_*, adlb.c:3072-3141) */
+int adlbsrv_info_get(adlbsrv *s, int key, double *val);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

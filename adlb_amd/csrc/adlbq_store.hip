@@ -662,6 +662,21 @@ __global__ void k_rq_delete(int k, int *rq_live, DevCounters *ctr, int *res) {
     }
 }
 
+// SS_RFR_RESP failure's retry for the original Reserve (adlb.c:2007-2041): if
+// rqseqno k+1 is still parked, its first type with a donor gets a new SS_RFR
+__global__ void k_rfr_retry(DonorCtx c, const int *__restrict__ rq_rank, const int *__restrict__ rq_types,
+                            const int *rq_live, const DevCounters *ctr, int k, int *out2) {
+    int found = 0, cand = -1;
+    if (k >= 0 && k < ctr->rq_n && ld_agent(rq_live + k)) {
+        found = 1;
+        cand = rfr_select(c, rq_rank[k], rq_types + (long long)k * NREQ);
+    }
+    if (threadIdx.x == 0) {
+        out2[0] = found;
+        out2[1] = cand;
+    }
+}
+
 __global__ void k_set_int(int *p, int v) { *p = v; }
 
 __global__ void k_add_bytes(DevCounters *ctr, long long d) { bytes_add(ctr, d); }
@@ -682,8 +697,17 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
         return fail(ADLBQ_ERR_ARG, "adlbq_create: bad argument");
     if (ntypes > ADLBQ_MAX_TYPES) return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 64 work types");
     auto *h = new adlbq_server();
+    hipError_t e;
+    if (device < 0) {  // one GPU per server shard, round robin over the visible devices
+        int ndev = 0;
+        if ((e = hipGetDeviceCount(&ndev)) != hipSuccess || ndev < 1) {
+            delete h;
+            return hip_fail(e == hipSuccess ? hipErrorNoDevice : e, "hipGetDeviceCount");
+        }
+        device = my_server_idx % ndev;
+    }
     h->device = device;
-    hipError_t e = hipSetDevice(device);
+    e = hipSetDevice(device);
     if (e != hipSuccess) {
         delete h;
         return hip_fail(e, "hipSetDevice");
@@ -1112,6 +1136,83 @@ int adlbq_tq_add(adlbq_server *h, int app_rank, int work_type, int server_rank) 
     hipSetDevice(h->device);
     k_add_bytes<<<1, 1, 0, h->stream>>>(h->d_ctr, BYTES_TQ);  // tq_node_create (adlb.c:1176)
     AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
+int adlbq_tq_dec(adlbq_server *h, int app_rank, int work_type, int server_rank) {
+    if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_tq_dec");
+    for (size_t i = 0; i + 3 < h->tq.size(); i += 4)
+        if (h->tq[i] == app_rank && h->tq[i + 1] == work_type && h->tq[i + 2] == server_rank) {
+            if (--h->tq[i + 3] <= 0) {  // tq_delete (adlb.c:1942-1945, 2081-2083)
+                h->tq.erase(h->tq.begin() + (long)i, h->tq.begin() + (long)i + 4);
+                hipSetDevice(h->device);
+                k_add_bytes<<<1, 1, 0, h->stream>>>(h->d_ctr, -BYTES_TQ);
+                AQ_HIP(hipGetLastError());
+            }
+            h->tq_dirty = true;
+            return ADLBQ_OK;
+        }
+    return ADLBQ_OK;
+}
+
+int adlbq_rfr_failed(adlbq_server *h, int donor_rank, int for_rank, const int *types16) {
+    if (!ok_handle(h) || !types16) return fail(ADLBQ_ERR_ARG, "adlbq_rfr_failed");
+    const int idx = donor_rank - h->master;
+    if (idx < 0 || idx >= h->S) return fail(ADLBQ_ERR_ARG, "adlbq_rfr_failed: donor is not a server rank");
+    // a wildcard first entry stands for every declared type (adlb.c:1973-1978)
+    std::vector<int> list;
+    if (types16[0] < 0) list.assign(h->utypes.begin(), h->utypes.end());
+    else
+        for (int i = 0; i < NREQ && types16[i] >= 0; i++) list.push_back(types16[i]);
+    for (int v : list) {
+        int t = -1;
+        for (int j = 0; j < h->T; j++)
+            if (h->utypes[j] == v) t = j;
+        if (t < 0) continue;  // the reference prints "invalid type" and indexes out of bounds
+        h->qm_hi[(size_t)idx * h->T + t] = LOWEST;
+        h->qm_dirty = true;
+        // every tq record of (for_rank, donor, type) loses one unit (adlb.c:1988-2004)
+        for (size_t i = 0; i + 3 < h->tq.size();) {
+            if (h->tq[i] == for_rank && h->tq[i + 2] == donor_rank && h->tq[i + 1] == v && --h->tq[i + 3] <= 0) {
+                h->tq.erase(h->tq.begin() + (long)i, h->tq.begin() + (long)i + 4);
+                hipSetDevice(h->device);
+                k_add_bytes<<<1, 1, 0, h->stream>>>(h->d_ctr, -BYTES_TQ);
+                AQ_HIP(hipGetLastError());
+                h->tq_dirty = true;
+                continue;
+            }
+            if (h->tq[i] == for_rank && h->tq[i + 2] == donor_rank && h->tq[i + 1] == v) h->tq_dirty = true;
+            i += 4;
+        }
+    }
+    return ADLBQ_OK;
+}
+
+int adlbq_rfr_retry(adlbq_server *h, int rqseqno, int *found, int *donor_rank) {
+    if (!ok_handle(h) || !found || !donor_rank) return fail(ADLBQ_ERR_ARG, "adlbq_rfr_retry");
+    hipSetDevice(h->device);
+    int rc;
+    if ((rc = sync_tables(h))) return rc;
+    k_rfr_retry<<<1, 64, 0, h->stream>>>(donor_ctx(h), h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
+                                         rqseqno - 1, h->d_result);
+    AQ_HIP(hipGetLastError());
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 2, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *found = h->h_result[0];
+    *donor_rank = h->h_result[1];
+    return ADLBQ_OK;
+}
+
+int adlbq_unit_target(adlbq_server *h, int wqseqno, int *target_rank) {
+    if (!ok_handle(h) || !target_rank) return fail(ADLBQ_ERR_ARG, "adlbq_unit_target");
+    long long slot;
+    *target_rank = -1;
+    if (!find_slot(h, wqseqno, &slot)) return fail(ADLBQ_ERR_ARG, "adlbq_unit_target: no such unit");
+    hipSetDevice(h->device);
+    const char *p = reinterpret_cast<const char *>(h->d_cold1 + slot) + 3 * sizeof(int);  // cold1.w
+    AQ_HIP(hipMemcpyAsync(h->h_result, p, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *target_rank = h->h_result[0];
     return ADLBQ_OK;
 }
 

@@ -46,7 +46,8 @@ typedef struct adlbq_server adlbq_server;
 /* Replaces the per-server queue setup of ADLBP_Init (src/adlb.c:295-320:
  * wq/rq/iq/tq/cq = xq_create(), qmstat_tbl rows = LOWEST, next_wqseqno = 1,
  * next_rqseqno = 1, rfr_to_rank = -1, rfr_out = 0).  max_units is a sizing hint
- * for HBM (the store grows on demand).  device = HIP device ordinal. */
+ * for HBM (the store grows on demand).  device = HIP device ordinal, or -1
+ * for my_server_idx modulo the visible devices. */
 int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_app_ranks,
                  int num_servers, int my_server_idx, long long max_units, int device);
 int adlbq_destroy(adlbq_server *h);
@@ -127,6 +128,25 @@ int adlbq_tq_add(adlbq_server *h, int app_rank, int work_type, int server_rank);
 
 /* Remove a parked Reserve by rqseqno (rq_find_seqno + rq_delete, adlb.c:1883-1933). */
 int adlbq_rq_delete(adlbq_server *h, int rqseqno, int *found);
+
+/* tq_find_rtr + num_stored-- (delete at 0): SS_RFR_RESP for a targeted unit
+ * (adlb.c:1935-1947) and SS_MOVING_TARGETED_WORK (2077-2084). */
+int adlbq_tq_dec(adlbq_server *h, int app_rank, int work_type, int server_rank);
+
+/* SS_RFR_RESP failure (adlb.c:1971-2005): the donor's qmstat row gets
+ * type_hi_prio = LOWEST for every type of the request (a wildcard first entry
+ * = every declared type) and each tq record (for_rank, donor, type) loses one
+ * unit.  types16 = the request's req_types as the SS_RFR_RESP echoes them. */
+int adlbq_rfr_failed(adlbq_server *h, int donor_rank, int for_rank, const int *types16);
+
+/* The retry that follows (adlb.c:2007-2041): if rqseqno is still parked
+ * (*found = 1), its first type with a donor gets a new SS_RFR: *donor_rank =
+ * that server (rfr_to_rank / rfr_out set) or -1. */
+int adlbq_rfr_retry(adlbq_server *h, int rqseqno, int *found, int *donor_rank);
+
+/* target_rank of a live unit (kept through a pin): the prev_target field of the
+ * donor's SS_RFR_RESP (adlb.c:1824, 1837).  ADLBQ_ERR_ARG if no such unit. */
+int adlbq_unit_target(adlbq_server *h, int wqseqno, int *target_rank);
 
 /* ---- steal round: replaces the SS_RFR / SS_RFR_RESP round
  * trips (adlb.c:1280-1308, 1802-1933, 3536-3579) between co-resident servers

@@ -1,0 +1,61 @@
+"""CPU checks of the ADLB server library (no GPU calls): libadlb.so exports the
+whole public API the reference's libadlb.a does, the core
+binding matches its header, and the recorded config-1 fixtures are
+self-consistent."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from nq_fixture import Fixture, normalise
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBADLB = os.path.join(ROOT, "adlb_amd", "libadlb.so")
+HEADER = os.path.join(ROOT, "include", "adlb", "adlb.h")
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+
+
+def test_libadlb_exports_public_api():
+    if not os.path.exists(LIBADLB):
+        pytest.skip("libadlb.so not built")
+    exp = _exports(LIBADLB)
+    declared = set(re.findall(r"^int\s+(ADLBP?_\w+)\s*\(", open(HEADER).read(), re.M))
+    # the symbols the reference's examples and adlb_prof.c reach besides the header
+    extra = {"adlbp_dbgprintf", "adlbp_Reserve", "adlbp_Get_reserved_timed", "adlbp_Probe", "adlb_Probe",
+             "dmalloc", "dfree", "pmalloc"}
+    missing = sorted((declared | extra) - exp)
+    assert not missing, missing
+
+
+def test_core_binding_covers_header():
+    from adlb_amd import core
+    txt = open(core.HEADER).read()
+    declared = set(re.findall(r"\b(adlbsrv_[a-z_0-9]+)\s*\(", txt)) - {"adlbsrv_emit_fn"}
+    assert declared == set(core.SIGNATURES)
+    if os.path.exists(core.LIB_PATH):
+        assert declared <= _exports(core.LIB_PATH)
+
+
+@pytest.mark.parametrize("name", ["nq_np4_n8.npz", "nq_np6_n9_s2_r4.npz", "nq_np6_n9_s2_r5.npz"])
+def test_nq_fixture_consistent(name):
+    fx = Fixture(os.path.join(GOLD, name))
+    kinds = [e[0] for e in fx.events]
+    exp = fx.expected()
+    # every Put is acked twice (header, done), every Get answered with an ack and its payload
+    puts, gets, res = kinds.count("put"), kinds.count("get"), kinds.count("reserve")
+    acks = [x for x in exp if x[2] == 1020]
+    assert len([a for a in acks if a[0] == "put"]) == 2 * puts
+    assert len([x for x in exp if x[2] == 1010]) == gets
+    # every Reserve is answered exactly once (immediately, by a Put, by exhaustion)
+    assert len([x for x in exp if x[2] == 1008]) == res
+    got_units = [normalise(*x)[2][5] for x in exp if x[2] == 1008 and normalise(*x)[2][0] == 1]
+    assert len(got_units) == len(set(got_units)) == gets
+    assert kinds.count("exhausted") == 1
+    assert fx.types.tolist() == [1000, 2000, 3000]
