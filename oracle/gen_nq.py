@@ -9,6 +9,8 @@ fixture under tests/golden/:
   nq_np4_n8.npz        mpirun -np 4 nq -n 8 -q                (1 server, 92 solutions)
   nq_np6_n9_s2_r4.npz  mpirun -np 6 nq -n 9 -q -nservers 2    (server rank 4 of 2, 352)
   nq_np6_n9_s2_r5.npz  ... server rank 5
+  mix_np6_s2_r{4,5}.npz, mix_np7_s3_r{4,5,6}.npz   tests/apps/adlb_mix.c on the reference
+                       library: steals, targeted work, a common-prefix batch
 
 Fixture = the server's inbound events in the order its loop handled them and
 every reply it sent, attributed to the event that caused it:
@@ -96,7 +98,7 @@ def events_of(recs):
     return ev, ex
 
 
-def write_fixture(path, ev, ex, A, S, me):
+def write_fixture(path, ev, ex, A, S, me, types=NQ_TYPES, max_malloc=NQ_MAX_MALLOC):
     def pack(chunks):
         off = np.zeros(len(chunks), np.int64)
         ln = np.zeros(len(chunks), np.int64)
@@ -108,28 +110,28 @@ def write_fixture(path, ev, ex, A, S, me):
     eo, el, eb = pack([e[2] for e in ev])
     xo, xl, xb = pack([x[3] for x in ex])
     np.savez_compressed(
-        path, meta=np.array([len(NQ_TYPES), A, S, me, NQ_MAX_MALLOC], np.int64),
-        types=np.array(NQ_TYPES, np.int32),
+        path, meta=np.array([len(types), A, S, me, max_malloc], np.int64),
+        types=np.array(types, np.int32),
         ev_kind=np.array([KINDS[e[0]] for e in ev], np.int8), ev_src=np.array([e[1] for e in ev], np.int32),
         ev_off=eo, ev_len=el, ev_blob=eb,
         ex_ev=np.array([x[0] for x in ex], np.int32), ex_dest=np.array([x[1] for x in ex], np.int32),
         ex_tag=np.array([x[2] for x in ex], np.int32), ex_off=xo, ex_len=xl, ex_blob=xb)
 
 
-def run_case(np_, args, servers, name):
-    subprocess.run(["make", "-s", "-C", HERE, "nqref"], check=True)
+def run_case(np_, args, servers, name, exe="nq", types=NQ_TYPES, max_malloc=NQ_MAX_MALLOC):
+    subprocess.run(["make", "-s", "-C", HERE, "nqref" if exe == "nq" else f"_ref/{exe}"], check=True)
     with tempfile.TemporaryDirectory() as d:
         env = dict(os.environ, ADLB_MSGLOG_DIR=d)
-        r = subprocess.run(["/opt/conda/bin/mpirun", "-np", str(np_), os.path.join(HERE, "_ref", "nq"), *args],
+        r = subprocess.run(["/opt/conda/bin/mpirun", "-np", str(np_), os.path.join(HERE, "_ref", exe), *args],
                            env=env, capture_output=True, text=True, timeout=300)
-        found = [ln for ln in r.stdout.splitlines() if ln.startswith("found")]
+        found = [ln for ln in r.stdout.splitlines() if ln.startswith(("found", "adlb_mix"))]
         print(name, found)
         A = np_ - len(servers)
         for s in servers:
             ev, ex = events_of(parse_log(os.path.join(d, f"rank{s}.bin")))
             suffix = f"_r{s}" if len(servers) > 1 else ""
             path = os.path.join(OUT, f"{name}{suffix}.npz")
-            write_fixture(path, ev, ex, A, len(servers), s)
+            write_fixture(path, ev, ex, A, len(servers), s, types, max_malloc)
             print(f"  {path}: {len(ev)} events, {len(ex)} replies")
         return found
 
@@ -139,6 +141,10 @@ def main():
         sys.exit("needs the reference sources (build container only)")
     run_case(4, ["-n", "8", "-q"], [3], "nq_np4_n8")
     run_case(6, ["-n", "9", "-q", "-nservers", "2"], [4, 5], "nq_np6_n9_s2")
+    # tests/apps/adlb_mix.c: steals (SS_RFR / SS_RFR_RESP / SS_UNRESERVE), targeted units,
+    # a common-prefix batch, Ireserve and info queries (types 11, 22, 33, 44; hi 1e8)
+    run_case(6, ["-nservers", "2", "-n", "200"], [4, 5], "mix_np6_s2", "mix", [11, 22, 33, 44], 100000000)
+    run_case(7, ["-nservers", "3", "-n", "150"], [4, 5, 6], "mix_np7_s3", "mix", [11, 22, 33, 44], 100000000)
 
 
 if __name__ == "__main__":

@@ -22,14 +22,26 @@ from nq_fixture import Fixture, compare, replay
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
-FIXTURES = ["nq_np4_n8.npz", "nq_np6_n9_s2_r4.npz", "nq_np6_n9_s2_r5.npz"]
+FIXTURES = sorted(f for f in os.listdir(GOLD) if f.startswith(("nq_", "mix_")))
+MIX = os.path.join(ROOT, "tests", "apps", "adlb_mix")
 NQ_AMD = os.path.join(ROOT, "oracle", "_ref", "nq_amd")
 MPIRUN = "/opt/conda/bin/mpirun"
 
 
+# The reference zeroes rfr_out only for app ranks (adlb.c:339-340: the loop runs
+# to num_app_ranks over an array of num_world_nodes), so a server's entries for
+# the other servers are uninitialised heap.  In the recorded 3-server mix run
+# server rank 4 read them as non-zero and never sent an SS_RFR (the job ended
+# by exhaustion with 100 units unconsumed); this implementation zeroes them,
+# and its replay of that stream steals where the reference could not.
+REF_UB = {"mix_np7_s3_r4.npz"}
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch", [True, False])
-@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("name", [pytest.param(f, marks=pytest.mark.xfail(reason="reference reads uninitialised "
+                                                                        "rfr_out (adlb.c:339-340)", strict=False))
+                                  if f in REF_UB else f for f in FIXTURES])
 def test_nq_event_stream_replay(name, batch):
     from adlb_amd.core import Core
     fx = Fixture(os.path.join(GOLD, name))
@@ -60,3 +72,37 @@ def test_nq_one_server_92():
 def test_nq_two_servers_352():
     out = _run_nq(6, ["-n", "9", "-q", "-nservers", "2"])
     assert "found 352 solutions" in out, out[-2000:]
+
+
+def _run_mix(np_, args, timeout=240):
+    if not os.path.exists(MIX):
+        pytest.skip("tests/apps/adlb_mix not built")
+    env = dict(os.environ, ADLB_DEVICE="0")
+    r = subprocess.run([MPIRUN, "-np", str(np_), MIX, *args], env=env, capture_output=True, text=True,
+                       timeout=timeout)
+    assert r.returncode == 0, f"rc={r.returncode}\nstdout:\n{r.stdout[-3000:]}\nstderr:\n{r.stderr[-3000:]}"
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("adlb_mix:")]
+    assert line, r.stdout[-2000:]
+    v = line[0].split()
+    return r.stdout, (int(v[2]), int(v[4])), (int(v[6]), int(v[7]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("np_,ns,n", [(6, 2, 200), (7, 3, 150), (10, 4, 300)])
+def test_mix_every_unit_once(np_, ns, n):
+    """Steals, targeted units, a common-prefix batch: every unit is consumed
+    exactly once before exhaustion (the reference run of the 3-server case
+    declares exhaustion with units left; see oracle/gen_nq.py)."""
+    out, got, exp = _run_mix(np_, ["-nservers", str(ns), "-n", str(n)])
+    assert got == exp, out[-2000:]
+
+
+@pytest.mark.gpu
+def test_mix_put_rejection_walk():
+    """hi_malloc small enough that servers reject puts: the client walks the
+    servers (ADLB_PUT_REJECTED hints), targeted units land away from their
+    home server (FA_DID_PUT_AT_REMOTE + tq) and are still all consumed."""
+    out, got, exp = _run_mix(6, ["-nservers", "2", "-n", "100", "-len", "2000", "-hi", "120000"])
+    assert got == exp, out[-2000:]
+    rej = [float(ln.split()[-1]) for ln in out.splitlines() if ln.startswith("server")]
+    assert rej and sum(rej) > 0, out[-2000:]
