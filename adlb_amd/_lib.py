@@ -48,6 +48,14 @@ SIGNATURES = {
     "adlbq_steal_check": (c_int, [P, P, P]),
     "adlbq_steal_merge": (c_int, [c_int, c_int, P, c_int, P, P, P, c_int, P, P, P]),
     "adlbq_grant_batch": (c_int, [P, c_int, P, P]),
+    "adlbq_steal_group_create": (c_int, [P, P, c_int, c_int, c_int]),
+    "adlbq_steal_group_blob_ints": (c_ll, [P]),
+    "adlbq_steal_group_export": (c_int, [P, P]),
+    "adlbq_steal_group_settle": (c_int, [P, P, c_int, P, P]),
+    "adlbq_steal_group_responses": (c_int, [P, c_int, P, P]),
+    "adlbq_steal_group_grants": (c_int, [P, c_int, P, P]),
+    "adlbq_steal_group_check": (c_int, [P, P, P]),
+    "adlbq_steal_group_destroy": (c_int, [P]),
     "adlbq_rq_delete_batch": (c_int, [P, c_int, P, P]),
     "adlbq_push_select": (c_int, [P, c_double, P, P]),
     "adlbq_info": (c_int, [P, P, P, P]),

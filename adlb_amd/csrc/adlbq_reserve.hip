@@ -409,7 +409,8 @@ __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ candlen, int *__restrict__ candoff_out,
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
     const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
-    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv, int R) {
+    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
+    unsigned char *__restrict__ rtype, int R) {
     constexpr int RT = TB <= RANK_FAST_T ? TB : 1;  // types of the fast ranking
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
@@ -625,7 +626,8 @@ __global__ __launch_bounds__(256) void k_select_open(
                         g += lb[u];
                     }
                     crank[at] = ((unsigned int)g << 6) | (unsigned int)t;
-                    // level rows, sampled every LV_STEP ranks (the chain's guess interpolates)
+                    if (lv != nullptr && g < R) rtype[g] = (unsigned char)t;
+                    // level rows, sampled every LV_STEP ranks (rtype completes them between samples)
                     if (lv != nullptr && (g & (LV_STEP - 1)) == 0 && g < R)
 #pragma unroll
                         for (int u = 0; u < RT; u++)
@@ -1211,8 +1213,9 @@ __device__ __forceinline__ int lower_bound_key(const unsigned long long *L, int 
 // of each type ranked before it -- the lower bounds k_rank computes anyway --
 // i.e. the state in which the first g candidates in preference order are taken.
 struct LevelRows {
-    int *lv;  // [R][T], or nullptr (T > 8)
+    int *lv;              // [R][T], or nullptr (T > 8)
     int R;
+    unsigned char *rtype;  // [R] type of the candidate at rank g (with lv)
 };
 
 struct RankSort {
@@ -1389,6 +1392,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
             __syncthreads();
         }
         if (tid < n) crank[soff[t] + i0 + tid] = (g << 6) | (unsigned int)t;
+        if (lr.lv != nullptr && tid < n && (int)g < lr.R) lr.rtype[g] = (unsigned char)t;
         if (lr.lv != nullptr && tid < n && (int)g < lr.R && (g & (LV_STEP - 1)) == 0) {
 #pragma unroll
             for (int u = 0; u < 8; u++)
@@ -1446,6 +1450,7 @@ struct ChainArgs {
     unsigned long long *counters;    // [CH_GROUPS + 1] two-level arrival counters (zero between launches)
     DevCounters *ctr;
     const int *lv;                   // [R][T] k_rank's level rows (T <= 8), else nullptr
+    const unsigned char *rtype;      // [R] type index of the candidate at each global rank (with lv)
     unsigned long long *stamps;      // [nseg][8] s_memrealtime per phase (diagnostic build of the run), or nullptr
 };
 
@@ -1999,10 +2004,17 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
         const int G = __builtin_amdgcn_readlane(my_off, T);
         // the row at the sampled rank below J, the rest spread in proportion to the list lengths
         const int Js = J & ~(LV_STEP - 1);
+        // ranks [Js, J): one type byte per lane, counted per type (LV_STEP == 64)
+        const int tt = (Js + lane < J && Js + lane < G) ? (int)a.rtype[Js + lane] : 255;
+        int extra = 0;
+#pragma unroll
+        for (int q = 0; q < (TB <= 8 ? TB : 8); q++) {
+            const int c = __popcll(__ballot(tt == q));
+            if (lane == q) extra = c;
+        }
         guess = lane >= T || J == 0 ? 0
                 : J >= G            ? my_len
-                                    : min(my_len, (Js ? a.lv[(long long)(Js / LV_STEP) * T + lane] : 0) +
-                                                      (int)((long long)(J - Js) * my_len / max(G, 1)));
+                                    : min(my_len, (Js ? a.lv[(long long)(Js / LV_STEP) * T + lane] : 0) + extra);
     } else {
         guess = level_guess<(TB <= 8 ? TB : 8)>(a, J);
     }
@@ -2332,7 +2344,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipStreamSynchronize(h->stream));
     void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
                   h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht,
-                  h->d_chcnt, h->d_chE, h->d_chflag, h->d_pmask, h->d_lv};
+                  h->d_chcnt, h->d_chE, h->d_chflag, h->d_pmask, h->d_lv, h->d_rtype};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
@@ -2357,6 +2369,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     // the last arriver of every chain launch re-zeroes them
     AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 1)));
     AQ_HIP(hipMalloc((void **)&h->d_lv, sizeof(int) * 8 * (size_t)nc));
+    AQ_HIP(hipMalloc((void **)&h->d_rtype, (size_t)nc + 64));
     h->cap_req = nc;
     return ADLBQ_OK;
 }
@@ -2435,7 +2448,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
             h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr,
-            (sort || !h->rank_in_select) ? nullptr : h->d_crank, (!sort && T <= 8) ? h->d_lv : nullptr, R);
+            (sort || !h->rank_in_select) ? nullptr : h->d_crank, (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R);
         stage_end(h, "select", ev);
         if (sort) {  // a reserve batch sorts inside k_rank
             stage_begin(h, "sort", &ev);
@@ -2774,7 +2787,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         // (every loop is grid-strided: any grid is correct, the hint only sizes it)
         k_rank<<<rank_hint(h) ? 64 : 512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
                                     (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
-                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R}, h->d_ctr);
+                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr);
         stage_end(h, "rank", ev);
     }
     stage_begin(h, "chain", &ev);
@@ -2795,7 +2808,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, warm, gs, h->d_candoff, h->d_candlen, h->d_crank,
                      h->d_umatch, h->d_cht, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chS + nsT, h->d_chD + nsT,
                      h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_chcnt, h->d_ctr,
-                     (T <= 8 && np > 0) ? h->d_lv : nullptr, nullptr};
+                     (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr};
         if (h->chain_stamps) {
             if (nseg > h->cap_stamps) {
                 AQ_HIP(hipStreamSynchronize(s));

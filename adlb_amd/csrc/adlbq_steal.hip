@@ -188,7 +188,110 @@ struct HeadTree {
 inline int key_prio(unsigned long long k) { return (int)((unsigned int)(k >> 32) ^ 0x80000000u); }
 inline int key_shard(unsigned long long k) { return (int)(0xffffffffu - (unsigned int)k); }
 
+struct ShardView {
+    const int *recs;          // [T][k][8]
+    const int *nrec;          // [T]
+    const long long *navail;  // [T]
+};
+
 }  // namespace
+
+// the merge over S shards' exports, each given by a view (adlbq_steal_merge)
+static int merge_views(int S, int T, const int *user_types, int k, const ShardView *vw, int nreq, const int *reqs19,
+                       int *out3, int *n_decided) {
+    for (int r = 0; r < nreq; r++) {
+        const int *q = reqs19 + (size_t)r * 19;
+        if (q[0] < 0 || q[0] >= S) return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: shard index out of range");
+        if (r && (q[0] < q[-19] || (q[0] == q[-19] && q[1] <= q[-18])))
+            return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: requests not in (shard, rqseqno) order");
+    }
+    for (int s = 0; s < S; s++)
+        for (int t = 0; t < T; t++)
+            if (!vw[s].nrec || vw[s].nrec[t] < 0 || vw[s].nrec[t] > k || vw[s].navail[t] < vw[s].nrec[t])
+                return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: bad record counts (or a shard index without export)");
+    auto tindex = [&](int v) {
+        for (int t = 0; t < T; t++)
+            if (user_types[t] == v) return t;
+        return -1;
+    };
+    std::vector<int> head((size_t)S * T, 0), unk_cnt(T, 0);
+    std::vector<char> unk((size_t)S * T, 0);
+    std::vector<HeadTree> tree(T);
+    auto rec = [&](int s, int t, int i) { return vw[s].recs + ((size_t)t * k + i) * 8; };
+    // a list past its exported records is LOWEST when the shard had no more, else unknown
+    auto refresh = [&](int s, int t) {
+        const size_t st = (size_t)s * T + t;
+        const bool more = head[st] < vw[s].nrec[t];
+        const bool u = !more && vw[s].navail[t] > vw[s].nrec[t];
+        if (u && !unk[st]) unk_cnt[t]++;
+        unk[st] = u;
+        tree[t].set(s, more ? rec(s, t, head[st])[0] : LOWEST);
+    };
+    for (int t = 0; t < T; t++) {
+        tree[t].init(S);
+        for (int s = 0; s < S; s++) refresh(s, t);
+    }
+    int r = 0;
+    for (; r < nreq; r++) {
+        const int *q = reqs19 + (size_t)r * 19;
+        const int me = q[0];
+        const int *types = q + 3;
+        int *o = out3 + (size_t)r * 3;
+        o[0] = o[1] = o[2] = -1;
+        bool stop = false;
+        int donor = -1;
+        for (int e = 0; e < NREQ && donor < 0 && !stop; e++) {
+            const int v = types[e];
+            if (v < -1) break;
+            unsigned long long best = 0;
+            if (v == -1) {
+                for (int t = 0; t < T && !stop; t++) {
+                    stop = unk_cnt[t] - unk[(size_t)me * T + t] > 0;
+                    best = std::max(best, tree[t].except(me, S));
+                }
+            } else {
+                const int t = tindex(v);
+                if (t < 0) continue;  // undeclared type: no donor (the reference reads out of bounds)
+                stop = unk_cnt[t] - unk[(size_t)me * T + t] > 0;
+                best = tree[t].except(me, S);
+            }
+            // ties between types of one shard keep the lower shard (key order)
+            if (!stop && best && key_prio(best) > LOWEST) donor = key_shard(best);
+        }
+        if (stop) break;
+        if (donor < 0) continue;
+        // the donor's best unit over the request's whole type set
+        unsigned long long set = 0;
+        for (int e = 0; e < NREQ; e++) {
+            const int v = types[e];
+            if (v == -1) set = T == 64 ? ~0ull : ((1ull << T) - 1);
+            else {
+                const int t = tindex(v);
+                if (t >= 0) set |= 1ull << t;
+            }
+        }
+        int bt = -1, bp = LOWEST, bs = INT_MAX;
+        for (int t = 0; t < T && !stop; t++) {
+            if (!((set >> t) & 1)) continue;
+            const size_t st = (size_t)donor * T + t;
+            if (unk[st]) stop = true;
+            else if (head[st] < vw[donor].nrec[t]) {
+                const int *x = rec(donor, t, head[st]);
+                if (x[0] > bp || (x[0] == bp && x[1] < bs)) bt = t, bp = x[0], bs = x[1];
+            }
+        }
+        if (stop) break;
+        if (bt < 0) return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: donor without a unit (inconsistent records)");
+        o[0] = donor;
+        o[1] = bt;
+        o[2] = head[(size_t)donor * T + bt]++;
+        refresh(donor, bt);
+    }
+    *n_decided = r;
+    for (int i = r; i < nreq; i++) out3[3 * i] = out3[3 * i + 1] = out3[3 * i + 2] = -1;
+    return ADLBQ_OK;
+}
+
 
 static int ensure_steal_buffers(adlbq_server *h, int k, int rqcap) {
     const int T = h->T;
@@ -402,101 +505,228 @@ int adlbq_rq_delete_batch(adlbq_server *h, int n, const int *rqseqnos, int *foun
     return refresh_counters(h);
 }
 
+// ---------------------------------------------------------------- steal group
+// The steal round for the shards one process holds, without a per-shard host
+// round trip: every shard's export lands in one device blob (region per
+// shard), the blobs of all processes are gathered by the caller (RCCL) or
+// used as they are, one copy brings them to pinned host memory, the merge
+// runs here, and each local shard gets its grants / deletions enqueued on its
+// own stream (no synchronisation; adlbq_steal_group_check reads the counters).
+}  // extern "C"
+
+struct adlbq_steal_group {
+    std::vector<adlbq_server *> sh;
+    int n = 0, k = 0, T = 0, rqcap = 0;
+    long long off_recs = 0, off_nrec = 0, off_nav = 0, off_rq = 0, blob = 0;
+    int *d_own = nullptr;       // the local blob when the caller passes none
+    int *d_last = nullptr;      // where the last export went
+    int *h_all = nullptr;       // pinned copy of the gathered blobs
+    long long cap_h = 0;
+    std::vector<hipEvent_t> ev;
+    std::vector<int> reqs, out3, resp;  // merge scratch; resp [m][15] of the last settle
+    std::vector<std::vector<int>> grants, dels;
+};
+
+namespace {
+__global__ void k_group_hdr(int *region, int idx) { region[0] = idx; }
+}  // namespace
+
+extern "C" {
+
+int adlbq_steal_group_create(adlbq_steal_group **out, adlbq_server **shards, int n, int k, int rqcap) {
+    if (!out || !shards || n < 1 || k < 1 || rqcap < 0) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_create");
+    for (int j = 0; j < n; j++)
+        if (!shards[j] || shards[j]->T != shards[0]->T || shards[j]->device != shards[0]->device ||
+            shards[j]->utypes != shards[0]->utypes || shards[j]->S != shards[0]->S)
+            return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_create: shards differ in types, device or server count");
+    auto *g = new adlbq_steal_group();
+    g->sh.assign(shards, shards + n);
+    g->n = n, g->k = k, g->T = shards[0]->T, g->rqcap = rqcap;
+    const long long T = g->T;
+    g->off_recs = 2;                                  // [0] shard index, [1] pad
+    g->off_nrec = g->off_recs + T * k * 8;            // launch_export writes nrec right after the records
+    g->off_nav = (g->off_nrec + T + 1) & ~1ll;        // 8-byte aligned long long navail[T]
+    g->off_rq = g->off_nav + 2 * T;                   // count, then rqcap x 18
+    g->blob = (g->off_rq + 1 + 18ll * rqcap + 63) & ~63ll;
+    hipSetDevice(shards[0]->device);
+    g->ev.resize((size_t)n);
+    for (auto &e : g->ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            delete g;
+            return fail(ADLBQ_ERR_HIP, "adlbq_steal_group_create: hipEventCreate");
+        }
+    *out = g;
+    return ADLBQ_OK;
+}
+
+long long adlbq_steal_group_blob_ints(adlbq_steal_group *g) { return g ? g->blob * g->n : -1; }
+
+int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
+    if (!g) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_export");
+    hipSetDevice(g->sh[0]->device);
+    if (!d_blob) {
+        if (!g->d_own) AQ_HIP(hipMalloc((void **)&g->d_own, sizeof(int) * g->blob * g->n));
+        d_blob = g->d_own;
+    }
+    g->d_last = d_blob;
+    for (int j = 0; j < g->n; j++) {
+        adlbq_server *h = g->sh[(size_t)j];
+        int *r = d_blob + (size_t)j * g->blob;
+        // every SS_RFR of this shard's parks is answered by the round (adlb.c:1877-1878)
+        k_rfr_reset<<<(std::max(h->A, h->num_world) + 255) / 256, 256, 0, h->stream>>>(h->d_rfr_to_rank, h->A,
+                                                                                       h->d_rfr_out, h->num_world);
+        k_group_hdr<<<1, 1, 0, h->stream>>>(r, h->my_idx);
+        int rc;
+        if (g->T && (rc = launch_export(h, g->k, r + g->off_recs, reinterpret_cast<long long *>(r + g->off_nav))))
+            return rc;
+        if (h->rq_cap > 0 && g->rqcap > 0)
+            k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, g->rqcap,
+                                                    r + g->off_rq);
+        else
+            AQ_HIP(hipMemsetAsync(r + g->off_rq, 0, sizeof(int), h->stream));
+        AQ_HIP(hipGetLastError());
+        AQ_HIP(hipEventRecord(g->ev[(size_t)j], h->stream));
+    }
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, int *n_decided, int *n_settled) {
+    if (!g || nproc < 1 || (nproc > 1 && !d_all)) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle");
+    adlbq_server *h0 = g->sh[0];
+    hipSetDevice(h0->device);
+    if (!d_all) d_all = g->d_last;
+    if (!d_all) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle: no export");
+    const long long total = g->blob * g->n * nproc;
+    if (total > g->cap_h) {
+        if (g->h_all) AQ_HIP(hipHostFree(g->h_all));
+        AQ_HIP(hipHostMalloc((void **)&g->h_all, sizeof(int) * total, hipHostMallocDefault));
+        g->cap_h = total;
+    }
+    for (int j = 0; j < g->n; j++) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
+    AQ_HIP(hipMemcpyAsync(g->h_all, d_all, sizeof(int) * total, hipMemcpyDeviceToHost, h0->stream));
+    AQ_HIP(hipStreamSynchronize(h0->stream));
+    const int S = h0->S, T = g->T, nreg = g->n * nproc;
+    std::vector<ShardView> vw((size_t)S, ShardView{nullptr, nullptr, nullptr});
+    std::vector<int> local_of((size_t)S, -1);
+    for (int j = 0; j < g->n; j++) local_of[(size_t)g->sh[(size_t)j]->my_idx] = j;
+    g->reqs.clear();
+    for (int r = 0; r < nreg; r++) {
+        const int *b = g->h_all + (size_t)r * g->blob;
+        const int idx = b[0];
+        if (idx < 0 || idx >= S || vw[(size_t)idx].nrec) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle: bad or repeated shard index");
+        vw[(size_t)idx] = ShardView{b + g->off_recs, b + g->off_nrec, reinterpret_cast<const long long *>(b + g->off_nav)};
+        const int *rq = b + g->off_rq;
+        const int c = std::min(rq[0], g->rqcap);  // entries past rqcap wait for the next round
+        for (int i = 0; i < c; i++) {
+            g->reqs.push_back(idx);
+            g->reqs.insert(g->reqs.end(), rq + 1 + 18 * (size_t)i, rq + 1 + 18 * (size_t)i + 18);
+        }
+    }
+    const int nreq = (int)(g->reqs.size() / 19);
+    // (shard, rqseqno) order: regions come in any order, each region's rq in FIFO order
+    {
+        std::vector<int> ord((size_t)nreq);
+        for (int i = 0; i < nreq; i++) ord[(size_t)i] = i;
+        const int *q = g->reqs.data();
+        std::sort(ord.begin(), ord.end(), [q](int a, int b) {
+            return q[19 * (size_t)a] != q[19 * (size_t)b] ? q[19 * (size_t)a] < q[19 * (size_t)b]
+                                                          : q[19 * (size_t)a + 1] < q[19 * (size_t)b + 1];
+        });
+        std::vector<int> sorted((size_t)nreq * 19);
+        for (int i = 0; i < nreq; i++)
+            std::memcpy(&sorted[19 * (size_t)i], q + 19 * (size_t)ord[(size_t)i], sizeof(int) * 19);
+        g->reqs.swap(sorted);
+    }
+    g->out3.assign(3 * (size_t)nreq, -1);
+    int nd = 0, rc;
+    if (nreq && (rc = merge_views(S, T, h0->utypes.data(), g->k, vw.data(), nreq, g->reqs.data(), g->out3.data(), &nd)))
+        return rc;
+    g->grants.assign((size_t)g->n, {});
+    g->dels.assign((size_t)g->n, {});
+    g->resp.clear();
+    int won = 0;
+    for (int i = 0; i < nd; i++) {
+        const int d = g->out3[3 * (size_t)i];
+        if (d < 0) continue;
+        won++;
+        const int *q = &g->reqs[19 * (size_t)i];
+        const int *u = vw[(size_t)d].recs + ((size_t)g->out3[3 * (size_t)i + 1] * g->k + g->out3[3 * (size_t)i + 2]) * 8;
+        if (local_of[(size_t)d] >= 0) {  // donor side: pin for the requesting rank (adlb.c:1820-1824)
+            auto &gr = g->grants[(size_t)local_of[(size_t)d]];
+            gr.push_back(q[2]);
+            gr.push_back(u[1]);
+        }
+        const int lj = local_of[(size_t)q[0]];
+        if (lj >= 0) {  // requester side: rq_delete + the reply to the app (adlb.c:1884-1933)
+            g->dels[(size_t)lj].push_back(q[1]);
+            const int r15[15] = {q[0], q[1], q[2], 1, u[2], u[0], u[3], u[4], u[1], h0->master + d, u[5], u[6], u[7],
+                                 -1, -1};
+            g->resp.insert(g->resp.end(), r15, r15 + 15);
+        }
+    }
+    for (int j = 0; j < g->n; j++) {
+        const auto &gr = g->grants[(size_t)j];
+        const auto &dl = g->dels[(size_t)j];
+        if ((rc = adlbq_steal_apply(g->sh[(size_t)j], (int)(gr.size() / 2), gr.data(), (int)dl.size(), dl.data())))
+            return rc;
+    }
+    if (n_decided) *n_decided = nd;
+    if (n_settled) *n_settled = won;
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_group_responses(adlbq_steal_group *g, int cap, int *out15, int *count) {
+    if (!g || !count || cap < 0 || (cap && !out15)) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_responses");
+    const int m = (int)(g->resp.size() / 15);
+    if (out15) std::memcpy(out15, g->resp.data(), sizeof(int) * 15 * (size_t)std::min(m, cap));
+    *count = m;
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_group_grants(adlbq_steal_group *g, int cap, int *out3, int *count) {
+    if (!g || !count || cap < 0 || (cap && !out3)) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_grants");
+    int m = 0;
+    for (int j = 0; j < g->n && g->grants.size() == (size_t)g->n; j++) {
+        const auto &gr = g->grants[(size_t)j];
+        for (size_t i = 0; i + 1 < gr.size(); i += 2, m++)
+            if (m < cap) out3[3 * m] = j, out3[3 * m + 1] = gr[i], out3[3 * m + 2] = gr[i + 1];
+    }
+    *count = m;
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_group_check(adlbq_steal_group *g, int *bad_grants, int *bad_deletes) {
+    if (!g || !bad_grants || !bad_deletes) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_check");
+    *bad_grants = *bad_deletes = 0;
+    for (auto *h : g->sh) {
+        int a = 0, b = 0, rc;
+        if ((rc = adlbq_steal_check(h, &a, &b))) return rc;
+        *bad_grants += a;
+        *bad_deletes += b;
+    }
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_group_destroy(adlbq_steal_group *g) {
+    if (!g) return ADLBQ_OK;
+    hipSetDevice(g->sh[0]->device);
+    for (auto *h : g->sh) hipStreamSynchronize(h->stream);
+    for (auto &e : g->ev) hipEventDestroy(e);
+    if (g->d_own) hipFree(g->d_own);
+    if (g->h_all) hipHostFree(g->h_all);
+    delete g;
+    return ADLBQ_OK;
+}
+
 int adlbq_steal_merge(int S, int T, const int *user_types, int k, const int *recs8, const int *nrec,
                       const long long *navail, int nreq, const int *reqs19, int *out3, int *n_decided) {
     if (S < 1 || T < 0 || T > ADLBQ_MAX_TYPES || k < 0 || nreq < 0 || !n_decided ||
         (T && (!user_types || !nrec || !navail || (k && !recs8))) || (nreq && (!reqs19 || !out3)))
         return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: bad argument");
-    for (int r = 0; r < nreq; r++) {
-        const int *q = reqs19 + (size_t)r * 19;
-        if (q[0] < 0 || q[0] >= S) return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: shard index out of range");
-        if (r && (q[0] < q[-19] || (q[0] == q[-19] && q[1] <= q[-18])))
-            return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: requests not in (shard, rqseqno) order");
-    }
-    for (int i = 0; i < S * T; i++)
-        if (nrec[i] < 0 || nrec[i] > k || navail[i] < nrec[i])
-            return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: bad record counts");
-    auto tindex = [&](int v) {
-        for (int t = 0; t < T; t++)
-            if (user_types[t] == v) return t;
-        return -1;
-    };
-    std::vector<int> head((size_t)S * T, 0), unk_cnt(T, 0);
-    std::vector<char> unk((size_t)S * T, 0);
-    std::vector<HeadTree> tree(T);
-    auto rec = [&](int s, int t, int i) { return recs8 + (((size_t)s * T + t) * k + i) * 8; };
-    // a list past its exported records is LOWEST when the shard had no more, else unknown
-    auto refresh = [&](int s, int t) {
-        const size_t st = (size_t)s * T + t;
-        const bool more = head[st] < nrec[st];
-        const bool u = !more && navail[st] > nrec[st];
-        if (u && !unk[st]) unk_cnt[t]++;
-        unk[st] = u;
-        tree[t].set(s, more ? rec(s, t, head[st])[0] : LOWEST);
-    };
-    for (int t = 0; t < T; t++) {
-        tree[t].init(S);
-        for (int s = 0; s < S; s++) refresh(s, t);
-    }
-    int r = 0;
-    for (; r < nreq; r++) {
-        const int *q = reqs19 + (size_t)r * 19;
-        const int me = q[0];
-        const int *types = q + 3;
-        int *o = out3 + (size_t)r * 3;
-        o[0] = o[1] = o[2] = -1;
-        bool stop = false;
-        int donor = -1;
-        for (int e = 0; e < NREQ && donor < 0 && !stop; e++) {
-            const int v = types[e];
-            if (v < -1) break;
-            unsigned long long best = 0;
-            if (v == -1) {
-                for (int t = 0; t < T && !stop; t++) {
-                    stop = unk_cnt[t] - unk[(size_t)me * T + t] > 0;
-                    best = std::max(best, tree[t].except(me, S));
-                }
-            } else {
-                const int t = tindex(v);
-                if (t < 0) continue;  // undeclared type: no donor (the reference reads out of bounds)
-                stop = unk_cnt[t] - unk[(size_t)me * T + t] > 0;
-                best = tree[t].except(me, S);
-            }
-            // ties between types of one shard keep the lower shard (key order)
-            if (!stop && best && key_prio(best) > LOWEST) donor = key_shard(best);
-        }
-        if (stop) break;
-        if (donor < 0) continue;
-        // the donor's best unit over the request's whole type set
-        unsigned long long set = 0;
-        for (int e = 0; e < NREQ; e++) {
-            const int v = types[e];
-            if (v == -1) set = T == 64 ? ~0ull : ((1ull << T) - 1);
-            else {
-                const int t = tindex(v);
-                if (t >= 0) set |= 1ull << t;
-            }
-        }
-        int bt = -1, bp = LOWEST, bs = INT_MAX;
-        for (int t = 0; t < T && !stop; t++) {
-            if (!((set >> t) & 1)) continue;
-            const size_t st = (size_t)donor * T + t;
-            if (unk[st]) stop = true;
-            else if (head[st] < nrec[st]) {
-                const int *x = rec(donor, t, head[st]);
-                if (x[0] > bp || (x[0] == bp && x[1] < bs)) bt = t, bp = x[0], bs = x[1];
-            }
-        }
-        if (stop) break;
-        if (bt < 0) return fail(ADLBQ_ERR_ARG, "adlbq_steal_merge: donor without a unit (inconsistent records)");
-        o[0] = donor;
-        o[1] = bt;
-        o[2] = head[(size_t)donor * T + bt]++;
-        refresh(donor, bt);
-    }
-    *n_decided = r;
-    for (int i = r; i < nreq; i++) out3[3 * i] = out3[3 * i + 1] = out3[3 * i + 2] = -1;
-    return ADLBQ_OK;
+    std::vector<ShardView> v((size_t)S);
+    for (int s = 0; s < S; s++)
+        v[(size_t)s] = ShardView{recs8 + (size_t)s * T * k * 8, nrec + (size_t)s * T, navail + (size_t)s * T};
+    return merge_views(S, T, user_types, k, v.data(), nreq, reqs19, out3, n_decided);
 }
 
 }  // extern "C"

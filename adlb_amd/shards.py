@@ -249,3 +249,82 @@ def steal_round(servers, k: int, group=None, timing=None):
     local = {srv.my_server_idx: srv for srv in servers}
     return settle(local, servers[0].num_app_ranks, servers[0].user_types, k, recs, nrec, navail,
                   np.concatenate(allreqs), timing)
+
+
+# ------------------------------------------------------------------ steal group
+class StealGroup:
+    """The steal round of the shards this process holds, in the library
+    (adlbq_steal_group_*): one device blob for every shard's export, an
+    optional all-gather of the blobs over RCCL (device buffers end to end),
+    one copy to pinned memory, the merge and the per-shard grants / deletions
+    without a per-shard synchronisation."""
+
+    def __init__(self, servers, k: int, rqcap: int = 4096):
+        self.lib = _lib.load()
+        self.servers = list(servers)
+        arr = (ctypes.c_void_p * len(self.servers))(*[s.h.value for s in self.servers])
+        g = ctypes.c_void_p()
+        _lib.check(self.lib.adlbq_steal_group_create(ctypes.byref(g), arr, len(self.servers), int(k), int(rqcap)),
+                   "adlbq_steal_group_create")
+        self.g = g
+        self.blob_ints = int(self.lib.adlbq_steal_group_blob_ints(g))
+        self._dblob = None
+        self._gathered = None
+
+    def round(self, group=None, timing=None):
+        """One steal round.  Single process: the local blob is merged as it is;
+        with a process group: the blobs are all-gathered (device tensors) first.
+        Returns (decided, settled) over all shards."""
+        import torch
+        import torch.distributed as dist
+        t0 = time.perf_counter()
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        if multi and self._dblob is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            self._dblob = torch.empty(self.blob_ints, dtype=torch.int32, device=dev)
+            w = dist.get_world_size(group)
+            self._gathered = torch.empty(w * self.blob_ints, dtype=torch.int32, device=dev)
+        _lib.check(self.lib.adlbq_steal_group_export(self.g, self._dblob.data_ptr() if multi else None),
+                   "adlbq_steal_group_export")
+        d_all, nproc = None, 1
+        if multi:
+            # the export runs on the shards' streams: the collective's stream waits for them
+            for s in self.servers:
+                s.sync()
+            dist.all_gather_into_tensor(self._gathered, self._dblob, group=group)
+            torch.cuda.current_stream().synchronize()
+            d_all, nproc = self._gathered.data_ptr(), dist.get_world_size(group)
+        t0 = _tick(timing, "export", t0)
+        nd, ns = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_group_settle(self.g, d_all, nproc, ctypes.byref(nd), ctypes.byref(ns)),
+                   "adlbq_steal_group_settle")
+        _tick(timing, "merge_apply", t0)
+        return nd.value, ns.value
+
+    def responses(self) -> np.ndarray:
+        c = ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_group_responses(self.g, 0, None, ctypes.byref(c)), "responses")
+        out = np.empty((c.value, 15), np.int32)
+        if c.value:
+            _lib.check(self.lib.adlbq_steal_group_responses(self.g, c.value, out.ctypes.data, ctypes.byref(c)),
+                       "responses")
+        return out
+
+    def grants(self) -> np.ndarray:
+        """(m, 3) {local shard j, rank, wqseqno} pinned by the last round"""
+        c = ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_group_grants(self.g, 0, None, ctypes.byref(c)), "grants")
+        out = np.empty((c.value, 3), np.int32)
+        if c.value:
+            _lib.check(self.lib.adlbq_steal_group_grants(self.g, c.value, out.ctypes.data, ctypes.byref(c)), "grants")
+        return out
+
+    def check(self):
+        a, b = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_group_check(self.g, ctypes.byref(a), ctypes.byref(b)), "check")
+        return a.value, b.value
+
+    def close(self):
+        if getattr(self, "g", None):
+            self.lib.adlbq_steal_group_destroy(self.g)
+            self.g = None

@@ -34,6 +34,7 @@ import subprocess
 import sys
 import tempfile
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -64,6 +65,8 @@ def parse():
     ap.add_argument("--c3-reserves", type=int, default=8192, help="config 3: Reserves per shard per step")
     ap.add_argument("--c3-k", type=int, default=1024, help="config 3: exported units per type per shard")
     ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--c3-rqcap", type=int, default=4096, help="config 3: parked Reserves per shard a round considers")
+    ap.add_argument("--c3-threads", type=int, default=0, help="config 3: enqueue the shards' batches from threads")
     ap.add_argument("--c3-warmup", type=int, default=3, help="config 3: untimed steps (rq and export buffers grow)")
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
@@ -215,24 +218,42 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     torch.cuda.synchronize()
     keep, parts, sparts = [], {"batches": 0.0, "steal": 0.0, "unreserve": 0.0}, {}
 
+    group = shards.StealGroup(srvs, k, rqcap=args.c3_rqcap)
+    pool = ThreadPoolExecutor(max_workers=len(srvs)) if args.c3_threads else None
+
+    class Res:
+        def __init__(self, decided, settled):
+            self.decided, self.settled = decided, settled
+
+    def enqueue(j, b):
+        srvs[j].reserve_batch_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
+
     def step(b, timed_parts=False):
         t0 = time.perf_counter()
-        for j, srv in enumerate(srvs):
-            srv.reserve_batch_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
+        if pool is not None:
+            list(pool.map(lambda j: enqueue(j, b), range(len(srvs))))
+        else:
+            for j in range(len(srvs)):
+                enqueue(j, b)
         if timed_parts:
+            parts["batches_enqueue"] = parts.get("batches_enqueue", 0.0) + time.perf_counter() - t0
             torch.cuda.synchronize()
         t1 = time.perf_counter()
         tm = sparts if timed_parts else None
-        res = shards.steal_round(srvs, k, timing=tm) if world > 1 else shards.steal_round_local(srvs, k, timing=tm)
+        nd, ns = group.round(timing=tm)
         t2 = time.perf_counter()
+        g = group.grants()
         for j, srv in enumerate(srvs):
             srv.unreserve_resp_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
-            g = res.grants.get(srv.my_server_idx)
-            if g is not None and g.size:
-                # pinned staging, free again: the last round's steal_check synchronised this stream
-                m = g.shape[0]
+            mine = g[g[:, 0] == j]
+            if mine.shape[0]:
+                # pinned staging, free again: the previous round's copy from it has completed
+                m = mine.shape[0]
+                if m > g_host[j].shape[0]:
+                    g_host[j] = torch.empty((2 * m, 3), dtype=torch.int32).pin_memory()
+                    g_dev[j] = torch.empty((2 * m, 3), dtype=torch.int32, device=dev)
                 hb = g_host[j].numpy()
-                hb[:m, :2] = g
+                hb[:m, :2] = mine[:, 1:]
                 hb[:m, 2] = -1
                 with torch.cuda.stream(streams[j]):
                     g_dev[j][:m].copy_(g_host[j][:m], non_blocking=True)
@@ -242,7 +263,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
             parts["batches"] += t1 - t0
             parts["steal"] += t2 - t1
             parts["unreserve"] += time.perf_counter() - t2
-        return res
+        return Res(nd, ns)
 
     for b in range(W3):                  # warm-up
         step(b)
@@ -286,6 +307,11 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
                               if args.c3_parts else None),
         "scaling": "weak",
     }
+    bg, bd = group.check()
+    out["steal_check"] = {"bad_grants": bg, "bad_deletes": bd}
+    group.close()
+    if pool is not None:
+        pool.shutdown()
     for srv in srvs:
         srv.close()
     return out

@@ -209,6 +209,31 @@ int adlbq_rq_delete_batch(adlbq_server *h, int n, const int *rqseqnos, int *foun
 int adlbq_steal_apply(adlbq_server *h, int ngrant, const int *pairs2, int ndel, const int *rqseqnos);
 int adlbq_steal_check(adlbq_server *h, int *bad_grants, int *bad_deletes);
 
+/* ---- the steal round of the shards one process holds, with
+ * no per-shard host round trip.  _create: n handles on one device (same types
+ * and server count), k records per type, at most rqcap parked Reserves per
+ * shard per round (later ones wait for the next round).  _export enqueues, on
+ * each shard's stream, the SS_RFR_RESP reset, the top-k scan and the rq
+ * compaction into one device blob of _blob_ints ints (region j = shard j;
+ * d_blob = NULL: an internal buffer).  The caller may all-gather the blobs of
+ * nproc processes (RCCL) into d_all = [nproc][blob]; _settle then copies
+ * d_all (NULL: the local blob, nproc = 1) to pinned memory once, runs the
+ * merge of adlbq_steal_merge over every shard in it, and enqueues each local
+ * shard's grants and rq deletions (adlbq_steal_apply) without synchronising.
+ * _responses: the replies of the local Reserves the round settled, rows
+ * {shard, rqseqno, rank, TA_RESERVE_RESP[12]}; _check: adlbq_steal_check
+ * summed over the shards (synchronises). */
+typedef struct adlbq_steal_group adlbq_steal_group;
+int adlbq_steal_group_create(adlbq_steal_group **g, adlbq_server **shards, int n, int k, int rqcap);
+long long adlbq_steal_group_blob_ints(adlbq_steal_group *g);
+int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob);
+int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, int *n_decided, int *n_settled);
+int adlbq_steal_group_responses(adlbq_steal_group *g, int cap, int *out15, int *count);
+/* the units the local shards pinned in the last settle: rows {local shard j, rank, wqseqno} */
+int adlbq_steal_group_grants(adlbq_steal_group *g, int cap, int *out3, int *count);
+int adlbq_steal_group_check(adlbq_steal_group *g, int *bad_grants, int *bad_deletes);
+int adlbq_steal_group_destroy(adlbq_steal_group *g);
+
 /* Memory-pressure push choice (src/adlb.c:513-528): the first unpinned unit
  * (wq_find_unpinned, xq.c:266-281) and the server with the smallest
  * nbytes_used below threshold (strict <, lowest index wins).  -1 when none. */

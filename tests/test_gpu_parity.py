@@ -21,7 +21,9 @@ from exact_check import check_batch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
 
 pytestmark = pytest.mark.gpu
-GOLD = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+# server event streams (nq_*, mix_*: oracle/gen_nq.py) are replayed by test_gpu_server.py
+GOLD = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
+              if not os.path.basename(p).startswith(("nq_", "mix_")))
 
 
 def run_abi(ut, cfg, trace, max_units=1 << 16, params=None, stats=None):

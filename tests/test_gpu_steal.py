@@ -18,14 +18,31 @@ from steal_case import build_case, rounds
 pytestmark = pytest.mark.gpu
 
 
-def _run(S, n_units, R, seed, k, **kw):
+class _GroupRound:
+    """adlbq_steal_group_* (the in-library round the bench times) as a round function."""
+
+    def __init__(self, srvs, k):
+        self.g = shards.StealGroup(srvs, k, rqcap=1 << 14)
+
+    def __call__(self):
+        nd, ns = self.g.round()
+        assert self.g.check() == (0, 0)
+        return shards.StealResult(self.g.responses(), nd, ns, {})
+
+
+def _run(S, n_units, R, seed, k, path="host", **kw):
     ws, orcs, resps = build_case(S, n_units, R, seed, **kw)
     srvs = [Server(w.user_types, w.num_app_ranks, S, s, max_units=w.n_units) for s, w in enumerate(ws)]
+    grp = None
     try:
         for s, (w, srv) in enumerate(zip(ws, srvs)):
             out = synth.split_outputs(replay.replay(srv, synth.workload_trace(w)))
             np.testing.assert_array_equal(np.asarray(out[w.n_units:], np.int32), resps[s])
-        got = rounds(lambda: shards.steal_round_local(srvs, k=k))
+        if path == "group":
+            grp = _GroupRound(srvs, k)
+            got = rounds(grp)
+        else:
+            got = rounds(lambda: shards.steal_round_local(srvs, k=k))
         exp = oracle.serial_steal_round(orcs, ws[0].num_app_ranks)
         assert exp.shape[0] > 0
         np.testing.assert_array_equal(got, exp)
@@ -52,22 +69,30 @@ def _run(S, n_units, R, seed, k, **kw):
                                  synth.simple_events(synth.OP_CHECKREM), synth.simple_events(synth.OP_INFO)])
             np.testing.assert_array_equal(replay.replay(srv, tr), orcs[s].replay(tr))
     finally:
+        if grp is not None:
+            grp.g.close()
         for srv in srvs:
             srv.close()
 
 
+PATHS = ["host", "group"]
+
+
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("S,k", [(2, 4096), (3, 4096), (4, 3)])
-def test_steal_round_vs_oracle(gpu_available, S, k):
-    _run(S, n_units=3000, R=512, seed=40 + S, k=k)
+def test_steal_round_vs_oracle(gpu_available, S, k, path):
+    _run(S, n_units=3000, R=512, seed=40 + S, k=k, path=path)
 
 
-def test_steal_round_ties_small_k(gpu_available):
-    _run(3, n_units=2000, R=512, seed=47, k=2, prio_hi=4)
+@pytest.mark.parametrize("path", PATHS)
+def test_steal_round_ties_small_k(gpu_available, path):
+    _run(3, n_units=2000, R=512, seed=47, k=2, path=path, prio_hi=4)
 
 
-def test_steal_round_config3_medium(gpu_available):
+@pytest.mark.parametrize("path", PATHS)
+def test_steal_round_config3_medium(gpu_available, path):
     """Config 3 shape at reduced size: 10% of Reserves have no local type."""
-    _run(4, n_units=50_000, R=2048, seed=3, k=1024, p_remote=0.1, prio_hi=1024)
+    _run(4, n_units=50_000, R=2048, seed=3, k=1024, path=path, p_remote=0.1, prio_hi=1024)
 
 
 def test_steal_export_matches_scan(gpu_available):
