@@ -55,6 +55,8 @@ SIGNATURES = {
     "adlbq_steal_group_responses": (c_int, [P, c_int, P, P]),
     "adlbq_steal_group_grants": (c_int, [P, c_int, P, P]),
     "adlbq_steal_group_check": (c_int, [P, P, P]),
+    "adlbq_steal_group_unreserve_grants": (c_int, [P]),
+    "adlbq_steal_group_stat": (c_ll, [P, c_char_p]),
     "adlbq_steal_group_destroy": (c_int, [P]),
     "adlbq_rq_delete_batch": (c_int, [P, c_int, P, P]),
     "adlbq_push_select": (c_int, [P, c_double, P, P]),

@@ -38,7 +38,9 @@
 #include "adlbq_impl.h"
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <string>
 #include <cstring>
 
 using namespace adlbq;
@@ -70,10 +72,11 @@ __global__ void k_grant(const int *__restrict__ pairs, int n, const long long *_
     if (bad && (threadIdx.x & 63) == 0 && b) atomicAdd(bad, __popcll(b));
 }
 
-__global__ void k_rfr_reset(int *rfr_to_rank, int A, int *rfr_out, int nworld) {
+__global__ void k_rfr_reset(int *rfr_to_rank, int A, int *rfr_out, int nworld, int *hdr = nullptr, int idx = 0) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < A) rfr_to_rank[i] = -1;
     if (i < nworld) rfr_out[i] = 0;
+    if (hdr && i == 0) hdr[0] = idx;  // a steal group region's shard index
 }
 
 // rq_find_seqno + rq_delete for many rqseqnos (adlb.c:1883, 1933)
@@ -264,6 +267,7 @@ static int merge_views(int S, int T, const int *user_types, int k, const ShardVi
         unsigned long long set = 0;
         for (int e = 0; e < NREQ; e++) {
             const int v = types[e];
+            if (v < -1) break;  // padding: the client fills every entry after the list's end with -2
             if (v == -1) set = T == 64 ? ~0ull : ((1ull << T) - 1);
             else {
                 const int t = tindex(v);
@@ -525,11 +529,10 @@ struct adlbq_steal_group {
     std::vector<hipEvent_t> ev;
     std::vector<int> reqs, out3, resp;  // merge scratch; resp [m][15] of the last settle
     std::vector<std::vector<int>> grants, dels;
+    int *h_unr = nullptr, *d_unr = nullptr;  // SS_UNRESERVE staging of the grants
+    long long cap_unr = 0;
+    long long ns_copy = 0, ns_merge = 0, ns_apply = 0, nreq_last = 0;  // the last settle's host phases
 };
-
-namespace {
-__global__ void k_group_hdr(int *region, int idx) { region[0] = idx; }
-}  // namespace
 
 extern "C" {
 
@@ -573,9 +576,8 @@ int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
         adlbq_server *h = g->sh[(size_t)j];
         int *r = d_blob + (size_t)j * g->blob;
         // every SS_RFR of this shard's parks is answered by the round (adlb.c:1877-1878)
-        k_rfr_reset<<<(std::max(h->A, h->num_world) + 255) / 256, 256, 0, h->stream>>>(h->d_rfr_to_rank, h->A,
-                                                                                       h->d_rfr_out, h->num_world);
-        k_group_hdr<<<1, 1, 0, h->stream>>>(r, h->my_idx);
+        k_rfr_reset<<<(std::max(std::max(h->A, h->num_world), 1) + 255) / 256, 256, 0, h->stream>>>(
+            h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world, r, h->my_idx);
         int rc;
         if (g->T && (rc = launch_export(h, g->k, r + g->off_recs, reinterpret_cast<long long *>(r + g->off_nav))))
             return rc;
@@ -602,9 +604,12 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
         AQ_HIP(hipHostMalloc((void **)&g->h_all, sizeof(int) * total, hipHostMallocDefault));
         g->cap_h = total;
     }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     for (int j = 0; j < g->n; j++) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
     AQ_HIP(hipMemcpyAsync(g->h_all, d_all, sizeof(int) * total, hipMemcpyDeviceToHost, h0->stream));
     AQ_HIP(hipStreamSynchronize(h0->stream));
+    const auto t1 = clk::now();
     const int S = h0->S, T = g->T, nreg = g->n * nproc;
     std::vector<ShardView> vw((size_t)S, ShardView{nullptr, nullptr, nullptr});
     std::vector<int> local_of((size_t)S, -1);
@@ -641,6 +646,7 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
     int nd = 0, rc;
     if (nreq && (rc = merge_views(S, T, h0->utypes.data(), g->k, vw.data(), nreq, g->reqs.data(), g->out3.data(), &nd)))
         return rc;
+    const auto t2 = clk::now();
     g->grants.assign((size_t)g->n, {});
     g->dels.assign((size_t)g->n, {});
     g->resp.clear();
@@ -670,9 +676,56 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
         if ((rc = adlbq_steal_apply(g->sh[(size_t)j], (int)(gr.size() / 2), gr.data(), (int)dl.size(), dl.data())))
             return rc;
     }
+    const auto t3 = clk::now();
+    g->ns_copy = std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    g->ns_merge = std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+    g->ns_apply = std::chrono::duration_cast<std::chrono::nanoseconds>(t3 - t2).count();
+    g->nreq_last = nreq;
     if (n_decided) *n_decided = nd;
     if (n_settled) *n_settled = won;
     return ADLBQ_OK;
+}
+
+int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g) {
+    if (!g) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_unreserve_grants");
+    if (g->grants.size() != (size_t)g->n) return ADLBQ_OK;
+    long long total = 0;
+    for (const auto &gr : g->grants) total += (long long)(gr.size() / 2);
+    if (!total) return ADLBQ_OK;
+    hipSetDevice(g->sh[0]->device);
+    if (3 * total > g->cap_unr) {
+        for (auto *h : g->sh) AQ_HIP(hipStreamSynchronize(h->stream));
+        if (g->h_unr) AQ_HIP(hipHostFree(g->h_unr));
+        if (g->d_unr) AQ_HIP(hipFree(g->d_unr));
+        g->cap_unr = std::max(3 * total, 2 * g->cap_unr);
+        AQ_HIP(hipHostMalloc((void **)&g->h_unr, sizeof(int) * g->cap_unr, hipHostMallocDefault));
+        AQ_HIP(hipMalloc((void **)&g->d_unr, sizeof(int) * g->cap_unr));
+    }
+    // the staging is free: the previous round's copies completed before this round's settle returned
+    long long off = 0;
+    for (int j = 0; j < g->n; j++) {
+        const auto &gr = g->grants[(size_t)j];
+        const int m = (int)(gr.size() / 2);
+        if (!m) continue;
+        int *hb = g->h_unr + off;
+        for (int i = 0; i < m; i++) hb[3 * i] = gr[2 * (size_t)i], hb[3 * i + 1] = gr[2 * (size_t)i + 1], hb[3 * i + 2] = -1;
+        adlbq_server *h = g->sh[(size_t)j];
+        AQ_HIP(hipMemcpyAsync(g->d_unr + off, hb, sizeof(int) * 3 * (size_t)m, hipMemcpyHostToDevice, h->stream));
+        int rc;
+        if ((rc = adlbq_unreserve_batch_device(h, m, g->d_unr + off))) return rc;
+        off += 3ll * m;
+    }
+    return ADLBQ_OK;
+}
+
+long long adlbq_steal_group_stat(adlbq_steal_group *g, const char *name) {
+    if (!g || !name) return -1;
+    const std::string n(name);
+    if (n == "copy_ns") return g->ns_copy;
+    if (n == "merge_ns") return g->ns_merge;
+    if (n == "apply_ns") return g->ns_apply;
+    if (n == "requests") return g->nreq_last;
+    return -1;
 }
 
 int adlbq_steal_group_responses(adlbq_steal_group *g, int cap, int *out15, int *count) {
@@ -714,6 +767,8 @@ int adlbq_steal_group_destroy(adlbq_steal_group *g) {
     for (auto &e : g->ev) hipEventDestroy(e);
     if (g->d_own) hipFree(g->d_own);
     if (g->h_all) hipHostFree(g->h_all);
+    if (g->h_unr) hipHostFree(g->h_unr);
+    if (g->d_unr) hipFree(g->d_unr);
     delete g;
     return ADLBQ_OK;
 }

@@ -319,6 +319,12 @@ class StealGroup:
             _lib.check(self.lib.adlbq_steal_group_grants(self.g, c.value, out.ctypes.data, ctypes.byref(c)), "grants")
         return out
 
+    def unreserve_grants(self):
+        _lib.check(self.lib.adlbq_steal_group_unreserve_grants(self.g), "adlbq_steal_group_unreserve_grants")
+
+    def stat(self, name: str) -> int:
+        return int(self.lib.adlbq_steal_group_stat(self.g, name.encode()))
+
     def check(self):
         a, b = ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.adlbq_steal_group_check(self.g, ctypes.byref(a), ctypes.byref(b)), "check")

@@ -64,10 +64,10 @@ def parse():
     ap.add_argument("--c3-units", type=int, default=1_562_500, help="config 3: units per server shard")
     ap.add_argument("--c3-reserves", type=int, default=8192, help="config 3: Reserves per shard per step")
     ap.add_argument("--c3-k", type=int, default=1024, help="config 3: exported units per type per shard")
-    ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--c3-steps", type=int, default=40)
     ap.add_argument("--c3-rqcap", type=int, default=4096, help="config 3: parked Reserves per shard a round considers")
     ap.add_argument("--c3-threads", type=int, default=0, help="config 3: enqueue the shards' batches from threads")
-    ap.add_argument("--c3-warmup", type=int, default=3, help="config 3: untimed steps (rq and export buffers grow)")
+    ap.add_argument("--c3-warmup", type=int, default=8, help="config 3: untimed steps (rq and export buffers grow)")
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
@@ -193,7 +193,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     S, T = SL * world, 4
     W3 = max(1, args.c3_warmup)
     nb = args.c3_steps + W3
-    srvs, streams, d_reqs, d_resp, g_host, g_dev = [], [], [], [], [], []
+    srvs, streams, d_reqs, d_resp = [], [], [], []
     for j in range(SL):
         idx = rank * SL + j
         w = synth.config3_shard(idx, S, N, T, R, seed=args.seed)
@@ -211,8 +211,6 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         with torch.cuda.stream(st):
             d_reqs.append(torch.from_numpy(reqs).to(dev))
             d_resp.append(torch.empty((nb, R, 12), dtype=torch.int32, device=dev))
-            g_host.append(torch.empty((R, 3), dtype=torch.int32).pin_memory())
-            g_dev.append(torch.empty((R, 3), dtype=torch.int32, device=dev))
         srvs.append(srv)
         streams.append(st)
     torch.cuda.synchronize()
@@ -242,22 +240,12 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         tm = sparts if timed_parts else None
         nd, ns = group.round(timing=tm)
         t2 = time.perf_counter()
-        g = group.grants()
         for j, srv in enumerate(srvs):
             srv.unreserve_resp_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
-            mine = g[g[:, 0] == j]
-            if mine.shape[0]:
-                # pinned staging, free again: the previous round's copy from it has completed
-                m = mine.shape[0]
-                if m > g_host[j].shape[0]:
-                    g_host[j] = torch.empty((2 * m, 3), dtype=torch.int32).pin_memory()
-                    g_dev[j] = torch.empty((2 * m, 3), dtype=torch.int32, device=dev)
-                hb = g_host[j].numpy()
-                hb[:m, :2] = mine[:, 1:]
-                hb[:m, 2] = -1
-                with torch.cuda.stream(streams[j]):
-                    g_dev[j][:m].copy_(g_host[j][:m], non_blocking=True)
-                srv.unreserve_batch_device(m, g_dev[j].data_ptr())
+        group.unreserve_grants()
+        if timed_parts:
+            for key in ("copy_ns", "merge_ns", "apply_ns"):
+                sparts["settle_" + key[:-3]] = sparts.get("settle_" + key[:-3], 0.0) + group.stat(key) * 1e-9
         if timed_parts:
             torch.cuda.synchronize()
             parts["batches"] += t1 - t0
