@@ -55,7 +55,9 @@ def parse():
     ap.add_argument("--types", type=int, default=4)
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--equal-prio", action="store_true", help="config-2 variant: all priorities equal")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of each CPU baseline sample")
+    ap.add_argument("--cpu-cores", type=int, default=min(16, len(os.sched_getaffinity(0))),
+                    help="CPU baseline processes (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP event timing")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
@@ -155,27 +157,55 @@ def traffic_of(pmc, stage):
     return round(hits[0]) if len(hits) == 1 else None
 
 
-def cpu_baseline(w, budget_s: float) -> dict:
-    """The oracle (repo restatement of xq's linked-list scans, one core) on the
-    same queue: build it once, then time Reserves from the same batch until the
-    budget is used.  Per-Reserve cost is ~constant (pinned units are still
-    visited), so the sample rate is the rate of the whole batch."""
+def cpu_baseline(w, budget_s: float, seed: int, cores: int, equal_prio: bool = False) -> dict:
+    """The CPU baseline on the GPU box's host: the reference's
+    own src/xq.c (oracle/_ref/libxqref.so, built from /root/reference in the
+    build container; this repo's restatement oracle/liboracle.so when that is
+    absent) on the metric queue.  Per-Reserve cost is ~constant (pinned units
+    are still visited), so a sample's rate is the batch's rate.
+      value            `cores` independent processes, each with its own replica
+                       of the whole queue (aggregate Reserves/s);
+      one_core         one process, one replica;
+      sharded          the ADLB-natural split: `cores` servers with 1/cores of
+                       the units each, Reserves routed round robin;
+    ns_per_node = seconds per Reserve / (2 x units held): the reference scans
+    the list twice per Reserve (xq.c:219-247 then 190-217)."""
+    import multiprocessing as mp
     import oracle
-    from adlb_amd import synth
-    o = oracle.Oracle("own")
-    o.init(w.user_types, w.num_app_ranks)
-    o.replay(synth.put_events(w))
-    done, t0 = 0, time.perf_counter()
-    chunk = 4
-    while time.perf_counter() - t0 < budget_s and done < w.n_reserves:
-        k = min(chunk, w.n_reserves - done)
-        o.replay(synth.reserve_events(w.r_rank[done:done + k], w.r_types[done:done + k],
-                                      w.r_hang[done:done + k]))
-        done += k
-    el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "assignments/s", "cores": 1, "kind": "port",
-            "sample": f"first {done} Reserves of the step-0 batch on a {w.n_units}-unit queue "
-                      f"({el:.1f} s, oracle/liboracle.so: linked-list restatement of xq.c scans)"}
+    from oracle.baseline import sample
+    N, T, R = w.n_units, int(w.user_types.size), w.n_reserves
+
+    def pick(units):
+        # the reference build holds its queue under adlb.c's own allocation cap (max_malloc =
+        # 500 MB until ADLB_Server runs, adlb.c:218, 3439-3452): ~140 B per unit with payload
+        return "ref" if oracle.available("ref") and units * 150 < 4.5e8 else "own"
+
+    def summary(res, what, kind):
+        done = sum(r[0] for r in res)
+        rate = sum(r[0] / r[1] for r in res if r[1] > 0)
+        per = [r[1] / max(r[0], 1) / (2.0 * r[2]) * 1e9 for r in res]
+        src = ("oracle/_ref/libxqref.so (the reference's src/xq.c, compiled in the build container)" if kind == "ref"
+               else "oracle/liboracle.so (this repo's restatement of xq.c)")
+        return {"value": rate, "unit": "assignments/s", "cores": len(res), "reserves_timed": done,
+                "kind": "reference" if kind == "ref" else "port", "ns_per_node": round(float(np.median(per)), 3),
+                "sample": f"{what}; {src}"}
+
+    k1, ks = pick(N), pick(N // max(cores, 1))
+    one = summary([sample((k1, N, T, R, seed, equal_prio, 0, 1, budget_s))],
+                  f"first Reserves of the step-0 batch on the {N}-unit queue, one process, {budget_s:.0f} s", k1)
+    ctx = mp.get_context("spawn")  # this process holds the GPU: no fork
+    lim = 10 * budget_s + 300
+    with ctx.Pool(cores) as pool:
+        rep = summary(pool.map_async(sample, [(k1, N, T, R, seed, equal_prio, 0, 1, budget_s)] * cores).get(lim),
+                      f"{cores} processes x one {N}-unit replica each, {budget_s:.0f} s each", k1)
+        shd = summary(pool.map_async(sample, [(ks, N, T, R, seed, equal_prio, c, cores, budget_s)
+                                              for c in range(cores)]).get(lim),
+                      f"{cores} server processes x {N // cores} units (units and Reserves dealt round robin), "
+                      f"{budget_s:.0f} s each", ks)
+    return {"value": rep["value"], "unit": "assignments/s", "cores": cores, "kind": rep["kind"],
+            "sample": rep["sample"], "ns_per_node": rep["ns_per_node"],
+            "one_core": one, "sharded": shd,
+            "host_cpus": {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}}
 
 
 def bench_config3(args, torch, dist, world, rank, local, dev):
@@ -610,7 +640,8 @@ def main():
         except Exception as e:  # reported, not fatal
             res["config4"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
+        res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, shards.shard_seed(args.seed, rank),
+                                           args.cpu_cores, args.equal_prio)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
