@@ -194,7 +194,10 @@ struct adlbq_server {
     int *d_seg_cnt = nullptr;          // [R/64] chain: untargeted-capable requests per 64 requests
     unsigned long long *d_pmask = nullptr;  // [R/64] k_finalize: ballots of the requests that park
     int *d_lv = nullptr;               // [R][T] k_rank: level rows for the chain's guess (T <= 8)
-    unsigned char *d_rtype = nullptr;  // [R] type of the candidate at each global rank (the guess between rows)
+    unsigned char *d_rtype = nullptr;
+    int *d_pm_over = nullptr;          // k_put_match_blk: the staged rq overflowed
+    void *h_putrec = nullptr;          // pinned staging of a Put batch's records
+    hipEvent_t put_ev = nullptr;       // its copy to the device completed  // [R] type of the candidate at each global rank (the guess between rows)
     // targeted units' sorted index (k_targeted_idx): keys/vals double buffers,
     // per (bucket, type) ranges, radix-sort scratch; rebuilt after targeted Puts
     unsigned long long *d_tkeys = nullptr, *d_tkeys2 = nullptr;

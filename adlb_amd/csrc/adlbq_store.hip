@@ -324,7 +324,8 @@ __global__ void k_put_scatter(const PutRec *__restrict__ r, int n, int *prio, ui
 // (rq_find_rank_queued_for_type, xq.c:388-405, at adlb.c:988-1042)
 __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__restrict__ rq_rank,
                             const int *__restrict__ rq_types, int *rq_live, DevCounters *ctr,
-                            uint32_t *meta, int *pin, int *out3) {
+                            uint32_t *meta, int *pin, int *out3, const int *gate) {
+    if (gate && *gate == 0) return;  // k_put_match_blk handled the batch
     const int lane = threadIdx.x;
     int head = ctr->rq_head, nrq = ctr->rq_n, live = ctr->rq_live;
     for (int i = 0; i < n; i++) {
@@ -375,6 +376,119 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
     if (lane == 0) {
         ctr->rq_live = live;
         ctr->rq_head = head;
+    }
+}
+
+// The same FIFO first-fit for a batch of Puts, one workgroup of 1024: the live
+// rq entries (up to PM_CAP) are staged in LDS once as (rank, type-index mask),
+// then each Put in order is one block-wide minimum over the entries it may
+// take (rank == target when targeted, its type in the entry's set or a -1
+// anywhere in it: rq_find_rank_queued_for_type, xq.c:388-405).  *over = 1 when
+// the live entries exceed PM_CAP (the caller then runs k_put_match).
+constexpr int PM_CAP = 4096, PM_THREADS = 1024, PM_PER = PM_CAP / PM_THREADS;
+__global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__restrict__ r, int n,
+                                                              const int *__restrict__ rq_rank,
+                                                              const int *__restrict__ rq_types, int *rq_live,
+                                                              DevCounters *ctr, uint32_t *meta, int *pin, int *out3,
+                                                              const int *__restrict__ utypes, int T, int *over) {
+    __shared__ int s_rank[PM_CAP], s_k[PM_CAP];
+    __shared__ unsigned long long s_mask[PM_CAP];
+    __shared__ int s_wmin[PM_THREADS / 64], s_cnt[PM_THREADS / 64], s_tot;
+    __shared__ int s_ut[ADLBQ_MAX_TYPES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int head = ctr->rq_head, nrq = ctr->rq_n;
+    for (int t = tid; t < T; t += PM_THREADS) s_ut[t] = utypes[t];
+    if (tid == 0) s_tot = 0;
+    __syncthreads();
+    // stage the live entries in FIFO order (compaction in chunks of 1024)
+    for (int c0 = head; c0 < nrq; c0 += PM_THREADS) {
+        const int k = c0 + tid;
+        const bool live = k < nrq && ld_agent(rq_live + k);
+        const unsigned long long b = __ballot(live);
+        if (lane == 0) s_cnt[w] = __popcll(b);
+        __syncthreads();
+        int pre = s_tot;
+        for (int q = 0; q < w; q++) pre += s_cnt[q];
+        const int pos = pre + __popcll(b & lanemask_lt());
+        if (live && pos < PM_CAP) {
+            const int *tv = rq_types + (long long)k * NREQ;
+            unsigned long long m = 0;
+            bool wild = false;
+#pragma unroll
+            for (int q = 0; q < NREQ; q++) {
+                const int v = tv[q];
+                wild |= v == -1;
+                for (int t = 0; t < T; t++)
+                    if (s_ut[t] == v) {  // get_type_idx: first declared match
+                        m |= 1ull << t;
+                        break;
+                    }
+            }
+            s_rank[pos] = rq_rank[k];
+            s_mask[pos] = wild ? ~0ull : m;
+            s_k[pos] = k;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int tot = s_tot;
+            for (int q = 0; q < PM_THREADS / 64; q++) tot += s_cnt[q];
+            s_tot = tot;
+        }
+        __syncthreads();
+    }
+    const int m = s_tot;
+    if (m > PM_CAP) {  // too many parked Reserves for the staging: the caller falls back
+        if (tid == 0) *over = 1;
+        return;
+    }
+    int live = ctr->rq_live;
+    for (int i = 0; i < n; i++) {
+        const PutRec u = r[i];
+        const unsigned long long bit = 1ull << (u.meta & (int)M_TYPE);
+        int best = INT_MAX;
+#pragma unroll
+        for (int e = 0; e < PM_PER; e++) {
+            const int j = tid * PM_PER + e;  // each thread owns PM_PER consecutive entries: its first hit wins
+            if (best == INT_MAX && j < m && s_rank[j] != INT_MIN && (s_mask[j] & bit) &&
+                (u.target == -1 || u.target == s_rank[j]))
+                best = j;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, 64));
+        if (lane == 0) s_wmin[w] = best;
+        __syncthreads();
+        if (tid == 0) {
+            int b = INT_MAX;
+            for (int q = 0; q < PM_THREADS / 64; q++) b = min(b, s_wmin[q]);
+            int *o = out3 + 3 * i;
+            o[0] = u.seq;
+            o[1] = -1;
+            o[2] = -1;
+            bytes_add(ctr, BYTES_WQ + u.len);  // pmalloc + wq_node_create (adlb.c:933, 963)
+            if (b != INT_MAX) {
+                const int k = s_k[b], rk = s_rank[b];
+                s_rank[b] = INT_MIN;  // taken
+                rq_live[k] = 0;
+                o[1] = rk;
+                o[2] = k + 1;  // rqseqno == slot + 1
+                bytes_add(ctr, -BYTES_RQ);  // rq_delete (adlb.c:1040)
+                pin[u.slot] = rk;
+                if (rk >= 0) meta[u.slot] = (uint32_t)u.meta | M_PINNED;
+                live--;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        // new FIFO head: the first staged entry still live (entries before the first staged one are dead)
+        int nh = nrq;
+        for (int j = 0; j < m; j++)
+            if (s_rank[j] != INT_MIN) {
+                nh = s_k[j];
+                break;
+            }
+        ctr->rq_live = live;
+        ctr->rq_head = m ? nh : head;
     }
 }
 
@@ -793,7 +907,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
-                    h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv, h->d_rtype,
+                    h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv, h->d_rtype, h->d_pm_over,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
                     h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem};
     for (void *p : ptrs)
@@ -803,6 +917,8 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->h_steal) hipHostFree(h->h_steal);
     if (h->h_apply) hipHostFree(h->h_apply);
     if (h->h_crem) hipHostFree(h->h_crem);
+    if (h->h_putrec) hipHostFree(h->h_putrec);
+    if (h->put_ev) hipEventDestroy(h->put_ev);
     if (h->steal_ev) hipEventDestroy(h->steal_ev);
     if (h->apply_ev) hipEventDestroy(h->apply_ev);
     for (int i = 0; i < adlbq_server::NSNAP; i++)
@@ -834,8 +950,21 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
     hipSetDevice(h->device);
     for (int i = 0; i < n; i++)
         if (!h->tindex.count(units9[9 * i])) return fail(ADLBQ_ERR_TYPE, "adlbq_put_batch: undeclared work type");
-    std::vector<PutRec> rec(n);
     int rc;
+    // records are staged in pinned memory; the previous batch's copy out of it must have completed
+    if (h->put_ev) AQ_HIP(hipEventSynchronize(h->put_ev));
+    else AQ_HIP(hipEventCreateWithFlags(&h->put_ev, hipEventDisableTiming));
+    if (n > h->cap_put) {
+        AQ_HIP(hipStreamSynchronize(h->stream));
+        if (h->d_putrec) AQ_HIP(hipFree(h->d_putrec));
+        if (h->d_putout) AQ_HIP(hipFree(h->d_putout));
+        if (h->h_putrec) AQ_HIP(hipHostFree(h->h_putrec));
+        h->cap_put = std::max(n, 2 * h->cap_put);
+        AQ_HIP(hipMalloc((void **)&h->d_putrec, sizeof(PutRec) * (size_t)h->cap_put));
+        AQ_HIP(hipMalloc((void **)&h->d_putout, sizeof(int) * 3 * (size_t)h->cap_put));
+        AQ_HIP(hipHostMalloc((void **)&h->h_putrec, sizeof(PutRec) * (size_t)h->cap_put, hipHostMallocDefault));
+    }
+    PutRec *rec = reinterpret_cast<PutRec *>(h->h_putrec);
     for (int i = 0; i < n; i++) {
         const int *u = units9 + 9 * i;
         int tgt = u[3];
@@ -895,18 +1024,10 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         if ((rc = grow(&h->d_seq2slot, h->cap_seq, nc, h->stream, 0xff))) return rc;
         h->cap_seq = nc;
     }
-    // persistent staging: the records go through a pageable copy (consumed
-    // before the call returns), so only a possible rq match synchronises
-    if (n > h->cap_put) {
-        AQ_HIP(hipStreamSynchronize(h->stream));
-        if (h->d_putrec) AQ_HIP(hipFree(h->d_putrec));
-        if (h->d_putout) AQ_HIP(hipFree(h->d_putout));
-        h->cap_put = std::max(n, 2 * h->cap_put);
-        AQ_HIP(hipMalloc((void **)&h->d_putrec, sizeof(PutRec) * (size_t)h->cap_put));
-        AQ_HIP(hipMalloc((void **)&h->d_putout, sizeof(int) * 3 * (size_t)h->cap_put));
-    }
+    // only a possible rq match synchronises
     PutRec *d_rec = reinterpret_cast<PutRec *>(h->d_putrec);
-    AQ_HIP(hipMemcpyAsync(d_rec, rec.data(), sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
+    AQ_HIP(hipMemcpyAsync(d_rec, rec, sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
+    AQ_HIP(hipEventRecord(h->put_ev, h->stream));
     // a parked Reserve can only exist if the last known count, plus every
     // Reserve launched since, is positive
     bool may_match = h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0);
@@ -917,8 +1038,14 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
                                                           h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor,
                                                           h->d_rrec, h->d_ctr, add_bytes);
     if (may_match) {
+        // one workgroup over the staged rq; too many parked Reserves: the one-wave scan of the whole rq
+        if (!h->d_pm_over) AQ_HIP(hipMalloc((void **)&h->d_pm_over, sizeof(int)));
+        AQ_HIP(hipMemsetAsync(h->d_pm_over, 0, sizeof(int), h->stream));
+        k_put_match_blk<<<1, PM_THREADS, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live,
+                                                         h->d_ctr, h->d_meta, h->d_pin, h->d_putout, h->d_utypes,
+                                                         h->T, h->d_pm_over);
         k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
-                                             h->d_meta, h->d_pin, h->d_putout);
+                                             h->d_meta, h->d_pin, h->d_putout, h->d_pm_over);
         AQ_HIP(hipMemcpyAsync(out3, h->d_putout, sizeof(int) * 3 * n, hipMemcpyDeviceToHost, h->stream));
         AQ_HIP(hipGetLastError());
         if ((rc = refresh_counters(h))) return rc;

@@ -73,6 +73,11 @@ def parse():
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 stream measurement")
+    ap.add_argument("--config5-only", action="store_true", help="only the config-5 leg")
+    ap.add_argument("--c5-shards", type=int, default=8, help="config 5: server shards (own event stream each)")
+    ap.add_argument("--c5-ranks", type=int, default=512, help="config 5: app ranks per shard")
+    ap.add_argument("--c5-rounds", type=int, default=60, help="config 5: stream rounds per shard")
     ap.add_argument("--config4-only", action="store_true", help="only the config-4 leg (profiling)")
     ap.add_argument("--c4-units", type=int, default=10_000_000, help="config 4: units (80%% targeted)")
     ap.add_argument("--c4-steps", type=int, default=5)
@@ -120,7 +125,7 @@ def pmc_traffic(args) -> dict | None:
     if prof is None:
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu", "--no-pmc",
-             "--no-config3", "--no-config4",
+             "--no-config3", "--no-config4", "--no-config5",
              "--no-profile", "--units", str(args.units), "--reserves", str(args.reserves), "--types",
              str(args.types), "--seed", str(args.seed)] + (["--equal-prio"] if args.equal_prio else [])
     out = {}
@@ -351,6 +356,69 @@ def zipf_type_sets(rng, n_types, R, lo=1, hi=4):
     return out
 
 
+def bench_config5(args, torch, dist, world, rank, local, dev):
+    """Config 5: tsp.c-style branch-and-bound streams.  Each of
+    c5_shards servers has its own stream (synth.config5_stream: work Puts with
+    prio 1+len, targeted bound updates at prio 999999999, Reserves {2, 1} / {1}
+    / wildcard, Gets, unreserves, and every few rounds the qmstat rows, a
+    check_remote, tq updates, RFR completions, push choice and info queries).
+    The streams react to outcomes, so they are recorded first with the oracle
+    as the server (untimed; the GPU must give the same outcomes, checked), then
+    replayed through the C ABI in the timed region: consecutive Puts, Reserves
+    and Gets go as one batch each, every other event one call.  The same traces
+    replayed by the oracle on one core are the CPU figure.  Reports events/s."""
+    import oracle
+    from adlb_amd import replay, synth
+    from adlb_amd.server import Server
+    S, A, nr = args.c5_shards, args.c5_ranks, args.c5_rounds
+    traces, expect = [], []
+    t0 = time.perf_counter()
+    for s_ in range(S):
+        idx = rank * S + s_
+        o = oracle.Oracle("own", private=True)
+        o.init([1, 2], A, S * world, idx)
+        tr = synth.config5_stream(lambda ev: synth.split_outputs(o.replay(ev)), n_ranks=A, n_rounds=nr,
+                                  n_servers=S * world, my_idx=idx, seed=args.seed + 17 * idx,
+                                  n_seed_units=4 * A)
+        traces.append(np.ascontiguousarray(tr, dtype=np.int32))
+    gen_s = time.perf_counter() - t0
+    n_ev = [sum(a.shape[0] for _, a in replay._runs(tr, 2)) for tr in traces]
+    n_batches = [sum(1 for _ in replay._runs(tr, 2)) for tr in traces]
+    # CPU: the oracle replaying the recorded streams (one core)
+    t0 = time.perf_counter()
+    for s_, tr in enumerate(traces):
+        o = oracle.Oracle("own", private=True)
+        o.init([1, 2], A, S * world, rank * S + s_)
+        expect.append(o.replay(tr))
+    cpu_s = time.perf_counter() - t0
+    srvs = [Server([1, 2], A, S * world, rank * S + s_, max_units=1 << 16, device=local) for s_ in range(S)]
+    # warm-up: a short stream on a throwaway handle (kernels loaded, buffers sized)
+    with Server([1, 2], A, S * world, rank * S, max_units=1 << 16, device=local) as tmp:
+        replay.replay(tmp, traces[0][: min(traces[0].size, 20000)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    got = [replay.replay(srv, tr) for srv, tr in zip(srvs, traces)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    same = all(np.array_equal(g, e) for g, e in zip(got, expect))
+    total = sum(n_ev)
+    for srv in srvs:
+        srv.close()
+    if world > 1:
+        el, total = shards.reduce_step_timing(el, total)
+    return {"workload": f"config5: {S * world} server shards x a tsp-style stream ({A} ranks, {nr} rounds each: "
+                        f"{sum(n_ev)} events on this GPU in {sum(n_batches)} calls)",
+            "value": total / el, "unit": "events/s", "seconds": el, "events": total,
+            "events_per_call": round(sum(n_ev) / max(sum(n_batches), 1), 1),
+            "parity_with_oracle": bool(same),
+            "cpu_oracle_events_per_s": sum(n_ev) / cpu_s, "cpu_cores": 1,
+            "trace_generation_s": round(gen_s, 1), "scaling": "weak"}
+
+
 def bench_config4(args, torch, dist, world, rank, local, dev):
     """Config 4: c4_units units with 80% targeted (target ~
     Zipf(1.1) over 1,024 app ranks), 32 types with Zipf(1.1) popularity, prio ~
@@ -470,6 +538,13 @@ def main():
         out = bench_config4(args, torch, dist, world, rank, local, dev)
         if rank == 0:
             print(json.dumps({"config4": out}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if args.config5_only:
+        out = bench_config5(args, torch, dist, world, rank, local, dev)
+        if rank == 0:
+            print(json.dumps({"config5": out}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -639,6 +714,11 @@ def main():
             res["config4"] = bench_config4(args, torch, dist, world, rank, local, dev)
         except Exception as e:  # reported, not fatal
             res["config4"] = {"error": f"{type(e).__name__}: {e}"}
+    if not args.no_config5:
+        try:
+            res["config5"] = bench_config5(args, torch, dist, world, rank, local, dev)
+        except Exception as e:  # reported, not fatal
+            res["config5"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, shards.shard_seed(args.seed, rank),
                                            args.cpu_cores, args.equal_prio)

@@ -280,3 +280,30 @@ def test_bytes_hwm_vs_oracle(gpu_available, seed):
     tr = gen_golden.bytes_stream(seed=seed, n_events=500, kind="own", hwm=True)
     cfg = (16, 3, 1)
     assert_same(run_abi([0, 1, 2], cfg, tr), run_oracle([0, 1, 2], cfg, tr))
+
+
+@pytest.mark.parametrize("n_parked", [3000, 6000])
+def test_put_side_fifo_vs_oracle(gpu_available, n_parked):
+    """Put-side matching (FA_PUT_HDR, adlb.c:963-1046; rq_find_rank_queued_for_type,
+    xq.c:388-405) on a large rq: Reserves of 1-2 types or the wildcard park on an
+    empty queue, then batches of untargeted and targeted Puts take them first-fit
+    in FIFO order.  3000 parked: the LDS-staged block kernel; 6000: beyond its
+    4096 staging entries, the one-wave scan."""
+    rng = np.random.default_rng(n_parked)
+    ut = np.array([3, 5, 7, 9], np.int32)
+    A = 8192
+    ranks = rng.permutation(A)[:n_parked]
+    tv = synth.type_vectors(rng, ut, n_parked)
+    parts = [synth.reserve_events(ranks, tv, np.ones(n_parked, np.uint8)), synth.simple_events(synth.OP_INFO)]
+    n_put = n_parked + 500
+    w = synth.config2(n_units=n_put, n_reserves=1, seed=n_parked)
+    w.u_type[:] = ut[rng.integers(0, 4, n_put)]
+    tgt = rng.random(n_put) < 0.3
+    w.u_target[:] = np.where(tgt, ranks[rng.integers(0, n_parked, n_put)], -1)
+    w.u_target[rng.random(n_put) < 0.05] = A - 1  # targeted at a rank with nothing parked
+    for lo in range(0, n_put, 700):  # several Put batches, each one adlbq_put_batch
+        parts += [synth.put_events(w, lo, min(n_put, lo + 700)), synth.simple_events(synth.OP_INFO),
+                  synth.simple_events(synth.OP_BYTES)]
+    trace = np.concatenate(parts)
+    cfg = (A, 1, 0)
+    assert_same(run_abi(ut, cfg, trace, max_units=1 << 14), run_oracle(ut, cfg, trace))
