@@ -205,6 +205,16 @@ struct adlbq_server {
     int *d_tstart = nullptr, *d_tend = nullptr; long long cap_trange = 0;
     void *d_tsort = nullptr; size_t cap_tsort = 0;
     bool tindex_dirty = true;
+    // incremental index: entries [0, tidx_n) of d_tkeys / d_tvals are real (sorted);
+    // the keys of targeted units Put since the last build wait in tnew_*
+    long long tidx_n = 0; bool tidx_valid = false;
+    std::vector<unsigned long long> tnew_keys;
+    std::vector<int> tnew_vals;
+    unsigned long long *d_tnewk = nullptr; int *d_tnewv = nullptr; long long cap_tnew = 0;
+    long long tidx_merges = 0, tidx_rebuilds = 0;
+    std::vector<unsigned long long> tnew_sk;  // host staging of the sorted new keys / positions
+    std::vector<int> tnew_sv;
+    hipEvent_t tnew_ev = nullptr;
     // segmented radix sort of the multi-prio-bin candidate lists (launched
     // when the newest landed batch needed one; k_rank sorts otherwise)
     int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort
@@ -223,6 +233,7 @@ struct adlbq_server {
     unsigned int chain_epoch = 0;      // per batch, never 0 once used
     int chain_passes = 0;              // round 0's in-launch passes, 0 = auto (adlbq_set_param "chain_passes")
     int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
+    int put_match_block = 1, put_always_match = 0;  // diagnostics ("put_match_block", "put_always_match")
     int rank_in_select = 1;            // k_select_open ranks the candidates when it can ("rank_in_select")
     int chain_stamps = 0;              // diagnostic: phase stamps of the first chain launch ("chain_stamps")
     unsigned long long *d_stamps = nullptr; int cap_stamps = 0, n_stamps = 0;

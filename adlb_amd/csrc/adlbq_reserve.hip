@@ -30,6 +30,8 @@
 #include "adlbq_donor.h"
 #include "adlbq_impl.h"
 
+#include <rocprim/device/device_merge.hpp>
+
 using namespace adlbq;
 
 
@@ -2360,14 +2362,14 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_chLP, sizeof(int) * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * CHAIN_MAX_PASSES * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * CHAIN_MAX_PASSES * nseg));
-    AQ_HIP(hipMemset(h->d_chflag, 0, sizeof(int) * CHAIN_MAX_PASSES * nseg));  // epochs start at 1
+    AQ_HIP(hipMemsetAsync(h->d_chflag, 0, sizeof(int) * CHAIN_MAX_PASSES * nseg, h->stream));  // epochs start at 1
     AQ_HIP(hipMalloc((void **)&h->d_chGT, sizeof(int) * CH_GROUPS * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chGO, sizeof(int) * CH_GROUPS * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chclean, sizeof(int)));
     AQ_HIP(hipMalloc((void **)&h->d_cht, (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * (CH_GROUPS + 1)));
     // the last arriver of every chain launch re-zeroes them
-    AQ_HIP(hipMemset(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 1)));
+    AQ_HIP(hipMemsetAsync(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 1), h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_lv, sizeof(int) * 8 * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_rtype, (size_t)nc + 64));
     h->cap_req = nc;
@@ -2466,6 +2468,16 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
 // The targeted units' sorted index (k_targeted_idx), rebuilt after targeted
 // Puts: keys/vals over every slot of every rank-bucket page (holes sort last),
 // one stable radix sort, then the (bucket, type) ranges.
+static int tindex_ranges(adlbq_server *h, int nb) {
+    hipStream_t s = h->stream;
+    AQ_HIP(hipMemsetAsync(h->d_tstart, 0, sizeof(int) * (size_t)nb * 64, s));
+    AQ_HIP(hipMemsetAsync(h->d_tend, 0, sizeof(int) * (size_t)nb * 64, s));
+    if (h->tidx_n > 0)
+        k_tindex_ranges<<<(int)((h->tidx_n + 255) / 256), 256, 0, s>>>(h->d_tkeys, h->tidx_n, h->d_tstart, h->d_tend);
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
 static int ensure_tindex(adlbq_server *h) {
     if (!h->tindex_dirty) return ADLBQ_OK;
     hipStream_t s = h->stream;
@@ -2483,6 +2495,7 @@ static int ensure_tindex(adlbq_server *h) {
         AQ_HIP(hipMalloc((void **)&h->d_tkeys2, sizeof(unsigned long long) * h->cap_tidx));
         AQ_HIP(hipMalloc((void **)&h->d_tvals, sizeof(int) * h->cap_tidx));
         AQ_HIP(hipMalloc((void **)&h->d_tvals2, sizeof(int) * h->cap_tidx));
+        h->tidx_valid = false;  // the sorted entries were in the freed arrays
     }
     if ((long long)nb * 64 > h->cap_trange) {
         AQ_HIP(hipStreamSynchronize(s));
@@ -2492,6 +2505,58 @@ static int ensure_tindex(adlbq_server *h) {
         AQ_HIP(hipMalloc((void **)&h->d_tstart, sizeof(int) * h->cap_trange));
         AQ_HIP(hipMalloc((void **)&h->d_tend, sizeof(int) * h->cap_trange));
     }
+    const long long m = (long long)h->tnew_keys.size();
+    // incremental: the new units' keys (sorted on the host, ties kept in Put order) merged into the
+    // sorted index -- old entries first on equal keys, as their bucket positions are lower
+    if (h->tidx_valid && m > 0 && h->tidx_n + m <= h->cap_tidx && m * 4 <= h->tidx_n + 4096) {
+        if (m > h->cap_tnew) {
+            AQ_HIP(hipStreamSynchronize(s));
+            if (h->d_tnewk) AQ_HIP(hipFree(h->d_tnewk));
+            if (h->d_tnewv) AQ_HIP(hipFree(h->d_tnewv));
+            h->cap_tnew = std::max(m, 2 * h->cap_tnew);
+            AQ_HIP(hipMalloc((void **)&h->d_tnewk, sizeof(unsigned long long) * h->cap_tnew));
+            AQ_HIP(hipMalloc((void **)&h->d_tnewv, sizeof(int) * h->cap_tnew));
+        }
+        std::vector<int> ord((size_t)m);
+        for (long long i = 0; i < m; i++) ord[(size_t)i] = (int)i;
+        const auto &K = h->tnew_keys;
+        std::stable_sort(ord.begin(), ord.end(), [&K](int a, int b) { return K[(size_t)a] < K[(size_t)b]; });
+        // host staging kept until the copy has run (the event of the previous merge)
+        if (h->tnew_ev) AQ_HIP(hipEventSynchronize(h->tnew_ev));
+        else AQ_HIP(hipEventCreateWithFlags(&h->tnew_ev, hipEventDisableTiming));
+        h->tnew_sk.resize((size_t)m);
+        h->tnew_sv.resize((size_t)m);
+        for (long long i = 0; i < m; i++) {
+            h->tnew_sk[(size_t)i] = K[(size_t)ord[(size_t)i]];
+            h->tnew_sv[(size_t)i] = h->tnew_vals[(size_t)ord[(size_t)i]];
+        }
+        AQ_HIP(hipMemcpyAsync(h->d_tnewk, h->tnew_sk.data(), sizeof(unsigned long long) * m, hipMemcpyHostToDevice, s));
+        AQ_HIP(hipMemcpyAsync(h->d_tnewv, h->tnew_sv.data(), sizeof(int) * m, hipMemcpyHostToDevice, s));
+        AQ_HIP(hipEventRecord(h->tnew_ev, s));
+        size_t tmp = 0;
+        AQ_HIP(rocprim::merge(nullptr, tmp, h->d_tkeys, h->d_tnewk, h->d_tkeys2, h->d_tvals, h->d_tnewv, h->d_tvals2,
+                              (size_t)h->tidx_n, (size_t)m, rocprim::less<unsigned long long>(), s));
+        if (tmp > h->cap_tsort) {
+            AQ_HIP(hipStreamSynchronize(s));
+            if (h->d_tsort) AQ_HIP(hipFree(h->d_tsort));
+            h->cap_tsort = std::max(tmp, 2 * h->cap_tsort);
+            AQ_HIP(hipMalloc(&h->d_tsort, h->cap_tsort));
+        }
+        size_t t2 = h->cap_tsort;
+        AQ_HIP(rocprim::merge(h->d_tsort, t2, h->d_tkeys, h->d_tnewk, h->d_tkeys2, h->d_tvals, h->d_tnewv,
+                              h->d_tvals2, (size_t)h->tidx_n, (size_t)m, rocprim::less<unsigned long long>(), s));
+        std::swap(h->d_tkeys, h->d_tkeys2);
+        std::swap(h->d_tvals, h->d_tvals2);
+        h->tidx_n += m;
+        h->tidx_merges++;
+        h->tnew_keys.clear();
+        h->tnew_vals.clear();
+        int rc;
+        if ((rc = tindex_ranges(h, nb))) return rc;
+        h->tindex_dirty = false;
+        return ADLBQ_OK;
+    }
+    // full build: keys over every slot of every rank-bucket page (holes sort last), one stable sort
     size_t tmp = 0;
     hipcub::DoubleBuffer<unsigned long long> dk(h->d_tkeys, h->d_tkeys2);
     hipcub::DoubleBuffer<int> dv(h->d_tvals, h->d_tvals2);
@@ -2502,6 +2567,9 @@ static int ensure_tindex(adlbq_server *h) {
         h->cap_tsort = std::max(tmp, 2 * h->cap_tsort);
         AQ_HIP(hipMalloc(&h->d_tsort, h->cap_tsort));
     }
+    long long filled = 0;
+    for (int k = 0; k < nb; k++)
+        if (!h->rankb[k].pages.empty()) filled += (long long)(h->rankb[k].pages.size() - 1) * PAGE + h->rankb[k].tail_fill;
     if (npg > 0) {
         k_tindex_keys<<<npg, 256, 0, s>>>(h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill, nb, h->d_prio, h->d_meta,
                                           h->d_tkeys, h->d_tvals);
@@ -2512,10 +2580,13 @@ static int ensure_tindex(adlbq_server *h) {
             std::swap(h->d_tvals, h->d_tvals2);
         }
     }
-    AQ_HIP(hipMemsetAsync(h->d_tstart, 0, sizeof(int) * (size_t)nb * 64, s));
-    AQ_HIP(hipMemsetAsync(h->d_tend, 0, sizeof(int) * (size_t)nb * 64, s));
-    if (n > 0) k_tindex_ranges<<<(int)((n + 255) / 256), 256, 0, s>>>(h->d_tkeys, n, h->d_tstart, h->d_tend);
-    AQ_HIP(hipGetLastError());
+    h->tidx_n = filled;  // the holes sorted past the filled slots
+    h->tidx_valid = true;
+    h->tidx_rebuilds++;
+    h->tnew_keys.clear();
+    h->tnew_vals.clear();
+    int rc;
+    if ((rc = tindex_ranges(h, nb))) return rc;
     h->tindex_dirty = false;
     return ADLBQ_OK;
 }
@@ -2744,7 +2815,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                 if (h->d_tcnt) AQ_HIP(hipFree(h->d_tcnt));
                 h->cap_tcnt = std::max<long long>(nb, 2 * h->cap_tcnt);
                 AQ_HIP(hipMalloc((void **)&h->d_tcnt, sizeof(int) * h->cap_tcnt));
-                AQ_HIP(hipMemset(h->d_tcnt, 0, sizeof(int) * h->cap_tcnt));  // k_targeted_idx re-zeroes its own
+                AQ_HIP(hipMemsetAsync(h->d_tcnt, 0, sizeof(int) * h->cap_tcnt, s));  // k_targeted_idx re-zeroes its own
             }
             if ((long long)nb * tcap > h->cap_tlist) {
                 if (h->d_tlist) AQ_HIP(hipFree(h->d_tlist));

@@ -865,15 +865,15 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMalloc((void **)&h->d_qm_hi, sizeof(int) * num_servers * T1));
     AQ_HIP(hipMalloc((void **)&h->d_qm_qlen, sizeof(int) * num_servers));
     AQ_HIP(hipMalloc((void **)&h->d_rfr_out, sizeof(int) * std::max(h->num_world, 1)));
-    AQ_HIP(hipMemset(h->d_rfr_out, 0, sizeof(int) * std::max(h->num_world, 1)));  // SURVEY hard part 4
+    AQ_HIP(hipMemsetAsync(h->d_rfr_out, 0, sizeof(int) * std::max(h->num_world, 1), h->stream));  // SURVEY hard part 4
     AQ_HIP(hipMalloc((void **)&h->d_rfr_to_rank, sizeof(int) * std::max(num_app_ranks, 1)));
-    AQ_HIP(hipMemset(h->d_rfr_to_rank, 0xff, sizeof(int) * std::max(num_app_ranks, 1)));
+    AQ_HIP(hipMemsetAsync(h->d_rfr_to_rank, 0xff, sizeof(int) * std::max(num_app_ranks, 1), h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_ctr, sizeof(DevCounters)));
-    AQ_HIP(hipMemset(h->d_ctr, 0, sizeof(DevCounters)));
+    AQ_HIP(hipMemsetAsync(h->d_ctr, 0, sizeof(DevCounters), h->stream));
     AQ_HIP(hipHostMalloc((void **)&h->h_snap, sizeof(DevCounters) * adlbq_server::NSNAP, hipHostMallocMapped));
     for (int i = 0; i < adlbq_server::NSNAP; i++) AQ_HIP(hipEventCreateWithFlags(&h->snap_ev[i], hipEventDisableTiming));
     AQ_HIP(hipMalloc((void **)&h->d_dem, sizeof(int) * T1));
-    AQ_HIP(hipMemset(h->d_dem, 0, sizeof(int) * T1));  // k_finalize re-zeroes it after every batch
+    AQ_HIP(hipMemsetAsync(h->d_dem, 0, sizeof(int) * T1, h->stream));  // k_finalize re-zeroes it after every batch
     AQ_HIP(hipMalloc((void **)&h->d_theta, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_need, sizeof(int) * T1));
     AQ_HIP(hipMalloc((void **)&h->d_candoff, sizeof(int) * (T1 + 1)));
@@ -882,9 +882,9 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMalloc((void **)&h->d_binoff, sizeof(int) * T1 * NB));
     AQ_HIP(hipMalloc((void **)&h->d_coltot, sizeof(unsigned int) * T1 * NB));
     AQ_HIP(hipMalloc((void **)&h->d_type_cnt, sizeof(int) * T1));
-    AQ_HIP(hipMemset(h->d_type_cnt, 0, sizeof(int) * T1));
+    AQ_HIP(hipMemsetAsync(h->d_type_cnt, 0, sizeof(int) * T1, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_rank_sync, sizeof(int) * (ADLBQ_MAX_TYPES + 2)));
-    AQ_HIP(hipMemset(h->d_rank_sync, 0, sizeof(int) * (ADLBQ_MAX_TYPES + 2)));
+    AQ_HIP(hipMemsetAsync(h->d_rank_sync, 0, sizeof(int) * (ADLBQ_MAX_TYPES + 2), h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     long long pages = std::max<long long>(16, (max_units + PAGE - 1) / PAGE + 16);
@@ -918,7 +918,10 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->h_apply) hipHostFree(h->h_apply);
     if (h->h_crem) hipHostFree(h->h_crem);
     if (h->h_putrec) hipHostFree(h->h_putrec);
+    if (h->d_tnewk) hipFree(h->d_tnewk);
+    if (h->d_tnewv) hipFree(h->d_tnewv);
     if (h->put_ev) hipEventDestroy(h->put_ev);
+    if (h->tnew_ev) hipEventDestroy(h->tnew_ev);
     if (h->steal_ev) hipEventDestroy(h->steal_ev);
     if (h->apply_ev) hipEventDestroy(h->apply_ev);
     for (int i = 0; i < adlbq_server::NSNAP; i++)
@@ -969,11 +972,12 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         const int *u = units9 + 9 * i;
         int tgt = u[3];
         Bucket *b;
+        int bk = -1;
         if (tgt < 0) {
             b = &h->open;
         } else {
-            int k = rank_bucket(h, tgt);
-            b = &h->rankb[k];
+            bk = rank_bucket(h, tgt);
+            b = &h->rankb[bk];
         }
         if (b->pages.empty() || b->tail_fill == PAGE) {
             if (h->n_pages == h->cap_pages && (rc = grow_pages(h, h->n_pages + 1))) return rc;
@@ -1016,6 +1020,10 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         if (tgt >= 0) {
             h->live_targeted++;
             h->tindex_dirty = true;
+            // the unit's targeted-index entry (k_tindex_keys' key): merged in at the next build
+            const unsigned int inv = ~((unsigned int)u[1] ^ 0x80000000u);
+            h->tnew_keys.push_back(((unsigned long long)bk << 38) | ((unsigned long long)ti << 32) | inv);
+            h->tnew_vals.push_back((int)((b->pages.size() - 1) * PAGE + (b->tail_fill - 1)));
         }
         if (h->live_units > h->max_count) h->max_count = h->live_units;
     }
@@ -1030,7 +1038,7 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
     AQ_HIP(hipEventRecord(h->put_ev, h->stream));
     // a parked Reserve can only exist if the last known count, plus every
     // Reserve launched since, is positive
-    bool may_match = h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0);
+    bool may_match = h->put_always_match || (h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0));
     long long add_bytes = 0;  // bytes of the batch's units (k_put_match adds them one Put at a time)
     if (!may_match)
         for (int i = 0; i < n; i++) add_bytes += BYTES_WQ + rec[i].len;
@@ -1040,8 +1048,9 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
     if (may_match) {
         // one workgroup over the staged rq; too many parked Reserves: the one-wave scan of the whole rq
         if (!h->d_pm_over) AQ_HIP(hipMalloc((void **)&h->d_pm_over, sizeof(int)));
-        AQ_HIP(hipMemsetAsync(h->d_pm_over, 0, sizeof(int), h->stream));
-        k_put_match_blk<<<1, PM_THREADS, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live,
+        AQ_HIP(hipMemsetAsync(h->d_pm_over, h->put_match_block ? 0 : 1, sizeof(int), h->stream));
+        if (h->put_match_block)
+            k_put_match_blk<<<1, PM_THREADS, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live,
                                                          h->d_ctr, h->d_meta, h->d_pin, h->d_putout, h->d_utypes,
                                                          h->T, h->d_pm_over);
         k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
@@ -1525,6 +1534,14 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->rank_in_select = value ? 1 : 0;
         return ADLBQ_OK;
     }
+    if (n == "put_match_block") {  // diagnostic: 0 = always the one-wave rq scan
+        h->put_match_block = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
+    if (n == "put_always_match") {  // diagnostic: run the put-side match even when rq is known empty
+        h->put_always_match = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "chain_stamps") {
         h->chain_stamps = value ? 1 : 0;
         return ADLBQ_OK;
@@ -1600,6 +1617,8 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n == "parked") return h->ctr.n_parked_last;
     if (n == "spec_lists") return h->ctr.spec_page0;
     if (n == "rank_fast") return h->ctr.rank_fast;
+    if (n == "tindex_merges") return h->tidx_merges;   // targeted index: incremental merges
+    if (n == "tindex_rebuilds") return h->tidx_rebuilds;  // and full rebuilds
     if (n == "candidates") {
         int v = 0;
         if (h->T > 0 && hipMemcpy(&v, h->d_candoff + h->T, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;

@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--config4-only", action="store_true", help="only the config-4 leg (profiling)")
     ap.add_argument("--c4-units", type=int, default=10_000_000, help="config 4: units (80%% targeted)")
     ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-puts", type=int, default=2048,
+                    help="config 4: Puts per step before the Reserve batch (same mix: 80%% targeted), so the "
+                         "targeted index update is timed")
     ap.add_argument("--c4-chain-passes", type=int, default=None,
                     help="config 4: in-launch neighbour passes of the ordered choice's round 0 (adlbq 'chain_passes')")
     ap.add_argument("--c4-chain-rounds", type=int, default=None,
@@ -458,7 +461,17 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         d_resp = torch.empty((nb, R, 12), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
+    P = args.c4_puts
+    puts = None
+    if P > 0:  # each step's new units, drawn like the queue (targets, types, prios)
+        wp = synth.config4(n_units=nb * P, n_reserves=1, seed=shards.shard_seed(args.seed + 43, rank))
+        puts = np.stack([wp.u_type, wp.u_prio, wp.u_answer, wp.u_target, wp.u_len, np.full(nb * P, -1),
+                         np.zeros(nb * P), np.full(nb * P, -1), np.full(nb * P, -1)], axis=1).astype(np.int32)
+        puts = puts.reshape(nb, P, 9)
+
     def step(b):
+        if puts is not None:
+            srv.put_batch(puts[b])
         srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
         srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
 
@@ -500,7 +513,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
                                                           "chain_fallback", "chain_timeouts")}})
     out = {
         "workload": f"config4: {N} units/shard (80% targeted, Zipf(1.1) over 1024 ranks), 32 Zipf types, "
-                    f"prio U[0,2^16), {R} hanging Reserves/step with 1-4 types",
+                    f"prio U[0,2^16), {R} hanging Reserves/step with 1-4 types, {P} Puts (same mix) before each",
+        "targeted_index": {"merges": srv.stat("tindex_merges"), "rebuilds": srv.stat("tindex_rebuilds")},
         "value": matched / el,
         "unit": "assignments/s",
         "ms_per_step": el * 1e3 / steps,

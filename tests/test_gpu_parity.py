@@ -307,3 +307,30 @@ def test_put_side_fifo_vs_oracle(gpu_available, n_parked):
     trace = np.concatenate(parts)
     cfg = (A, 1, 0)
     assert_same(run_abi(ut, cfg, trace, max_units=1 << 14), run_oracle(ut, cfg, trace))
+
+
+def test_targeted_index_incremental_vs_oracle(gpu_available):
+    """Targeted Puts between Reserve batches (config-4 shape at reduced size):
+    the targeted index takes each batch's new units by a merge into its sorted
+    entries (no full rebuild after the first), and every batch equals the
+    oracle's sequential wq_find_pre_targeted_hi_prio / wq_find_hi_prio."""
+    w = synth.config4(n_units=40_000, n_reserves=4096, seed=91)
+    cfg = (w.num_app_ranks, 1, 0)
+    rng = np.random.default_rng(91)
+    n0 = 30_000
+    parts = [synth.put_events(w, 0, n0)]
+    R, nb = w.n_reserves, 4
+    lo_u = n0
+    for b in range(nb):
+        lo, hi = b * R // nb, (b + 1) * R // nb
+        parts.append(synth.reserve_events(w.r_rank[lo:hi], w.r_types[lo:hi], np.zeros(hi - lo, np.uint8)))
+        hi_u = min(w.n_units, lo_u + 2500)   # the next slice of units: ~80% targeted
+        parts.append(synth.put_events(w, lo_u, hi_u))
+        lo_u = hi_u
+        parts.append(synth.simple_events(synth.OP_INFO))
+    trace = np.concatenate(parts)
+    with Server(w.user_types, *cfg, max_units=w.n_units) as s:
+        got = replay.replay(s, trace)
+        merges, rebuilds = s.stat("tindex_merges"), s.stat("tindex_rebuilds")
+    assert_same(got, run_oracle(w.user_types, cfg, trace))
+    assert rebuilds <= 2 and merges >= 2, (merges, rebuilds)
