@@ -22,6 +22,7 @@ SIGNATURES = {
     "adlbq_create": (c_int, [P, c_int, P, c_int, c_int, c_int, c_ll, c_int]),
     "adlbq_destroy": (c_int, [P]),
     "adlbq_put_batch": (c_int, [P, c_int, P, P]),
+    "adlbq_put_batch_device": (c_int, [P, c_int, P, P]),
     "adlbq_reserve_batch": (c_int, [P, c_int, P, P]),
     "adlbq_reserve_batch_device": (c_int, [P, c_int, P, P]),
     "adlbq_get_reserved": (c_int, [P, c_int, c_int, P]),

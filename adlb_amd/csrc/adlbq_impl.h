@@ -196,8 +196,9 @@ struct adlbq_server {
     int *d_lv = nullptr;               // [R][T] k_rank: level rows for the chain's guess (T <= 8)
     unsigned char *d_rtype = nullptr;
     int *d_pm_over = nullptr;          // k_put_match_blk: the staged rq overflowed
-    void *h_putrec = nullptr;          // pinned staging of a Put batch's records
-    hipEvent_t put_ev = nullptr;       // its copy to the device completed  // [R] type of the candidate at each global rank (the guess between rows)
+    void *h_putrec[2] = {nullptr, nullptr};     // pinned staging of Put batches' records, used in turn
+    hipEvent_t put_ev[2] = {nullptr, nullptr};  // the batch that used it has finished on the device
+    int put_slot = 0;  // [R] type of the candidate at each global rank (the guess between rows)
     // targeted units' sorted index (k_targeted_idx): keys/vals double buffers,
     // per (bucket, type) ranges, radix-sort scratch; rebuilt after targeted Puts
     unsigned long long *d_tkeys = nullptr, *d_tkeys2 = nullptr;

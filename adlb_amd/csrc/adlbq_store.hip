@@ -492,6 +492,16 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
     }
 }
 
+// the results of a Put batch that cannot match a parked Reserve: {wqseqno, -1, -1}
+__global__ void k_put_out(const PutRec *__restrict__ r, int n, int *out3) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        out3[3 * i] = r[i].seq;
+        out3[3 * i + 1] = -1;
+        out3[3 * i + 2] = -1;
+    }
+}
+
 __global__ void k_get(int slot, int rank, int seq, const int *prio, uint32_t *meta, const int *pin,
                       const int *seqa, const int4 *cold0, const int4 *cold1, int *res, DevCounters *ctr) {
     uint32_t m = meta[slot];
@@ -917,10 +927,12 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->h_steal) hipHostFree(h->h_steal);
     if (h->h_apply) hipHostFree(h->h_apply);
     if (h->h_crem) hipHostFree(h->h_crem);
-    if (h->h_putrec) hipHostFree(h->h_putrec);
+    for (int q = 0; q < 2; q++)
+        if (h->h_putrec[q]) hipHostFree(h->h_putrec[q]);
     if (h->d_tnewk) hipFree(h->d_tnewk);
     if (h->d_tnewv) hipFree(h->d_tnewv);
-    if (h->put_ev) hipEventDestroy(h->put_ev);
+    for (int q = 0; q < 2; q++)
+        if (h->put_ev[q]) hipEventDestroy(h->put_ev[q]);
     if (h->tnew_ev) hipEventDestroy(h->tnew_ev);
     if (h->steal_ev) hipEventDestroy(h->steal_ev);
     if (h->apply_ev) hipEventDestroy(h->apply_ev);
@@ -947,27 +959,33 @@ static int rank_bucket(adlbq_server *h, int target) {
     return k;
 }
 
-int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
-    if (!ok_handle(h) || n < 0 || (n && (!units9 || !out3))) return fail(ADLBQ_ERR_ARG, "adlbq_put_batch");
+// out3: host results (synchronises when a parked Reserve may match); d_out3:
+// device results, nothing waits (adlbq_put_batch_device)
+static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d_out3) {
     if (n == 0) return ADLBQ_OK;
     hipSetDevice(h->device);
     for (int i = 0; i < n; i++)
         if (!h->tindex.count(units9[9 * i])) return fail(ADLBQ_ERR_TYPE, "adlbq_put_batch: undeclared work type");
     int rc;
-    // records are staged in pinned memory; the previous batch's copy out of it must have completed
-    if (h->put_ev) AQ_HIP(hipEventSynchronize(h->put_ev));
-    else AQ_HIP(hipEventCreateWithFlags(&h->put_ev, hipEventDisableTiming));
+    // records are staged in pinned memory, two buffers used in turn: the copy out of
+    // this one (two batches ago) must have completed; so must the device record buffer's readers
+    const int sb = h->put_slot;
+    h->put_slot ^= 1;
+    if (h->put_ev[sb]) AQ_HIP(hipEventSynchronize(h->put_ev[sb]));
+    else AQ_HIP(hipEventCreateWithFlags(&h->put_ev[sb], hipEventDisableTiming));
     if (n > h->cap_put) {
         AQ_HIP(hipStreamSynchronize(h->stream));
         if (h->d_putrec) AQ_HIP(hipFree(h->d_putrec));
         if (h->d_putout) AQ_HIP(hipFree(h->d_putout));
-        if (h->h_putrec) AQ_HIP(hipHostFree(h->h_putrec));
+        for (int q = 0; q < 2; q++)
+            if (h->h_putrec[q]) AQ_HIP(hipHostFree(h->h_putrec[q]));
         h->cap_put = std::max(n, 2 * h->cap_put);
-        AQ_HIP(hipMalloc((void **)&h->d_putrec, sizeof(PutRec) * (size_t)h->cap_put));
+        AQ_HIP(hipMalloc((void **)&h->d_putrec, sizeof(PutRec) * 2 * (size_t)h->cap_put));
         AQ_HIP(hipMalloc((void **)&h->d_putout, sizeof(int) * 3 * (size_t)h->cap_put));
-        AQ_HIP(hipHostMalloc((void **)&h->h_putrec, sizeof(PutRec) * (size_t)h->cap_put, hipHostMallocDefault));
+        for (int q = 0; q < 2; q++)
+            AQ_HIP(hipHostMalloc((void **)&h->h_putrec[q], sizeof(PutRec) * (size_t)h->cap_put, hipHostMallocDefault));
     }
-    PutRec *rec = reinterpret_cast<PutRec *>(h->h_putrec);
+    PutRec *rec = reinterpret_cast<PutRec *>(h->h_putrec[sb]);
     for (int i = 0; i < n; i++) {
         const int *u = units9 + 9 * i;
         int tgt = u[3];
@@ -1033,9 +1051,8 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         h->cap_seq = nc;
     }
     // only a possible rq match synchronises
-    PutRec *d_rec = reinterpret_cast<PutRec *>(h->d_putrec);
+    PutRec *d_rec = reinterpret_cast<PutRec *>(h->d_putrec) + (size_t)sb * h->cap_put;
     AQ_HIP(hipMemcpyAsync(d_rec, rec, sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
-    AQ_HIP(hipEventRecord(h->put_ev, h->stream));
     // a parked Reserve can only exist if the last known count, plus every
     // Reserve launched since, is positive
     bool may_match = h->put_always_match || (h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0));
@@ -1051,13 +1068,23 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
         AQ_HIP(hipMemsetAsync(h->d_pm_over, h->put_match_block ? 0 : 1, sizeof(int), h->stream));
         if (h->put_match_block)
             k_put_match_blk<<<1, PM_THREADS, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live,
-                                                         h->d_ctr, h->d_meta, h->d_pin, h->d_putout, h->d_utypes,
-                                                         h->T, h->d_pm_over);
+                                                         h->d_ctr, h->d_meta, h->d_pin,
+                                                         d_out3 ? d_out3 : h->d_putout, h->d_utypes, h->T,
+                                                         h->d_pm_over);
         k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
-                                             h->d_meta, h->d_pin, h->d_putout, h->d_pm_over);
-        AQ_HIP(hipMemcpyAsync(out3, h->d_putout, sizeof(int) * 3 * n, hipMemcpyDeviceToHost, h->stream));
+                                             h->d_meta, h->d_pin, d_out3 ? d_out3 : h->d_putout, h->d_pm_over);
         AQ_HIP(hipGetLastError());
+        AQ_HIP(hipEventRecord(h->put_ev[sb], h->stream));
+        if (d_out3) {
+            h->ctr_stale = true;
+            return ADLBQ_OK;
+        }
+        AQ_HIP(hipMemcpyAsync(out3, h->d_putout, sizeof(int) * 3 * n, hipMemcpyDeviceToHost, h->stream));
         if ((rc = refresh_counters(h))) return rc;
+    } else if (d_out3) {
+        k_put_out<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, d_out3);
+        AQ_HIP(hipGetLastError());
+        AQ_HIP(hipEventRecord(h->put_ev[sb], h->stream));
     } else {
         for (int i = 0; i < n; i++) {
             out3[3 * i] = rec[i].seq;
@@ -1065,8 +1092,19 @@ int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
             out3[3 * i + 2] = -1;
         }
         AQ_HIP(hipGetLastError());
+        AQ_HIP(hipEventRecord(h->put_ev[sb], h->stream));
     }
     return ADLBQ_OK;
+}
+
+int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3) {
+    if (!ok_handle(h) || n < 0 || (n && (!units9 || !out3))) return fail(ADLBQ_ERR_ARG, "adlbq_put_batch");
+    return put_impl(h, n, units9, out3, nullptr);
+}
+
+int adlbq_put_batch_device(adlbq_server *h, int n, const int *units9, int *d_out3) {
+    if (!ok_handle(h) || n < 0 || (n && (!units9 || !d_out3))) return fail(ADLBQ_ERR_ARG, "adlbq_put_batch_device");
+    return put_impl(h, n, units9, nullptr, d_out3);
 }
 
 static int find_slot(adlbq_server *h, int seq, long long *slot) {

@@ -71,6 +71,12 @@ class Server:
         _lib.check(self.lib.adlbq_put_batch(self.h, u.shape[0], _ptr(u), _ptr(out)), "adlbq_put_batch")
         return out
 
+    def put_batch_device(self, units9, d_out3: int) -> None:
+        """adlbq_put_batch_device: results {wqseqno, matched_rank, matched_rqseqno}
+        land in device memory at d_out3 (n x 3 int32), in stream order."""
+        u = np.ascontiguousarray(np.asarray(units9, dtype=np.int32).reshape(-1, PUT_INTS))
+        _lib.check(self.lib.adlbq_put_batch_device(self.h, u.shape[0], _ptr(u), int(d_out3)), "adlbq_put_batch_device")
+
     def put(self, work_type, prio, answer_rank=0, target_rank=-1, length=8, home_server=-1,
             common_len=0, common_server=-1, common_seqno=-1):
         return self.put_batch([[work_type, prio, answer_rank, target_rank, length, home_server,

@@ -61,6 +61,9 @@ int adlbq_destroy(adlbq_server *h);
  * out3[i]   = {wqseqno, matched_rank or -1, matched_rqseqno or -1}; on a match
  * the caller sends TA_RESERVE_RESP to matched_rank (adlb.c:996-1008). */
 int adlbq_put_batch(adlbq_server *h, int n, const int *units9, int *out3);
+/* The same with out3 in device memory: nothing waits for the device (a
+ * GPU-resident front end reads the matches from d_out3 in stream order). */
+int adlbq_put_batch_device(adlbq_server *h, int n, const int *units9, int *d_out3);
 
 /* n FA_RESERVE messages in arrival order (src/adlb.c:1199-1317): for each,
  * wq_find_pre_targeted_hi_prio(rank) then wq_find_hi_prio (xq.c:190-247), pin

@@ -334,3 +334,43 @@ def test_targeted_index_incremental_vs_oracle(gpu_available):
         merges, rebuilds = s.stat("tindex_merges"), s.stat("tindex_rebuilds")
     assert_same(got, run_oracle(w.user_types, cfg, trace))
     assert rebuilds <= 2 and merges >= 2, (merges, rebuilds)
+
+
+def test_put_batch_device_matches_host_variant(gpu_available):
+    """adlbq_put_batch_device (results left in device memory, nothing waits)
+    gives the results adlbq_put_batch does, including Puts that take parked
+    Reserves, and leaves the same queue behind (a Reserve batch after it)."""
+    import torch
+    rng = np.random.default_rng(5)
+    ut = np.array([3, 5, 7], np.int32)
+    A = 4096
+    ranks = rng.permutation(A)[:1500]
+    tv = synth.type_vectors(rng, ut, 1500)
+    outs = []
+    for dev_path in (False, True):
+        with Server(ut, A, max_units=1 << 14) as s:
+            s.reserve_batch(np.concatenate([ranks[:, None], np.ones((1500, 1), np.int32), tv], axis=1))
+            got = []
+            for b in range(4):
+                w = synth.config2(n_units=600, n_reserves=1, seed=50 + b)
+                units = np.stack([ut[rng.integers(0, 3, 600)], w.u_prio, w.u_answer,
+                                  np.where(rng.random(600) < 0.3, ranks[rng.integers(0, 1500, 600)], -1), w.u_len,
+                                  np.full(600, -1), np.zeros(600), np.full(600, -1), np.full(600, -1)],
+                                 axis=1).astype(np.int32)
+                if dev_path:
+                    d = torch.empty((600, 3), dtype=torch.int32, device="cuda")
+                    s.put_batch_device(units, d.data_ptr())
+                    s.sync()
+                    got.append(d.cpu().numpy())
+                else:
+                    got.append(s.put_batch(units))
+            tv2 = synth.type_vectors(rng, ut, 512)
+            got.append(s.reserve_batch(np.concatenate([np.arange(512)[:, None], np.zeros((512, 1), np.int32), tv2],
+                                                      axis=1)))
+            got.append(np.asarray(s.info(), np.int64))
+        outs.append(got)
+        rng = np.random.default_rng(5)  # the same draws for the second pass
+        ranks = rng.permutation(A)[:1500]
+        tv = synth.type_vectors(rng, ut, 1500)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
