@@ -493,8 +493,11 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host = 0.0
     for b in range(W4, nb):
+        th = time.perf_counter()
         step(b)
+        host += time.perf_counter() - th
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -521,6 +524,7 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "unit": "assignments/s",
         "ms_per_step": el * 1e3 / steps,
         "matched_per_step": matched / steps,
+        "host_call_ms_per_step": round(host * 1e3 / steps, 3),
         "stages_ms": stages,
         "scaling": "weak",
     }
