@@ -79,6 +79,12 @@ def edge_cases():
     # T12 get failure and removal path
     cases["t12_get"] = (put(0, 4) + put(1, 4) + res(3, [0, 1]) + [G, 2, 1] + [G, 3, 1] + [G, 3, 1]
                         + res(3, [-1]) + [G, 3, 2] + [synth.OP_INFO])
+    # T16 a -1 wildcard after real types (legal at xq level: xq.c:205, 235, 398), on the
+    # Reserve side (untargeted and pre-targeted scans) and on the parked / put side
+    cases["t16_wild_nonzero"] = (put(0, 2) + put(1, 8) + put(2, 5, target=3) + put(3, 6) + put(2, 4)
+                                 + res(0, [0, -1]) + res(3, [1, -1]) + res(3, [0, 2, -1]) + res(1, [3, 1, -1])
+                                 + res(5, [0, -1]) + res(6, [1, -1, 2]) + res(7, [3, -1], 0)
+                                 + put(3, 1) + put(1, 9) + put(0, 1, target=6) + [synth.OP_INFO])
     return {k: np.asarray(v, np.int32) for k, v in cases.items()}
 
 
@@ -192,6 +198,9 @@ def main():
             save("t14_bytes", [0, 1, 2], 6, 4, 0, bytes_case())
         if "t15_bytes_stream" in only:
             save("t15_bytes_stream", [0, 1, 2], 16, 3, 1, bytes_stream())
+        for name, tr in edge_cases().items():
+            if name in only:
+                save(name, [0, 1, 2, 3], 8, 1, 0, tr)
         return
     save("t14_bytes", [0, 1, 2], 6, 4, 0, bytes_case())
     save("t15_bytes_stream", [0, 1, 2], 16, 3, 1, bytes_stream())
