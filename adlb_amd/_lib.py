@@ -47,6 +47,11 @@ SIGNATURES = {
     "adlbq_steal_collect": (c_int, [P, P, P, P, c_int, P, P]),
     "adlbq_steal_apply": (c_int, [P, c_int, P, c_int, P]),
     "adlbq_steal_check": (c_int, [P, P, P]),
+    "adlbq_push_accept": (c_int, [P, P, P]),
+    "adlbq_set_qmstat_nbytes": (c_int, [P, c_int, c_double]),
+    "adlbq_push_take": (c_int, [P, c_int, P]),
+    "adlbq_push_commit": (c_int, [P, c_int, P]),
+    "adlbq_push_discard": (c_int, [P, c_int, P]),
     "adlbq_steal_merge": (c_int, [c_int, c_int, P, c_int, P, P, P, c_int, P, P, P]),
     "adlbq_grant_batch": (c_int, [P, c_int, P, P]),
     "adlbq_steal_group_create": (c_int, [P, P, c_int, c_int, c_int]),

@@ -41,6 +41,13 @@ SIGNATURES = {
     "adlbsrv_rfr": (c_int, [P, c_int, P]),
     "adlbsrv_rfr_resp": (c_int, [P, c_int, P]),
     "adlbsrv_unreserve": (c_int, [P, c_int, P]),
+    "adlbsrv_push_tick": (c_int, [P]),
+    "adlbsrv_push_query": (c_int, [P, c_int, P]),
+    "adlbsrv_push_query_resp": (c_int, [P, c_int, P]),
+    "adlbsrv_push_len": (c_int, [P, c_int]),
+    "adlbsrv_push_hdr": (c_int, [P, c_int, P, P, c_int]),
+    "adlbsrv_push_del": (c_int, [P, c_int, P]),
+    "adlbsrv_moving_targeted": (c_int, [P, c_int, P]),
     "adlbsrv_num_parked": (c_int, [P]),
     "adlbsrv_activity": (ctypes.c_longlong, [P]),
     "adlbsrv_rfr_outstanding": (c_int, [P]),
@@ -176,6 +183,41 @@ class Core:
     def unreserve(self, src, buf12):
         b = _i32(buf12)
         self._chk(load().adlbsrv_unreserve(self._h, src, b.ctypes.data), "unreserve")
+        return self._take()
+
+    # -- memory-pressure push (adlb.c:509-556, 2109-2362) ------------------------------
+    def push_tick(self):
+        """The loop-top check; returns (sent, replies)."""
+        sent = self._chk(load().adlbsrv_push_tick(self._h), "push_tick")
+        return sent, self._take()
+
+    def push_query(self, src, d12):
+        d = np.ascontiguousarray(np.asarray(d12, np.float64))
+        self._chk(load().adlbsrv_push_query(self._h, src, d.ctypes.data), "push_query")
+        return self._take()
+
+    def push_query_resp(self, src, d12):
+        d = np.ascontiguousarray(np.asarray(d12, np.float64))
+        self._chk(load().adlbsrv_push_query_resp(self._h, src, d.ctypes.data), "push_query_resp")
+        return self._take()
+
+    def push_len(self, wqseqno) -> int:
+        return load().adlbsrv_push_len(self._h, int(wqseqno))
+
+    def push_hdr(self, src, buf12, payload: bytes):
+        b = _i32(buf12)
+        p = ctypes.create_string_buffer(payload, max(len(payload), 1))
+        self._chk(load().adlbsrv_push_hdr(self._h, src, b.ctypes.data, p, len(payload)), "push_hdr")
+        return self._take()
+
+    def push_del(self, src, buf12):
+        b = _i32(buf12)
+        self._chk(load().adlbsrv_push_del(self._h, src, b.ctypes.data), "push_del")
+        return self._take()
+
+    def moving_targeted(self, src, buf12):
+        b = _i32(buf12)
+        self._chk(load().adlbsrv_moving_targeted(self._h, src, b.ctypes.data), "moving_targeted")
         return self._take()
 
     def num_parked(self) -> int:

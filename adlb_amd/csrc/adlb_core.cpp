@@ -34,12 +34,18 @@ double now() {
 struct Unit {
     std::vector<char> buf;
     double t = 0.0;  // ws->time_stamp (adlb.c:972)
+    int fields[ADLBQ_PUT_INTS];  // the Put's record (a push re-sends it, adlb.c:533-543)
+    bool has_fields = false;
 };
 
 struct Common {
     std::vector<char> buf;
     int refcnt = -1;  // unknown until FA_PUT_BATCH_DONE (adlb.c:1144)
     int ngets = 0;
+};
+
+struct Held {  // a unit accepted by SS_PUSH_QUERY, until SS_PUSH_HDR / SS_PUSH_DEL
+    int type = 0, prio = 0, len = 0, answer = -1, target = -1, home = -1, clen = 0, csrv = -1, cseq = -1;
 };
 
 struct Parked {
@@ -68,6 +74,11 @@ struct adlbsrv {
     double time_on_rq = 0.0;
     std::vector<char> first_time_on_rq;
     std::vector<int> reqs, resp, pairs, out5, crem, rqx;
+    // push protocol (adlb.c:93, 493, 509-556)
+    bool push_out = false;
+    long long push_seen = -1;  // state stamp of the last loop-top check that sent nothing
+    long long npushed_from = 0, npushed_to = 0, table_events = 0;
+    std::unordered_map<int, Held> held;
 
     int rc(int r, const char *what) {
         if (r) g_err = std::string(what) + ": " + adlbq_last_error();
@@ -192,6 +203,8 @@ int adlbsrv_put_payload(adlbsrv *s, int src, const int *hdr, const void *buf, in
     Unit &unit = s->units[o[0]];
     unit.buf.assign((const char *)buf, (const char *)buf + (len > 0 ? len : 0));
     unit.t = now();
+    std::memcpy(unit.fields, u, sizeof u);
+    unit.has_fields = true;
     s->activity++;
     if (o[1] >= 0) {  // the parked Reserve gets this unit (adlb.c:989-1042)
         int b[WIRE_IBUF] = {WIRE_SUCCESS, hdr[0], hdr[1], hdr[4], hdr[2], o[0], s->me, hdr[7], hdr[8], hdr[9]};
@@ -362,6 +375,7 @@ int adlbsrv_qmstat(adlbsrv *s, const int *qlen, const double *nbytes, const int 
         if (i != mine &&
             s->rc(adlbq_set_qmstat_row(s->q, i, qlen[i], nbytes[i], hi + (size_t)i * s->T), "adlbq_set_qmstat_row"))
             return -1;
+    s->table_events++;
     return s->check_remote();  // adlb.c:1755
 }
 
@@ -434,6 +448,155 @@ int adlbsrv_unreserve(adlbsrv *s, int src, const int *b) {
     return 0;
 }
 
+// ---------------------------------------------------------------- push (adlb.c:509-556, 2109-2362)
+static double threshold_to_start_push(const adlbsrv *s) { return 0.95 * s->max_malloc; }  // adlb.c:93
+
+int adlbsrv_push_tick(adlbsrv *s) {
+    if (s->push_out || s->S < 2) return 0;  // adlb.c:511
+    // the condition only changes with queue or table events: skip the device read when none happened
+    const long long stamp = s->activity + s->table_events;
+    if (stamp == s->push_seen) return 0;
+    double curr = 0, hwm = 0;
+    if (s->rc(adlbq_bytes(s->q, &curr, &hwm), "adlbq_bytes")) return -1;
+    if (!(curr > threshold_to_start_push(s))) {  // adlb.c:509
+        s->push_seen = stamp;
+        return 0;
+    }
+    int cand = -1, seq = -1;
+    if (s->rc(adlbq_push_select(s->q, threshold_to_start_push(s), &cand, &seq), "adlbq_push_select")) return -1;
+    if (cand < 0 || seq < 0) {  // no unpinned unit or no server below the threshold (adlb.c:513-529)
+        s->push_seen = stamp;
+        return 0;
+    }
+    // the unit's fields: its target from the engine, the rest kept from the Put
+    auto it = s->units.find(seq);
+    int tgt = -1;
+    if (s->rc(adlbq_unit_target(s->q, seq, &tgt), "adlbq_unit_target")) return -1;
+    int qa[ADLBQ_PUT_INTS];
+    if (it == s->units.end() || !it->second.has_fields) return fail("push: no record of unit " + std::to_string(seq));
+    std::memcpy(qa, it->second.fields, sizeof qa);
+    double d[WIRE_IBUF] = {(double)qa[0], (double)qa[1], (double)qa[4], (double)qa[2], it->second.t, (double)tgt,
+                           (double)qa[5], (double)seq, (double)qa[6], (double)qa[7], (double)qa[8]};
+    s->send(cand, TAG_SS_PUSH_QUERY, d, (int)sizeof d);  // adlb.c:531-550
+    s->push_out = true;
+    return 1;
+}
+
+int adlbsrv_push_query(adlbsrv *s, int src, const double *d) {
+    // the pushee (adlb.c:2113-2160): room for it below the threshold, or a decline
+    double curr = 0, hwm = 0;
+    if (s->rc(adlbq_bytes(s->q, &curr, &hwm), "adlbq_bytes")) return -1;
+    const int len = (int)d[2];
+    double r[WIRE_IBUF] = {-1.0, curr, d[7], 0.0};
+    if (curr + len >= threshold_to_start_push(s)) {  // adlb.c:2122-2134
+        r[3] = -1.0;  // (the reference sends the seqno it would have had; a decline never uses it)
+        s->send(src, TAG_SS_PUSH_QUERY_RESP, r, (int)sizeof r);
+        return 0;
+    }
+    Held h;
+    h.type = (int)d[0];
+    h.prio = (int)d[1];
+    h.len = len;
+    h.answer = (int)d[3];
+    h.target = (int)d[5];
+    h.home = (int)d[6];
+    h.clen = (int)d[8];
+    h.csrv = (int)d[9];
+    h.cseq = (int)d[10];
+    const int u[ADLBQ_PUT_INTS] = {h.type, h.prio, h.answer, h.target, h.len, h.home, h.clen, h.csrv, h.cseq};
+    int seq = -1;
+    if (s->rc(adlbq_push_accept(s->q, u, &seq), "adlbq_push_accept")) return -1;
+    r[0] = (double)s->me;
+    r[3] = (double)seq;  // next_wqseqno (adlb.c:2139)
+    s->send(src, TAG_SS_PUSH_QUERY_RESP, r, (int)sizeof r);
+    s->held[seq] = h;
+    s->activity++;
+    return 0;
+}
+
+int adlbsrv_push_query_resp(adlbsrv *s, int src, const double *d) {
+    // the pusher (adlb.c:2162-2225)
+    const int to = (int)d[0];
+    s->push_out = false;
+    if (s->rc(adlbq_set_qmstat_nbytes(s->q, src - s->master, d[1]), "adlbq_set_qmstat_nbytes")) return -1;
+    s->table_events++;  // the table changed: the loop-top check looks again
+    if (to < 0) return 0;
+    int o[10];
+    if (s->rc(adlbq_push_take(s->q, (int)d[2], o), "adlbq_push_take")) return -1;
+    int b[WIRE_IBUF] = {(int)d[3]};
+    if (o[0] != 1) {  // a Reserve or a Get took it meanwhile (adlb.c:2182-2192)
+        s->send_ints(to, TAG_SS_PUSH_DEL, b, WIRE_IBUF);
+        return 0;
+    }
+    s->send_ints(to, TAG_SS_PUSH_HDR, b, WIRE_IBUF);  // adlb.c:2194-2207
+    auto it = s->units.find((int)d[2]);
+    if (it != s->units.end()) {
+        s->send(to, TAG_SS_PUSH_WORK, it->second.buf.data(), (int)it->second.buf.size());
+        s->units.erase(it);
+    } else {
+        s->send(to, TAG_SS_PUSH_WORK, nullptr, 0);
+    }
+    s->npushed_from++;
+    return 0;
+}
+
+int adlbsrv_push_len(adlbsrv *s, int wqseqno) {
+    auto it = s->held.find(wqseqno);
+    return it == s->held.end() ? -1 : it->second.len;
+}
+
+int adlbsrv_push_hdr(adlbsrv *s, int src, const int *b, const void *payload, int len) {
+    // the pushee (adlb.c:2228-2346)
+    const int seq = b[0];
+    auto hit = s->held.find(seq);
+    if (hit == s->held.end()) return fail("SS_PUSH_HDR: invalid wqseqno " + std::to_string(seq));  // adlb.c:2233-2238
+    const Held h = hit->second;
+    s->held.erase(hit);
+    int o[3];
+    if (s->rc(adlbq_push_commit(s->q, seq, o), "adlbq_push_commit")) return -1;
+    if (o[0] != 1) return fail("SS_PUSH_HDR: wqseqno " + std::to_string(seq) + " not held");
+    Unit &unit = s->units[seq];
+    unit.buf.assign((const char *)payload, (const char *)payload + (len > 0 ? len : 0));
+    unit.t = now();
+    const int f[ADLBQ_PUT_INTS] = {h.type, h.prio, h.answer, h.target, h.len, h.home, h.clen, h.csrv, h.cseq};
+    std::memcpy(unit.fields, f, sizeof f);
+    unit.has_fields = true;
+    s->npushed_to++;
+    s->activity++;
+    if (h.target >= 0) {  // adlb.c:2246-2272
+        if (h.home == s->me) {
+            if (s->rc(adlbq_tq_dec(s->q, h.target, h.type, src), "adlbq_tq_dec")) return -1;
+        } else {
+            int m[WIRE_IBUF] = {h.target, h.type, src, s->me};
+            s->send_ints(h.home, TAG_SS_MOVING_TARGETED_WORK, m, WIRE_IBUF);
+        }
+    }
+    if (o[1] >= 0) {  // a parked Reserve takes it (adlb.c:2287-2339)
+        int r[WIRE_IBUF] = {WIRE_SUCCESS, h.type, h.prio, h.len, h.answer, seq, s->me, h.clen, h.csrv, h.cseq};
+        s->send_ints(o[1], TAG_RESERVE_RESP, r, WIRE_IBUF);
+        s->served(o[2]);
+    }
+    return 0;
+}
+
+int adlbsrv_push_del(adlbsrv *s, int src, const int *b) {
+    (void)src;
+    int found = 0;
+    if (s->rc(adlbq_push_discard(s->q, b[0], &found), "adlbq_push_discard")) return -1;
+    if (!found) return fail("SS_PUSH_DEL: invalid wqseqno " + std::to_string(b[0]));  // adlb.c:2354-2359
+    s->held.erase(b[0]);
+    s->activity++;
+    return 0;
+}
+
+int adlbsrv_moving_targeted(adlbsrv *s, int src, const int *b) {
+    // the home server's tq follows the unit (adlb.c:2075-2106)
+    (void)src;
+    if (s->rc(adlbq_tq_dec(s->q, b[0], b[1], b[2]), "adlbq_tq_dec")) return -1;
+    if (b[3] != s->me && s->rc(adlbq_tq_add(s->q, b[0], b[1], b[3]), "adlbq_tq_add")) return -1;
+    return s->check_remote();
+}
+
 int adlbsrv_num_parked(adlbsrv *s) { return (int)s->parked.size(); }
 long long adlbsrv_activity(adlbsrv *s) { return s->activity; }
 int adlbsrv_rfr_outstanding(adlbsrv *s) { return s->rfr_out; }
@@ -450,7 +613,13 @@ int adlbsrv_info_get(adlbsrv *s, int key, double *val) {
     case 2:  // ADLB_INFO_AVG_TIME_ON_RQ
         *val = s->n_rq_timed ? s->time_on_rq / (double)s->n_rq_timed : 0.0;
         return 0;
-    case 3: case 4: case 6: case 7: case 8: case 9:  // push / qmstat-ring timings: no push, no ring here
+    case 3:  // ADLB_INFO_NPUSHED_FROM_HERE
+        *val = (double)s->npushed_from;
+        return 0;
+    case 4:  // ADLB_INFO_NPUSHED_TO_HERE
+        *val = (double)s->npushed_to;
+        return 0;
+    case 6: case 7: case 8: case 9:  // qmstat-ring timings: no ring here
         *val = 0.0;
         return 0;
     case 5:  // ADLB_INFO_NREJECTED_PUTS

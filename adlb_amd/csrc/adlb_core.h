@@ -60,6 +60,22 @@ int adlbsrv_rfr(adlbsrv *s, int src, const int *buf28);
 int adlbsrv_rfr_resp(adlbsrv *s, int src, const int *buf28);
 int adlbsrv_unreserve(adlbsrv *s, int src, const int *buf12);
 
+/* Memory-pressure push (adlb.c:509-556, 2109-2362).  push_tick: the loop-top
+ * check -- above 0.95 max_malloc with no query out, the first unpinned unit
+ * goes as SS_PUSH_QUERY to the server with the smallest nbytes_used below the
+ * threshold; returns 1 if a query was sent.  push_query (pushee, double[12]),
+ * push_query_resp (pusher, double[12]: SS_PUSH_HDR + SS_PUSH_WORK or
+ * SS_PUSH_DEL), push_hdr (pushee, int[12] + the SS_PUSH_WORK payload; len of
+ * that payload from push_len), push_del (pushee), moving_targeted (home
+ * server, SS_MOVING_TARGETED_WORK int[12], adlb.c:2071-2108). */
+int adlbsrv_push_tick(adlbsrv *s);
+int adlbsrv_push_query(adlbsrv *s, int src, const double *d12);
+int adlbsrv_push_query_resp(adlbsrv *s, int src, const double *d12);
+int adlbsrv_push_len(adlbsrv *s, int wqseqno);
+int adlbsrv_push_hdr(adlbsrv *s, int src, const int *b12, const void *payload, int len);
+int adlbsrv_push_del(adlbsrv *s, int src, const int *b12);
+int adlbsrv_moving_targeted(adlbsrv *s, int src, const int *b12);
+
 /* state for the driver */
 int adlbsrv_num_parked(adlbsrv *s);     /* rq->count */
 long long adlbsrv_activity(adlbsrv *s); /* events that changed a queue (exhaustion check) */

@@ -227,6 +227,7 @@ void serve(Loop *L, double max_malloc) {
             emit(L, g_debug, 1031 /* DS_LOG */, b, (int)sizeof b);
             t_ds = t;
         }
+        check(adlbsrv_push_tick(g_srv), "push");  // memory-pressure push (adlb.c:509-556)
         int flag = 0;
         MPI_Status st;
         MPI_Iprobe(MPI_ANY_SOURCE, MPI_ANY_TAG, g_all, &flag, &st);
@@ -348,6 +349,40 @@ void serve(Loop *L, double max_malloc) {
             int b[WIRE_IBUF];
             recv_ints<WIRE_IBUF>(b, from, tag);
             check(adlbsrv_unreserve(g_srv, from, b), "SS_UNRESERVE");
+            break;
+        }
+        case TAG_SS_PUSH_QUERY: {
+            double d[WIRE_IBUF];
+            MPI_Recv(d, (int)sizeof d, MPI_BYTE, from, tag, g_all, MPI_STATUS_IGNORE);
+            check(adlbsrv_push_query(g_srv, from, d), "SS_PUSH_QUERY");
+            break;
+        }
+        case TAG_SS_PUSH_QUERY_RESP: {
+            double d[WIRE_IBUF];
+            MPI_Recv(d, (int)sizeof d, MPI_BYTE, from, tag, g_all, MPI_STATUS_IGNORE);
+            check(adlbsrv_push_query_resp(g_srv, from, d), "SS_PUSH_QUERY_RESP");
+            break;
+        }
+        case TAG_SS_PUSH_HDR: {  // the payload follows as SS_PUSH_WORK (adlb.c:2243-2244)
+            int b[WIRE_IBUF];
+            recv_ints<WIRE_IBUF>(b, from, tag);
+            const int len = adlbsrv_push_len(g_srv, b[0]);
+            if (len < 0) die("SS_PUSH_HDR for a unit this server does not hold");
+            std::vector<char> p((size_t)std::max(len, 1));
+            MPI_Recv(p.data(), len, MPI_BYTE, from, TAG_SS_PUSH_WORK, g_all, MPI_STATUS_IGNORE);
+            check(adlbsrv_push_hdr(g_srv, from, b, p.data(), len), "SS_PUSH_HDR");
+            break;
+        }
+        case TAG_SS_PUSH_DEL: {
+            int b[WIRE_IBUF];
+            recv_ints<WIRE_IBUF>(b, from, tag);
+            check(adlbsrv_push_del(g_srv, from, b), "SS_PUSH_DEL");
+            break;
+        }
+        case TAG_SS_MOVING_TARGETED_WORK: {
+            int b[WIRE_IBUF];
+            recv_ints<WIRE_IBUF>(b, from, tag);
+            check(adlbsrv_moving_targeted(g_srv, from, b), "SS_MOVING_TARGETED_WORK");
             break;
         }
         case TAG_SRV_EXH_QUERY: {

@@ -30,8 +30,13 @@ enum {
     TAG_SS_RFR_RESP = 1019,       /* int[28] {rc, rqseqno, for_rank, type, prio, len, answer, wqseqno,
                                      prev_target, common x3} or {-2, rqseqno, for_rank, req_types[16]} */
     TAG_ACK_AND_RC = 1020,        /* int[12] or double[12] */
+    TAG_SS_PUSH_QUERY = 1021,     /* double[12] {type, prio, len, answer, time, target, home, wqseqno, common x3} */
+    TAG_SS_PUSH_QUERY_RESP = 1022, /* double[12] {to_rank or -1, nbytes_used, wqseqno on pusher, on pushee} */
+    TAG_SS_PUSH_HDR = 1023,       /* int[12] {wqseqno on pushee} */
+    TAG_SS_PUSH_WORK = 1024,      /* payload bytes */
+    TAG_SS_PUSH_DEL = 1025,       /* int[12] {wqseqno on pushee} */
     TAG_SS_UNRESERVE = 1028,      /* int[12] {for_rank, wqseqno, new_pin} */
-    TAG_SS_MOVING_TARGETED_WORK = 1029,
+    TAG_SS_MOVING_TARGETED_WORK = 1029, /* int[12] {target, type, from server, to server} */
     TAG_FA_ABORT = 1027,
     TAG_DS_END = 1032,
     TAG_INFO_NUM_WORK_UNITS = 1037, /* int[12] {type} -> int[12] {max_prio, n_at_max, n, nmw} */

@@ -380,12 +380,21 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
 }
 
 // The same FIFO first-fit for a batch of Puts, one workgroup of 1024: the live
-// rq entries (up to PM_CAP) are staged in LDS once as (rank, type-index mask),
-// then each Put in order is one block-wide minimum over the entries it may
-// take (rank == target when targeted, its type in the entry's set or a -1
-// anywhere in it: rq_find_rank_queued_for_type, xq.c:388-405).  *over = 1 when
-// the live entries exceed PM_CAP (the caller then runs k_put_match).
-constexpr int PM_CAP = 4096, PM_THREADS = 1024, PM_PER = PM_CAP / PM_THREADS;
+// rq entries (up to PM_CAP) are staged in LDS once as (rank, type-index mask);
+// the Puts go in chunks of PM_CAP, PM_PER consecutive ones per thread.  A Put
+// may take an entry when rank == target (targeted) and its type is in the
+// entry's set or a -1 is anywhere in it (rq_find_rank_queued_for_type,
+// xq.c:388-405).  Puts in order each taking the first such entry still free
+// is a serial dictatorship with one preference order on each side (Puts rank
+// entries by FIFO position, entries rank Puts by arrival), whose stable
+// matching is unique: the entries in FIFO order each taking the first
+// compatible Put still free give the same pairs.  So each chunk loops over
+// whichever side is shorter, one block-wide minimum per step, and stops when
+// no live entry is left (no step at all when nothing is parked).  Byte
+// accounting keeps the sequential high-water mark: the peak is the largest
+// running sum just after a Put's allocation (adlb.c:933, 963, 1040).  *over = 1
+// when the live entries exceed PM_CAP (the caller then runs k_put_match).
+constexpr int PM_CAP = 4096, PM_THREADS = 1024, PM_PER = PM_CAP / PM_THREADS, PM_WAVES = PM_THREADS / 64;
 __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__restrict__ r, int n,
                                                               const int *__restrict__ rq_rank,
                                                               const int *__restrict__ rq_types, int *rq_live,
@@ -393,7 +402,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                                                               const int *__restrict__ utypes, int T, int *over) {
     __shared__ int s_rank[PM_CAP], s_k[PM_CAP];
     __shared__ unsigned long long s_mask[PM_CAP];
-    __shared__ int s_wmin[PM_THREADS / 64], s_cnt[PM_THREADS / 64], s_tot;
+    __shared__ int s_wmin[PM_WAVES], s_cnt[PM_WAVES], s_tot;
+    __shared__ long long s_wsum[PM_WAVES], s_wpk[PM_WAVES];
     __shared__ int s_ut[ADLBQ_MAX_TYPES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int head = ctr->rq_head, nrq = ctr->rq_n;
@@ -431,7 +441,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
         __syncthreads();
         if (tid == 0) {
             int tot = s_tot;
-            for (int q = 0; q < PM_THREADS / 64; q++) tot += s_cnt[q];
+            for (int q = 0; q < PM_WAVES; q++) tot += s_cnt[q];
             s_tot = tot;
         }
         __syncthreads();
@@ -441,45 +451,133 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
         if (tid == 0) *over = 1;
         return;
     }
-    int live = ctr->rq_live;
-    for (int i = 0; i < n; i++) {
-        const PutRec u = r[i];
-        const unsigned long long bit = 1ull << (u.meta & (int)M_TYPE);
-        int best = INT_MAX;
+    // block-wide minimum of v (every thread gets it); two barriers
+    auto block_min = [&](int v) {
 #pragma unroll
-        for (int e = 0; e < PM_PER; e++) {
-            const int j = tid * PM_PER + e;  // each thread owns PM_PER consecutive entries: its first hit wins
-            if (best == INT_MAX && j < m && s_rank[j] != INT_MIN && (s_mask[j] & bit) &&
-                (u.target == -1 || u.target == s_rank[j]))
-                best = j;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) best = min(best, __shfl_xor(best, o, 64));
-        if (lane == 0) s_wmin[w] = best;
+        for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+        if (lane == 0) s_wmin[w] = v;
         __syncthreads();
-        if (tid == 0) {
-            int b = INT_MAX;
-            for (int q = 0; q < PM_THREADS / 64; q++) b = min(b, s_wmin[q]);
-            int *o = out3 + 3 * i;
-            o[0] = u.seq;
+        int b = INT_MAX;
+#pragma unroll
+        for (int q = 0; q < PM_WAVES; q++) b = min(b, s_wmin[q]);
+        __syncthreads();
+        return b;
+    };
+    int mlive = m, nmatch = 0;
+    long long run = 0, peak = LLONG_MIN;  // running byte delta before the chunk; peak over the batch
+    for (int c0 = 0; c0 < n; c0 += PM_CAP) {
+        const int nc = min(PM_CAP, n - c0);
+        PutRec u[PM_PER];
+        int res[PM_PER];
+        unsigned long long bit[PM_PER];
+#pragma unroll
+        for (int q = 0; q < PM_PER; q++) {
+            const int i = tid * PM_PER + q;
+            res[q] = -1;
+            if (i < nc) u[q] = r[c0 + i];
+            bit[q] = i < nc ? 1ull << (u[q].meta & (int)M_TYPE) : 0ull;
+        }
+        if (mlive > 0 && mlive <= nc) {
+            // entry side: each live entry in FIFO order takes the first compatible Put still free
+            for (int e = 0; e < m && mlive > 0; e++) {
+                const int rk = s_rank[e];
+                if (rk == INT_MIN) continue;  // taken (uniform: written before the last barrier)
+                const unsigned long long em = s_mask[e];
+                int best = INT_MAX;
+#pragma unroll
+                for (int q = 0; q < PM_PER; q++)
+                    if (best == INT_MAX && res[q] < 0 && (em & bit[q]) && (u[q].target == -1 || u[q].target == rk))
+                        best = tid * PM_PER + q;
+                const int b = block_min(best);
+                if (b != INT_MAX) {
+                    if (b / PM_PER == tid) res[b % PM_PER] = e;
+                    if (tid == 0) s_rank[e] = INT_MIN;
+                    mlive--;
+                }
+                __syncthreads();
+            }
+        } else if (mlive > 0) {
+            // Put side: each Put in order takes the first compatible entry still free
+            for (int i = 0; i < nc && mlive > 0; i++) {
+                const PutRec ui = r[c0 + i];
+                const unsigned long long pb = 1ull << (ui.meta & (int)M_TYPE);
+                int best = INT_MAX;
+#pragma unroll
+                for (int e = 0; e < PM_PER; e++) {
+                    const int j = tid * PM_PER + e;  // each thread owns PM_PER consecutive entries: its first hit wins
+                    if (best == INT_MAX && j < m && s_rank[j] != INT_MIN && (s_mask[j] & pb) &&
+                        (ui.target == -1 || ui.target == s_rank[j]))
+                        best = j;
+                }
+                const int b = block_min(best);
+                if (b != INT_MAX) {
+                    if (i / PM_PER == tid) res[i % PM_PER] = b;
+                    if (tid == 0) s_rank[b] = INT_MIN;
+                    mlive--;
+                }
+                __syncthreads();
+            }
+        }
+        // results, pins, and the byte deltas of this thread's Puts in order
+        long long acc = 0, pk = LLONG_MIN;
+#pragma unroll
+        for (int q = 0; q < PM_PER; q++) {
+            const int i = tid * PM_PER + q;
+            if (i >= nc) break;
+            int *o = out3 + 3ll * (c0 + i);
+            const long long wb = BYTES_WQ + u[q].len;  // pmalloc + wq_node_create
+            pk = max(pk, acc + wb);
+            acc += wb;
+            o[0] = u[q].seq;
             o[1] = -1;
             o[2] = -1;
-            bytes_add(ctr, BYTES_WQ + u.len);  // pmalloc + wq_node_create (adlb.c:933, 963)
-            if (b != INT_MAX) {
-                const int k = s_k[b], rk = s_rank[b];
-                s_rank[b] = INT_MIN;  // taken
+            const int e = res[q];
+            if (e >= 0) {
+                const int k = s_k[e], rk = rq_rank[k];
                 rq_live[k] = 0;
                 o[1] = rk;
                 o[2] = k + 1;  // rqseqno == slot + 1
-                bytes_add(ctr, -BYTES_RQ);  // rq_delete (adlb.c:1040)
-                pin[u.slot] = rk;
-                if (rk >= 0) meta[u.slot] = (uint32_t)u.meta | M_PINNED;
-                live--;
+                pin[u[q].slot] = rk;
+                if (rk >= 0) meta[u[q].slot] = (uint32_t)u[q].meta | M_PINNED;
+                acc -= BYTES_RQ;  // rq_delete (adlb.c:1040)
+                nmatch++;
             }
         }
+        // block exclusive scan of acc in Put order, the peak, the chunk total
+        long long x = acc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        long long px = pk == LLONG_MIN ? LLONG_MIN : pk + (x - acc);  // peak within the wave's prefix
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) px = max(px, __shfl_xor(px, o, 64));
+        if (lane == 63) s_wsum[w] = x;
+        if (lane == 0) s_wpk[w] = px;
+        __syncthreads();
+        long long wpre = 0, tot = 0, cpk = LLONG_MIN;
+        for (int q = 0; q < PM_WAVES; q++) {
+            if (s_wpk[q] != LLONG_MIN) cpk = max(cpk, tot + s_wpk[q]);
+            tot += s_wsum[q];
+        }
+        (void)wpre;
+        if (cpk != LLONG_MIN) peak = max(peak, run + cpk);
+        run += tot;
         __syncthreads();
     }
+    // matches of every thread
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nmatch += __shfl_xor(nmatch, o, 64);
+    if (lane == 0) s_cnt[w] = nmatch;
+    __syncthreads();
     if (tid == 0) {
+        int tm = 0;
+        for (int q = 0; q < PM_WAVES; q++) tm += s_cnt[q];
+        const long long b0 = ctr->bytes;
+        if (peak != LLONG_MIN && b0 + peak > ctr->bytes_hwm) ctr->bytes_hwm = b0 + peak;
+        ctr->bytes = b0 + run;
+        ctr->rq_live -= tm;
         // new FIFO head: the first staged entry still live (entries before the first staged one are dead)
         int nh = nrq;
         for (int j = 0; j < m; j++)
@@ -487,7 +585,6 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                 nh = s_k[j];
                 break;
             }
-        ctr->rq_live = live;
         ctr->rq_head = m ? nh : head;
     }
 }
@@ -801,6 +898,112 @@ __global__ void k_rfr_retry(DonorCtx c, const int *__restrict__ rq_rank, const i
     }
 }
 
+// ---- memory-pressure push (adlb.c:2109-2362): single-unit control operations
+// a unit accepted by SS_PUSH_QUERY is held for the server (pinned to it) until SS_PUSH_HDR
+__global__ void k_push_hold(int slot, int pin_rank, uint32_t *meta, int *pin) {
+    meta[slot] |= M_PINNED;
+    pin[slot] = pin_rank;
+}
+
+// SS_PUSH_QUERY_RESP at the pusher: the unit leaves if still live and unpinned (adlb.c:2179-2222)
+__global__ void k_push_take(int slot, int seq, const int *prio, uint32_t *meta, const int *seqa,
+                            const int4 *cold0, const int4 *cold1, int *res, DevCounters *ctr) {
+    const uint32_t m = meta[slot];
+    res[0] = 0;
+    if ((m & (M_LIVE | M_PINNED)) == M_LIVE && seqa[slot] == seq) {
+        const int4 c0 = cold0[slot], c1 = cold1[slot];  // {answer, len, home, clen}, {csrv, cseq, utype, target}
+        res[0] = 1;
+        res[1] = c1.z;
+        res[2] = prio[slot];
+        res[3] = c0.y;
+        res[4] = c0.x;
+        res[5] = c1.w;
+        res[6] = c0.z;
+        res[7] = c0.w;
+        res[8] = c1.x;
+        res[9] = c1.y;
+        meta[slot] = 0;
+        bytes_add(ctr, -(BYTES_WQ + c0.y));  // wq_delete (the payload leaves with the Isend, adlb.c:2221)
+    }
+}
+
+// SS_PUSH_HDR at the pushee (adlb.c:2232-2340): unpin, then the put-side FIFO
+// match of k_put_match for this one unit (rq_find_rank_queued_for_type,
+// xq.c:388-405); one wavefront
+__global__ void k_push_commit(int slot, int seq, const int *prio, uint32_t *meta, int *pin, const int *seqa,
+                              const int4 *cold1, const int *__restrict__ rq_rank, const int *__restrict__ rq_types,
+                              int *rq_live, DevCounters *ctr, long long *anchor, int *res) {
+    const int lane = threadIdx.x;
+    const uint32_t m = meta[slot];
+    if (!((m & M_LIVE) && seqa[slot] == seq)) {
+        if (lane == 0) res[0] = 0, res[1] = -1, res[2] = -1;
+        return;
+    }
+    const int4 c1 = cold1[slot];
+    const int utype = c1.z, target = c1.w;
+    const int head = ctr->rq_head, nrq = ctr->rq_n;
+    int found = -1;
+    if (ctr->rq_live > 0) {
+        for (int base = head; base < nrq; base += 64) {
+            const int k = base + lane;
+            bool hit = false;
+            if (k < nrq && ld_agent(rq_live + k)) {
+                const int rk = rq_rank[k];
+                if (target == -1 || target == rk) {
+                    const int *tv = rq_types + (long long)k * NREQ;
+#pragma unroll
+                    for (int q = 0; q < NREQ; q++) hit |= (tv[q] == -1 || tv[q] == utype);
+                }
+            }
+            const unsigned long long b = __ballot(hit);
+            if (b) {
+                found = base + __ffsll((long long)b) - 1;
+                break;
+            }
+        }
+    }
+    if (lane == 0) {
+        res[0] = 1;
+        res[1] = -1;
+        res[2] = -1;
+        pin[slot] = -1;
+        meta[slot] = m & ~M_PINNED;
+        if (found >= 0) {
+            const int rk = rq_rank[found];
+            st_agent(rq_live + found, 0);
+            res[1] = rk;
+            res[2] = found + 1;  // rqseqno == slot + 1
+            bytes_add(ctr, -BYTES_RQ);  // rq_delete (adlb.c:2338)
+            pin[slot] = rk;
+            if (rk >= 0) meta[slot] = m | M_PINNED;
+            ctr->rq_live -= 1;
+        } else {
+            atomicMax(&anchor[m & M_TYPE], (long long)prio[slot]);  // available: the anchor bounds it
+        }
+    }
+    if (found >= 0 && found == head) {  // advance the FIFO head past dead entries
+        if (lane == 0) {
+            int hd = head;
+            while (hd < nrq && !ld_agent(rq_live + hd)) hd++;
+            ctr->rq_head = hd;
+        }
+    }
+}
+
+// SS_PUSH_DEL at the pushee (adlb.c:2353-2360): the held unit is dropped
+__global__ void k_push_discard(int slot, int seq, uint32_t *meta, const int *seqa, const int4 *cold0,
+                               const int4 *cold1, int *res, DevCounters *ctr) {
+    const uint32_t m = meta[slot];
+    res[0] = 0;
+    if ((m & M_LIVE) && seqa[slot] == seq) {
+        const int4 c0 = cold0[slot];
+        res[0] = 1;
+        res[1] = cold1[slot].w;
+        meta[slot] = 0;
+        bytes_add(ctr, -(BYTES_WQ + c0.y));  // wq_delete frees node, record and the payload buffer
+    }
+}
+
 __global__ void k_set_int(int *p, int v) { *p = v; }
 
 __global__ void k_add_bytes(DevCounters *ctr, long long d) { bytes_add(ctr, d); }
@@ -961,7 +1164,8 @@ static int rank_bucket(adlbq_server *h, int target) {
 
 // out3: host results (synchronises when a parked Reserve may match); d_out3:
 // device results, nothing waits (adlbq_put_batch_device)
-static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d_out3) {
+// hold_rank >= 0: one unit held for that server (adlbq_push_accept): pinned, no rq match
+static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d_out3, int hold_rank = -1) {
     if (n == 0) return ADLBQ_OK;
     hipSetDevice(h->device);
     for (int i = 0; i < n; i++)
@@ -1055,13 +1259,15 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
     AQ_HIP(hipMemcpyAsync(d_rec, rec, sizeof(PutRec) * n, hipMemcpyHostToDevice, h->stream));
     // a parked Reserve can only exist if the last known count, plus every
     // Reserve launched since, is positive
-    bool may_match = h->put_always_match || (h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0));
+    bool may_match = hold_rank < 0 &&
+                     (h->put_always_match || (h->ctr_stale ? (rq_live_upper(h) > 0) : (h->ctr.rq_live > 0)));
     long long add_bytes = 0;  // bytes of the batch's units (k_put_match adds them one Put at a time)
     if (!may_match)
         for (int i = 0; i < n; i++) add_bytes += BYTES_WQ + rec[i].len;
     k_put_scatter<<<(n + 255) / 256, 256, 0, h->stream>>>(d_rec, n, h->d_prio, h->d_meta, h->d_pin, h->d_seq,
                                                           h->d_cold0, h->d_cold1, h->d_seq2slot, h->d_anchor,
                                                           h->d_rrec, h->d_ctr, add_bytes);
+    if (hold_rank >= 0) k_push_hold<<<1, 1, 0, h->stream>>>(rec[0].slot, hold_rank, h->d_meta, h->d_pin);
     if (may_match) {
         // one workgroup over the staged rq; too many parked Reserves: the one-wave scan of the whole rq
         if (!h->d_pm_over) AQ_HIP(hipMalloc((void **)&h->d_pm_over, sizeof(int)));
@@ -1255,6 +1461,13 @@ int adlbq_set_qmstat_row(adlbq_server *h, int server_idx, int qlen, double nbyte
     h->qm_qlen[server_idx] = qlen;
     h->qm_bytes[server_idx] = nbytes_used;
     for (int t = 0; t < h->T; t++) h->qm_hi[(size_t)server_idx * h->T + t] = type_hi_prio[t];
+    h->qm_dirty = true;
+    return ADLBQ_OK;
+}
+
+int adlbq_set_qmstat_nbytes(adlbq_server *h, int server_idx, double nbytes_used) {
+    if (!ok_handle(h) || server_idx < 0 || server_idx >= h->S) return fail(ADLBQ_ERR_ARG, "adlbq_set_qmstat_nbytes");
+    h->qm_bytes[server_idx] = nbytes_used;
     h->qm_dirty = true;
     return ADLBQ_OK;
 }
@@ -1466,6 +1679,72 @@ int adlbq_push_select(adlbq_server *h, double threshold, int *cand_server_rank, 
     if (h->h_result[0] == INT_MAX) return ADLBQ_OK;
     *cand_server_rank = reject_hint(h, threshold);  // argmin nbytes_used (adlb.c:516-528)
     *wqseqno = h->h_result[0];
+    return ADLBQ_OK;
+}
+
+int adlbq_push_accept(adlbq_server *h, const int *units9, int *wqseqno) {
+    if (!ok_handle(h) || !units9 || !wqseqno) return fail(ADLBQ_ERR_ARG, "adlbq_push_accept");
+    int out3[3];
+    int rc = put_impl(h, 1, units9, out3, nullptr, h->my_world);  // held for this server (adlb.c:2151, 2158)
+    if (rc) return rc;
+    *wqseqno = out3[0];
+    return ADLBQ_OK;
+}
+
+// a unit left the store on the device: the host's maps and counts follow
+static int unit_removed(adlbq_server *h, int seq, int target) {
+    h->seq2slot[seq] = -1;
+    h->live_units--;
+    if (target >= 0) h->live_targeted--;
+    AQ_HIP(hipMemsetAsync(h->d_seq2slot + seq, 0xff, sizeof(long long), h->stream));
+    return ADLBQ_OK;
+}
+
+int adlbq_push_take(adlbq_server *h, int wqseqno, int *out10) {
+    if (!ok_handle(h) || !out10) return fail(ADLBQ_ERR_ARG, "adlbq_push_take");
+    hipSetDevice(h->device);
+    long long slot;
+    memset(out10, 0, sizeof(int) * 10);
+    if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
+    k_push_take<<<1, 1, 0, h->stream>>>((int)slot, wqseqno, h->d_prio, h->d_meta, h->d_seq, h->d_cold0, h->d_cold1,
+                                        h->d_result, h->d_ctr);
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 10, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    if (h->h_result[0] != 1) return ADLBQ_OK;  // out10 stays zero
+    memcpy(out10, h->h_result, sizeof(int) * 10);
+    return unit_removed(h, wqseqno, out10[5]);
+}
+
+int adlbq_push_commit(adlbq_server *h, int wqseqno, int *out3) {
+    if (!ok_handle(h) || !out3) return fail(ADLBQ_ERR_ARG, "adlbq_push_commit");
+    hipSetDevice(h->device);
+    long long slot;
+    out3[0] = 0;
+    out3[1] = out3[2] = -1;
+    if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
+    int rc;
+    if ((rc = sync_tables(h))) return rc;
+    k_push_commit<<<1, 64, 0, h->stream>>>((int)slot, wqseqno, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold1,
+                                           h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr, h->d_anchor,
+                                           h->d_result);
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
+    if ((rc = refresh_counters(h))) return rc;  // synchronises; the rq counts follow the device
+    memcpy(out3, h->h_result, sizeof(int) * 3);
+    return ADLBQ_OK;
+}
+
+int adlbq_push_discard(adlbq_server *h, int wqseqno, int *found) {
+    if (!ok_handle(h) || !found) return fail(ADLBQ_ERR_ARG, "adlbq_push_discard");
+    hipSetDevice(h->device);
+    long long slot;
+    *found = 0;
+    if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
+    k_push_discard<<<1, 1, 0, h->stream>>>((int)slot, wqseqno, h->d_meta, h->d_seq, h->d_cold0, h->d_cold1,
+                                           h->d_result, h->d_ctr);
+    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 2, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    *found = h->h_result[0];
+    if (*found) return unit_removed(h, wqseqno, h->h_result[1]);
     return ADLBQ_OK;
 }
 

@@ -11,14 +11,16 @@ from __future__ import annotations
 import numpy as np
 
 from .server import Server
-from .synth import (OP_BYTES, OP_CHECKREM, OP_GET, OP_HWM, OP_INFO, OP_INFOTYPE, OP_PUSHSEL, OP_PUT,
-                    OP_PUTCHECK, OP_QMROW, OP_RESERVE, OP_RFRDONE, OP_RQDEL, OP_SETROW, OP_TQADD, OP_UNRESERVE)
+from .synth import (OP_BYTES, OP_CHECKREM, OP_GET, OP_HWM, OP_INFO, OP_INFOTYPE, OP_PUSHACCEPT, OP_PUSHCOMMIT,
+                    OP_PUSHDEL, OP_PUSHSEL, OP_PUSHTAKE, OP_PUT, OP_PUTCHECK, OP_QMROW, OP_RESERVE, OP_RFRDONE,
+                    OP_RQDEL, OP_SETROW, OP_TQADD, OP_UNRESERVE)
 
 
 def nargs(op: int, T: int) -> int:
     return {OP_PUT: 9, OP_RESERVE: 18, OP_GET: 2, OP_UNRESERVE: 3, OP_QMROW: 0, OP_SETROW: 3 + T,
             OP_CHECKREM: 0, OP_RFRDONE: 2, OP_TQADD: 3, OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1,
-            OP_INFOTYPE: 1, OP_BYTES: 0, OP_PUTCHECK: 2, OP_HWM: 0}[op]
+            OP_INFOTYPE: 1, OP_BYTES: 0, OP_PUTCHECK: 2, OP_HWM: 0, OP_PUSHACCEPT: 9, OP_PUSHTAKE: 1,
+            OP_PUSHCOMMIT: 1, OP_PUSHDEL: 1}[op]
 
 
 def _runs(tr: np.ndarray, T: int):
@@ -103,6 +105,14 @@ def replay(srv: Server, trace) -> np.ndarray:
                 emit([int(srv.bytes()[1])])
             elif op == OP_PUTCHECK:
                 emit(list(srv.put_check(x[0], x[1])))
+            elif op == OP_PUSHACCEPT:
+                emit([srv.push_accept(x)])
+            elif op == OP_PUSHTAKE:
+                emit(srv.push_take(x[0]).tolist())
+            elif op == OP_PUSHCOMMIT:
+                emit(srv.push_commit(x[0]).tolist())
+            elif op == OP_PUSHDEL:
+                emit([srv.push_discard(x[0])])
             else:
                 raise ValueError(f"unknown opcode {op}")
     return np.concatenate(out) if out else np.zeros(0, np.int32)

@@ -171,6 +171,31 @@ class Server:
                    "adlbq_push_select")
         return c.value, s.value
 
+    # -- push protocol (adlb.c:2109-2362) -------------------------------------------
+    def push_accept(self, unit9) -> int:
+        """SS_PUSH_QUERY at the pushee: the unit held for this server; its wqseqno."""
+        u = np.ascontiguousarray(np.asarray(unit9, dtype=np.int32).reshape(PUT_INTS))
+        s = ctypes.c_int()
+        _lib.check(self.lib.adlbq_push_accept(self.h, _ptr(u), ctypes.byref(s)), "adlbq_push_accept")
+        return s.value
+
+    def push_take(self, wqseqno) -> np.ndarray:
+        """SS_PUSH_QUERY_RESP at the pusher: {ok, type, prio, len, answer, target, home, clen, csrv, cseq}."""
+        out = np.zeros(10, dtype=np.int32)
+        _lib.check(self.lib.adlbq_push_take(self.h, int(wqseqno), _ptr(out)), "adlbq_push_take")
+        return out
+
+    def push_commit(self, wqseqno) -> np.ndarray:
+        """SS_PUSH_HDR at the pushee: {found, matched_rank, matched_rqseqno}."""
+        out = np.zeros(3, dtype=np.int32)
+        _lib.check(self.lib.adlbq_push_commit(self.h, int(wqseqno), _ptr(out)), "adlbq_push_commit")
+        return out
+
+    def push_discard(self, wqseqno) -> int:
+        f = ctypes.c_int()
+        _lib.check(self.lib.adlbq_push_discard(self.h, int(wqseqno), ctypes.byref(f)), "adlbq_push_discard")
+        return f.value
+
     # -- steal round (SURVEY §8(e); adlb_amd/shards.py) ----------------------------
     def steal_export(self, k: int):
         """Per type, the k best available units (SS_RFR donor side for every request

@@ -20,6 +20,7 @@ LOWEST_PRIO = -999999999     # ADLB_LOWEST_PRIO, adlb.h:22
 OP_PUT, OP_RESERVE, OP_GET, OP_UNRESERVE = 1, 2, 3, 4
 OP_QMROW, OP_SETROW, OP_CHECKREM, OP_RFRDONE, OP_TQADD = 5, 6, 7, 8, 9
 OP_PUSHSEL, OP_INFO, OP_RQDEL, OP_INFOTYPE = 10, 11, 12, 13
+OP_PUSHACCEPT, OP_PUSHTAKE, OP_PUSHCOMMIT, OP_PUSHDEL = 19, 20, 21, 22  # the SS_PUSH_* handlers (adlb.c:2109-2362)
 OP_BYTES, OP_PUTCHECK, OP_HWM = 16, 17, 18  # queue bytes beyond init; FA_PUT_HDR memory check (work_len, max_malloc); their high-water mark
 
 

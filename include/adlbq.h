@@ -116,6 +116,9 @@ int adlbq_qmstat_row(adlbq_server *h, int *qlen, int *type_hi_prio);
 int adlbq_set_qmstat_row(adlbq_server *h, int server_idx, int qlen, double nbytes_used,
                          const int *type_hi_prio);
 
+/* SS_PUSH_QUERY_RESP's update of the pushee's nbytes_used alone (adlb.c:2168-2169). */
+int adlbq_set_qmstat_nbytes(adlbq_server *h, int server_idx, double nbytes_used);
+
 /* check_remote_work_for_queued_apps (src/adlb.c:3536-3579): for each parked
  * Reserve in FIFO order without an outstanding RFR, the first type with a donor
  * (tq_find_first_rt, else qmstat argmax) gets an SS_RFR.  out3[k] = {rqseqno,
@@ -246,6 +249,27 @@ int adlbq_steal_group_destroy(adlbq_steal_group *g);
  * (wq_find_unpinned, xq.c:266-281) and the server with the smallest
  * nbytes_used below threshold (strict <, lowest index wins).  -1 when none. */
 int adlbq_push_select(adlbq_server *h, double threshold, int *cand_server_rank, int *wqseqno);
+
+/* ---- the push protocol that follows (SS_PUSH_*, adlb.c:2109-2362).
+ * Pushee, SS_PUSH_QUERY with room (adlb.c:2146-2160): a unit with the next
+ * wqseqno, held for this server (pinned to it: nothing matches it, it is not
+ * available) until adlbq_push_commit or adlbq_push_discard.  units9 as
+ * adlbq_put_batch, target_rank = the unit's real target (the reference keeps
+ * it aside as temp_target_rank); bytes as a put. */
+int adlbq_push_accept(adlbq_server *h, const int *units9, int *wqseqno);
+/* Pusher, SS_PUSH_QUERY_RESP (adlb.c:2179-2222): if wqseqno is still live
+ * and unpinned, remove it and return its fields: out10 = {1, work_type,
+ * work_prio, work_len, answer_rank, target_rank, home_server_rank,
+ * common_len, common_server_rank, common_seqno}; else out10[0] = 0 (a Reserve
+ * or Get took it meanwhile: the caller sends SS_PUSH_DEL). */
+int adlbq_push_take(adlbq_server *h, int wqseqno, int *out10);
+/* Pushee, SS_PUSH_HDR (adlb.c:2232-2340): the held unit becomes available
+ * (unpinned, its real target), then the put-side parked-Reserve match
+ * (rq_find_rank_queued_for_type, xq.c:388-405): out3 = {found, matched_rank
+ * or -1, matched_rqseqno or -1}; on a match the caller sends TA_RESERVE_RESP. */
+int adlbq_push_commit(adlbq_server *h, int wqseqno, int *out3);
+/* Pushee, SS_PUSH_DEL (adlb.c:2353-2360): the held unit is removed. */
+int adlbq_push_discard(adlbq_server *h, int wqseqno, int *found);
 
 /* ---- byte accounting (SURVEY hard part 5; adlb.c:3419-3474).  The handle
  * keeps the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced for the

@@ -34,6 +34,7 @@ LIBS = {
 OP_PUT, OP_RESERVE, OP_GET, OP_UNRESERVE, OP_QMROW, OP_SETROW = 1, 2, 3, 4, 5, 6
 OP_CHECKREM, OP_RFRDONE, OP_TQADD, OP_PUSHSEL, OP_INFO, OP_RQDEL, OP_INFOTYPE = 7, 8, 9, 10, 11, 12, 13
 OP_RFR, OP_RQLIST, OP_BYTES, OP_PUTCHECK, OP_HWM = 14, 15, 16, 17, 18
+OP_PUSHACCEPT, OP_PUSHTAKE, OP_PUSHCOMMIT, OP_PUSHDEL = 19, 20, 21, 22
 
 
 def build(ref: bool = False) -> None:
@@ -170,7 +171,8 @@ def event_nargs(op: int, ntypes: int) -> int:
     return {OP_PUT: 9, OP_RESERVE: 18, OP_GET: 2, OP_UNRESERVE: 3, OP_QMROW: 0,
             OP_SETROW: 3 + ntypes, OP_CHECKREM: 0, OP_RFRDONE: 2, OP_TQADD: 3,
             OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1, OP_INFOTYPE: 1, OP_RFR: 18, OP_RQLIST: 0,
-            OP_BYTES: 0, OP_PUTCHECK: 2, OP_HWM: 0}[op]
+            OP_BYTES: 0, OP_PUTCHECK: 2, OP_HWM: 0, OP_PUSHACCEPT: 9, OP_PUSHTAKE: 1, OP_PUSHCOMMIT: 1,
+            OP_PUSHDEL: 1}[op]
 
 
 def output_bound(tr: np.ndarray, ntypes: int) -> int:

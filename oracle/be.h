@@ -36,10 +36,12 @@ void *be_wq_find_pre_targeted_hi_prio(int rank, const int *types16);
 void *be_wq_find_hi_prio(const int *types16);
 void *be_wq_find_pinned_for_rank(int rank, int seqno);
 void *be_wq_find_unpinned(void);
+void *be_wq_find_seqno(int seqno);
 int   be_wq_num_unpinned_untargeted(void);
 int   be_wq_avail_hi_prio_of_type(int type);
 void  be_wq_view(void *u, be_unit_view *v);
 void  be_wq_set_pin(void *u, int pin_rank, int pinned);
+void  be_wq_set_target(void *u, int target_rank);
 void  be_wq_delete(void *u);
 int   be_wq_count(void);
 int   be_wq_max_count(void);

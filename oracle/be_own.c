@@ -242,6 +242,21 @@ void be_wq_set_pin(void *h, int pin_rank, int pinned)
     u->pinned = pinned;
 }
 
+void be_wq_set_target(void *h, int target_rank)
+{
+    ((unit_rec *)((link_t *)h)->rec)->target_rank = target_rank;
+}
+
+/* the first unit with this seqno in list order (wq_find_seqno) */
+void *be_wq_find_seqno(int seqno)
+{
+    FOR_EACH(units, l) {
+        if (((const unit_rec *)l->rec)->wqseqno == seqno)
+            return l;
+    }
+    return NULL;
+}
+
 void be_wq_delete(void *h)
 {
     const unit_rec *u = (const unit_rec *)((link_t *)h)->rec;

@@ -95,6 +95,8 @@ void be_wq_set_pin(void *h, int pin_rank, int pinned)
     ws->pinned = pinned;
 }
 
+void be_wq_set_target(void *h, int target_rank) { ((wq_struct_t *)((xq_node_t *)h)->data)->target_rank = target_rank; }
+void *be_wq_find_seqno(int seqno) { return wq_find_seqno(seqno); }
 void be_wq_delete(void *h) { wq_delete((xq_node_t *)h); }
 int be_wq_count(void) { return wq->count; }
 int be_wq_max_count(void) { return wq->max_count; }

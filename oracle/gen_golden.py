@@ -88,6 +88,27 @@ def edge_cases():
     return {k: np.asarray(v, np.int32) for k, v in cases.items()}
 
 
+def push_case():
+    """The SS_PUSH_* handlers (adlb.c:2109-2362) on both sides of a push, one
+    server (world rank 8 of 3 servers, 4 types), with the byte count after each step."""
+    A, B = synth.OP_PUSHACCEPT, synth.OP_BYTES
+    TK, CM, DL = synth.OP_PUSHTAKE, synth.OP_PUSHCOMMIT, synth.OP_PUSHDEL
+    ev = []
+    ev += put(0, 5) + put(1, 3, target=2) + put(2, 9, ln=100) + put(0, 5) + res(0, [2]) + [B]
+    # pusher: the choice (first unpinned unit, argmin nbytes below 0.95 max), then the take
+    ev += [synth.OP_SETROW, 1, 4, 5000, -5, -5, -5, -5, synth.OP_SETROW, 2, 4, 3000, -5, -5, -5, -5]
+    ev += [synth.OP_PUSHSEL, 100000, TK, 1, B, synth.OP_PUSHSEL, 100000]
+    ev += [TK, 3, TK, 1, TK, 99, TK, 2, B, synth.OP_INFO]  # pinned by the Reserve, gone, unknown, targeted
+    # pushee: held units are matched by nothing and not available, counted by info
+    ev += [A, 1, 7, 0, -1, 40, 9, -1, -1, -1, B] + res(1, [1]) + res(2, [1, -1]) + [synth.OP_QMROW]
+    ev += [synth.OP_INFOTYPE, 1, synth.OP_INFO]
+    ev += [CM, 5, B, synth.OP_QMROW]  # SS_PUSH_HDR: the first parked Reserve of a matching type gets it
+    ev += [A, 3, 4, 0, 3, 8, 9, -1, -1, -1, CM, 6] + res(3, [0]) + [synth.OP_QMROW]  # targeted at rank 3
+    ev += [A, 0, 11, 1, -1, 16, 8, 2, 9, 3, synth.OP_PUSHSEL, 100000, DL, 7, DL, 7, B, synth.OP_INFO]
+    ev += [A, 2, 6, 0, 5, 8, 9, -1, -1, -1] + res(5, [2]) + [CM, 8, CM, 77, synth.OP_INFO, B]
+    return np.asarray(ev, np.int32)
+
+
 def donor_case(T=3):
     """Donor selection: qmstat rows + tq + rfr_out throttling (adlb.c:3487-3579)."""
     ev = []
@@ -198,6 +219,8 @@ def main():
             save("t14_bytes", [0, 1, 2], 6, 4, 0, bytes_case())
         if "t15_bytes_stream" in only:
             save("t15_bytes_stream", [0, 1, 2], 16, 3, 1, bytes_stream())
+        if "t17_push" in only:
+            save("t17_push", [0, 1, 2, 3], 8, 3, 0, push_case())
         for name, tr in edge_cases().items():
             if name in only:
                 save(name, [0, 1, 2, 3], 8, 1, 0, tr)
@@ -207,6 +230,7 @@ def main():
     for name, tr in edge_cases().items():
         save(name, [0, 1, 2, 3], 8, 1, 0, tr)
     save("t13_donor", [0, 1, 2], 5, 4, 0, donor_case())
+    save("t17_push", [0, 1, 2, 3], 8, 3, 0, push_case())
     # config 2 at reduced scale, three variants
     w = synth.config2(n_units=20_000, n_reserves=4096, seed=21)
     save("c2_n20k_r4k", w.user_types, w.num_app_ranks, 1, 0, synth.workload_trace(w))

@@ -22,6 +22,8 @@ static struct {
     int *rfr_out;     /* [num_world]  (adlb.c:112, zeroed: SURVEY hard part 4) */
     int *rfr_to_rank; /* [num_app_ranks] */
     double bytes0;    /* the backend's byte count after init (queue bytes are relative to it) */
+    int *temp_target; /* [cap_tt] ws->temp_target_rank of units accepted by SS_PUSH_QUERY, by wqseqno */
+    int cap_tt;
 } S;
 
 int orc_init(int ntypes, const int *user_types, int num_app_ranks, int num_servers,
@@ -46,6 +48,9 @@ int orc_init(int ntypes, const int *user_types, int num_app_ranks, int num_serve
     S.qm_bytes = (double *)calloc(num_servers, sizeof(double));
     for (int i = 0; i < num_servers * ntypes; i++)
         S.qm_hi[i] = ORC_LOWEST_PRIO; /* adlb.c:301-316 */
+    free(S.temp_target);
+    S.temp_target = NULL;
+    S.cap_tt = 0;
     S.rfr_out = (int *)calloc(S.num_world, sizeof(int));
     S.rfr_to_rank = (int *)malloc(sizeof(int) * num_app_ranks);
     for (int i = 0; i < num_app_ranks; i++)
@@ -155,6 +160,10 @@ int orc_event_nargs(int op, int ntypes)
     case ORC_OP_BYTES: return 0;
     case ORC_OP_PUTCHECK: return 2;
     case ORC_OP_HWM: return 0;
+    case ORC_OP_PUSHACCEPT: return 9;
+    case ORC_OP_PUSHTAKE: return 1;
+    case ORC_OP_PUSHCOMMIT: return 1;
+    case ORC_OP_PUSHDEL: return 1;
     default: return -1;
     }
 }
@@ -329,6 +338,71 @@ long orc_replay(const int *tr, long ntrace, int *out, long outcap)
             double c, h;
             be_bytes(&c, &h);
             o[0] = (int)(c - S.bytes0);
+            n = 1;
+            break;
+        }
+        case ORC_OP_PUSHACCEPT: {
+            /* SS_PUSH_QUERY at the pushee, room left (adlb.c:2146-2160): a unit
+             * with the next local seqno, targeted at and pinned to this server
+             * until SS_PUSH_HDR; the real target is kept aside */
+            int seq = S.next_wqseqno++;
+            void *u = be_wq_add(a[0], a[1], seq, a[2], S.my_world_rank, a[4], a[5], a[6], a[7], a[8]);
+            be_wq_set_pin(u, S.my_world_rank, 1);
+            if (seq >= S.cap_tt) {
+                int nc = 2 * seq + 16;
+                S.temp_target = (int *)realloc(S.temp_target, sizeof(int) * nc);
+                S.cap_tt = nc;
+            }
+            S.temp_target[seq] = a[3];
+            o[0] = seq;
+            n = 1;
+            break;
+        }
+        case ORC_OP_PUSHTAKE: {
+            /* SS_PUSH_QUERY_RESP at the pusher (adlb.c:2179-2222): the unit goes
+             * unless a Reserve pinned it or a Get took it meanwhile */
+            void *u = be_wq_find_seqno(a[0]);
+            be_unit_view v;
+            memset(o, 0, sizeof(int) * 10);
+            if (u) be_wq_view(u, &v);
+            if (u && !v.pinned) {
+                o[0] = 1; o[1] = v.work_type; o[2] = v.work_prio; o[3] = v.work_len; o[4] = v.answer_rank;
+                o[5] = v.target_rank; o[6] = v.home_server_rank; o[7] = v.common_len;
+                o[8] = v.common_server_rank; o[9] = v.common_server_commseqno;
+                be_wq_delete(u); /* 2221-2222 (the payload leaves with the Isend) */
+            }
+            n = 10;
+            break;
+        }
+        case ORC_OP_PUSHCOMMIT: {
+            /* SS_PUSH_HDR at the pushee (adlb.c:2232-2340): the real target,
+             * unpinned, then the parked-Reserve match of a put */
+            void *u = be_wq_find_seqno(a[0]);
+            o[0] = 0; o[1] = -1; o[2] = -1;
+            if (u) {
+                be_unit_view v;
+                be_wq_set_target(u, a[0] < S.cap_tt ? S.temp_target[a[0]] : -1); /* 2240 */
+                be_wq_set_pin(u, -1, 0);                                         /* 2241-2242 */
+                be_wq_view(u, &v);
+                o[0] = 1;
+                void *r = be_rq_find_rank_queued_for_type(v.target_rank, v.work_type); /* 2287 */
+                if (r) {
+                    int rank, rqs, types[ORC_REQ_TYPES];
+                    be_rq_view(r, &rank, &rqs, types);
+                    be_wq_set_pin(u, rank, rank >= 0 ? 1 : 0); /* 2291-2293 */
+                    o[1] = rank;
+                    o[2] = rqs;
+                    be_rq_delete(r); /* 2338 */
+                }
+            }
+            n = 3;
+            break;
+        }
+        case ORC_OP_PUSHDEL: {
+            /* SS_PUSH_DEL at the pushee (adlb.c:2353-2360) */
+            void *u = be_wq_find_seqno(a[0]);
+            o[0] = u != NULL;
+            if (u) be_wq_delete(u);
             n = 1;
             break;
         }

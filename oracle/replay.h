@@ -32,6 +32,11 @@ enum {
     ORC_OP_BYTES = 16,    /*                                                    -> [curr] bytes the queues hold beyond init (adlb.c:3419-3474) */
     ORC_OP_PUTCHECK = 17, /* work_len max_malloc                               -> [rejected, hint_server_rank] (adlb.c:908-931) */
     ORC_OP_HWM = 18,      /*                                                    -> [hwm] their high-water mark beyond init (-1: backend cannot tell) */
+    /* memory-pressure push (adlb.c:2109-2362) */
+    ORC_OP_PUSHACCEPT = 19, /* type prio answer target len home clen csrv cseq  -> [wqseqno] SS_PUSH_QUERY at the pushee (2146-2160) */
+    ORC_OP_PUSHTAKE = 20,   /* wqseqno                                          -> [ok, type, prio, len, answer, target, home, clen, csrv, cseq] SS_PUSH_QUERY_RESP at the pusher (2179-2222) */
+    ORC_OP_PUSHCOMMIT = 21, /* wqseqno                                          -> [found, matched_rank, matched_rqseqno] SS_PUSH_HDR at the pushee (2232-2340) */
+    ORC_OP_PUSHDEL = 22,    /* wqseqno                                          -> [found] SS_PUSH_DEL at the pushee (2353-2360) */
 };
 
 /* TA_RESERVE_RESP layout (adlb.c:1213-1222), plus two slots this build uses

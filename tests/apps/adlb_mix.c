@@ -60,10 +60,12 @@ int main(int argc, char **argv) {
     if (ADLB_Init(nservers, 0, 0, 4, types, &am_server, &am_debug, &app_comm) != ADLB_SUCCESS) MPI_Abort(MPI_COMM_WORLD, 1);
     if (am_server) {
         ADLB_Server(hi, 0.0);
-        double hwm = 0, nrej = 0;
+        double hwm = 0, nrej = 0, pfrom = 0, pto = 0;
         ADLB_Info_get(ADLB_INFO_MALLOC_HWM, &hwm);
+        ADLB_Info_get(ADLB_INFO_NPUSHED_FROM_HERE, &pfrom);
+        ADLB_Info_get(ADLB_INFO_NPUSHED_TO_HERE, &pto);
         ADLB_Info_get(ADLB_INFO_NREJECTED_PUTS, &nrej);
-        printf("server %d: malloc hwm %.0f rejected puts %.0f\n", rank, hwm, nrej);
+        printf("server %d: malloc hwm %.0f pushed %.0f %.0f rejected puts %.0f\n", rank, hwm, pfrom, pto, nrej);
         ADLB_Finalize();
         MPI_Finalize();
         return 0;
