@@ -23,6 +23,16 @@
 
 namespace adlbq {
 
+// the ordered choice (adlbq_reserve.hip): requests per segment (one wavefront)
+// and the largest pass-1 warm-up replayed before a segment (T <= 8), a multiple of it
+#ifndef ADLBQ_CHAIN_SEG
+#define ADLBQ_CHAIN_SEG 256
+#endif
+#ifndef ADLBQ_CHAIN_WARM
+#define ADLBQ_CHAIN_WARM 512
+#endif
+constexpr int SEG = ADLBQ_CHAIN_SEG;
+constexpr int CHAIN_WARM = ADLBQ_CHAIN_WARM;
 constexpr int PAGE_SHIFT = 12;
 constexpr int PAGE = 1 << PAGE_SHIFT;       // 4096 slots per page
 constexpr int SPEC_CAP = 128;              // pass-1 speculative candidates per wave quarter of a page

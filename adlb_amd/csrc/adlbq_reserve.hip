@@ -35,9 +35,7 @@
 using namespace adlbq;
 
 
-constexpr int SEG = 256;               // chain segment: requests per wavefront (one prep_block)
-constexpr int SEG_BLOCKS = SEG / 64;
-constexpr int CHAIN_WARM = 512;        // largest round-0 warm-up before a segment (T <= 8), a multiple of SEG
+constexpr int SEG_BLOCKS = SEG / 64;   // SEG, CHAIN_WARM: adlbq_impl.h
 constexpr int PREP_BLOCK = 256;        // prep_block workgroup
 constexpr int RANK_FAST_T = 8;         // k_select_open ranks the candidates itself for up to this many types
 constexpr int LV_STEP = 64;            // the chain's level rows are kept for every LV_STEP-th global rank

@@ -1869,8 +1869,8 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         return ADLBQ_OK;
     }
     if (n == "chain_warm") {
-        if (value != -1 && value != 0 && value != 256 && value != 512)
-            return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 (auto), 0, 256 or 512");
+        if (value != -1 && (value < 0 || value > CHAIN_WARM || value % SEG != 0))
+            return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 (auto) or a multiple of the segment up to CHAIN_WARM");
         h->chain_warm = (int)value;
         return ADLBQ_OK;
     }
