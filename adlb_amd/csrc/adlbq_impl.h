@@ -69,6 +69,8 @@ struct DevCounters {
     int chain_timeouts;    // bounded hand-off waits of round 0's neighbour passes that gave up (cumulative)
     int spec_page0;        // the last scan's page 0, wave 0 read pass 1's list (diagnostic)
     int needsort_last;     // the last reserve batch had a type whose threshold fell in a multi-prio bin
+    int plan_g, plan_lo;   // the last candidate sort plan: candidates in all, lowest key bit any list varies in
+    int plan_missed;       // sync-free sorts whose plan did not hold (k_rank sorted in-launch), cumulative
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
     // the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced (adlb.c:3419-3474) over the
     // structures this handle replaces, plus what the caller adds (adlbq_bytes_adjust)
@@ -229,6 +231,10 @@ struct adlbq_server {
     // segmented radix sort of the multi-prio-bin candidate lists (launched
     // when the newest landed batch needed one; k_rank sorts otherwise)
     int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort
+    // launch_segsort's sync-free path: sorted merged keys / slots land here, the plan (valid, G, lo) on the device
+    unsigned long long *d_ckey3 = nullptr; int *d_cslot3 = nullptr; long long cap_c3 = 0; int *d_plan = nullptr;
+    int segsort_async = 1;             // "segsort_async": plan the merged sort from the last landed batch (no sync)
+    long long n_sort_async = 0;
     long long n_segsort = 0;                          // lists given a device-wide sort (cumulative)
     long long ssort_items = 0;
     // ordered choice (k_chain0 / k_chainr): per segment start used and delta, the
@@ -295,6 +301,7 @@ int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
+bool plan_hint(adlbq_server *h, int *g, int *lo);  // newest landed batch's candidate sort plan
 bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);

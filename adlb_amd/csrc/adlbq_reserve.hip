@@ -2680,6 +2680,108 @@ __global__ __launch_bounds__(256) void k_unmerge_keys(const int *__restrict__ ca
     if (blockIdx.x == 0 && threadIdx.x == 0 && needsort[t] == 1) needsort[t] = 2;
 }
 
+// The merged sort without a host read-back: the host sizes it from the last
+// landed batch's plan (G_bound candidates, key bits from lo_hint up); this
+// kernel checks the plan against this batch (every list's keys constant in the
+// top bits, G <= G_bound, no key varying below lo_hint) and records this
+// batch's own figures for the next one.  If the plan does not hold,
+// k_unmerge_plan leaves the lists alone and k_rank sorts them inside its launch
+// (needsort stays 1), so a stale plan costs time, never results.
+__global__ void k_sort_plan(int T, const int *__restrict__ candoff, const int *__restrict__ candlen,
+                            const int *__restrict__ needsort, const unsigned long long *__restrict__ kb, int g_bound,
+                            int lo_hint, int *plan, DevCounters *ctr) {
+    const int t = threadIdx.x;
+    const bool has = t < T && candlen[t] > 0;
+    const unsigned long long diff = has ? (kb[t] ^ kb[ADLBQ_MAX_TYPES + t]) : 0ull;
+    const bool bad_top = (diff >> LIST_SHIFT) != 0ull;
+    int lo = diff ? __ffsll((long long)diff) - 1 : 64;
+    const bool wants = t < T && needsort[t] == 1 && candlen[t] > 1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lo = min(lo, __shfl_xor(lo, o, 64));
+    const bool ok = __ballot(bad_top) == 0ull, nsort = __ballot(wants) != 0ull;
+    if (t == 0) {
+        const int G = candoff[T];
+        lo = min(lo, LIST_SHIFT);
+        plan[0] = (ok && nsort && G <= g_bound && lo >= lo_hint) ? 1 : 0;
+        plan[1] = G;
+        if (g_bound > 0 && nsort && !plan[0]) ctr->plan_missed += 1;
+        ctr->plan_g = G;
+        ctr->plan_lo = ok ? lo : 0;
+    }
+}
+
+// merged keys of every list (k_merge_keys), and sentinel keys (0: last in a
+// descending sort) from G up to the planned bound
+__global__ __launch_bounds__(256) void k_merge_pad(const int *__restrict__ plan, int g_bound,
+                                                   unsigned long long *mkey) {
+    for (int i = plan[1] + blockIdx.x * blockDim.x + threadIdx.x; i < g_bound; i += gridDim.x * blockDim.x)
+        mkey[i] = 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_unmerge_plan(const int *__restrict__ plan, const int *__restrict__ candoff,
+                                                      const int *__restrict__ candlen,
+                                                      const unsigned long long *__restrict__ kb,
+                                                      const unsigned long long *__restrict__ mkey,
+                                                      const int *__restrict__ s2, unsigned long long *key, int *slot,
+                                                      int *needsort) {
+    if (!plan[0]) return;  // k_rank sorts the lists that need it
+    const int t = blockIdx.y, b = candoff[t], e = b + candlen[t];
+    const unsigned long long top = kb[ADLBQ_MAX_TYPES + t] & ~LIST_LOW;
+    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x) {
+        key[i] = top | (mkey[i] & LIST_LOW);
+        slot[i] = s2[i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && needsort[t] == 1) needsort[t] = 2;
+}
+
+// the sync-free merged sort (see k_sort_plan); false when no plan has landed yet
+static int launch_segsort_planned(adlbq_server *h, bool *done) {
+    *done = false;
+    int g_last = 0, lo_last = 0;
+    if (!h->segsort_merged || !h->segsort_async || !plan_hint(h, &g_last, &lo_last)) return ADLBQ_OK;
+    const int T = h->T;
+    hipStream_t s = h->stream;
+    const long long gb = std::min<long long>(h->cap_cand, (long long)g_last + g_last / 4 + 4096);
+    const int g_bound = (int)gb;
+    const int lo_hint = std::max(0, (lo_last & ~7) - 8);  // a digit of margin; lower bits cost a pass each
+    if (gb > h->cap_c3) {
+        AQ_HIP(hipStreamSynchronize(s));
+        if (h->d_ckey3) AQ_HIP(hipFree(h->d_ckey3));
+        if (h->d_cslot3) AQ_HIP(hipFree(h->d_cslot3));
+        h->cap_c3 = std::max(gb, h->cap_cand / 4);
+        h->cap_c3 = std::min(h->cap_c3, h->cap_cand);
+        AQ_HIP(hipMalloc((void **)&h->d_ckey3, sizeof(unsigned long long) * h->cap_c3));
+        AQ_HIP(hipMalloc((void **)&h->d_cslot3, sizeof(int) * h->cap_c3));
+    }
+    if (!h->d_plan) AQ_HIP(hipMalloc((void **)&h->d_plan, sizeof(int) * 4));
+    const int kgx = 16;
+    AQ_HIP(hipMemsetAsync(h->d_kb, 0, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
+    AQ_HIP(hipMemsetAsync(h->d_kb + ADLBQ_MAX_TYPES, 0xff, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
+    k_keybits<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_kb);
+    k_sort_plan<<<1, 64, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_needsort, h->d_kb, g_bound, lo_hint, h->d_plan,
+                                 h->d_ctr);
+    k_merge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_ckey2);
+    k_merge_pad<<<std::min(1024, (g_bound + 255) / 256 + 1), 256, 0, s>>>(h->d_plan, g_bound, h->d_ckey2);
+    size_t tmp = 0;
+    AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey2, h->d_ckey3, h->d_cslot,
+                                                        h->d_cslot3, g_bound, lo_hint, 64, s));
+    if (tmp > h->cap_ssort) {
+        AQ_HIP(hipStreamSynchronize(s));
+        if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
+        h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
+        AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
+    }
+    size_t t2 = h->cap_ssort;
+    AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey2, h->d_ckey3, h->d_cslot,
+                                                        h->d_cslot3, g_bound, lo_hint, 64, s));
+    k_unmerge_plan<<<dim3(kgx, T), 256, 0, s>>>(h->d_plan, h->d_candoff, h->d_candlen, h->d_kb, h->d_ckey3,
+                                                 h->d_cslot3, h->d_ckey, h->d_cslot, h->d_needsort);
+    AQ_HIP(hipGetLastError());
+    h->n_sort_async++;
+    *done = true;
+    return ADLBQ_OK;
+}
+
 static int launch_segsort(adlbq_server *h) {
     const int T = h->T;
     hipStream_t s = h->stream;
@@ -2689,6 +2791,9 @@ static int launch_segsort(adlbq_server *h) {
         AQ_HIP(hipMemsetAsync(h->d_kb, 0, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
         AQ_HIP(hipMemsetAsync(h->d_kb + ADLBQ_MAX_TYPES, 0xff, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
         k_keybits<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_kb);
+        // this batch's plan figures for the next batch's sync-free path (plan[0] unused here)
+        if (!h->d_plan) AQ_HIP(hipMalloc((void **)&h->d_plan, sizeof(int) * 4));
+        k_sort_plan<<<1, 64, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_needsort, h->d_kb, 0, 64, h->d_plan, h->d_ctr);
         AQ_HIP(hipGetLastError());
     }
     std::vector<int> hb(3 * (size_t)T + 1);
@@ -2845,7 +2950,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     if (np > 0 && T > 0 && sort_hint(h)) {
         stage_begin(h, "sort", &ev);
-        if ((rc = launch_segsort(h))) return rc;
+        bool planned = false;
+        if ((rc = launch_segsort_planned(h, &planned))) return rc;
+        if (!planned && (rc = launch_segsort(h))) return rc;
         stage_end(h, "sort", ev);
     }
     if (np > 0 && T > 0) {

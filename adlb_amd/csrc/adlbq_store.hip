@@ -102,6 +102,20 @@ bool rank_hint(adlbq_server *h) {  // the newest landed batch ranked its candida
     return false;
 }
 
+// the newest landed batch's candidate sort plan (G, lowest varying key bit), or false
+bool plan_hint(adlbq_server *h, int *g, int *lo) {
+    const int N = adlbq_server::NSNAP;
+    for (int k = 1; k <= N; k++) {
+        const int i = (h->snap_next - k + N) % N;
+        if (!h->snap_at[i]) continue;
+        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
+        *g = h->h_snap[i].plan_g;
+        *lo = h->h_snap[i].plan_lo;
+        return *g > 0;
+    }
+    return false;
+}
+
 bool sort_hint(adlbq_server *h) {
     const int N = adlbq_server::NSNAP;
     for (int k = 1; k <= N; k++) {
@@ -1122,7 +1136,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv, h->d_rtype, h->d_pm_over,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
-                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem};
+                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
+                    h->d_ckey3, h->d_cslot3, h->d_plan};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1868,6 +1883,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_rounds = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "segsort_async") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "segsort_async must be 0 or 1");
+        h->segsort_async = (int)value;
+        return ADLBQ_OK;
+    }
     if (n == "chain_warm") {
         if (value != -1 && (value < 0 || value > CHAIN_WARM || value % SEG != 0))
             return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 (auto) or a multiple of the segment up to CHAIN_WARM");
@@ -1942,6 +1962,11 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         return v;
     }
     if (n == "device_sorted_lists") return h->n_segsort;  // candidate lists given a device-wide sort (cumulative)
+    if (n == "sort_async") return h->n_sort_async;         // merged sorts planned from the last landed batch (cumulative)
+    if (n == "sort_async_bad") {  // ... whose plan did not hold (k_rank sorted them), as of the newest landed batch
+        refresh_counters(h);
+        return h->ctr.plan_missed;
+    }
     if (n == "sort_timeouts") {  // k_rank waits for an in-launch sort that gave up (cumulative; 0 unless broken)
         int v = 0;
         if (hipMemcpy(&v, h->d_rank_sync + ADLBQ_MAX_TYPES + 1, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;

@@ -98,6 +98,8 @@ def parse():
     ap.add_argument("--chain-warm", type=int, default=None, help="metric leg: adlbq 'chain_warm' (0, 256, 512)")
     ap.add_argument("--c4-chain-stats", action="store_true",
                     help="config 4: after the timed region, replay each batch alone and report its chain counters")
+    ap.add_argument("--c4-segsort-async", type=int, default=None,
+                    help="config 4: adlbq 'segsort_async' (1: candidate sort planned from the last batch, no sync)")
     ap.add_argument("--c4-segsort-wide", type=int, default=None,
                     help="config 4: sort list by list (no merged sort); length from which a list gets a device-wide "
                          "sort (adlbq 'segsort_wide')")
@@ -445,6 +447,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         srv.set_param("chain_modes", args.c4_chain_modes)
     if args.c4_chain_rounds is not None:
         srv.set_param("chain_rounds", args.c4_chain_rounds)
+    if args.c4_segsort_async is not None:
+        srv.set_param("segsort_async", args.c4_segsort_async)
     if args.c4_segsort_wide is not None:
         srv.set_param("segsort_merged", 0)
         srv.set_param("segsort_wide", args.c4_segsort_wide)
@@ -520,6 +524,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "workload": f"config4: {N} units/shard (80% targeted, Zipf(1.1) over 1024 ranks), 32 Zipf types, "
                     f"prio U[0,2^16), {R} hanging Reserves/step with 1-4 types, {P} Puts (same mix) before each",
         "targeted_index": {"merges": srv.stat("tindex_merges"), "rebuilds": srv.stat("tindex_rebuilds")},
+        "candidate_sort": {"planned": srv.stat("sort_async"), "plan_missed": srv.stat("sort_async_bad"),
+                           "device_sorted_lists": srv.stat("device_sorted_lists")},
         "value": matched / el,
         "unit": "assignments/s",
         "ms_per_step": el * 1e3 / steps,
