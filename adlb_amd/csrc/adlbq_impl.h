@@ -170,6 +170,10 @@ struct adlbq_server {
     hipEvent_t snap_ev[NSNAP] = {};
     long long snap_at[NSNAP] = {};         // reserves launched up to and including that batch
     int snap_next = 0;
+    adlbq::DevCounters *d_snap = nullptr;   // device address of h_snap (mapped)
+    // the newest landed snapshot, looked up once per launch (hint_stamp): index or -1
+    long long hint_stamp = 0, landed_stamp = -1;
+    int landed_idx = -1;
     long long launched_reserves = 0;
 
     // ---- qmstat / donor selection
@@ -265,6 +269,11 @@ struct adlbq_server {
     int *d_rqx = nullptr; long long cap_rqx = 0;         // [1 count | cap*18 rq entries]
     int *h_steal = nullptr; long long cap_hsteal = 0;    // pinned: recs | nrec | navail (2T) | count | rq
     int steal_k = -1, steal_rqcap = 0;                   // shape of the export in flight (-1: none)
+    // a steal group's shard (adlbq_steal_group_create): each reserve batch lists export_extra
+    // candidates per type beyond its demand, so that an export right after it is a gather
+    // (k_export_after) instead of another scan; batch_export_k = that depth while nothing
+    // else has changed the wq since the batch (0: the export scans)
+    int export_extra = 0, batch_export_k = 0, batch_export_R = 0;
     hipEvent_t steal_ev = nullptr;
     int *h_apply = nullptr; long long cap_happly = 0;    // pinned staging of grants / deletions
     int *d_apply = nullptr; long long cap_dapply = 0;
@@ -301,13 +310,15 @@ int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
-bool plan_hint(adlbq_server *h, int *g, int *lo);  // newest landed batch's candidate sort plan
+bool plan_hint(adlbq_server *h, int *g, int *lo);
+inline void wq_changed(adlbq_server *h) { h->batch_export_k = 0; }  // the last batch's lists no longer describe the wq  // newest landed batch's candidate sort plan
 bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
 int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail);
+bool launch_export_after(adlbq_server *h, int k, int *d_recs, int *d_nrec, long long *d_navail);
 
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ unsigned long long make_key(int prio, unsigned int order) {

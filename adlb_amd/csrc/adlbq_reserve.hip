@@ -71,6 +71,7 @@ struct PrepArgs {
     int *tcnt;          // [buckets] appended entries (k_targeted_idx resets its own)
     int *tlist;         // [buckets][tcap] request indices, any order
     int tcap;
+    int dem_extra;      // candidates listed per type beyond the demand (a steal group's export depth)
 };
 
 template <int TB>  // TB >= T; TB <= 8: the user types are compared in registers
@@ -151,8 +152,10 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
         for (unsigned long long b = m; b; b &= b - 1) atomicAdd(&sd[__ffsll((long long)b) - 1], 1);
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += blockDim.x)
-        if (sd[t]) atomicAdd(&dem[t], sd[t]);
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        const int d = sd[t] + (blk == 0 ? a.dem_extra : 0);
+        if (d) atomicAdd(&dem[t], d);
+    }
 }
 
 // ---------------------------------------------------------------- pass 1
@@ -2897,6 +2900,7 @@ static int launch_segsort(adlbq_server *h) {
 
 int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
+    h->hint_stamp++;  // landed-snapshot hints are looked up once for this launch
     if ((rc = ensure_req_capacity(h, R))) return rc;
     if ((rc = sync_tables(h))) return rc;
     if ((rc = ensure_rq_capacity(h, R))) return rc;
@@ -2907,7 +2911,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipEvent_t ev;
 
     PrepArgs pa{d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch,
-                nullptr, 0, nullptr, nullptr, 0};
+                nullptr, 0, nullptr, nullptr, 0, h->export_extra};
     const int nb = (int)h->bucket_ranks.size();
     const bool targeted = h->live_targeted > 0 && nb > 0;
     if (targeted && nb < (1 << 20)) {  // per-bucket Reserve lists for k_targeted_idx
@@ -3024,8 +3028,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     stage_begin(h, "finalize", &ev);
     {
         const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
-        DevCounters *snap = nullptr;
-        AQ_HIP(hipHostGetDevicePointer((void **)&snap, h->h_snap + h->snap_next, 0));
+        DevCounters *snap = h->d_snap + h->snap_next;
         k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
                                                    h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
@@ -3034,18 +3037,70 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                                    h->d_gcut_next, h->d_rrec, h->d_needsort);
     }
     stage_end(h, "finalize", ev);
+    // the lists hold export_extra more per type: a steal export right after this batch gathers them
+    h->batch_export_k = (np > 0 && T > 0) ? h->export_extra : 0;
+    h->batch_export_R = R;
     h->launched_reserves += R;
     h->snap_at[h->snap_next] = h->launched_reserves;
     AQ_HIP(hipEventRecord(h->snap_ev[h->snap_next], s));
     h->snap_next = (h->snap_next + 1) % adlbq_server::NSNAP;
+    h->hint_stamp++;  // a new snapshot slot is in flight: look again next time
     AQ_HIP(hipGetLastError());
     h->ctr_stale = true;
     h->rq_n_upper += R;
     return ADLBQ_OK;
 }
 
+// The export right after a reserve batch whose lists ran export_extra >= k
+// deep beyond the demand: the ordered choice took a prefix of every list (its
+// heads, in order), so the k best available units of type t are the list
+// entries from h_t on, h_t = the batch's choices of type t (cht); the available
+// count is the scan's column total less h_t.  Records as k_export_gather.
+__global__ __launch_bounds__(256) void k_export_after(int T, int k, int R, const unsigned char *__restrict__ cht,
+                                                      const int *__restrict__ candoff, const int *__restrict__ candlen,
+                                                      const int *__restrict__ cslot, const int *__restrict__ prio,
+                                                      const int *__restrict__ seqa, const int4 *__restrict__ cold0,
+                                                      const int4 *__restrict__ cold1, int *__restrict__ recs,
+                                                      int *__restrict__ nrec, long long *__restrict__ navail,
+                                                      const unsigned int *__restrict__ coltot) {
+    __shared__ int s_h[4];
+    const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int c = 0;
+    for (int j = threadIdx.x; j < R; j += blockDim.x) c += cht[j] == t;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) s_h[w] = c;
+    __syncthreads();
+    const int ht = s_h[0] + s_h[1] + s_h[2] + s_h[3];
+    if (threadIdx.x < 64) {
+        unsigned long long a = coltot[t * NB + threadIdx.x];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        if (threadIdx.x == 0) navail[t] = (long long)a - ht;
+    }
+    const int n = max(0, min(k, candlen[t] - ht)), off = candoff[t] + ht;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int slot = cslot[off + i];
+        const int4 c0 = cold0[slot], c1 = cold1[slot];
+        int4 *r = reinterpret_cast<int4 *>(recs + ((long long)t * k + i) * 8);
+        r[0] = make_int4(prio[slot], seqa[slot], c1.z, c0.y);
+        r[1] = make_int4(c0.x, c0.w, c1.x, c1.y);
+    }
+    if (threadIdx.x == 0) nrec[t] = n;
+}
+
+// true (and the gather enqueued) when the last reserve batch's lists serve an export of depth k
+bool launch_export_after(adlbq_server *h, int k, int *d_recs, int *d_nrec, long long *d_navail) {
+    if (h->batch_export_k < k || h->T < 1) return false;
+    k_export_after<<<h->T, 256, 0, h->stream>>>(h->T, k, h->batch_export_R, h->d_cht, h->d_candoff, h->d_candlen,
+                                                h->d_cslot, h->d_prio, h->d_seq, h->d_cold0, h->d_cold1, d_recs,
+                                                d_nrec, d_navail, h->d_coltot);
+    return true;
+}
+
 // recs8 [T][k][8] then nrec [T] land in d_out, navail [T] in d_navail (device)
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
+    wq_changed(h);  // the export scan rebuilds the candidate lists
     int rc;
     if ((rc = sync_tables(h))) return rc;
     const int T = h->T, C = T * NB;

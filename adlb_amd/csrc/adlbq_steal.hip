@@ -297,6 +297,28 @@ static int merge_views(int S, int T, const int *user_types, int k, const ShardVi
 }
 
 
+// the grants (k_grant) and rq deletions of one shard from device-resident inputs,
+// on the shard's stream (adlbq_steal_apply, and the group's one-copy settle)
+static int steal_apply_launch(adlbq_server *h, int ngrant, const int *d_pairs, int ndel, const int *d_dels) {
+    wq_changed(h);
+    if (!h->d_apply_bad) {
+        AQ_HIP(hipMalloc((void **)&h->d_apply_bad, sizeof(int) * 3));
+        AQ_HIP(hipMemsetAsync(h->d_apply_bad, 0, sizeof(int) * 3, h->stream));
+    }
+    if (ngrant)
+        k_grant<<<(ngrant + 255) / 256, 256, 0, h->stream>>>(d_pairs, ngrant, h->d_seq2slot, h->next_wqseqno,
+                                                            h->d_meta, h->d_pin, h->d_seq, h->d_cold1, nullptr,
+                                                            h->d_apply_bad);
+    if (ndel) {
+        k_rq_delete_batch<<<(ndel + 255) / 256, 256, 0, h->stream>>>(d_dels, ndel, h->d_rq_live, h->d_ctr, nullptr,
+                                                                    h->d_apply_bad + 2, h->d_apply_bad + 1);
+        k_rq_delete_fix<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_ctr, h->d_apply_bad + 2);
+        h->ctr_stale = true;
+    }
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
 static int ensure_steal_buffers(adlbq_server *h, int k, int rqcap) {
     const int T = h->T;
     const long long n_out = (long long)T * k * 8 + T, n_rq = 1 + (long long)rqcap * 18;
@@ -390,6 +412,7 @@ int adlbq_steal_export(adlbq_server *h, int k, int *recs8, int *nrec, long long 
 }
 
 int adlbq_steal_apply(adlbq_server *h, int ngrant, const int *pairs2, int ndel, const int *rqseqnos) {
+    if (h) wq_changed(h);
     if (!h || ngrant < 0 || ndel < 0 || (ngrant && !pairs2) || (ndel && !rqseqnos))
         return fail(ADLBQ_ERR_ARG, "adlbq_steal_apply");
     if (!ngrant && !ndel) return ADLBQ_OK;
@@ -410,27 +433,11 @@ int adlbq_steal_apply(adlbq_server *h, int ngrant, const int *pairs2, int ndel, 
         AQ_HIP(hipMalloc((void **)&h->d_apply, sizeof(int) * nc));
         h->cap_dapply = nc;
     }
-    if (!h->d_apply_bad) {
-        AQ_HIP(hipMalloc((void **)&h->d_apply_bad, sizeof(int) * 3));
-        AQ_HIP(hipMemsetAsync(h->d_apply_bad, 0, sizeof(int) * 3, h->stream));
-    }
     if (ngrant) std::memcpy(h->h_apply, pairs2, sizeof(int) * 2 * (size_t)ngrant);
     if (ndel) std::memcpy(h->h_apply + 2 * (size_t)ngrant, rqseqnos, sizeof(int) * (size_t)ndel);
     AQ_HIP(hipMemcpyAsync(h->d_apply, h->h_apply, sizeof(int) * need, hipMemcpyHostToDevice, h->stream));
     AQ_HIP(hipEventRecord(h->apply_ev, h->stream));
-    if (ngrant)
-        k_grant<<<(ngrant + 255) / 256, 256, 0, h->stream>>>(h->d_apply, ngrant, h->d_seq2slot, h->next_wqseqno,
-                                                            h->d_meta, h->d_pin, h->d_seq, h->d_cold1, nullptr,
-                                                            h->d_apply_bad);
-    if (ndel) {
-        k_rq_delete_batch<<<(ndel + 255) / 256, 256, 0, h->stream>>>(h->d_apply + 2 * (size_t)ngrant, ndel,
-                                                                    h->d_rq_live, h->d_ctr, nullptr,
-                                                                    h->d_apply_bad + 2, h->d_apply_bad + 1);
-        k_rq_delete_fix<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_ctr, h->d_apply_bad + 2);
-        h->ctr_stale = true;
-    }
-    AQ_HIP(hipGetLastError());
-    return ADLBQ_OK;
+    return steal_apply_launch(h, ngrant, h->d_apply, ndel, h->d_apply + 2 * (size_t)ngrant);
 }
 
 int adlbq_steal_check(adlbq_server *h, int *bad_grants, int *bad_deletes) {
@@ -476,6 +483,7 @@ int adlbq_rq_export(adlbq_server *h, int cap, int *out18, int *count) {
 }
 
 int adlbq_grant_batch(adlbq_server *h, int n, const int *pairs2, int *found) {
+    if (h) wq_changed(h);
     if (!h || n < 0 || (n && (!pairs2 || !found))) return fail(ADLBQ_ERR_ARG, "adlbq_grant_batch");
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
@@ -531,6 +539,9 @@ struct adlbq_steal_group {
     std::vector<std::vector<int>> grants, dels;
     int *h_unr = nullptr, *d_unr = nullptr;  // SS_UNRESERVE staging of the grants
     long long cap_unr = 0;
+    int *h_app = nullptr, *d_app = nullptr;  // every shard's grants + rq deletions, one copy per settle
+    long long cap_app = 0;
+    hipEvent_t app_ev = nullptr;
     long long ns_copy = 0, ns_merge = 0, ns_apply = 0, nreq_last = 0;  // the last settle's host phases
 };
 
@@ -544,6 +555,7 @@ int adlbq_steal_group_create(adlbq_steal_group **out, adlbq_server **shards, int
             return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_create: shards differ in types, device or server count");
     auto *g = new adlbq_steal_group();
     g->sh.assign(shards, shards + n);
+    for (int j = 0; j < n; j++) shards[j]->export_extra = std::max(shards[j]->export_extra, k);
     g->n = n, g->k = k, g->T = shards[0]->T, g->rqcap = rqcap;
     const long long T = g->T;
     g->off_recs = 2;                                  // [0] shard index, [1] pad
@@ -579,7 +591,9 @@ int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
         k_rfr_reset<<<(std::max(std::max(h->A, h->num_world), 1) + 255) / 256, 256, 0, h->stream>>>(
             h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world, r, h->my_idx);
         int rc;
-        if (g->T && (rc = launch_export(h, g->k, r + g->off_recs, reinterpret_cast<long long *>(r + g->off_nav))))
+        long long *nav = reinterpret_cast<long long *>(r + g->off_nav);
+        if (g->T && !launch_export_after(h, g->k, r + g->off_recs, r + g->off_nrec, nav) &&
+            (rc = launch_export(h, g->k, r + g->off_recs, nav)))
             return rc;
         if (h->rq_cap > 0 && g->rqcap > 0)
             k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, g->rqcap,
@@ -670,11 +684,42 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
             g->resp.insert(g->resp.end(), r15, r15 + 15);
         }
     }
-    for (int j = 0; j < g->n; j++) {
-        const auto &gr = g->grants[(size_t)j];
-        const auto &dl = g->dels[(size_t)j];
-        if ((rc = adlbq_steal_apply(g->sh[(size_t)j], (int)(gr.size() / 2), gr.data(), (int)dl.size(), dl.data())))
-            return rc;
+    // every shard's grants and deletions staged together: one copy on the first
+    // shard's stream, each shard's kernels behind its event
+    long long tot = 0;
+    for (int j = 0; j < g->n; j++) tot += (long long)g->grants[(size_t)j].size() + (long long)g->dels[(size_t)j].size();
+    if (tot > 0) {
+        if (g->app_ev) AQ_HIP(hipEventSynchronize(g->app_ev));  // the previous settle's copy has left the staging
+        else AQ_HIP(hipEventCreateWithFlags(&g->app_ev, hipEventDisableTiming));
+        if (tot > g->cap_app) {
+            for (auto *h : g->sh) AQ_HIP(hipStreamSynchronize(h->stream));
+            if (g->h_app) AQ_HIP(hipHostFree(g->h_app));
+            if (g->d_app) AQ_HIP(hipFree(g->d_app));
+            g->cap_app = std::max(tot, 2 * g->cap_app);
+            AQ_HIP(hipHostMalloc((void **)&g->h_app, sizeof(int) * g->cap_app, hipHostMallocDefault));
+            AQ_HIP(hipMalloc((void **)&g->d_app, sizeof(int) * g->cap_app));
+        }
+        long long off = 0;
+        for (int j = 0; j < g->n; j++) {
+            for (const auto *v : {&g->grants[(size_t)j], &g->dels[(size_t)j]}) {
+                if (!v->empty()) std::memcpy(g->h_app + off, v->data(), sizeof(int) * v->size());
+                off += (long long)v->size();
+            }
+        }
+        AQ_HIP(hipMemcpyAsync(g->d_app, g->h_app, sizeof(int) * tot, hipMemcpyHostToDevice, h0->stream));
+        AQ_HIP(hipEventRecord(g->app_ev, h0->stream));
+        off = 0;
+        for (int j = 0; j < g->n; j++) {
+            adlbq_server *h = g->sh[(size_t)j];
+            const auto &gr = g->grants[(size_t)j];
+            const auto &dl = g->dels[(size_t)j];
+            const int ng = (int)(gr.size() / 2), nd2 = (int)dl.size();
+            if (ng || nd2) {
+                if (h != h0) AQ_HIP(hipStreamWaitEvent(h->stream, g->app_ev, 0));
+                if ((rc = steal_apply_launch(h, ng, g->d_app + off, nd2, g->d_app + off + 2ll * ng))) return rc;
+            }
+            off += (long long)gr.size() + nd2;
+        }
     }
     const auto t3 = clk::now();
     g->ns_copy = std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
@@ -769,6 +814,9 @@ int adlbq_steal_group_destroy(adlbq_steal_group *g) {
     if (g->h_all) hipHostFree(g->h_all);
     if (g->h_unr) hipHostFree(g->h_unr);
     if (g->d_unr) hipFree(g->d_unr);
+    if (g->h_app) hipHostFree(g->h_app);
+    if (g->d_app) hipFree(g->d_app);
+    if (g->app_ev) hipEventDestroy(g->app_ev);
     delete g;
     return ADLBQ_OK;
 }

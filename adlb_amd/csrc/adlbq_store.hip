@@ -55,6 +55,21 @@ static int grow_pages(adlbq_server *h, int need) {
     return ADLBQ_OK;
 }
 
+// the newest reserve-batch snapshot that has landed in host memory, or -1; the
+// event queries run once per hint_stamp (one launch), older answers stay valid
+static int newest_landed(adlbq_server *h) {
+    if (h->landed_stamp == h->hint_stamp) return h->landed_idx;
+    const int N = adlbq_server::NSNAP;
+    int found = -1;
+    for (int k = 1; k <= N && found < 0; k++) {
+        const int i = (h->snap_next - k + N) % N;
+        if (h->snap_at[i] && hipEventQuery(h->snap_ev[i]) == hipSuccess) found = i;
+    }
+    h->landed_idx = found;
+    h->landed_stamp = h->hint_stamp;
+    return found;
+}
+
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest) {
     const int N = adlbq_server::NSNAP;
     if (wait_oldest) {  // backpressure: let the oldest batch still tracked land
@@ -79,52 +94,29 @@ void tighten_rq_bound(adlbq_server *h, bool wait_oldest) {
 // Upper bound of the parked Reserves alive now, from the newest landed batch
 // snapshot plus every Reserve launched after it (no synchronisation).
 long long rq_live_upper(adlbq_server *h) {
-    const int N = adlbq_server::NSNAP;
-    for (int k = 1; k <= N; k++) {
-        const int i = (h->snap_next - k + N) % N;
-        if (!h->snap_at[i]) continue;
-        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
-        if (h->snap_at[i] != h->launched_reserves) return (long long)h->h_snap[i].rq_live + (h->launched_reserves - h->snap_at[i]);
-        return h->h_snap[i].rq_live;
-    }
-    return LLONG_MAX;  // nothing landed yet: assume a match is possible
+    const int i = newest_landed(h);
+    if (i < 0) return LLONG_MAX;  // nothing landed yet: assume a match is possible
+    return (long long)h->h_snap[i].rq_live + (h->launched_reserves - h->snap_at[i]);
 }
 
 // Whether the newest landed reserve batch needed a multi-prio-bin sort.
 bool rank_hint(adlbq_server *h) {  // the newest landed batch ranked its candidates in k_select_open
-    const int N = adlbq_server::NSNAP;
-    for (int k = 1; k <= N; k++) {
-        const int i = (h->snap_next - k + N) % N;
-        if (!h->snap_at[i]) continue;
-        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
-        return h->h_snap[i].rank_fast != 0;
-    }
-    return false;
+    const int i = newest_landed(h);
+    return i >= 0 && h->h_snap[i].rank_fast != 0;
 }
 
 // the newest landed batch's candidate sort plan (G, lowest varying key bit), or false
 bool plan_hint(adlbq_server *h, int *g, int *lo) {
-    const int N = adlbq_server::NSNAP;
-    for (int k = 1; k <= N; k++) {
-        const int i = (h->snap_next - k + N) % N;
-        if (!h->snap_at[i]) continue;
-        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
-        *g = h->h_snap[i].plan_g;
-        *lo = h->h_snap[i].plan_lo;
-        return *g > 0;
-    }
-    return false;
+    const int i = newest_landed(h);
+    if (i < 0) return false;
+    *g = h->h_snap[i].plan_g;
+    *lo = h->h_snap[i].plan_lo;
+    return *g > 0;
 }
 
 bool sort_hint(adlbq_server *h) {
-    const int N = adlbq_server::NSNAP;
-    for (int k = 1; k <= N; k++) {
-        const int i = (h->snap_next - k + N) % N;
-        if (!h->snap_at[i]) continue;
-        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
-        return h->h_snap[i].needsort_last != 0;
-    }
-    return false;
+    const int i = newest_landed(h);
+    return i >= 0 && h->h_snap[i].needsort_last != 0;
 }
 
 int ensure_rq_capacity(adlbq_server *h, int extra) {
@@ -1098,6 +1090,7 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMalloc((void **)&h->d_ctr, sizeof(DevCounters)));
     AQ_HIP(hipMemsetAsync(h->d_ctr, 0, sizeof(DevCounters), h->stream));
     AQ_HIP(hipHostMalloc((void **)&h->h_snap, sizeof(DevCounters) * adlbq_server::NSNAP, hipHostMallocMapped));
+    AQ_HIP(hipHostGetDevicePointer((void **)&h->d_snap, h->h_snap, 0));
     for (int i = 0; i < adlbq_server::NSNAP; i++) AQ_HIP(hipEventCreateWithFlags(&h->snap_ev[i], hipEventDisableTiming));
     AQ_HIP(hipMalloc((void **)&h->d_dem, sizeof(int) * T1));
     AQ_HIP(hipMemsetAsync(h->d_dem, 0, sizeof(int) * T1, h->stream));  // k_finalize re-zeroes it after every batch
@@ -1181,6 +1174,7 @@ static int rank_bucket(adlbq_server *h, int target) {
 // device results, nothing waits (adlbq_put_batch_device)
 // hold_rank >= 0: one unit held for that server (adlbq_push_accept): pinned, no rq match
 static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d_out3, int hold_rank = -1) {
+    if (h) wq_changed(h);
     if (n == 0) return ADLBQ_OK;
     hipSetDevice(h->device);
     for (int i = 0; i < n; i++)
@@ -1335,6 +1329,7 @@ static int find_slot(adlbq_server *h, int seq, long long *slot) {
 }
 
 int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5) {
+    if (h) wq_changed(h);
     if (!ok_handle(h) || !out5) return fail(ADLBQ_ERR_ARG, "adlbq_get_reserved");
     hipSetDevice(h->device);
     long long slot;
@@ -1357,6 +1352,7 @@ int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5) {
 }
 
 static int launch_get_batch(adlbq_server *h, int n, const int *d_pairs, int *d_out5) {
+    if (h) wq_changed(h);
     if ((long long)h->next_wqseqno > h->cap_getclaim) {
         AQ_HIP(hipStreamSynchronize(h->stream));
         if (h->d_getclaim) AQ_HIP(hipFree(h->d_getclaim));
@@ -1407,6 +1403,7 @@ int adlbq_get_reserved_batch(adlbq_server *h, int n, const int *pairs2, int *out
 }
 
 int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, int *found) {
+    if (h) wq_changed(h);
     if (!ok_handle(h) || !found) return fail(ADLBQ_ERR_ARG, "adlbq_unreserve");
     hipSetDevice(h->device);
     long long slot;
@@ -1421,6 +1418,7 @@ int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, in
 }
 
 int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12) {
+    if (h) wq_changed(h);
     if (!ok_handle(h) || n < 0 || (n && (!d_reqs18 || !d_resp12)))
         return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_device");
     if (!n) return ADLBQ_OK;
@@ -1432,6 +1430,7 @@ int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, con
 }
 
 int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples) {
+    if (h) wq_changed(h);
     if (!ok_handle(h) || n < 0) return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_batch_device");
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
@@ -1716,6 +1715,7 @@ static int unit_removed(adlbq_server *h, int seq, int target) {
 }
 
 int adlbq_push_take(adlbq_server *h, int wqseqno, int *out10) {
+    if (h) wq_changed(h);
     if (!ok_handle(h) || !out10) return fail(ADLBQ_ERR_ARG, "adlbq_push_take");
     hipSetDevice(h->device);
     long long slot;
@@ -1731,6 +1731,7 @@ int adlbq_push_take(adlbq_server *h, int wqseqno, int *out10) {
 }
 
 int adlbq_push_commit(adlbq_server *h, int wqseqno, int *out3) {
+    if (h) wq_changed(h);
     if (!ok_handle(h) || !out3) return fail(ADLBQ_ERR_ARG, "adlbq_push_commit");
     hipSetDevice(h->device);
     long long slot;
@@ -1749,6 +1750,7 @@ int adlbq_push_commit(adlbq_server *h, int wqseqno, int *out3) {
 }
 
 int adlbq_push_discard(adlbq_server *h, int wqseqno, int *found) {
+    if (h) wq_changed(h);
     if (!ok_handle(h) || !found) return fail(ADLBQ_ERR_ARG, "adlbq_push_discard");
     hipSetDevice(h->device);
     long long slot;

@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--c3-reserves", type=int, default=8192, help="config 3: Reserves per shard per step")
     ap.add_argument("--c3-k", type=int, default=1024, help="config 3: exported units per type per shard")
     ap.add_argument("--c3-steps", type=int, default=40)
-    ap.add_argument("--c3-rqcap", type=int, default=4096, help="config 3: parked Reserves per shard a round considers")
+    ap.add_argument("--c3-rqcap", type=int, default=2048, help="config 3: parked Reserves per shard a round considers (~820 park per step)")
     ap.add_argument("--c3-threads", type=int, default=0, help="config 3: enqueue the shards' batches from threads")
     ap.add_argument("--c3-warmup", type=int, default=8, help="config 3: untimed steps (rq and export buffers grow)")
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
@@ -323,7 +323,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     steps = nb - W3
     out = {
         "workload": f"config3: {S} server shards ({SL}/GPU) x {N} units, {T} types with one type missing per "
-                    f"shard, {R} Reserves/shard/step (~10% only the missing type), steal round k={k}",
+                    f"shard, {R} Reserves/shard/step (~10% only the missing type), steal round k={k}, rqcap={args.c3_rqcap}",
         "value": (local_matched + settled) / el,
         "unit": "assignments/s",
         "ms_per_step": el * 1e3 / steps,

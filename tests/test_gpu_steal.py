@@ -35,11 +35,14 @@ def _run(S, n_units, R, seed, k, path="host", **kw):
     srvs = [Server(w.user_types, w.num_app_ranks, S, s, max_units=w.n_units) for s, w in enumerate(ws)]
     grp = None
     try:
+        if path == "group_batch":  # shards in a group before their batches: the first export gathers from them
+            grp = _GroupRound(srvs, k)
         for s, (w, srv) in enumerate(zip(ws, srvs)):
             out = synth.split_outputs(replay.replay(srv, synth.workload_trace(w)))
             np.testing.assert_array_equal(np.asarray(out[w.n_units:], np.int32), resps[s])
         if path == "group":
             grp = _GroupRound(srvs, k)
+        if grp is not None:
             got = rounds(grp)
         else:
             got = rounds(lambda: shards.steal_round_local(srvs, k=k))
@@ -75,7 +78,8 @@ def _run(S, n_units, R, seed, k, path="host", **kw):
             srv.close()
 
 
-PATHS = ["host", "group"]
+# group_batch: the group's first export reads the last Reserve batch's candidate lists (k_export_after)
+PATHS = ["host", "group", "group_batch"]
 
 
 @pytest.mark.parametrize("path", PATHS)
