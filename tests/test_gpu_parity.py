@@ -192,6 +192,16 @@ def test_config4_2m_exact(gpu_available, merged, wide, rounds):
     assert stats["sort_timeouts"] == 0
 
 
+def test_full_size_config4_exact(gpu_available):
+    """Config 4 at its BASELINE size (10M units, 80% targeted over 1024 ranks,
+    32 Zipf types, 65,536 Reserves of 1-4 types): two batches, the second with
+    the candidate lists sorted before the rank pass."""
+    w = synth.config4(n_units=10_000_000, n_reserves=65_536, n_ranks=1024, seed=10)
+    stats = {}
+    _exact_full(w, batches=2, stats=stats)
+    assert stats["sort_timeouts"] == 0
+
+
 REPEAT = {
     "c2": lambda: synth.config2(n_units=50_000, n_reserves=4096, seed=221),
     "c2_eq": lambda: synth.config2(n_units=50_000, n_reserves=4096, seed=222, equal_prio=True),
