@@ -123,6 +123,9 @@ struct adlbq_server {
     std::vector<adlbq::Bucket> rankb;     // per target app rank
     std::vector<int> bucket_ranks;        // ranks that own a bucket, in creation order
     std::unordered_map<int, int> rank_index;  // target rank -> index into rankb
+    std::vector<int> rank_index_dense;        // the same for target ranks in [0, A): -1 = no bucket yet
+    std::vector<int> tindex_dense;            // type value - tindex_lo -> type index (-1: undeclared), small ranges
+    int tindex_lo = 0;
     bool tables_dirty = true;
     // per page id: base prio of the packed offsets, and whether some unit did not fit (wide)
     std::vector<int> page_base, page_wide;
@@ -139,6 +142,11 @@ struct adlbq_server {
     int tcap = 0;
     int *d_all_pages = nullptr;   int cap_all_pages = 0;    // every page, with fills
     int *d_all_fill = nullptr;    int cap_all_fill = 0;
+    // the page tables above are views into d_tab, uploaded by sync_tables in one copy from
+    // one of two pinned staging buffers (used in turn behind an event)
+    int *d_tab = nullptr; long long cap_dtab = 0;
+    int *h_tab[2] = {nullptr, nullptr}; long long cap_htab[2] = {0, 0}; hipEvent_t tab_ev[2] = {nullptr, nullptr};
+    int tab_slot = 0;
 
     // wqseqno -> slot (host mirror for single-event calls, device copy for batches)
     int next_wqseqno = 1;

@@ -119,19 +119,24 @@ bool sort_hint(adlbq_server *h) {
     return i >= 0 && h->h_snap[i].needsort_last != 0;
 }
 
+constexpr long long RQ_GROW_MAX = 1ll << 24;  // rq entries grown to rather than waited for
+
 int ensure_rq_capacity(adlbq_server *h, int extra) {
     long long need = (h->ctr_stale ? h->rq_n_upper : (long long)h->ctr.rq_n) + extra;
     if (need <= h->rq_cap) return ADLBQ_OK;
     if (h->ctr_stale) {
         // the bound is loose by the batches still in flight: use the newest
-        // landed snapshot and, if that is not enough, wait for the oldest
-        // tracked batch (the host then runs at most NSNAP batches ahead)
+        // landed snapshot; if that is not enough, grow (the rq costs 76 B per
+        // entry: room for the batches in flight is cheaper than waiting for
+        // them), and only past RQ_GROW_MAX wait for the oldest tracked batch
         tighten_rq_bound(h, false);
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
-        tighten_rq_bound(h, true);
-        need = h->rq_n_upper + extra;
-        if (need <= h->rq_cap) return ADLBQ_OK;
+        if (need > RQ_GROW_MAX) {
+            tighten_rq_bound(h, true);
+            need = h->rq_n_upper + extra;
+            if (need <= h->rq_cap) return ADLBQ_OK;
+        }
     }
     long long nc = std::max<long long>(need, (long long)h->rq_cap * 2);
     nc = std::max<long long>(nc, 1024);
@@ -174,47 +179,81 @@ static int upload(T **dptr, int *cap, const std::vector<T> &v, hipStream_t s) {
 }
 
 int sync_tables(adlbq_server *h) {
-    int rc;
-    if (h->tables_dirty) {
-        if ((rc = upload(&h->d_open_pages, &h->cap_open_pages, h->open.pages, h->stream))) return rc;
-        std::vector<int> rp, pstart, fill;
-        pstart.push_back(0);
-        for (size_t k = 0; k < h->bucket_ranks.size(); k++) {
-            const Bucket &b = h->rankb[k];
-            rp.insert(rp.end(), b.pages.begin(), b.pages.end());
-            pstart.push_back((int)rp.size());
-            fill.push_back(b.pages.empty() ? 0 : b.tail_fill);
+    if (h->tables_dirty || h->pinfo_dirty) {
+        // every page table in one pinned staging buffer and one copy: the open pages,
+        // the rank buckets' pages (CSR) with their fills, bucket ranks, rank -> bucket,
+        // every page with its fill (whole-store scans), per-page offset base and wide flag
+        const std::vector<int> &op = h->open.pages;
+        const size_t nb = h->bucket_ranks.size(), A = (size_t)std::max(h->A, 1), npg = h->page_base.size();
+        size_t nrp = 0;
+        for (size_t k = 0; k < nb; k++) nrp += h->rankb[k].pages.size();
+        const size_t nall = op.size() + nrp;
+        auto al = [](size_t n) { return (n + 15) & ~(size_t)15; };  // 64-B aligned sections
+        const size_t o_open = 0, o_rp = o_open + al(op.size()), o_ps = o_rp + al(nrp), o_fill = o_ps + al(nb + 1),
+                     o_br = o_fill + al(nb), o_r2b = o_br + al(nb), o_ap = o_r2b + al(A), o_af = o_ap + al(nall),
+                     o_pb = o_af + al(nall), o_pw = o_pb + al(npg), total = o_pw + al(npg);
+        const int sl = h->tab_slot;
+        h->tab_slot ^= 1;
+        if (h->tab_ev[sl]) AQ_HIP(hipEventSynchronize(h->tab_ev[sl]));  // its last copy has left the buffer
+        else AQ_HIP(hipEventCreateWithFlags(&h->tab_ev[sl], hipEventDisableTiming));
+        if ((long long)total > h->cap_htab[sl]) {
+            if (h->h_tab[sl]) AQ_HIP(hipHostFree(h->h_tab[sl]));
+            h->cap_htab[sl] = std::max((long long)total, 2 * h->cap_htab[sl]);
+            AQ_HIP(hipHostMalloc((void **)&h->h_tab[sl], sizeof(int) * h->cap_htab[sl], hipHostMallocDefault));
         }
-        if ((rc = upload(&h->d_rank_pages, &h->cap_rank_pages, rp, h->stream))) return rc;
-        if ((rc = upload(&h->d_rank_pstart, &h->cap_rank_pstart, pstart, h->stream))) return rc;
-        if ((rc = upload(&h->d_rank_fill, &h->cap_rank_fill, fill, h->stream))) return rc;
-        if ((rc = upload(&h->d_bucket_ranks, &h->cap_bucket_ranks, h->bucket_ranks, h->stream))) return rc;
-        std::vector<int> r2b(std::max(h->A, 1), -1);
-        for (size_t k = 0; k < h->bucket_ranks.size(); k++)
-            if (h->bucket_ranks[k] >= 0 && h->bucket_ranks[k] < h->A) r2b[h->bucket_ranks[k]] = (int)k;
-        if ((rc = upload(&h->d_rank2b, &h->cap_rank2b, r2b, h->stream))) return rc;
-        // every page with its fill, for whole-store scans
-        std::vector<int> ap, af;
-        for (size_t i = 0; i < h->open.pages.size(); i++) {
-            ap.push_back(h->open.pages[i]);
-            af.push_back(i + 1 == h->open.pages.size() ? h->open.tail_fill : PAGE);
+        if ((long long)total > h->cap_dtab) {
+            AQ_HIP(hipStreamSynchronize(h->stream));  // kernels in flight read the old tables
+            if (h->d_tab) AQ_HIP(hipFree(h->d_tab));
+            h->cap_dtab = std::max((long long)total, 2 * h->cap_dtab);
+            AQ_HIP(hipMalloc((void **)&h->d_tab, sizeof(int) * h->cap_dtab));
         }
-        for (size_t k = 0; k < h->bucket_ranks.size(); k++) {
-            const Bucket &b = h->rankb[k];
-            for (size_t i = 0; i < b.pages.size(); i++) {
-                ap.push_back(b.pages[i]);
-                af.push_back(i + 1 == b.pages.size() ? b.tail_fill : PAGE);
+        int *t = h->h_tab[sl];
+        if (!op.empty()) std::memcpy(t + o_open, op.data(), sizeof(int) * op.size());
+        size_t r = 0, q = 0;
+        t[o_ps] = 0;
+        for (size_t k = 0; k < nb; k++) {
+            const Bucket &bk = h->rankb[k];
+            if (!bk.pages.empty()) std::memcpy(t + o_rp + r, bk.pages.data(), sizeof(int) * bk.pages.size());
+            r += bk.pages.size();
+            t[o_ps + k + 1] = (int)r;
+            t[o_fill + k] = bk.pages.empty() ? 0 : bk.tail_fill;
+            t[o_br + k] = h->bucket_ranks[k];
+        }
+        for (size_t i = 0; i < A; i++) t[o_r2b + i] = -1;
+        for (size_t k = 0; k < nb; k++)
+            if (h->bucket_ranks[k] >= 0 && h->bucket_ranks[k] < h->A) t[o_r2b + h->bucket_ranks[k]] = (int)k;
+        for (size_t i = 0; i < op.size(); i++, q++) {
+            t[o_ap + q] = op[i];
+            t[o_af + q] = i + 1 == op.size() ? h->open.tail_fill : PAGE;
+        }
+        for (size_t k = 0; k < nb; k++) {
+            const Bucket &bk = h->rankb[k];
+            for (size_t i = 0; i < bk.pages.size(); i++, q++) {
+                t[o_ap + q] = bk.pages[i];
+                t[o_af + q] = i + 1 == bk.pages.size() ? bk.tail_fill : PAGE;
             }
         }
-        if ((rc = upload(&h->d_all_pages, &h->cap_all_pages, ap, h->stream))) return rc;
-        if ((rc = upload(&h->d_all_fill, &h->cap_all_fill, af, h->stream))) return rc;
+        if (npg) {
+            std::memcpy(t + o_pb, h->page_base.data(), sizeof(int) * npg);
+            std::memcpy(t + o_pw, h->page_wide.data(), sizeof(int) * npg);
+        }
+        AQ_HIP(hipMemcpyAsync(h->d_tab, t, sizeof(int) * total, hipMemcpyHostToDevice, h->stream));
+        AQ_HIP(hipEventRecord(h->tab_ev[sl], h->stream));
+        int *d = h->d_tab;
+        h->d_open_pages = d + o_open;
+        h->d_rank_pages = d + o_rp;
+        h->d_rank_pstart = d + o_ps;
+        h->d_rank_fill = d + o_fill;
+        h->d_bucket_ranks = d + o_br;
+        h->d_rank2b = d + o_r2b;
+        h->d_all_pages = d + o_ap;
+        h->d_all_fill = d + o_af;
+        h->d_pbase = d + o_pb;
+        h->d_pwide = d + o_pw;
         h->tables_dirty = false;
-    }
-    if (h->pinfo_dirty) {
-        if ((rc = upload(&h->d_pbase, &h->cap_pbase, h->page_base, h->stream))) return rc;
-        if ((rc = upload(&h->d_pwide, &h->cap_pwide, h->page_wide, h->stream))) return rc;
         h->pinfo_dirty = false;
     }
+    int rc;
     if (h->qm_dirty) {
         if (h->S * h->T > 0)
             AQ_HIP(hipMemcpyAsync(h->d_qm_hi, h->qm_hi.data(), sizeof(int) * h->S * h->T,
@@ -1119,9 +1158,8 @@ int adlbq_destroy(adlbq_server *h) {
     if (!h) return ADLBQ_OK;
     hipSetDevice(h->device);
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
-    void *ptrs[] = {h->d_pbase, h->d_pwide, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_rrec, h->d_open_pages,
-                    h->d_rank_pages, h->d_rank_pstart, h->d_rank_fill, h->d_bucket_ranks, h->d_rank2b, h->d_tcnt, h->d_tlist, h->d_all_pages,
-                    h->d_all_fill, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_gcut, h->d_gcut_next, h->d_spec, h->d_specn, h->d_utypes, h->d_rq_rank, h->d_rq_types,
+    void *ptrs[] = {h->d_tab, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_rrec,
+                    h->d_tcnt, h->d_tlist, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_gcut, h->d_gcut_next, h->d_spec, h->d_specn, h->d_utypes, h->d_rq_rank, h->d_rq_types,
                     h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
@@ -1135,6 +1173,10 @@ int adlbq_destroy(adlbq_server *h) {
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
     if (h->h_snap) hipHostFree(h->h_snap);
+    for (int q = 0; q < 2; q++) {
+        if (h->h_tab[q]) hipHostFree(h->h_tab[q]);
+        if (h->tab_ev[q]) hipEventDestroy(h->tab_ev[q]);
+    }
     if (h->h_steal) hipHostFree(h->h_steal);
     if (h->h_apply) hipHostFree(h->h_apply);
     if (h->h_crem) hipHostFree(h->h_crem);
@@ -1160,13 +1202,40 @@ int adlbq_destroy(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
+// the put path's type lookup (get_type_idx, adlb.c:3476-3485): a dense table over
+// the declared types' value range when it is small, the map otherwise
+static inline int type_index(adlbq_server *h, int v) {
+    if (h->tindex.empty()) return -1;
+    if (h->tindex_dense.empty() && h->tindex.size() <= 4096) {
+        int lo = INT_MAX, hi = INT_MIN;
+        for (const auto &kv : h->tindex) lo = std::min(lo, kv.first), hi = std::max(hi, kv.first);
+        if ((long long)hi - lo < (1 << 20)) {
+            h->tindex_lo = lo;
+            h->tindex_dense.assign((size_t)((long long)hi - lo + 1), -1);
+            for (const auto &kv : h->tindex) h->tindex_dense[(size_t)(kv.first - lo)] = kv.second;
+        }
+    }
+    if (!h->tindex_dense.empty()) {
+        const long long d = (long long)v - h->tindex_lo;
+        return (d >= 0 && d < (long long)h->tindex_dense.size()) ? h->tindex_dense[(size_t)d] : -1;
+    }
+    auto it = h->tindex.find(v);
+    return it == h->tindex.end() ? -1 : it->second;
+}
+
 static int rank_bucket(adlbq_server *h, int target) {
+    if (target < h->A && h->rank_index_dense.size() == (size_t)h->A && h->rank_index_dense[(size_t)target] >= 0)
+        return h->rank_index_dense[(size_t)target];
     auto it = h->rank_index.find(target);
     if (it != h->rank_index.end()) return it->second;
     int k = (int)h->bucket_ranks.size();
     h->bucket_ranks.push_back(target);
     h->rankb.emplace_back();
     h->rank_index[target] = k;
+    if (target < h->A) {
+        if (h->rank_index_dense.size() != (size_t)h->A) h->rank_index_dense.assign((size_t)h->A, -1);
+        h->rank_index_dense[(size_t)target] = k;
+    }
     return k;
 }
 
@@ -1178,7 +1247,7 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
     if (n == 0) return ADLBQ_OK;
     hipSetDevice(h->device);
     for (int i = 0; i < n; i++)
-        if (!h->tindex.count(units9[9 * i])) return fail(ADLBQ_ERR_TYPE, "adlbq_put_batch: undeclared work type");
+        if (type_index(h, units9[9 * i]) < 0) return fail(ADLBQ_ERR_TYPE, "adlbq_put_batch: undeclared work type");
     int rc;
     // records are staged in pinned memory, two buffers used in turn: the copy out of
     // this one (two batches ago) must have completed; so must the device record buffer's readers
@@ -1222,7 +1291,7 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
         h->tables_dirty = true;
         long long slot = ((long long)b->pages.back() << PAGE_SHIFT) + b->tail_fill++;
         int seq = h->next_wqseqno++;
-        int ti = h->tindex[u[0]];
+        const int ti = type_index(h, u[0]);
         PutRec &r = rec[i];
         r.slot = (int)slot;
         r.prio = u[1];

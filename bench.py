@@ -475,11 +475,19 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         with torch.cuda.stream(stream):
             d_pout = torch.empty((P, 3), dtype=torch.int32, device=dev)
 
+    host_parts = {"put": 0.0, "reserve": 0.0, "unreserve": 0.0}
+
     def step(b):
+        t0 = time.perf_counter()
         if puts is not None:  # device-resident results: no host round trip
             srv.put_batch_device(puts[b], d_pout.data_ptr())
+        t1 = time.perf_counter()
         srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        t2 = time.perf_counter()
         srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        host_parts["put"] += t1 - t0
+        host_parts["reserve"] += t2 - t1
+        host_parts["unreserve"] += time.perf_counter() - t2
 
     for b in range(W4):
         step(b)
@@ -498,6 +506,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     host = 0.0
+    for k in host_parts:
+        host_parts[k] = 0.0
     for b in range(W4, nb):
         th = time.perf_counter()
         step(b)
@@ -531,6 +541,7 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "ms_per_step": el * 1e3 / steps,
         "matched_per_step": matched / steps,
         "host_call_ms_per_step": round(host * 1e3 / steps, 3),
+        "host_call_parts_ms": {k: round(v * 1e3 / steps, 3) for k, v in host_parts.items()},
         "stages_ms": stages,
         "scaling": "weak",
     }
