@@ -229,6 +229,10 @@ int adlbq_steal_check(adlbq_server *h, int *bad_grants, int *bad_deletes);
  * _responses: the replies of the local Reserves the round settled, rows
  * {shard, rqseqno, rank, TA_RESERVE_RESP[12]}; _check: adlbq_steal_check
  * summed over the shards (synchronises). */
+/* A group's shards list every later Reserve batch's candidates k deeper than
+ * its demand: an export right after a shard's batch (nothing else changed its
+ * wq since) gathers the k best available units per type from that batch's
+ * lists instead of scanning again; results are the same either way. */
 typedef struct adlbq_steal_group adlbq_steal_group;
 int adlbq_steal_group_create(adlbq_steal_group **g, adlbq_server **shards, int n, int k, int rqcap);
 long long adlbq_steal_group_blob_ints(adlbq_steal_group *g);
@@ -337,7 +341,9 @@ long long adlbq_stat(adlbq_server *h, const char *name);
  * sort of its own rather than a shared segmented sort (default 16384) when the
  * lists are not sorted together; "segsort_merged" = 1 (default) sorts every
  * list in one device-wide radix sort when no list's keys differ in their top
- * 6 bits, 0 always sorts list by list.
+ * 6 bits, 0 always sorts list by list; "segsort_async" = 1 (default) sizes
+ * that merged sort from the last landed batch's plan instead of reading the
+ * list bounds back (a plan that does not hold leaves the sort to k_rank).
  * Results never depend on them; tests lower them to force the other paths. */
 int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);
