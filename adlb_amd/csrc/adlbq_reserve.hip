@@ -31,7 +31,6 @@
 #include "adlbq_impl.h"
 
 #include <rocprim/device/device_merge.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
 
 using namespace adlbq;
 
@@ -2738,18 +2737,6 @@ __global__ __launch_bounds__(256) void k_unmerge_plan(const int *__restrict__ pl
     if (blockIdx.x == 0 && threadIdx.x == 0 && needsort[t] == 1) needsort[t] = 2;
 }
 
-// The merged candidate sort: rocPRIM's onesweep radix sort at every size (its
-// default sorts below 2^20 items by block sort + merge passes, ~20 launches of
-// a few µs each at config-4 sizes; onesweep is one launch per 8-bit digit).
-// Stable, like hipcub's.
-using OnesweepAlways = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                  rocprim::default_config, 0>;
-static hipError_t sort_pairs_desc(void *tmp, size_t &bytes, unsigned long long *kin, unsigned long long *kout,
-                                  int *vin, int *vout, int n, int lo, hipStream_t s) {
-    return rocprim::radix_sort_pairs_desc<OnesweepAlways>(tmp, bytes, kin, kout, vin, vout, (size_t)n,
-                                                          (unsigned int)lo, 64u, s);
-}
-
 // the sync-free merged sort (see k_sort_plan); false when no plan has landed yet
 static int launch_segsort_planned(adlbq_server *h, bool *done) {
     *done = false;
@@ -2779,7 +2766,8 @@ static int launch_segsort_planned(adlbq_server *h, bool *done) {
     k_merge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_ckey2);
     k_merge_pad<<<std::min(1024, (g_bound + 255) / 256 + 1), 256, 0, s>>>(h->d_plan, g_bound, h->d_ckey2);
     size_t tmp = 0;
-    AQ_HIP(sort_pairs_desc(nullptr, tmp, h->d_ckey2, h->d_ckey3, h->d_cslot, h->d_cslot3, g_bound, lo_hint, s));
+    AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey2, h->d_ckey3, h->d_cslot,
+                                                        h->d_cslot3, g_bound, lo_hint, 64, s));
     if (tmp > h->cap_ssort) {
         AQ_HIP(hipStreamSynchronize(s));
         if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
@@ -2787,7 +2775,8 @@ static int launch_segsort_planned(adlbq_server *h, bool *done) {
         AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
     }
     size_t t2 = h->cap_ssort;
-    AQ_HIP(sort_pairs_desc(h->d_ssort, t2, h->d_ckey2, h->d_ckey3, h->d_cslot, h->d_cslot3, g_bound, lo_hint, s));
+    AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey2, h->d_ckey3, h->d_cslot,
+                                                        h->d_cslot3, g_bound, lo_hint, 64, s));
     k_unmerge_plan<<<dim3(kgx, T), 256, 0, s>>>(h->d_plan, h->d_candoff, h->d_candlen, h->d_kb, h->d_ckey3,
                                                  h->d_cslot3, h->d_ckey, h->d_cslot, h->d_needsort);
     AQ_HIP(hipGetLastError());
