@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
 FIXTURES = sorted(f for f in os.listdir(GOLD) if f.startswith(("nq_", "mix_")))
 MIX = os.path.join(ROOT, "tests", "apps", "adlb_mix")
+PUSH = os.path.join(ROOT, "tests", "apps", "adlb_push")
 NQ_AMD = os.path.join(ROOT, "oracle", "_ref", "nq_amd")
 MPIRUN = "/opt/conda/bin/mpirun"
 
@@ -106,3 +107,24 @@ def test_mix_put_rejection_walk():
     assert got == exp, out[-2000:]
     rej = [float(ln.split()[-1]) for ln in out.splitlines() if ln.startswith("server")]
     assert rej and sum(rej) > 0, out[-2000:]
+
+
+@pytest.mark.gpu
+def test_push_live():
+    """Memory-pressure push under MPI (tests/apps/adlb_push.c): one server
+    holds every targeted unit past 0.95 x its memory limit and pushes units to
+    the other; the target rank still receives every unit exactly once (through
+    SS_MOVING_TARGETED_WORK, the tq and SS_RFR)."""
+    if not os.path.exists(PUSH):
+        pytest.skip("tests/apps/adlb_push not built")
+    env = dict(os.environ, ADLB_DEVICE="0")
+    r = subprocess.run([MPIRUN, "-np", "6", PUSH, "-n", "300", "-len", "1000", "-hi", "80000"], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"rc={r.returncode}\nstdout:\n{r.stdout[-3000:]}\nstderr:\n{r.stderr[-3000:]}"
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("adlb_push:")]
+    assert line, r.stdout[-2000:]
+    v = line[0].split()
+    assert (int(v[2]), int(v[4])) == (int(v[6]), int(v[7])), r.stdout[-2000:]
+    pushed = [ln.split() for ln in r.stdout.splitlines() if ln.startswith("server")]
+    assert sum(int(p[3]) for p in pushed) > 0, r.stdout[-2000:]
+    assert sum(int(p[3]) for p in pushed) == sum(int(p[4]) for p in pushed), r.stdout[-2000:]
