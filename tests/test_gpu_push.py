@@ -44,7 +44,7 @@ def only(replies, tag):
 
 
 @pytest.fixture
-def cores(gpu_available):
+def cores():
     from adlb_amd.core import Core
     # the pusher holds little (threshold 0.95 * 2000 B); the pushee has room
     with Core(TYPES, A_RANKS, 2, PUSHER, max_malloc=2000, device=0) as a, \
@@ -111,7 +111,7 @@ def test_push_del_when_reserved_meanwhile(cores):
     assert a.info_get(3) == 0 and b.info_get(4) == 0
 
 
-def test_push_declined_when_pushee_full(gpu_available):
+def test_push_declined_when_pushee_full():
     from adlb_amd.core import Core
     with Core(TYPES, A_RANKS, 2, PUSHER, max_malloc=2000, device=0) as a, \
             Core(TYPES, A_RANKS, 2, PUSHEE, max_malloc=500, device=0) as b:
