@@ -119,26 +119,26 @@ bool sort_hint(adlbq_server *h) {
     return i >= 0 && h->h_snap[i].needsort_last != 0;
 }
 
-constexpr long long RQ_GROW_MAX = 1ll << 24;  // rq entries grown to rather than waited for
+constexpr long long RQ_GROW_MAX = 1ll << 24;  // rq entries a growth step reserves at most for batches in flight
 
 int ensure_rq_capacity(adlbq_server *h, int extra) {
     long long need = (h->ctr_stale ? h->rq_n_upper : (long long)h->ctr.rq_n) + extra;
     if (need <= h->rq_cap) return ADLBQ_OK;
     if (h->ctr_stale) {
         // the bound is loose by the batches still in flight: use the newest
-        // landed snapshot; if that is not enough, grow (the rq costs 76 B per
-        // entry: room for the batches in flight is cheaper than waiting for
-        // them), and only past RQ_GROW_MAX wait for the oldest tracked batch
+        // landed snapshot and, if that is not enough, wait for the oldest
+        // tracked batch (the host then runs at most NSNAP batches ahead)
         tighten_rq_bound(h, false);
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
-        if (need > RQ_GROW_MAX) {
-            tighten_rq_bound(h, true);
-            need = h->rq_n_upper + extra;
-            if (need <= h->rq_cap) return ADLBQ_OK;
-        }
+        tighten_rq_bound(h, true);
+        need = h->rq_n_upper + extra;
+        if (need <= h->rq_cap) return ADLBQ_OK;
     }
+    // room for NSNAP batches of this size in flight at once (76 B per entry),
+    // so that the wait above is the snapshot ring's, not a reallocation's
     long long nc = std::max<long long>(need, (long long)h->rq_cap * 2);
+    nc = std::max<long long>(nc, std::min<long long>((long long)(adlbq_server::NSNAP + 1) * extra, RQ_GROW_MAX));
     nc = std::max<long long>(nc, 1024);
     int rc;
     if ((rc = grow(&h->d_rq_rank, h->rq_cap, nc, h->stream))) return rc;

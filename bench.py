@@ -38,6 +38,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
+ADLBQ_RESERVE_INTS = 18  # include/adlbq.h
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -89,6 +91,8 @@ def parse():
     ap.add_argument("--c4-chain-rounds", type=int, default=None,
                     help="config 4: ordered-choice round launches after round 0 (adlbq 'chain_rounds')")
     ap.add_argument("--chain-rounds", type=int, default=None, help="metric leg: adlbq 'chain_rounds'")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="metric leg: skip the host-buffer (PCIe-inclusive) adlbq_reserve_batch measurement")
     ap.add_argument("--chain-stamps", action="store_true",
                     help="metric leg: after the timed region, one batch with the chain's phase stamps (diagnostic)")
     ap.add_argument("--c4-chain-modes", type=int, default=None, help="config 4: adlbq 'chain_modes'")
@@ -131,7 +135,7 @@ def pmc_traffic(args) -> dict | None:
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu", "--no-pmc",
              "--no-config3", "--no-config4", "--no-config5",
-             "--no-profile", "--units", str(args.units), "--reserves", str(args.reserves), "--types",
+             "--no-profile", "--no-host-path", "--units", str(args.units), "--reserves", str(args.reserves), "--types",
              str(args.types), "--seed", str(args.seed)] + (["--equal-prio"] if args.equal_prio else [])
     out = {}
     tmp = tempfile.mkdtemp(prefix="adlbq_pmc_")
@@ -672,6 +676,31 @@ def main():
             dom_timed = round((ms - base_dom[0]) / (n - base_dom[1]), 4)
             stages[dominant] = dom_timed
 
+    # the host-buffer boundary (adlbq_reserve_batch: requests from host memory,
+    # responses back, synchronous): the PCIe-inclusive rate, reported beside
+    # `value`, never as it (untimed by the driver's clock)
+    host_path = None
+    if not args.no_host_path:
+        hb = min(args.steps, 10)
+        torch.cuda.synchronize()
+        t_res = 0.0
+        t1 = time.perf_counter()
+        for i in range(hb):
+            b = args.warmup + i % max(args.steps, 1)
+            th = time.perf_counter()
+            resp = srv.reserve_batch(reqs[b])
+            t_res += time.perf_counter() - th
+            d_resp[b].copy_(torch.from_numpy(resp).to(dev))  # restore the queue from these responses
+            torch.cuda.synchronize()
+            srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+            srv.sync()
+        host_path = {"entry": "adlbq_reserve_batch (host buffers, synchronous)",
+                     "ms_per_batch": round(t_res * 1e3 / hb, 4),
+                     "assignments_per_s": round(int((d_resp[args.warmup:args.warmup + hb, :, 0] == 1).sum().item())
+                                                / t_res, 1) if t_res else None,
+                     "bytes_over_pcie_per_batch": (ADLBQ_RESERVE_INTS * 4 + 12 * 4) * R,
+                     "step_ms_with_restore": round((time.perf_counter() - t1) * 1e3 / hb, 4)}
+
     phases = None
     if args.chain_stamps:
         srv.set_param("chain_stamps", 1)
@@ -718,6 +747,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps,
         "host_submit_ms_per_step": round(t_submit * 1e3 / args.steps, 4),
+        "host_buffer_path": host_path,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
