@@ -113,7 +113,7 @@ def parse():
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
 KERNEL_OF = {"hist": "k_prep_hist", "thresholds": "k_thresholds",
              "select": "k_select_open", "sort": "k_keybits + merged hipcub radix sort",
-             "targeted": "k_targeted_idx", "rank": "k_rank", "chain": "k_chain", "finalize": "k_finalize"}
+             "targeted": "k_targeted_idx", "rank": "k_rank", "chain": "k_chain0", "finalize": "k_finalize"}
 
 
 def _kernel_base(name: str) -> str:
