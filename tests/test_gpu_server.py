@@ -25,6 +25,7 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 FIXTURES = sorted(f for f in os.listdir(GOLD) if f.startswith(("nq_", "mix_")))
 MIX = os.path.join(ROOT, "tests", "apps", "adlb_mix")
 PUSH = os.path.join(ROOT, "tests", "apps", "adlb_push")
+FCALL = os.path.join(ROOT, "tests", "apps", "adlb_fcall")
 NQ_AMD = os.path.join(ROOT, "oracle", "_ref", "nq_amd")
 MPIRUN = "/opt/conda/bin/mpirun"
 
@@ -128,3 +129,22 @@ def test_push_live():
     pushed = [ln.split() for ln in r.stdout.splitlines() if ln.startswith("server")]
     assert sum(int(p[3]) for p in pushed) > 0, r.stdout[-2000:]
     assert sum(int(p[3]) for p in pushed) == sum(int(p[4]) for p in pushed), r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_fortran_bindings_live():
+    """An application driven only through the Fortran entry points
+    (tests/apps/adlb_fcall.c calls adlb_init_ ... adlb_finalize_ by reference,
+    as compiled Fortran does; reference src/adlbf.c): a batch with a common
+    prefix, Reserve/Ireserve/Get_reserved(_timed), Info_num_work_units, and
+    the job ends by exhaustion with every unit taken once."""
+    if not os.path.exists(FCALL):
+        pytest.skip("tests/apps/adlb_fcall not built")
+    env = dict(os.environ, ADLB_DEVICE="0")
+    r = subprocess.run([MPIRUN, "-np", "6", FCALL, "-n", "200"], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, f"rc={r.returncode}\nstdout:\n{r.stdout[-3000:]}\nstderr:\n{r.stderr[-3000:]}"
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("adlb_fcall:")]
+    assert line, r.stdout[-2000:]
+    v = line[0].split()
+    assert (int(v[2]), int(v[4])) == (int(v[6]), int(v[7])), r.stdout[-2000:]

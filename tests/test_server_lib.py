@@ -34,6 +34,21 @@ def test_libadlb_exports_public_api():
     assert not missing, missing
 
 
+# the Fortran bindings of reference src/adlbf.c:6-103 (lower-case + '_')
+FORTRAN = ["adlb_init_", "adlb_server_", "adlb_debug_server_", "adlb_put_", "adlb_reserve_", "adlb_ireserve_",
+           "adlb_get_reserved_", "adlb_get_reserved_timed_", "adlb_begin_batch_put_", "adlb_end_batch_put_",
+           "adlb_begin_batch_put_2_", "adlb_end_batch_put_2_", "adlb_set_no_more_work_",
+           "adlb_set_problem_done_", "adlb_info_get_", "adlb_info_num_work_units_", "adlb_finalize_",
+           "adlb_abort_"]
+
+
+def test_libadlb_exports_fortran_bindings():
+    if not os.path.exists(LIBADLB):
+        pytest.skip("libadlb.so not built")
+    missing = sorted(set(FORTRAN) - _exports(LIBADLB))
+    assert not missing, missing
+
+
 def test_core_binding_covers_header():
     from adlb_amd import core
     txt = open(core.HEADER).read()
