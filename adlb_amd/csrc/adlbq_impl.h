@@ -14,6 +14,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -92,6 +93,7 @@ struct StageTimer {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     double total_ms = 0;
     long long launches = 0;
+    long long host_ns = 0;  // host time spent issuing the stage (stage_begin .. stage_end)
 };
 
 }  // namespace adlbq
@@ -300,6 +302,7 @@ struct adlbq_server {
     std::string profile_only;                 // empty: every stage
     std::vector<hipEvent_t> event_pool;
     std::unordered_map<std::string, adlbq::StageTimer> timers;
+    std::chrono::steady_clock::time_point stage_host_t0;
 };
 
 namespace adlbq {
@@ -324,6 +327,8 @@ bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
+// host time since t0 added to stage `name` (profiling only; no events)
+void host_stage_add(adlbq_server *h, const char *name, std::chrono::steady_clock::time_point t0);
 int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail);
 bool launch_export_after(adlbq_server *h, int k, int *d_recs, int *d_nrec, long long *d_navail);

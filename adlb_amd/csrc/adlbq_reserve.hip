@@ -2900,6 +2900,7 @@ static int launch_segsort(adlbq_server *h) {
 
 int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
+    const auto host_t0 = std::chrono::steady_clock::now();
     h->hint_stamp++;  // landed-snapshot hints are looked up once for this launch
     if ((rc = ensure_req_capacity(h, R))) return rc;
     if ((rc = sync_tables(h))) return rc;
@@ -2937,11 +2938,16 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         pa.tlist = h->d_tlist;
         pa.tcap = tcap;
     }
+    host_stage_add(h, "pre", host_t0);
+    const auto scan_t0 = std::chrono::steady_clock::now();
     if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) return rc;
+    host_stage_add(h, "scan", scan_t0);
     h->last_scan_units = h->live_units - h->live_targeted;
 
     if (targeted) {
+        const auto ti_t0 = std::chrono::steady_clock::now();
         if (nb < (1 << 20) && (rc = ensure_tindex(h))) return rc;
+        host_stage_add(h, "tindex", ti_t0);
         stage_begin(h, "targeted", &ev);
         if (nb < (1 << 20))
             k_targeted_idx<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_tkeys,

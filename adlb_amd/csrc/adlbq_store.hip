@@ -307,13 +307,23 @@ void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev) {
     if (!stage_on(h, name)) return;
     *ev = pooled_event(h);
     hipEventRecord(*ev, h->stream);
+    h->stage_host_t0 = std::chrono::steady_clock::now();
 }
 
 void stage_end(adlbq_server *h, const char *name, hipEvent_t ev) {
     if (!ev) return;
     hipEvent_t e2 = pooled_event(h);
     hipEventRecord(e2, h->stream);
-    h->timers[name].pending.push_back({ev, e2});
+    auto &t = h->timers[name];
+    t.pending.push_back({ev, e2});
+    t.host_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                      h->stage_host_t0).count();
+}
+
+void host_stage_add(adlbq_server *h, const char *name, std::chrono::steady_clock::time_point t0) {
+    if (!stage_on(h, name)) return;
+    h->timers[name].host_ns +=
+        std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 
 }  // namespace adlbq
@@ -2033,6 +2043,10 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         return v;
     }
     if (n == "device_sorted_lists") return h->n_segsort;  // candidate lists given a device-wide sort (cumulative)
+    if (n.rfind("host_ns:", 0) == 0) {  // host time issuing a profiled stage (adlbq_profile_only)
+        auto it = h->timers.find(n.substr(8));
+        return it == h->timers.end() ? 0 : it->second.host_ns;
+    }
     if (n == "sort_async") return h->n_sort_async;         // merged sorts planned from the last landed batch (cumulative)
     if (n == "sort_async_bad") {  // ... whose plan did not hold (k_rank sorted them), as of the newest landed batch
         refresh_counters(h);

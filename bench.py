@@ -498,12 +498,16 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     torch.cuda.synchronize()
     srv.profile(True)
     base = {st: srv.profile_read(st) for st in STAGES}
+    hbase = {st: srv.stat("host_ns:" + st) for st in (*STAGES, "pre", "scan", "tindex")}
     step(W4 - 1)
-    stages = {}
+    stages, stages_host = {}, {}
     for st in STAGES:
         ms, n = srv.profile_read(st)
         if n - base[st][1]:
             stages[st] = round((ms - base[st][0]) / (n - base[st][1]), 4)
+            stages_host[st] = round((srv.stat("host_ns:" + st) - hbase[st]) / 1e6 / (n - base[st][1]), 4)
+    for st in ("pre", "scan", "tindex"):  # host-only parts of the reserve call (one profiled step)
+        stages_host[st] = round((srv.stat("host_ns:" + st) - hbase.get(st, 0)) / 1e6, 4)
     srv.profile(False)
     if world > 1:
         dist.barrier()
@@ -547,6 +551,7 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "host_call_ms_per_step": round(host * 1e3 / steps, 3),
         "host_call_parts_ms": {k: round(v * 1e3 / steps, 3) for k, v in host_parts.items()},
         "stages_ms": stages,
+        "stages_host_ms": stages_host,
         "scaling": "weak",
     }
     if per_batch:
