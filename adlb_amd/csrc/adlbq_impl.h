@@ -72,6 +72,7 @@ struct DevCounters {
     int needsort_last;     // the last reserve batch had a type whose threshold fell in a multi-prio bin
     int plan_g, plan_lo;   // the last candidate sort plan: candidates in all, lowest key bit any list varies in
     int plan_missed;       // sync-free sorts whose plan did not hold (k_rank sorted in-launch), cumulative
+    int plan_phi;          // highest bit of the prio field any candidate list varies in (-1: none)
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
     // the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced (adlb.c:3419-3474) over the
     // structures this handle replaces, plus what the caller adds (adlbq_bytes_adjust)
@@ -247,6 +248,11 @@ struct adlbq_server {
     int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort
     // launch_segsort's sync-free path: sorted merged keys / slots land here, the plan (valid, G, lo) on the device
     unsigned long long *d_ckey3 = nullptr; int *d_cslot3 = nullptr; long long cap_c3 = 0; int *d_plan = nullptr;
+    // the candidate radix sort (rsort_*): 32-bit keys + indices, ping-pong; per-(digit, tile) counts; per-list OR / AND
+    unsigned int *d_rs = nullptr; long long cap_rs = 0; int *d_rs_cnt = nullptr; long long cap_rs_cnt = 0;
+    unsigned int *d_rs_acc = nullptr; int rs_parity = 0;
+    int segsort_radix = 1;             // "segsort_radix": the hand-written list-stable radix sort in the sync-free plan
+    long long n_sort_radix = 0;
     int segsort_async = 1;             // "segsort_async": plan the merged sort from the last landed batch (no sync)
     long long n_sort_async = 0;
     long long n_segsort = 0;                          // lists given a device-wide sort (cumulative)
@@ -321,7 +327,7 @@ int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
-bool plan_hint(adlbq_server *h, int *g, int *lo);
+bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi = nullptr);
 inline void wq_changed(adlbq_server *h) { h->batch_export_k = 0; }  // the last batch's lists no longer describe the wq  // newest landed batch's candidate sort plan
 bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);

@@ -308,17 +308,19 @@ __device__ __forceinline__ long long cut_of(int th, long long an) {
 // write-through and read back the same way) finds the bin where the type's
 // demand is reached and how many units of it are needed.  Candidate list
 // offsets (the prefix of candlen over types) follow in k_select_open.
-__global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
+constexpr int TH_THREADS = 1024;  // one pass over up to 1024 chunks (33M units) per column
+__global__ __launch_bounds__(TH_THREADS) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
                                                      int *type_cnt, const long long *__restrict__ anchor,
                                                      long long *__restrict__ anchor_next,
                                                      long long *__restrict__ gcut_next, int guess) {
-    __shared__ unsigned int wsum[4];
+    constexpr int NW = TH_THREADS / 64;
+    __shared__ unsigned int wsum[NW];
     __shared__ bool s_last;
     const int c = blockIdx.x, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     unsigned int carry = 0;
-    for (int k0 = 0; k0 < nchunks; k0 += 256) {
+    for (int k0 = 0; k0 < nchunks; k0 += TH_THREADS) {
         const int k = k0 + threadIdx.x;
         const unsigned int v = k < nchunks ? csum[(long long)k * C + c] : 0u;
         unsigned int x = v;  // block inclusive scan
@@ -332,7 +334,8 @@ __global__ __launch_bounds__(256) void k_thresholds(int T, const int *__restrict
         unsigned int pre = carry;
         for (int q = 0; q < w; q++) pre += wsum[q];
         if (k < nchunks) csum[(long long)k * C + c] = pre + x - v;
-        carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+#pragma unroll
+        for (int q = 0; q < NW; q++) carry += wsum[q];
         __syncthreads();
     }
     if (threadIdx.x == 0) {
@@ -2441,7 +2444,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     if (scan) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
         stage_begin(h, "thresholds", &ev);
-        k_thresholds<<<C, 256, 0, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
+        k_thresholds<<<C, TH_THREADS, 0, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                        h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor,
                                        h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0);
         stage_end(h, "thresholds", ev);
@@ -2702,8 +2705,12 @@ __global__ void k_sort_plan(int T, const int *__restrict__ candoff, const int *_
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) lo = min(lo, __shfl_xor(lo, o, 64));
     const bool ok = __ballot(bad_top) == 0ull, nsort = __ballot(wants) != 0ull;
+    unsigned int up = (unsigned int)(diff >> 32);  // prio-field bits this list varies in
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) up |= __shfl_xor(up, o, 64);
     if (t == 0) {
         const int G = candoff[T];
+        ctr->plan_phi = up ? 31 - __clz(up) : -1;
         lo = min(lo, LIST_SHIFT);
         plan[0] = (ok && nsort && G <= g_bound && lo >= lo_hint) ? 1 : 0;
         plan[1] = G;
@@ -2781,6 +2788,329 @@ static int launch_segsort_planned(adlbq_server *h, bool *done) {
                                                  h->d_cslot3, h->d_ckey, h->d_cslot, h->d_needsort);
     AQ_HIP(hipGetLastError());
     h->n_sort_async++;
+    *done = true;
+    return ADLBQ_OK;
+}
+
+// ---------------------------------------------------------------- list-stable radix sort
+// The candidate lists leave k_select_open in (column, bucket position) order,
+// and a list's columns cover descending, disjoint prio ranges: entries of equal
+// prio are already in key order.  Sorting every list STABLY by prio,
+// descending, therefore yields the full key order.  Sort key (32 bits): the
+// list index above the low pb bits of ~(key >> 32); the prio-field bits at and
+// above pb must be constant inside each list (checked on the device: per-list
+// OR / AND of the field).  LSD radix sort, 8-bit digits, RS_TILE entries per
+// 1024-thread workgroup, two launches per digit: count (per-tile digit counts)
+// and scatter (each tile sums the counts of the tiles before it and of the
+// smaller digits itself, then ranks its entries stably, a wave per 256).  The
+// payload moves once: k_rs_keys copies the lists aside (ckey3 / cslot3) and
+// the last scatter writes them back in order.  If the plan does not hold
+// (more candidates than planned, a list varying at or above pb, or nothing to
+// sort) every launch after k_rs_keys returns at once and k_rank sorts
+// in-launch (needsort stays 1): a stale plan costs time, never results.
+constexpr int RS_TILE = 4096, RS_THREADS = 1024, RS_WAVES = RS_THREADS / 64;
+constexpr int RS_WAVE_ITEMS = RS_TILE / RS_WAVES, RS_STEPS = RS_WAVE_ITEMS / 64;  // 4 steps of 64 per wave
+constexpr int RS_PARTS = RS_THREADS / 256;  // threads per digit in the tile-prefix sums
+
+struct RsArgs {
+    int T, pb, g_bound, nblk;
+    const int *candoff, *candlen;
+    int *needsort;
+    unsigned int *acc;       // [64] OR, [64] AND of each list's prio field (this batch)
+    unsigned int *acc_next;  // the other parity: reset here for the next batch
+    int *cnt;                // [nblk][256] digit counts per tile
+    DevCounters *ctr;
+};
+
+// does the plan hold for this batch
+__device__ __forceinline__ bool rs_plan_ok(const RsArgs &a, int *G_out, unsigned int *U_out, bool *want_out) {
+    unsigned int U = 0;
+    bool want = false;
+    for (int t = 0; t < a.T; t++) {
+        if (a.candlen[t] > 0) U |= a.acc[t] ^ a.acc[64 + t];
+        want |= a.needsort[t] == 1 && a.candlen[t] > 1;
+    }
+    const int G = a.candoff[a.T];
+    if (G_out) *G_out = G;
+    if (U_out) *U_out = U;
+    if (want_out) *want_out = want;
+    return want && G <= a.g_bound && (a.pb >= 32 || (U >> a.pb) == 0u);
+}
+
+__global__ __launch_bounds__(256) void k_rs_keys(RsArgs a, const unsigned long long *__restrict__ ckey,
+                                                 const int *__restrict__ cslot, unsigned long long *__restrict__ ckey3,
+                                                 int *__restrict__ cslot3, unsigned int *__restrict__ K,
+                                                 unsigned int *__restrict__ I) {
+    __shared__ int soff[ADLBQ_MAX_TYPES + 1];
+    __shared__ unsigned int sor[ADLBQ_MAX_TYPES], sand[ADLBQ_MAX_TYPES];
+    const int T = a.T;
+    for (int t = threadIdx.x; t <= T; t += blockDim.x) soff[t] = a.candoff[t];
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        sor[t] = 0u;
+        sand[t] = ~0u;
+        if (blockIdx.x == 0) {  // the next batch accumulates into the other parity
+            a.acc_next[t] = 0u;
+            a.acc_next[64 + t] = ~0u;
+        }
+    }
+    __syncthreads();
+    const int G = min(soff[T], a.g_bound);
+    const unsigned int pmask = a.pb >= 32 ? ~0u : ((1u << a.pb) - 1u);
+    for (int i0 = blockIdx.x * blockDim.x; i0 < G; i0 += gridDim.x * blockDim.x) {
+        const int i = i0 + threadIdx.x;
+        int t = 0;
+        unsigned int pf = 0;
+        if (i < G) {
+            int lo = 0, hi = T - 1;  // the last list starting at or before i
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (soff[mid] <= i) lo = mid;
+                else hi = mid - 1;
+            }
+            t = lo;
+            const unsigned long long k = ckey[i];
+            const int sl = cslot[i];
+            ckey3[i] = k;
+            cslot3[i] = sl;
+            pf = (unsigned int)(k >> 32);
+            K[i] = ((unsigned int)t << a.pb) | (~pf & pmask);
+            I[i] = (unsigned int)i;
+        }
+        // per-list OR / AND: one LDS update per wave when the wave lies in one list
+        const bool valid = i < G;
+        const int t0 = __shfl(t, 0, 64);
+        const bool uni = __ballot(valid && t != t0) == 0ull, any = __ballot(valid) != 0ull;
+        if (uni) {
+            unsigned int o = valid ? pf : 0u, n = valid ? pf : ~0u;
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) {
+                o |= __shfl_xor(o, d, 64);
+                n &= __shfl_xor(n, d, 64);
+            }
+            if ((threadIdx.x & 63) == 0 && any) {
+                atomicOr(&sor[t0], o);
+                atomicAnd(&sand[t0], n);
+            }
+        } else if (valid) {
+            atomicOr(&sor[t], pf);
+            atomicAnd(&sand[t], pf);
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+        if (sand[t] != ~0u || sor[t] != 0u) {
+            atomicOr(&a.acc[t], sor[t]);
+            atomicAnd(&a.acc[64 + t], sand[t]);
+        }
+}
+
+// lanes of this wave with the same 8-bit digit (valid lanes only)
+__device__ __forceinline__ unsigned long long rs_peers(unsigned int d, bool valid) {
+    unsigned long long m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const unsigned long long bb = __ballot((d >> b) & 1u);
+        m &= ((d >> b) & 1u) ? bb : ~bb;
+    }
+    return m;
+}
+
+__global__ __launch_bounds__(RS_THREADS) void k_rs_count(RsArgs a, int pass, const unsigned int *__restrict__ K) {
+    __shared__ unsigned int sc[256];
+    __shared__ int s_ok, s_G;
+    if (threadIdx.x == 0) {
+        int G = 0;
+        s_ok = rs_plan_ok(a, &G, nullptr, nullptr);
+        s_G = G;
+    }
+    if (threadIdx.x < 256) sc[threadIdx.x] = 0u;
+    __syncthreads();
+    if (!s_ok) return;
+    const int G = s_G, b = blockIdx.x, sh = 8 * pass, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int st = 0; st < RS_STEPS; st++) {
+        const int i = b * RS_TILE + w * RS_WAVE_ITEMS + st * 64 + lane;
+        const bool valid = i < G;
+        const unsigned int d = valid ? (K[i] >> sh) & 255u : 0u;
+        const unsigned long long pe = rs_peers(d, valid);
+        if (valid && (pe & lt) == 0ull) atomicAdd(&sc[d], (unsigned int)__popcll(pe));
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) a.cnt[(long long)b * 256 + threadIdx.x] = (int)sc[threadIdx.x];
+}
+
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsArgs a, int pass, int last,
+                                                           const unsigned int *__restrict__ K,
+                                                           const unsigned int *__restrict__ I,
+                                                           unsigned int *__restrict__ Ko, unsigned int *__restrict__ Io,
+                                                           const unsigned long long *__restrict__ ckey3,
+                                                           const int *__restrict__ cslot3, unsigned long long *ckey,
+                                                           int *cslot) {
+    __shared__ unsigned int wc[RS_WAVES][256];
+    __shared__ unsigned int spre[RS_PARTS][256], stot[RS_PARTS][256];
+    __shared__ unsigned int wsum[4];
+    __shared__ int s_ok, s_G;
+    const int b = blockIdx.x, sh = 8 * pass, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        int G = 0;
+        unsigned int U = 0;
+        bool want = false;
+        const bool ok = rs_plan_ok(a, &G, &U, &want);
+        if (last && b == 0) {  // this batch's figures, for the next batch's plan
+            if (want && !ok) a.ctr->plan_missed += 1;
+            a.ctr->plan_g = G;
+            a.ctr->plan_phi = U ? 31 - __clz(U) : -1;
+            a.ctr->plan_lo = 0;
+        }
+        s_ok = ok;
+        s_G = G;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int G = s_G;
+    {  // counts of digit d in the tiles before this one, and in all tiles
+        const int d = threadIdx.x & 255, q = threadIdx.x >> 8;
+        unsigned int pre = 0, tot = 0;
+        for (int bb = q; bb < a.nblk; bb += RS_PARTS) {
+            const unsigned int v = (unsigned int)a.cnt[(long long)bb * 256 + d];
+            tot += v;
+            pre += bb < b ? v : 0u;
+        }
+        spre[q][d] = pre;
+        stot[q][d] = tot;
+    }
+    for (int q = 0; q < RS_WAVES; q++)
+        if (threadIdx.x < 256) wc[q][threadIdx.x] = 0u;
+    __syncthreads();
+    if (threadIdx.x < 256) {  // exclusive scan of the digit totals: this tile's start per digit
+        const int d = threadIdx.x;
+        unsigned int tot = 0, pre = 0;
+#pragma unroll
+        for (int q = 0; q < RS_PARTS; q++) {
+            tot += stot[q][d];
+            pre += spre[q][d];
+        }
+        unsigned int x = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        spre[0][d] = x - tot + pre;  // wave-local exclusive prefix + earlier tiles (waves added below)
+    }
+    __syncthreads();
+    unsigned int key[RS_STEPS], idx[RS_STEPS], pos[RS_STEPS];
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int st = 0; st < RS_STEPS; st++) {
+        const int i = b * RS_TILE + w * RS_WAVE_ITEMS + st * 64 + lane;
+        const bool valid = i < G;
+        key[st] = valid ? K[i] : 0u;
+        idx[st] = valid ? I[i] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int st = 0; st < RS_STEPS; st++) {
+        const bool valid = idx[st] != 0xffffffffu;
+        const unsigned int d = (key[st] >> sh) & 255u;
+        const unsigned long long pe = rs_peers(d, valid);
+        const unsigned int before = wc[w][d];
+        pos[st] = before + (unsigned int)__popcll(pe & lt);
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (pe & lt) == 0ull) wc[w][d] = before + (unsigned int)__popcll(pe);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) {  // per digit: the tile's global start plus the counts of the earlier waves
+        const int d = threadIdx.x;
+        unsigned int run = spre[0][d];
+        for (int q = 0; q < (d >> 6); q++) run += wsum[q];
+        for (int q = 0; q < RS_WAVES; q++) {
+            const unsigned int c = wc[q][d];
+            wc[q][d] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < RS_STEPS; st++) {
+        if (idx[st] == 0xffffffffu) continue;
+        const unsigned int d = (key[st] >> sh) & 255u;
+        const unsigned int dst = wc[w][d] + pos[st];
+        if (!last) {
+            Ko[dst] = key[st];
+            Io[dst] = idx[st];
+        } else {
+            ckey[dst] = ckey3[idx[st]];
+            cslot[dst] = cslot3[idx[st]];
+        }
+    }
+    if (last && b == 0)
+        for (int t = threadIdx.x; t < a.T; t += blockDim.x)
+            if (a.needsort[t] == 1) a.needsort[t] = 2;
+}
+
+// the sync-free plan as the list-stable radix sort; false (not done) when no
+// plan has landed or the keys would not fit 32 bits
+static int launch_segsort_radix(adlbq_server *h, bool *done) {
+    *done = false;
+    int g_last = 0, lo_last = 0, phi_last = -1;
+    if (!h->segsort_radix || !h->segsort_async || !plan_hint(h, &g_last, &lo_last, &phi_last)) return ADLBQ_OK;
+    const int T = h->T;
+    if (T < 1 || T > ADLBQ_MAX_TYPES) return ADLBQ_OK;
+    const int tb = T > 1 ? 32 - __builtin_clz((unsigned int)(T - 1)) : 0;
+    int pb = std::max(1, std::min(31, phi_last + 3));  // two bits of margin above the last batch's
+    const int passes = (tb + pb + 7) / 8;
+    pb = std::min(31, passes * 8 - tb);  // the last digit's spare bits widen the margin for free
+    if (tb + pb > 32 || pb <= phi_last) return ADLBQ_OK;
+    hipStream_t s = h->stream;
+    const long long gb = std::min<long long>(h->cap_cand, (long long)g_last + g_last / 4 + 4096);
+    const int nblk = (int)((gb + RS_TILE - 1) / RS_TILE);
+    if (gb > h->cap_c3 || 4 * gb > h->cap_rs || 256ll * nblk > h->cap_rs_cnt) {
+        AQ_HIP(hipStreamSynchronize(s));
+        if (gb > h->cap_c3) {
+            if (h->d_ckey3) AQ_HIP(hipFree(h->d_ckey3));
+            if (h->d_cslot3) AQ_HIP(hipFree(h->d_cslot3));
+            h->cap_c3 = std::min(std::max(gb, h->cap_cand / 4), h->cap_cand);
+            AQ_HIP(hipMalloc((void **)&h->d_ckey3, sizeof(unsigned long long) * h->cap_c3));
+            AQ_HIP(hipMalloc((void **)&h->d_cslot3, sizeof(int) * h->cap_c3));
+        }
+        if (4 * gb > h->cap_rs) {
+            if (h->d_rs) AQ_HIP(hipFree(h->d_rs));
+            h->cap_rs = 4 * std::max(gb, h->cap_cand / 4);
+            AQ_HIP(hipMalloc((void **)&h->d_rs, sizeof(unsigned int) * h->cap_rs));
+        }
+        if (256ll * nblk > h->cap_rs_cnt) {
+            if (h->d_rs_cnt) AQ_HIP(hipFree(h->d_rs_cnt));
+            h->cap_rs_cnt = 256ll * std::max<long long>(nblk, (h->cap_cand / 4 + RS_TILE - 1) / RS_TILE);
+            AQ_HIP(hipMalloc((void **)&h->d_rs_cnt, sizeof(int) * h->cap_rs_cnt));
+        }
+    }
+    if (!h->d_rs_acc) {  // two parities of [64] OR, [64] AND
+        AQ_HIP(hipMalloc((void **)&h->d_rs_acc, sizeof(unsigned int) * 256));
+        for (int q = 0; q < 2; q++) {
+            AQ_HIP(hipMemsetAsync(h->d_rs_acc + 128 * q, 0, sizeof(unsigned int) * 64, s));
+            AQ_HIP(hipMemsetAsync(h->d_rs_acc + 128 * q + 64, 0xff, sizeof(unsigned int) * 64, s));
+        }
+    }
+    h->rs_parity ^= 1;
+    const RsArgs ra{T, pb, (int)gb, nblk, h->d_candoff, h->d_candlen, h->d_needsort,
+                    h->d_rs_acc + 128 * h->rs_parity, h->d_rs_acc + 128 * (h->rs_parity ^ 1), h->d_rs_cnt, h->d_ctr};
+    unsigned int *K0 = h->d_rs, *I0 = h->d_rs + gb, *K1 = h->d_rs + 2 * gb, *I1 = h->d_rs + 3 * gb;
+    k_rs_keys<<<(int)std::min<long long>(1024, (gb + 255) / 256), 256, 0, s>>>(ra, h->d_ckey, h->d_cslot, h->d_ckey3,
+                                                                          h->d_cslot3, K0, I0);
+    for (int p = 0; p < passes; p++) {
+        const bool last = p == passes - 1;
+        k_rs_count<<<nblk, RS_THREADS, 0, s>>>(ra, p, K0);
+        k_rs_scatter<<<nblk, RS_THREADS, 0, s>>>(ra, p, last ? 1 : 0, K0, I0, K1, I1, h->d_ckey3, h->d_cslot3,
+                                                 h->d_ckey, h->d_cslot);
+        std::swap(K0, K1);
+        std::swap(I0, I1);
+    }
+    AQ_HIP(hipGetLastError());
+    h->n_sort_async++;
+    h->n_sort_radix++;
     *done = true;
     return ADLBQ_OK;
 }
@@ -2961,7 +3291,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if (np > 0 && T > 0 && sort_hint(h)) {
         stage_begin(h, "sort", &ev);
         bool planned = false;
-        if ((rc = launch_segsort_planned(h, &planned))) return rc;
+        if ((rc = launch_segsort_radix(h, &planned))) return rc;
+        if (!planned && (rc = launch_segsort_planned(h, &planned))) return rc;
         if (!planned && (rc = launch_segsort(h))) return rc;
         stage_end(h, "sort", ev);
     }

@@ -106,11 +106,12 @@ bool rank_hint(adlbq_server *h) {  // the newest landed batch ranked its candida
 }
 
 // the newest landed batch's candidate sort plan (G, lowest varying key bit), or false
-bool plan_hint(adlbq_server *h, int *g, int *lo) {
+bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi) {
     const int i = newest_landed(h);
     if (i < 0) return false;
     *g = h->h_snap[i].plan_g;
     *lo = h->h_snap[i].plan_lo;
+    if (phi) *phi = h->h_snap[i].plan_phi;
     return *g > 0;
 }
 
@@ -1178,7 +1179,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv, h->d_rtype, h->d_pm_over,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
                     h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
-                    h->d_ckey3, h->d_cslot3, h->d_plan};
+                    h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1979,6 +1980,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_modes = value;
         return ADLBQ_OK;
     }
+    if (n == "segsort_radix") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "segsort_radix must be 0 or 1");
+        h->segsort_radix = (int)value;
+        return ADLBQ_OK;
+    }
     if (n == "segsort_merged") {
         if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "segsort_merged must be 0 or 1");
         h->segsort_merged = (int)value;
@@ -2047,6 +2053,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         auto it = h->timers.find(n.substr(8));
         return it == h->timers.end() ? 0 : it->second.host_ns;
     }
+    if (n == "sort_radix") return h->n_sort_radix;         // planned sorts issued as the list-stable radix sort
     if (n == "sort_async") return h->n_sort_async;         // merged sorts planned from the last landed batch (cumulative)
     if (n == "sort_async_bad") {  // ... whose plan did not hold (k_rank sorted them), as of the newest landed batch
         refresh_counters(h);

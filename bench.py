@@ -542,7 +542,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "workload": f"config4: {N} units/shard (80% targeted, Zipf(1.1) over 1024 ranks), 32 Zipf types, "
                     f"prio U[0,2^16), {R} hanging Reserves/step with 1-4 types, {P} Puts (same mix) before each",
         "targeted_index": {"merges": srv.stat("tindex_merges"), "rebuilds": srv.stat("tindex_rebuilds")},
-        "candidate_sort": {"planned": srv.stat("sort_async"), "plan_missed": srv.stat("sort_async_bad"),
+        "candidate_sort": {"planned": srv.stat("sort_async"), "planned_radix": srv.stat("sort_radix"),
+                           "plan_missed": srv.stat("sort_async_bad"),
                            "device_sorted_lists": srv.stat("device_sorted_lists")},
         "value": matched / el,
         "unit": "assignments/s",

@@ -157,7 +157,7 @@ def _exact_full(w, batches=1, stats=None, params=()):
                 s.unreserve_batch_device(m.size, trip.data_ptr())
                 s.sync()
         if stats is not None:
-            for k in ("device_sorted_lists", "sort_timeouts"):
+            for k in ("device_sorted_lists", "sort_timeouts", "sort_radix", "sort_async_bad"):
                 stats[k] = s.stat(k)
         return first
 
@@ -173,22 +173,27 @@ def test_full_size_config2_equal_prio_exact(gpu_available):
     _exact_full(w)
 
 
-@pytest.mark.parametrize("merged,wide,rounds",
-                         [(1, 16384, -1), (0, 16384, -1), (0, 256, -1), (1, 16384, 0), (1, 16384, 1)])
-def test_config4_2m_exact(gpu_available, merged, wide, rounds):
-    """Three batches: from the second on the multi-prio-bin candidate lists are
+@pytest.mark.parametrize("merged,wide,rounds,radix",
+                         [(1, 16384, -1, 1), (1, 16384, -1, 0), (0, 16384, -1, 1), (0, 256, -1, 1),
+                          (1, 16384, 0, 1), (1, 16384, 1, 1)])
+def test_config4_2m_exact(gpu_available, merged, wide, rounds, radix):
+    """Four batches: from the second on the multi-prio-bin candidate lists are
     sorted before the rank pass (launch_segsort): all lists in one merged
     device-wide radix sort (merged=1), or list by list, lists of `wide`
     entries or more by a device-wide sort each and shorter ones by a shared
-    segmented sort (256 forces the device-wide path).  rounds: prefix-round
-    launches of the 32-type ordered choice after round 0 (-1 = auto; 0 and 1
-    leave the in-order walk more to do)."""
+    segmented sort (256 forces the device-wide path).  From the third batch on
+    the sort is planned from the last landed batch without a read-back: the
+    hand-written list-stable radix sort (radix=1) or the merged library sort.
+    rounds: prefix-round launches of the 32-type ordered choice after round 0
+    (-1 = auto; 0 and 1 leave the in-order walk more to do)."""
     w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
     stats = {}
-    _exact_full(w, batches=3, stats=stats, params=[("segsort_merged", merged), ("segsort_wide", wide),
-                                                       ("chain_rounds", rounds)])
+    _exact_full(w, batches=4, stats=stats, params=[("segsort_merged", merged), ("segsort_wide", wide),
+                                                       ("chain_rounds", rounds), ("segsort_radix", radix)])
     if merged or wide == 256:
         assert stats["device_sorted_lists"] > 0, "the device-wide list sort did not run"
+    if merged and radix:
+        assert stats["sort_radix"] >= 2 and stats["sort_async_bad"] == 0, stats
     assert stats["sort_timeouts"] == 0
 
 
@@ -198,8 +203,8 @@ def test_full_size_config4_exact(gpu_available):
     the candidate lists sorted before the rank pass."""
     w = synth.config4(n_units=10_000_000, n_reserves=65_536, n_ranks=1024, seed=10)
     stats = {}
-    _exact_full(w, batches=2, stats=stats)
-    assert stats["sort_timeouts"] == 0
+    _exact_full(w, batches=3, stats=stats)
+    assert stats["sort_timeouts"] == 0 and stats["sort_radix"] >= 1, stats
 
 
 REPEAT = {
