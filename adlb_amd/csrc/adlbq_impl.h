@@ -231,6 +231,7 @@ struct adlbq_server {
     unsigned long long *d_tkeys = nullptr, *d_tkeys2 = nullptr;
     int *d_tvals = nullptr, *d_tvals2 = nullptr; long long cap_tidx = 0;
     int *d_tstart = nullptr, *d_tend = nullptr; long long cap_trange = 0;
+    long long tidx_groups = 0;  // (bucket, type) groups d_tstart / d_tend hold, as lower bounds; 0: none
     void *d_tsort = nullptr; size_t cap_tsort = 0;
     bool tindex_dirty = true;
     // incremental index: entries [0, tidx_n) of d_tkeys / d_tvals are real (sorted);

@@ -308,7 +308,7 @@ __device__ __forceinline__ long long cut_of(int th, long long an) {
 // write-through and read back the same way) finds the bin where the type's
 // demand is reached and how many units of it are needed.  Candidate list
 // offsets (the prefix of candlen over types) follow in k_select_open.
-constexpr int TH_THREADS = 1024;  // one pass over up to 1024 chunks (33M units) per column
+constexpr int TH_THREADS = 256;  // chunks per step of the column scan
 __global__ __launch_bounds__(TH_THREADS) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
@@ -825,7 +825,8 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
 // of the bucket per Reserve, the bucket's units are kept in an index sorted
 // by (bucket, type, prio desc, bucket position asc) -- one stable radix sort,
 // rebuilt only after targeted Puts (k_tindex_keys, hipcub) -- with the range
-// of every (bucket, type) (k_tindex_ranges).  A Reserve's best unit is then
+// of every (bucket, type) as lower bounds (k_tindex_bounds; after an
+// incremental merge, k_tindex_shift).  A Reserve's best unit is then
 // the best head among its types' ranges: lane t of wave 0 keeps type t's
 // head, skips units no longer available (pinned, deleted, prio <= LOWEST),
 // and the wave takes the minimum of (prio desc, position asc).
@@ -861,15 +862,34 @@ __global__ __launch_bounds__(256) void k_tindex_keys(const int *__restrict__ pst
     }
 }
 
-__global__ void k_tindex_ranges(const unsigned long long *__restrict__ keys, long long n, int *tstart, int *tend) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const unsigned long long k = keys[i];
-    if (k >> TIDX_KEY_BITS) return;  // a hole
-    const unsigned int g = (unsigned int)(k >> TIDX_PRIO_BITS);  // bucket << 6 | type
-    if (i == 0 || (unsigned int)(keys[i - 1] >> TIDX_PRIO_BITS) != g) tstart[g] = (int)i;
-    if (i == n - 1 || (keys[i + 1] >> TIDX_KEY_BITS) || (unsigned int)(keys[i + 1] >> TIDX_PRIO_BITS) != g)
-        tend[g] = (int)(i + 1);
+// (bucket, type) group g's range as lower bounds, empty groups included:
+// tstart[g] = #entries of groups < g, tend[g] = #entries of groups <= g
+__device__ __forceinline__ int tidx_lower(const unsigned long long *__restrict__ keys, int n, unsigned long long v) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_tindex_bounds(const unsigned long long *__restrict__ keys, int n, int G, int *tstart, int *tend) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    tstart[g] = tidx_lower(keys, n, (unsigned long long)g << TIDX_PRIO_BITS);
+    tend[g] = tidx_lower(keys, n, (unsigned long long)(g + 1) << TIDX_PRIO_BITS);
+}
+
+// after merging m sorted new keys into the index: every group's bounds move up
+// by the new keys of the groups before it (groups past G_old held n_old)
+__global__ void k_tindex_shift(const unsigned long long *__restrict__ nkeys, int m, int G_old, int n_old, int G,
+                               int *tstart, int *tend) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G) return;
+    const int os = g < G_old ? tstart[g] : n_old, oe = g < G_old ? tend[g] : n_old;
+    tstart[g] = os + tidx_lower(nkeys, m, (unsigned long long)g << TIDX_PRIO_BITS);
+    tend[g] = oe + tidx_lower(nkeys, m, (unsigned long long)(g + 1) << TIDX_PRIO_BITS);
 }
 
 // One block per target-rank bucket: that rank's Reserves in arrival order
@@ -885,7 +905,7 @@ __global__ void k_tindex_ranges(const unsigned long long *__restrict__ keys, lon
 // cache runs dry walks its range in global memory (a deep run of pinned
 // units).  The pins are k_finalize's.
 constexpr int TGT_REQ = 1024;    // Reserves per batch of the block
-constexpr int TGT_CACHE = 2048;  // cached index entries per block
+constexpr int TGT_CACHE = 1024;  // cached index entries per block (32 KB of LDS in all: five blocks per CU)
 constexpr int TGT_PER = TGT_CACHE / 256;
 
 __device__ __forceinline__ long long tidx_slot(const int *__restrict__ rpages, int p0, int L) {
@@ -2474,11 +2494,11 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
 // one stable radix sort, then the (bucket, type) ranges.
 static int tindex_ranges(adlbq_server *h, int nb) {
     hipStream_t s = h->stream;
-    AQ_HIP(hipMemsetAsync(h->d_tstart, 0, sizeof(int) * (size_t)nb * 64, s));
-    AQ_HIP(hipMemsetAsync(h->d_tend, 0, sizeof(int) * (size_t)nb * 64, s));
-    if (h->tidx_n > 0)
-        k_tindex_ranges<<<(int)((h->tidx_n + 255) / 256), 256, 0, s>>>(h->d_tkeys, h->tidx_n, h->d_tstart, h->d_tend);
+    const int G = nb * 64;
+    if (G > 0)
+        k_tindex_bounds<<<(G + 255) / 256, 256, 0, s>>>(h->d_tkeys, (int)h->tidx_n, G, h->d_tstart, h->d_tend);
     AQ_HIP(hipGetLastError());
+    h->tidx_groups = G;
     return ADLBQ_OK;
 }
 
@@ -2508,6 +2528,7 @@ static int ensure_tindex(adlbq_server *h) {
         h->cap_trange = std::max((long long)nb * 64, 2 * h->cap_trange);
         AQ_HIP(hipMalloc((void **)&h->d_tstart, sizeof(int) * h->cap_trange));
         AQ_HIP(hipMalloc((void **)&h->d_tend, sizeof(int) * h->cap_trange));
+        h->tidx_groups = 0;  // the bounds were in the freed arrays
     }
     const long long m = (long long)h->tnew_keys.size();
     // incremental: the new units' keys (sorted on the host, ties kept in Put order) merged into the
@@ -2551,12 +2572,21 @@ static int ensure_tindex(adlbq_server *h) {
                               h->d_tvals2, (size_t)h->tidx_n, (size_t)m, rocprim::less<unsigned long long>(), s));
         std::swap(h->d_tkeys, h->d_tkeys2);
         std::swap(h->d_tvals, h->d_tvals2);
+        const long long n_old = h->tidx_n;
         h->tidx_n += m;
         h->tidx_merges++;
         h->tnew_keys.clear();
         h->tnew_vals.clear();
         int rc;
-        if ((rc = tindex_ranges(h, nb))) return rc;
+        if (h->tidx_groups > 0 && h->tidx_groups <= (long long)nb * 64) {  // shift the bounds
+            const int G = nb * 64;
+            k_tindex_shift<<<(G + 255) / 256, 256, 0, s>>>(h->d_tnewk, (int)m, (int)h->tidx_groups, (int)n_old, G,
+                                                          h->d_tstart, h->d_tend);
+            AQ_HIP(hipGetLastError());
+            h->tidx_groups = G;
+        } else if ((rc = tindex_ranges(h, nb))) {
+            return rc;
+        }
         h->tindex_dirty = false;
         return ADLBQ_OK;
     }
