@@ -650,10 +650,11 @@ __global__ __launch_bounds__(256) void k_select_open(
 }
 
 // ---------------------------------------------------------------- per-type sort (multi-priority bins only)
-__device__ inline void bitonic_desc_4096(unsigned long long *sk, int *ss) {
-    for (int k = 2; k <= 4096; k <<= 1) {
+constexpr int SORT_BLK = 2048;  // entries per LDS bitonic block of sort_type
+__device__ inline void bitonic_desc_blk(unsigned long long *sk, int *ss) {
+    for (int k = 2; k <= SORT_BLK; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+            for (int i = threadIdx.x; i < SORT_BLK; i += blockDim.x) {
                 int ixj = i ^ j;
                 if (ixj > i) {
                     unsigned long long a = sk[i], b = sk[ixj];
@@ -672,31 +673,31 @@ __device__ inline void bitonic_desc_4096(unsigned long long *sk, int *ss) {
     }
 }
 
-// Type t's candidate list by key, descending: 4096-entry bitonic blocks in
+// Type t's candidate list by key, descending: SORT_BLK-entry bitonic blocks in
 // LDS (sk, ss), then pairwise merges through key2/slot2.  Any block size.
 __device__ void sort_type(const int off, const int n, unsigned long long *key, int *slot, unsigned long long *key2,
                           int *slot2, unsigned long long *sk, int *ss) {
-    for (int c0 = 0; c0 < n; c0 += 4096) {
-        const int m = min(4096, n - c0);
-        for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+    for (int c0 = 0; c0 < n; c0 += SORT_BLK) {
+        const int m = min(SORT_BLK, n - c0);
+        for (int i = threadIdx.x; i < SORT_BLK; i += blockDim.x) {
             sk[i] = i < m ? key[off + c0 + i] : 0ull;
             ss[i] = i < m ? slot[off + c0 + i] : -1;
         }
         __syncthreads();
-        bitonic_desc_4096(sk, ss);
+        bitonic_desc_blk(sk, ss);
         for (int i = threadIdx.x; i < m; i += blockDim.x) {
             key[off + c0 + i] = sk[i];
             slot[off + c0 + i] = ss[i];
         }
         __syncthreads();
     }
-    if (n <= 4096) return;
+    if (n <= SORT_BLK) return;
     __threadfence();
     __syncthreads();
     unsigned long long *sK = key + off, *dK = key2 + off;
     int *sS = slot + off, *dS = slot2 + off;
     constexpr int ITEMS = 4;
-    for (long long wdt = 4096; wdt < n; wdt *= 2) {
+    for (long long wdt = SORT_BLK; wdt < n; wdt *= 2) {
         for (long long a0 = 0; a0 < n; a0 += 2 * wdt) {
             const long long na = min((long long)n - a0, wdt);
             const long long nb = max(0ll, min((long long)n - a0 - wdt, wdt));
@@ -746,8 +747,8 @@ __global__ __launch_bounds__(1024) void k_sort_types(const int *__restrict__ nee
                                                      int *slot, unsigned long long *key2, int *slot2) {
     const int t = blockIdx.x;
     if (!needsort[t] || candlen[t] <= 1) return;
-    __shared__ unsigned long long sk[4096];
-    __shared__ int ss[4096];
+    __shared__ unsigned long long sk[SORT_BLK];
+    __shared__ int ss[SORT_BLK];
     sort_type(candoff[t], candlen[t], key, slot, key2, slot2, sk, ss);
 }
 
@@ -1216,7 +1217,7 @@ __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) 
 // last keys: one wave finds both (32-ary searches, three probe rounds), loads
 // that stretch of list u into LDS and the tile's threads search it there.
 // The waves of a workgroup take the other types in turn.
-constexpr int RANK_TILE = 256, RANK_SPAN = 2048;
+constexpr int RANK_TILE = 256, RANK_SPAN = 1024;  // 32 KB of spans: five workgroups per CU
 
 __device__ __forceinline__ int lower_bound_key(const unsigned long long *L, int n, unsigned long long key) {
     int lo = 0, hi = n;  // first position whose key is not better than `key` (L descending)
@@ -1261,7 +1262,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
                                                     LevelRows lr, const DevCounters *ctr) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
     __shared__ unsigned long long span[4][RANK_SPAN];  // also the sort's LDS blocks
-    static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * 4096,
+    static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * SORT_BLK,
                   "sort_type's LDS fits in span");
     __shared__ unsigned long long s_first, s_last, s_sortmask;
     __shared__ int s_a0[4], s_len[4], s_tk;
@@ -1291,7 +1292,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
             for (int q = 0; q < tk; q++) mm &= mm - 1;
             const int t = __ffsll((long long)mm) - 1;
             unsigned long long *sk = &span[0][0];
-            int *ss = reinterpret_cast<int *>(sk + 4096);
+            int *ss = reinterpret_cast<int *>(sk + SORT_BLK);
             sort_type(candoff[t], candlen[t], ckey, rs.cslot, rs.ckey2, rs.cslot2, sk, ss);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -3332,7 +3333,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch};
         // a small grid when the last landed batch was ranked in k_select_open
         // (every loop is grid-strided: any grid is correct, the hint only sizes it)
-        k_rank<<<rank_hint(h) ? 64 : 512, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
+        k_rank<<<rank_hint(h) ? 64 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
                                     (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
                                     h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr);
         stage_end(h, "rank", ev);

@@ -3,7 +3,7 @@
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "config4 or golden or c4 or targeted" > $R/gpurun_out/p4.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $R/gpurun_out/p4.log 2>&1
 rc=$?; echo "[parity] rc=$rc $(tail -1 $R/gpurun_out/p4.log)"
 if [ $rc -ne 0 ]; then tail -40 $R/gpurun_out/p4.log; exit 1; fi
 cd /tmp
