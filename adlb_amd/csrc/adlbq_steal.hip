@@ -118,13 +118,71 @@ __global__ __launch_bounds__(1024) void k_rq_delete_fix(const int *rq_live, DevC
     if (threadIdx.x == 0) ctr->rq_head = s_first;
 }
 
+// k_rq_delete_batch + k_rq_delete_fix in one launch: the last workgroup to
+// arrive (ticket) does the bookkeeping and finds the new FIFO head, reading
+// rq_live at agent scope (the other workgroups' exchanges, not a stale line)
+__global__ __launch_bounds__(256) void k_rq_delete_settle(const int *__restrict__ rqseqnos, int n, int *rq_live,
+                                                          DevCounters *ctr, int *ndel, int *bad, int *ticket) {
+    __shared__ int s_first;
+    __shared__ bool s_last;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int hit = 0;
+    if (i < n) {
+        const int k = rqseqnos[i] - 1;
+        if (k >= 0 && k < ctr->rq_n && atomicExch(&rq_live[k], 0)) hit = 1;
+    }
+    const unsigned long long b = __ballot(hit), m = __ballot(i < n && !hit);
+    if ((threadIdx.x & 63) == 0) {
+        if (b) atomicAdd(ndel, __popcll(b));
+        if (m) atomicAdd(bad, __popcll(m));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        s_last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const int head = ctr->rq_head, nn = ctr->rq_n;
+    if (threadIdx.x == 0) {
+        const int nd = __hip_atomic_load(ndel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ctr->rq_live -= nd;
+        bytes_add(ctr, -BYTES_RQ * nd);  // rq_delete per settled Reserve (adlb.c:1933)
+        *ndel = 0;
+        *ticket = 0;
+        s_first = nn;
+    }
+    __syncthreads();
+    for (int base = head; base < nn; base += blockDim.x) {
+        const int k = base + threadIdx.x;
+        if (k < nn && __hip_atomic_load(rq_live + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(&s_first, k);
+        __syncthreads();
+        const int f = s_first;
+        __syncthreads();  // every thread has read it before the next step may lower it
+        if (f < nn) break;
+    }
+    if (threadIdx.x == 0) ctr->rq_head = s_first;
+}
+
 // The live rq entries in FIFO order, compacted: out[0] = count, then up to cap
 // entries {rqseqno, world_rank, req_types[16]}.  One workgroup of 1024.
+struct RfrReset {  // k_rfr_reset's work, done by k_rq_compact when it runs anyway (rfr_to_rank == nullptr: none)
+    int *rfr_to_rank, A, *rfr_out, nworld, *hdr, idx;
+};
+
 __global__ __launch_bounds__(1024) void k_rq_compact(const int *__restrict__ rq_live, const int *__restrict__ rq_rank,
                                                      const int *__restrict__ rq_types, const DevCounters *ctr,
-                                                     int cap, int *__restrict__ out) {
+                                                     int cap, int *__restrict__ out, RfrReset rr) {
     __shared__ int wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (rr.rfr_to_rank) {
+        for (int i = tid; i < rr.A || i < rr.nworld; i += blockDim.x) {
+            if (i < rr.A) rr.rfr_to_rank[i] = -1;
+            if (i < rr.nworld) rr.rfr_out[i] = 0;
+        }
+        if (rr.hdr && tid == 0) rr.hdr[0] = rr.idx;
+    }
     const int head = ctr->rq_head, n = ctr->rq_n;
     int base = 0;
     for (int c0 = head; c0 < n; c0 += 1024) {
@@ -301,18 +359,18 @@ static int merge_views(int S, int T, const int *user_types, int k, const ShardVi
 // on the shard's stream (adlbq_steal_apply, and the group's one-copy settle)
 static int steal_apply_launch(adlbq_server *h, int ngrant, const int *d_pairs, int ndel, const int *d_dels) {
     wq_changed(h);
-    if (!h->d_apply_bad) {
-        AQ_HIP(hipMalloc((void **)&h->d_apply_bad, sizeof(int) * 3));
-        AQ_HIP(hipMemsetAsync(h->d_apply_bad, 0, sizeof(int) * 3, h->stream));
+    if (!h->d_apply_bad) {  // [bad grants, bad deletes, deleted, settle ticket]
+        AQ_HIP(hipMalloc((void **)&h->d_apply_bad, sizeof(int) * 4));
+        AQ_HIP(hipMemsetAsync(h->d_apply_bad, 0, sizeof(int) * 4, h->stream));
     }
     if (ngrant)
         k_grant<<<(ngrant + 255) / 256, 256, 0, h->stream>>>(d_pairs, ngrant, h->d_seq2slot, h->next_wqseqno,
                                                             h->d_meta, h->d_pin, h->d_seq, h->d_cold1, nullptr,
                                                             h->d_apply_bad);
     if (ndel) {
-        k_rq_delete_batch<<<(ndel + 255) / 256, 256, 0, h->stream>>>(d_dels, ndel, h->d_rq_live, h->d_ctr, nullptr,
-                                                                    h->d_apply_bad + 2, h->d_apply_bad + 1);
-        k_rq_delete_fix<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_ctr, h->d_apply_bad + 2);
+        k_rq_delete_settle<<<(ndel + 255) / 256, 256, 0, h->stream>>>(d_dels, ndel, h->d_rq_live, h->d_ctr,
+                                                                     h->d_apply_bad + 2, h->d_apply_bad + 1,
+                                                                     h->d_apply_bad + 3);
         h->ctr_stale = true;
     }
     AQ_HIP(hipGetLastError());
@@ -355,8 +413,8 @@ int adlbq_steal_begin(adlbq_server *h, int k) {
     // the round answers every SS_RFR the parks of this shard sent (resp[11]):
     // as each SS_RFR_RESP would (adlb.c:1877-1878), rfr_to_rank = -1 and
     // rfr_out = 0, so later parks and check_remote see no RFR outstanding
-    k_rfr_reset<<<(std::max(h->A, h->num_world) + 255) / 256, 256, 0, h->stream>>>(h->d_rfr_to_rank, h->A,
-                                                                                   h->d_rfr_out, h->num_world);
+    // (k_rfr_reset, or inside k_rq_compact below; the export reads neither table)
+    const RfrReset rr{h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world, nullptr, 0};
     // every live rq entry fits: the landed-snapshot bound, else the whole capacity
     const long long up = rq_live_upper(h);
     const int rqcap = (int)std::max(0ll, std::min<long long>(up, h->rq_cap));
@@ -364,8 +422,11 @@ int adlbq_steal_begin(adlbq_server *h, int k) {
     if ((rc = ensure_steal_buffers(h, k, rqcap))) return rc;
     if (T && (rc = launch_export(h, k, h->d_export, h->d_navail))) return rc;
     if (h->rq_cap > 0) {
-        k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, rqcap, h->d_rqx);
+        k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, rqcap, h->d_rqx,
+                                                rr);
     } else {
+        k_rfr_reset<<<(std::max(std::max(h->A, h->num_world), 1) + 255) / 256, 256, 0, h->stream>>>(
+            h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world);
         AQ_HIP(hipMemsetAsync(h->d_rqx, 0, sizeof(int), h->stream));
     }
     AQ_HIP(hipGetLastError());
@@ -542,6 +603,7 @@ struct adlbq_steal_group {
     int *h_app = nullptr, *d_app = nullptr;  // every shard's grants + rq deletions, one copy per settle
     long long cap_app = 0;
     hipEvent_t app_ev = nullptr;
+    hipEvent_t unr_ev = nullptr;  // the grants' SS_UNRESERVE staging copy (first shard's stream)
     long long ns_copy = 0, ns_merge = 0, ns_apply = 0, nreq_last = 0;  // the last settle's host phases
 };
 
@@ -587,19 +649,22 @@ int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
     for (int j = 0; j < g->n; j++) {
         adlbq_server *h = g->sh[(size_t)j];
         int *r = d_blob + (size_t)j * g->blob;
-        // every SS_RFR of this shard's parks is answered by the round (adlb.c:1877-1878)
-        k_rfr_reset<<<(std::max(std::max(h->A, h->num_world), 1) + 255) / 256, 256, 0, h->stream>>>(
-            h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world, r, h->my_idx);
+        // every SS_RFR of this shard's parks is answered by the round (adlb.c:1877-1878):
+        // the reset rides in k_rq_compact (the export reads neither table)
+        const RfrReset rr{h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world, r, h->my_idx};
         int rc;
         long long *nav = reinterpret_cast<long long *>(r + g->off_nav);
         if (g->T && !launch_export_after(h, g->k, r + g->off_recs, r + g->off_nrec, nav) &&
             (rc = launch_export(h, g->k, r + g->off_recs, nav)))
             return rc;
-        if (h->rq_cap > 0 && g->rqcap > 0)
+        if (h->rq_cap > 0 && g->rqcap > 0) {
             k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, g->rqcap,
-                                                    r + g->off_rq);
-        else
+                                                    r + g->off_rq, rr);
+        } else {
+            k_rfr_reset<<<(std::max(std::max(h->A, h->num_world), 1) + 255) / 256, 256, 0, h->stream>>>(
+                h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world, r, h->my_idx);
             AQ_HIP(hipMemsetAsync(r + g->off_rq, 0, sizeof(int), h->stream));
+        }
         AQ_HIP(hipGetLastError());
         AQ_HIP(hipEventRecord(g->ev[(size_t)j], h->stream));
     }
@@ -746,16 +811,27 @@ int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g) {
         AQ_HIP(hipHostMalloc((void **)&g->h_unr, sizeof(int) * g->cap_unr, hipHostMallocDefault));
         AQ_HIP(hipMalloc((void **)&g->d_unr, sizeof(int) * g->cap_unr));
     }
-    // the staging is free: the previous round's copies completed before this round's settle returned
+    // the staging is free: the previous round's copy (first shard's stream) completed
+    // before this round's settle returned.  Every shard's triples in one copy; each
+    // shard's kernel behind its event
+    adlbq_server *h0 = g->sh[0];
     long long off = 0;
     for (int j = 0; j < g->n; j++) {
         const auto &gr = g->grants[(size_t)j];
         const int m = (int)(gr.size() / 2);
-        if (!m) continue;
         int *hb = g->h_unr + off;
         for (int i = 0; i < m; i++) hb[3 * i] = gr[2 * (size_t)i], hb[3 * i + 1] = gr[2 * (size_t)i + 1], hb[3 * i + 2] = -1;
+        off += 3ll * m;
+    }
+    if (!g->unr_ev) AQ_HIP(hipEventCreateWithFlags(&g->unr_ev, hipEventDisableTiming));
+    AQ_HIP(hipMemcpyAsync(g->d_unr, g->h_unr, sizeof(int) * (size_t)off, hipMemcpyHostToDevice, h0->stream));
+    AQ_HIP(hipEventRecord(g->unr_ev, h0->stream));
+    off = 0;
+    for (int j = 0; j < g->n; j++) {
+        const int m = (int)(g->grants[(size_t)j].size() / 2);
+        if (!m) continue;
         adlbq_server *h = g->sh[(size_t)j];
-        AQ_HIP(hipMemcpyAsync(g->d_unr + off, hb, sizeof(int) * 3 * (size_t)m, hipMemcpyHostToDevice, h->stream));
+        if (h != h0) AQ_HIP(hipStreamWaitEvent(h->stream, g->unr_ev, 0));
         int rc;
         if ((rc = adlbq_unreserve_batch_device(h, m, g->d_unr + off))) return rc;
         off += 3ll * m;
@@ -817,6 +893,7 @@ int adlbq_steal_group_destroy(adlbq_steal_group *g) {
     if (g->h_app) hipHostFree(g->h_app);
     if (g->d_app) hipFree(g->d_app);
     if (g->app_ev) hipEventDestroy(g->app_ev);
+    if (g->unr_ev) hipEventDestroy(g->unr_ev);
     delete g;
     return ADLBQ_OK;
 }

@@ -3,7 +3,9 @@
 usage: python tools/step_timeline.py <rocprofv3 output dir>
 
 A step starts at each k_prep_hist launch (the first kernel of a reserve batch);
-the last five complete steps are averaged per kernel position.  'span' is the
+the last five complete steps without a copy (the device-resident timed region,
+not the host-buffer batches the bench runs after it) are averaged per kernel
+position.  'span' is the
 first kernel start to the last kernel end of a step, 'busy' the sum of the
 kernel durations (the difference is the idle time between kernels).
 """
@@ -16,7 +18,8 @@ def main(d):
     f = glob.glob(d + "/**/*kernel_trace.csv", recursive=True)[0]
     rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if "k_prep_hist" in r["Kernel_Name"]]
-    steps = [rows[a:b] for a, b in zip(idx[-6:-1], idx[-5:])]
+    steps = [rows[a:b] for a, b in zip(idx[:-1], idx[1:])]
+    steps = [st for st in steps if not any("copyBuffer" in r["Kernel_Name"] for r in st)][-5:]
     agg = {}
     for st in steps:
         for n, r in enumerate(st):
