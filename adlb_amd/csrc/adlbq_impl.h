@@ -252,6 +252,10 @@ struct adlbq_server {
     // the candidate radix sort (rsort_*): 32-bit keys + indices, ping-pong; per-(digit, tile) counts; per-list OR / AND
     unsigned int *d_rs = nullptr; long long cap_rs = 0; int *d_rs_cnt = nullptr; long long cap_rs_cnt = 0;
     unsigned int *d_rs_acc = nullptr; int rs_parity = 0;
+    // zero-copy staging of the synchronous host-buffer Get batch: mapped pinned memory the
+    // kernels read and write directly, and a mapped copy of the counters
+    int *h_zc = nullptr, *d_zc = nullptr; long long cap_zc = 0;
+    adlbq::DevCounters *h_zctr = nullptr, *d_zctr = nullptr;
     int segsort_radix = 1;             // "segsort_radix": the hand-written list-stable radix sort in the sync-free plan
     long long n_sort_radix = 0;
     int segsort_async = 1;             // "segsort_async": plan the merged sort from the last landed batch (no sync)

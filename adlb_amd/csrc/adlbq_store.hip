@@ -150,9 +150,33 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
     return ADLBQ_OK;
 }
 
+static void apply_counters(adlbq_server *h);
+
+// the counters into mapped host memory (one thread; visible once the stream is synchronised)
+__global__ void k_ctr_out(const DevCounters *__restrict__ src, DevCounters *dst) { *dst = *src; }
+
+// the counters land in mapped pinned memory (one-thread kernel): no staged copy
+static int ensure_zctr(adlbq_server *h) {
+    if (!h->h_zctr) {
+        AQ_HIP(hipHostMalloc((void **)&h->h_zctr, sizeof(DevCounters), hipHostMallocMapped));
+        AQ_HIP(hipHostGetDevicePointer((void **)&h->d_zctr, h->h_zctr, 0));
+    }
+    return ADLBQ_OK;
+}
+
 int refresh_counters(adlbq_server *h) {
-    AQ_HIP(hipMemcpyAsync(&h->ctr, h->d_ctr, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    int rc;
+    if ((rc = ensure_zctr(h))) return rc;
+    k_ctr_out<<<1, 1, 0, h->stream>>>(h->d_ctr, h->d_zctr);
+    AQ_HIP(hipGetLastError());
     AQ_HIP(hipStreamSynchronize(h->stream));
+    h->ctr = *h->h_zctr;
+    apply_counters(h);
+    return ADLBQ_OK;
+}
+
+// the host's view after h->ctr has been refreshed
+static void apply_counters(adlbq_server *h) {
     h->ctr_stale = false;
     h->rq_n_upper = h->ctr.rq_n;
     // units the device-side Get batches removed since the last look
@@ -160,7 +184,6 @@ int refresh_counters(adlbq_server *h) {
     h->live_targeted -= h->ctr.got_targeted - h->got_t_seen;
     h->got_seen = h->ctr.got;
     h->got_t_seen = h->ctr.got_targeted;
-    return ADLBQ_OK;
 }
 
 template <typename T>
@@ -831,6 +854,7 @@ __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ page
     res[2] = cn;
 }
 
+
 // SS_UNRESERVE of every unit a reserve batch handed out, read straight from the
 // batch's requests and TA_RESERVE_RESP records (rc 1 = matched, [5] = wqseqno;
 // the new pin is -1, i.e. the unit is available again)
@@ -1184,6 +1208,8 @@ int adlbq_destroy(adlbq_server *h) {
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
     if (h->h_snap) hipHostFree(h->h_snap);
+    if (h->h_zc) hipHostFree(h->h_zc);
+    if (h->h_zctr) hipHostFree(h->h_zctr);
     for (int q = 0; q < 2; q++) {
         if (h->h_tab[q]) hipHostFree(h->h_tab[q]);
         if (h->tab_ev[q]) hipEventDestroy(h->tab_ev[q]);
@@ -1462,18 +1488,27 @@ int adlbq_get_reserved_batch(adlbq_server *h, int n, const int *pairs2, int *out
     if (!ok_handle(h) || n < 0 || (n && (!pairs2 || !out5))) return fail(ADLBQ_ERR_ARG, "adlbq_get_reserved_batch");
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
-    if ((long long)n * 7 > h->cap_getbuf) {
+    int rc0;
+    // zero-copy: the pairs, the records and the counters go through mapped pinned
+    // memory (no copies to stage for a few dozen Gets; the call is synchronous, so
+    // the staging is free again when it returns)
+    if ((long long)n * 7 > h->cap_zc) {
         AQ_HIP(hipStreamSynchronize(h->stream));
-        if (h->d_getbuf) AQ_HIP(hipFree(h->d_getbuf));
-        h->cap_getbuf = std::max<long long>((long long)n * 7, 2 * h->cap_getbuf);
-        AQ_HIP(hipMalloc((void **)&h->d_getbuf, sizeof(int) * h->cap_getbuf));
+        if (h->h_zc) AQ_HIP(hipHostFree(h->h_zc));
+        h->cap_zc = std::max<long long>({(long long)n * 7, 2 * h->cap_zc, 4096});
+        AQ_HIP(hipHostMalloc((void **)&h->h_zc, sizeof(int) * h->cap_zc, hipHostMallocMapped));
+        AQ_HIP(hipHostGetDevicePointer((void **)&h->d_zc, h->h_zc, 0));
     }
-    AQ_HIP(hipMemcpyAsync(h->d_getbuf, pairs2, sizeof(int) * 2 * (size_t)n, hipMemcpyHostToDevice, h->stream));
+    if ((rc0 = ensure_zctr(h))) return rc0;
+    std::memcpy(h->h_zc, pairs2, sizeof(int) * 2 * (size_t)n);
     int rc;
-    if ((rc = launch_get_batch(h, n, h->d_getbuf, h->d_getbuf + 2 * (size_t)n))) return rc;
-    AQ_HIP(hipMemcpyAsync(out5, h->d_getbuf + 2 * (size_t)n, sizeof(int) * 5 * (size_t)n, hipMemcpyDeviceToHost,
-                          h->stream));
-    if ((rc = refresh_counters(h))) return rc;  // synchronises; folds the removed units into the host counts
+    if ((rc = launch_get_batch(h, n, h->d_zc, h->d_zc + 2 * (size_t)n))) return rc;
+    k_ctr_out<<<1, 1, 0, h->stream>>>(h->d_ctr, h->d_zctr);
+    AQ_HIP(hipGetLastError());
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    std::memcpy(out5, h->h_zc + 2 * (size_t)n, sizeof(int) * 5 * (size_t)n);
+    h->ctr = *h->h_zctr;
+    apply_counters(h);  // folds the removed units into the host counts
     for (int i = 0; i < n; i++)
         if (out5[5 * i] == 1) {
             const int seq = pairs2[2 * i + 1];
