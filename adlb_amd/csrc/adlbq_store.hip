@@ -164,6 +164,18 @@ static int ensure_zctr(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
+// mapped pinned staging of at least n ints for a synchronous entry point
+static int ensure_zc(adlbq_server *h, long long n) {
+    if (n > h->cap_zc) {
+        AQ_HIP(hipStreamSynchronize(h->stream));
+        if (h->h_zc) AQ_HIP(hipHostFree(h->h_zc));
+        h->cap_zc = std::max<long long>({n, 2 * h->cap_zc, 4096});
+        AQ_HIP(hipHostMalloc((void **)&h->h_zc, sizeof(int) * h->cap_zc, hipHostMallocMapped));
+        AQ_HIP(hipHostGetDevicePointer((void **)&h->d_zc, h->h_zc, 0));
+    }
+    return ADLBQ_OK;
+}
+
 int refresh_counters(adlbq_server *h) {
     int rc;
     if ((rc = ensure_zctr(h))) return rc;
@@ -1442,15 +1454,16 @@ int adlbq_get_reserved(adlbq_server *h, int rank, int wqseqno, int *out5) {
     out5[0] = -1;
     out5[1] = out5[2] = out5[3] = out5[4] = 0;
     if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
+    int rc;
+    if ((rc = ensure_zc(h, 6))) return rc;
     k_get<<<1, 1, 0, h->stream>>>((int)slot, rank, wqseqno, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0,
-                                  h->d_cold1, h->d_result, h->d_ctr);
-    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 6, hipMemcpyDeviceToHost, h->stream));
+                                  h->d_cold1, h->d_zc, h->d_ctr);  // the record straight into mapped memory
     AQ_HIP(hipStreamSynchronize(h->stream));
-    memcpy(out5, h->h_result, sizeof(int) * 5);
+    memcpy(out5, h->h_zc, sizeof(int) * 5);
     if (out5[0] == 1) {
         h->seq2slot[wqseqno] = -1;
         h->live_units--;
-        if (h->h_result[5] >= 0) h->live_targeted--;
+        if (h->h_zc[5] >= 0) h->live_targeted--;
         // keep the device map consistent for batch unreserves
         AQ_HIP(hipMemsetAsync(h->d_seq2slot + wqseqno, 0xff, sizeof(long long), h->stream));
     }
@@ -1492,14 +1505,7 @@ int adlbq_get_reserved_batch(adlbq_server *h, int n, const int *pairs2, int *out
     // zero-copy: the pairs, the records and the counters go through mapped pinned
     // memory (no copies to stage for a few dozen Gets; the call is synchronous, so
     // the staging is free again when it returns)
-    if ((long long)n * 7 > h->cap_zc) {
-        AQ_HIP(hipStreamSynchronize(h->stream));
-        if (h->h_zc) AQ_HIP(hipHostFree(h->h_zc));
-        h->cap_zc = std::max<long long>({(long long)n * 7, 2 * h->cap_zc, 4096});
-        AQ_HIP(hipHostMalloc((void **)&h->h_zc, sizeof(int) * h->cap_zc, hipHostMallocMapped));
-        AQ_HIP(hipHostGetDevicePointer((void **)&h->d_zc, h->h_zc, 0));
-    }
-    if ((rc0 = ensure_zctr(h))) return rc0;
+    if ((rc0 = ensure_zc(h, (long long)n * 7)) || (rc0 = ensure_zctr(h))) return rc0;
     std::memcpy(h->h_zc, pairs2, sizeof(int) * 2 * (size_t)n);
     int rc;
     if ((rc = launch_get_batch(h, n, h->d_zc, h->d_zc + 2 * (size_t)n))) return rc;
@@ -1524,11 +1530,12 @@ int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, in
     long long slot;
     *found = 0;
     if (!find_slot(h, wqseqno, &slot)) return ADLBQ_OK;
+    int rc;
+    if ((rc = ensure_zc(h, 1))) return rc;
     k_unreserve<<<1, 1, 0, h->stream>>>((int)slot, rank, wqseqno, new_pin_rank, h->d_meta, h->d_pin, h->d_seq,
-                                        h->d_result, h->d_prio, h->d_anchor);
-    AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+                                        h->d_zc, h->d_prio, h->d_anchor);  // found straight into mapped memory
     AQ_HIP(hipStreamSynchronize(h->stream));
-    *found = h->h_result[0];
+    *found = h->h_zc[0];
     return ADLBQ_OK;
 }
 
