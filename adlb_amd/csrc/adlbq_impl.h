@@ -328,6 +328,7 @@ int hip_fail(hipError_t e, const char *where);
 
 int ensure_req_capacity(adlbq_server *h, int n);
 int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
+int ensure_zc(adlbq_server *h, long long n);  // mapped pinned staging of >= n ints (h_zc / d_zc)
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);

@@ -3489,11 +3489,22 @@ int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
 
 extern "C" {
 
+constexpr int RESERVE_ZC_MAX = 512;  // host-buffer batches up to this size go zero-copy
+
 int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12) {
     if (!h || n < 0 || (n && (!reqs18 || !resp12))) return fail(ADLBQ_ERR_ARG, "adlbq_reserve_batch");
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
     int rc;
+    if (n <= RESERVE_ZC_MAX) {  // a small batch: requests and replies through mapped pinned memory, no copies
+        const size_t ni = (size_t)ADLBQ_RESERVE_INTS * n, no = (size_t)ADLBQ_RESP_INTS * n;
+        if ((rc = ensure_zc(h, (long long)(ni + no)))) return rc;
+        std::memcpy(h->h_zc, reqs18, sizeof(int) * ni);
+        if ((rc = launch_reserve(h, n, h->d_zc, h->d_zc + ni))) return rc;
+        if ((rc = refresh_counters(h))) return rc;  // synchronises
+        std::memcpy(resp12, h->h_zc + ni, sizeof(int) * no);
+        return ADLBQ_OK;
+    }
     if ((rc = ensure_req_capacity(h, n))) return rc;
     AQ_HIP(hipMemcpyAsync(h->d_reqbuf, reqs18, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)n, hipMemcpyHostToDevice,
                           h->stream));

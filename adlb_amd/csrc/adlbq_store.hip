@@ -165,7 +165,7 @@ static int ensure_zctr(adlbq_server *h) {
 }
 
 // mapped pinned staging of at least n ints for a synchronous entry point
-static int ensure_zc(adlbq_server *h, long long n) {
+int ensure_zc(adlbq_server *h, long long n) {
     if (n > h->cap_zc) {
         AQ_HIP(hipStreamSynchronize(h->stream));
         if (h->h_zc) AQ_HIP(hipHostFree(h->h_zc));
