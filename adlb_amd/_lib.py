@@ -58,6 +58,8 @@ SIGNATURES = {
     "adlbq_steal_group_blob_ints": (c_ll, [P]),
     "adlbq_steal_group_export": (c_int, [P, P]),
     "adlbq_steal_group_settle": (c_int, [P, P, c_int, P, P]),
+    "adlbq_steal_group_export_host": (c_int, [P, P]),
+    "adlbq_steal_group_settle_host": (c_int, [P, P, c_int, P, P]),
     "adlbq_steal_group_responses": (c_int, [P, c_int, P, P]),
     "adlbq_steal_group_grants": (c_int, [P, c_int, P, P]),
     "adlbq_steal_group_check": (c_int, [P, P, P]),

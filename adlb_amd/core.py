@@ -50,6 +50,7 @@ SIGNATURES = {
     "adlbsrv_moving_targeted": (c_int, [P, c_int, P]),
     "adlbsrv_num_parked": (c_int, [P]),
     "adlbsrv_activity": (ctypes.c_longlong, [P]),
+    "adlbsrv_row_stamp": (ctypes.c_longlong, [P]),
     "adlbsrv_rfr_outstanding": (c_int, [P]),
     "adlbsrv_nmw": (c_int, [P]),
     "adlbsrv_info_get": (c_int, [P, c_int, P]),

@@ -46,6 +46,7 @@ struct Common {
 
 struct Held {  // a unit accepted by SS_PUSH_QUERY, until SS_PUSH_HDR / SS_PUSH_DEL
     int type = 0, prio = 0, len = 0, answer = -1, target = -1, home = -1, clen = 0, csrv = -1, cseq = -1;
+    double t = 0.0;  // the pusher's time stamp (dbls_info_buf[4], adlb.c:2150)
 };
 
 struct Parked {
@@ -78,6 +79,7 @@ struct adlbsrv {
     bool push_out = false;
     long long push_seen = -1;  // state stamp of the last loop-top check that sent nothing
     long long npushed_from = 0, npushed_to = 0, table_events = 0;
+    long long row_events = 0;  // changes to this server's qmstat row that are not queue activity (bytes, RFR misses)
     std::unordered_map<int, Held> held;
 
     int rc(int r, const char *what) {
@@ -106,6 +108,7 @@ struct adlbsrv {
             n_rq_timed++;
         }
         parked.erase(it);
+        row_events++;
     }
     // check_remote_work_for_queued_apps (adlb.c:3536-3579)
     int check_remote() {
@@ -124,18 +127,25 @@ struct adlbsrv {
     int drain_rq(int code) {
         if (parked.empty()) return 0;
         int count = 0;
-        rqx.resize(18 * parked.size());
-        if (rc(adlbq_rq_export(q, (int)parked.size(), rqx.data(), &count), "adlbq_rq_export")) return -1;
-        count = std::min<int>(count, (int)parked.size());
+        rqx.resize(18 * (parked.size() + 1));  // room for one more: an engine holding more is caught too
+        if (rc(adlbq_rq_export(q, (int)parked.size() + 1, rqx.data(), &count), "adlbq_rq_export")) return -1;
+        // the engine's rq and the host's parked map hold the same Reserves; a
+        // disagreement would leave apps waiting forever: fail loudly instead
+        if (count != (int)parked.size())
+            return fail("drain_rq: the engine holds " + std::to_string(count) + " parked Reserves, the server " +
+                        std::to_string(parked.size()));
+        for (int i = 0; i < count; i++)
+            if (!parked.count(rqx[18 * (size_t)i]))
+                return fail("drain_rq: parked rqseqno " + std::to_string(rqx[18 * (size_t)i]) + " unknown to the server");
         std::vector<int> seqs((size_t)count), found((size_t)count);
         for (int i = 0; i < count; i++) {
             send_rc(rqx[18 * (size_t)i + 1], TAG_RESERVE_RESP, code);
             seqs[(size_t)i] = rqx[18 * (size_t)i];
-            parked.erase(seqs[(size_t)i]);
         }
         if (count && rc(adlbq_rq_delete_batch(q, count, seqs.data(), found.data()), "adlbq_rq_delete_batch"))
             return -1;
         parked.clear();
+        row_events++;
         return 0;
     }
 };
@@ -239,6 +249,7 @@ int adlbsrv_put_common_payload(adlbsrv *s, int src, const void *buf, int len) {
     Common &c = s->cq[s->next_cq];
     c.buf.assign((const char *)buf, (const char *)buf + (len > 0 ? len : 0));
     adlbq_bytes_adjust(s->q, (double)len);
+    s->row_events++;  // nbytes_used of the row changed
     int b[WIRE_IBUF] = {WIRE_SUCCESS, s->next_cq};
     s->next_cq++;
     s->send_ints(src, TAG_ACK_AND_RC, b, WIRE_IBUF);
@@ -249,6 +260,7 @@ static void cq_maybe_free(adlbsrv *s, int cqseqno) {
     auto it = s->cq.find(cqseqno);
     if (it != s->cq.end() && it->second.refcnt == it->second.ngets) {  // cq_delete (adlb.c:1145, 1330)
         adlbq_bytes_adjust(s->q, -(double)it->second.buf.size());
+        s->row_events++;
         s->cq.erase(it);
     }
 }
@@ -310,6 +322,7 @@ int adlbsrv_reserve_batch(adlbsrv *s, int n, const int *src, const int *bufs17) 
             std::memcpy(p.types, s->reqs.data() + (size_t)i * ADLBQ_RESERVE_INTS + 2, sizeof(p.types));
             p.t = t;
             s->num_put_on_rq++;
+            s->row_events++;
             if (r[11] >= 0) s->send_rfr(r[11], r[10], p);
         }
     }
@@ -399,6 +412,7 @@ int adlbsrv_rfr(adlbsrv *s, int src, const int *b) {
         std::memcpy(o, v, sizeof v);
         s->activity++;
     } else {  // adlb.c:1848-1863
+        s->row_events++;  // update_local_state after the miss (adlb.c:1863): the row goes out again
         o[0] = WIRE_NO_CURR_WORK;
         o[1] = b[0];
         o[2] = b[1];
@@ -503,6 +517,7 @@ int adlbsrv_push_query(adlbsrv *s, int src, const double *d) {
     h.clen = (int)d[8];
     h.csrv = (int)d[9];
     h.cseq = (int)d[10];
+    h.t = d[4];  // steady_clock seconds: one clock for every server process of a node
     const int u[ADLBQ_PUT_INTS] = {h.type, h.prio, h.answer, h.target, h.len, h.home, h.clen, h.csrv, h.cseq};
     int seq = -1;
     if (s->rc(adlbq_push_accept(s->q, u, &seq), "adlbq_push_accept")) return -1;
@@ -557,7 +572,7 @@ int adlbsrv_push_hdr(adlbsrv *s, int src, const int *b, const void *payload, int
     if (o[0] != 1) return fail("SS_PUSH_HDR: wqseqno " + std::to_string(seq) + " not held");
     Unit &unit = s->units[seq];
     unit.buf.assign((const char *)payload, (const char *)payload + (len > 0 ? len : 0));
-    unit.t = now();
+    unit.t = h.t;  // ws->time_stamp = dbls_info_buf[4] (adlb.c:2150): the queued time keeps counting
     const int f[ADLBQ_PUT_INTS] = {h.type, h.prio, h.answer, h.target, h.len, h.home, h.clen, h.csrv, h.cseq};
     std::memcpy(unit.fields, f, sizeof f);
     unit.has_fields = true;
@@ -599,6 +614,7 @@ int adlbsrv_moving_targeted(adlbsrv *s, int src, const int *b) {
 
 int adlbsrv_num_parked(adlbsrv *s) { return (int)s->parked.size(); }
 long long adlbsrv_activity(adlbsrv *s) { return s->activity; }
+long long adlbsrv_row_stamp(adlbsrv *s) { return s->activity + s->row_events; }  // both only grow
 int adlbsrv_rfr_outstanding(adlbsrv *s) { return s->rfr_out; }
 int adlbsrv_nmw(adlbsrv *s) { return s->nmw ? 1 : 0; }
 

@@ -79,6 +79,7 @@ int adlbsrv_moving_targeted(adlbsrv *s, int src, const int *b12);
 /* state for the driver */
 int adlbsrv_num_parked(adlbsrv *s);     /* rq->count */
 long long adlbsrv_activity(adlbsrv *s); /* events that changed a queue (exhaustion check) */
+long long adlbsrv_row_stamp(adlbsrv *s); /* changes when this server's qmstat row may have (queues, bytes, misses) */
 int adlbsrv_rfr_outstanding(adlbsrv *s);
 int adlbsrv_nmw(adlbsrv *s);
 /* ADLB_Info_get keys (adlb.h ADLB_INFO_*, adlb.c:3072-3141) */

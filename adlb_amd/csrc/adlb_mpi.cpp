@@ -128,8 +128,9 @@ bool locally_idle(Loop *L) {
 }
 
 void send_qmstat_row(Loop *L) {
-    // update_local_state (adlb.c:3581-3593) only when a queue changed since the last row
-    const long long act = adlbsrv_activity(g_srv) + adlbsrv_num_parked(g_srv);
+    // update_local_state (adlb.c:3581-3593) only when the row may have changed since the last one
+    // (queue events, byte changes of common prefixes, an SS_RFR this server could not serve)
+    const long long act = adlbsrv_row_stamp(g_srv);
     if (act == L->row_activity) return;
     L->row_activity = act;
     const int T = (int)g_types.size();

@@ -58,7 +58,7 @@ constexpr long long BYTES_WQ = 24 + 72, BYTES_RQ = 24 + 80, BYTES_TQ = 24 + 16;
 struct DevCounters {
     unsigned long long fin_group[8];  // k_finalize arrivals per group: parked << 32 | workgroups
     unsigned long long fin_top;       // groups done: parked << 32 | groups (all reset by the last)
-    int rq_n;          // rq slots used (== next_rqseqno - 1)
+    int rq_n;          // rq slots used (slot k holds rqseqno rq_seq[k]; k_rq_reclaim compacts them)
     int rq_live;       // parked entries alive
     int rq_hwm;        // rq->max_count
     int rq_head;       // lowest rq slot that may be alive
@@ -74,6 +74,9 @@ struct DevCounters {
     int plan_missed;       // sync-free sorts whose plan did not hold (k_rank sorted in-launch), cumulative
     int plan_phi;          // highest bit of the prio field any candidate list varies in (-1: none)
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
+    int batch_failed;      // batches answered ADLB_ERROR because an in-launch candidate sort gave up (cumulative)
+    int rq_next;           // rqseqnos handed out (next_rqseqno - 1, adlb.c:1244)
+    int rq_reclaims;       // k_rq_reclaim compactions (cumulative)
     // the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced (adlb.c:3419-3474) over the
     // structures this handle replaces, plus what the caller adds (adlbq_bytes_adjust)
     long long bytes, bytes_hwm;
@@ -170,10 +173,12 @@ struct adlbq_server {
     // ---- parked reserves
     int rq_cap = 0;
     int *d_rq_rank = nullptr, *d_rq_types = nullptr, *d_rq_live = nullptr, *d_rq_req = nullptr;
+    int *d_rq_seq = nullptr;  // rqseqno per rq slot, ascending
     adlbq::DevCounters *d_ctr = nullptr;
     adlbq::DevCounters ctr{};      // host copy
     bool ctr_stale = false;
     long long rq_n_upper = 0;      // upper bound on rq_n while ctr is stale
+    long long rq_next_upper = 0;   // ... and on rq_next
     // rq_n snapshots written by k_finalize into mapped host memory at the end of
     // each reserve batch, so the rq capacity bound tightens without a sync
     static constexpr int NSNAP = 8;
@@ -277,6 +282,7 @@ struct adlbq_server {
     int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
     int put_match_block = 1, put_always_match = 0;  // diagnostics ("put_match_block", "put_always_match")
     int rank_in_select = 1;            // k_select_open ranks the candidates when it can ("rank_in_select")
+    int sort_fail_test = 0;            // test hook ("sort_fail_test"): the error path of a failed sort wait
     int chain_stamps = 0;              // diagnostic: phase stamps of the first chain launch ("chain_stamps")
     unsigned long long *d_stamps = nullptr; int cap_stamps = 0, n_stamps = 0;
     int chain_warm = -1;               // round-0 warm-up requests (T <= 8), -1 = auto ("chain_warm")
@@ -350,6 +356,18 @@ __device__ __forceinline__ unsigned long long make_key(int prio, unsigned int or
     // larger key == better: priority descending, then `order` ascending
     return ((unsigned long long)((unsigned int)prio ^ 0x80000000u) << 32) |
            (unsigned long long)(~order);
+}
+
+// The rq slot holding rqseqno (-1: none).  rq_seq is ascending over the
+// slots in use: FIFO order is rqseqno order, and k_rq_reclaim keeps it.
+__device__ __forceinline__ int rq_slot_of(const int *rq_seq, int n, int rqseqno) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rq_seq[mid] < rqseqno) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < n && rq_seq[lo] == rqseqno) ? lo : -1;
 }
 
 __device__ __forceinline__ int bin_of(long long d) {

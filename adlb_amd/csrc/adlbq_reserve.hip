@@ -1251,6 +1251,7 @@ struct RankSort {
     int *cslot, *cslot2;
     int *sync;  // [t] sorted epochs, [ADLBQ_MAX_TYPES] ticket, [ADLBQ_MAX_TYPES + 1] timed-out waits
     unsigned int epoch;
+    int fail_test;  // adlbq_set_param("sort_fail_test"): count one timed-out wait (tests the error path)
 };
 
 __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict__ candoff,
@@ -1267,6 +1268,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     __shared__ unsigned long long s_first, s_last, s_sortmask;
     __shared__ int s_a0[4], s_len[4], s_tk;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (rs.fail_test && blockIdx.x == 0 && tid == 0) atomicAdd(rs.sync + ADLBQ_MAX_TYPES + 1, 1);
     if (tid < 64) {
         const bool ns = tid < T && rs.needsort[tid] == 1 && candlen[tid] > 1;  // 2: already sorted
         const unsigned long long m = __ballot(ns);
@@ -2136,9 +2138,9 @@ __global__ __launch_bounds__(64) void k_chainr(ChainArgs a, int round, int final
 // by that last workgroup, so no two workgroups store the same bytes.
 __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__ reqs, int R,
                           const unsigned long long *pmask, int *rq_rank, int *rq_types, int *rq_live, int *rq_req,
-                          DevCounters *ctr, int *resp) {
+                          int *rq_seq, DevCounters *ctr, int *resp) {
     __shared__ int wsum[16];
-    __shared__ int s_n0, s_total, s_stop;
+    __shared__ int s_n0, s_total, s_stop, s_seq0;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nth = blockDim.x;
     // the parked requests are the set bits of the per-wave ballots every
     // workgroup published (pmask[j >> 6]); thread tid takes a contiguous run
@@ -2161,7 +2163,10 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
         if (lane >= o) x += y;
     }
     if (lane == 63) wsum[w] = x;
-    if (tid == 0) s_n0 = ctr->rq_n;
+    if (tid == 0) {
+        s_n0 = ctr->rq_n;
+        s_seq0 = ctr->rq_next;
+    }
     __syncthreads();
     int wpre = 0;
     for (int q = 0; q < w; q++) wpre += wsum[q];
@@ -2177,7 +2182,9 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
             for (int k = 0; k < NREQ; k++) rq_types[(long long)pos * NREQ + k] = rq[2 + k];
             rq_live[pos] = 1;
             rq_req[pos] = jj;
-            resp[(long long)ADLBQ_RESP_INTS * jj + 10] = pos + 1;  // rqseqno (next_rqseqno++, adlb.c:1244)
+            const int seq = s_seq0 + (pos - s_n0) + 1;  // next_rqseqno++ (adlb.c:1244)
+            rq_seq[pos] = seq;
+            resp[(long long)ADLBQ_RESP_INTS * jj + 10] = seq;
             pos++;
         }
     }
@@ -2206,6 +2213,7 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     for (int k = s_stop + tid; k < n0 + np; k += nth) resp[(long long)ADLBQ_RESP_INTS * rq_req[k] + 11] = -1;
     if (tid == 0) {
         ctr->rq_n = n0 + np;
+        ctr->rq_next += np;
         ctr->rq_live += np;
         bytes_add(ctr, BYTES_RQ * np);  // rq_node_create per parked Reserve (adlb.c:1244-1276)
         if (ctr->rq_live > ctr->rq_hwm) ctr->rq_hwm = ctr->rq_live;
@@ -2220,21 +2228,29 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
                                                   int my_world, int *__restrict__ resp, DevCounters *ctr,
                                                   DonorCtx dc, int donors, int *rq_rank, int *rq_types,
-                                                  int *rq_live, int *rq_req, int *dem, int T, DevCounters *snap,
+                                                  int *rq_live, int *rq_req, int *rq_seq, int *dem, int T,
+                                                  DevCounters *snap,
                                                   long long *anchor, long long *anchor_next,
                                                   unsigned long long *pmask, long long *gcut, long long *gcut_next,
-                                                  const int4 *__restrict__ rrec, const int *__restrict__ needsort) {
+                                                  const int4 *__restrict__ rrec, const int *__restrict__ needsort,
+                                                  int *sortfail) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (threadIdx.x == 0) s_parked = 0;
+    // k_rank gave up waiting for an in-launch candidate sort: the lists may be
+    // out of order, so the batch is answered ADLB_ERROR (nothing pinned, nothing
+    // parked) instead of with possibly wrong matches
+    const bool failed = __hip_atomic_load(sortfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     __syncthreads();
     if (j < R) {
         const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
-        const int rank = rq[0], hang = rq[1];
-        const int slot = tmatch[j] >= 0 ? tmatch[j] : (umatch[j] >= 0 ? cslot[umatch[j]] : -1);
+        const int rank = rq[0], hang = failed ? 0 : rq[1];
+        const int slot = failed ? -1 : tmatch[j] >= 0 ? tmatch[j] : (umatch[j] >= 0 ? cslot[umatch[j]] : -1);
         int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
-        if (slot >= 0) {
+        if (failed) {
+            o[0] = -1;  // ADLB_ERROR
+        } else if (slot >= 0) {
             pin[slot] = rank;  // adlb.c:1210-1212
             if (rank >= 0) __hip_atomic_fetch_or(meta + slot, M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int4 c0 = rrec[2ll * slot], c1 = rrec[2ll * slot + 1];  // one 32 B record
@@ -2297,9 +2313,13 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
             gcut_next[threadIdx.x] = LLONG_MIN;
         }
     }
-    if (total > 0) park_tail(dc, donors, reqs, R, pmask, rq_rank, rq_types, rq_live, rq_req, ctr, resp);
+    if (total > 0) park_tail(dc, donors, reqs, R, pmask, rq_rank, rq_types, rq_live, rq_req, rq_seq, ctr, resp);
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (failed) {
+            ctr->batch_failed += 1;
+            __hip_atomic_store(sortfail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // per batch
+        }
         if (total == 0) ctr->n_parked_last = 0;
         int ns = 0;
         for (int t = 0; t < T; t++) ns |= needsort[t];
@@ -3330,7 +3350,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if (np > 0 && T > 0) {
         stage_begin(h, "rank", &ev);
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
-        const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch};
+        const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch,
+                          h->sort_fail_test};
         // a small grid when the last landed batch was ranked in k_select_open
         // (every loop is grid-strided: any grid is correct, the hint only sizes it)
         k_rank<<<rank_hint(h) ? 64 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
@@ -3400,9 +3421,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
                                                    h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
-                                                   h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_dem, T, snap,
+                                                   h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, T,
+                                                   snap,
                                                    h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut,
-                                                   h->d_gcut_next, h->d_rrec, h->d_needsort);
+                                                   h->d_gcut_next, h->d_rrec, h->d_needsort,
+                                                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1);
     }
     stage_end(h, "finalize", ev);
     // the lists hold export_extra more per type: a steal export right after this batch gathers them
@@ -3416,6 +3439,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     AQ_HIP(hipGetLastError());
     h->ctr_stale = true;
     h->rq_n_upper += R;
+    h->rq_next_upper += R;
     return ADLBQ_OK;
 }
 
@@ -3491,11 +3515,22 @@ extern "C" {
 
 constexpr int RESERVE_ZC_MAX = 512;  // host-buffer batches up to this size go zero-copy
 
+// The synchronous entry returns ADLBQ_ERR_DEVICE when k_finalize answered the
+// batch ADLB_ERROR (a device-side wait gave up; nothing was pinned or parked).
+static int batch_outcome(adlbq_server *h, int failed_before) {
+    if (h->ctr.batch_failed != failed_before)
+        return fail(ADLBQ_ERR_DEVICE, "adlbq_reserve_batch: an in-launch candidate sort did not finish in time; "
+                                      "the batch was answered ADLB_ERROR and left the queues unchanged");
+    return ADLBQ_OK;
+}
+
 int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12) {
     if (!h || n < 0 || (n && (!reqs18 || !resp12))) return fail(ADLBQ_ERR_ARG, "adlbq_reserve_batch");
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
     int rc;
+    if ((rc = refresh_counters(h))) return rc;
+    const int failed0 = h->ctr.batch_failed;
     if (n <= RESERVE_ZC_MAX) {  // a small batch: requests and replies through mapped pinned memory, no copies
         const size_t ni = (size_t)ADLBQ_RESERVE_INTS * n, no = (size_t)ADLBQ_RESP_INTS * n;
         if ((rc = ensure_zc(h, (long long)(ni + no)))) return rc;
@@ -3503,7 +3538,7 @@ int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12) 
         if ((rc = launch_reserve(h, n, h->d_zc, h->d_zc + ni))) return rc;
         if ((rc = refresh_counters(h))) return rc;  // synchronises
         std::memcpy(resp12, h->h_zc + ni, sizeof(int) * no);
-        return ADLBQ_OK;
+        return batch_outcome(h, failed0);
     }
     if ((rc = ensure_req_capacity(h, n))) return rc;
     AQ_HIP(hipMemcpyAsync(h->d_reqbuf, reqs18, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)n, hipMemcpyHostToDevice,
@@ -3511,7 +3546,8 @@ int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12) 
     if ((rc = launch_reserve(h, n, h->d_reqbuf, h->d_respbuf))) return rc;
     AQ_HIP(hipMemcpyAsync(resp12, h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)n, hipMemcpyDeviceToHost,
                           h->stream));
-    return refresh_counters(h);
+    if ((rc = refresh_counters(h))) return rc;
+    return batch_outcome(h, failed0);
 }
 
 int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int *d_resp12) {

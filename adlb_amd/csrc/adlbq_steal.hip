@@ -80,13 +80,14 @@ __global__ void k_rfr_reset(int *rfr_to_rank, int A, int *rfr_out, int nworld, i
 }
 
 // rq_find_seqno + rq_delete for many rqseqnos (adlb.c:1883, 1933)
-__global__ void k_rq_delete_batch(const int *__restrict__ rqseqnos, int n, int *rq_live, const DevCounters *ctr,
-                                  int *found, int *ndel, int *bad) {
+__global__ void k_rq_delete_batch(const int *__restrict__ rqseqnos, int n, int *rq_live,
+                                  const int *__restrict__ rq_seq, const DevCounters *ctr, int *found, int *ndel,
+                                  int *bad) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     int hit = 0;
     if (i < n) {
-        const int k = rqseqnos[i] - 1;
-        if (k >= 0 && k < ctr->rq_n && atomicExch(&rq_live[k], 0)) hit = 1;
+        const int k = rq_slot_of(rq_seq, ctr->rq_n, rqseqnos[i]);
+        if (k >= 0 && atomicExch(&rq_live[k], 0)) hit = 1;
         if (found) found[i] = hit;
     }
     const unsigned long long b = __ballot(hit), m = __ballot(i < n && !hit);
@@ -122,14 +123,15 @@ __global__ __launch_bounds__(1024) void k_rq_delete_fix(const int *rq_live, DevC
 // arrive (ticket) does the bookkeeping and finds the new FIFO head, reading
 // rq_live at agent scope (the other workgroups' exchanges, not a stale line)
 __global__ __launch_bounds__(256) void k_rq_delete_settle(const int *__restrict__ rqseqnos, int n, int *rq_live,
-                                                          DevCounters *ctr, int *ndel, int *bad, int *ticket) {
+                                                          const int *__restrict__ rq_seq, DevCounters *ctr,
+                                                          int *ndel, int *bad, int *ticket) {
     __shared__ int s_first;
     __shared__ bool s_last;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     int hit = 0;
     if (i < n) {
-        const int k = rqseqnos[i] - 1;
-        if (k >= 0 && k < ctr->rq_n && atomicExch(&rq_live[k], 0)) hit = 1;
+        const int k = rq_slot_of(rq_seq, ctr->rq_n, rqseqnos[i]);
+        if (k >= 0 && atomicExch(&rq_live[k], 0)) hit = 1;
     }
     const unsigned long long b = __ballot(hit), m = __ballot(i < n && !hit);
     if ((threadIdx.x & 63) == 0) {
@@ -172,7 +174,8 @@ struct RfrReset {  // k_rfr_reset's work, done by k_rq_compact when it runs anyw
 };
 
 __global__ __launch_bounds__(1024) void k_rq_compact(const int *__restrict__ rq_live, const int *__restrict__ rq_rank,
-                                                     const int *__restrict__ rq_types, const DevCounters *ctr,
+                                                     const int *__restrict__ rq_types,
+                                                     const int *__restrict__ rq_seq, const DevCounters *ctr,
                                                      int cap, int *__restrict__ out, RfrReset rr) {
     __shared__ int wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(1024) void k_rq_compact(const int *__restrict__ rq_
         const int pos = pre + __popcll(b & lanemask_lt());
         if (live && pos < cap) {
             int *o = out + 1 + (long long)pos * 18;
-            o[0] = k + 1;
+            o[0] = rq_seq[k];
             o[1] = rq_rank[k];
             const int4 *src = reinterpret_cast<const int4 *>(rq_types + (long long)k * NREQ);
 #pragma unroll
@@ -368,7 +371,8 @@ static int steal_apply_launch(adlbq_server *h, int ngrant, const int *d_pairs, i
                                                             h->d_meta, h->d_pin, h->d_seq, h->d_cold1, nullptr,
                                                             h->d_apply_bad);
     if (ndel) {
-        k_rq_delete_settle<<<(ndel + 255) / 256, 256, 0, h->stream>>>(d_dels, ndel, h->d_rq_live, h->d_ctr,
+        k_rq_delete_settle<<<(ndel + 255) / 256, 256, 0, h->stream>>>(d_dels, ndel, h->d_rq_live, h->d_rq_seq,
+                                                                     h->d_ctr,
                                                                      h->d_apply_bad + 2, h->d_apply_bad + 1,
                                                                      h->d_apply_bad + 3);
         h->ctr_stale = true;
@@ -422,7 +426,7 @@ int adlbq_steal_begin(adlbq_server *h, int k) {
     if ((rc = ensure_steal_buffers(h, k, rqcap))) return rc;
     if (T && (rc = launch_export(h, k, h->d_export, h->d_navail))) return rc;
     if (h->rq_cap > 0) {
-        k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, rqcap, h->d_rqx,
+        k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_rq_seq, h->d_ctr, rqcap, h->d_rqx,
                                                 rr);
     } else {
         k_rfr_reset<<<(std::max(std::max(h->A, h->num_world), 1) + 255) / 256, 256, 0, h->stream>>>(
@@ -522,8 +526,9 @@ int adlbq_rq_export(adlbq_server *h, int cap, int *out18, int *count) {
     const int k0 = h->ctr.rq_head, n = h->ctr.rq_n - k0;
     *count = 0;
     if (n <= 0) return ADLBQ_OK;
-    std::vector<int> live(n), rank(n), types((size_t)n * NREQ);
+    std::vector<int> live(n), rank(n), seq(n), types((size_t)n * NREQ);
     AQ_HIP(hipMemcpyAsync(live.data(), h->d_rq_live + k0, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
+    AQ_HIP(hipMemcpyAsync(seq.data(), h->d_rq_seq + k0, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipMemcpyAsync(rank.data(), h->d_rq_rank + k0, sizeof(int) * n, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipMemcpyAsync(types.data(), h->d_rq_types + (size_t)k0 * NREQ, sizeof(int) * types.size(),
                           hipMemcpyDeviceToHost, h->stream));
@@ -533,7 +538,7 @@ int adlbq_rq_export(adlbq_server *h, int cap, int *out18, int *count) {
         if (!live[i]) continue;
         if (c < cap) {
             int *o = out18 + (size_t)c * 18;
-            o[0] = k0 + i + 1;  // rqseqno
+            o[0] = seq[i];  // rqseqno
             o[1] = rank[i];
             std::memcpy(o + 2, types.data() + (size_t)i * NREQ, sizeof(int) * NREQ);
         }
@@ -568,7 +573,8 @@ int adlbq_rq_delete_batch(adlbq_server *h, int n, const int *rqseqnos, int *foun
     AQ_HIP(hipMallocAsync((void **)&d, sizeof(int) * (2 * (size_t)n + 1), h->stream));
     AQ_HIP(hipMemcpyAsync(d, rqseqnos, sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
     AQ_HIP(hipMemsetAsync(d + 2 * (size_t)n, 0, sizeof(int), h->stream));
-    k_rq_delete_batch<<<(n + 255) / 256, 256, 0, h->stream>>>(d, n, h->d_rq_live, h->d_ctr, d + n, d + 2 * (size_t)n,
+    k_rq_delete_batch<<<(n + 255) / 256, 256, 0, h->stream>>>(d, n, h->d_rq_live, h->d_rq_seq, h->d_ctr, d + n,
+                                                              d + 2 * (size_t)n,
                                                               nullptr);
     k_rq_delete_fix<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_ctr, d + 2 * (size_t)n);
     AQ_HIP(hipGetLastError());
@@ -658,7 +664,7 @@ int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
             (rc = launch_export(h, g->k, r + g->off_recs, nav)))
             return rc;
         if (h->rq_cap > 0 && g->rqcap > 0) {
-            k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_ctr, g->rqcap,
+            k_rq_compact<<<1, 1024, 0, h->stream>>>(h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_rq_seq, h->d_ctr, g->rqcap,
                                                     r + g->off_rq, rr);
         } else {
             k_rfr_reset<<<(std::max(std::max(h->A, h->num_world), 1) + 255) / 256, 256, 0, h->stream>>>(
@@ -671,6 +677,23 @@ int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
     return ADLBQ_OK;
 }
 
+}  // extern "C"
+
+static int group_host_cap(adlbq_steal_group *g, long long total) {
+    if (total > g->cap_h) {
+        if (g->h_all) AQ_HIP(hipHostFree(g->h_all));
+        g->h_all = nullptr;
+        AQ_HIP(hipHostMalloc((void **)&g->h_all, sizeof(int) * total, hipHostMallocDefault));
+        g->cap_h = total;
+    }
+    return ADLBQ_OK;
+}
+
+static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, int *n_settled,
+                               std::chrono::steady_clock::time_point t0, std::chrono::steady_clock::time_point t1);
+
+extern "C" {
+
 int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, int *n_decided, int *n_settled) {
     if (!g || nproc < 1 || (nproc > 1 && !d_all)) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle");
     adlbq_server *h0 = g->sh[0];
@@ -678,17 +701,46 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
     if (!d_all) d_all = g->d_last;
     if (!d_all) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle: no export");
     const long long total = g->blob * g->n * nproc;
-    if (total > g->cap_h) {
-        if (g->h_all) AQ_HIP(hipHostFree(g->h_all));
-        AQ_HIP(hipHostMalloc((void **)&g->h_all, sizeof(int) * total, hipHostMallocDefault));
-        g->cap_h = total;
-    }
+    int rc;
+    if ((rc = group_host_cap(g, total))) return rc;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     for (int j = 0; j < g->n; j++) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
     AQ_HIP(hipMemcpyAsync(g->h_all, d_all, sizeof(int) * total, hipMemcpyDeviceToHost, h0->stream));
     AQ_HIP(hipStreamSynchronize(h0->stream));
-    const auto t1 = clk::now();
+    return group_settle_staged(g, nproc, n_decided, n_settled, t0, clk::now());
+}
+
+int adlbq_steal_group_export_host(adlbq_steal_group *g, int *h_blob) {
+    if (!g || !h_blob) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_export_host");
+    int rc;
+    if ((rc = adlbq_steal_group_export(g, nullptr))) return rc;
+    adlbq_server *h0 = g->sh[0];
+    for (int j = 0; j < g->n; j++) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
+    AQ_HIP(hipMemcpyAsync(h_blob, g->d_last, sizeof(int) * g->blob * g->n, hipMemcpyDeviceToHost, h0->stream));
+    AQ_HIP(hipStreamSynchronize(h0->stream));
+    return ADLBQ_OK;
+}
+
+int adlbq_steal_group_settle_host(adlbq_steal_group *g, const int *h_all, int nproc, int *n_decided, int *n_settled) {
+    if (!g || nproc < 1 || !h_all) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle_host");
+    hipSetDevice(g->sh[0]->device);
+    const long long total = g->blob * g->n * nproc;
+    int rc;
+    if ((rc = group_host_cap(g, total))) return rc;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    std::memcpy(g->h_all, h_all, sizeof(int) * total);
+    return group_settle_staged(g, nproc, n_decided, n_settled, t0, clk::now());
+}
+
+}  // extern "C"
+
+// The merge and the local side of it over g->h_all = [nproc][n][blob] (any region order).
+static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, int *n_settled,
+                               std::chrono::steady_clock::time_point t0, std::chrono::steady_clock::time_point t1) {
+    using clk = std::chrono::steady_clock;
+    adlbq_server *h0 = g->sh[0];
     const int S = h0->S, T = g->T, nreg = g->n * nproc;
     std::vector<ShardView> vw((size_t)S, ShardView{nullptr, nullptr, nullptr});
     std::vector<int> local_of((size_t)S, -1);
@@ -795,6 +847,8 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
     if (n_settled) *n_settled = won;
     return ADLBQ_OK;
 }
+
+extern "C" {
 
 int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g) {
     if (!g) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_unreserve_grants");

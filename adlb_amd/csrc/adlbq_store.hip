@@ -122,7 +122,67 @@ bool sort_hint(adlbq_server *h) {
 
 constexpr long long RQ_GROW_MAX = 1ll << 24;  // rq entries a growth step reserves at most for batches in flight
 
+// Stable in-place compaction of the live rq entries into slots [0, live), FIFO
+// order kept (the reference frees each entry at rq_delete, xq.c:379; here the
+// slots of dead entries are reclaimed in bulk before the rq would grow).
+// Chunks of 1024 go in order and an entry only moves down; every entry of a
+// chunk is read before any of the chunk is written, so nothing is overwritten
+// before it is read.  rq_seq moves with its entry and stays ascending.
+__global__ __launch_bounds__(1024) void k_rq_reclaim(int *rq_rank, int *rq_types, int *rq_live, int *rq_seq,
+                                                     DevCounters *ctr) {
+    __shared__ int wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int head = ctr->rq_head, n = ctr->rq_n;
+    int base = 0;
+    for (int c0 = head; c0 < n; c0 += 1024) {
+        const int k = c0 + tid;
+        const bool live = k < n && rq_live[k];
+        int rk = 0, sq = 0;
+        int4 ty[NREQ / 4];
+        if (live) {
+            rk = rq_rank[k];
+            sq = rq_seq[k];
+            const int4 *src = reinterpret_cast<const int4 *>(rq_types + (long long)k * NREQ);
+#pragma unroll
+            for (int q = 0; q < NREQ / 4; q++) ty[q] = src[q];
+        }
+        const unsigned long long b = __ballot(live);
+        if (lane == 0) wsum[w] = __popcll(b);
+        __syncthreads();  // also: the whole chunk has been read
+        int pre = base, tot = 0;
+        for (int q = 0; q < 16; q++) {
+            pre += q < w ? wsum[q] : 0;
+            tot += wsum[q];
+        }
+        if (live) {
+            const int pos = pre + __popcll(b & lanemask_lt());
+            rq_rank[pos] = rk;
+            rq_seq[pos] = sq;
+            rq_live[pos] = 1;
+            int4 *dst = reinterpret_cast<int4 *>(rq_types + (long long)pos * NREQ);
+#pragma unroll
+            for (int q = 0; q < NREQ / 4; q++) dst[q] = ty[q];
+        }
+        base += tot;
+        __syncthreads();
+    }
+    for (int k = base + tid; k < n; k += 1024) rq_live[k] = 0;
+    if (tid == 0) {
+        ctr->rq_n = base;
+        ctr->rq_head = 0;
+        ctr->rq_reclaims += 1;
+    }
+}
+
+__global__ void k_set_rq_next(DevCounters *ctr, int v) { ctr->rq_next = v; }
+
 int ensure_rq_capacity(adlbq_server *h, int extra) {
+    if ((h->ctr_stale ? h->rq_next_upper : (long long)h->ctr.rq_next) + extra > INT_MAX) {
+        int rc;
+        if ((rc = refresh_counters(h))) return rc;
+        if ((long long)h->ctr.rq_next + extra > INT_MAX)  // next_rqseqno is an int (adlb.c:1244)
+            return fail(ADLBQ_ERR_NOMEM, "rq: rqseqnos would overflow an int");
+    }
     long long need = (h->ctr_stale ? h->rq_n_upper : (long long)h->ctr.rq_n) + extra;
     if (need <= h->rq_cap) return ADLBQ_OK;
     if (h->ctr_stale) {
@@ -136,6 +196,14 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
     }
+    if (h->rq_cap > 0 && h->d_rq_seq) {  // reclaim the slots of dead entries, then the exact count
+        k_rq_reclaim<<<1, 1024, 0, h->stream>>>(h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr);
+        AQ_HIP(hipGetLastError());
+        int rc;
+        if ((rc = refresh_counters(h))) return rc;  // synchronises
+        need = (long long)h->ctr.rq_n + extra;
+        if (need <= h->rq_cap) return ADLBQ_OK;
+    }
     // room for NSNAP batches of this size in flight at once (76 B per entry),
     // so that the wait above is the snapshot ring's, not a reallocation's
     long long nc = std::max<long long>(need, (long long)h->rq_cap * 2);
@@ -146,6 +214,7 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
     if ((rc = grow(&h->d_rq_types, (long long)h->rq_cap * NREQ, nc * NREQ, h->stream))) return rc;
     if ((rc = grow(&h->d_rq_live, h->rq_cap, nc, h->stream, 0))) return rc;
     if ((rc = grow(&h->d_rq_req, h->rq_cap, nc, h->stream))) return rc;
+    if ((rc = grow(&h->d_rq_seq, h->rq_cap, nc, h->stream))) return rc;
     h->rq_cap = (int)nc;
     return ADLBQ_OK;
 }
@@ -191,6 +260,7 @@ int refresh_counters(adlbq_server *h) {
 static void apply_counters(adlbq_server *h) {
     h->ctr_stale = false;
     h->rq_n_upper = h->ctr.rq_n;
+    h->rq_next_upper = h->ctr.rq_next;
     // units the device-side Get batches removed since the last look
     h->live_units -= h->ctr.got - h->got_seen;
     h->live_targeted -= h->ctr.got_targeted - h->got_t_seen;
@@ -414,8 +484,8 @@ __global__ void k_put_scatter(const PutRec *__restrict__ r, int n, int *prio, ui
 // Put-side FIFO match, one wavefront, Puts strictly in order
 // (rq_find_rank_queued_for_type, xq.c:388-405, at adlb.c:988-1042)
 __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__restrict__ rq_rank,
-                            const int *__restrict__ rq_types, int *rq_live, DevCounters *ctr,
-                            uint32_t *meta, int *pin, int *out3, const int *gate) {
+                            const int *__restrict__ rq_types, int *rq_live, const int *__restrict__ rq_seq,
+                            DevCounters *ctr, uint32_t *meta, int *pin, int *out3, const int *gate) {
     if (gate && *gate == 0) return;  // k_put_match_blk handled the batch
     const int lane = threadIdx.x;
     int head = ctr->rq_head, nrq = ctr->rq_n, live = ctr->rq_live;
@@ -451,7 +521,7 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
                 int rk = rq_rank[found];
                 st_agent(rq_live + found, 0);
                 o[1] = rk;
-                o[2] = found + 1;  // rqseqno == slot + 1
+                o[2] = rq_seq[found];
                 bytes_add(ctr, -BYTES_RQ);  // rq_delete (adlb.c:1040)
                 pin[u.slot] = rk;
                 if (rk >= 0) meta[u.slot] = (uint32_t)u.meta | M_PINNED;
@@ -489,6 +559,7 @@ constexpr int PM_CAP = 4096, PM_THREADS = 1024, PM_PER = PM_CAP / PM_THREADS, PM
 __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__restrict__ r, int n,
                                                               const int *__restrict__ rq_rank,
                                                               const int *__restrict__ rq_types, int *rq_live,
+                                                              const int *__restrict__ rq_seq,
                                                               DevCounters *ctr, uint32_t *meta, int *pin, int *out3,
                                                               const int *__restrict__ utypes, int T, int *over) {
     __shared__ int s_rank[PM_CAP], s_k[PM_CAP];
@@ -627,7 +698,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                 const int k = s_k[e], rk = rq_rank[k];
                 rq_live[k] = 0;
                 o[1] = rk;
-                o[2] = k + 1;  // rqseqno == slot + 1
+                o[2] = rq_seq[k];
                 pin[u[q].slot] = rk;
                 if (rk >= 0) meta[u[q].slot] = (uint32_t)u[q].meta | M_PINNED;
                 acc -= BYTES_RQ;  // rq_delete (adlb.c:1040)
@@ -943,7 +1014,8 @@ __global__ void k_first_unpinned(const int *__restrict__ pages, const int *__res
 
 // check_remote_work_for_queued_apps, one wavefront over rq in FIFO order
 __global__ void k_checkrem(DonorCtx c, const int *__restrict__ rq_rank, const int *__restrict__ rq_types,
-                           const int *rq_live, const DevCounters *ctr, int cap, int *out3, int *count) {
+                           const int *rq_live, const int *__restrict__ rq_seq, const DevCounters *ctr, int cap,
+                           int *out3, int *count) {
     int k0 = ctr->rq_head, nrq = ctr->rq_n, n = 0;
     for (int k = k0; k < nrq; k++) {
         if (!ld_agent(rq_live + k)) continue;
@@ -952,7 +1024,7 @@ __global__ void k_checkrem(DonorCtx c, const int *__restrict__ rq_rank, const in
         int cand = rfr_select(c, rank, rq_types + (long long)k * NREQ);
         if (cand >= 0) {
             if (threadIdx.x == 0 && n < cap) {
-                out3[3 * n] = k + 1;
+                out3[3 * n] = rq_seq[k];
                 out3[3 * n + 1] = rank;
                 out3[3 * n + 2] = cand;
             }
@@ -962,9 +1034,10 @@ __global__ void k_checkrem(DonorCtx c, const int *__restrict__ rq_rank, const in
     if (threadIdx.x == 0) *count = n;
 }
 
-__global__ void k_rq_delete(int k, int *rq_live, DevCounters *ctr, int *res) {
+__global__ void k_rq_delete(int rqseqno, const int *__restrict__ rq_seq, int *rq_live, DevCounters *ctr, int *res) {
     res[0] = 0;
-    if (k >= 0 && k < ctr->rq_n && rq_live[k]) {
+    const int k = rq_slot_of(rq_seq, ctr->rq_n, rqseqno);
+    if (k >= 0 && rq_live[k]) {
         rq_live[k] = 0;
         ctr->rq_live--;
         bytes_add(ctr, -BYTES_RQ);
@@ -976,11 +1049,13 @@ __global__ void k_rq_delete(int k, int *rq_live, DevCounters *ctr, int *res) {
 }
 
 // SS_RFR_RESP failure's retry for the original Reserve (adlb.c:2007-2041): if
-// rqseqno k+1 is still parked, its first type with a donor gets a new SS_RFR
+// rqseqno is still parked, its first type with a donor gets a new SS_RFR
 __global__ void k_rfr_retry(DonorCtx c, const int *__restrict__ rq_rank, const int *__restrict__ rq_types,
-                            const int *rq_live, const DevCounters *ctr, int k, int *out2) {
+                            const int *rq_live, const int *__restrict__ rq_seq, const DevCounters *ctr, int rqseqno,
+                            int *out2) {
     int found = 0, cand = -1;
-    if (k >= 0 && k < ctr->rq_n && ld_agent(rq_live + k)) {
+    const int k = rq_slot_of(rq_seq, ctr->rq_n, rqseqno);
+    if (k >= 0 && ld_agent(rq_live + k)) {
         found = 1;
         cand = rfr_select(c, rq_rank[k], rq_types + (long long)k * NREQ);
     }
@@ -1024,7 +1099,8 @@ __global__ void k_push_take(int slot, int seq, const int *prio, uint32_t *meta, 
 // xq.c:388-405); one wavefront
 __global__ void k_push_commit(int slot, int seq, const int *prio, uint32_t *meta, int *pin, const int *seqa,
                               const int4 *cold1, const int *__restrict__ rq_rank, const int *__restrict__ rq_types,
-                              int *rq_live, DevCounters *ctr, long long *anchor, int *res) {
+                              int *rq_live, const int *__restrict__ rq_seq, DevCounters *ctr, long long *anchor,
+                              int *res) {
     const int lane = threadIdx.x;
     const uint32_t m = meta[slot];
     if (!((m & M_LIVE) && seqa[slot] == seq)) {
@@ -1064,7 +1140,7 @@ __global__ void k_push_commit(int slot, int seq, const int *prio, uint32_t *meta
             const int rk = rq_rank[found];
             st_agent(rq_live + found, 0);
             res[1] = rk;
-            res[2] = found + 1;  // rqseqno == slot + 1
+            res[2] = rq_seq[found];
             bytes_add(ctr, -BYTES_RQ);  // rq_delete (adlb.c:2338)
             pin[slot] = rk;
             if (rk >= 0) meta[slot] = m | M_PINNED;
@@ -1207,7 +1283,7 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->own_stream) hipStreamSynchronize(h->own_stream);
     void *ptrs[] = {h->d_tab, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1, h->d_rrec,
                     h->d_tcnt, h->d_tlist, h->d_seq2slot, h->d_anchor, h->d_anchor_next, h->d_gcut, h->d_gcut_next, h->d_spec, h->d_specn, h->d_utypes, h->d_rq_rank, h->d_rq_types,
-                    h->d_rq_live, h->d_rq_req, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
+                    h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_ctr, h->d_qm_hi, h->d_qm_qlen, h->d_rfr_out, h->d_rfr_to_rank, h->d_tq,
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
@@ -1401,10 +1477,10 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
         AQ_HIP(hipMemsetAsync(h->d_pm_over, h->put_match_block ? 0 : 1, sizeof(int), h->stream));
         if (h->put_match_block)
             k_put_match_blk<<<1, PM_THREADS, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live,
-                                                         h->d_ctr, h->d_meta, h->d_pin,
+                                                         h->d_rq_seq, h->d_ctr, h->d_meta, h->d_pin,
                                                          d_out3 ? d_out3 : h->d_putout, h->d_utypes, h->T,
                                                          h->d_pm_over);
-        k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
+        k_put_match<<<1, 64, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr,
                                              h->d_meta, h->d_pin, d_out3 ? d_out3 : h->d_putout, h->d_pm_over);
         AQ_HIP(hipGetLastError());
         AQ_HIP(hipEventRecord(h->put_ev[sb], h->stream));
@@ -1624,7 +1700,7 @@ int adlbq_check_remote(adlbq_server *h, int cap, int *out3, int *count) {
         AQ_HIP(hipMalloc((void **)&h->d_crem, sizeof(int) * h->cap_crem));
         AQ_HIP(hipHostMalloc((void **)&h->h_crem, sizeof(int) * h->cap_crem, hipHostMallocDefault));
     }
-    k_checkrem<<<1, 64, 0, h->stream>>>(donor_ctx(h), h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr, capd,
+    k_checkrem<<<1, 64, 0, h->stream>>>(donor_ctx(h), h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr, capd,
                                         h->d_crem + 1, h->d_crem);
     AQ_HIP(hipGetLastError());
     AQ_HIP(hipMemcpyAsync(h->h_crem, h->d_crem, sizeof(int) * (3 * (size_t)capd + 1), hipMemcpyDeviceToHost,
@@ -1716,8 +1792,8 @@ int adlbq_rfr_retry(adlbq_server *h, int rqseqno, int *found, int *donor_rank) {
     hipSetDevice(h->device);
     int rc;
     if ((rc = sync_tables(h))) return rc;
-    k_rfr_retry<<<1, 64, 0, h->stream>>>(donor_ctx(h), h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr,
-                                         rqseqno - 1, h->d_result);
+    k_rfr_retry<<<1, 64, 0, h->stream>>>(donor_ctx(h), h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq,
+                                         h->d_ctr, rqseqno, h->d_result);
     AQ_HIP(hipGetLastError());
     AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 2, hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
@@ -1788,7 +1864,7 @@ int adlbq_put_check(adlbq_server *h, int work_len, double max_malloc, int *rejec
 int adlbq_rq_delete(adlbq_server *h, int rqseqno, int *found) {
     if (!ok_handle(h) || !found) return fail(ADLBQ_ERR_ARG, "adlbq_rq_delete");
     hipSetDevice(h->device);
-    k_rq_delete<<<1, 1, 0, h->stream>>>(rqseqno - 1, h->d_rq_live, h->d_ctr, h->d_result);
+    k_rq_delete<<<1, 1, 0, h->stream>>>(rqseqno, h->d_rq_seq, h->d_rq_live, h->d_ctr, h->d_result);
     AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     AQ_HIP(hipStreamSynchronize(h->stream));
     *found = h->h_result[0];
@@ -1863,8 +1939,8 @@ int adlbq_push_commit(adlbq_server *h, int wqseqno, int *out3) {
     int rc;
     if ((rc = sync_tables(h))) return rc;
     k_push_commit<<<1, 64, 0, h->stream>>>((int)slot, wqseqno, h->d_prio, h->d_meta, h->d_pin, h->d_seq, h->d_cold1,
-                                           h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_ctr, h->d_anchor,
-                                           h->d_result);
+                                           h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr,
+                                           h->d_anchor, h->d_result);
     AQ_HIP(hipMemcpyAsync(h->h_result, h->d_result, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
     if ((rc = refresh_counters(h))) return rc;  // synchronises; the rq counts follow the device
     memcpy(out3, h->h_result, sizeof(int) * 3);
@@ -2002,6 +2078,19 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_stamps = value ? 1 : 0;
         return ADLBQ_OK;
     }
+    if (n == "sort_fail_test") {  // test: every batch's candidate sort wait reports giving up
+        h->sort_fail_test = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
+    if (n == "rq_next") {  // test: the next rqseqno less one (only while nothing is parked)
+        int rc;
+        if ((rc = refresh_counters(h))) return rc;
+        if (h->ctr.rq_live != 0 || value < h->ctr.rq_next || value > INT_MAX)
+            return fail(ADLBQ_ERR_ARG, "rq_next: only forward, and only with no Reserve parked");
+        k_set_rq_next<<<1, 1, 0, h->stream>>>(h->d_ctr, (int)value);
+        AQ_HIP(hipGetLastError());
+        return refresh_counters(h);
+    }
     if (n == "chain_rounds") {
         if (value < -1 || value > 30) return fail(ADLBQ_ERR_ARG, "chain_rounds must be in [-1, 30] (-1 = auto)");
         h->chain_rounds = (int)value;
@@ -2081,6 +2170,19 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         return mx ? d.back() : d[d.size() / 2];
     }
     if (n == "parked") return h->ctr.n_parked_last;
+    if (n == "rq_cap") return h->rq_cap;  // rq slots allocated
+    if (n == "rq_slots") {                // rq slots in use, and rqseqnos handed out / compactions
+        refresh_counters(h);
+        return h->ctr.rq_n;
+    }
+    if (n == "rq_next") {
+        refresh_counters(h);
+        return h->ctr.rq_next;
+    }
+    if (n == "rq_reclaims") {
+        refresh_counters(h);
+        return h->ctr.rq_reclaims;
+    }
     if (n == "spec_lists") return h->ctr.spec_page0;
     if (n == "rank_fast") return h->ctr.rank_fast;
     if (n == "tindex_merges") return h->tidx_merges;   // targeted index: incremental merges
@@ -2101,10 +2203,9 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         refresh_counters(h);
         return h->ctr.plan_missed;
     }
-    if (n == "sort_timeouts") {  // k_rank waits for an in-launch sort that gave up (cumulative; 0 unless broken)
-        int v = 0;
-        if (hipMemcpy(&v, h->d_rank_sync + ADLBQ_MAX_TYPES + 1, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-        return v;
+    if (n == "sort_timeouts" || n == "batch_failed") {  // batches answered ADLB_ERROR because k_rank's wait
+        refresh_counters(h);                                // for an in-launch sort gave up (0 unless broken)
+        return h->ctr.batch_failed;
     }
     return -1;
 }

@@ -270,15 +270,22 @@ class StealGroup:
         self.blob_ints = int(self.lib.adlbq_steal_group_blob_ints(g))
         self._dblob = None
         self._gathered = None
+        self._hblob = None
+        self._hall = None
 
     def round(self, group=None, timing=None):
         """One steal round.  Single process: the local blob is merged as it is;
-        with a process group: the blobs are all-gathered (device tensors) first.
-        Returns (decided, settled) over all shards."""
+        with a process group: the blobs are all-gathered first -- device
+        tensors end to end over RCCL ("nccl"), or through pinned host memory
+        over a host backend (gloo; adlbq_steal_group_export_host / _settle_host,
+        the path a node's MPI server processes take).  Returns (decided,
+        settled) over all shards."""
         import torch
         import torch.distributed as dist
         t0 = time.perf_counter()
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        if multi and dist.get_backend(group) != "nccl":
+            return self._round_host(group, timing, t0)
         if multi and self._dblob is None:
             dev = torch.device("cuda", torch.cuda.current_device())
             self._dblob = torch.empty(self.blob_ints, dtype=torch.int32, device=dev)
@@ -298,6 +305,24 @@ class StealGroup:
         nd, ns = ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.adlbq_steal_group_settle(self.g, d_all, nproc, ctypes.byref(nd), ctypes.byref(ns)),
                    "adlbq_steal_group_settle")
+        _tick(timing, "merge_apply", t0)
+        return nd.value, ns.value
+
+    def _round_host(self, group, timing, t0):
+        import torch
+        import torch.distributed as dist
+        w = dist.get_world_size(group)
+        if self._hblob is None:
+            self._hblob = torch.empty(self.blob_ints, dtype=torch.int32).pin_memory()
+            self._hall = torch.empty(w * self.blob_ints, dtype=torch.int32)
+        _lib.check(self.lib.adlbq_steal_group_export_host(self.g, self._hblob.data_ptr()),
+                   "adlbq_steal_group_export_host")
+        parts = list(self._hall.view(w, self.blob_ints).unbind(0))
+        dist.all_gather(parts, self._hblob, group=group)
+        t0 = _tick(timing, "export", t0)
+        nd, ns = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_group_settle_host(self.g, self._hall.data_ptr(), w, ctypes.byref(nd),
+                                                          ctypes.byref(ns)), "adlbq_steal_group_settle_host")
         _tick(timing, "merge_apply", t0)
         return nd.value, ns.value
 

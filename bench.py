@@ -171,6 +171,43 @@ def traffic_of(pmc, stage):
     return round(hits[0]) if len(hits) == 1 else None
 
 
+def _exact_check():
+    """tests/exact_check.py: the size-independent parity checker (test
+    infrastructure; run after the timed region on one timed batch per leg)."""
+    d = os.path.join(ROOT, "tests")
+    if d not in sys.path:
+        sys.path.insert(0, d)
+    import exact_check
+    return exact_check
+
+
+def parity_of(fn) -> dict:
+    """{"parity": True, "parity_detail": ...} if fn() returns, else False with the failure."""
+    try:
+        return {"parity": True, "parity_detail": fn()}
+    except AssertionError as e:
+        return {"parity": False, "parity_detail": f"AssertionError: {e}"}
+
+
+def all_ranks_true(ok: bool) -> bool:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def check_units(ec, w, seq, avail, reqs18, resp, server_rank):
+    """One Reserve batch against the sequential result (exact_check.check_batch,
+    every TA_RESERVE_RESP field)."""
+    n = w.u_type.size
+    common = np.empty((n, 3), np.int32)
+    common[:, 0], common[:, 1:] = 0, -1
+    return ec.check_batch(w.user_types, w.u_type, w.u_prio, w.u_target, seq, avail, reqs18[:, 0], reqs18[:, 2:],
+                          reqs18[:, 1], resp, u_len=w.u_len, u_answer=w.u_answer, u_common=common,
+                          server_rank=server_rank)
+
+
 def cpu_baseline(w, budget_s: float, seed: int, cores: int, equal_prio: bool = False) -> dict:
     """The CPU baseline on the GPU box's host: the reference's
     own src/xq.c (oracle/_ref/libxqref.so, built from /root/reference in the
@@ -237,7 +274,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     S, T = SL * world, 4
     W3 = max(1, args.c3_warmup)
     nb = args.c3_steps + W3
-    srvs, streams, d_reqs, d_resp = [], [], [], []
+    srvs, streams, d_reqs, d_resp, wks, h_reqs = [], [], [], [], [], []
     for j in range(SL):
         idx = rank * SL + j
         w = synth.config3_shard(idx, S, N, T, R, seed=args.seed)
@@ -257,6 +294,8 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
             d_resp.append(torch.empty((nb, R, 12), dtype=torch.int32, device=dev))
         srvs.append(srv)
         streams.append(st)
+        wks.append(w)
+        h_reqs.append(reqs)
     torch.cuda.synchronize()
     keep, parts, sparts = [], {"batches": 0.0, "steal": 0.0, "unreserve": 0.0}, {}
 
@@ -315,6 +354,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         r = step(b)
         settled += r.settled
         decided += r.decided
+    last_round = r
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -341,11 +381,59 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     }
     bg, bd = group.check()
     out["steal_check"] = {"bad_grants": bg, "bad_deletes": bd}
+    par = parity_of(lambda: config3_parity(_exact_check(), wks, h_reqs, d_resp, nb - 1, group, last_round,
+                                           rank * SL, S, decided, settled, nb - W3))
+    if world > 1:
+        par["parity"] = all_ranks_true(par["parity"])
+    out.update(par)
+    if not par["parity"]:
+        out["value"] = None
     group.close()
     if pool is not None:
         pool.shutdown()
     for srv in srvs:
         srv.close()
+    return out
+
+
+def config3_parity(ec, wks, h_reqs, d_resp, b, group, last, idx0, S, decided, settled, steps):
+    """The last timed step of the config-3 leg: every local shard's Reserve
+    batch against the sequential result, then the steal round that followed
+    it against the serial RFR exchanges (exact_check.serial_steal_expect).
+    Needs a clean state before that step: every round decided and settled all
+    parked Reserves (so none was left parked) and every match and grant was
+    unreserved."""
+    R = h_reqs[0].shape[1]
+    resp = [d[b].cpu().numpy() for d in d_resp]
+    nparked = sum(int((r[:, 0] == 0).sum()) for r in resp)
+    assert decided == settled, f"{decided - settled} decided Reserves were not settled (left parked)"
+    assert last.decided == last.settled, "the checked round left Reserves parked"
+    out = {"batches": []}
+    for j, (w, rq, r) in enumerate(zip(wks, h_reqs, resp)):
+        n = w.u_type.size
+        out["batches"].append(check_units(ec, w, np.arange(1, n + 1, dtype=np.int64), np.ones(n, bool), rq[b], r,
+                                          w.num_app_ranks + idx0 + j)["matched"])
+    if S != len(wks):  # several processes: the round's other shards are not held here
+        out["round"] = "per-process batches only (the round spans other processes' shards)"
+        return out
+    assert last.decided == nparked, "the checked round did not consider every parked Reserve"
+    shards_ = []
+    for j, (w, rq, r) in enumerate(zip(wks, h_reqs, resp)):
+        n = w.u_type.size
+        taken = np.zeros(n, bool)
+        taken[r[r[:, 0] == 1, 5] - 1] = True
+        park = np.nonzero(r[:, 0] == 0)[0]
+        rows = np.empty((park.size, 18), np.int32)
+        rows[:, 0], rows[:, 1], rows[:, 2:] = r[park, 10], rq[b][park, 0], rq[b][park, 2:]
+        rows = rows[np.argsort(rows[:, 0], kind="stable")]
+        assert (w.u_target < 0).all()
+        shards_.append({"type": w.u_type, "prio": w.u_prio, "seq": np.arange(1, n + 1), "len": w.u_len,
+                        "answer": w.u_answer, "avail": ~taken, "rq": rows})
+    exp = ec.serial_steal_expect(wks[0].user_types, wks[0].num_app_ranks, shards_, last.decided)
+    got = group.responses()
+    assert got.shape == exp.shape, f"round: {got.shape[0]} settlements, serial model {exp.shape[0]}"
+    assert np.array_equal(got, exp), "round settlements differ from the serial RFR exchanges"
+    out["round_settled"] = int(exp.shape[0])
     return out
 
 
@@ -419,13 +507,39 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
         srv.close()
     if world > 1:
         el, total = shards.reduce_step_timing(el, total)
+        same = all_ranks_true(same)
     return {"workload": f"config5: {S * world} server shards x a tsp-style stream ({A} ranks, {nr} rounds each: "
                         f"{sum(n_ev)} events on this GPU in {sum(n_batches)} calls)",
-            "value": total / el, "unit": "events/s", "seconds": el, "events": total,
+            "value": total / el if same else None, "unit": "events/s", "seconds": el, "events": total,
             "events_per_call": round(sum(n_ev) / max(sum(n_batches), 1), 1),
-            "parity_with_oracle": bool(same),
+            "parity": bool(same), "parity_with_oracle": bool(same),
             "cpu_oracle_events_per_s": sum(n_ev) / cpu_s, "cpu_cores": 1,
             "trace_generation_s": round(gen_s, 1), "scaling": "weak"}
+
+
+def config4_parity(ec, w, puts, applied, reqs, d_resp, d_pout, b, R, server_rank):
+    """Batch b (the last timed one) of the config-4 leg against the sequential
+    result over the queue it saw: the initial units, then every Put batch in
+    the order it went in (wqseqnos in that order), all unpinned (no Reserve
+    ever parked, so no Put matched one, and every match was unreserved)."""
+    from adlb_amd import synth
+    allr = d_resp[:, :, 0].cpu().numpy()
+    assert (allr == 1).all(), "a Reserve parked: the queue state before the batch is not reconstructible here"
+    if puts is not None and applied:
+        pz = np.concatenate([puts[i] for i in applied])
+        n0 = w.u_type.size
+        po = d_pout.cpu().numpy()
+        last = puts[applied[-1]].shape[0]
+        assert (po[:, 0] == np.arange(n0 + pz.shape[0] - last + 1, n0 + pz.shape[0] + 1)).all(), "Put wqseqnos"
+        assert (po[:, 1] == -1).all(), "a Put matched a parked Reserve"
+        w = synth.Workload(user_types=w.user_types, num_app_ranks=w.num_app_ranks,
+                           u_type=np.concatenate([w.u_type, pz[:, 0]]), u_prio=np.concatenate([w.u_prio, pz[:, 1]]),
+                           u_target=np.concatenate([w.u_target, pz[:, 3]]),
+                           u_answer=np.concatenate([w.u_answer, pz[:, 2]]), u_len=np.concatenate([w.u_len, pz[:, 4]]),
+                           r_rank=w.r_rank, r_types=w.r_types, r_hang=w.r_hang, name="config4")
+    n = w.u_type.size
+    return check_units(ec, w, np.arange(1, n + 1, dtype=np.int64), np.ones(n, bool), reqs[b], d_resp[b].cpu().numpy(),
+                       server_rank)
 
 
 def bench_config4(args, torch, dist, world, rank, local, dev):
@@ -480,11 +594,13 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
             d_pout = torch.empty((P, 3), dtype=torch.int32, device=dev)
 
     host_parts = {"put": 0.0, "reserve": 0.0, "unreserve": 0.0}
+    applied = []  # put batches in the order they went in (wqseqnos follow it)
 
     def step(b):
         t0 = time.perf_counter()
         if puts is not None:  # device-resident results: no host round trip
             srv.put_batch_device(puts[b], d_pout.data_ptr())
+            applied.append(b)
         t1 = time.perf_counter()
         srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
         t2 = time.perf_counter()
@@ -528,6 +644,10 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     if world > 1:
         el, matched = shards.reduce_step_timing(el, matched)
     steps = nb - W4
+    par = parity_of(lambda: config4_parity(_exact_check(), w, puts, applied, reqs, d_resp, d_pout, nb - 1, R,
+                                           w.num_app_ranks + rank))
+    if world > 1:
+        par["parity"] = all_ranks_true(par["parity"])
     per_batch = []
     if args.c4_chain_stats:
         for b in range(W4, nb):
@@ -545,7 +665,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "candidate_sort": {"planned": srv.stat("sort_async"), "planned_radix": srv.stat("sort_radix"),
                            "plan_missed": srv.stat("sort_async_bad"),
                            "device_sorted_lists": srv.stat("device_sorted_lists")},
-        "value": matched / el,
+        "value": matched / el if par["parity"] else None,
+        **par,
         "unit": "assignments/s",
         "ms_per_step": el * 1e3 / steps,
         "matched_per_step": matched / steps,
@@ -681,6 +802,14 @@ def main():
         if n - base_dom[1]:
             dom_timed = round((ms - base_dom[0]) / (n - base_dom[1]), 4)
             stages[dominant] = dom_timed
+    # parity gate: the last timed batch against the sequential
+    # result, untimed; every earlier matched unit was unreserved before it
+    ec = _exact_check()
+    par = parity_of(lambda: check_units(ec, w, np.arange(1, N + 1, dtype=np.int64), np.ones(N, bool), reqs[nb - 1],
+                                        d_resp[nb - 1].cpu().numpy(), w.num_app_ranks + rank))
+    par["parity_batch"] = nb - 1
+    if world > 1:
+        par["parity"] = all_ranks_true(par["parity"])
 
     # the host-buffer boundary (adlbq_reserve_batch: requests from host memory,
     # responses back, synchronous): the PCIe-inclusive rate, reported beside
@@ -746,7 +875,8 @@ def main():
     scan_tr = [kernels[k]["traffic"] for k in ("hist", "select") if k in kernels]
     res = {
         "metric": "matched Reserve assignments/sec at 10M-unit queue",
-        "value": matched / el,
+        "value": matched / el if par["parity"] else None,   # no number without parity
+        **par,
         "unit": "assignments/s",
         "n_gpus": world,
         "steps": args.steps,

@@ -33,6 +33,8 @@ extern "C" {
 #define ADLBQ_ERR_NOMEM         -3
 #define ADLBQ_ERR_TYPE          -4   /* work type not declared at create (ADLBP_Put aborts: adlb.c:2762) */
 #define ADLBQ_ERR_UNSUPPORTED   -5   /* e.g. more than ADLBQ_MAX_TYPES types */
+#define ADLBQ_ERR_DEVICE        -6   /* a device-side wait gave up: the batch was answered ADLB_ERROR
+                                        (-1 in word 0 of every reply), nothing pinned or parked */
 
 #define ADLBQ_MAX_TYPES          64  /* request type sets are 64-bit masks on the device */
 #define ADLBQ_REQ_TYPES          16  /* REQ_TYPE_VECT_SZ, src/xq.h:37 */
@@ -75,7 +77,10 @@ int adlbq_put_batch_device(adlbq_server *h, int n, const int *units9, int *d_out
  *              server_rank, common_len, common_server, common_seqno} with
  *              rc = 1 (SUCCESS) / -2 (NO_CURR_WORK) / 0 (parked), and
  *              [10] = rqseqno if parked, [11] = server rank an SS_RFR goes to
- *              (-1 if none). */
+ *              (-1 if none).
+ * ADLBQ_ERR_DEVICE (never a silent wrong match): a device-side wait of the
+ * batch gave up; every reply is ADLB_ERROR and the queues are unchanged.  The
+ * _device variant writes the same replies (stat "batch_failed" counts them). */
 int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12);
 
 /* Same, with reqs18/resp12 in device memory, enqueued on the handle's stream
@@ -238,6 +243,12 @@ int adlbq_steal_group_create(adlbq_steal_group **g, adlbq_server **shards, int n
 long long adlbq_steal_group_blob_ints(adlbq_steal_group *g);
 int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob);
 int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, int *n_decided, int *n_settled);
+/* The same round over a host transport (an MPI_Allgather among a node's
+ * server processes, or gloo): _export_host runs _export into the internal
+ * buffer and copies the blob to h_blob (_blob_ints ints; synchronises);
+ * _settle_host takes the gathered host blobs h_all = [nproc][blob]. */
+int adlbq_steal_group_export_host(adlbq_steal_group *g, int *h_blob);
+int adlbq_steal_group_settle_host(adlbq_steal_group *g, const int *h_all, int nproc, int *n_decided, int *n_settled);
 int adlbq_steal_group_responses(adlbq_steal_group *g, int cap, int *out15, int *count);
 /* the units the local shards pinned in the last settle: rows {local shard j, rank, wqseqno} */
 int adlbq_steal_group_grants(adlbq_steal_group *g, int cap, int *out3, int *count);

@@ -149,3 +149,39 @@ def test_steal_round_allgather_gloo():
         np.testing.assert_array_equal(g[np.lexsort((g[:, 1], g[:, 0]))], e[np.lexsort((e[:, 1], e[:, 0]))])
         for s, left in zip([r, r + 2], got[r][2]):
             assert left == orcs[s].rq_list()[:, 0].tolist()
+
+
+# ------------------------------------------------------------------ the bench's array restatement
+def _array_shards(ws, resps, orcs):
+    out = []
+    for s, w in enumerate(ws):
+        un = w.u_target < 0
+        seq = np.arange(1, w.n_units + 1, dtype=np.int32)
+        taken = np.zeros(w.n_units, bool)
+        r = resps[s]
+        taken[r[r[:, 0] == 1, 5] - 1] = True
+        out.append({"type": w.u_type[un], "prio": w.u_prio[un], "seq": seq[un], "len": w.u_len[un],
+                    "answer": w.u_answer[un], "avail": ~taken[un], "rq": orcs[s].rq_list()})
+    return out
+
+
+@pytest.mark.parametrize("S,seed,kw", [(2, 41, {}), (3, 43, {}), (4, 3, dict(p_remote=0.1, prio_hi=1024)),
+                                       (3, 47, dict(prio_hi=4))])
+def test_serial_steal_expect_matches_oracle(S, seed, kw):
+    """exact_check.serial_steal_expect (the bench's config-3 round check, over
+    sorted arrays) equals oracle.serial_steal_round (the RFR exchanges
+    serialised over the restated linked lists) on the steal-round cases."""
+    from exact_check import serial_steal_expect
+    ws, orcs, resps = build_case(S, n_units=3000, R=512, seed=seed, **kw)
+    sh = _array_shards(ws, resps, orcs)
+    n = sum(x["rq"].shape[0] for x in sh)
+    got = serial_steal_expect(ws[0].user_types, ws[0].num_app_ranks, sh, n)
+    exp = oracle.serial_steal_round(orcs, ws[0].num_app_ranks)
+    assert exp.shape[0] > 0
+    np.testing.assert_array_equal(got, exp)
+    # a decided prefix: the rows of the first requests only
+    cut = sh[0]["rq"].shape[0] + 3
+    part = serial_steal_expect(ws[0].user_types, ws[0].num_app_ranks, _array_shards(ws, resps, build_case(
+        S, n_units=3000, R=512, seed=seed, **kw)[1]), cut)
+    keep = (exp[:, 0] == 0) | ((exp[:, 0] == 1) & np.isin(exp[:, 1], sh[1]["rq"][:3, 0]))
+    np.testing.assert_array_equal(part, exp[keep])
