@@ -54,6 +54,13 @@ SIGNATURES = {
     "adlbsrv_rfr_outstanding": (c_int, [P]),
     "adlbsrv_nmw": (c_int, [P]),
     "adlbsrv_info_get": (c_int, [P, c_int, P]),
+    "adlbsrv_group_create": (c_int, [P, c_int, c_int]),
+    "adlbsrv_group_blob_ints": (ctypes.c_longlong, [P]),
+    "adlbsrv_group_export": (c_int, [P, P]),
+    "adlbsrv_group_settle": (c_int, [P, P, c_int, P]),
+    "adlbsrv_group_stat": (ctypes.c_longlong, [P, c_int]),
+    "adlbsrv_replay_many": (c_int, [P, c_int, c_int, P, P, P, P, P, P]),
+    "adlbsrv_replay_error": (ctypes.c_char_p, []),
 }
 
 _lib = None

@@ -9,8 +9,11 @@
 #include "adlb_core.h"
 
 #include <chrono>
+#include <climits>
 #include <cstring>
+#include <map>
 #include <string>
+#include <tuple>
 #include <unordered_map>
 #include <vector>
 
@@ -81,6 +84,14 @@ struct adlbsrv {
     long long npushed_from = 0, npushed_to = 0, table_events = 0;
     long long row_events = 0;  // changes to this server's qmstat row that are not queue activity (bytes, RFR misses)
     std::unordered_map<int, Held> held;
+    // steal group (adlbsrv_group_*): the node's servers settle their parked
+    // Reserves in export -> all-gather -> merge rounds instead of SS_RFR round
+    // trips; an SS_RFR still goes where the donor may be a tq entry (targeted
+    // units put away from their home server), which a round never exports.
+    adlbq_steal_group *grp = nullptr;
+    std::map<std::tuple<int, int, int>, int> tq;  // (app rank, type, server) -> units: the engine's tq, mirrored
+    long long grp_rounds = 0, grp_settled = 0, rfr_sent = 0;
+    std::vector<int> grp_rows;
 
     int rc(int r, const char *what) {
         if (r) g_err = std::string(what) + ": " + adlbq_last_error();
@@ -92,7 +103,21 @@ struct adlbsrv {
         int b[WIRE_IBUF] = {code};
         send_ints(dest, tag, b, WIRE_IBUF);
     }
+    bool tq_has(int rank, int server) const {
+        auto it = tq.lower_bound(std::make_tuple(rank, INT_MIN, INT_MIN));
+        for (; it != tq.end() && std::get<0>(it->first) == rank; ++it)
+            if (std::get<2>(it->first) == server && it->second > 0) return true;
+        return false;
+    }
+    void tq_add(int rank, int type, int server) { tq[std::make_tuple(rank, type, server)]++; }
+    void tq_dec(int rank, int type, int server) {
+        auto it = tq.find(std::make_tuple(rank, type, server));
+        if (it != tq.end() && --it->second <= 0) tq.erase(it);
+    }
     void send_rfr(int donor, int rqseqno, const Parked &p) {
+        // in a steal group the next round answers it, unless the donor holds targeted work for the rank
+        if (grp && !tq_has(p.rank, donor)) return;
+        rfr_sent++;
         int b[WIRE_RFR] = {rqseqno, p.rank};
         std::memcpy(b + 2, p.types, sizeof(p.types));
         send_ints(donor, TAG_SS_RFR, b, WIRE_RFR);
@@ -181,6 +206,7 @@ int adlbsrv_create(adlbsrv **out, int ntypes, const int *user_types, int num_app
 
 int adlbsrv_destroy(adlbsrv *s) {
     if (!s) return 0;
+    if (s->grp) adlbq_steal_group_destroy(s->grp);
     if (s->q) adlbq_destroy(s->q);
     delete s;
     return 0;
@@ -288,6 +314,7 @@ int adlbsrv_get_common(adlbsrv *s, int src, int cqseqno) {
 
 int adlbsrv_did_put_at_remote(adlbsrv *s, int type, int target, int server_rank) {
     if (s->rc(adlbq_tq_add(s->q, target, type, server_rank), "adlbq_tq_add")) return -1;
+    s->tq_add(target, type, server_rank);
     return s->check_remote();  // adlb.c:1179
 }
 
@@ -436,7 +463,10 @@ int adlbsrv_rfr_resp(adlbsrv *s, int src, const int *b) {
             s->send_ints(rank, TAG_RESERVE_RESP, r, WIRE_IBUF);
             s->served(rqseqno);
             s->activity++;
-            if (for_rank == b[8] && s->rc(adlbq_tq_dec(s->q, for_rank, b[3], src), "adlbq_tq_dec")) return -1;
+            if (for_rank == b[8]) {
+                if (s->rc(adlbq_tq_dec(s->q, for_rank, b[3], src), "adlbq_tq_dec")) return -1;
+                s->tq_dec(for_rank, b[3], src);
+            }
         } else {  // a Put answered it meanwhile: give the unit back (adlb.c:1949-1963)
             int u[WIRE_IBUF] = {for_rank, b[7], b[8]};
             s->send_ints(src, TAG_SS_UNRESERVE, u, WIRE_IBUF);
@@ -581,6 +611,7 @@ int adlbsrv_push_hdr(adlbsrv *s, int src, const int *b, const void *payload, int
     if (h.target >= 0) {  // adlb.c:2246-2272
         if (h.home == s->me) {
             if (s->rc(adlbq_tq_dec(s->q, h.target, h.type, src), "adlbq_tq_dec")) return -1;
+            s->tq_dec(h.target, h.type, src);
         } else {
             int m[WIRE_IBUF] = {h.target, h.type, src, s->me};
             s->send_ints(h.home, TAG_SS_MOVING_TARGETED_WORK, m, WIRE_IBUF);
@@ -608,8 +639,74 @@ int adlbsrv_moving_targeted(adlbsrv *s, int src, const int *b) {
     // the home server's tq follows the unit (adlb.c:2075-2106)
     (void)src;
     if (s->rc(adlbq_tq_dec(s->q, b[0], b[1], b[2]), "adlbq_tq_dec")) return -1;
-    if (b[3] != s->me && s->rc(adlbq_tq_add(s->q, b[0], b[1], b[3]), "adlbq_tq_add")) return -1;
+    s->tq_dec(b[0], b[1], b[2]);
+    if (b[3] != s->me) {
+        if (s->rc(adlbq_tq_add(s->q, b[0], b[1], b[3]), "adlbq_tq_add")) return -1;
+        s->tq_add(b[0], b[1], b[3]);
+    }
     return s->check_remote();
+}
+
+// ---------------------------------------------------------------- steal group
+int adlbsrv_group_create(adlbsrv *s, int k, int rqcap) {
+    if (s->grp) return 0;
+    return s->rc(adlbq_steal_group_create(&s->grp, &s->q, 1, k, rqcap), "adlbq_steal_group_create");
+}
+
+long long adlbsrv_group_blob_ints(adlbsrv *s) { return s->grp ? adlbq_steal_group_blob_ints(s->grp) : -1; }
+
+int adlbsrv_group_export(adlbsrv *s, int *blob) {
+    if (!s->grp) return fail("adlbsrv_group_export: no steal group");
+    return s->rc(adlbq_steal_group_export_host(s->grp, blob), "adlbq_steal_group_export_host");
+}
+
+int adlbsrv_group_settle(adlbsrv *s, const int *all, int nproc, int *settled) {
+    // the round's SS_RFR_RESP successes (adlb.c:1877-1948) for this server's
+    // parked Reserves, and its donor side (1807-1827) for the others'
+    if (!s->grp) return fail("adlbsrv_group_settle: no steal group");
+    int nd = 0, won = 0, cnt = 0;
+    if (s->rc(adlbq_steal_group_settle_host(s->grp, all, nproc, &nd, &won), "adlbq_steal_group_settle_host"))
+        return -1;
+    if (s->rc(adlbq_steal_group_responses(s->grp, 0, nullptr, &cnt), "adlbq_steal_group_responses")) return -1;
+    s->grp_rows.resize(15 * (size_t)cnt);
+    if (cnt && s->rc(adlbq_steal_group_responses(s->grp, cnt, s->grp_rows.data(), &cnt), "adlbq_steal_group_responses"))
+        return -1;
+    for (int i = 0; i < cnt; i++) {
+        const int *r = s->grp_rows.data() + 15 * (size_t)i;
+        auto it = s->parked.find(r[1]);
+        if (it == s->parked.end() || it->second.rank != r[2])
+            return fail("steal round: settled rqseqno " + std::to_string(r[1]) + " is not parked here");
+        int b[WIRE_IBUF];
+        std::memcpy(b, r + 3, sizeof(int) * 10);
+        b[0] = WIRE_SUCCESS;
+        b[10] = b[11] = 0;
+        s->send_ints(r[2], TAG_RESERVE_RESP, b, WIRE_IBUF);
+        s->served(r[1]);
+        s->activity++;
+    }
+    int ng = 0;
+    if (s->rc(adlbq_steal_group_grants(s->grp, 0, nullptr, &ng), "adlbq_steal_group_grants")) return -1;
+    s->activity += ng;  // units this server pinned for other servers' apps
+    if (ng) s->row_events++;
+    int bad_g = 0, bad_d = 0;
+    if (s->rc(adlbq_steal_group_check(s->grp, &bad_g, &bad_d), "adlbq_steal_group_check")) return -1;
+    if (bad_g || bad_d)
+        return fail("steal round: " + std::to_string(bad_g) + " grant(s) found their unit taken, " +
+                    std::to_string(bad_d) + " settled Reserve(s) no longer parked");
+    s->grp_rounds++;
+    s->grp_settled += cnt;
+    if (settled) *settled = cnt;
+    // Reserves the round could not reach (past rqcap, or behind an undecided one) wait for the next round
+    return 0;
+}
+
+long long adlbsrv_group_stat(adlbsrv *s, int which) {
+    switch (which) {
+    case 0: return s->grp_rounds;
+    case 1: return s->grp_settled;
+    case 2: return s->rfr_sent;
+    default: return -1;
+    }
 }
 
 int adlbsrv_num_parked(adlbsrv *s) { return (int)s->parked.size(); }

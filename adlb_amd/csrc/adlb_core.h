@@ -76,6 +76,38 @@ int adlbsrv_push_hdr(adlbsrv *s, int src, const int *b12, const void *payload, i
 int adlbsrv_push_del(adlbsrv *s, int src, const int *b12);
 int adlbsrv_moving_targeted(adlbsrv *s, int src, const int *b12);
 
+/* Steal group (the north star's cross-shard merge): the
+ * node's server processes settle their parked Reserves by rounds of export ->
+ * all-gather of the blobs (the driver's transport: MPI_Allgather among the
+ * servers) -> the deterministic merge of adlbq_steal_merge, which replays the
+ * SS_RFR round trips (adlb.c:1280-1308, 1802-1948, 3536-3579) on one snapshot.
+ * _create: k exported units per type, rqcap parked Reserves per round; from
+ * then on parks send no SS_RFR unless the donor may hold targeted work for
+ * the rank (a tq entry: adlb.c:3493-3500), which a round never exports.
+ * _export writes this server's blob (_blob_ints ints); _settle takes the
+ * gathered blobs of all nproc servers ([nproc][blob], any order), answers the
+ * Reserves of this server the round settled (TA_RESERVE_RESP), pins the units
+ * it donates, and checks that every grant and deletion applied (*settled =
+ * this server's answered Reserves).  Between _export and _settle the caller
+ * must not hand the server any other message.  _stat: 0 rounds, 1 Reserves
+ * settled by rounds, 2 SS_RFRs sent. */
+int adlbsrv_group_create(adlbsrv *s, int k, int rqcap);
+long long adlbsrv_group_blob_ints(adlbsrv *s);
+int adlbsrv_group_export(adlbsrv *s, int *blob);
+int adlbsrv_group_settle(adlbsrv *s, const int *all, int nproc, int *settled);
+long long adlbsrv_group_stat(adlbsrv *s, int which);
+
+/* A native server-loop driver for recorded event streams (adlb_replay.cpp):
+ * n shards' traces (oracle/replay.h format) through the engine ABI, one host
+ * thread per shard; runs of Puts / Reserves / Gets as one batch call each.
+ * outs[j] (caps[j] ints) receives adlb_amd/replay.py's output layout;
+ * nouts[j] = ints written, ncalls[j] = ABI calls made (may be NULL).
+ * Returns 0, -1 (an engine error: adlbsrv_replay_error), -2 (output full). */
+typedef struct adlbq_server adlbq_server;
+int adlbsrv_replay_many(adlbq_server **hs, int n, int ntypes, const int *const *traces, const long long *lens,
+                        int *const *outs, const long long *caps, long long *nouts, long long *ncalls);
+const char *adlbsrv_replay_error(void);
+
 /* state for the driver */
 int adlbsrv_num_parked(adlbsrv *s);     /* rq->count */
 long long adlbsrv_activity(adlbsrv *s); /* events that changed a queue (exhaustion check) */

@@ -13,6 +13,18 @@
 // servers: each server sends its qmstat row to every other server every
 // qmstat interval, and the master decides exhaustion from two consecutive
 // all-idle polls with no queue activity in between.
+//
+// Steal group (the north star's cross-shard merge): when every
+// server shares one node (or ADLB_STEAL_GROUP=1), parked Reserves are not
+// stolen by SS_RFR / SS_RFR_RESP round trips (adlb.c:1280-1308, 1802-2050).
+// Every ADLB_STEAL_INTERVAL s the master opens a round (SRV_STEAL to every
+// server); each server exports its k best available units per type and its
+// parked Reserves, the blobs are all-gathered among the servers
+// (MPI_Allgather), and every server runs the same deterministic merge and
+// settles its own side: answers its parked Reserves the round served, pins
+// the units it donates.  A server takes no other message between its export
+// and its settle, so the merge sees every queue as it is applied.
+// ADLB_STEAL_GROUP=0 keeps the reference's SS_RFR protocol.
 #include <mpi.h>
 
 #include <algorithm>
@@ -31,6 +43,7 @@
 namespace {
 
 MPI_Comm g_all = MPI_COMM_NULL;  // dup of MPI_COMM_WORLD (adlb.c:317)
+MPI_Comm g_srvcomm = MPI_COMM_NULL;  // the server ranks (steal-group all-gather)
 int g_world = 0, g_rank = 0, g_S = 1, g_A = 0, g_master = 0, g_debug = -1;
 int g_home = -1;  // an app's server (adlb.c:258)
 int g_next_put = -1;
@@ -79,6 +92,9 @@ struct Loop {
     int exh_epoch = 0, exh_wait = 0;
     bool exh_all_idle = true, exh_prev_idle = false;
     long long exh_sum = 0, exh_prev_sum = -1;
+    // steal group
+    bool group = false;
+    std::vector<int> blob, blobs;
 };
 Loop *g_loop = nullptr;
 
@@ -179,6 +195,15 @@ void exh_poll(Loop *L) {
     to_servers(L, TAG_SRV_EXH_QUERY, q, (int)sizeof q);
 }
 
+// one steal round: export, all-gather among the servers, settle (no other message in between)
+void steal_round(Loop *L) {
+    check(adlbsrv_group_export(g_srv, L->blob.data()), "steal round export");
+    const int n = (int)L->blob.size();
+    MPI_Allgather(L->blob.data(), n, MPI_INT, L->blobs.data(), n, MPI_INT, g_srvcomm);
+    int settled = 0;
+    check(adlbsrv_group_settle(g_srv, L->blobs.data(), g_S, &settled), "steal round settle");
+}
+
 template <int N>
 void recv_ints(int *b, int src, int tag) {
     MPI_Recv(b, N * (int)sizeof(int), MPI_BYTE, src, tag, g_all, MPI_STATUS_IGNORE);
@@ -208,8 +233,9 @@ void serve(Loop *L, double max_malloc) {
     const double qm_int = env_d("ADLB_QMSTAT_INTERVAL", 0.1);   // adlb.c:165
     const double exh_int = env_d("ADLB_EXHAUST_INTERVAL", 0.5);  // the reference waits 5 s (adlb.c:490)
     const double ds_int = 10.0;
+    const double st_int = env_d("ADLB_STEAL_INTERVAL", 0.01);
     const int T = (int)g_types.size();
-    double t_qm = MPI_Wtime(), t_exh = MPI_Wtime(), t_ds = MPI_Wtime();
+    double t_qm = MPI_Wtime(), t_exh = MPI_Wtime(), t_ds = MPI_Wtime(), t_st = MPI_Wtime();
     std::vector<int> src, buf, one;
     (void)max_malloc;
     while (!L->done) {
@@ -222,6 +248,11 @@ void serve(Loop *L, double max_malloc) {
         if (g_rank == g_master && t - t_exh > exh_int) {
             exh_poll(L);
             t_exh = t;
+        }
+        if (L->group && g_rank == g_master && t - t_st > st_int) {  // open a steal round
+            to_servers(L, TAG_SRV_STEAL, nullptr, 0);
+            steal_round(L);
+            t_st = MPI_Wtime();
         }
         if (g_debug >= 0 && g_rank == g_master && t - t_ds > ds_int) {  // keeps the debug server's watchdog fed
             int b[WIRE_IBUF] = {0};
@@ -320,6 +351,10 @@ void serve(Loop *L, double max_malloc) {
         case TAG_SRV_END:
             MPI_Recv(nullptr, 0, MPI_BYTE, from, tag, g_all, MPI_STATUS_IGNORE);
             L->done = true;
+            break;
+        case TAG_SRV_STEAL:
+            MPI_Recv(nullptr, 0, MPI_BYTE, from, tag, g_all, MPI_STATUS_IGNORE);
+            if (L->group) steal_round(L);
             break;
         case TAG_SRV_QMSTAT: {
             std::vector<char> m(sizeof(int) * (2 + (size_t)T) + sizeof(double));
@@ -473,9 +508,7 @@ int ADLBP_Init(int nservers, int use_debug_server, int aprintf_flag, int ntypes,
     } else {
         *am_server = 1;
         *am_debug_server = 0;
-        MPI_Comm sc;
-        MPI_Comm_split(MPI_COMM_WORLD, 1, g_rank - g_A, &sc);
-        MPI_Comm_free(&sc);
+        MPI_Comm_split(MPI_COMM_WORLD, 1, g_rank - g_A, &g_srvcomm);
         g_is_server = true;
     }
     MPI_Comm_dup(MPI_COMM_WORLD, &g_all);
@@ -500,10 +533,34 @@ int ADLBP_Server(double hi_malloc, double periodic_logging_time) {
         std::string m = std::string("server create: ") + adlbsrv_last_error();
         die(m.c_str());
     }
+    // steal group: every server on one node (or forced by ADLB_STEAL_GROUP); the
+    // decision is collective so that all servers run the rounds or none does
+    int want = 0;
+    if (g_S > 1) {
+        MPI_Comm node;
+        int nn = 0;
+        MPI_Comm_split_type(g_srvcomm, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
+        MPI_Comm_size(node, &nn);
+        MPI_Comm_free(&node);
+        const char *sg = getenv("ADLB_STEAL_GROUP");
+        want = sg && *sg ? atoi(sg) != 0 : nn == g_S;
+    }
+    int all_want = 0;
+    MPI_Allreduce(&want, &all_want, 1, MPI_INT, MPI_MIN, g_srvcomm);
+    if (all_want) {
+        const int k = std::max(1, (int)env_d("ADLB_STEAL_K", 64)), rqcap = std::max(1, (int)env_d("ADLB_STEAL_RQCAP", 1024));
+        check(adlbsrv_group_create(g_srv, k, rqcap), "steal group");
+        L.group = true;
+        L.blob.assign((size_t)adlbsrv_group_blob_ints(g_srv), 0);
+        L.blobs.assign(L.blob.size() * (size_t)g_S, 0);
+    }
     g_loop = &L;
     if (L.my_apps == 0 && g_rank != g_master) emit(&L, g_master, TAG_SRV_DONE, nullptr, 0);
     if (L.my_apps == 0 && g_rank == g_master && ++L.servers_done == g_S) L.done = true;
     serve(&L, hi_malloc);
+    if (L.group && getenv("ADLB_STEAL_REPORT"))
+        fprintf(stderr, "%06d: steal group: %lld rounds, %lld Reserves settled by the merge, %lld SS_RFR sent\n", g_rank,
+                adlbsrv_group_stat(g_srv, 0), adlbsrv_group_stat(g_srv, 1), adlbsrv_group_stat(g_srv, 2));
     g_loop = nullptr;
     return ADLB_SUCCESS;
 }
@@ -547,6 +604,7 @@ int ADLBP_Finalize(void) {
         int dummy = 0;
         MPI_Ssend(&dummy, 0, MPI_INT, g_home, TAG_LOCAL_APP_DONE, g_all);  // adlb.c:3158
     }
+    if (g_srvcomm != MPI_COMM_NULL) MPI_Comm_free(&g_srvcomm);
     if (g_all != MPI_COMM_NULL) MPI_Comm_free(&g_all);
     return ADLB_SUCCESS;
 }

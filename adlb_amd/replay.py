@@ -116,3 +116,30 @@ def replay(srv: Server, trace) -> np.ndarray:
             else:
                 raise ValueError(f"unknown opcode {op}")
     return np.concatenate(out) if out else np.zeros(0, np.int32)
+
+
+def replay_many(servers, traces, cap_factor: int = 8):
+    """The traces of several shards replayed at once by the native driver
+    (adlb_amd/csrc/adlb_replay.cpp, one host thread per shard, each handle on
+    its own stream): the same calls and output stream as replay() per shard.
+    Returns (outputs, ABI calls per shard)."""
+    import ctypes
+
+    from . import core
+    lib = core.load()
+    n = len(servers)
+    trs = [np.ascontiguousarray(np.asarray(t, dtype=np.int32)) for t in traces]
+    outs = [np.empty(cap_factor * t.size + (1 << 20), np.int32) for t in trs]
+    PA = ctypes.c_void_p * n
+    LA = ctypes.c_longlong * n
+    hs = PA(*[s.h.value if hasattr(s.h, "value") else s.h for s in servers])
+    tp = PA(*[t.ctypes.data for t in trs])
+    lens = LA(*[t.size for t in trs])
+    op = PA(*[o.ctypes.data for o in outs])
+    caps = LA(*[o.size for o in outs])
+    nout, ncall = LA(), LA()
+    T = servers[0].T
+    rc = lib.adlbsrv_replay_many(hs, n, T, tp, lens, op, caps, nout, ncall)
+    if rc:  # -2: an output buffer was too small (the servers have moved on: no retry)
+        raise RuntimeError(f"adlbsrv_replay_many: {lib.adlbsrv_replay_error().decode(errors='replace')}")
+    return [o[: nout[j]].copy() for j, o in enumerate(outs)], [ncall[j] for j in range(n)]

@@ -126,6 +126,31 @@ def test_stream_vs_oracle(gpu_available):
     assert_same(run_abi([1, 2], cfg, tr), run_oracle([1, 2], cfg, tr))
 
 
+def test_stream_native_concurrent_vs_oracle(gpu_available):
+    """Four shards' config-5 streams replayed at once by the native driver
+    (adlb_replay.cpp: one host thread and HIP stream per shard, the bench's
+    config-5 path): every shard's output equals the oracle's, and equals the
+    Python driver's on the same handle type."""
+    S, A = 4, 128
+    traces, exp = [], []
+    for j in range(S):
+        o = oracle.Oracle("own", private=True)
+        o.init([1, 2], A, S, j)
+        tr = synth.config5_stream(lambda ev: synth.split_outputs(o.replay(ev)), n_rounds=120, n_ranks=A,
+                                  n_servers=S, my_idx=j, seed=700 + j)
+        traces.append(np.asarray(tr, np.int32))
+        exp.append(run_oracle([1, 2], (A, S, j), tr))
+    srvs = [Server([1, 2], A, S, j, max_units=1 << 16) for j in range(S)]
+    try:
+        got, calls = replay.replay_many(srvs, traces)
+    finally:
+        for s in srvs:
+            s.close()
+    for j in range(S):
+        assert calls[j] > 0
+        assert_same(got[j], exp[j])
+
+
 def _exact_full(w, batches=1, stats=None, params=()):
     with Server(w.user_types, w.num_app_ranks, max_units=w.n_units) as s:
         for k, v in params:

@@ -97,27 +97,47 @@ def test_nq_two_servers_352():
     assert "found 352 solutions" in out, out[-2000:]
 
 
-def _run_mix(np_, args, timeout=240):
+def _run_mix(np_, args, timeout=240, env_extra=None):
     if not os.path.exists(MIX):
         pytest.skip("tests/apps/adlb_mix not built")
-    env = dict(os.environ, ADLB_DEVICE="0")
+    env = dict(os.environ, ADLB_DEVICE="0", **(env_extra or {}))
     r = subprocess.run([MPIRUN, "-np", str(np_), MIX, *args], env=env, capture_output=True, text=True,
                        timeout=timeout)
     assert r.returncode == 0, f"rc={r.returncode}\nstdout:\n{r.stdout[-3000:]}\nstderr:\n{r.stderr[-3000:]}"
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("adlb_mix:")]
     assert line, r.stdout[-2000:]
     v = line[0].split()
+    if env_extra is not None:
+        return r.stdout, (int(v[2]), int(v[4])), (int(v[6]), int(v[7])), r.stderr
     return r.stdout, (int(v[2]), int(v[4])), (int(v[6]), int(v[7]))
 
 
+def _steal_report(err):
+    """per server: (rounds, Reserves settled by the merge, SS_RFRs sent)"""
+    rows = [ln.split(": steal group: ")[1] for ln in err.splitlines() if ": steal group: " in ln]
+    return [(int(r.split()[0]), int(r.split()[2]), int(r.split()[-3])) for r in rows]
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("group", ["0", "1"])
 @pytest.mark.parametrize("np_,ns,n", [(6, 2, 200), (7, 3, 150), (10, 4, 300)])
-def test_mix_every_unit_once(np_, ns, n):
+def test_mix_every_unit_once(np_, ns, n, group):
     """Steals, targeted units, a common-prefix batch: every unit is consumed
     exactly once before exhaustion (the reference run of the 3-server case
-    declares exhaustion with units left; see oracle/gen_nq.py)."""
-    out, got, exp = _run_mix(np_, ["-nservers", str(ns), "-n", str(n)])
+    declares exhaustion with units left; see oracle/gen_nq.py).  group "0":
+    the reference's SS_RFR round trips; "1": the steal group, where the
+    servers settle parked Reserves by export -> MPI_Allgather -> merge rounds
+    (no SS_RFR for untargeted work) -- the rounds must have settled some."""
+    out, got, exp, err = _run_mix(np_, ["-nservers", str(ns), "-n", str(n)],
+                                  env_extra={"ADLB_STEAL_GROUP": group, "ADLB_STEAL_REPORT": "1"})
     assert got == exp, out[-2000:]
+    rep = _steal_report(err)
+    if group == "1":
+        assert len(rep) == ns, err[-2000:]
+        assert all(r[0] > 0 for r in rep), rep
+        assert sum(r[1] for r in rep) > 0, f"no Reserve settled by a steal round: {rep}"
+    else:
+        assert rep == [], err[-2000:]
 
 
 @pytest.mark.gpu
