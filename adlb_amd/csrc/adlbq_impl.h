@@ -81,6 +81,9 @@ struct DevCounters {
     // structures this handle replaces, plus what the caller adds (adlbq_bytes_adjust)
     long long bytes, bytes_hwm;
     long long got, got_targeted;  // units removed by device-side Get batches (folded into the host counts)
+    // in a batch snapshot (mapped host memory): the batch's tag, stored after every other
+    // field has been written back; the host reads the snapshot once the tag matches
+    unsigned long long snap_tag;
 };
 
 __device__ __forceinline__ void bytes_add(DevCounters *c, long long d) {  // one thread, in event order
@@ -183,7 +186,8 @@ struct adlbq_server {
     // each reserve batch, so the rq capacity bound tightens without a sync
     static constexpr int NSNAP = 8;
     adlbq::DevCounters *h_snap = nullptr;   // [NSNAP] pinned, device-visible
-    hipEvent_t snap_ev[NSNAP] = {};
+    unsigned long long snap_tag[NSNAP] = {};  // the tag k_finalize stores last into that snapshot (0: unused)
+    unsigned long long snap_tags = 0;          // tags handed out
     long long snap_at[NSNAP] = {};         // reserves launched up to and including that batch
     int snap_next = 0;
     adlbq::DevCounters *d_snap = nullptr;   // device address of h_snap (mapped)
@@ -281,6 +285,8 @@ struct adlbq_server {
     int chain_passes = 0;              // round 0's in-launch passes, 0 = auto (adlbq_set_param "chain_passes")
     int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
     int put_match_block = 1, put_always_match = 0;  // diagnostics ("put_match_block", "put_always_match")
+    int hist_diag = 0;                 // diagnostic ("hist_diag"): parts of pass 1 skipped (wrong results)
+    int split_prep = 0;                // diagnostic ("split_prep"): request preparation and pass 1 as two launches
     int rank_in_select = 1;            // k_select_open ranks the candidates when it can ("rank_in_select")
     int sort_fail_test = 0;            // test hook ("sort_fail_test"): the error path of a failed sort wait
     int chain_stamps = 0;              // diagnostic: phase stamps of the first chain launch ("chain_stamps")
@@ -316,6 +322,8 @@ struct adlbq_server {
     long long last_scan_units = 0;
 
     bool profiling = false;
+    int profile_every = 1;                    // stage events on every n-th reserve batch only ("profile_every")
+    long long reserve_batches = 0;            // reserve batches launched
     std::string profile_only;                 // empty: every stage
     std::vector<hipEvent_t> event_pool;
     std::unordered_map<std::string, adlbq::StageTimer> timers;

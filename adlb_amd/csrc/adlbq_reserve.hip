@@ -178,6 +178,7 @@ struct HistArgs {
     unsigned int *spec;      // [npages][4][SPEC_CAP] per wave: (column << 12 | slot-in-page), slot order
     int *specn;              // [npages][4] entries found (> SPEC_CAP: overflowed, not usable)
     const int *pbase, *pwide;  // per page id: packed-offset base, wide flag
+    int diag;                  // diagnostic ("hist_diag", wrong results): bit 0 no lists, 1 no epilogue, 2 no counts
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -251,8 +252,8 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
             const int t = mm[q] & M_TYPE;
             const int2 ag = sag[t];
             col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
-            in[q] = av && pr[q] >= ag.y;
-            if (av) atomicAdd(&my[col[q] * HK], 1u);
+            in[q] = av && pr[q] >= ag.y && !(a.diag & 1);
+            if (av && !(a.diag & 4)) atomicAdd(&my[col[q] * HK], 1u);
         }
         const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
                                  b3 = __ballot(in[3]);
@@ -270,6 +271,7 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
     }
     if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
+    if (a.diag & 2) return;
     unsigned int *cs = csum + (long long)(p / CHUNK) * C;
     unsigned short *g = gh + (long long)p * C;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -2229,7 +2231,7 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
                                                   int my_world, int *__restrict__ resp, DevCounters *ctr,
                                                   DonorCtx dc, int donors, int *rq_rank, int *rq_types,
                                                   int *rq_live, int *rq_req, int *rq_seq, int *dem, int T,
-                                                  DevCounters *snap,
+                                                  DevCounters *snap, unsigned long long snap_tag,
                                                   long long *anchor, long long *anchor_next,
                                                   unsigned long long *pmask, long long *gcut, long long *gcut_next,
                                                   const int4 *__restrict__ rrec, const int *__restrict__ needsort,
@@ -2326,7 +2328,10 @@ __global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, 
         ctr->needsort_last = ns;  // the host launches the segmented sort while this holds
         for (int g = 0; g < 8; g++) ctr->fin_group[g] = 0;
         ctr->fin_top = 0;
-        *snap = *ctr;  // mapped host memory; visible to the host once the kernel has completed
+        // mapped host memory: every field written back, then the tag the host waits for
+        *snap = *ctr;
+        __threadfence_system();
+        __hip_atomic_store(&snap->snap_tag, snap_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2472,14 +2477,23 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     hipEvent_t ev;
     const bool scan = np > 0 && T > 0;
     const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, h->d_csum,
-                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide};
+                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0};
     const int grid = nprep + (scan ? np : 0);
     if (grid > 0) {
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0, scan ? sizeof(unsigned int) * HK * C : 0);
         stage_begin(h, "hist", &ev);
-        if (T <= 4) k_prep_hist<4><<<grid, 256, lds, s>>>(pa, nprep, ha);
-        else if (T <= 8) k_prep_hist<8><<<grid, 256, lds, s>>>(pa, nprep, ha);
-        else k_prep_hist<64><<<grid, 256, lds, s>>>(pa, nprep, ha);
+        auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
+        if (h->hist_diag && scan) {  // diagnostic: an extra pass 1 (no epilogue) with parts skipped, before the real one
+            HistArgs hd = ha;
+            hd.diag = h->hist_diag | 2;
+            kph<<<np, 256, lds, s>>>(pa, 0, hd);
+        }
+        if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
+            kph<<<nprep, 256, lds, s>>>(pa, nprep, ha);
+            kph<<<np, 256, lds, s>>>(pa, 0, ha);
+        } else {
+            kph<<<grid, 256, lds, s>>>(pa, nprep, ha);
+        }
         stage_end(h, "hist", ev);
     }
     if (scan) {
@@ -3283,6 +3297,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
     const auto host_t0 = std::chrono::steady_clock::now();
     h->hint_stamp++;  // landed-snapshot hints are looked up once for this launch
+    h->reserve_batches++;
     if ((rc = ensure_req_capacity(h, R))) return rc;
     if ((rc = sync_tables(h))) return rc;
     if ((rc = ensure_rq_capacity(h, R))) return rc;
@@ -3418,11 +3433,13 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     {
         const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
         DevCounters *snap = h->d_snap + h->snap_next;
+        h->snap_tag[h->snap_next] = ++h->snap_tags;
+        __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);  // not landed until k_finalize stores it
         k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
                                                    h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
                                                    h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
                                                    h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, T,
-                                                   snap,
+                                                   snap, h->snap_tag[h->snap_next],
                                                    h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut,
                                                    h->d_gcut_next, h->d_rrec, h->d_needsort,
                                                    h->d_rank_sync + ADLBQ_MAX_TYPES + 1);
@@ -3433,7 +3450,6 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     h->batch_export_R = R;
     h->launched_reserves += R;
     h->snap_at[h->snap_next] = h->launched_reserves;
-    AQ_HIP(hipEventRecord(h->snap_ev[h->snap_next], s));
     h->snap_next = (h->snap_next + 1) % adlbq_server::NSNAP;
     h->hint_stamp++;  // a new snapshot slot is in flight: look again next time
     AQ_HIP(hipGetLastError());

@@ -55,15 +55,22 @@ static int grow_pages(adlbq_server *h, int need) {
     return ADLBQ_OK;
 }
 
+// Snapshot slot i has landed: k_finalize stores the slot's tag after writing
+// the rest back (no event per batch: an event record stalls the queue for
+// several microseconds behind the kernel before it).
+static bool snap_landed(const adlbq_server *h, int i) {
+    return h->snap_tag[i] != 0 && __atomic_load_n(&h->h_snap[i].snap_tag, __ATOMIC_ACQUIRE) == h->snap_tag[i];
+}
+
 // the newest reserve-batch snapshot that has landed in host memory, or -1; the
-// event queries run once per hint_stamp (one launch), older answers stay valid
+// tag checks run once per hint_stamp (one launch), older answers stay valid
 static int newest_landed(adlbq_server *h) {
     if (h->landed_stamp == h->hint_stamp) return h->landed_idx;
     const int N = adlbq_server::NSNAP;
     int found = -1;
     for (int k = 1; k <= N && found < 0; k++) {
         const int i = (h->snap_next - k + N) % N;
-        if (h->snap_at[i] && hipEventQuery(h->snap_ev[i]) == hipSuccess) found = i;
+        if (h->snap_at[i] && snap_landed(h, i)) found = i;
     }
     h->landed_idx = found;
     h->landed_stamp = h->hint_stamp;
@@ -72,19 +79,14 @@ static int newest_landed(adlbq_server *h) {
 
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest) {
     const int N = adlbq_server::NSNAP;
-    if (wait_oldest) {  // backpressure: let the oldest batch still tracked land
-        for (int k = N; k >= 1; k--) {
-            const int i = (h->snap_next - k + N) % N;
-            if (h->snap_at[i]) {
-                hipEventSynchronize(h->snap_ev[i]);
-                break;
-            }
-        }
+    if (wait_oldest) {  // backpressure: let the batches in flight land (every snapshot tag is then stored)
+        hipStreamSynchronize(h->stream);
+        h->hint_stamp++;
     }
     for (int k = 1; k <= N; k++) {
         const int i = (h->snap_next - k + N) % N;
         if (!h->snap_at[i]) continue;
-        if (hipEventQuery(h->snap_ev[i]) != hipSuccess) continue;
+        if (!snap_landed(h, i)) continue;
         const long long bound = (long long)h->h_snap[i].rq_n + (h->launched_reserves - h->snap_at[i]);
         if (bound < h->rq_n_upper) h->rq_n_upper = bound;
         return;
@@ -405,7 +407,10 @@ static hipEvent_t pooled_event(adlbq_server *h) {
 }
 
 static bool stage_on(adlbq_server *h, const char *name) {
-    return h->profiling && (h->profile_only.empty() || h->profile_only == name);
+    // "profile_every" n: only every n-th reserve batch carries stage events (an
+    // event record stalls the queue for microseconds behind the kernel before it)
+    return h->profiling && (h->profile_only.empty() || h->profile_only == name) &&
+           (h->profile_every <= 1 || h->reserve_batches % h->profile_every == 0);
 }
 
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev) {
@@ -1252,8 +1257,8 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMalloc((void **)&h->d_ctr, sizeof(DevCounters)));
     AQ_HIP(hipMemsetAsync(h->d_ctr, 0, sizeof(DevCounters), h->stream));
     AQ_HIP(hipHostMalloc((void **)&h->h_snap, sizeof(DevCounters) * adlbq_server::NSNAP, hipHostMallocMapped));
+    memset(h->h_snap, 0, sizeof(DevCounters) * adlbq_server::NSNAP);
     AQ_HIP(hipHostGetDevicePointer((void **)&h->d_snap, h->h_snap, 0));
-    for (int i = 0; i < adlbq_server::NSNAP; i++) AQ_HIP(hipEventCreateWithFlags(&h->snap_ev[i], hipEventDisableTiming));
     AQ_HIP(hipMalloc((void **)&h->d_dem, sizeof(int) * T1));
     AQ_HIP(hipMemsetAsync(h->d_dem, 0, sizeof(int) * T1, h->stream));  // k_finalize re-zeroes it after every batch
     AQ_HIP(hipMalloc((void **)&h->d_theta, sizeof(int) * T1));
@@ -1314,8 +1319,6 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->tnew_ev) hipEventDestroy(h->tnew_ev);
     if (h->steal_ev) hipEventDestroy(h->steal_ev);
     if (h->apply_ev) hipEventDestroy(h->apply_ev);
-    for (int i = 0; i < adlbq_server::NSNAP; i++)
-        if (h->snap_ev[i]) hipEventDestroy(h->snap_ev[i]);
     for (auto &kv : h->timers)
         for (auto &pe : kv.second.pending) {
             hipEventDestroy(pe.first);
@@ -2060,6 +2063,18 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (n == "chain_passes") {
         if (value < 0 || value > 8) return fail(ADLBQ_ERR_ARG, "chain_passes must be in [0, 8] (0 = auto)");
         h->chain_passes = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "profile_every") {
+        h->profile_every = (int)std::max(1ll, value);
+        return ADLBQ_OK;
+    }
+    if (n == "hist_diag") {
+        h->hist_diag = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "split_prep") {
+        h->split_prep = value ? 1 : 0;
         return ADLBQ_OK;
     }
     if (n == "rank_in_select") {

@@ -62,6 +62,8 @@ def parse():
                     help="CPU baseline processes (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP event timing")
+    ap.add_argument("--profile-every", type=int, default=4,
+                    help="timed region: HIP events around the dominant kernel on every n-th batch")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 steal-round measurement")
     ap.add_argument("--c3-servers", type=int, default=8, help="config 3: server shards per GPU")
@@ -100,6 +102,8 @@ def parse():
     ap.add_argument("--chain-modes", type=int, default=None, help="metric leg: adlbq 'chain_modes'")
     ap.add_argument("--rank-in-select", type=int, default=None, help="metric leg: adlbq 'rank_in_select'")
     ap.add_argument("--chain-warm", type=int, default=None, help="metric leg: adlbq 'chain_warm' (0, 256, 512)")
+    ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
+                    help="metric leg: any adlbq_set_param (diagnostics), repeatable")
     ap.add_argument("--c4-chain-stats", action="store_true",
                     help="config 4: after the timed region, replay each batch alone and report its chain counters")
     ap.add_argument("--c4-segsort-async", type=int, default=None,
@@ -739,6 +743,9 @@ def main():
         srv.set_param("chain_rounds", args.chain_rounds)
     if args.rank_in_select is not None:
         srv.set_param("rank_in_select", args.rank_in_select)
+    for kv in args.param:
+        k, v = kv.split("=", 1)
+        srv.set_param(k, int(v))
     # one explicit stream for the library and the torch glue ops (the handle's
     # own stream is non-blocking and would not order against torch's null stream)
     stream = torch.cuda.Stream(dev)
@@ -784,6 +791,9 @@ def main():
         dominant = max(stages, key=stages.get) if stages else None
         # the timed region carries events around the dominant stage only
         srv.profile_only(dominant)
+        # every n-th timed batch carries the two events (each event record holds
+        # the queue ~5 us behind the kernel before it)
+        srv.set_param("profile_every", args.profile_every)
         base_dom = srv.profile_read(dominant)
     if world > 1:
         dist.barrier()
