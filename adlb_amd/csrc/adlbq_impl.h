@@ -378,18 +378,37 @@ __device__ __forceinline__ int rq_slot_of(const int *rq_seq, int n, int rqseqno)
     return (lo < n && rq_seq[lo] == rqseqno) ? lo : -1;
 }
 
+// Histogram bins of a distance d = anchor - prio: [0, NBX) exact (one
+// priority each), then NBH half-octave bins up to 2^(5 + NBH/2), then octaves;
+// the last bin (NB - 1) is unbounded.  A threshold in a multi-priority bin
+// takes the whole bin into the candidate list (sorted later), so the finer
+// bins where thresholds usually fall keep that overshoot at most 50%.
+constexpr int NBH = 24;
+constexpr int OCT_H = 5 + NBH / 2;  // first octave with a single bin
 __device__ __forceinline__ int bin_of(long long d) {
     if (d < NBX) return (int)d;
-    int o = 63 - __clzll((unsigned long long)d);  // 5 .. 33
-    int b = NBX + (o - 5);
+    const int o = 63 - __clzll((unsigned long long)d);  // >= 5
+    const int b = o < OCT_H ? NBX + 2 * (o - 5) + (int)((d >> (o - 1)) & 1) : NBX + NBH + (o - OCT_H);
     return b < NB ? b : NB - 1;
 }
 
 // bin_of for a distance known to fit 32 bits (an int anchor less an int prio)
 __device__ __forceinline__ int bin_of32(unsigned int d) {
     if (d < (unsigned int)NBX) return (int)d;
-    const int b = NBX + (31 - __clz((int)d)) - 5;
+    const int o = 31 - __clz((int)d);
+    const int b = o < OCT_H ? NBX + 2 * (o - 5) + (int)((d >> (o - 1)) & 1u) : NBX + NBH + (o - OCT_H);
     return b < NB ? b : NB - 1;
+}
+
+// the smallest distance bin b holds, and the largest (NB - 1: unbounded)
+__host__ __device__ __forceinline__ long long bin_lo(int b) {
+    if (b < NBX) return b;
+    const int k = b - NBX;
+    if (k < NBH) return (long long)(2 + (k & 1)) << (5 + k / 2 - 1);
+    return 1ll << (OCT_H + (k - NBH));
+}
+__host__ __device__ __forceinline__ long long bin_hi(int b) {
+    return b >= NB - 1 ? (1ll << 40) : bin_lo(b + 1) - 1;
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() {

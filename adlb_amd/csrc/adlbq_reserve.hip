@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistA
 // below NBX, then powers of two); no bin (th < 0) cuts above every prio.
 __device__ __forceinline__ long long cut_of(int th, long long an) {
     if (th < 0) return 1ll << 40;
-    const long long dmax = th < NBX ? th : th >= NB - 1 ? (1ll << 40) : (1ll << (th - NBX + 6)) - 1;
+    const long long dmax = bin_hi(th);
     return std::max(an - dmax, (long long)LOWEST + 1);
 }
 
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(int T, const int *__r
             // the live maximum is at most anchor - (smallest distance of the first
             // non-empty bin): the next batch's anchor (applied when this batch ends)
             const int bb = __ffsll((long long)nz) - 1;
-            anchor_next[t] = anchor[t] - (bb < NBX ? bb : (1ll << (bb - NBX + 5)));
+            anchor_next[t] = anchor[t] - bin_lo(bb);
         }
         if (hit) {
             th = __ffsll((long long)hit) - 1;

@@ -119,7 +119,9 @@ bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi) {
 
 bool sort_hint(adlbq_server *h) {
     const int i = newest_landed(h);
-    return i >= 0 && h->h_snap[i].needsort_last != 0;
+    // nothing landed yet (the first batches): sort whatever needs it through the
+    // read-back path, never through k_rank's in-launch sort (milliseconds on long lists)
+    return i < 0 || h->h_snap[i].needsort_last != 0;
 }
 
 constexpr long long RQ_GROW_MAX = 1ll << 24;  // rq entries a growth step reserves at most for batches in flight

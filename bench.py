@@ -95,6 +95,8 @@ def parse():
     ap.add_argument("--chain-rounds", type=int, default=None, help="metric leg: adlbq 'chain_rounds'")
     ap.add_argument("--no-host-path", action="store_true",
                     help="metric leg: skip the host-buffer (PCIe-inclusive) adlbq_reserve_batch measurement")
+    ap.add_argument("--chain-per-batch", action="store_true",
+                    help="metric leg: the chain's counters of every timed batch (untimed replay)")
     ap.add_argument("--chain-stamps", action="store_true",
                     help="metric leg: after the timed region, one batch with the chain's phase stamps (diagnostic)")
     ap.add_argument("--c4-chain-modes", type=int, default=None, help="config 4: adlbq 'chain_modes'")
@@ -438,6 +440,32 @@ def config3_parity(ec, wks, h_reqs, d_resp, b, group, last, idx0, S, decided, se
     assert got.shape == exp.shape, f"round: {got.shape[0]} settlements, serial model {exp.shape[0]}"
     assert np.array_equal(got, exp), "round settlements differ from the serial RFR exchanges"
     out["round_settled"] = int(exp.shape[0])
+    return out
+
+
+def host_latency_table(srv, torch, dev, reqs, d_reqs, d_resp, sizes=(1, 16, 256, 4096), reps=20):
+    """Latency of the synchronous host-buffer entry point libadlb.so calls
+    (adlbq_reserve_batch: requests from host memory, responses back) against
+    the batch size R, on the metric queue: median and p90 over `reps` calls of
+    the first R Reserves of one batch, each followed (untimed) by SS_UNRESERVE
+    of its matches so every call sees the same queue."""
+    out = []
+    for r in sizes:
+        if r > reqs.shape[0]:
+            continue
+        sub = np.ascontiguousarray(reqs[:r])
+        ts = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            resp = srv.reserve_batch(sub)
+            ts.append(time.perf_counter() - t)
+            d_resp[:r].copy_(torch.from_numpy(resp).to(dev))
+            srv.unreserve_resp_device(r, d_reqs.data_ptr(), d_resp.data_ptr())
+            srv.sync()
+        ts = np.sort(np.array(ts)) * 1e3
+        out.append({"R": r, "ms_median": round(float(np.median(ts)), 4),
+                    "ms_p90": round(float(ts[int(0.9 * (len(ts) - 1))]), 4),
+                    "assignments_per_s_median": round(r / (float(np.median(ts)) * 1e-3), 1)})
     return out
 
 
@@ -847,7 +875,18 @@ def main():
                                                 / t_res, 1) if t_res else None,
                      "bytes_over_pcie_per_batch": (ADLBQ_RESERVE_INTS * 4 + 12 * 4) * R,
                      "step_ms_with_restore": round((time.perf_counter() - t1) * 1e3 / hb, 4)}
+        host_path["latency_vs_batch"] = host_latency_table(srv, torch, dev, reqs[args.warmup], d_reqs[args.warmup],
+                                                           d_resp[args.warmup])
 
+    chain_batches = None
+    if args.chain_per_batch:  # untimed: the timed batches again, one at a time, with the chain's counters
+        chain_batches = []
+        for b in range(args.warmup, nb):
+            srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+            srv.sync()
+            chain_batches.append([srv.stat("chain_" + k) for k in ("passes", "recomputed", "fallback", "timeouts")])
+            srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        srv.sync()
     phases = None
     if args.chain_stamps:
         srv.set_param("chain_stamps", 1)
@@ -917,6 +956,8 @@ def main():
     }
     if phases:
         res["chain_phases_ns"] = phases
+    if chain_batches is not None:
+        res["chain_per_batch"] = {"fields": ["passes", "recomputed", "fallback", "timeouts"], "batches": chain_batches}
     srv.close()
     del d_reqs, d_resp
     if not args.no_config3:

@@ -13,6 +13,7 @@ HB=$!
 trap "kill $HB" EXIT
 cd /tmp
 timeout -k 10 200 python3 -c "import torch; print('torch', torch.__version__, torch.cuda.is_available())" || exit 1
+if [ -x $R/tools/ubench_scan ] && [ -n "$UBENCH" ]; then timeout -k 10 120 $R/tools/ubench_scan > $O/ubench_scan.txt 2>&1; cat $O/ubench_scan.txt; fi
 for v in "${VARIANTS[@]}"; do
     n=${v%%:*}; a=${v#*:}
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$n -o $n -- python3 $R/bench.py --steps 30 --warmup 5 --no-cpu --no-pmc --no-config3 --no-config4 --no-config5 --no-host-path $a "$@" > $O/$n.json 2> $O/$n.err

@@ -111,5 +111,32 @@ int main() {
         printf("variant %d: %.2f us per launch, %.0f GB/s on %lld MB of meta\n", v, us, n * 4 / us / 1e3, n * 4 >> 20);
     };
     for (int v = 0; v <= 4; v++) run(v);
+    // the same variants with the infinity cache flushed before each launch (1 GiB written in between):
+    // the scan as it runs inside a reserve batch, where other kernels' traffic sits between two scans
+    void *junk;
+    hipMalloc(&junk, 1ll << 30);
+    hipEvent_t c, d;
+    hipEventCreate(&c);
+    hipEventCreate(&d);
+    for (int v = 0; v <= 3; v++) {
+        double tot = 0;
+        for (int rep = 0; rep < 12; rep++) {
+            hipMemsetAsync(junk, rep, 1ll << 30, 0);
+            hipEventRecord(c, 0);
+            switch (v) {
+            case 0: k_page<0><<<npages, 256>>>(meta, npages, gh, csum, spec, specn, sink, 1008); break;
+            case 1: k_page<1><<<npages, 256>>>(meta, npages, gh, csum, spec, specn, sink, 1008); break;
+            case 2: k_page<2><<<npages, 256>>>(meta, npages, gh, csum, spec, specn, sink, 1008); break;
+            case 3: k_page<3><<<npages, 256>>>(meta, npages, gh, csum, spec, specn, sink, 1008); break;
+            }
+            hipEventRecord(d, 0);
+            hipEventSynchronize(d);
+            float ms = 0;
+            hipEventElapsedTime(&ms, c, d);
+            if (rep >= 2) tot += ms;
+        }
+        const double us = tot * 1000.0 / 10;
+        printf("variant %d, cache flushed: %.2f us per launch, %.0f GB/s\n", v, us, n * 4 / us / 1e3);
+    }
     return 0;
 }
