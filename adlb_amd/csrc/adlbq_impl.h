@@ -250,6 +250,13 @@ struct adlbq_server {
     std::vector<int> tnew_vals;
     unsigned long long *d_tnewk = nullptr; int *d_tnewv = nullptr; long long cap_tnew = 0;
     long long tidx_merges = 0, tidx_rebuilds = 0;
+    // delta index (k_targeted_idx reads it beside the main one): the sorted keys of targeted units
+    // Put since the main index was last merged or rebuilt; folded into the main index only when it
+    // would grow past tdel_max ("tindex_delta", 0: every Put batch merges into the main index)
+    unsigned long long *d_dkeys = nullptr, *d_dkeys2 = nullptr;
+    int *d_dvals = nullptr, *d_dvals2 = nullptr; long long cap_del = 0, tdel_n = 0, tdel_max = 1 << 18;
+    int *d_dstart = nullptr, *d_dend = nullptr; long long cap_drange = 0;
+    long long tidx_delta_merges = 0, tidx_folds = 0;
     std::vector<unsigned long long> tnew_sk;  // host staging of the sorted new keys / positions
     std::vector<int> tnew_sv;
     hipEvent_t tnew_ev = nullptr;
@@ -285,6 +292,7 @@ struct adlbq_server {
     int chain_passes = 0;              // round 0's in-launch passes, 0 = auto (adlbq_set_param "chain_passes")
     int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
     int put_match_block = 1, put_always_match = 0;  // diagnostics ("put_match_block", "put_always_match")
+    int hist_ppb = 1;                  // pass-1 pages per workgroup, 1 or 2 (T <= 8) ("hist_ppb")
     int hist_diag = 0;                 // diagnostic ("hist_diag"): parts of pass 1 skipped (wrong results)
     int split_prep = 0;                // diagnostic ("split_prep"): request preparation and pass 1 as two launches
     int rank_in_select = 1;            // k_select_open ranks the candidates when it can ("rank_in_select")

@@ -213,26 +213,19 @@ __device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const
 
 // Every type is counted, demand or not: k_thresholds ignores the columns of a
 // type without demand, and k_rank re-zeroes every chunk sum.
-__device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist /* [C][HK] */) {
-    // per type: the anchor (an int: it bounds live prios, which are ints) and
-    // the guessed cut, rounded down to an int (a looser guess only lists more units)
-    __shared__ int2 sag[ADLBQ_MAX_TYPES];
-    const int *__restrict__ prio = a.prio;
-    const uint32_t *__restrict__ meta = a.meta;
-    const int T = a.T, npages = a.npages, tail_fill = a.tail_fill;
-    const long long *__restrict__ anchor = a.anchor;
-    unsigned short *__restrict__ gh = a.gh;
-    unsigned int *__restrict__ csum = a.csum;
+// The per-type anchor and guessed cut of pass 1, staged in LDS.
+__device__ __forceinline__ void hist_stage_types(const HistArgs &a, int2 *sag) {
+    for (int t = threadIdx.x; t < a.T; t += blockDim.x)
+        sag[t] = make_int2((int)a.anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
+}
+
+// Page p's counts from its loaded quarter (pv, mv): histogram (hist zeroed and
+// sag staged before the barrier the caller ran), speculative lists, per-page
+// row and chunk sums.  Ends with a barrier: hist may be reused afterwards.
+__device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const int4 (&pv)[4], const uint4 (&mv)[4],
+                                           const int2 *sag, unsigned int *__restrict__ hist /* [C][HK] */) {
+    const int T = a.T;
     const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int fill = (p == npages - 1) ? tail_fill : PAGE;
-    int4 pv[4];
-    uint4 mv[4];
-    load_quarter(prio, meta, a.pbase, a.pwide, a.pages[p], fill, w, pv, mv);
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        sag[t] = make_int2((int)anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
-    }
-    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-    __syncthreads();
     unsigned int *my = hist + (lane % HK);
     // units at or above the guessed cut go to this wave's speculative list, in
     // slot order: k_select_open reads the list instead of the page when the
@@ -271,15 +264,47 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
     }
     if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
-    if (a.diag & 2) return;
-    unsigned int *cs = csum + (long long)(p / CHUNK) * C;
-    unsigned short *g = gh + (long long)p * C;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        unsigned int v = 0;
+    if (!(a.diag & 2)) {
+        unsigned int *cs = a.csum + (long long)(p / CHUNK) * C;
+        unsigned short *g = a.gh + (long long)p * C;
+        for (int c = threadIdx.x; c < C; c += blockDim.x) {
+            unsigned int v = 0;
 #pragma unroll
-        for (int k = 0; k < HK; k++) v += hist[c * HK + k];
-        g[c] = (unsigned short)v;
-        if (v) atomicAdd(&cs[c], v);
+            for (int k = 0; k < HK; k++) v += hist[c * HK + k];
+            g[c] = (unsigned short)v;
+            if (v) atomicAdd(&cs[c], v);
+        }
+    }
+    __syncthreads();
+}
+
+// Every type is counted, demand or not: k_thresholds ignores the columns of a
+// type without demand, and k_rank re-zeroes every chunk sum.  PPB pages per
+// workgroup, every page's loads issued before the first is counted.
+template <int PPB>
+__device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsigned int *__restrict__ hist) {
+    __shared__ int2 sag[ADLBQ_MAX_TYPES];
+    const int C = a.T * NB, w = threadIdx.x >> 6;
+    int4 pv[PPB][4];
+    uint4 mv[PPB][4];
+#pragma unroll
+    for (int q = 0; q < PPB; q++) {
+        const int p = p0 + q;
+        if (p < a.npages)
+            load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pages[p], p == a.npages - 1 ? a.tail_fill : PAGE, w,
+                         pv[q], mv[q]);
+    }
+    hist_stage_types(a, sag);
+    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PPB; q++) {
+        if (p0 + q >= a.npages) break;
+        if (q > 0) {
+            for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+            __syncthreads();
+        }
+        hist_count(a, p0 + q, pv[q], mv[q], sag, hist);
     }
 }
 
@@ -287,12 +312,12 @@ __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsign
 // workgroups [0, nprep) prepare 256 requests each, the rest count one page.
 constexpr int PREP_LDS = (int)sizeof(int) * PREP_BLOCK * PREP_ROW;
 
-template <int TB>
+template <int TB, int PPB = 1>
 __global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha) {
     static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
     extern __shared__ unsigned int lds[];
     if ((int)blockIdx.x < nprep) prep_block<TB>(pa, blockIdx.x, reinterpret_cast<int *>(lds));
-    else hist_page(ha, blockIdx.x - nprep, lds);
+    else hist_pages<PPB>(ha, (blockIdx.x - nprep) * PPB, lds);
 }
 
 // The lowest prio in bins 0..th of a type with anchor an (bin_of: exact bins
@@ -915,19 +940,50 @@ __device__ __forceinline__ long long tidx_slot(const int *__restrict__ rpages, i
     return ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
 }
 
+// The delta index: the keys of targeted units Put since the main index was
+// last merged or rebuilt, sorted the same way, with its own group bounds.  A
+// group's entries are the merge of its main and delta ranges; a delta entry
+// of a bucket always lies later in the bucket than its main entries (Puts
+// append), so (inverted prio, bucket position) orders the two alike.
+struct TDelta {
+    const unsigned long long *keys;
+    const int *vals;
+    const int *start, *end;  // [groups] lower bounds, as tstart / tend
+    int n;                   // 0: no delta
+};
+
+// cache / walk key of an index entry: inverted prio << 32 | position in the bucket + 1
+// (never 0: 0 marks an empty cache, ~0 no head)
+__device__ __forceinline__ unsigned long long tidx_ck(unsigned long long k, int L) {
+    return ((k & 0xffffffffull) << 32) | ((unsigned int)L + 1u);
+}
+
+// first index in [lo, hi) of a group whose entry comes after key ck (a walk restart)
+__device__ __forceinline__ int tidx_after(const unsigned long long *__restrict__ keys, const int *__restrict__ vals,
+                                          int lo, int hi, unsigned long long ck) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (tidx_ck(keys[mid], vals[mid]) <= ck) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bucket_ranks,
                                                       const int *__restrict__ pstart, const int *__restrict__ rpages,
                                                       const unsigned long long *__restrict__ tkeys,
                                                       const int *__restrict__ tvals, const int *__restrict__ tstart,
-                                                      const int *__restrict__ tend, int T, const uint32_t *meta,
+                                                      const int *__restrict__ tend, TDelta dl, int T, const uint32_t *meta,
                                                       const unsigned long long *__restrict__ mask,
                                                       const int *__restrict__ reqs, int R, int *tmatch, int *seg_cnt,
                                                       int *tcnt, const int *__restrict__ tlist, int tcap) {
     __shared__ int sreq[TGT_REQ];                   // the batch's Reserves in arrival order
     __shared__ unsigned long long smk[TGT_REQ];     // their type masks
     __shared__ unsigned long long ckey[TGT_CACHE];  // cached heads: inverted prio << 32 | position in the bucket
-    __shared__ int cslot[TGT_CACHE], cgi[TGT_CACHE], cex[TGT_CACHE + 1];
-    __shared__ int dem[64], coff[65], gbase[64], gend[64], ccnt[64];
+    __shared__ int cslot[TGT_CACHE], cex[TGT_CACHE + 1];
+    __shared__ int dem[64], coff[65], cmid[64], gbase[64], gend[64], dbase[64], dend[64], ccnt[64];
+    __shared__ int gnext[64], dnext[64], amain[64];
+    __shared__ unsigned long long cut[64];
     __shared__ int nlist, wcnt[4], wsum[4], s_over;
     const int b = blockIdx.x, r = bucket_ranks[b], p0 = pstart[b];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -935,9 +991,12 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
         if (tid == 0) tcnt[b] = 0;
         return;
     }
+    const bool has_delta = dl.n > 0;
     if (tid < 64) {
         gbase[tid] = tid < T ? tstart[b * 64 + tid] : 0;
         gend[tid] = tid < T ? tend[b * 64 + tid] : 0;
+        dbase[tid] = (tid < T && has_delta) ? dl.start[b * 64 + tid] : 0;
+        dend[tid] = (tid < T && has_delta) ? dl.end[b * 64 + tid] : 0;
     }
     if (tid == 0) {
         const int n = tcnt[b];
@@ -996,23 +1055,36 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
         __syncthreads();
         if (n == 0) break;
         for (int k = tid; k < n; k += blockDim.x) smk[k] = mask[sreq[k]];
-        if (tid < 64) dem[tid] = 0;
+        if (tid < 64) {
+            dem[tid] = 0;
+            cut[tid] = ~0ull;
+            gnext[tid] = 0;
+            dnext[tid] = 0;
+            ccnt[tid] = 0;
+        }
         __syncthreads();
         // ---- per type: the Reserves that can take it (each takes at most one unit)
         for (int k = tid; k < n; k += blockDim.x)
             for (unsigned long long m = smk[k]; m; m &= m - 1) atomicAdd(&dem[__ffsll((long long)m) - 1], 1);
         __syncthreads();
-        // ---- cache regions: twice the demand + 8 per type (less when the cache is short)
+        // ---- cache regions: per type, twice the demand + 8 of the main range, then as many of
+        // the delta range (less when the cache is short)
         if (tid == 0) {
             int tot = 0;
-            for (int t = 0; t < T; t++) tot += min(2 * dem[t] + 8, gend[t] - gbase[t]);
+            for (int t = 0; t < T; t++)
+                tot += min(2 * dem[t] + 8, gend[t] - gbase[t]) + min(2 * dem[t] + 8, dend[t] - dbase[t]);
             const bool big = tot > TGT_CACHE;
             int acc = 0;
             for (int t = 0; t < T; t++) {
-                int want = min(big ? dem[t] : 2 * dem[t] + 8, gend[t] - gbase[t]);
-                want = max(0, min(want, TGT_CACHE - acc));
+                const int wt = big ? dem[t] : 2 * dem[t] + 8;
+                const int wm = max(0, min(min(wt, gend[t] - gbase[t]), TGT_CACHE - acc));
+                const int wd = max(0, min(min(wt, dend[t] - dbase[t]), TGT_CACHE - acc - wm));
                 coff[t] = acc;
-                acc += want;
+                cmid[t] = acc + wm;
+                acc += wm + wd;
+                // a range cut short: the cache is valid only up to its last fetched entry (set
+                // below); cut short with nothing fetched, the cache holds nothing of the type
+                if ((gbase[t] + wm < gend[t] && wm == 0) || (dbase[t] + wd < dend[t] && wd == 0)) cut[t] = 0ull;
             }
             coff[T] = acc;
         }
@@ -1021,12 +1093,14 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
         // ---- fetch: thread tid takes flat entries [tid * TGT_PER, +TGT_PER), three dependent rounds of loads
         unsigned long long kv[TGT_PER];
         long long sl[TGT_PER];
-        int gi[TGT_PER];
-        bool av[TGT_PER];
+        int gi[TGT_PER], ty[TGT_PER];
+        bool av[TGT_PER], dpart[TGT_PER];
 #pragma unroll
         for (int q = 0; q < TGT_PER; q++) {
             const int f = tid * TGT_PER + q;
             gi[q] = -1;
+            ty[q] = 0;
+            dpart[q] = false;
             kv[q] = ~0ull;
             if (f < F) {
                 int lo = 0, hi = T;  // type of flat entry f: coff[t] <= f < coff[t+1]
@@ -1034,15 +1108,27 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                     const int mid = (lo + hi) >> 1;
                     if (coff[mid] <= f) lo = mid; else hi = mid;
                 }
-                gi[q] = gbase[lo] + (f - coff[lo]);
-                kv[q] = tkeys[gi[q]];
+                ty[q] = lo;
+                dpart[q] = f >= cmid[lo];
+                gi[q] = dpart[q] ? dbase[lo] + (f - cmid[lo]) : gbase[lo] + (f - coff[lo]);
+                kv[q] = dpart[q] ? dl.keys[gi[q]] : tkeys[gi[q]];
             }
         }
         int L[TGT_PER];
 #pragma unroll
-        for (int q = 0; q < TGT_PER; q++) L[q] = gi[q] >= 0 ? tvals[gi[q]] : 0;
+        for (int q = 0; q < TGT_PER; q++) L[q] = gi[q] >= 0 ? (dpart[q] ? dl.vals[gi[q]] : tvals[gi[q]]) : 0;
 #pragma unroll
         for (int q = 0; q < TGT_PER; q++) sl[q] = gi[q] >= 0 ? tidx_slot(rpages, p0, L[q]) : 0;
+        // the last fetched entry of a range cut short bounds the cache's valid prefix
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) {
+            const int f = tid * TGT_PER + q;
+            if (gi[q] < 0) continue;
+            const int t = ty[q];
+            const bool last_m = !dpart[q] && f == cmid[t] - 1 && gi[q] + 1 < gend[t];
+            const bool last_d = dpart[q] && f == coff[t + 1] - 1 && gi[q] + 1 < dend[t];
+            if (last_m || last_d) atomicMin(&cut[t], tidx_ck(kv[q], L[q]));
+        }
         int cnt = 0;
 #pragma unroll
         for (int q = 0; q < TGT_PER; q++) {
@@ -1073,51 +1159,89 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
         }
         if (tid == 255) cex[F] = pre;
         __syncthreads();
-        // compacted in order into each type's region
+        // where the walk resumes after the cache: per range, the fetched entries up to the cut
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) {
+            if (gi[q] < 0 || tidx_ck(kv[q], L[q]) > cut[ty[q]]) continue;
+            atomicAdd(dpart[q] ? &dnext[ty[q]] : &gnext[ty[q]], 1);
+        }
+        if (tid < T) amain[tid] = cex[cmid[tid]] - cex[coff[tid]];  // available main entries of the type
+        // the main range's available entries, compacted in order at the region's start ...
+        int at[TGT_PER];
 #pragma unroll
         for (int q = 0; q < TGT_PER; q++) {
             const int f = tid * TGT_PER + q;
+            at[q] = -1;
             if (f < F && av[q]) {
-                int lo = 0, hi = T;
-                while (hi - lo > 1) {
-                    const int mid = (lo + hi) >> 1;
-                    if (coff[mid] <= f) lo = mid; else hi = mid;
-                }
-                const int at = coff[lo] + (cex[f] - cex[coff[lo]]);
-                ckey[at] = ((kv[q] & 0xffffffffull) << 32) | (unsigned int)L[q];
-                cslot[at] = (int)sl[q];
-                cgi[at] = gi[q];
+                const int t = ty[q];
+                at[q] = coff[t] + (cex[f] - cex[coff[t]]);  // main first, then delta (flat order)
+                ckey[at[q]] = tidx_ck(kv[q], L[q]);
             }
         }
-        if (tid < T) ccnt[tid] = cex[coff[tid + 1]] - cex[coff[tid]];
+        __syncthreads();
+        // ... then both runs merged in place: an entry moves up by the entries of the other run before it
+        if (has_delta) {
+#pragma unroll
+            for (int q = 0; q < TGT_PER; q++) {
+                if (at[q] < 0) continue;
+                const int t = ty[q], c0 = coff[t], am = amain[t], ad = cex[coff[t + 1]] - cex[cmid[t]];
+                const unsigned long long k = ckey[at[q]];
+                int lo, hi;
+                if (!dpart[q]) { lo = c0 + am; hi = c0 + am + ad; }  // delta run
+                else { lo = c0; hi = c0 + am; }                      // main run
+                const int base = lo;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (ckey[mid] < k) lo = mid + 1;
+                    else hi = mid;
+                }
+                at[q] = dpart[q] ? at[q] - am + (lo - base) : at[q] + (lo - base);
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int q = 0; q < TGT_PER; q++) {
+            if (at[q] < 0) continue;
+            const unsigned long long k = tidx_ck(kv[q], L[q]);
+            ckey[at[q]] = k;
+            cslot[at[q]] = (int)sl[q];
+            if (k <= cut[ty[q]]) atomicAdd(&ccnt[ty[q]], 1);  // the valid prefix of the merged cache
+        }
         __syncthreads();
         // ---- serve the Reserves in order (wave 0): lane t holds type t's head
         // (and the one after it) in registers; per Reserve a scalar loop over
         // its types compares the heads (readlane), the winner's lane advances
         if (w == 0) {
             const bool tl = lane < T;
-            const int co = tl ? coff[lane] : 0, cn = tl ? ccnt[lane] : 0, ge = tl ? gend[lane] : 0;
-            int hd = 0;                                                     // cached heads consumed
-            int gn = tl ? gbase[lane] + (coff[lane + 1] - coff[lane]) : 0;  // next index past the fetch
-            int pg = -1;  // global index of a head found by the walk (cache dry), -1: from the cache
+            const int co = tl ? coff[lane] : 0, cn = tl ? ccnt[lane] : 0;
+            const int ge = tl ? gend[lane] : 0, de = tl ? dend[lane] : 0;
+            int hd = 0;                                      // cached heads consumed
+            int gn = tl ? gbase[lane] + gnext[lane] : 0;     // main and delta positions past the cache
+            int dn = tl ? dbase[lane] + dnext[lane] : 0;
             unsigned long long hk = ~0ull, nk = ~0ull;  // head key and the next cached one
+            unsigned long long lastk = 0ull;            // key of the type's last unit taken (0: none)
             int hs = -1, ns = -1;
-            auto walk = [&](unsigned long long &k, int &sl) {  // next available unit past the fetch (slow path)
+            auto walk = [&](unsigned long long &k, int &sl) {  // next available unit past the cache (slow path)
                 k = ~0ull;
                 sl = -1;
-                for (; gn < ge; gn++) {
-                    const unsigned long long kk = tkeys[gn];
-                    const int pr = (int)(~(unsigned int)kk ^ 0x80000000u);
+                while (gn < ge || dn < de) {
+                    const unsigned long long km = gn < ge ? tidx_ck(tkeys[gn], tvals[gn]) : ~0ull;
+                    const unsigned long long kd = dn < de ? tidx_ck(dl.keys[dn], dl.vals[dn]) : ~0ull;
+                    const bool fromd = kd < km;
+                    const unsigned long long kk = fromd ? kd : km;
+                    const int pr = (int)(~(unsigned int)(kk >> 32) ^ 0x80000000u);
                     if (pr <= LOWEST) {  // prio descending: nothing after it matches either
-                        gn = ge;
-                        break;
+                        if (fromd) dn = de;
+                        else gn = ge;
+                        continue;
                     }
-                    const int LL = tvals[gn];
+                    const int LL = (int)(unsigned int)kk - 1;
                     const long long ss = tidx_slot(rpages, p0, LL);
+                    if (fromd) dn++;
+                    else gn++;
                     if ((meta[ss] & (M_LIVE | M_PINNED)) == M_LIVE) {
-                        k = ((kk & 0xffffffffull) << 32) | (unsigned int)LL;
+                        k = kk;
                         sl = (int)ss;
-                        pg = gn++;
                         break;
                     }
                 }
@@ -1133,7 +1257,7 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                 for (int kk = 0; kk < kn; kk++) {
                     const unsigned long long m = readlane64(mv, kk);
                     // a type whose cache ran dry walks before it competes (uniform loop over such types)
-                    const unsigned long long dry = __ballot(tl && hk == ~0ull && hd >= cn && gn < ge) & m;
+                    const unsigned long long dry = __ballot(tl && hk == ~0ull && hd >= cn && (gn < ge || dn < de)) & m;
                     if (dry && ((dry >> lane) & 1ull)) walk(hk, hs);
                     unsigned long long best = ~0ull;
                     int bt = -1;
@@ -1152,8 +1276,8 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                         atomicSub(&seg_cnt[j >> 6], 1);
                     }
                     if (lane == bt) {  // advance: the next cached head, else the walk later
+                        lastk = hk;
                         if (hd < cn) hd++;
-                        if (pg >= 0 && hd >= cn) pg = -1;
                         if (hd < cn) {
                             hk = nk;
                             hs = ns;
@@ -1165,8 +1289,11 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                     }
                 }
             }
-            // the first unconsumed index of each type, for the next batch (overflow only)
-            if (tl) gbase[lane] = (hd >= cn && hk != ~0ull && pg >= 0) ? pg : hd < cn ? cgi[co + hd] : gn;
+            // overflow only: the next Reserves of the rank resume after the last unit taken of each type
+            if (over && tl && lastk != 0ull) {
+                gbase[lane] = tidx_after(tkeys, tvals, gbase[lane], ge, lastk);
+                if (has_delta) dbase[lane] = tidx_after(dl.keys, dl.vals, dbase[lane], de, lastk);
+            }
         }
         __syncthreads();
         if (!over || j0 >= R) break;
@@ -2478,19 +2605,22 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     const bool scan = np > 0 && T > 0;
     const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, h->d_csum,
                       h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0};
-    const int grid = nprep + (scan ? np : 0);
+    const int ppb = (h->hist_ppb == 2 && T <= 8) ? 2 : 1;  // pages per pass-1 workgroup
+    const int npb = (np + ppb - 1) / ppb;
+    const int grid = nprep + (scan ? npb : 0);
     if (grid > 0) {
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0, scan ? sizeof(unsigned int) * HK * C : 0);
         stage_begin(h, "hist", &ev);
-        auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
+        auto kph = ppb == 2 ? (T <= 4 ? k_prep_hist<4, 2> : k_prep_hist<8, 2>)
+                            : T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
         if (h->hist_diag && scan) {  // diagnostic: an extra pass 1 (no epilogue) with parts skipped, before the real one
             HistArgs hd = ha;
             hd.diag = h->hist_diag | 2;
-            kph<<<np, 256, lds, s>>>(pa, 0, hd);
+            kph<<<npb, 256, lds, s>>>(pa, 0, hd);
         }
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
             kph<<<nprep, 256, lds, s>>>(pa, nprep, ha);
-            kph<<<np, 256, lds, s>>>(pa, 0, ha);
+            kph<<<npb, 256, lds, s>>>(pa, 0, ha);
         } else {
             kph<<<grid, 256, lds, s>>>(pa, nprep, ha);
         }
@@ -2567,8 +2697,9 @@ static int ensure_tindex(adlbq_server *h) {
     }
     const long long m = (long long)h->tnew_keys.size();
     // incremental: the new units' keys (sorted on the host, ties kept in Put order) merged into the
-    // sorted index -- old entries first on equal keys, as their bucket positions are lower
-    if (h->tidx_valid && m > 0 && h->tidx_n + m <= h->cap_tidx && m * 4 <= h->tidx_n + 4096) {
+    // delta index, or into the sorted main index -- old entries first on equal keys, as their
+    // bucket positions are lower
+    if (h->tidx_valid && m > 0 && h->tidx_n + h->tdel_n + m <= h->cap_tidx && m * 4 <= h->tidx_n + 4096) {
         if (m > h->cap_tnew) {
             AQ_HIP(hipStreamSynchronize(s));
             if (h->d_tnewk) AQ_HIP(hipFree(h->d_tnewk));
@@ -2593,35 +2724,98 @@ static int ensure_tindex(adlbq_server *h) {
         AQ_HIP(hipMemcpyAsync(h->d_tnewk, h->tnew_sk.data(), sizeof(unsigned long long) * m, hipMemcpyHostToDevice, s));
         AQ_HIP(hipMemcpyAsync(h->d_tnewv, h->tnew_sv.data(), sizeof(int) * m, hipMemcpyHostToDevice, s));
         AQ_HIP(hipEventRecord(h->tnew_ev, s));
-        size_t tmp = 0;
-        AQ_HIP(rocprim::merge(nullptr, tmp, h->d_tkeys, h->d_tnewk, h->d_tkeys2, h->d_tvals, h->d_tnewv, h->d_tvals2,
-                              (size_t)h->tidx_n, (size_t)m, rocprim::less<unsigned long long>(), s));
-        if (tmp > h->cap_tsort) {
-            AQ_HIP(hipStreamSynchronize(s));
-            if (h->d_tsort) AQ_HIP(hipFree(h->d_tsort));
-            h->cap_tsort = std::max(tmp, 2 * h->cap_tsort);
-            AQ_HIP(hipMalloc(&h->d_tsort, h->cap_tsort));
+        h->tnew_keys.clear();
+        h->tnew_vals.clear();
+        const int G = nb * 64;
+        int rc;
+        // sorted runs a, b merged into (ok, ov) (rocprim, stable: a's entries first on equal keys)
+        auto merge_into = [&](const unsigned long long *ak, const int *av, long long na, const unsigned long long *bk,
+                              const int *bv, long long nbk, unsigned long long *ok, int *ov) -> int {
+            size_t tmp = 0;
+            AQ_HIP(rocprim::merge(nullptr, tmp, ak, bk, ok, av, bv, ov, (size_t)na, (size_t)nbk,
+                                  rocprim::less<unsigned long long>(), s));
+            if (tmp > h->cap_tsort) {
+                AQ_HIP(hipStreamSynchronize(s));
+                if (h->d_tsort) AQ_HIP(hipFree(h->d_tsort));
+                h->cap_tsort = std::max(tmp, 2 * h->cap_tsort);
+                AQ_HIP(hipMalloc(&h->d_tsort, h->cap_tsort));
+            }
+            size_t t2 = h->cap_tsort;
+            AQ_HIP(rocprim::merge(h->d_tsort, t2, ak, bk, ok, av, bv, ov, (size_t)na, (size_t)nbk,
+                                  rocprim::less<unsigned long long>(), s));
+            return ADLBQ_OK;
+        };
+        // the main index's bounds after m2 sorted keys (nk) joined it (m2 = 0: new groups only)
+        auto shift_main = [&](const unsigned long long *nk, long long m2, long long n_old) -> int {
+            if (h->tidx_groups > 0 && h->tidx_groups <= (long long)G) {
+                k_tindex_shift<<<(G + 255) / 256, 256, 0, s>>>(nk, (int)m2, (int)h->tidx_groups, (int)n_old, G,
+                                                              h->d_tstart, h->d_tend);
+                AQ_HIP(hipGetLastError());
+                h->tidx_groups = G;
+                return ADLBQ_OK;
+            }
+            return tindex_ranges(h, nb);
+        };
+        if (h->tdel_max > 0 && h->tdel_n + m <= h->tdel_max && (h->tdel_n == 0 || h->tdel_max <= h->cap_del)) {
+            // into the delta index (the main index stays where it is: no 8M-entry move per Put batch)
+            if (h->tdel_max > h->cap_del || (long long)G > h->cap_drange) {
+                AQ_HIP(hipStreamSynchronize(s));
+                if (h->tdel_max > h->cap_del) {
+                    void *ps[] = {h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2};
+                    for (void *p : ps)
+                        if (p) AQ_HIP(hipFree(p));
+                    h->cap_del = h->tdel_max;
+                    AQ_HIP(hipMalloc((void **)&h->d_dkeys, sizeof(unsigned long long) * h->cap_del));
+                    AQ_HIP(hipMalloc((void **)&h->d_dkeys2, sizeof(unsigned long long) * h->cap_del));
+                    AQ_HIP(hipMalloc((void **)&h->d_dvals, sizeof(int) * h->cap_del));
+                    AQ_HIP(hipMalloc((void **)&h->d_dvals2, sizeof(int) * h->cap_del));
+                }
+                if ((long long)G > h->cap_drange) {
+                    if (h->d_dstart) AQ_HIP(hipFree(h->d_dstart));
+                    if (h->d_dend) AQ_HIP(hipFree(h->d_dend));
+                    h->cap_drange = std::max((long long)G, 2 * h->cap_drange);
+                    AQ_HIP(hipMalloc((void **)&h->d_dstart, sizeof(int) * h->cap_drange));
+                    AQ_HIP(hipMalloc((void **)&h->d_dend, sizeof(int) * h->cap_drange));
+                }
+            }
+            if (h->tdel_n == 0) {
+                AQ_HIP(hipMemcpyAsync(h->d_dkeys, h->d_tnewk, sizeof(unsigned long long) * m, hipMemcpyDeviceToDevice, s));
+                AQ_HIP(hipMemcpyAsync(h->d_dvals, h->d_tnewv, sizeof(int) * m, hipMemcpyDeviceToDevice, s));
+            } else {
+                if ((rc = merge_into(h->d_dkeys, h->d_dvals, h->tdel_n, h->d_tnewk, h->d_tnewv, m, h->d_dkeys2,
+                                     h->d_dvals2)))
+                    return rc;
+                std::swap(h->d_dkeys, h->d_dkeys2);
+                std::swap(h->d_dvals, h->d_dvals2);
+            }
+            h->tdel_n += m;
+            if (h->tidx_groups != (long long)G && (rc = shift_main(h->d_tnewk, 0, h->tidx_n))) return rc;  // new buckets
+            k_tindex_bounds<<<(G + 255) / 256, 256, 0, s>>>(h->d_dkeys, (int)h->tdel_n, G, h->d_dstart, h->d_dend);
+            AQ_HIP(hipGetLastError());
+            h->tidx_delta_merges++;
+            h->tindex_dirty = false;
+            return ADLBQ_OK;
         }
-        size_t t2 = h->cap_tsort;
-        AQ_HIP(rocprim::merge(h->d_tsort, t2, h->d_tkeys, h->d_tnewk, h->d_tkeys2, h->d_tvals, h->d_tnewv,
-                              h->d_tvals2, (size_t)h->tidx_n, (size_t)m, rocprim::less<unsigned long long>(), s));
+        if (h->tdel_n > 0) {  // fold the delta into the main index first
+            if ((rc = merge_into(h->d_tkeys, h->d_tvals, h->tidx_n, h->d_dkeys, h->d_dvals, h->tdel_n, h->d_tkeys2,
+                                 h->d_tvals2)))
+                return rc;
+            std::swap(h->d_tkeys, h->d_tkeys2);
+            std::swap(h->d_tvals, h->d_tvals2);
+            const long long n_old = h->tidx_n;
+            h->tidx_n += h->tdel_n;
+            if ((rc = shift_main(h->d_dkeys, h->tdel_n, n_old))) return rc;
+            h->tdel_n = 0;
+            h->tidx_folds++;
+        }
+        if ((rc = merge_into(h->d_tkeys, h->d_tvals, h->tidx_n, h->d_tnewk, h->d_tnewv, m, h->d_tkeys2, h->d_tvals2)))
+            return rc;
         std::swap(h->d_tkeys, h->d_tkeys2);
         std::swap(h->d_tvals, h->d_tvals2);
         const long long n_old = h->tidx_n;
         h->tidx_n += m;
         h->tidx_merges++;
-        h->tnew_keys.clear();
-        h->tnew_vals.clear();
-        int rc;
-        if (h->tidx_groups > 0 && h->tidx_groups <= (long long)nb * 64) {  // shift the bounds
-            const int G = nb * 64;
-            k_tindex_shift<<<(G + 255) / 256, 256, 0, s>>>(h->d_tnewk, (int)m, (int)h->tidx_groups, (int)n_old, G,
-                                                          h->d_tstart, h->d_tend);
-            AQ_HIP(hipGetLastError());
-            h->tidx_groups = G;
-        } else if ((rc = tindex_ranges(h, nb))) {
-            return rc;
-        }
+        if ((rc = shift_main(h->d_tnewk, m, n_old))) return rc;
         h->tindex_dirty = false;
         return ADLBQ_OK;
     }
@@ -2650,6 +2844,7 @@ static int ensure_tindex(adlbq_server *h) {
         }
     }
     h->tidx_n = filled;  // the holes sorted past the filled slots
+    h->tdel_n = 0;       // every targeted unit is in the main index again
     h->tidx_valid = true;
     h->tidx_rebuilds++;
     h->tnew_keys.clear();
@@ -3347,7 +3542,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_begin(h, "targeted", &ev);
         if (nb < (1 << 20))
             k_targeted_idx<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_tkeys,
-                                              h->d_tvals, h->d_tstart, h->d_tend, T, h->d_meta, h->d_mask, d_reqs, R,
+                                              h->d_tvals, h->d_tstart, h->d_tend,
+                                              TDelta{h->d_dkeys, h->d_dvals, h->d_dstart, h->d_dend, (int)h->tdel_n},
+                                              T, h->d_meta, h->d_mask, d_reqs, R,
                                               h->d_tmatch, h->d_seg_cnt, h->d_tcnt, h->d_tlist, h->tcap);
         else
             k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,

@@ -1298,7 +1298,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv, h->d_rtype, h->d_pm_over,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
                     h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
-                    h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc};
+                    h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
+                    h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -2071,6 +2072,15 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->profile_every = (int)std::max(1ll, value);
         return ADLBQ_OK;
     }
+    if (n == "tindex_delta") {  // delta index capacity (0: merge every Put batch into the main index)
+        if (value < 0 || value > (1ll << 26)) return fail(ADLBQ_ERR_ARG, "adlbq_set_param: tindex_delta");
+        h->tdel_max = value;
+        return ADLBQ_OK;
+    }
+    if (n == "hist_ppb") {
+        h->hist_ppb = value == 2 ? 2 : 1;
+        return ADLBQ_OK;
+    }
     if (n == "hist_diag") {
         h->hist_diag = (int)value;
         return ADLBQ_OK;
@@ -2203,6 +2213,8 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n == "spec_lists") return h->ctr.spec_page0;
     if (n == "rank_fast") return h->ctr.rank_fast;
     if (n == "tindex_merges") return h->tidx_merges;   // targeted index: incremental merges
+    if (n == "tindex_delta_merges") return h->tidx_delta_merges;  // Put batches merged into the delta index
+    if (n == "tindex_folds") return h->tidx_folds;      // delta folded into the main index
     if (n == "tindex_rebuilds") return h->tidx_rebuilds;  // and full rebuilds
     if (n == "candidates") {
         int v = 0;

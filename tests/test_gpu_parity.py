@@ -349,11 +349,14 @@ def test_put_side_fifo_vs_oracle(gpu_available, n_parked):
     assert_same(run_abi(ut, cfg, trace, max_units=1 << 14), run_oracle(ut, cfg, trace))
 
 
-def test_targeted_index_incremental_vs_oracle(gpu_available):
+@pytest.mark.parametrize("delta", [None, 0, 3000])
+def test_targeted_index_incremental_vs_oracle(gpu_available, delta):
     """Targeted Puts between Reserve batches (config-4 shape at reduced size):
-    the targeted index takes each batch's new units by a merge into its sorted
-    entries (no full rebuild after the first), and every batch equals the
-    oracle's sequential wq_find_pre_targeted_hi_prio / wq_find_hi_prio."""
+    the targeted index takes each batch's new units into a sorted delta index
+    read beside the main one (delta=None: the default capacity; 3000: folded
+    into the main index when full; 0: merged into the main index every time),
+    no full rebuild after the first, and every batch equals the oracle's
+    sequential wq_find_pre_targeted_hi_prio / wq_find_hi_prio."""
     w = synth.config4(n_units=40_000, n_reserves=4096, seed=91)
     cfg = (w.num_app_ranks, 1, 0)
     rng = np.random.default_rng(91)
@@ -370,10 +373,56 @@ def test_targeted_index_incremental_vs_oracle(gpu_available):
         parts.append(synth.simple_events(synth.OP_INFO))
     trace = np.concatenate(parts)
     with Server(w.user_types, *cfg, max_units=w.n_units) as s:
+        if delta is not None:
+            s.set_param("tindex_delta", delta)
         got = replay.replay(s, trace)
         merges, rebuilds = s.stat("tindex_merges"), s.stat("tindex_rebuilds")
+        dmerges, folds = s.stat("tindex_delta_merges"), s.stat("tindex_folds")
     assert_same(got, run_oracle(w.user_types, cfg, trace))
-    assert rebuilds <= 2 and merges >= 2, (merges, rebuilds)
+    assert rebuilds <= 2 and merges + dmerges >= 2, (merges, dmerges, rebuilds)
+    if delta == 0:
+        assert dmerges == 0
+    if delta == 3000:
+        assert folds >= 1 and dmerges >= 1, (folds, dmerges)
+
+
+@pytest.mark.parametrize("delta", [None, 0])
+def test_targeted_index_delta_overflow_vs_oracle(gpu_available, delta):
+    """One rank sends more Reserves in a batch than a targeted workgroup takes
+    at once (TGT_REQ = 1024): its later Reserves resume after the last unit
+    each type gave, across the main and the delta index alike."""
+    rng = np.random.default_rng(17)
+    ut = np.array([4, 9, 13], np.int32)
+    A = 8
+    n0, n1 = 6000, 1500
+    def units(n, seed):
+        r = np.random.default_rng(seed)
+        tgt = np.where(r.random(n) < 0.9, r.integers(0, A, n), -1)
+        return np.stack([ut[r.integers(0, 3, n)], r.integers(0, 200, n), r.integers(0, A, n), tgt,
+                         np.ones(n), np.full(n, -1), np.zeros(n), np.full(n, -1), np.full(n, -1)],
+                        axis=1).astype(np.int32)
+    u0, u1 = units(n0, 3), units(n1, 4)
+    R = 3000
+    reqs = np.full((R, 18), -2, np.int32)
+    reqs[:, 0] = np.where(rng.random(R) < 0.8, 2, rng.integers(0, A, R))  # rank 2: ~2400 Reserves
+    reqs[:, 1] = 0
+    k = rng.integers(1, 3, R)
+    for j in range(R):
+        reqs[j, 2:2 + k[j]] = rng.choice(ut, k[j], replace=False)
+    def put_units(u):  # OP_PUT events of unit rows (type, prio, answer, target, len, 4 common fields)
+        ev = np.empty((u.shape[0], 10), np.int32)
+        ev[:, 0] = synth.OP_PUT
+        ev[:, 1:] = u
+        return ev.ravel()
+    trace = np.concatenate([put_units(u0), synth.reserve_events(reqs[:500, 0], reqs[:500, 2:], reqs[:500, 1]),
+                            put_units(u1),
+                            synth.reserve_events(reqs[500:, 0], reqs[500:, 2:], reqs[500:, 1])])
+    cfg = (A, 1, 0)
+    with Server(ut, *cfg, max_units=n0 + n1) as s:
+        if delta is not None:
+            s.set_param("tindex_delta", delta)
+        got = replay.replay(s, trace)
+    assert_same(got, run_oracle(ut, cfg, trace))
 
 
 def test_put_batch_device_matches_host_variant(gpu_available):

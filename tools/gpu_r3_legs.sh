@@ -13,6 +13,8 @@ cd /tmp
 for leg in "$@"; do
     case $leg in
         c3) args="--config3-only --no-pmc --no-cpu" ;;
+        c3t) args="--config3-only --no-pmc --no-cpu --c3-threads 1" ;;
+        c3p) args="--config3-only --no-pmc --no-cpu --c3-parts" ;;
         c4) args="--config4-only --no-pmc --no-cpu" ;;
         c5) args="--config5-only --no-pmc --no-cpu" ;;
     esac
