@@ -1383,13 +1383,79 @@ struct RankSort {
     int fail_test;  // adlbq_set_param("sort_fail_test"): count one timed-out wait (tests the error path)
 };
 
+// The chain's round-0 start guesses, one per segment (T <= 8, ranks from
+// k_select_open): the level state after J untargeted choices, J = requests
+// before the segment's first (warm-up) request that can take an untargeted
+// unit -- what k_chain0 would otherwise find itself with three dependent
+// loads.  Block 0 of k_rank, and only when no request's count was adjusted in
+// this launch (every type has candidates); sg[0] = epoch marks them valid.
+struct SegGuess {
+    int *sg;            // [1 + nseg * T]
+    int nseg, warm;
+    unsigned int epoch;
+};
+
+__device__ void seg_guesses(const SegGuess &g, int T, const int *soff, const int *slen, const int *seg_cnt, int R,
+                            const LevelRows &lr, int *pre /* LDS scratch */, int cap) {
+    const int tid = threadIdx.x, nq = (R + 63) / 64;
+    bool ok = lr.lv != nullptr && T <= 8 && nq + 1 <= cap;
+    for (int t = 0; t < T && ok; t++) ok = slen[t] > 0;  // else k_rank drops requests from seg_cnt
+    if (!ok) {
+        if (tid == 0) g.sg[0] = 0;
+        return;
+    }
+    // exclusive prefix of seg_cnt: thread tid sums a contiguous run, then a block scan of the runs
+    __shared__ int wtot[RANK_TILE / 64];
+    const int per = (nq + blockDim.x - 1) / blockDim.x, q0 = tid * per;
+    int run = 0;
+    for (int q = q0; q < min(nq, q0 + per); q++) run += seg_cnt[q];
+    int x = run;
+    const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
+    __syncthreads();
+    int acc = x - run;
+    for (int q = 0; q < w; q++) acc += wtot[q];
+    for (int q = q0; q < min(nq, q0 + per); q++) {
+        pre[q] = acc;
+        acc += seg_cnt[q];
+    }
+    if (q0 < nq && q0 + per >= nq) pre[nq] = acc;  // the thread whose run ends the array
+    __syncthreads();
+    const int G = soff[T];
+    for (int s = tid; s < g.nseg; s += blockDim.x) {
+        const int jb = max(0, s * SEG - g.warm);
+        const int J = pre[min(jb >> 6, nq)];
+        const int Js = J & ~(LV_STEP - 1);
+        int extra[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (J > 0 && J < G)
+            for (int r = Js; r < J; r++) {
+                const int tt = lr.rtype[r];
+#pragma unroll
+                for (int u = 0; u < 8; u++) extra[u] += tt == u;
+            }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            if (u >= T) break;
+            const int gs = J == 0 ? 0 : J >= G ? slen[u] : min(slen[u], (Js ? lr.lv[(long long)(Js / LV_STEP) * T + u] : 0) + extra[u]);
+            g.sg[1 + s * T + u] = gs;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) g.sg[0] = (int)g.epoch;
+}
+
 __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict__ candoff,
                                                     const int *__restrict__ candlen,
                                                     unsigned long long *ckey,  // sorted in this launch: not restrict
                                                     unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
                                                     long long ncsum, const unsigned long long *__restrict__ mask,
                                                     const int *__restrict__ tmatch, int R, int *seg_cnt, RankSort rs,
-                                                    LevelRows lr, const DevCounters *ctr) {
+                                                    LevelRows lr, const DevCounters *ctr, SegGuess sgv) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
     __shared__ unsigned long long span[4][RANK_SPAN];  // also the sort's LDS blocks
     static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * SORT_BLK,
@@ -1486,7 +1552,13 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         stile[T] = acc;
     }
     __syncthreads();
-    if (ctr->rank_fast) return;  // k_select_open ranked the candidates and wrote the level rows
+    if (ctr->rank_fast) {  // k_select_open ranked the candidates and wrote the level rows
+        if (blockIdx.x == 0 && sgv.sg != nullptr)
+            seg_guesses(sgv, T, soff, slen, seg_cnt, R, lr, reinterpret_cast<int *>(&span[0][0]),
+                        (int)(sizeof(span) / sizeof(int)));
+        return;
+    }
+    if (blockIdx.x == 0 && sgv.sg != nullptr && tid == 0) sgv.sg[0] = 0;  // the chain computes its own
     for (int tile = blockIdx.x; tile < stile[T]; tile += gridDim.x) {
         int t = 0;
         while (t + 1 < T && stile[t + 1] <= tile) t++;
@@ -1610,6 +1682,8 @@ struct ChainArgs {
     const int *lv;                   // [R][T] k_rank's level rows (T <= 8), else nullptr
     const unsigned char *rtype;      // [R] type index of the candidate at each global rank (with lv)
     unsigned long long *stamps;      // [nseg][8] s_memrealtime per phase (diagnostic build of the run), or nullptr
+    const int *sg;                   // k_rank's start guesses (SegGuess), valid when sg[0] == sg_epoch; or nullptr
+    unsigned int sg_epoch;
 };
 
 // diagnostic phase stamps (100 MHz constant clock), lane 0 of a segment
@@ -2145,8 +2219,11 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
     }
     // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
     const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
+    // k_rank's guess for this segment, when it made them (one load instead of the three dependent ones below)
+    const bool sg_ok = a.sg != nullptr && a.lv != nullptr && a.sg[0] == (int)a.sg_epoch;
+    const int sg_v = (a.sg != nullptr && lane < T) ? a.sg[1 + s * T + lane] : 0;
     int J = 0;  // requests before jb that take an untargeted unit
-    {
+    if (!sg_ok) {
         const int nq = jb >> 6;
         int cv[16];
 #pragma unroll
@@ -2158,7 +2235,9 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
     int guess;
-    if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
+    if (sg_ok) {
+        guess = sg_v;
+    } else if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
         const int G = __builtin_amdgcn_readlane(my_off, T);
         // the row at the sampled rank below J, the rest spread in proportion to the list lengths
         const int Js = J & ~(LV_STEP - 1);
@@ -2549,6 +2628,9 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMemsetAsync(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 1), h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_lv, sizeof(int) * 8 * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_rtype, (size_t)nc + 64));
+    if (h->d_sg) AQ_HIP(hipFree(h->d_sg));
+    AQ_HIP(hipMalloc((void **)&h->d_sg, sizeof(int) * (1 + 8 * nseg)));
+    AQ_HIP(hipMemsetAsync(h->d_sg, 0, sizeof(int), h->stream));
     h->cap_req = nc;
     return ADLBQ_OK;
 }
@@ -3566,9 +3648,12 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                           h->sort_fail_test};
         // a small grid when the last landed batch was ranked in k_select_open
         // (every loop is grid-strided: any grid is correct, the hint only sizes it)
+        const int warm0 = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
+        const SegGuess sgv{(T <= 8 && h->seg_guess) ? h->d_sg : nullptr, (R + SEG - 1) / SEG, warm0, h->rank_epoch};
         k_rank<<<rank_hint(h) ? 64 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
                                     (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
-                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr);
+                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr,
+                                    sgv);
         stage_end(h, "rank", ev);
     }
     stage_begin(h, "chain", &ev);
@@ -3589,7 +3674,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, warm, gs, h->d_candoff, h->d_candlen, h->d_crank,
                      h->d_umatch, h->d_cht, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chS + nsT, h->d_chD + nsT,
                      h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_chcnt, h->d_ctr,
-                     (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr};
+                     (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr,
+                     (T <= 8 && np > 0 && h->seg_guess) ? h->d_sg : nullptr, h->rank_epoch};
         if (h->chain_stamps) {
             if (nseg > h->cap_stamps) {
                 AQ_HIP(hipStreamSynchronize(s));

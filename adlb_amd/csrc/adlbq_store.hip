@@ -1299,7 +1299,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
                     h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
-                    h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend};
+                    h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -2070,6 +2070,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     }
     if (n == "profile_every") {
         h->profile_every = (int)std::max(1ll, value);
+        return ADLBQ_OK;
+    }
+    if (n == "seg_guess") {
+        h->seg_guess = value ? 1 : 0;
         return ADLBQ_OK;
     }
     if (n == "tindex_delta") {  // delta index capacity (0: merge every Put batch into the main index)

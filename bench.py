@@ -104,6 +104,8 @@ def parse():
     ap.add_argument("--chain-modes", type=int, default=None, help="metric leg: adlbq 'chain_modes'")
     ap.add_argument("--rank-in-select", type=int, default=None, help="metric leg: adlbq 'rank_in_select'")
     ap.add_argument("--chain-warm", type=int, default=None, help="metric leg: adlbq 'chain_warm' (0, 256, 512)")
+    ap.add_argument("--c4-param", action="append", default=[], metavar="NAME=V",
+                    help="config-4 leg: any adlbq_set_param (diagnostics), repeatable")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
                     help="metric leg: any adlbq_set_param (diagnostics), repeatable")
     ap.add_argument("--c4-chain-stats", action="store_true",
@@ -599,6 +601,9 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         srv.set_param("chain_modes", args.c4_chain_modes)
     if args.c4_chain_rounds is not None:
         srv.set_param("chain_rounds", args.c4_chain_rounds)
+    for kv in args.c4_param:
+        k_, v_ = kv.split("=", 1)
+        srv.set_param(k_, int(v_))
     if args.c4_segsort_async is not None:
         srv.set_param("segsort_async", args.c4_segsort_async)
     if args.c4_segsort_wide is not None:

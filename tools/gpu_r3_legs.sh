@@ -16,6 +16,7 @@ for leg in "$@"; do
         c3t) args="--config3-only --no-pmc --no-cpu --c3-threads 1" ;;
         c3p) args="--config3-only --no-pmc --no-cpu --c3-parts" ;;
         c4) args="--config4-only --no-pmc --no-cpu" ;;
+        c4nd) args="--config4-only --no-pmc --no-cpu --c4-param tindex_delta=0" ;;
         c5) args="--config5-only --no-pmc --no-cpu" ;;
     esac
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$leg -o $leg -- python3 $R/bench.py $args > $O/$leg.json 2> $O/$leg.err
