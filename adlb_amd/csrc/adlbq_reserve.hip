@@ -2344,6 +2344,103 @@ __global__ __launch_bounds__(64) void k_chainr(ChainArgs a, int round, int final
 // last appends them to rq in arrival order and chooses their RFR donors
 // (1238-1310).  Response words [10], [11] of a parked request are written only
 // by that last workgroup, so no two workgroups store the same bytes.
+// The RFR donors of a batch's parked Reserves (wave 0 of k_finalize's last
+// workgroup), in FIFO order: the same choices as rfr_select per Reserve
+// (adlb.c:1280-1308, 3487-3534), with the donor state held by the wave
+// instead of re-read from memory per Reserve -- lane i holds server i's qlen,
+// RFR-outstanding flag and maximum prio over types, its qmstat row sits in
+// LDS, and the tq in LDS; 64 Reserves at a time have their rank's current
+// rfr_to_rank and their type vector in registers.  Returns the first FIFO
+// position left without a donor check (every later one has none).
+constexpr int DONOR_TQ_LDS = 256;  // tq entries the fast path stages
+__device__ int park_donors_fast(const DonorCtx &c, const int *__restrict__ reqs, const int *rq_req, int n0, int np,
+                                int *resp, int *s_hi, int *s_tq) {
+    const int lane = threadIdx.x & 63, S = c.S, T = c.T;
+    for (int q = lane; q < S * T; q += 64) s_hi[q] = c.qm_hi[q];
+    for (int q = lane; q < 4 * c.n_tq; q += 64) s_tq[q] = c.tq[q];
+    const int ut = lane < T ? c.utypes[lane] : INT_MIN;
+    const int srv = c.master + lane;
+    const bool mine = lane < S;
+    int qlen = mine ? c.qm_qlen[lane] : 0;
+    int rfo = (mine && srv < c.num_world) ? ld_agent(c.rfr_out + srv) : 1;
+    __builtin_amdgcn_wave_barrier();
+    int rowmax = LOWEST;
+    if (mine)
+        for (int t = 0; t < T; t++) rowmax = max(rowmax, s_hi[lane * T + t]);
+    const bool self = srv == c.my_world;
+    auto eligible = [&]() { return mine && !self && !rfo && qlen > 0; };
+    auto any_open = [&]() { return c.n_tq > 0 || __ballot(eligible() && rowmax > LOWEST) != 0ull; };
+    // find_cand from the staged state (wave-uniform): tq first, then the argmax over servers
+    auto cand_of = [&](int rank, int wt) -> int {
+        for (int base = 0; base < c.n_tq; base += 64) {
+            const int k = base + lane;
+            bool hit = false;
+            int sv = -1;
+            if (k < c.n_tq) {
+                hit = s_tq[4 * k] == rank && (wt == -1 || wt == s_tq[4 * k + 1]);
+                sv = s_tq[4 * k + 2];
+            }
+            const unsigned long long b = __ballot(hit);
+            if (b) return __shfl(sv, __ffsll((long long)b) - 1, 64);
+        }
+        int ti = -1;
+        if (wt >= 0) {
+            const unsigned long long b = __ballot(lane < T && ut == wt);
+            if (!b) return -1;  // undeclared type
+            ti = __ffsll((long long)b) - 1;
+        }
+        unsigned long long key = 0;
+        if (eligible()) {
+            const int v = wt < 0 ? rowmax : s_hi[lane * T + ti];
+            if (v > LOWEST)
+                key = ((unsigned long long)((unsigned int)v ^ 0x80000000u) << 32) | (0xffffffffull - (unsigned int)lane);
+        }
+        key = wave_max_u64(key);
+        return key ? c.master + (int)(0xffffffffu - (unsigned int)(key & 0xffffffffu)) : -1;
+    };
+    int k = n0;
+    bool open = any_open();
+    for (int k0 = n0; k0 < n0 + np && open; k0 += 64) {
+        // the next 64 parked Reserves: request index, rank, its rfr_to_rank, type vector
+        __builtin_amdgcn_s_waitcnt(0);  // the last batch's rfr stores have reached L2 before these loads
+        const int kk = k0 + lane;
+        const bool in = kk < n0 + np;
+        const int j = in ? rq_req[kk] : 0;
+        const int *rr = reqs + (long long)ADLBQ_RESERVE_INTS * j;
+        const int rank = in ? rr[0] : -1;
+        int tv[NREQ];
+#pragma unroll
+        for (int e = 0; e < NREQ; e++) tv[e] = in ? rr[2 + e] : -2;
+        int rtr = (in && rank >= 0 && rank < c.A) ? ld_agent(c.rfr_to_rank + rank) : 0;
+        const int kn = min(64, n0 + np - k0);
+        for (int i = 0; i < kn && open; i++, k++) {
+            const int rk = __builtin_amdgcn_readlane(rank, i), jj = __builtin_amdgcn_readlane(j, i);
+            int cand = -1;
+            if (rk >= 0 && rk < c.A && __builtin_amdgcn_readlane(rtr, i) < 0) {
+#pragma unroll
+                for (int e = 0; e < NREQ; e++) {
+                    const int wt = __builtin_amdgcn_readlane(tv[e], i);
+                    if (wt < -1) break;
+                    cand = cand_of(rk, wt);
+                    if (cand >= 0) break;
+                }
+                if (cand >= 0) {  // rfr_to_rank[rank] = cand, rfr_out[cand] = 1 (adlb.c:1300-1304)
+                    if (lane == 0) {
+                        st_agent(c.rfr_to_rank + rk, cand);
+                        if (cand < c.num_world) st_agent(c.rfr_out + cand, 1);
+                    }
+                    if (mine && srv == cand) rfo = 1;
+                    if (rank == rk) rtr = cand;  // this rank's later Reserves see the RFR outstanding
+                }
+            }
+            if (lane == 0) resp[(long long)ADLBQ_RESP_INTS * jj + 11] = cand;
+            if (cand >= 0 && c.n_tq == 0) open = any_open();
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    return k;
+}
+
 __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__ reqs, int R,
                           const unsigned long long *pmask, int *rq_rank, int *rq_types, int *rq_live, int *rq_req,
                           int *rq_seq, DevCounters *ctr, int *resp) {
@@ -2402,7 +2499,11 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     // the RFR donors in FIFO order (rfr_out / rfr_to_rank chain them); once no
     // server can be a donor any more (each RFR sets rfr_out), the rest get -1
     // in parallel
-    if (w == 0) {
+    __shared__ int s_hi[ADLBQ_MAX_TYPES * 64], s_tq[4 * DONOR_TQ_LDS];
+    if (w == 0 && donors && c.S <= 64 && c.n_tq <= DONOR_TQ_LDS) {
+        const int k = park_donors_fast(c, reqs, rq_req, n0, np, resp, s_hi, s_tq);
+        if (lane == 0) s_stop = k;
+    } else if (w == 0) {
         bool open = donors && (c.n_tq > 0 || any_donor(c));
         int k = n0;
         for (; k < n0 + np && open; k++) {
