@@ -223,7 +223,9 @@ struct adlbq_server {
     unsigned int rank_epoch = 0;       // per reserve batch, never 0 once used
     unsigned short *d_gh = nullptr; long long cap_gh = 0;   // [open pages][T*NB]
     unsigned int *d_spec = nullptr; int *d_specn = nullptr; long long cap_spec = 0;  // [open pages][4][SPEC_CAP], [open pages][4]
-    unsigned int *d_csum = nullptr; long long cap_csum = 0; // [chunks][T*NB] sums -> exclusive prefix in place
+    unsigned int *d_csum = nullptr; long long cap_csum = 0; // 2 x [chunks][T*NB] sums -> exclusive prefix in place
+    int csum_par = 0;                  // the buffer the next scan uses
+    long long csum_used[2] = {0, 0};   // entries of each buffer left to zero
     unsigned long long *d_ckey = nullptr, *d_ckey2 = nullptr; long long cap_cand = 0;
     int *d_cslot = nullptr, *d_cslot2 = nullptr;
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate

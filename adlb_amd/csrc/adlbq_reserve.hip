@@ -179,6 +179,8 @@ struct HistArgs {
     int *specn;              // [npages][4] entries found (> SPEC_CAP: overflowed, not usable)
     const int *pbase, *pwide;  // per page id: packed-offset base, wide flag
     int diag;                  // diagnostic ("hist_diag", wrong results): bit 0 no lists, 1 no epilogue, 2 no counts
+    unsigned int *zcs;         // the other chunk-sum buffer (the previous scan's): zeroed here, a slice per workgroup
+    long long zn;
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -287,6 +289,11 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
     const int C = a.T * NB, w = threadIdx.x >> 6;
     int4 pv[PPB][4];
     uint4 mv[PPB][4];
+    if (a.zn > 0) {  // the previous scan's chunk sums, consumed: zeroed for the scan after this one
+        const int nblk = (a.npages + PPB - 1) / PPB, blk = p0 / PPB;
+        const long long per = (a.zn + nblk - 1) / nblk, z0 = (long long)blk * per, z1 = min(a.zn, z0 + per);
+        for (long long i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
+    }
 #pragma unroll
     for (int q = 0; q < PPB; q++) {
         const int p = p0 + q;
@@ -2354,7 +2361,7 @@ __global__ __launch_bounds__(64) void k_chainr(ChainArgs a, int round, int final
 // position left without a donor check (every later one has none).
 constexpr int DONOR_TQ_LDS = 256;  // tq entries the fast path stages
 __device__ int park_donors_fast(const DonorCtx &c, const int *__restrict__ reqs, const int *rq_req, int n0, int np,
-                                int *resp, int *s_hi, int *s_tq) {
+                                int *resp, int *s_hi, int *s_tq, int *s_tv) {
     const int lane = threadIdx.x & 63, S = c.S, T = c.T;
     for (int q = lane; q < S * T; q += 64) s_hi[q] = c.qm_hi[q];
     for (int q = lane; q < 4 * c.n_tq; q += 64) s_tq[q] = c.tq[q];
@@ -2408,18 +2415,17 @@ __device__ int park_donors_fast(const DonorCtx &c, const int *__restrict__ reqs,
         const int j = in ? rq_req[kk] : 0;
         const int *rr = reqs + (long long)ADLBQ_RESERVE_INTS * j;
         const int rank = in ? rr[0] : -1;
-        int tv[NREQ];
 #pragma unroll
-        for (int e = 0; e < NREQ; e++) tv[e] = in ? rr[2 + e] : -2;
+        for (int e = 0; e < NREQ; e++) s_tv[lane * NREQ + e] = in ? rr[2 + e] : -2;
         int rtr = (in && rank >= 0 && rank < c.A) ? ld_agent(c.rfr_to_rank + rank) : 0;
         const int kn = min(64, n0 + np - k0);
+        __builtin_amdgcn_wave_barrier();  // one wave owns s_tv: its LDS ops complete in order
         for (int i = 0; i < kn && open; i++, k++) {
             const int rk = __builtin_amdgcn_readlane(rank, i), jj = __builtin_amdgcn_readlane(j, i);
             int cand = -1;
             if (rk >= 0 && rk < c.A && __builtin_amdgcn_readlane(rtr, i) < 0) {
-#pragma unroll
                 for (int e = 0; e < NREQ; e++) {
-                    const int wt = __builtin_amdgcn_readlane(tv[e], i);
+                    const int wt = s_tv[i * NREQ + e];
                     if (wt < -1) break;
                     cand = cand_of(rk, wt);
                     if (cand >= 0) break;
@@ -2499,9 +2505,9 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     // the RFR donors in FIFO order (rfr_out / rfr_to_rank chain them); once no
     // server can be a donor any more (each RFR sets rfr_out), the rest get -1
     // in parallel
-    __shared__ int s_hi[ADLBQ_MAX_TYPES * 64], s_tq[4 * DONOR_TQ_LDS];
+    __shared__ int s_hi[ADLBQ_MAX_TYPES * 64], s_tq[4 * DONOR_TQ_LDS], s_tv[64 * NREQ];
     if (w == 0 && donors && c.S <= 64 && c.n_tq <= DONOR_TQ_LDS) {
-        const int k = park_donors_fast(c, reqs, rq_req, n0, np, resp, s_hi, s_tq);
+        const int k = park_donors_fast(c, reqs, rq_req, n0, np, resp, s_hi, s_tq, s_tv);
         if (lane == 0) s_stop = k;
     } else if (w == 0) {
         bool open = donors && (c.n_tq > 0 || any_donor(c));
@@ -2751,9 +2757,10 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
     if (need_cs > h->cap_csum) {
         if (h->d_csum) AQ_HIP(hipFree(h->d_csum));
         h->cap_csum = std::max(need_cs, 2 * h->cap_csum);
-        AQ_HIP(hipMalloc((void **)&h->d_csum, sizeof(unsigned int) * h->cap_csum));
-        // zero once; every batch's k_rank re-zeroes the rows it used
-        AQ_HIP(hipMemsetAsync(h->d_csum, 0, sizeof(unsigned int) * h->cap_csum, h->stream));
+        // two buffers used by the scans in turn: a scan's pass 1 zeroes the one the previous scan used
+        AQ_HIP(hipMalloc((void **)&h->d_csum, sizeof(unsigned int) * 2 * h->cap_csum));
+        AQ_HIP(hipMemsetAsync(h->d_csum, 0, sizeof(unsigned int) * 2 * h->cap_csum, h->stream));
+        h->csum_used[0] = h->csum_used[1] = 0;
     }
     if ((long long)npages * 4 > h->cap_spec) {
         if (h->d_spec) AQ_HIP(hipFree(h->d_spec));
@@ -2786,8 +2793,15 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     hipStream_t s = h->stream;
     hipEvent_t ev;
     const bool scan = np > 0 && T > 0;
-    const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, h->d_csum,
-                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0};
+    const int par = h->csum_par;
+    unsigned int *csum = h->d_csum + (long long)par * h->cap_csum, *zcs = h->d_csum + (long long)(par ^ 1) * h->cap_csum;
+    const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
+                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0, zcs, h->csum_used[par ^ 1]};
+    if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
+        h->csum_used[par] = (long long)((np + CHUNK - 1) / CHUNK) * C;
+        h->csum_used[par ^ 1] = 0;
+        h->csum_par = par ^ 1;
+    }
     const int ppb = (h->hist_ppb == 2 && T <= 8) ? 2 : 1;  // pages per pass-1 workgroup
     const int npb = (np + ppb - 1) / ppb;
     const int grid = nprep + (scan ? npb : 0);
@@ -2799,6 +2813,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         if (h->hist_diag && scan) {  // diagnostic: an extra pass 1 (no epilogue) with parts skipped, before the real one
             HistArgs hd = ha;
             hd.diag = h->hist_diag | 2;
+            hd.zn = 0;
             kph<<<npb, 256, lds, s>>>(pa, 0, hd);
         }
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
@@ -2812,7 +2827,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     if (scan) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
         stage_begin(h, "thresholds", &ev);
-        k_thresholds<<<C, TH_THREADS, 0, s>>>(T, h->d_dem, h->d_csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
+        k_thresholds<<<C, TH_THREADS, 0, s>>>(T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                        h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor,
                                        h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0);
         stage_end(h, "thresholds", ev);
@@ -2820,7 +2835,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         auto sel = T <= 4 ? k_select_open<4> : T <= 8 ? k_select_open<8> : k_select_open<64>;
         sel<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
-            h->d_need, h->d_binoff, h->d_csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
+            h->d_need, h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
             h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr,
             (sort || !h->rank_in_select) ? nullptr : h->d_crank, (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R);
         stage_end(h, "select", ev);
@@ -3679,7 +3694,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if ((rc = ensure_req_capacity(h, R))) return rc;
     if ((rc = sync_tables(h))) return rc;
     if ((rc = ensure_rq_capacity(h, R))) return rc;
-    const int T = h->T, C = T * NB;
+    const int T = h->T;
     const int np = (int)h->open.pages.size();
     if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
     hipStream_t s = h->stream;
@@ -3747,12 +3762,12 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
         const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch,
                           h->sort_fail_test};
-        // a small grid when the last landed batch was ranked in k_select_open
-        // (every loop is grid-strided: any grid is correct, the hint only sizes it)
         const int warm0 = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
         const SegGuess sgv{(T <= 8 && h->seg_guess) ? h->d_sg : nullptr, (R + SEG - 1) / SEG, warm0, h->rank_epoch};
-        k_rank<<<rank_hint(h) ? 64 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, h->d_csum,
-                                    (long long)((np + CHUNK - 1) / CHUNK) * C, h->d_mask, h->d_tmatch, R,
+        // a small grid when the last landed batch was ranked in k_select_open (every loop is
+        // grid-strided: any grid is correct, the hint only sizes it); chunk sums: zeroed by the next scan
+        k_rank<<<rank_hint(h) ? 4 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, nullptr,
+                                    0, h->d_mask, h->d_tmatch, R,
                                     h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr,
                                     sgv);
         stage_end(h, "rank", ev);
@@ -3895,15 +3910,14 @@ int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
     wq_changed(h);  // the export scan rebuilds the candidate lists
     int rc;
     if ((rc = sync_tables(h))) return rc;
-    const int T = h->T, C = T * NB;
+    const int T = h->T;
     const int np = (int)h->open.pages.size();
     if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
     k_export_begin<<<1, 64, 0, h->stream>>>(h->d_dem, T, k);
     if ((rc = launch_scan(h, PrepArgs{}, 0, true, 0))) return rc;
-    const long long ncsum = np > 0 ? (long long)((np + CHUNK - 1) / CHUNK) * C : 0;
     k_export_gather<<<T, 256, 0, h->stream>>>(T, k, h->d_candoff, h->d_candlen, h->d_cslot, h->d_prio, h->d_seq,
                                               h->d_cold0, h->d_cold1, d_out, d_out + (size_t)T * k * 8, d_navail,
-                                              h->d_coltot, np > 0 ? 1 : 0, h->d_csum, ncsum, h->d_dem, h->d_anchor,
+                                              h->d_coltot, np > 0 ? 1 : 0, nullptr, 0, h->d_dem, h->d_anchor,
                                               h->d_anchor_next);
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
