@@ -2081,6 +2081,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->tdel_max = value;
         return ADLBQ_OK;
     }
+    if (n == "select_chunk") {
+        h->select_chunk = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "hist_ppb") {
         h->hist_ppb = value == 2 ? 2 : 1;
         return ADLBQ_OK;

@@ -8,7 +8,7 @@ mkdir -p $O
 HB=$!
 trap "kill $HB" EXIT
 cd $R
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread > $O/parity.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/parity.log 2>&1
 rc=$?
 tail -5 $O/parity.log
 if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/parity.log | head -30; exit 1; fi
