@@ -84,6 +84,42 @@ def test_fresh_vs_oracle(gpu_available, name):
     assert_same(run_abi(w.user_types, cfg, tr, max_units=w.n_units), run_oracle(w.user_types, cfg, tr))
 
 
+VARIANTS = {
+    "select_chunk": {"select_chunk": 1},   # pass 2: one workgroup per chunk of pages
+    "hist_ppb2": {"hist_ppb": 2},          # pass 1: two pages per workgroup
+    "no_seg_guess": {"seg_guess": 0},      # the chain finds its own start guesses
+    "all": {"select_chunk": 1, "hist_ppb": 2},
+}
+
+
+@pytest.mark.parametrize("name", ["c2_n200k_r16k", "c2_eq_n200k_r16k", "c2_mixed_wide_pages", "c2_exhaust",
+                                  "c4_t8_tied", "c2_t1"])
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
+def test_pipeline_variants_vs_oracle(gpu_available, name, variant):
+    """The scan and chain variants (adlbq_set_param) give the sequential result."""
+    w = CASES[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    assert_same(run_abi(w.user_types, cfg, tr, max_units=w.n_units, params=VARIANTS[variant]),
+                run_oracle(w.user_types, cfg, tr))
+
+
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
+def test_pipeline_variants_depletion(gpu_available, variant):
+    """Several Reserve batches in a row through each variant (the guessed cut,
+    chunk sums and start guesses carry from batch to batch)."""
+    w = synth.config2(n_units=30_000, n_reserves=4096, seed=311)
+    rng = np.random.default_rng(9)
+    parts = [synth.put_events(w)]
+    for _ in range(5):
+        parts.append(synth.reserve_events(w.r_rank, synth.type_vectors(rng, w.user_types, w.n_reserves), w.r_hang))
+        parts.append(synth.simple_events(synth.OP_INFO))
+    tr = np.concatenate(parts)
+    cfg = (w.num_app_ranks, 1, 0)
+    assert_same(run_abi(w.user_types, cfg, tr, max_units=w.n_units, params=VARIANTS[variant]),
+                run_oracle(w.user_types, cfg, tr))
+
+
 @pytest.mark.parametrize("name", ["c2_n200k_r16k", "c2_t64_wide", "c4_n200k", "c4_t8_tied"])
 @pytest.mark.parametrize("passes", [1, 2, 3])
 def test_chain_fixup_path(gpu_available, name, passes):
