@@ -181,6 +181,7 @@ struct HistArgs {
     int diag;                  // diagnostic ("hist_diag", wrong results): bit 0 no lists, 1 no epilogue, 2 no counts
     unsigned int *zcs;         // the other chunk-sum buffer (the previous scan's): zeroed here, a slice per workgroup
     long long zn;
+    int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -277,7 +278,6 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
             if (v) atomicAdd(&cs[c], v);
         }
     }
-    __syncthreads();
 }
 
 // Every type is counted, demand or not: k_thresholds ignores the columns of a
@@ -291,15 +291,16 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
     uint4 mv[PPB][4];
     if (a.zn > 0) {  // the previous scan's chunk sums, consumed: zeroed for the scan after this one
         const int nblk = (a.npages + PPB - 1) / PPB, blk = p0 / PPB;
-        const long long per = (a.zn + nblk - 1) / nblk, z0 = (long long)blk * per, z1 = min(a.zn, z0 + per);
-        for (long long i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
+        const int per = (int)((a.zn + nblk - 1) / nblk);  // zn < 2^31
+        const int z0 = blk * per, z1 = min((int)a.zn, z0 + per);
+        for (int i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
     }
 #pragma unroll
     for (int q = 0; q < PPB; q++) {
         const int p = p0 + q;
         if (p < a.npages)
-            load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pages[p], p == a.npages - 1 ? a.tail_fill : PAGE, w,
-                         pv[q], mv[q]);
+            load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p],
+                         p == a.npages - 1 ? a.tail_fill : PAGE, w, pv[q], mv[q]);
     }
     hist_stage_types(a, sag);
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
@@ -308,6 +309,7 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
     for (int q = 0; q < PPB; q++) {
         if (p0 + q >= a.npages) break;
         if (q > 0) {
+            __syncthreads();  // the previous page's epilogue has read hist
             for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
             __syncthreads();
         }
@@ -440,10 +442,7 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(int T, const int *__r
 //   3. per column: page prefix + counts of the earlier waves;
 //   4. a candidate's rank in its column = that start + the number of equal
 //      columns earlier in the wave's list (64 list entries per step).
-// PPB pages per workgroup, in order (PPB == CHUNK: one chunk, whose prefix is
-// the chunk's row alone); each page's column counts carry into the next, and
-// the next page's speculative list is loaded while the current one is ranked.
-template <int TB, int PPB>  // TB >= T; the candidates are ranked here only for TB <= RT
+template <int TB>  // TB >= T; the candidates are ranked here only for TB <= RT
 __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
     const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
@@ -454,7 +453,254 @@ __global__ __launch_bounds__(256) void k_select_open(
     const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
     const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
     unsigned char *__restrict__ rtype, int R) {
-    static_assert(PPB == 1 || PPB == CHUNK, "a workgroup takes one page or one whole chunk");
+    constexpr int RT = TB <= RANK_FAST_T ? TB : 1;  // types of the fast ranking
+    extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
+    __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
+    __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES], slen[RT];
+    __shared__ int sbo[RT * NB];  // binoff (fast ranking)
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = blockIdx.x;
+    unsigned int *wc = lds;
+    unsigned int *list = lds + 4 * C + w * 1024;
+    const long long base = (long long)pages[p] << PAGE_SHIFT;
+    const int fill = (p == npages - 1) ? tail_fill : PAGE;
+    // Pass 1's speculative list of this wave's quarter is usable when it did
+    // not overflow and, for every type with demand, the guessed cut is at or
+    // below the real one (lane t checks type t; T <= 64): then the list holds
+    // every candidate and the page's columns are not read again.
+    // All of the prologue's loads are issued together: lane t's type-t
+    // parameters, the list (read whether or not it is used) and, below, the
+    // page prefix rows.
+    const bool tl = lane < T;
+    const int th_l = tl ? theta[lane] : -1, nd_l = tl ? need[lane] : 0, len_l = tl ? candlen[lane] : 0;
+    const long long an_l = tl ? anchor[lane] : 0, gc_l = tl ? gcut[lane] : 0;
+    const int sn = specn[(long long)p * 4 + w];
+    // binoff for the fast ranking (T <= 8: at most two columns per thread), in flight with the rest
+    int bo_r[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int c = threadIdx.x + q * 256;
+        bo_r[q] = (TB <= RANK_FAST_T && crank != nullptr && c < C) ? binoff[c] : 0;
+    }
+    const unsigned int *__restrict__ sp = spec + ((long long)p * 4 + w) * SPEC_CAP;
+    unsigned int se[SPEC_CAP / 64];
+#pragma unroll
+    for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
+    const long long cut_l = cut_of(th_l, an_l);
+    const bool use_spec = __ballot(th_l >= 0 && gc_l > cut_l) == 0 && sn <= SPEC_CAP;  // wave-uniform
+    int4 pv[4];
+    uint4 mv[4];
+    if (!use_spec) load_quarter(prio, meta, pbase, pwide, pages[p], fill, w, pv, mv);
+    if (p == 0 && threadIdx.x == 0) ctr->spec_page0 = use_spec ? 1 : 0;
+    // rank of this page's first unit in each of the thread's columns (only
+    // columns at or below a threshold): the chunk's exclusive prefix
+    // (k_thresholds) plus the counts of the chunk's earlier pages (hist_page)
+    constexpr int CPT = (ADLBQ_MAX_TYPES * NB) / 256;  // columns per thread, at most
+    unsigned int ppv[CPT];
+    const int p0 = (p / CHUNK) * CHUNK;
+#pragma unroll
+    for (int r = 0; r < CPT; r++) {
+        const int c = threadIdx.x + r * 256;
+        ppv[r] = 0;
+        if (r * 256 >= C) break;
+        const int thc = __shfl(th_l, (c / NB) & 63, 64);
+        if (c < C && (c % NB) <= thc) {
+            unsigned int v = csum[(long long)(p / CHUNK) * C + c];
+            unsigned short g[CHUNK - 1];
+#pragma unroll
+            for (int q = 0; q < CHUNK - 1; q++) g[q] = p0 + q < p ? gh[(long long)(p0 + q) * C + c] : (unsigned short)0;
+#pragma unroll
+            for (int q = 0; q < CHUNK - 1; q++) v += g[q];
+            ppv[r] = v;
+        }
+    }
+    if (w == 0 && tl) {
+        sanc[lane] = an_l;
+        sth[lane] = th_l;
+        sneed[lane] = nd_l;
+        scut[lane] = cut_l;
+        if (lane < RT) slen[lane] = len_l;
+    }
+    // ranks computed here (k_rank then skips its tiles) when every threshold
+    // lies in an exact bin: every candidate list is then in (prio desc,
+    // position asc) order by construction, and a unit of another type u with
+    // the same prio precedes this one iff it lies earlier in the open bucket
+    const bool fast = TB <= RANK_FAST_T && crank != nullptr && __ballot(tl && th_l >= NBX) == 0;
+    if (fast)  // binoff (only read for the types with demand, the ones k_thresholds wrote it for)
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            if (threadIdx.x + q * 256 < C) sbo[threadIdx.x + q * 256] = bo_r[q];
+    for (int c = threadIdx.x; c < 4 * C; c += blockDim.x) wc[c] = 0;
+    if (threadIdx.x < 64) {  // candidate list offsets: exclusive prefix of candlen over types
+        const int len = len_l;
+        int x = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (threadIdx.x >= o) x += y;
+        }
+        if (threadIdx.x < T) soff[threadIdx.x] = x - len;
+        if (p == 0 && threadIdx.x < T) candoff_out[threadIdx.x] = x - len;
+        if (p == 0 && threadIdx.x == T - 1) candoff_out[T] = x;
+    }
+    __syncthreads();
+    int n = 0;  // this wave's candidates so far (uniform)
+    const unsigned long long lt = lanemask_lt();
+    if (use_spec) {  // filter the list: entries in bins up to the type's threshold
+#pragma unroll
+        for (int k = 0; k < SPEC_CAP / 64; k++) {
+            if (k * 64 >= sn) break;
+            const unsigned int e = se[k];
+            const int col = (int)(e >> 12), ct = col / NB;
+            const bool c = k * 64 + lane < sn && col - ct * NB <= sth[ct];
+            const unsigned long long b = __ballot(c);
+            if (c) {
+                list[n + __popcll(b & lt)] = e;
+                atomicAdd(&wc[w * C + col], 1u);
+            }
+            n += __popcll(b);
+        }
+    } else
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
+        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+        bool cnd[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            cnd[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && (long long)pr[q] >= scut[mm[q] & M_TYPE];
+        const unsigned long long b0 = __ballot(cnd[0]), b1 = __ballot(cnd[1]), b2 = __ballot(cnd[2]),
+                                 b3 = __ballot(cnd[3]);
+        if (!(b0 | b1 | b2 | b3)) continue;
+        int pos = n + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (cnd[q]) {
+                const int t = mm[q] & M_TYPE;
+                const int col = t * NB + bin_of(sanc[t] - pr[q]);
+                atomicAdd(&wc[w * C + col], 1u);
+                list[pos++] = ((unsigned int)col << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+            }
+        }
+        n += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < CPT; r++) {
+        const int c = threadIdx.x + r * 256;
+        if (c < C && (c % NB) <= sth[c / NB]) {
+            unsigned int run = ppv[r];
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+                const unsigned int x = wc[v * C + c];
+                wc[v * C + c] = run;
+                run += x;
+            }
+        }
+    }
+    __syncthreads();
+    unsigned int *run = wc + w * C;
+    // the fast ranking's per-type constants, uniform over the wave (from LDS once)
+    long long an_u[RT];
+    int th_u[RT], nd_u[RT], len_u[RT];
+    if (fast) {
+#pragma unroll
+        for (int u = 0; u < RT; u++) {
+            const bool ok = u < T;
+            an_u[u] = ok ? sanc[u] : 0;
+            th_u[u] = ok ? sth[u] : -1;
+            nd_u[u] = ok ? sneed[u] : 0;
+            len_u[u] = ok ? slen[u] : 0;
+        }
+    }
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        const unsigned int e = i < n ? list[i] : 0u;
+        const int col = (int)(e >> 12), so = (int)(e & (PAGE - 1));
+        // key order = (prio desc, position in the open bucket asc): the bucket
+        // holds its units in wqseqno order, so this is the reference's order.
+        // An exact bin fixes the prio (anchor - bin); only a multi-prio bin reads it.
+        const int ct = col / NB, cb = col - ct * NB;
+        const int pr = i >= n ? 0 : cb < NBX ? (int)(sanc[ct] - cb) : prio[base + so];
+        const unsigned int bpos = ((unsigned int)p << PAGE_SHIFT) | (unsigned int)so;
+        // fast ranking: per type u, the column holding prio pr (exact bins at
+        // or below u's threshold), else -1 (u has no unit of prio pr among its
+        // candidates: all of them are better, or none)
+        int tcol[RT], cnt[RT];
+        if (fast) {
+#pragma unroll
+            for (int u = 0; u < RT; u++) {
+                const long long bu = an_u[u] - (long long)pr;
+                tcol[u] = (bu >= 0 && bu <= th_u[u]) ? u * NB + (int)bu : -1;
+                cnt[u] = 0;
+            }
+        }
+        int rank = 0;
+        const int jn = min(n - i0, 64);
+        for (int j = 0; j < jn; j++) {
+            const int cj = (int)(list[i0 + j] >> 12);
+            const int before = j < lane;
+            rank += before & (cj == col);
+            if (fast) {
+#pragma unroll
+                for (int u = 0; u < RT; u++) cnt[u] += before & (cj == tcol[u]);
+            }
+        }
+        if (i < n) {
+            const unsigned int r = run[col] + rank;
+            const int t = col / NB, b = col - t * NB;
+            if (b < sth[t] || b >= NBX || (int)r < sneed[t]) {  // exact threshold bin: its first `need` only
+                const long long at = (long long)soff[t] + binoff[col] + r;
+                ckey[at] = make_key(pr, bpos);
+                cslot[at] = (int)(base + so);
+                if (fast) {
+                    // global rank: per type u, its candidates better than this one
+                    int lb[RT], g = 0;
+#pragma unroll
+                    for (int u = 0; u < RT; u++) {
+                        lb[u] = 0;
+                        if (tcol[u] >= 0) {
+                            int c = (int)run[tcol[u]] + cnt[u];  // units of prio pr earlier in the bucket
+                            if (tcol[u] - u * NB == th_u[u]) c = min(c, nd_u[u]);  // the threshold bin's first `need`
+                            lb[u] = sbo[tcol[u]] + c;
+                        } else if (an_u[u] >= (long long)pr) {
+                            lb[u] = len_u[u];  // every candidate of u is better
+                        }
+                        g += lb[u];
+                    }
+                    crank[at] = ((unsigned int)g << 6) | (unsigned int)t;
+                    if (lv != nullptr && g < R) rtype[g] = (unsigned char)t;
+                    // level rows, sampled every LV_STEP ranks (rtype completes them between samples)
+                    if (lv != nullptr && (g & (LV_STEP - 1)) == 0 && g < R)
+#pragma unroll
+                        for (int u = 0; u < RT; u++)
+                            if (u < T) lv[(long long)(g / LV_STEP) * T + u] = lb[u];
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (i < n) atomicAdd(&run[col], 1u);  // after every lane of the step has read run[]
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (fast && p == 0 && threadIdx.x == 0) ctr->rank_fast = 1;
+    if (!fast && crank != nullptr && p == 0 && threadIdx.x == 0) ctr->rank_fast = 0;
+}
+
+// k_select_open with one workgroup per chunk of CHUNK pages, in order (the
+// chunk's prefix is its row alone; each page's column counts carry into the
+// next; the next page's speculative list is loaded while the current one is
+// ranked).  Option "select_chunk" (T <= 8).
+template <int TB, int PPB = CHUNK>  // TB >= T; the candidates are ranked here only for TB <= RT
+__global__ __launch_bounds__(256) void k_select_chunk(
+    const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
+    const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
+    const int *__restrict__ theta, const int *__restrict__ need,
+    const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
+    const int *__restrict__ candlen, int *__restrict__ candoff_out,
+    unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
+    const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
+    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
+    unsigned char *__restrict__ rtype, int R) {
+    static_assert(PPB == CHUNK, "a workgroup takes one whole chunk");
     constexpr int RT = TB <= RANK_FAST_T ? TB : 1;  // types of the fast ranking
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
@@ -494,7 +740,7 @@ __global__ __launch_bounds__(256) void k_select_open(
     // columns at or below a threshold): the chunk's exclusive prefix
     // (k_thresholds) plus the counts of the chunk's earlier pages (hist_count);
     // then carried from page to page
-    constexpr int CPT = (ADLBQ_MAX_TYPES * NB) / 256;  // columns per thread, at most
+    constexpr int CPT = (TB * NB + 255) / 256;  // columns per thread, at most
     unsigned int ppv[CPT];
     const int p0 = (pfirst / CHUNK) * CHUNK;
 #pragma unroll
@@ -1462,12 +1708,23 @@ __device__ void seg_guesses(const SegGuess &g, int T, const int *soff, const int
         const int J = pre[min(jb >> 6, nq)];
         const int Js = J & ~(LV_STEP - 1);
         int extra[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (J > 0 && J < G)
-            for (int r = Js; r < J; r++) {
-                const int tt = lr.rtype[r];
+        if (J > 0 && J < G) {  // type bytes of ranks [Js, J): four 16-byte loads (Js is 64-aligned)
+            const uint4 *rt4 = reinterpret_cast<const uint4 *>(lr.rtype + Js);
+            uint4 v4[4];
 #pragma unroll
-                for (int u = 0; u < 8; u++) extra[u] += tt == u;
+            for (int q = 0; q < 4; q++) v4[q] = rt4[q];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const unsigned int wd[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
+#pragma unroll
+                for (int b = 0; b < 16; b++) {
+                    const int tt = (int)((wd[b >> 2] >> (8 * (b & 3))) & 0xffu);
+                    const bool in = Js + q * 16 + b < J;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) extra[u] += (in && tt == u) ? 1 : 0;
+                }
             }
+        }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             if (u >= T) break;
@@ -2816,10 +3073,14 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     hipStream_t s = h->stream;
     hipEvent_t ev;
     const bool scan = np > 0 && T > 0;
+    // the open bucket's pages in one run of ids (one bulk Put): pass 1 computes the page id
+    int pg0 = np > 0 ? h->open.pages[0] : -1;
+    for (int i = 1; i < np && pg0 >= 0; i++)
+        if (h->open.pages[(size_t)i] != pg0 + i) pg0 = -1;
     const int par = h->csum_par;
     unsigned int *csum = h->d_csum + (long long)par * h->cap_csum, *zcs = h->d_csum + (long long)(par ^ 1) * h->cap_csum;
     const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
-                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0, zcs, h->csum_used[par ^ 1]};
+                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0, zcs, h->csum_used[par ^ 1], pg0};
     if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
         h->csum_used[par] = (long long)((np + CHUNK - 1) / CHUNK) * C;
         h->csum_used[par ^ 1] = 0;
@@ -2856,8 +3117,8 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         stage_end(h, "thresholds", ev);
         stage_begin(h, "select", &ev);
         const bool chunked = h->select_chunk && T <= 8;  // one workgroup per chunk of pages
-        auto sel = chunked ? (T <= 4 ? k_select_open<4, CHUNK> : k_select_open<8, CHUNK>)
-                           : T <= 4 ? k_select_open<4, 1> : T <= 8 ? k_select_open<8, 1> : k_select_open<64, 1>;
+        auto sel = chunked ? (T <= 4 ? k_select_chunk<4> : k_select_chunk<8>)
+                           : T <= 4 ? k_select_open<4> : T <= 8 ? k_select_open<8> : k_select_open<64>;
         sel<<<chunked ? nchunks : np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
