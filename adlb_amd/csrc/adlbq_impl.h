@@ -232,7 +232,8 @@ struct adlbq_server {
     int *d_seg_cnt = nullptr;          // [R/64] chain: untargeted-capable requests per 64 requests
     unsigned long long *d_pmask = nullptr;  // [R/64] k_finalize: ballots of the requests that park
     int *d_sg = nullptr;               // [1 + nseg * 8] k_rank's per-segment start guesses for the chain (T <= 8)
-    int seg_guess = 1;                 // "seg_guess": k_rank makes them (0: every chain segment finds its own)
+    int seg_guess = 0;                 // "seg_guess": k_rank makes them (0: every chain segment finds its own;
+                                       // measured: k_rank +7 us for -0.5 us of chain, so off by default)
     int *d_lv = nullptr;               // [R][T] k_rank: level rows for the chain's guess (T <= 8)
     unsigned char *d_rtype = nullptr;
     int *d_pm_over = nullptr;          // k_put_match_blk: the staged rq overflowed

@@ -302,6 +302,15 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
             load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p],
                          p == a.npages - 1 ? a.tail_fill : PAGE, w, pv[q], mv[q]);
     }
+    if (a.diag & 8) {  // diagnostic: the loads alone (one store of their sum per wave, so they are kept)
+        unsigned int acc = 0;
+#pragma unroll
+        for (int q = 0; q < PPB; q++)
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc += mv[q][k].x + mv[q][k].y + mv[q][k].z + mv[q][k].w;
+        if (acc == 0x9e3779b9u) a.specn[0] = (int)acc;  // practically never taken
+        return;
+    }
     hist_stage_types(a, sag);
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
     __syncthreads();
@@ -3094,11 +3103,11 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         stage_begin(h, "hist", &ev);
         auto kph = ppb == 2 ? (T <= 4 ? k_prep_hist<4, 2> : k_prep_hist<8, 2>)
                             : T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
-        if (h->hist_diag && scan) {  // diagnostic: an extra pass 1 (no epilogue) with parts skipped, before the real one
+        if (h->hist_diag && scan) {  // diagnostic: extra passes 1 (no epilogue) with parts skipped, before the real one
             HistArgs hd = ha;
-            hd.diag = h->hist_diag | 2;
+            hd.diag = (h->hist_diag & 0xff) | 2;
             hd.zn = 0;
-            kph<<<npb, 256, lds, s>>>(pa, 0, hd);
+            for (int r = 0; r < std::max(1, h->hist_diag >> 8); r++) kph<<<npb, 256, lds, s>>>(pa, 0, hd);
         }
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
             kph<<<nprep, 256, lds, s>>>(pa, nprep, ha);
