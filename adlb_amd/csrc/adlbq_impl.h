@@ -262,9 +262,11 @@ struct adlbq_server {
     int *d_dvals = nullptr, *d_dvals2 = nullptr; long long cap_del = 0, tdel_n = 0, tdel_max = 1 << 18;
     int *d_dstart = nullptr, *d_dend = nullptr; long long cap_drange = 0;
     long long tidx_delta_merges = 0, tidx_folds = 0;
-    std::vector<unsigned long long> tnew_sk;  // host staging of the sorted new keys / positions
-    std::vector<int> tnew_sv;
-    hipEvent_t tnew_ev = nullptr;
+    unsigned long long *h_tnewk[2] = {nullptr, nullptr};  // pinned staging of the sorted new keys / positions,
+    int *h_tnewv[2] = {nullptr, nullptr};                 // two buffers used in turn behind their events
+    long long cap_htnew[2] = {0, 0};
+    hipEvent_t tnew_ev[2] = {nullptr, nullptr};
+    int tnew_slot = 0;
     // segmented radix sort of the multi-prio-bin candidate lists (launched
     // when the newest landed batch needed one; k_rank sorts otherwise)
     int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort

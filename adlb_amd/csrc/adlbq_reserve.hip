@@ -3205,18 +3205,26 @@ static int ensure_tindex(adlbq_server *h) {
         for (long long i = 0; i < m; i++) ord[(size_t)i] = (int)i;
         const auto &K = h->tnew_keys;
         std::stable_sort(ord.begin(), ord.end(), [&K](int a, int b) { return K[(size_t)a] < K[(size_t)b]; });
-        // host staging kept until the copy has run (the event of the previous merge)
-        if (h->tnew_ev) AQ_HIP(hipEventSynchronize(h->tnew_ev));
-        else AQ_HIP(hipEventCreateWithFlags(&h->tnew_ev, hipEventDisableTiming));
-        h->tnew_sk.resize((size_t)m);
-        h->tnew_sv.resize((size_t)m);
-        for (long long i = 0; i < m; i++) {
-            h->tnew_sk[(size_t)i] = K[(size_t)ord[(size_t)i]];
-            h->tnew_sv[(size_t)i] = h->tnew_vals[(size_t)ord[(size_t)i]];
+        // pinned host staging, two buffers used in turn: a buffer is rewritten only once the
+        // copy of two merges ago has run (its event), so the host never waits for the last one
+        const int sl = h->tnew_slot;
+        h->tnew_slot ^= 1;
+        if (h->tnew_ev[sl]) AQ_HIP(hipEventSynchronize(h->tnew_ev[sl]));
+        else AQ_HIP(hipEventCreateWithFlags(&h->tnew_ev[sl], hipEventDisableTiming));
+        if (m > h->cap_htnew[sl]) {
+            if (h->h_tnewk[sl]) AQ_HIP(hipHostFree(h->h_tnewk[sl]));
+            if (h->h_tnewv[sl]) AQ_HIP(hipHostFree(h->h_tnewv[sl]));
+            h->cap_htnew[sl] = std::max(m, 2 * h->cap_htnew[sl]);
+            AQ_HIP(hipHostMalloc((void **)&h->h_tnewk[sl], sizeof(unsigned long long) * h->cap_htnew[sl], hipHostMallocDefault));
+            AQ_HIP(hipHostMalloc((void **)&h->h_tnewv[sl], sizeof(int) * h->cap_htnew[sl], hipHostMallocDefault));
         }
-        AQ_HIP(hipMemcpyAsync(h->d_tnewk, h->tnew_sk.data(), sizeof(unsigned long long) * m, hipMemcpyHostToDevice, s));
-        AQ_HIP(hipMemcpyAsync(h->d_tnewv, h->tnew_sv.data(), sizeof(int) * m, hipMemcpyHostToDevice, s));
-        AQ_HIP(hipEventRecord(h->tnew_ev, s));
+        for (long long i = 0; i < m; i++) {
+            h->h_tnewk[sl][i] = K[(size_t)ord[(size_t)i]];
+            h->h_tnewv[sl][i] = h->tnew_vals[(size_t)ord[(size_t)i]];
+        }
+        AQ_HIP(hipMemcpyAsync(h->d_tnewk, h->h_tnewk[sl], sizeof(unsigned long long) * m, hipMemcpyHostToDevice, s));
+        AQ_HIP(hipMemcpyAsync(h->d_tnewv, h->h_tnewv[sl], sizeof(int) * m, hipMemcpyHostToDevice, s));
+        AQ_HIP(hipEventRecord(h->tnew_ev[sl], s));
         h->tnew_keys.clear();
         h->tnew_vals.clear();
         const int G = nb * 64;

@@ -1319,7 +1319,11 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->d_tnewv) hipFree(h->d_tnewv);
     for (int q = 0; q < 2; q++)
         if (h->put_ev[q]) hipEventDestroy(h->put_ev[q]);
-    if (h->tnew_ev) hipEventDestroy(h->tnew_ev);
+    for (int q = 0; q < 2; q++) {
+        if (h->tnew_ev[q]) hipEventDestroy(h->tnew_ev[q]);
+        if (h->h_tnewk[q]) hipHostFree(h->h_tnewk[q]);
+        if (h->h_tnewv[q]) hipHostFree(h->h_tnewv[q]);
+    }
     if (h->steal_ev) hipEventDestroy(h->steal_ev);
     if (h->apply_ev) hipEventDestroy(h->apply_ev);
     for (auto &kv : h->timers)
