@@ -226,7 +226,8 @@ __device__ __forceinline__ void hist_stage_types(const HistArgs &a, int2 *sag) {
 // sag staged before the barrier the caller ran), speculative lists, per-page
 // row and chunk sums.  Ends with a barrier: hist may be reused afterwards.
 __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const int4 (&pv)[4], const uint4 (&mv)[4],
-                                           const int2 *sag, unsigned int *__restrict__ hist /* [C][HK] */) {
+                                           const int2 *sag, unsigned int *__restrict__ hist /* [C][HK] */,
+                                           const int2 (&rag)[4]) {
     const int T = a.T;
     const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned int *my = hist + (lane % HK);
@@ -246,7 +247,7 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
         for (int q = 0; q < 4; q++) {
             const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
             const int t = mm[q] & M_TYPE;
-            const int2 ag = sag[t];
+            const int2 ag = (a.diag & 16) ? (t == 0 ? rag[0] : t == 1 ? rag[1] : t == 2 ? rag[2] : rag[3]) : sag[t];
             col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
             in[q] = av && pr[q] >= ag.y && !(a.diag & 1);
             if (av && !(a.diag & 4)) atomicAdd(&my[col[q] * HK], 1u);
@@ -311,9 +312,19 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
         if (acc == 0x9e3779b9u) a.specn[0] = (int)acc;  // practically never taken
         return;
     }
-    hist_stage_types(a, sag);
-    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-    __syncthreads();
+    int2 rag[4];
+    if (a.diag & 16) {  // diagnostic: anchor and cut of types 0-3 in registers
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            rag[t] = t < a.T ? make_int2((int)a.anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX),
+                                                                           (long long)INT_MIN))
+                             : make_int2(0, 0);
+    }
+    if (!(a.diag & 32)) {  // diagnostic 32: no staging barrier (wrong counts)
+        hist_stage_types(a, sag);
+        for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+        __syncthreads();
+    }
 #pragma unroll
     for (int q = 0; q < PPB; q++) {
         if (p0 + q >= a.npages) break;
@@ -322,7 +333,7 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
             for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
             __syncthreads();
         }
-        hist_count(a, p0 + q, pv[q], mv[q], sag, hist);
+        hist_count(a, p0 + q, pv[q], mv[q], sag, hist, rag);
     }
 }
 
