@@ -214,27 +214,21 @@ __device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const
     }
 }
 
-// Every type is counted, demand or not: k_thresholds ignores the columns of a
-// type without demand, and k_rank re-zeroes every chunk sum.
-// The per-type anchor and guessed cut of pass 1, staged in LDS.
-__device__ __forceinline__ void hist_stage_types(const HistArgs &a, int2 *sag) {
-    for (int t = threadIdx.x; t < a.T; t += blockDim.x)
-        sag[t] = make_int2((int)a.anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
-}
-
 // Page p's counts from its loaded quarter (pv, mv): histogram (hist zeroed and
 // sag staged before the barrier the caller ran), speculative lists, per-page
-// row and chunk sums.  Ends with a barrier: hist may be reused afterwards.
+// row and chunk sums.
 __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const int4 (&pv)[4], const uint4 (&mv)[4],
                                            const int2 *sag, unsigned int *__restrict__ hist /* [C][HK] */,
-                                           const int2 (&rag)[4]) {
+                                           unsigned int *__restrict__ slist /* [4][SPEC_CAP] */) {
     const int T = a.T;
     const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned int *my = hist + (lane % HK);
     // units at or above the guessed cut go to this wave's speculative list, in
     // slot order: k_select_open reads the list instead of the page when the
-    // guess holds (every real cut at or above it) and the list did not overflow
-    unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
+    // guess holds (every real cut at or above it) and the list did not overflow.
+    // The list is built in LDS and written out once at the end: a global store
+    // inside the loop would make every later wait on the loads wait for it too
+    unsigned int *wl = slist + w * SPEC_CAP;
     const unsigned long long lt = lanemask_lt();
     int sn = 0;
 #pragma unroll
@@ -247,27 +241,30 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
         for (int q = 0; q < 4; q++) {
             const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
             const int t = mm[q] & M_TYPE;
-            const int2 ag = (a.diag & 16) ? (t == 0 ? rag[0] : t == 1 ? rag[1] : t == 2 ? rag[2] : rag[3]) : sag[t];
+            const int2 ag = sag[t];
             col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
-            in[q] = av && pr[q] >= ag.y && !(a.diag & 1);
-            if (av && !(a.diag & 4)) atomicAdd(&my[col[q] * HK], 1u);
+            in[q] = av && pr[q] >= ag.y;
+            if (av) atomicAdd(&my[col[q] * HK], 1u);
         }
         const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
                                  b3 = __ballot(in[3]);
-        if (!(b0 | b1 | b2 | b3)) continue;
         int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            if (in[q]) {
-                if (pos < SPEC_CAP)
-                    sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
-                pos++;
-            }
+            if (in[q] && pos < SPEC_CAP)
+                wl[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+            pos += in[q];
         }
         sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
     }
-    if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
+    // the wave's list out to global memory (coalesced), then the page's column row and chunk sums
+    unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
+    const int nl = min(sn, SPEC_CAP);
+#pragma unroll
+    for (int k = 0; k < SPEC_CAP / 64; k++)
+        if (k * 64 + lane < nl) sp[k * 64 + lane] = wl[k * 64 + lane];
+    if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     if (!(a.diag & 2)) {
         unsigned int *cs = a.csum + (long long)(p / CHUNK) * C;
         unsigned short *g = a.gh + (long long)p * C;
@@ -282,7 +279,7 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
 }
 
 // Every type is counted, demand or not: k_thresholds ignores the columns of a
-// type without demand, and k_rank re-zeroes every chunk sum.  PPB pages per
+// type without demand; the next scan's pass 1 zeroes this one's chunk sums.  PPB pages per
 // workgroup, every page's loads issued before the first is counted.
 template <int PPB>
 __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsigned int *__restrict__ hist) {
@@ -290,18 +287,20 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
     const int C = a.T * NB, w = threadIdx.x >> 6;
     int4 pv[PPB][4];
     uint4 mv[PPB][4];
-    if (a.zn > 0) {  // the previous scan's chunk sums, consumed: zeroed for the scan after this one
-        const int nblk = (a.npages + PPB - 1) / PPB, blk = p0 / PPB;
-        const int per = (int)((a.zn + nblk - 1) / nblk);  // zn < 2^31
-        const int z0 = blk * per, z1 = min((int)a.zn, z0 + per);
-        for (int i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
-    }
+    // every load issued before anything waits: the pages, then the per-type
+    // anchor / cut (staged in LDS before the barrier, so that wait covers all)
 #pragma unroll
     for (int q = 0; q < PPB; q++) {
         const int p = p0 + q;
         if (p < a.npages)
             load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p],
                          p == a.npages - 1 ? a.tail_fill : PAGE, w, pv[q], mv[q]);
+    }
+    const int tt = threadIdx.x;
+    long long an = 0, gc = 0;
+    if (tt < a.T) {
+        an = __builtin_nontemporal_load(a.anchor + tt);
+        gc = __builtin_nontemporal_load(a.gcut + tt);
     }
     if (a.diag & 8) {  // diagnostic: the loads alone (one store of their sum per wave, so they are kept)
         unsigned int acc = 0;
@@ -312,18 +311,14 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
         if (acc == 0x9e3779b9u) a.specn[0] = (int)acc;  // practically never taken
         return;
     }
-    int2 rag[4];
-    if (a.diag & 16) {  // diagnostic: anchor and cut of types 0-3 in registers
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-            rag[t] = t < a.T ? make_int2((int)a.anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX),
-                                                                           (long long)INT_MIN))
-                             : make_int2(0, 0);
-    }
-    if (!(a.diag & 32)) {  // diagnostic 32: no staging barrier (wrong counts)
-        hist_stage_types(a, sag);
-        for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-        __syncthreads();
+    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+    if (tt < a.T) sag[tt] = make_int2((int)an, (int)std::max(std::min(gc, (long long)INT_MAX), (long long)INT_MIN));
+    __syncthreads();
+    if (a.zn > 0) {  // the previous scan's chunk sums, consumed: zeroed for the scan after this one
+        const int nblk = (a.npages + PPB - 1) / PPB, blk = p0 / PPB;
+        const int per = (int)((a.zn + nblk - 1) / nblk);  // zn < 2^31
+        const int z0 = blk * per, z1 = min((int)a.zn, z0 + per);
+        for (int i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
     }
 #pragma unroll
     for (int q = 0; q < PPB; q++) {
@@ -333,7 +328,7 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
             for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
             __syncthreads();
         }
-        hist_count(a, p0 + q, pv[q], mv[q], sag, hist, rag);
+        hist_count(a, p0 + q, pv[q], mv[q], sag, hist, hist + C * HK);
     }
 }
 
@@ -3110,7 +3105,9 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     const int npb = (np + ppb - 1) / ppb;
     const int grid = nprep + (scan ? npb : 0);
     if (grid > 0) {
-        const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0, scan ? sizeof(unsigned int) * HK * C : 0);
+        // pass 1: the histogram copies, then the four waves' speculative lists
+        const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0,
+                                      scan ? sizeof(unsigned int) * (HK * C + 4 * SPEC_CAP) : 0);
         stage_begin(h, "hist", &ev);
         auto kph = ppb == 2 ? (T <= 4 ? k_prep_hist<4, 2> : k_prep_hist<8, 2>)
                             : T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
