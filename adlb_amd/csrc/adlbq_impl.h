@@ -408,12 +408,13 @@ __device__ __forceinline__ int bin_of(long long d) {
     return b < NB ? b : NB - 1;
 }
 
-// bin_of for a distance known to fit 32 bits (an int anchor less an int prio)
+// bin_of for a distance known to fit 32 bits (an int anchor less an int prio),
+// branch-free (selects only: it runs once per unit in pass 1)
 __device__ __forceinline__ int bin_of32(unsigned int d) {
-    if (d < (unsigned int)NBX) return (int)d;
-    const int o = 31 - __clz((int)d);
-    const int b = o < OCT_H ? NBX + 2 * (o - 5) + (int)((d >> (o - 1)) & 1u) : NBX + NBH + (o - OCT_H);
-    return b < NB ? b : NB - 1;
+    const int o = 31 - __clz((int)(d | 32u));  // >= 5
+    const int bh = NBX + 2 * (o - 5) + (int)((d >> (o - 1)) & 1u), bo = NBX + NBH + (o - OCT_H);
+    const int b = min(o < OCT_H ? bh : bo, NB - 1);
+    return d < (unsigned int)NBX ? (int)d : b;
 }
 
 // the smallest distance bin b holds, and the largest (NB - 1: unbounded)

@@ -181,6 +181,7 @@ struct HistArgs {
     int diag;                  // diagnostic ("hist_diag", wrong results): bit 0 no lists, 1 no epilogue, 2 no counts
     unsigned int *zcs;         // the other chunk-sum buffer (the previous scan's): zeroed here, a slice per workgroup
     long long zn;
+    int zper;                  // entries of zcs each workgroup zeroes
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
 };
 
@@ -231,21 +232,47 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
     unsigned int *wl = slist + w * SPEC_CAP;
     const unsigned long long lt = lanemask_lt();
     int sn = 0;
+    // every unit's (anchor, cut) read first, all LDS reads in flight together;
+    // then the columns (branch-free), then the counts (an unavailable unit adds 0)
+    int2 ag[4][4];
+    if (T <= 4) {  // up to four types: from registers, selected by type
+        int2 a4[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) a4[u] = sag[u < T ? u : 0];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {  // two selects per component on the type's bits
+                const bool b0 = mm[q] & 1u, b1 = mm[q] & 2u;
+                const int x0 = b0 ? a4[1].x : a4[0].x, x1 = b0 ? a4[3].x : a4[2].x;
+                const int y0 = b0 ? a4[1].y : a4[0].y, y1 = b0 ? a4[3].y : a4[2].y;
+                ag[k][q] = make_int2(b1 ? x1 : x0, b1 ? y1 : y0);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) ag[k][q] = sag[min((int)(mm[q] & M_TYPE), T - 1)];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
         const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
         int col[4];
-        bool in[4];
+        bool in[4], av[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
+            av[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
             const int t = mm[q] & M_TYPE;
-            const int2 ag = sag[t];
-            col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
-            in[q] = av && pr[q] >= ag.y;
-            if (av) atomicAdd(&my[col[q] * HK], 1u);
+            col[q] = av[q] ? t * NB + bin_of32((unsigned int)ag[k][q].x - (unsigned int)pr[q]) : 0;  // distance < 2^32
+            in[q] = av[q] && pr[q] >= ag[k][q].y;
         }
+#pragma unroll
+        for (int q = 0; q < 4; q++) atomicAdd(&my[col[q] * HK], av[q] ? 1u : 0u);
         const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
                                  b3 = __ballot(in[3]);
         int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
@@ -315,9 +342,7 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
     if (tt < a.T) sag[tt] = make_int2((int)an, (int)std::max(std::min(gc, (long long)INT_MAX), (long long)INT_MIN));
     __syncthreads();
     if (a.zn > 0) {  // the previous scan's chunk sums, consumed: zeroed for the scan after this one
-        const int nblk = (a.npages + PPB - 1) / PPB, blk = p0 / PPB;
-        const int per = (int)((a.zn + nblk - 1) / nblk);  // zn < 2^31
-        const int z0 = blk * per, z1 = min((int)a.zn, z0 + per);
+        const int z0 = (p0 / PPB) * a.zper, z1 = min((int)a.zn, z0 + a.zper);
         for (int i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
     }
 #pragma unroll
@@ -3094,8 +3119,9 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         if (h->open.pages[(size_t)i] != pg0 + i) pg0 = -1;
     const int par = h->csum_par;
     unsigned int *csum = h->d_csum + (long long)par * h->cap_csum, *zcs = h->d_csum + (long long)(par ^ 1) * h->cap_csum;
-    const HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
-                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0, zcs, h->csum_used[par ^ 1], pg0};
+    HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
+                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0, zcs, h->csum_used[par ^ 1],
+                      0, pg0};
     if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
         h->csum_used[par] = (long long)((np + CHUNK - 1) / CHUNK) * C;
         h->csum_used[par ^ 1] = 0;
@@ -3103,6 +3129,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     }
     const int ppb = (h->hist_ppb == 2 && T <= 8) ? 2 : 1;  // pages per pass-1 workgroup
     const int npb = (np + ppb - 1) / ppb;
+    ha.zper = npb > 0 ? (int)((ha.zn + npb - 1) / npb) : 0;
     const int grid = nprep + (scan ? npb : 0);
     if (grid > 0) {
         // pass 1: the histogram copies, then the four waves' speculative lists
