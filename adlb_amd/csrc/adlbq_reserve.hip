@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256) void k_select_open(
         int rank = 0;
         const int jn = min(n - i0, 64);
         for (int j = 0; j < jn; j++) {
-            const int cj = (int)(list[i0 + j] >> 12);
+            const int cj = __builtin_amdgcn_readlane(col, j);  // lane j's column (no LDS read per step)
             const int before = j < lane;
             rank += before & (cj == col);
             if (fast) {
@@ -942,7 +942,7 @@ __global__ __launch_bounds__(256) void k_select_chunk(
             int rank = 0;
             const int jn = min(n - i0, 64);
             for (int j = 0; j < jn; j++) {
-                const int cj = (int)(list[i0 + j] >> 12);
+                const int cj = __builtin_amdgcn_readlane(col, j);  // lane j's column (no LDS read per step)
                 const int before = j < lane;
                 rank += before & (cj == col);
                 if (fast) {
