@@ -396,9 +396,22 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(int T, const int *__r
     __shared__ bool s_last;
     const int c = blockIdx.x, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     unsigned int carry = 0;
+    // the first TH_PRE rows' loads all in flight before the first scan step
+    constexpr int TH_PRE = 4;
+    unsigned int pre_v[TH_PRE];
+#pragma unroll
+    for (int q = 0; q < TH_PRE; q++) {
+        const int k = q * TH_THREADS + threadIdx.x;
+        pre_v[q] = k < nchunks ? csum[(long long)k * C + c] : 0u;
+    }
     for (int k0 = 0; k0 < nchunks; k0 += TH_THREADS) {
         const int k = k0 + threadIdx.x;
-        const unsigned int v = k < nchunks ? csum[(long long)k * C + c] : 0u;
+        const int q0 = k0 / TH_THREADS;
+        unsigned int v = 0u;
+#pragma unroll
+        for (int q = 0; q < TH_PRE; q++)
+            if (q == q0) v = pre_v[q];
+        if (q0 >= TH_PRE) v = k < nchunks ? csum[(long long)k * C + c] : 0u;
         unsigned int x = v;  // block inclusive scan
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
