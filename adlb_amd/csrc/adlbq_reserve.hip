@@ -215,11 +215,44 @@ __device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const
     }
 }
 
+// A quarter page of the scan columns as stored: meta (4 B per unit), and the
+// prio column only on a wide page (a narrow page's prios are pb + meta >> 10).
+__device__ __forceinline__ void load_quarter_raw(const int *__restrict__ prio, const uint32_t *__restrict__ meta,
+                                                 const int *__restrict__ pbase, const int *__restrict__ pwide,
+                                                 int pg, int fill, int w, int4 (&pv)[4], uint4 (&mv)[4], int &wide,
+                                                 int &pb) {
+    const int lane = threadIdx.x & 63;
+    const long long base = (long long)pg << PAGE_SHIFT;
+    const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
+    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
+    wide = pwide[pg];
+    pb = pbase[pg];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = (w * 4 + k) * 64 + lane;
+        mv[k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+    }
+    if (wide) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int idx = (w * 4 + k) * 64 + lane;
+            pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
+        }
+    }
+}
+
 // Page p's counts from its loaded quarter (pv, mv): histogram (hist zeroed and
 // sag staged before the barrier the caller ran), speculative lists, per-page
 // row and chunk sums.
+// Per unit: off = the prio relative to the page base (narrow: meta >> 10; wide:
+// the prio itself, pb = 0); sagp[t] = {anchor - pb, cut - pb} and lowrel =
+// LOWEST - pb were rebased for this page, so the distance, the cut test and
+// the availability test need no per-unit prio reconstruction.  Every unit's
+// sagp read is issued before any is used; columns and counts are branch-free.
+template <bool NARROW>
 __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const int4 (&pv)[4], const uint4 (&mv)[4],
-                                           const int2 *sag, unsigned int *__restrict__ hist /* [C][HK] */,
+                                           const int2 *sagp, int lowrel,
+                                           unsigned int *__restrict__ hist /* [C][HK] */,
                                            unsigned int *__restrict__ slist /* [4][SPEC_CAP] */) {
     const int T = a.T;
     const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -230,59 +263,47 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
     // The list is built in LDS and written out once at the end: a global store
     // inside the loop would make every later wait on the loads wait for it too
     unsigned int *wl = slist + w * SPEC_CAP;
-    const unsigned long long lt = lanemask_lt();
     int sn = 0;
-    // every unit's (anchor, cut) read first, all LDS reads in flight together;
-    // then the columns (branch-free), then the counts (an unavailable unit adds 0)
     int2 ag[4][4];
-    if (T <= 4) {  // up to four types: from registers, selected by type
-        int2 a4[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) a4[u] = sag[u < T ? u : 0];
+    for (int k = 0; k < 4; k++) {
+        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-#pragma unroll
-            for (int q = 0; q < 4; q++) {  // two selects per component on the type's bits
-                const bool b0 = mm[q] & 1u, b1 = mm[q] & 2u;
-                const int x0 = b0 ? a4[1].x : a4[0].x, x1 = b0 ? a4[3].x : a4[2].x;
-                const int y0 = b0 ? a4[1].y : a4[0].y, y1 = b0 ? a4[3].y : a4[2].y;
-                ag[k][q] = make_int2(b1 ? x1 : x0, b1 ? y1 : y0);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-#pragma unroll
-            for (int q = 0; q < 4; q++) ag[k][q] = sag[min((int)(mm[q] & M_TYPE), T - 1)];
-        }
+        for (int q = 0; q < 4; q++) ag[k][q] = sagp[min((int)(mm[q] & M_TYPE), T - 1)];
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
+        const int pw[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
         const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
         int col[4];
         bool in[4], av[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            av[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
-            const int t = mm[q] & M_TYPE;
-            col[q] = av[q] ? t * NB + bin_of32((unsigned int)ag[k][q].x - (unsigned int)pr[q]) : 0;  // distance < 2^32
-            in[q] = av[q] && pr[q] >= ag[k][q].y;
+            const int off = NARROW ? (int)(mm[q] >> M_OFF_SHIFT) : pw[q];
+            av[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && off > lowrel;
+            // no branch: an unavailable unit gets some in-range column and adds 0 to it
+            const int t = av[q] ? (int)(mm[q] & M_TYPE) : 0;
+            const unsigned int d = av[q] ? (unsigned int)ag[k][q].x - (unsigned int)off : 0u;  // distance < 2^32
+            col[q] = t * NB + bin_of32(d);
+            in[q] = av[q] && off >= ag[k][q].y;
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) atomicAdd(&my[col[q] * HK], av[q] ? 1u : 0u);
-        const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
-                                 b3 = __ballot(in[3]);
-        int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+        // the few units at or above the cut, appended in slot order (lane-major, then q)
+        // by a scalar walk over the set bits: no per-lane position arithmetic
+        const unsigned long long B[4] = {__ballot(in[0]), __ballot(in[1]), __ballot(in[2]), __ballot(in[3])};
+        for (unsigned long long any = B[0] | B[1] | B[2] | B[3]; any; any &= any - 1) {
+            const int l = __ffsll((long long)any) - 1;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (in[q] && pos < SPEC_CAP)
-                wl[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
-            pos += in[q];
+            for (int q = 0; q < 4; q++) {
+                if ((B[q] >> l) & 1ull) {
+                    const int cq = __builtin_amdgcn_readlane(col[q], l);
+                    if (lane == 0 && sn < SPEC_CAP)
+                        wl[sn] = ((unsigned int)cq << 12) | (unsigned int)((w * 4 + k) * 256 + l * 4 + q);
+                    sn++;
+                }
+            }
         }
-        sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
     }
     __syncthreads();
     // the wave's list out to global memory (coalesced), then the page's column row and chunk sums
@@ -310,19 +331,17 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
 // workgroup, every page's loads issued before the first is counted.
 template <int PPB>
 __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsigned int *__restrict__ hist) {
-    __shared__ int2 sag[ADLBQ_MAX_TYPES];
+    static_assert(PPB == 1, "one page per workgroup (two measured slower)");
+    __shared__ int2 sagp[ADLBQ_MAX_TYPES];
     const int C = a.T * NB, w = threadIdx.x >> 6;
-    int4 pv[PPB][4];
-    uint4 mv[PPB][4];
-    // every load issued before anything waits: the pages, then the per-type
+    int4 pv[4];
+    uint4 mv[4];
+    int wide = 0, pb = 0;
+    // every load issued before anything waits: the page, then the per-type
     // anchor / cut (staged in LDS before the barrier, so that wait covers all)
-#pragma unroll
-    for (int q = 0; q < PPB; q++) {
-        const int p = p0 + q;
-        if (p < a.npages)
-            load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p],
-                         p == a.npages - 1 ? a.tail_fill : PAGE, w, pv[q], mv[q]);
-    }
+    const int p = p0;
+    load_quarter_raw(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p],
+                     p == a.npages - 1 ? a.tail_fill : PAGE, w, pv, mv, wide, pb);
     const int tt = threadIdx.x;
     long long an = 0, gc = 0;
     if (tt < a.T) {
@@ -332,29 +351,23 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
     if (a.diag & 8) {  // diagnostic: the loads alone (one store of their sum per wave, so they are kept)
         unsigned int acc = 0;
 #pragma unroll
-        for (int q = 0; q < PPB; q++)
-#pragma unroll
-            for (int k = 0; k < 4; k++) acc += mv[q][k].x + mv[q][k].y + mv[q][k].z + mv[q][k].w;
+        for (int k = 0; k < 4; k++) acc += mv[k].x + mv[k].y + mv[k].z + mv[k].w;
         if (acc == 0x9e3779b9u) a.specn[0] = (int)acc;  // practically never taken
         return;
     }
+    // this page's rebased constants: a narrow page's units carry prio - pb (wide: pb = 0)
+    const long long base = wide ? 0 : pb;
+    auto clampi = [](long long v) { return (int)std::max(std::min(v, (long long)INT_MAX), (long long)INT_MIN); };
+    const int lowrel = clampi((long long)LOWEST - base);
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-    if (tt < a.T) sag[tt] = make_int2((int)an, (int)std::max(std::min(gc, (long long)INT_MAX), (long long)INT_MIN));
+    if (tt < a.T) sagp[tt] = make_int2((int)((unsigned int)an - (unsigned int)base), clampi(gc - base));
     __syncthreads();
     if (a.zn > 0) {  // the previous scan's chunk sums, consumed: zeroed for the scan after this one
-        const int z0 = (p0 / PPB) * a.zper, z1 = min((int)a.zn, z0 + a.zper);
+        const int z0 = p0 * a.zper, z1 = min((int)a.zn, z0 + a.zper);
         for (int i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
     }
-#pragma unroll
-    for (int q = 0; q < PPB; q++) {
-        if (p0 + q >= a.npages) break;
-        if (q > 0) {
-            __syncthreads();  // the previous page's epilogue has read hist
-            for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-            __syncthreads();
-        }
-        hist_count(a, p0 + q, pv[q], mv[q], sag, hist, hist + C * HK);
-    }
+    if (wide) hist_count<false>(a, p, pv, mv, sagp, lowrel, hist, hist + C * HK);
+    else hist_count<true>(a, p, pv, mv, sagp, lowrel, hist, hist + C * HK);
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
@@ -3140,7 +3153,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         h->csum_used[par ^ 1] = 0;
         h->csum_par = par ^ 1;
     }
-    const int ppb = (h->hist_ppb == 2 && T <= 8) ? 2 : 1;  // pages per pass-1 workgroup
+    const int ppb = 1;  // pages per pass-1 workgroup
     const int npb = (np + ppb - 1) / ppb;
     ha.zper = npb > 0 ? (int)((ha.zn + npb - 1) / npb) : 0;
     const int grid = nprep + (scan ? npb : 0);
@@ -3149,8 +3162,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0,
                                       scan ? sizeof(unsigned int) * (HK * C + 4 * SPEC_CAP) : 0);
         stage_begin(h, "hist", &ev);
-        auto kph = ppb == 2 ? (T <= 4 ? k_prep_hist<4, 2> : k_prep_hist<8, 2>)
-                            : T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
+        auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
         if (h->hist_diag && scan) {  // diagnostic: extra passes 1 (no epilogue) with parts skipped, before the real one
             HistArgs hd = ha;
             hd.diag = (h->hist_diag & 0xff) | 2;
