@@ -299,6 +299,7 @@ struct adlbq_server {
     int chain_passes = 0;              // round 0's in-launch passes, 0 = auto (adlbq_set_param "chain_passes")
     int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
     int put_match_block = 1, put_always_match = 0;  // diagnostics ("put_match_block", "put_always_match")
+    int hist_variant = 0;              // pass 1: 0 the round-2 loop, 1 the rebased loop ("hist_variant")
     int select_chunk = 0;              // pass 2: one workgroup per chunk of CHUNK pages (T <= 8) ("select_chunk")
     int hist_ppb = 1;                  // pass-1 pages per workgroup, 1 or 2 (T <= 8) ("hist_ppb")
     int hist_diag = 0;                 // diagnostic ("hist_diag"): parts of pass 1 skipped (wrong results)

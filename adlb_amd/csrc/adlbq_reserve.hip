@@ -181,7 +181,8 @@ struct HistArgs {
     int diag;                  // diagnostic ("hist_diag", wrong results): bit 0 no lists, 1 no epilogue, 2 no counts
     unsigned int *zcs;         // the other chunk-sum buffer (the previous scan's): zeroed here, a slice per workgroup
     long long zn;
-    int zper;                  // entries of zcs each workgroup zeroes
+    int zper;                  // (unused: k_thresholds zeroes the other buffer)
+    int variant;               // "hist_variant": 0 the round-2 loop, 1 the rebased one
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
 };
 
@@ -362,12 +363,75 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsi
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
     if (tt < a.T) sagp[tt] = make_int2((int)((unsigned int)an - (unsigned int)base), clampi(gc - base));
     __syncthreads();
-    if (a.zn > 0) {  // the previous scan's chunk sums, consumed: zeroed for the scan after this one
-        const int z0 = p0 * a.zper, z1 = min((int)a.zn, z0 + a.zper);
-        for (int i = z0 + threadIdx.x; i < z1; i += blockDim.x) a.zcs[i] = 0u;
-    }
     if (wide) hist_count<false>(a, p, pv, mv, sagp, lowrel, hist, hist + C * HK);
     else hist_count<true>(a, p, pv, mv, sagp, lowrel, hist, hist + C * HK);
+}
+
+// Pass 1, variant 0 ("hist_variant" 0): the round-2 form (per-unit anchor /
+// cut from LDS, list stores in the loop); kept beside the rebased form below
+// for measurement.
+__device__ __forceinline__ void hist_page_v0(const HistArgs &a, const int p, unsigned int *__restrict__ hist /* [C][HK] */) {
+    __shared__ int2 sag[ADLBQ_MAX_TYPES];
+    const int *__restrict__ prio = a.prio;
+    const uint32_t *__restrict__ meta = a.meta;
+    const int T = a.T, npages = a.npages, tail_fill = a.tail_fill;
+    const long long *__restrict__ anchor = a.anchor;
+    unsigned short *__restrict__ gh = a.gh;
+    unsigned int *__restrict__ csum = a.csum;
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int fill = (p == npages - 1) ? tail_fill : PAGE;
+    int4 pv[4];
+    uint4 mv[4];
+    load_quarter(prio, meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p], fill, w, pv, mv);
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        sag[t] = make_int2((int)anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
+    }
+    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
+    unsigned int *my = hist + (lane % HK);
+    unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
+    const unsigned long long lt = lanemask_lt();
+    int sn = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
+        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+        int col[4];
+        bool in[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
+            const int t = mm[q] & M_TYPE;
+            const int2 ag = sag[t];
+            col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
+            in[q] = av && pr[q] >= ag.y;
+            if (av) atomicAdd(&my[col[q] * HK], 1u);
+        }
+        const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
+                                 b3 = __ballot(in[3]);
+        if (!(b0 | b1 | b2 | b3)) continue;
+        int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (in[q]) {
+                if (pos < SPEC_CAP)
+                    sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+                pos++;
+            }
+        }
+        sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+    }
+    if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
+    __syncthreads();
+    unsigned int *cs = csum + (long long)(p / CHUNK) * C;
+    unsigned short *g = gh + (long long)p * C;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        unsigned int v = 0;
+#pragma unroll
+        for (int k = 0; k < HK; k++) v += hist[c * HK + k];
+        g[c] = (unsigned short)v;
+        if (v) atomicAdd(&cs[c], v);
+    }
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
@@ -379,6 +443,7 @@ __global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistA
     static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
     extern __shared__ unsigned int lds[];
     if ((int)blockIdx.x < nprep) prep_block<TB>(pa, blockIdx.x, reinterpret_cast<int *>(lds));
+    else if (ha.variant == 0) hist_page_v0(ha, blockIdx.x - nprep, lds);
     else hist_pages<PPB>(ha, (blockIdx.x - nprep) * PPB, lds);
 }
 
@@ -398,7 +463,7 @@ __device__ __forceinline__ long long cut_of(int th, long long an) {
 // demand is reached and how many units of it are needed.  Candidate list
 // offsets (the prefix of candlen over types) follow in k_select_open.
 constexpr int TH_THREADS = 256;  // chunks per step of the column scan
-__global__ __launch_bounds__(TH_THREADS) void k_thresholds(int T, const int *__restrict__ dem, unsigned int *csum,
+__global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, long long zn, int T, const int *__restrict__ dem, unsigned int *csum,
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
                                                      int *type_cnt, const long long *__restrict__ anchor,
@@ -444,6 +509,11 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(int T, const int *__r
         __hip_atomic_store(coltot + c, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         s_last = atomicAdd(&type_cnt[t], 1) == NB - 1;
+    }
+    // the previous scan's chunk sums (consumed): zeroed for the scan after this one, a slice per workgroup
+    if (zn > 0) {
+        const long long per = (zn + gridDim.x - 1) / gridDim.x, z0 = (long long)blockIdx.x * per;
+        for (long long i = z0 + threadIdx.x; i < min(zn, z0 + per); i += TH_THREADS) zcs[i] = 0u;
     }
     __syncthreads();
     if (!s_last || threadIdx.x >= 64) return;
@@ -3147,7 +3217,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     unsigned int *csum = h->d_csum + (long long)par * h->cap_csum, *zcs = h->d_csum + (long long)(par ^ 1) * h->cap_csum;
     HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
                       h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0, zcs, h->csum_used[par ^ 1],
-                      0, pg0};
+                      0, h->hist_variant, pg0};
     if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
         h->csum_used[par] = (long long)((np + CHUNK - 1) / CHUNK) * C;
         h->csum_used[par ^ 1] = 0;
@@ -3180,7 +3250,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     if (scan) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
         stage_begin(h, "thresholds", &ev);
-        k_thresholds<<<C, TH_THREADS, 0, s>>>(T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
+        k_thresholds<<<C, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                        h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor,
                                        h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0);
         stage_end(h, "thresholds", ev);

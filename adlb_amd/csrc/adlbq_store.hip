@@ -2085,6 +2085,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->tdel_max = value;
         return ADLBQ_OK;
     }
+    if (n == "hist_variant") {
+        h->hist_variant = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "select_chunk") {
         h->select_chunk = value ? 1 : 0;
         return ADLBQ_OK;
