@@ -11,4 +11,4 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 2
 rc=$?
 tail -3 $O/parity.log
 if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/parity.log | head -30; exit 1; fi
-VARIANTS_FILE=tools/var_s6.txt bash tools/gpu_r3_prof.sh s6 || exit 1
+VARIANTS_FILE=${VF:-tools/var_s6.txt} bash tools/gpu_r3_prof.sh s6 || exit 1
