@@ -1884,13 +1884,22 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * SORT_BLK,
                   "sort_type's LDS fits in span");
     __shared__ unsigned long long s_first, s_last, s_sortmask;
-    __shared__ int s_a0[4], s_len[4], s_tk;
+    __shared__ int s_a0[4], s_len[4], s_tk, s_fast;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (rs.fail_test && blockIdx.x == 0 && tid == 0) atomicAdd(rs.sync + ADLBQ_MAX_TYPES + 1, 1);
+    // every input of the prologue in one round of loads: list offsets / lengths,
+    // the sort flags, the fast-ranking flag k_select_open left
+    if (tid <= T) soff[tid] = candoff[tid];
     if (tid < 64) {
-        const bool ns = tid < T && rs.needsort[tid] == 1 && candlen[tid] > 1;  // 2: already sorted
-        const unsigned long long m = __ballot(ns);
-        if (tid == 0) s_sortmask = m;
+        const int len = tid < T ? candlen[tid] : 0;
+        const int ns = tid < T ? rs.needsort[tid] : 0;
+        if (tid < T) slen[tid] = len;
+        const int fast = tid == 0 ? ctr->rank_fast : 0;
+        const unsigned long long m = __ballot(ns == 1 && len > 1);  // 2: already sorted
+        if (tid == 0) {
+            s_sortmask = m;
+            s_fast = fast;
+        }
     }
     // the scan's chunk sums are consumed (k_select_open): leave them zeroed for the next batch
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < ncsum; i += (long long)gridDim.x * blockDim.x)
@@ -1906,14 +1915,16 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
             s_tk = tk;
         }
         __syncthreads();
-        const int tk = s_tk;
-        if (tk < nsort) {
-            unsigned long long mm = sortmask;  // the tk-th type that needs sorting
-            for (int q = 0; q < tk; q++) mm &= mm - 1;
+        // the block with ticket tk sorts the tk-th, (tk + grid)-th, ... type that needs it:
+        // the first blocks to run take the work, and a grid smaller than the sort count
+        // (the small grid of a rank hint) still sorts every list
+        for (int q = s_tk; q < nsort; q += gridDim.x) {
+            unsigned long long mm = sortmask;
+            for (int r = 0; r < q; r++) mm &= mm - 1;
             const int t = __ffsll((long long)mm) - 1;
             unsigned long long *sk = &span[0][0];
             int *ss = reinterpret_cast<int *>(sk + SORT_BLK);
-            sort_type(candoff[t], candlen[t], ckey, rs.cslot, rs.ckey2, rs.cslot2, sk, ss);
+            sort_type(soff[t], slen[t], ckey, rs.cslot, rs.ckey2, rs.cslot2, sk, ss);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (tid == 0) {
@@ -1940,11 +1951,6 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         }
         __syncthreads();
     }
-    for (int t = tid; t <= T; t += blockDim.x) {
-        soff[t] = candoff[t];
-        if (t < T) slen[t] = candlen[t];
-    }
-    __syncthreads();
     {
         // the chain's level guess counts the requests that take an untargeted
         // unit: drop those whose types have no candidate at all (prep_block
@@ -1975,7 +1981,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         stile[T] = acc;
     }
     __syncthreads();
-    if (ctr->rank_fast) {  // k_select_open ranked the candidates and wrote the level rows
+    if (s_fast) {  // k_select_open ranked the candidates and wrote the level rows
         if (blockIdx.x == 0 && sgv.sg != nullptr)
             seg_guesses(sgv, T, soff, slen, seg_cnt, R, lr, reinterpret_cast<int *>(&span[0][0]),
                         (int)(sizeof(span) / sizeof(int)));
@@ -2447,7 +2453,7 @@ __device__ __forceinline__ int seg_solve(const ChainArgs a, int s, int jb, int m
 constexpr unsigned long long CNT20 = (1ull << 20) - 1;
 
 template <int TB>
-__device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, int dv, int solved, int bad, int rounds,
+__device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, int dv, int solved, int bad, int rounds,
                                              int round, int passes, bool final, bool prefix, unsigned int *win) {
     const int lane = threadIdx.x, T = a.T, nseg = a.nseg;
     if (lane < T) {
@@ -2466,7 +2472,7 @@ __device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, i
         v = atomicAdd(&a.counters[g], mine) + mine;
         last = (int)(v & CNT20) == gn;
     }
-    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    if (!__builtin_amdgcn_readfirstlane(last)) return false;
     chain_stamp(a, s, 6);
     // the group's last arriver: local exclusive prefix of the deltas, and the group total
     if (prefix && lane < T) {
@@ -2491,7 +2497,7 @@ __device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, i
         tot = atomicAdd(&a.counters[CH_GROUPS], up) + up;
         last = (int)(tot & CNT20) == ng;
     }
-    if (!__builtin_amdgcn_readfirstlane(last)) return;
+    if (!__builtin_amdgcn_readfirstlane(last)) return false;
     chain_stamp(a, s, 7);
     // ---- the last arriver of the launch
     if (prefix && lane < T) {
@@ -2523,7 +2529,7 @@ __device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, i
             a.ctr->chain_recomputed += nsolved;
         }
     }
-    if (!final || clean) return;
+    if (!final || clean) return true;
     const int my_off = lane <= T ? ld_sc1(a.candoff + lane) : 0, my_len = lane < T ? ld_sc1(a.candlen + lane) : 0;
     // ---- walk: every segment before the first inconsistent one (start !=
     // predecessor's end) is exact; from there on, in order, re-solve each
@@ -2571,6 +2577,7 @@ __device__ __forceinline__ void chain_arrive(const ChainArgs a, int s, int sv, i
         a.ctr->chain_fallback = redo;
         atomicAdd(&a.ctr->chain_rounds, rounds_w);
     }
+    return true;
 }
 
 // In-launch neighbour passes of round 0 (T <= 64 ints per hand-off), following
@@ -2611,121 +2618,6 @@ struct ChainPass {
     unsigned int epoch;  // per batch, never 0
     int passes;          // in-launch passes, 1 .. CHAIN_MAX_PASSES (1: round 0 alone)
 };
-
-// Round 0: every segment from its level guess (lane t = type t's head), then
-// passes 2 .. P in the same launch: segment s waits for segment s-1's end of
-// the previous pass and re-solves (seeded) only if it differs from its own
-// start; finally each segment checks its start against its predecessor's last
-// end.  A launch in which every check holds is the fixed point.
-template <int TB>
-__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final) {
-    extern __shared__ unsigned int win[];
-    const int lane = threadIdx.x, T = a.T, s = blockIdx.x, nseg = a.nseg, P = cp.passes;
-    chain_stamp(a, s, 0);
-    if (s == 0 && lane == 0) *a.clean = 0;
-    if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
-    int rounds = 0;
-    const int jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
-    // the type masks of [jb, segment end) in flight with the guess's loads (T <= 8: staged in LDS)
-    constexpr int NRB = TB <= 8 ? (SEG + CHAIN_WARM) / 64 : 1;
-    unsigned long long mk[NRB];
-    int tm[NRB];
-    const int j1 = min(a.R, s * SEG + SEG);
-    if constexpr (TB <= 8) {
-#pragma unroll
-        for (int i = 0; i < NRB; i++) {
-            const int j = jb + i * 64 + lane;
-            const bool ok = j < j1;
-            mk[i] = ok ? a.mask[j] : 0ull;
-            tm[i] = ok ? a.tmatch[j] : 0;
-        }
-    }
-    // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
-    const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
-    // k_rank's guess for this segment, when it made them (one load instead of the three dependent ones below)
-    const bool sg_ok = a.sg != nullptr && a.lv != nullptr && a.sg[0] == (int)a.sg_epoch;
-    const int sg_v = (a.sg != nullptr && lane < T) ? a.sg[1 + s * T + lane] : 0;
-    int J = 0;  // requests before jb that take an untargeted unit
-    if (!sg_ok) {
-        const int nq = jb >> 6;
-        int cv[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) cv[u] = u * 64 + lane < nq ? a.seg_cnt[u * 64 + lane] : 0;
-#pragma unroll
-        for (int u = 0; u < 16; u++) J += cv[u];
-        for (int q = 1024 + lane; q < nq; q += 64) J += a.seg_cnt[q];  // batches above 65,536 Reserves
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
-    int guess;
-    if (sg_ok) {
-        guess = sg_v;
-    } else if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
-        const int G = __builtin_amdgcn_readlane(my_off, T);
-        // the row at the sampled rank below J, the rest spread in proportion to the list lengths
-        const int Js = J & ~(LV_STEP - 1);
-        // ranks [Js, J): one type byte per lane, counted per type (LV_STEP == 64)
-        const int tt = (Js + lane < J && Js + lane < G) ? (int)a.rtype[Js + lane] : 255;
-        int extra = 0;
-#pragma unroll
-        for (int q = 0; q < (TB <= 8 ? TB : 8); q++) {
-            const int c = __popcll(__ballot(tt == q));
-            if (lane == q) extra = c;
-        }
-        guess = lane >= T || J == 0 ? 0
-                : J >= G            ? my_len
-                                    : min(my_len, (Js ? a.lv[(long long)(Js / LV_STEP) * T + lane] : 0) + extra);
-    } else {
-        guess = level_guess<(TB <= 8 ? TB : 8)>(a, J);
-    }
-    if constexpr (TB <= 8) {
-        unsigned long long *smk = staged_masks<TB>(a, win);
-#pragma unroll
-        for (int i = 0; i < NRB; i++)
-            if (jb + i * 64 < j1) smk[i * 64 + lane] = tm[i] < 0 ? mk[i] : 0ull;
-    }
-    chain_stamp(a, s, 1);
-    int start;
-    int end = seg_solve<TB>(a, s, jb, guess, win, false, TB > 8, 0, my_off, my_len, start, rounds);
-    chain_stamp(a, s, 2);
-    int solves = 0, timeouts = 0;
-    auto E = [&](int k, int q) { return cp.E + ((long long)k * nseg + q) * T; };
-    auto F = [&](int k, int q) { return cp.flags + (long long)k * nseg + q; };
-    publish_state(E(0, s), F(0, s), cp.epoch, end, T);
-    for (int k = 1; k < P; k++) {
-        if (s > 0) {
-            if (wait_flag(F(k - 1, s - 1), cp.epoch)) {
-                const int pe = lane < T ? ld_sc1(E(k - 1, s - 1) + lane) : 0;
-                if (__ballot(lane < T && pe != start)) {
-                    int rec;
-                    __builtin_amdgcn_wave_barrier();  // win is refilled
-                    end = seg_solve<TB>(a, s, s * SEG, pe, win, true, TB > 8, s * SEG - jb, my_off, my_len, rec, rounds);
-                    start = pe;
-                    solves++;
-                }
-            } else {
-                timeouts++;
-            }
-        }
-        publish_state(E(k, s), F(k, s), cp.epoch, end, T);
-    }
-    chain_stamp(a, s, 3);
-    // own check: the final start against the predecessor's final end
-    int bad = 0;
-    if (s > 0) {
-        if (wait_flag(F(P - 1, s - 1), cp.epoch)) {
-            const int pe = lane < T ? ld_sc1(E(P - 1, s - 1) + lane) : 0;
-            bad = __ballot(lane < T && pe != start) ? 1 : 0;
-        } else {
-            timeouts++;
-            bad = 1;  // unknown: a later round or the walk looks
-        }
-    }
-    if (timeouts && lane == 0) atomicAdd(&a.ctr->chain_timeouts, timeouts);
-    chain_stamp(a, s, 4);
-    chain_arrive<TB>(a, s, start, end - start, solves, bad, rounds, 0, P, final != 0, prefix_next != 0, win);
-    chain_stamp(a, s, 5);
-}
 
 // Round k >= 1: a segment re-solves when its start differs from the estimate
 // of its exact start, seeded with its previous choices.  mode 0 (neighbour):
@@ -2952,116 +2844,376 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     }
 }
 
-__global__ __launch_bounds__(256) void k_finalize(const int *__restrict__ reqs, int R, const int *__restrict__ tmatch,
-                                                  const int *__restrict__ umatch, const int *__restrict__ cslot,
-                                                  const int *__restrict__ prio,
-                                                  uint32_t *meta, int *pin, const int *__restrict__ seqa,
-                                                  const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
-                                                  int my_world, int *__restrict__ resp, DevCounters *ctr,
-                                                  DonorCtx dc, int donors, int *rq_rank, int *rq_types,
-                                                  int *rq_live, int *rq_req, int *rq_seq, int *dem, int T,
-                                                  DevCounters *snap, unsigned long long snap_tag,
-                                                  long long *anchor, long long *anchor_next,
-                                                  unsigned long long *pmask, long long *gcut, long long *gcut_next,
-                                                  const int4 *__restrict__ rrec, const int *__restrict__ needsort,
-                                                  int *sortfail) {
+struct FinArgs {
+    const int *reqs;
+    int R;
+    const int *tmatch, *umatch, *cslot;
+    uint32_t *meta;
+    int *pin;
+    int my_world;
+    int *resp;
+    DevCounters *ctr;
+    DonorCtx dc;
+    int donors;
+    int *rq_rank, *rq_types, *rq_live, *rq_req, *rq_seq, *dem;
+    int T;
+    DevCounters *snap;
+    unsigned long long snap_tag;
+    long long *anchor, *anchor_next;
+    unsigned long long *pmask;
+    long long *gcut, *gcut_next;
+    const int4 *rrec;
+    const int *needsort;
+    int *sortfail;
+    int *done;  // fused into k_chain0: [0] = the chain epoch once the choices are final
+};
+
+// k_rank gave up waiting for an in-launch candidate sort: the lists may be
+// out of order, so the batch is answered ADLB_ERROR (nothing pinned, nothing
+// parked) instead of with possibly wrong matches
+__device__ __forceinline__ bool fin_failed(const FinArgs &f) {
+    return __hip_atomic_load(f.sortfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+// Request j (j < R): pin its unit and write its response; true when it parks
+// (words [10], [11] are then left to the park tail).
+__device__ __forceinline__ bool fin_request(const FinArgs &f, int j, bool failed) {
+    const int *rq = f.reqs + (long long)ADLBQ_RESERVE_INTS * j;
+    const int rank = rq[0], hang = failed ? 0 : rq[1];
+    const int tm = f.tmatch[j], um = f.umatch[j];
+    const int slot = failed ? -1 : tm >= 0 ? tm : (um >= 0 ? f.cslot[um] : -1);
+    int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
+    if (failed) {
+        o[0] = -1;  // ADLB_ERROR
+    } else if (slot >= 0) {
+        f.pin[slot] = rank;  // adlb.c:1210-1212
+        if (rank >= 0) __hip_atomic_fetch_or(f.meta + slot, M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int4 c0 = f.rrec[2ll * slot], c1 = f.rrec[2ll * slot + 1];  // one 32 B record
+        o[0] = 1;
+        o[1] = c1.z;
+        o[2] = c1.w;
+        o[3] = c0.y;
+        o[4] = c0.x;
+        o[5] = c0.z;
+        o[6] = f.my_world;
+        o[7] = c0.w;
+        o[8] = c1.x;
+        o[9] = c1.y;
+    } else if (!hang) {
+        o[0] = -2;  // NO_CURR_WORK
+    }
+    const bool parks = slot < 0 && hang;
+    int *out = f.resp + (long long)ADLBQ_RESP_INTS * j;
+#pragma unroll
+    for (int i = 0; i < 10; i++) out[i] = o[i];
+    if (!parks) {
+        out[10] = -1;
+        out[11] = -1;
+    }
+    return parks;
+}
+
+// Two-level arrival of workgroup bid of nb (8 groups, then one top counter)
+// keeps every counter's atomics to about nb / 8; a count rides in the high
+// half.  One thread; returns (parked in the batch << 32) | 1 for the last.
+__device__ __forceinline__ unsigned long long fin_arrive(const FinArgs &f, int parked, unsigned int nb,
+                                                         unsigned int bid) {
+    const unsigned int g = bid & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
+    unsigned long long v = atomicAdd(&f.ctr->fin_group[g], ((unsigned long long)parked << 32) | 1ull);
+    if ((unsigned int)v == ng - 1u) {
+        const unsigned long long tg = (v >> 32) + (unsigned long long)parked;
+        const unsigned long long top = atomicAdd(&f.ctr->fin_top, (tg << 32) | 1ull);
+        if ((unsigned int)top == ngroups - 1u) return (((top >> 32) + tg) << 32) | 1ull;
+    }
+    return 0ull;
+}
+
+// The last workgroup of the batch (every thread of it): anchors and cuts for
+// the next scan, the parked Reserves, counters, then the counter snapshot.
+__device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool failed) {
+    const int T = f.T;
+    if ((int)threadIdx.x < T) {
+        f.dem[threadIdx.x] = 0;  // prep_block of the next batch accumulates into it
+        const long long a = f.anchor_next[threadIdx.x];
+        if (a != LLONG_MIN) {  // lower the anchor to the live maximum k_thresholds saw
+            f.anchor[threadIdx.x] = a;
+            f.anchor_next[threadIdx.x] = LLONG_MIN;
+        }
+        const long long g = f.gcut_next[threadIdx.x];
+        if (g != LLONG_MIN) {  // the next scan's pass-1 guess
+            f.gcut[threadIdx.x] = g;
+            f.gcut_next[threadIdx.x] = LLONG_MIN;
+        }
+    }
+    if (total > 0)
+        park_tail(f.dc, f.donors, f.reqs, f.R, f.pmask, f.rq_rank, f.rq_types, f.rq_live, f.rq_req, f.rq_seq, f.ctr,
+                  f.resp);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        DevCounters *ctr = f.ctr;
+        if (failed) {
+            ctr->batch_failed += 1;
+            __hip_atomic_store(f.sortfail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // per batch
+        }
+        if (total == 0) ctr->n_parked_last = 0;
+        int ns = 0;
+        for (int t = 0; t < T; t++) ns |= f.needsort[t];
+        ctr->needsort_last = ns;  // the host launches the segmented sort while this holds
+        for (int g = 0; g < 8; g++) ctr->fin_group[g] = 0;
+        ctr->fin_top = 0;
+        // mapped host memory: every field written back, then the tag the host waits for
+        *f.snap = *ctr;
+        __threadfence_system();
+        __hip_atomic_store(&f.snap->snap_tag, f.snap_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (threadIdx.x == 0) s_parked = 0;
-    // k_rank gave up waiting for an in-launch candidate sort: the lists may be
-    // out of order, so the batch is answered ADLB_ERROR (nothing pinned, nothing
-    // parked) instead of with possibly wrong matches
-    const bool failed = __hip_atomic_load(sortfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    const bool failed = fin_failed(f);
     __syncthreads();
-    if (j < R) {
-        const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * j;
-        const int rank = rq[0], hang = failed ? 0 : rq[1];
-        const int slot = failed ? -1 : tmatch[j] >= 0 ? tmatch[j] : (umatch[j] >= 0 ? cslot[umatch[j]] : -1);
-        int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
-        if (failed) {
-            o[0] = -1;  // ADLB_ERROR
-        } else if (slot >= 0) {
-            pin[slot] = rank;  // adlb.c:1210-1212
-            if (rank >= 0) __hip_atomic_fetch_or(meta + slot, M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int4 c0 = rrec[2ll * slot], c1 = rrec[2ll * slot + 1];  // one 32 B record
-            o[0] = 1;
-            o[1] = c1.z;
-            o[2] = c1.w;
-            o[3] = c0.y;
-            o[4] = c0.x;
-            o[5] = c0.z;
-            o[6] = my_world;
-            o[7] = c0.w;
-            o[8] = c1.x;
-            o[9] = c1.y;
-        } else if (!hang) {
-            o[0] = -2;  // NO_CURR_WORK
-        }
-        const bool parks = slot < 0 && hang;
-        int *out = resp + (long long)ADLBQ_RESP_INTS * j;
-#pragma unroll
-        for (int i = 0; i < 10; i++) out[i] = o[i];
-        if (!parks) {
-            out[10] = -1;
-            out[11] = -1;
-        }
+    if (j < f.R) {
+        const bool parks = fin_request(f, j, failed);
         const unsigned long long pb = __ballot(parks);
         if ((threadIdx.x & 63) == 0) {
             // published for the last workgroup's park (write-through, drained before the arrival below)
-            __hip_atomic_store(pmask + (j >> 6), pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(f.pmask + (j >> 6), pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (pb) atomicAdd(&s_parked, __popcll(pb));
             __builtin_amdgcn_s_waitcnt(0);  // this wave's store has landed before the block arrives
         }
     }
     __syncthreads();
-    // two-level arrival (8 groups, then one top counter) keeps every counter's
-    // atomics to about gridDim / 8; a count rides in the high half
-    if (threadIdx.x == 0) {
-        const unsigned int nb = gridDim.x, g = blockIdx.x & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
-        unsigned long long v = atomicAdd(&ctr->fin_group[g], ((unsigned long long)s_parked << 32) | 1ull);
-        s_ticket = 0;  // not last
-        if ((unsigned int)v == ng - 1u) {
-            const unsigned long long tg = (v >> 32) + (unsigned long long)s_parked;
-            const unsigned long long top = atomicAdd(&ctr->fin_top, (tg << 32) | 1ull);
-            if ((unsigned int)top == ngroups - 1u) s_ticket = (((top >> 32) + tg) << 32) | 1ull;
-        }
-    }
+    if (threadIdx.x == 0) s_ticket = fin_arrive(f, s_parked, gridDim.x, blockIdx.x);
     __syncthreads();
     if (!(s_ticket & 1ull)) return;
-    // the last workgroup of the batch
-    const int total = (int)(s_ticket >> 32);
-    if (threadIdx.x < T) {
-        dem[threadIdx.x] = 0;  // prep_block of the next batch accumulates into it
-        const long long a = anchor_next[threadIdx.x];
-        if (a != LLONG_MIN) {  // lower the anchor to the live maximum k_thresholds saw
-            anchor[threadIdx.x] = a;
-            anchor_next[threadIdx.x] = LLONG_MIN;
+    fin_tail(f, (int)(s_ticket >> 32), failed);
+}
+
+// k_finalize fused into the final k_chain0 launch (every segment one
+// workgroup, all of them resident: the host fuses only small grids).  The
+// launch's last arriver has the exact choices once its walk is done and
+// publishes the chain epoch; every other segment waits for it, then
+// finalizes its own SEG requests (their loads issued together, the three
+// dependent levels umatch -> cslot -> record one after the other), and the
+// last of those arrivals runs the batch tail.  The wait is bounded (one second
+// of wall clock): a segment that gives up answers ADLB_ERROR, never a guess.
+constexpr int FUSE_MAX_SEG = 512;                       // 131,072 Reserves
+constexpr long long FIN_WAIT_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
+__device__ __forceinline__ void fin_fused(const FinArgs &f, int s, bool last, unsigned int epoch) {
+    const int lane = threadIdx.x;
+    bool waited = true;
+    if (last) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the walk's choices have landed
+        if (lane == 0) st_sc1(f.done, (int)epoch);
+    } else {
+        int ok = 0;
+        if (lane == 0) {
+            const long long t0 = wall_clock64();
+            while (true) {
+                if (ld_sc1(f.done) == (int)epoch) {
+                    ok = 1;
+                    break;
+                }
+                if (wall_clock64() - t0 > FIN_WAIT_TICKS) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
         }
-        const long long g = gcut_next[threadIdx.x];
-        if (g != LLONG_MIN) {  // the next scan's pass-1 guess
-            gcut[threadIdx.x] = g;
-            gcut_next[threadIdx.x] = LLONG_MIN;
+        waited = __builtin_amdgcn_readfirstlane(ok) != 0;
+        if (!waited && lane == 0) atomicAdd(&f.ctr->chain_timeouts, 1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // other segments' choices: no stale L1 lines
+    const bool failed = !waited || fin_failed(f);
+    constexpr int U = SEG / 64;
+    const int j0 = s * SEG;
+    int rank[U], hang[U], tm[U], um[U], slot[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int j = j0 + u * 64 + lane;
+        const bool in = j < f.R;
+        const int *rq = f.reqs + (long long)ADLBQ_RESERVE_INTS * (in ? j : 0);
+        rank[u] = in ? rq[0] : 0;
+        hang[u] = in ? rq[1] : 0;
+        tm[u] = in ? f.tmatch[j] : -1;
+        um[u] = in ? f.umatch[j] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) slot[u] = failed ? -1 : tm[u] >= 0 ? tm[u] : (um[u] >= 0 ? f.cslot[um[u]] : -1);
+    int4 c0[U], c1[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        c0[u] = slot[u] >= 0 ? f.rrec[2ll * slot[u]] : make_int4(0, 0, 0, 0);
+        c1[u] = slot[u] >= 0 ? f.rrec[2ll * slot[u] + 1] : make_int4(0, 0, 0, 0);
+    }
+    int parked = 0;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const int j = j0 + u * 64 + lane;
+        if (j0 + u * 64 >= f.R) break;
+        bool parks = false;
+        if (j < f.R) {
+            const int sl = slot[u], hg = failed ? 0 : hang[u];
+            int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
+            if (failed) {
+                o[0] = -1;  // ADLB_ERROR
+            } else if (sl >= 0) {
+                f.pin[sl] = rank[u];  // adlb.c:1210-1212
+                if (rank[u] >= 0)
+                    __hip_atomic_fetch_or(f.meta + sl, M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                o[0] = 1;
+                o[1] = c1[u].z;
+                o[2] = c1[u].w;
+                o[3] = c0[u].y;
+                o[4] = c0[u].x;
+                o[5] = c0[u].z;
+                o[6] = f.my_world;
+                o[7] = c0[u].w;
+                o[8] = c1[u].x;
+                o[9] = c1[u].y;
+            } else if (!hg) {
+                o[0] = -2;  // NO_CURR_WORK
+            }
+            parks = sl < 0 && hg;
+            int *out = f.resp + (long long)ADLBQ_RESP_INTS * j;
+#pragma unroll
+            for (int i = 0; i < 10; i++) out[i] = o[i];
+            if (!parks) {
+                out[10] = -1;
+                out[11] = -1;
+            }
+        }
+        const unsigned long long pb = __ballot(parks);
+        if (lane == 0) __hip_atomic_store(f.pmask + ((j0 >> 6) + u), pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        parked += __popcll(pb);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // this segment's stores have landed before it arrives
+    unsigned long long tk = 0;
+    if (lane == 0) tk = fin_arrive(f, parked, gridDim.x, blockIdx.x);
+    const unsigned int lo = __builtin_amdgcn_readfirstlane((unsigned int)tk),
+                       hi = __builtin_amdgcn_readfirstlane((unsigned int)(tk >> 32));
+    if (!(lo & 1u)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    fin_tail(f, (int)hi, failed);
+}
+
+// Round 0: every segment from its level guess (lane t = type t's head), then
+// passes 2 .. P in the same launch: segment s waits for segment s-1's end of
+// the previous pass and re-solves (seeded) only if it differs from its own
+// start; finally each segment checks its start against its predecessor's last
+// end.  A launch in which every check holds is the fixed point.
+template <int TB>
+__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
+                                               int fuse) {
+    extern __shared__ unsigned int win[];
+    const int lane = threadIdx.x, T = a.T, s = blockIdx.x, nseg = a.nseg, P = cp.passes;
+    chain_stamp(a, s, 0);
+    if (s == 0 && lane == 0) *a.clean = 0;
+    if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
+    int rounds = 0;
+    const int jb = max(0, s * SEG - a.warm);  // a.warm is a multiple of SEG
+    // the type masks of [jb, segment end) in flight with the guess's loads (T <= 8: staged in LDS)
+    constexpr int NRB = TB <= 8 ? (SEG + CHAIN_WARM) / 64 : 1;
+    unsigned long long mk[NRB];
+    int tm[NRB];
+    const int j1 = min(a.R, s * SEG + SEG);
+    if constexpr (TB <= 8) {
+#pragma unroll
+        for (int i = 0; i < NRB; i++) {
+            const int j = jb + i * 64 + lane;
+            const bool ok = j < j1;
+            mk[i] = ok ? a.mask[j] : 0ull;
+            tm[i] = ok ? a.tmatch[j] : 0;
         }
     }
-    if (total > 0) park_tail(dc, donors, reqs, R, pmask, rq_rank, rq_types, rq_live, rq_req, rq_seq, ctr, resp);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (failed) {
-            ctr->batch_failed += 1;
-            __hip_atomic_store(sortfail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // per batch
-        }
-        if (total == 0) ctr->n_parked_last = 0;
-        int ns = 0;
-        for (int t = 0; t < T; t++) ns |= needsort[t];
-        ctr->needsort_last = ns;  // the host launches the segmented sort while this holds
-        for (int g = 0; g < 8; g++) ctr->fin_group[g] = 0;
-        ctr->fin_top = 0;
-        // mapped host memory: every field written back, then the tag the host waits for
-        *snap = *ctr;
-        __threadfence_system();
-        __hip_atomic_store(&snap->snap_tag, snap_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
+    const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
+    // k_rank's guess for this segment, when it made them (one load instead of the three dependent ones below)
+    const bool sg_ok = a.sg != nullptr && a.lv != nullptr && a.sg[0] == (int)a.sg_epoch;
+    const int sg_v = (a.sg != nullptr && lane < T) ? a.sg[1 + s * T + lane] : 0;
+    int J = 0;  // requests before jb that take an untargeted unit
+    if (!sg_ok) {
+        const int nq = jb >> 6;
+        int cv[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) cv[u] = u * 64 + lane < nq ? a.seg_cnt[u * 64 + lane] : 0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) J += cv[u];
+        for (int q = 1024 + lane; q < nq; q += 64) J += a.seg_cnt[q];  // batches above 65,536 Reserves
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
+    int guess;
+    if (sg_ok) {
+        guess = sg_v;
+    } else if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
+        const int G = __builtin_amdgcn_readlane(my_off, T);
+        // the row at the sampled rank below J, the rest spread in proportion to the list lengths
+        const int Js = J & ~(LV_STEP - 1);
+        // ranks [Js, J): one type byte per lane, counted per type (LV_STEP == 64)
+        const int tt = (Js + lane < J && Js + lane < G) ? (int)a.rtype[Js + lane] : 255;
+        int extra = 0;
+#pragma unroll
+        for (int q = 0; q < (TB <= 8 ? TB : 8); q++) {
+            const int c = __popcll(__ballot(tt == q));
+            if (lane == q) extra = c;
+        }
+        guess = lane >= T || J == 0 ? 0
+                : J >= G            ? my_len
+                                    : min(my_len, (Js ? a.lv[(long long)(Js / LV_STEP) * T + lane] : 0) + extra);
+    } else {
+        guess = level_guess<(TB <= 8 ? TB : 8)>(a, J);
+    }
+    if constexpr (TB <= 8) {
+        unsigned long long *smk = staged_masks<TB>(a, win);
+#pragma unroll
+        for (int i = 0; i < NRB; i++)
+            if (jb + i * 64 < j1) smk[i * 64 + lane] = tm[i] < 0 ? mk[i] : 0ull;
+    }
+    chain_stamp(a, s, 1);
+    int start;
+    int end = seg_solve<TB>(a, s, jb, guess, win, false, TB > 8, 0, my_off, my_len, start, rounds);
+    chain_stamp(a, s, 2);
+    int solves = 0, timeouts = 0;
+    auto E = [&](int k, int q) { return cp.E + ((long long)k * nseg + q) * T; };
+    auto F = [&](int k, int q) { return cp.flags + (long long)k * nseg + q; };
+    publish_state(E(0, s), F(0, s), cp.epoch, end, T);
+    for (int k = 1; k < P; k++) {
+        if (s > 0) {
+            if (wait_flag(F(k - 1, s - 1), cp.epoch)) {
+                const int pe = lane < T ? ld_sc1(E(k - 1, s - 1) + lane) : 0;
+                if (__ballot(lane < T && pe != start)) {
+                    int rec;
+                    __builtin_amdgcn_wave_barrier();  // win is refilled
+                    end = seg_solve<TB>(a, s, s * SEG, pe, win, true, TB > 8, s * SEG - jb, my_off, my_len, rec, rounds);
+                    start = pe;
+                    solves++;
+                }
+            } else {
+                timeouts++;
+            }
+        }
+        publish_state(E(k, s), F(k, s), cp.epoch, end, T);
+    }
+    chain_stamp(a, s, 3);
+    // own check: the final start against the predecessor's final end
+    int bad = 0;
+    if (s > 0) {
+        if (wait_flag(F(P - 1, s - 1), cp.epoch)) {
+            const int pe = lane < T ? ld_sc1(E(P - 1, s - 1) + lane) : 0;
+            bad = __ballot(lane < T && pe != start) ? 1 : 0;
+        } else {
+            timeouts++;
+            bad = 1;  // unknown: a later round or the walk looks
+        }
+    }
+    if (timeouts && lane == 0) atomicAdd(&a.ctr->chain_timeouts, timeouts);
+    chain_stamp(a, s, 4);
+    const bool last = chain_arrive<TB>(a, s, start, end - start, solves, bad, rounds, 0, P, final != 0,
+                                       prefix_next != 0, win);
+    chain_stamp(a, s, 5);
+    if (fuse) fin_fused(f, s, last, cp.epoch);
 }
 
 // ---------------------------------------------------------------- steal export
@@ -3144,7 +3296,8 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMemsetAsync(h->d_chflag, 0, sizeof(int) * CHAIN_MAX_PASSES * nseg, h->stream));  // epochs start at 1
     AQ_HIP(hipMalloc((void **)&h->d_chGT, sizeof(int) * CH_GROUPS * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chGO, sizeof(int) * CH_GROUPS * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chclean, sizeof(int)));
+    AQ_HIP(hipMalloc((void **)&h->d_chclean, sizeof(int) * 2));  // [1]: the fused finalize's epoch flag
+    AQ_HIP(hipMemsetAsync(h->d_chclean, 0, sizeof(int) * 2, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_cht, (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * (CH_GROUPS + 1)));
     // the last arriver of every chain launch re-zeroes them
@@ -4199,12 +4352,22 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         const SegGuess sgv{(T <= 8 && h->seg_guess) ? h->d_sg : nullptr, (R + SEG - 1) / SEG, warm0, h->rank_epoch};
         // a small grid when the last landed batch was ranked in k_select_open (every loop is
         // grid-strided: any grid is correct, the hint only sizes it); chunk sums: zeroed by the next scan
-        k_rank<<<rank_hint(h) ? 4 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, nullptr,
+        k_rank<<<h->rank_grid ? h->rank_grid : rank_hint(h) ? 4 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, nullptr,
                                     0, h->d_mask, h->d_tmatch, R,
                                     h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr,
                                     sgv);
         stage_end(h, "rank", ev);
     }
+    // k_finalize's arguments (its own launch, or fused into the final k_chain0 launch)
+    DevCounters *const snap = h->d_snap + h->snap_next;
+    h->snap_tag[h->snap_next] = ++h->snap_tags;
+    __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);  // not landed until k_finalize stores it
+    const FinArgs fa{d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_meta, h->d_pin, h->my_world, d_resp,
+                     h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
+                     h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, T, snap, h->snap_tag[h->snap_next],
+                     h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
+                     h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1};
+    bool fused = false;
     stage_begin(h, "chain", &ev);
     {
         const int nseg = (R + SEG - 1) / SEG;
@@ -4249,9 +4412,12 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         else if (T <= 8) lds = sizeof(unsigned int) * (8 * (SEG + warm) + 64) + 9 * (SEG + warm);
         else lds = sizeof(unsigned int) * T * SEG + sizeof(TypeRec) * ADLBQ_MAX_TYPES;
         auto mode_of = [&](int k) { return (k >= 1 && k <= K) ? (int)(((unsigned long long)modes >> (k - 1)) & 1ull) : 0; };
-        if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
-        else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
-        else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
+        // the finalize rides in k_chain0 when that launch is the final one and its
+        // grid is small enough to be resident at once (each segment waits there)
+        fused = h->fuse_finalize && K == 0 && T <= 8 && nseg <= FUSE_MAX_SEG;
+        if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
+        else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
+        else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
         for (int k = 1; k <= K; k++) {
             flip(k);
             const int mode = mode_of(k), pn = mode_of(k + 1);
@@ -4262,20 +4428,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     stage_end(h, "chain", ev);
     stage_begin(h, "finalize", &ev);
-    {
-        const int donors = (h->S > 1 || !h->tq.empty()) ? 1 : 0;
-        DevCounters *snap = h->d_snap + h->snap_next;
-        h->snap_tag[h->snap_next] = ++h->snap_tags;
-        __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);  // not landed until k_finalize stores it
-        k_finalize<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_prio,
-                                                   h->d_meta, h->d_pin, h->d_seq, h->d_cold0, h->d_cold1,
-                                                   h->my_world, d_resp, h->d_ctr, donor_ctx(h), donors, h->d_rq_rank,
-                                                   h->d_rq_types, h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, T,
-                                                   snap, h->snap_tag[h->snap_next],
-                                                   h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut,
-                                                   h->d_gcut_next, h->d_rrec, h->d_needsort,
-                                                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1);
-    }
+    if (!fused) k_finalize<<<(R + 255) / 256, 256, 0, s>>>(fa);
     stage_end(h, "finalize", ev);
     // the lists hold export_extra more per type: a steal export right after this batch gathers them
     h->batch_export_k = (np > 0 && T > 0) ? h->export_extra : 0;

@@ -2164,6 +2164,16 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->segsort_merged = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "fuse_finalize") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "fuse_finalize must be 0 or 1");
+        h->fuse_finalize = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "rank_grid") {  // test: k_rank's grid (0: sized by the rank hint)
+        if (value < 0 || value > 4096) return fail(ADLBQ_ERR_ARG, "rank_grid must be in [0, 4096]");
+        h->rank_grid = (int)value;
+        return ADLBQ_OK;
+    }
     if (n == "segsort_wide") {
         if (value < 2 || value > (1ll << 30)) return fail(ADLBQ_ERR_ARG, "segsort_wide must be in [2, 2^30]");
         h->segsort_wide = (int)value;

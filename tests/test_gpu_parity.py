@@ -89,6 +89,7 @@ VARIANTS = {
     "hist_ppb2": {"hist_ppb": 2},          # pass 1: two pages per workgroup
     "no_seg_guess": {"seg_guess": 0},      # the chain finds its own start guesses
     "all": {"select_chunk": 1, "hist_ppb": 2},
+    "no_fuse": {"fuse_finalize": 0},       # k_finalize as its own launch
 }
 
 
@@ -102,6 +103,19 @@ def test_pipeline_variants_vs_oracle(gpu_available, name, variant):
     cfg = (w.num_app_ranks, 1, 0)
     assert_same(run_abi(w.user_types, cfg, tr, max_units=w.n_units, params=VARIANTS[variant]),
                 run_oracle(w.user_types, cfg, tr))
+
+
+@pytest.mark.parametrize("name", ["c4_n200k", "c2_t64_wide", "c4_t8_tied"])
+@pytest.mark.parametrize("grid", [1, 4])
+def test_rank_small_grid_sorts_every_list(gpu_available, name, grid):
+    """k_rank's in-launch list sort on a grid smaller than the number of lists to
+    sort (the small grid a rank hint picks): each workgroup takes every grid-th
+    list, so no sort wait is left hanging and the lists come out ordered."""
+    w = CASES[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units, params={"rank_grid": grid, "segsort_wide": 1 << 30})
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))

@@ -1,0 +1,14 @@
+#!/bin/bash
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/s8
+mkdir -p $O
+( while sleep 20; do echo "hb $(date +%s)" >> $O/heartbeat.txt; done ) &
+HB=$!
+trap "kill $HB" EXIT
+cd $R
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steal.py tests/test_gpu_robust.py -x -q --timeout 200 --timeout-method thread -k "golden or fresh or variants or depletion or full_size or small_grid or steal or robust or sort" > $O/parity.log 2>&1
+rc=$?
+tail -3 $O/parity.log
+if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/parity.log | head -30; exit 1; fi
+VARIANTS_FILE=${VF:-tools/var_s8.txt} bash tools/gpu_r3_prof.sh s8 || exit 1
