@@ -1959,16 +1959,25 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         for (int t = 0; t < T; t++) cm |= slen[t] > 0 ? (1ull << t) : 0ull;
         const unsigned long long all = T >= 64 ? ~0ull : ((1ull << T) - 1);
         if (cm != all) {
+            // eight groups of 64 per wave per step, their loads in flight together (a small grid
+            // walks the whole batch: 16 waves over 1,024 groups at 65,536 Reserves)
+            constexpr int DU = 8;
             const int waves = gridDim.x * (RANK_TILE / 64);
-            for (int g = blockIdx.x * (RANK_TILE / 64) + w; g * 64 < R; g += waves) {
-                const int j = g * 64 + lane;
-                bool drop = false;
-                if (j < R) {
-                    const unsigned long long m = mask[j];
-                    drop = m != 0ull && !(m & cm) && tmatch[j] < 0;
+            for (int g0 = blockIdx.x * (RANK_TILE / 64) + w; g0 * 64 < R; g0 += waves * DU) {
+                unsigned long long m[DU];
+                int tmv[DU];
+#pragma unroll
+                for (int i = 0; i < DU; i++) {
+                    const int j = (g0 + i * waves) * 64 + lane;
+                    m[i] = j < R ? mask[j] : 0ull;
+                    tmv[i] = j < R ? tmatch[j] : 0;
                 }
-                const unsigned long long b = __ballot(drop);
-                if (lane == 0 && b) atomicSub(&seg_cnt[g], __popcll(b));
+#pragma unroll
+                for (int i = 0; i < DU; i++) {
+                    const int g = g0 + i * waves;
+                    const unsigned long long b = __ballot(m[i] != 0ull && !(m[i] & cm) && tmv[i] < 0);
+                    if (lane == 0 && b) atomicSub(&seg_cnt[g], __popcll(b));
+                }
             }
         }
     }
@@ -4449,6 +4458,12 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
 // heads, in order), so the k best available units of type t are the list
 // entries from h_t on, h_t = the batch's choices of type t (cht); the available
 // count is the scan's column total less h_t.  Records as k_export_gather.
+__device__ __forceinline__ int bytes_eq(unsigned int x, unsigned int t) {
+    return ((x & 0xffu) == t) + (((x >> 8) & 0xffu) == t) + (((x >> 16) & 0xffu) == t) + ((x >> 24) == t);
+}
+
+// Grid (T, ceil(k / 256)): block (t, y) counts h_t itself (16 choice bytes per
+// load, four loads in flight) and gathers records [256 y, 256 y + 256) of type t.
 __global__ __launch_bounds__(256) void k_export_after(int T, int k, int R, const unsigned char *__restrict__ cht,
                                                       const int *__restrict__ candoff, const int *__restrict__ candlen,
                                                       const int *__restrict__ cslot, const int *__restrict__ prio,
@@ -4457,35 +4472,48 @@ __global__ __launch_bounds__(256) void k_export_after(int T, int k, int R, const
                                                       int *__restrict__ nrec, long long *__restrict__ navail,
                                                       const unsigned int *__restrict__ coltot) {
     __shared__ int s_h[4];
-    const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int t = blockIdx.x, y = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned int ut = (unsigned int)t;
+    const uint4 *cv = reinterpret_cast<const uint4 *>(cht);
+    const int nv = R >> 4;
     int c = 0;
-    for (int j = threadIdx.x; j < R; j += blockDim.x) c += cht[j] == t;
+    for (int q0 = threadIdx.x; q0 < nv; q0 += 4 * blockDim.x) {
+        uint4 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int q = q0 + i * blockDim.x;
+            v[i] = q < nv ? cv[q] : make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) c += bytes_eq(v[i].x, ut) + bytes_eq(v[i].y, ut) + bytes_eq(v[i].z, ut) + bytes_eq(v[i].w, ut);
+    }
+    for (int j = (nv << 4) + threadIdx.x; j < R; j += blockDim.x) c += cht[j] == t;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     if (lane == 0) s_h[w] = c;
     __syncthreads();
     const int ht = s_h[0] + s_h[1] + s_h[2] + s_h[3];
-    if (threadIdx.x < 64) {
+    if (y == 0 && threadIdx.x < 64) {
         unsigned long long a = coltot[t * NB + threadIdx.x];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
         if (threadIdx.x == 0) navail[t] = (long long)a - ht;
     }
     const int n = max(0, min(k, candlen[t] - ht)), off = candoff[t] + ht;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    for (int i = y * blockDim.x + threadIdx.x; i < n; i += gridDim.y * blockDim.x) {
         const int slot = cslot[off + i];
         const int4 c0 = cold0[slot], c1 = cold1[slot];
         int4 *r = reinterpret_cast<int4 *>(recs + ((long long)t * k + i) * 8);
         r[0] = make_int4(prio[slot], seqa[slot], c1.z, c0.y);
         r[1] = make_int4(c0.x, c0.w, c1.x, c1.y);
     }
-    if (threadIdx.x == 0) nrec[t] = n;
+    if (y == 0 && threadIdx.x == 0) nrec[t] = n;
 }
 
 // true (and the gather enqueued) when the last reserve batch's lists serve an export of depth k
 bool launch_export_after(adlbq_server *h, int k, int *d_recs, int *d_nrec, long long *d_navail) {
     if (h->batch_export_k < k || h->T < 1) return false;
-    k_export_after<<<h->T, 256, 0, h->stream>>>(h->T, k, h->batch_export_R, h->d_cht, h->d_candoff, h->d_candlen,
+    k_export_after<<<dim3(h->T, std::min(8, std::max(1, (k + 255) / 256))), 256, 0, h->stream>>>(h->T, k, h->batch_export_R, h->d_cht, h->d_candoff, h->d_candlen,
                                                 h->d_cslot, h->d_prio, h->d_seq, h->d_cold0, h->d_cold1, d_recs,
                                                 d_nrec, d_navail, h->d_coltot);
     return true;

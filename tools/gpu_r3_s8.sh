@@ -12,3 +12,8 @@ rc=$?
 tail -3 $O/parity.log
 if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/parity.log | head -30; exit 1; fi
 VARIANTS_FILE=${VF:-tools/var_s8.txt} bash tools/gpu_r3_prof.sh s8 || exit 1
+cd $R
+timeout -k 10 300 python3 bench.py --config3-only --no-pmc --no-cpu > $O/c3.json 2> $O/c3.err || { echo c3 failed; tail -5 $O/c3.err; exit 1; }
+python3 -c "import json;d=json.loads(open('$O/c3.json').read().strip().splitlines()[-1])['config3'];print('c3 ms',d['ms_per_step'],'parity',d.get('parity'))"
+timeout -k 10 300 python3 bench.py --config3-only --no-pmc --no-cpu --c3-parts > $O/c3p.json 2> $O/c3p.err || { echo c3p failed; exit 1; }
+python3 -c "import json;d=json.loads(open('$O/c3p.json').read().strip().splitlines()[-1])['config3'];print('c3 parts',d['parts_ms_per_step'])"
