@@ -3015,7 +3015,9 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, int s, bool last, un
     const int lane = threadIdx.x;
     bool waited = true;
     if (last) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the walk's choices have landed
+        // the walk's choices (plain stores) and counters written back from this XCD's L2:
+        // segments finalized on the other XCDs read them after their acquire below
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         if (lane == 0) st_sc1(f.done, (int)epoch);
     } else {
         int ok = 0;
@@ -3033,7 +3035,7 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, int s, bool last, un
         waited = __builtin_amdgcn_readfirstlane(ok) != 0;
         if (!waited && lane == 0) atomicAdd(&f.ctr->chain_timeouts, 1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // other segments' choices: no stale L1 lines
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the walk's choices: no stale L1 / L2 lines
     const bool failed = !waited || fin_failed(f);
     constexpr int U = SEG / 64;
     const int j0 = s * SEG;

@@ -7,7 +7,7 @@ mkdir -p $O
 HB=$!
 trap "kill $HB" EXIT
 cd $R
-timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steal.py tests/test_gpu_robust.py -x -q --timeout 200 --timeout-method thread -k "golden or fresh or variants or depletion or full_size or small_grid or steal or robust or sort" > $O/parity.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_steal.py tests/test_gpu_robust.py -x -q --timeout 200 --timeout-method thread -k "golden or fresh or variants or depletion or full_size or small_grid or steal or robust or sort or fixup" > $O/parity.log 2>&1
 rc=$?
 tail -3 $O/parity.log
 if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/parity.log | head -30; exit 1; fi
