@@ -2122,6 +2122,8 @@ struct ChainArgs {
     unsigned long long *stamps;      // [nseg][8] s_memrealtime per phase (diagnostic build of the run), or nullptr
     const int *sg;                   // k_rank's start guesses (SegGuess), valid when sg[0] == sg_epoch; or nullptr
     unsigned int sg_epoch;
+    int *walked;                     // [nseg] fused finalize: == wepoch for a segment the walk re-solved (or nullptr)
+    unsigned int wepoch;
 };
 
 // diagnostic phase stamps (100 MHz constant clock), lane 0 of a segment
@@ -2576,6 +2578,7 @@ __device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, i
                     __builtin_amdgcn_wave_barrier();  // win is refilled
                     st = seg_solve<TB>(a, q, q * SEG, st, win, true, true, 0, my_off, my_len, rec, rounds_w);
                     redo++;
+                    if (a.walked != nullptr && lane == 0) st_sc1(a.walked + q, (int)a.wepoch);
                 } else {
                     st += dq[i];
                 }
@@ -2970,10 +2973,20 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
         ctr->needsort_last = ns;  // the host launches the segmented sort while this holds
         for (int g = 0; g < 8; g++) ctr->fin_group[g] = 0;
         ctr->fin_top = 0;
-        // mapped host memory: every field written back, then the tag the host waits for
-        *f.snap = *ctr;
-        __threadfence_system();
-        __hip_atomic_store(&f.snap->snap_tag, f.snap_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (threadIdx.x < 64) {
+        // mapped host memory: every field (sc1 loads: fields other XCDs' waves stored in this
+        // launch when the finalize rides in the chain), then the tag the host waits for
+        static_assert(sizeof(DevCounters) % 4 == 0, "DevCounters copies as ints");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int *src = reinterpret_cast<const int *>(f.ctr);
+        int *dst = reinterpret_cast<int *>(f.snap);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevCounters) / 4); i += 64) dst[i] = ld_sc1(src + i);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(&f.snap->snap_tag, f.snap_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -3011,32 +3024,13 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
 // of wall clock): a segment that gives up answers ADLB_ERROR, never a guess.
 constexpr int FUSE_MAX_SEG = 512;                       // 131,072 Reserves
 constexpr long long FIN_WAIT_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
-__device__ __forceinline__ void fin_fused(const FinArgs &f, int s, bool last, unsigned int epoch) {
+
+// The finalize of segment s's SEG requests by one wave (loads issued together,
+// the three dependent levels umatch -> cslot -> record one after the other);
+// returns how many park.  Reads umatch with plain loads: only the wave that
+// last wrote those choices (the segment's own, or the walker) may call it.
+__device__ __forceinline__ int fin_segment(const FinArgs &f, int s, bool failed) {
     const int lane = threadIdx.x;
-    bool waited = true;
-    if (last) {
-        // the walk's choices (plain stores) and counters written back from this XCD's L2:
-        // segments finalized on the other XCDs read them after their acquire below
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) st_sc1(f.done, (int)epoch);
-    } else {
-        int ok = 0;
-        if (lane == 0) {
-            const long long t0 = wall_clock64();
-            while (true) {
-                if (ld_sc1(f.done) == (int)epoch) {
-                    ok = 1;
-                    break;
-                }
-                if (wall_clock64() - t0 > FIN_WAIT_TICKS) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        waited = __builtin_amdgcn_readfirstlane(ok) != 0;
-        if (!waited && lane == 0) atomicAdd(&f.ctr->chain_timeouts, 1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the walk's choices: no stale L1 / L2 lines
-    const bool failed = !waited || fin_failed(f);
     constexpr int U = SEG / 64;
     const int j0 = s * SEG;
     int rank[U], hang[U], tm[U], um[U], slot[U];
@@ -3099,14 +3093,71 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, int s, bool last, un
         if (lane == 0) __hip_atomic_store(f.pmask + ((j0 >> 6) + u), pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         parked += __popcll(pb);
     }
-    __builtin_amdgcn_s_waitcnt(0);  // this segment's stores have landed before it arrives
+    __builtin_amdgcn_s_waitcnt(0);  // the segment's stores have landed before it arrives
+    return parked;
+}
+
+// One arrival for segment s (wave-uniform result: the batch's parked count, or -1 when not last).
+__device__ __forceinline__ int fin_seg_arrive(const FinArgs &f, int s, int parked, int nseg) {
     unsigned long long tk = 0;
-    if (lane == 0) tk = fin_arrive(f, parked, gridDim.x, blockIdx.x);
+    if (threadIdx.x == 0) tk = fin_arrive(f, parked, (unsigned int)nseg, (unsigned int)s);
     const unsigned int lo = __builtin_amdgcn_readfirstlane((unsigned int)tk),
                        hi = __builtin_amdgcn_readfirstlane((unsigned int)(tk >> 32));
-    if (!(lo & 1u)) return;
+    return (lo & 1u) ? (int)hi : -1;
+}
+
+// k_finalize fused into the final k_chain0 launch (every segment one
+// workgroup; the host fuses only grids small enough to be resident at once,
+// since each segment waits here).  Choices are read only by the wave that
+// wrote them last: per-XCD L2s are not coherent, and a segment's own plain
+// stores stay in its XCD's L2.  So the launch's last arriver finalizes the
+// segments its walk re-solved (flagged in `walked`), then publishes the
+// chain epoch; every other segment waits for it and, unless walked,
+// finalizes itself.  The last of the nseg arrivals runs the batch tail.  The
+// wait is bounded (one second of wall clock): a segment that gives up answers
+// ADLB_ERROR, never a guess.
+__device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, int s, bool last, unsigned int epoch,
+                                          int nseg) {
+    const int lane = threadIdx.x;
+    int total = -1;
+    bool failed = fin_failed(f);
+    if (last) {
+        for (int q0 = 0; q0 < nseg; q0 += 64) {
+            const bool w = q0 + lane < nseg && ld_sc1(walked + q0 + lane) == (int)epoch;
+            for (unsigned long long b = __ballot(w); b; b &= b - 1) {
+                const int q = q0 + __ffsll((long long)b) - 1;
+                const int t = fin_seg_arrive(f, q, fin_segment(f, q, failed), nseg);
+                if (t >= 0) total = t;
+            }
+        }
+        // the chain counters (plain stores) leave this XCD's L2 before the flag
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) st_sc1(f.done, (int)epoch);
+    } else {
+        int ok = 0;
+        if (lane == 0) {
+            const long long t0 = wall_clock64();
+            while (true) {
+                if (ld_sc1(f.done) == (int)epoch) {
+                    ok = 1;
+                    break;
+                }
+                if (wall_clock64() - t0 > FIN_WAIT_TICKS) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (!__builtin_amdgcn_readfirstlane(ok)) {
+            if (lane == 0) atomicAdd(&f.ctr->chain_timeouts, 1);
+            failed = true;
+        }
+    }
+    if (ld_sc1(walked + s) != (int)epoch) {  // not re-solved by the walk: this wave holds the choices
+        const int t = fin_seg_arrive(f, s, fin_segment(f, s, failed), nseg);
+        if (t >= 0) total = t;
+    }
+    if (total < 0) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    fin_tail(f, (int)hi, failed);
+    fin_tail(f, total, failed);
 }
 
 // Round 0: every segment from its level guess (lane t = type t's head), then
@@ -3224,7 +3275,7 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
     const bool last = chain_arrive<TB>(a, s, start, end - start, solves, bad, rounds, 0, P, final != 0,
                                        prefix_next != 0, win);
     chain_stamp(a, s, 5);
-    if (fuse) fin_fused(f, s, last, cp.epoch);
+    if (fuse) fin_fused(f, a.walked, s, last, cp.epoch, nseg);
 }
 
 // ---------------------------------------------------------------- steal export
@@ -3303,8 +3354,9 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_chD, sizeof(int) * 2 * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chLP, sizeof(int) * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * CHAIN_MAX_PASSES * nseg * T1));
-    AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * CHAIN_MAX_PASSES * nseg));
-    AQ_HIP(hipMemsetAsync(h->d_chflag, 0, sizeof(int) * CHAIN_MAX_PASSES * nseg, h->stream));  // epochs start at 1
+    // [CHAIN_MAX_PASSES][nseg] hand-off flags, then [nseg] the fused finalize's walked segments
+    AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));
+    AQ_HIP(hipMemsetAsync(h->d_chflag, 0, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg, h->stream));  // epochs start at 1
     AQ_HIP(hipMalloc((void **)&h->d_chGT, sizeof(int) * CH_GROUPS * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chGO, sizeof(int) * CH_GROUPS * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chclean, sizeof(int) * 2));  // [1]: the fused finalize's epoch flag
@@ -4398,7 +4450,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                      h->d_umatch, h->d_cht, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chS + nsT, h->d_chD + nsT,
                      h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_chcnt, h->d_ctr,
                      (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr,
-                     (T <= 8 && np > 0 && h->seg_guess) ? h->d_sg : nullptr, h->rank_epoch};
+                     (T <= 8 && np > 0 && h->seg_guess) ? h->d_sg : nullptr, h->rank_epoch, nullptr, 0u};
         if (h->chain_stamps) {
             if (nseg > h->cap_stamps) {
                 AQ_HIP(hipStreamSynchronize(s));
@@ -4426,6 +4478,10 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         // the finalize rides in k_chain0 when that launch is the final one and its
         // grid is small enough to be resident at once (each segment waits there)
         fused = h->fuse_finalize && K == 0 && T <= 8 && nseg <= FUSE_MAX_SEG;
+        if (fused) {
+            ca.walked = h->d_chflag + (size_t)CHAIN_MAX_PASSES * ((h->cap_req + SEG - 1) / SEG);
+            ca.wepoch = h->chain_epoch;
+        }
         if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
