@@ -2531,13 +2531,14 @@ __device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, i
     if (lane == 0) {
         for (int q = 0; q <= CH_GROUPS; q++) a.counters[q] = 0;  // for the next launch (kernel boundary in between)
         *a.clean = clean ? 1 : 0;
+        // sc1: a finalize fused into this launch snapshots them from another XCD
         if (round == 0) {
-            a.ctr->chain_passes = passes;
-            a.ctr->chain_recomputed = nsolved;
-            a.ctr->chain_fallback = 0;
+            st_sc1(&a.ctr->chain_passes, passes);
+            st_sc1(&a.ctr->chain_recomputed, nsolved);
+            st_sc1(&a.ctr->chain_fallback, 0);
         } else {
-            a.ctr->chain_passes += 1;
-            a.ctr->chain_recomputed += nsolved;
+            st_sc1(&a.ctr->chain_passes, ld_sc1(&a.ctr->chain_passes) + 1);
+            st_sc1(&a.ctr->chain_recomputed, ld_sc1(&a.ctr->chain_recomputed) + nsolved);
         }
     }
     if (!final || clean) return true;
@@ -2586,7 +2587,7 @@ __device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, i
         }
     }
     if (lane == 0) {
-        a.ctr->chain_fallback = redo;
+        st_sc1(&a.ctr->chain_fallback, redo);
         atomicAdd(&a.ctr->chain_rounds, rounds_w);
     }
     return true;
@@ -3025,58 +3026,66 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
 constexpr int FUSE_MAX_SEG = 512;                       // 131,072 Reserves
 constexpr long long FIN_WAIT_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
 
-// The finalize of segment s's SEG requests by one wave (loads issued together,
-// the three dependent levels umatch -> cslot -> record one after the other);
-// returns how many park.  Reads umatch with plain loads: only the wave that
-// last wrote those choices (the segment's own, or the walker) may call it.
-__device__ __forceinline__ int fin_segment(const FinArgs &f, int s, bool failed) {
-    const int lane = threadIdx.x;
-    constexpr int U = SEG / 64;
-    const int j0 = s * SEG;
-    int rank[U], hang[U], tm[U], um[U], slot[U];
+// The finalize of segment s's SEG requests by one wave: the loads (issued
+// together, the three dependent levels umatch -> cslot -> record one after
+// the other), then the pins, replies and park ballots; the store half returns
+// how many park.  Reads umatch with plain loads: only the wave that last wrote
+// those choices (the segment's own, or the walker) may load them.
+constexpr int FIN_U = SEG / 64;
+struct FinSeg {
+    int rank[FIN_U], hang[FIN_U], slot[FIN_U];
+    int4 c0[FIN_U], c1[FIN_U];
+};
+
+__device__ __forceinline__ void fin_seg_load(const FinArgs &f, int s, FinSeg &g) {
+    const int lane = threadIdx.x, j0 = s * SEG;
+    int tm[FIN_U], um[FIN_U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int u = 0; u < FIN_U; u++) {
         const int j = j0 + u * 64 + lane;
         const bool in = j < f.R;
         const int *rq = f.reqs + (long long)ADLBQ_RESERVE_INTS * (in ? j : 0);
-        rank[u] = in ? rq[0] : 0;
-        hang[u] = in ? rq[1] : 0;
+        g.rank[u] = in ? rq[0] : 0;
+        g.hang[u] = in ? rq[1] : 0;
         tm[u] = in ? f.tmatch[j] : -1;
         um[u] = in ? f.umatch[j] : -1;
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) slot[u] = failed ? -1 : tm[u] >= 0 ? tm[u] : (um[u] >= 0 ? f.cslot[um[u]] : -1);
-    int4 c0[U], c1[U];
+    for (int u = 0; u < FIN_U; u++) g.slot[u] = tm[u] >= 0 ? tm[u] : (um[u] >= 0 ? f.cslot[um[u]] : -1);
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-        c0[u] = slot[u] >= 0 ? f.rrec[2ll * slot[u]] : make_int4(0, 0, 0, 0);
-        c1[u] = slot[u] >= 0 ? f.rrec[2ll * slot[u] + 1] : make_int4(0, 0, 0, 0);
+    for (int u = 0; u < FIN_U; u++) {
+        g.c0[u] = g.slot[u] >= 0 ? f.rrec[2ll * g.slot[u]] : make_int4(0, 0, 0, 0);
+        g.c1[u] = g.slot[u] >= 0 ? f.rrec[2ll * g.slot[u] + 1] : make_int4(0, 0, 0, 0);
     }
+}
+
+__device__ __forceinline__ int fin_seg_store(const FinArgs &f, int s, const FinSeg &g, bool failed) {
+    const int lane = threadIdx.x, j0 = s * SEG;
     int parked = 0;
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int u = 0; u < FIN_U; u++) {
         const int j = j0 + u * 64 + lane;
         if (j0 + u * 64 >= f.R) break;
         bool parks = false;
         if (j < f.R) {
-            const int sl = slot[u], hg = failed ? 0 : hang[u];
+            const int sl = failed ? -1 : g.slot[u], hg = failed ? 0 : g.hang[u];
             int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
             if (failed) {
                 o[0] = -1;  // ADLB_ERROR
             } else if (sl >= 0) {
-                f.pin[sl] = rank[u];  // adlb.c:1210-1212
-                if (rank[u] >= 0)
+                f.pin[sl] = g.rank[u];  // adlb.c:1210-1212
+                if (g.rank[u] >= 0)
                     __hip_atomic_fetch_or(f.meta + sl, M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 o[0] = 1;
-                o[1] = c1[u].z;
-                o[2] = c1[u].w;
-                o[3] = c0[u].y;
-                o[4] = c0[u].x;
-                o[5] = c0[u].z;
+                o[1] = g.c1[u].z;
+                o[2] = g.c1[u].w;
+                o[3] = g.c0[u].y;
+                o[4] = g.c0[u].x;
+                o[5] = g.c0[u].z;
                 o[6] = f.my_world;
-                o[7] = c0[u].w;
-                o[8] = c1[u].x;
-                o[9] = c1[u].y;
+                o[7] = g.c0[u].w;
+                o[8] = g.c1[u].x;
+                o[9] = g.c1[u].y;
             } else if (!hg) {
                 o[0] = -2;  // NO_CURR_WORK
             }
@@ -3121,19 +3130,22 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, i
     const int lane = threadIdx.x;
     int total = -1;
     bool failed = fin_failed(f);
+    FinSeg mine;
     if (last) {
         for (int q0 = 0; q0 < nseg; q0 += 64) {
             const bool w = q0 + lane < nseg && ld_sc1(walked + q0 + lane) == (int)epoch;
             for (unsigned long long b = __ballot(w); b; b &= b - 1) {
                 const int q = q0 + __ffsll((long long)b) - 1;
-                const int t = fin_seg_arrive(f, q, fin_segment(f, q, failed), nseg);
+                FinSeg g;
+                fin_seg_load(f, q, g);
+                const int t = fin_seg_arrive(f, q, fin_seg_store(f, q, g, failed), nseg);
                 if (t >= 0) total = t;
             }
         }
-        // the chain counters (plain stores) leave this XCD's L2 before the flag
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chain counters went out sc1
         if (lane == 0) st_sc1(f.done, (int)epoch);
     } else {
+        fin_seg_load(f, s, mine);  // speculative: used only if the walk leaves this segment alone
         int ok = 0;
         if (lane == 0) {
             const long long t0 = wall_clock64();
@@ -3152,7 +3164,8 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, i
         }
     }
     if (ld_sc1(walked + s) != (int)epoch) {  // not re-solved by the walk: this wave holds the choices
-        const int t = fin_seg_arrive(f, s, fin_segment(f, s, failed), nseg);
+        if (last) fin_seg_load(f, s, mine);
+        const int t = fin_seg_arrive(f, s, fin_seg_store(f, s, mine, failed), nseg);
         if (t >= 0) total = t;
     }
     if (total < 0) return;
