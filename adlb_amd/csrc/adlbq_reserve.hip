@@ -2926,11 +2926,16 @@ __device__ __forceinline__ bool fin_request(const FinArgs &f, int j, bool failed
     return parks;
 }
 
+constexpr unsigned int FIN_FLAT = 512;  // grids up to this size arrive at one counter
 // Two-level arrival of workgroup bid of nb (8 groups, then one top counter)
 // keeps every counter's atomics to about nb / 8; a count rides in the high
 // half.  One thread; returns (parked in the batch << 32) | 1 for the last.
 __device__ __forceinline__ unsigned long long fin_arrive(const FinArgs &f, int parked, unsigned int nb,
                                                          unsigned int bid) {
+    if (nb <= FIN_FLAT) {  // a small grid: one counter, one returning atomic per workgroup
+        const unsigned long long top = atomicAdd(&f.ctr->fin_top, ((unsigned long long)parked << 32) | 1ull);
+        return (unsigned int)top == nb - 1u ? ((((top >> 32) + (unsigned long long)parked) << 32) | 1ull) : 0ull;
+    }
     const unsigned int g = bid & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
     unsigned long long v = atomicAdd(&f.ctr->fin_group[g], ((unsigned long long)parked << 32) | 1ull);
     if ((unsigned int)v == ng - 1u) {
@@ -2984,10 +2989,9 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
         int *dst = reinterpret_cast<int *>(f.snap);
         for (int i = threadIdx.x; i < (int)(sizeof(DevCounters) / 4); i += 64) dst[i] = ld_sc1(src + i);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (threadIdx.x == 0) {
-            __threadfence_system();
+        // the tag's system-scope release store orders the wave's drained snapshot stores before it
+        if (threadIdx.x == 0)
             __hip_atomic_store(&f.snap->snap_tag, f.snap_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
     }
 }
 
@@ -3023,7 +3027,7 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
 // dependent levels umatch -> cslot -> record one after the other), and the
 // last of those arrivals runs the batch tail.  The wait is bounded (one second
 // of wall clock): a segment that gives up answers ADLB_ERROR, never a guess.
-constexpr int FUSE_MAX_SEG = 512;                       // 131,072 Reserves
+constexpr int FUSE_MAX_SEG = 256;                       // 65,536 Reserves
 constexpr long long FIN_WAIT_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
 
 // The finalize of segment s's SEG requests by one wave: the loads (issued
@@ -3169,8 +3173,7 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, i
         if (t >= 0) total = t;
     }
     if (total < 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    fin_tail(f, total, failed);
+    fin_tail(f, total, failed);  // reads other segments' data only through sc1 / atomic loads
 }
 
 // Round 0: every segment from its level guess (lane t = type t's head), then

@@ -745,34 +745,31 @@ static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, 
     std::vector<ShardView> vw((size_t)S, ShardView{nullptr, nullptr, nullptr});
     std::vector<int> local_of((size_t)S, -1);
     for (int j = 0; j < g->n; j++) local_of[(size_t)g->sh[(size_t)j]->my_idx] = j;
-    g->reqs.clear();
+    // (shard, rqseqno) order: each region's rq is in FIFO (rqseqno) order, so the
+    // regions in shard order (regions may come in any order) give it directly
+    std::vector<int> reg_of((size_t)S, -1);
     for (int r = 0; r < nreg; r++) {
         const int *b = g->h_all + (size_t)r * g->blob;
         const int idx = b[0];
-        if (idx < 0 || idx >= S || vw[(size_t)idx].nrec) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle: bad or repeated shard index");
+        if (idx < 0 || idx >= S || reg_of[(size_t)idx] >= 0)
+            return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle: bad or repeated shard index");
+        reg_of[(size_t)idx] = r;
         vw[(size_t)idx] = ShardView{b + g->off_recs, b + g->off_nrec, reinterpret_cast<const long long *>(b + g->off_nav)};
-        const int *rq = b + g->off_rq;
+    }
+    g->reqs.clear();
+    for (int idx = 0; idx < S; idx++) {
+        if (reg_of[(size_t)idx] < 0) continue;
+        const int *rq = g->h_all + (size_t)reg_of[(size_t)idx] * g->blob + g->off_rq;
         const int c = std::min(rq[0], g->rqcap);  // entries past rqcap wait for the next round
-        for (int i = 0; i < c; i++) {
-            g->reqs.push_back(idx);
-            g->reqs.insert(g->reqs.end(), rq + 1 + 18 * (size_t)i, rq + 1 + 18 * (size_t)i + 18);
+        const size_t o = g->reqs.size();
+        g->reqs.resize(o + 19 * (size_t)c);
+        int *dst = g->reqs.data() + o;
+        for (int i = 0; i < c; i++, dst += 19) {
+            dst[0] = idx;
+            std::memcpy(dst + 1, rq + 1 + 18 * (size_t)i, sizeof(int) * 18);
         }
     }
     const int nreq = (int)(g->reqs.size() / 19);
-    // (shard, rqseqno) order: regions come in any order, each region's rq in FIFO order
-    {
-        std::vector<int> ord((size_t)nreq);
-        for (int i = 0; i < nreq; i++) ord[(size_t)i] = i;
-        const int *q = g->reqs.data();
-        std::sort(ord.begin(), ord.end(), [q](int a, int b) {
-            return q[19 * (size_t)a] != q[19 * (size_t)b] ? q[19 * (size_t)a] < q[19 * (size_t)b]
-                                                          : q[19 * (size_t)a + 1] < q[19 * (size_t)b + 1];
-        });
-        std::vector<int> sorted((size_t)nreq * 19);
-        for (int i = 0; i < nreq; i++)
-            std::memcpy(&sorted[19 * (size_t)i], q + 19 * (size_t)ord[(size_t)i], sizeof(int) * 19);
-        g->reqs.swap(sorted);
-    }
     g->out3.assign(3 * (size_t)nreq, -1);
     int nd = 0, rc;
     if (nreq && (rc = merge_views(S, T, h0->utypes.data(), g->k, vw.data(), nreq, g->reqs.data(), g->out3.data(), &nd)))
