@@ -312,7 +312,7 @@ struct adlbq_server {
     long long chain_modes = -1;        // bit k-1: round k uses prefix starts, -1 = auto ("chain_modes")
     int segsort_merged = 1;            // one merged sort of every list when the keys allow ("segsort_merged")
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
-    int fuse_finalize = 1;             // "fuse_finalize": k_finalize inside the final k_chain0 launch when it can
+    int fuse_finalize = 0;             // "fuse_finalize": k_finalize inside the final k_chain0 launch (measured even: off)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror

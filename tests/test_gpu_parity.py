@@ -89,7 +89,7 @@ VARIANTS = {
     "hist_ppb2": {"hist_ppb": 2},          # pass 1: two pages per workgroup
     "no_seg_guess": {"seg_guess": 0},      # the chain finds its own start guesses
     "all": {"select_chunk": 1, "hist_ppb": 2},
-    "no_fuse": {"fuse_finalize": 0},       # k_finalize as its own launch
+    "fused": {"fuse_finalize": 1},         # k_finalize inside the final k_chain0 launch
 }
 
 
@@ -147,6 +147,22 @@ def test_chain_fixup_path(gpu_available, name, passes):
                   stats=st)
     assert_same(got, run_oracle(w.user_types, cfg, tr))
     if name == "c2_n200k_r16k" and passes == 1:
+        assert st["chain_fallback"] > 0, st
+
+
+@pytest.mark.parametrize("name", ["c2_n200k_r16k", "c4_t8_tied", "c2_exhaust"])
+def test_fused_finalize_after_walk(gpu_available, name):
+    """The finalize fused into the chain launch: segments the last arriver's walk
+    re-solved are finalized by that walker (their own wave's choices are stale),
+    every other segment by its own wave."""
+    w = CASES[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    st = {}
+    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units,
+                  params={"fuse_finalize": 1, "chain_passes": 1, "chain_warm": 0}, stats=st)
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
+    if name == "c2_n200k_r16k":
         assert st["chain_fallback"] > 0, st
 
 
