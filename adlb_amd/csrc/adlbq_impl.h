@@ -385,6 +385,52 @@ __device__ __forceinline__ unsigned long long make_key(int prio, unsigned int or
            (unsigned long long)(~order);
 }
 
+// Keep anchor[t] >= prio.  Most calls do not raise it, so the anchor is read
+// first; the lanes of a wave that do raise it agree on one atomic per type
+// (a single device-scope word per type would otherwise serialise them).
+// Every lane of the wave must call it (INT_MIN: nothing to raise).
+__device__ __forceinline__ void raise_anchor(long long *anchor, int t, int prio) {
+    bool up = __hip_atomic_load(anchor + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (long long)prio;
+    while (true) {
+        const unsigned long long b = __ballot(up);
+        if (!b) break;
+        const int leader = __ffsll((long long)b) - 1;
+        const int lt = __shfl(t, leader, 64);
+        int m = (up && t == lt) ? prio : INT_MIN;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        if (__lane_id() == leader) atomicMax(anchor + lt, (long long)m);
+        if (t == lt) up = false;
+    }
+}
+
+// SS_UNRESERVE of triple i (rank, wqseqno, new pin) (adlb.c:2057-2063): a unit
+// still live, pinned for that rank and with that wqseqno goes back to the
+// queue.  Every lane of the wave calls it (raise_anchor).
+__device__ __forceinline__ void unreserve_triple(int i, const int *__restrict__ trip, int n,
+                                                 const long long *__restrict__ seq2slot, long long nseq,
+                                                 uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
+                                                 long long *anchor) {
+    int t = 0, up = INT_MIN;
+    if (i < n) {
+        int rank = trip[3 * i], seq = trip[3 * i + 1], np = trip[3 * i + 2];
+        long long slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
+        if (slot >= 0) {
+            // meta, pin and the slot's response record (wqseqno, prio) in one round trip
+            const uint32_t m = meta[slot];
+            const int pn = pin[slot];
+            const int4 r0 = rrec[2 * slot], r1 = rrec[2 * slot + 1];
+            if ((m & M_LIVE) && pn == rank && r0.z == seq) {
+                pin[slot] = np;
+                meta[slot] = m & ~M_PINNED;
+                t = m & M_TYPE;
+                up = r1.w;
+            }
+        }
+    }
+    raise_anchor(anchor, t, up);  // available again: keep the anchor above it
+}
+
 // The rq slot holding rqseqno (-1: none).  rq_seq is ascending over the
 // slots in use: FIFO order is rqseqno order, and k_rq_reclaim keeps it.
 __device__ __forceinline__ int rq_slot_of(const int *rq_seq, int n, int rqseqno) {

@@ -50,10 +50,10 @@ namespace {
 // donor side of SS_RFR: pin_rank = for_rank, pinned = (for_rank >= 0)
 // (adlb.c:1820-1824) for units still live, unpinned and untargeted.
 // found (optional) per pair; bad (optional) counts the pairs that were not.
-__global__ void k_grant(const int *__restrict__ pairs, int n, const long long *__restrict__ seq2slot,
-                        long long nseq, uint32_t *meta, int *pin, const int *__restrict__ seqa,
-                        const int4 *__restrict__ cold1, int *__restrict__ found, int *bad) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void grant_pair(int i, const int *__restrict__ pairs, int n,
+                                           const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta,
+                                           int *pin, const int *__restrict__ seqa, const int4 *__restrict__ cold1,
+                                           int *__restrict__ found, int *bad) {
     int ok = 0;
     if (i < n) {
         const int rank = pairs[2 * i], seq = pairs[2 * i + 1];
@@ -70,6 +70,12 @@ __global__ void k_grant(const int *__restrict__ pairs, int n, const long long *_
     }
     const unsigned long long b = __ballot(i < n && !ok);
     if (bad && (threadIdx.x & 63) == 0 && b) atomicAdd(bad, __popcll(b));
+}
+
+__global__ void k_grant(const int *__restrict__ pairs, int n, const long long *__restrict__ seq2slot,
+                        long long nseq, uint32_t *meta, int *pin, const int *__restrict__ seqa,
+                        const int4 *__restrict__ cold1, int *__restrict__ found, int *bad) {
+    grant_pair(blockIdx.x * blockDim.x + threadIdx.x, pairs, n, seq2slot, nseq, meta, pin, seqa, cold1, found, bad);
 }
 
 __global__ void k_rfr_reset(int *rfr_to_rank, int A, int *rfr_out, int nworld, int *hdr = nullptr, int idx = 0) {
@@ -122,12 +128,12 @@ __global__ __launch_bounds__(1024) void k_rq_delete_fix(const int *rq_live, DevC
 // k_rq_delete_batch + k_rq_delete_fix in one launch: the last workgroup to
 // arrive (ticket) does the bookkeeping and finds the new FIFO head, reading
 // rq_live at agent scope (the other workgroups' exchanges, not a stale line)
-__global__ __launch_bounds__(256) void k_rq_delete_settle(const int *__restrict__ rqseqnos, int n, int *rq_live,
-                                                          const int *__restrict__ rq_seq, DevCounters *ctr,
-                                                          int *ndel, int *bad, int *ticket) {
+__device__ __forceinline__ void rq_delete_settle_blk(int bid, int nblk, const int *__restrict__ rqseqnos, int n,
+                                                     int *rq_live, const int *__restrict__ rq_seq, DevCounters *ctr,
+                                                     int *ndel, int *bad, int *ticket) {
     __shared__ int s_first;
     __shared__ bool s_last;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = bid * blockDim.x + threadIdx.x;
     int hit = 0;
     if (i < n) {
         const int k = rq_slot_of(rq_seq, ctr->rq_n, rqseqnos[i]);
@@ -141,7 +147,7 @@ __global__ __launch_bounds__(256) void k_rq_delete_settle(const int *__restrict_
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
-        s_last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+        s_last = atomicAdd(ticket, 1) == nblk - 1;
     }
     __syncthreads();
     if (!s_last) return;
@@ -165,6 +171,64 @@ __global__ __launch_bounds__(256) void k_rq_delete_settle(const int *__restrict_
         if (f < nn) break;
     }
     if (threadIdx.x == 0) ctr->rq_head = s_first;
+}
+
+// k_rq_delete_batch + k_rq_delete_fix in one launch: the last workgroup to
+// arrive (ticket) does the bookkeeping and finds the new FIFO head, reading
+// rq_live at agent scope (the other workgroups' exchanges, not a stale line)
+__global__ __launch_bounds__(256) void k_rq_delete_settle(const int *__restrict__ rqseqnos, int n, int *rq_live,
+                                                          const int *__restrict__ rq_seq, DevCounters *ctr,
+                                                          int *ndel, int *bad, int *ticket) {
+    rq_delete_settle_blk(blockIdx.x, gridDim.x, rqseqnos, n, rq_live, rq_seq, ctr, ndel, bad, ticket);
+}
+
+// One group settle's grants and rq deletions for every local shard in one
+// launch: blockIdx.y = shard, blocks [0, gb) of a row grant, the rest delete
+// (the last of those to arrive fixes that shard's rq head).
+struct ShardApply {
+    const int *pairs, *dels;
+    int ngrant, ndel;
+    const long long *seq2slot;
+    long long nseq;
+    uint32_t *meta;
+    int *pin;
+    const int *seqa;
+    const int4 *cold1;
+    int *apply_bad;  // [bad grants, bad deletes, deleted, settle ticket]
+    int *rq_live;
+    const int *rq_seq;
+    DevCounters *ctr;
+};
+
+__global__ __launch_bounds__(256) void k_group_apply(const ShardApply *__restrict__ tab, int gb) {
+    const ShardApply a = tab[blockIdx.y];
+    if ((int)blockIdx.x < gb) {
+        if ((int)blockIdx.x * 256 < a.ngrant)
+            grant_pair(blockIdx.x * 256 + threadIdx.x, a.pairs, a.ngrant, a.seq2slot, a.nseq, a.meta, a.pin, a.seqa,
+                       a.cold1, nullptr, a.apply_bad);
+        return;
+    }
+    if (a.ndel == 0) return;
+    rq_delete_settle_blk((int)blockIdx.x - gb, (int)gridDim.x - gb, a.dels, a.ndel, a.rq_live, a.rq_seq, a.ctr,
+                         a.apply_bad + 2, a.apply_bad + 1, a.apply_bad + 3);
+}
+
+// The grants' SS_UNRESERVE for every local shard in one launch (blockIdx.y = shard).
+struct ShardUnres {
+    const int *trip;
+    int n;
+    const long long *seq2slot;
+    long long nseq;
+    uint32_t *meta;
+    int *pin;
+    const int4 *rrec;
+    long long *anchor;
+};
+
+__global__ __launch_bounds__(256) void k_group_unreserve(const ShardUnres *__restrict__ tab) {
+    const ShardUnres a = tab[blockIdx.y];
+    if ((int)blockIdx.x * 256 >= a.n) return;  // whole waves return together (raise_anchor)
+    unreserve_triple(blockIdx.x * 256 + threadIdx.x, a.trip, a.n, a.seq2slot, a.nseq, a.meta, a.pin, a.rrec, a.anchor);
 }
 
 // The live rq entries in FIFO order, compacted: out[0] = count, then up to cap
@@ -609,6 +673,7 @@ struct adlbq_steal_group {
     int *h_app = nullptr, *d_app = nullptr;  // every shard's grants + rq deletions, one copy per settle
     long long cap_app = 0;
     hipEvent_t app_ev = nullptr;
+    hipEvent_t app_done_ev = nullptr;  // after k_group_apply: the other shards' streams wait for it
     hipEvent_t unr_ev = nullptr;  // the grants' SS_UNRESERVE staging copy (first shard's stream)
     long long ns_copy = 0, ns_merge = 0, ns_apply = 0, nreq_last = 0;  // the last settle's host phases
 };
@@ -798,42 +863,58 @@ static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, 
             g->resp.insert(g->resp.end(), r15, r15 + 15);
         }
     }
-    // every shard's grants and deletions staged together: one copy on the first
-    // shard's stream, each shard's kernels behind its event
+    // every shard's grants and deletions staged together with a table of
+    // per-shard arguments: one copy and one launch (k_group_apply) on the first
+    // shard's stream, the other shards' streams ordered behind it
     long long tot = 0;
-    for (int j = 0; j < g->n; j++) tot += (long long)g->grants[(size_t)j].size() + (long long)g->dels[(size_t)j].size();
+    int mg = 0, md = 0;
+    for (int j = 0; j < g->n; j++) {
+        tot += (long long)g->grants[(size_t)j].size() + (long long)g->dels[(size_t)j].size();
+        mg = std::max(mg, (int)(g->grants[(size_t)j].size() / 2));
+        md = std::max(md, (int)g->dels[(size_t)j].size());
+    }
     if (tot > 0) {
+        const long long toff = (tot + 1) & ~1ll;  // the table 8-byte aligned after the payload
+        const long long need = toff + (long long)(sizeof(ShardApply) / sizeof(int)) * g->n;
         if (g->app_ev) AQ_HIP(hipEventSynchronize(g->app_ev));  // the previous settle's copy has left the staging
         else AQ_HIP(hipEventCreateWithFlags(&g->app_ev, hipEventDisableTiming));
-        if (tot > g->cap_app) {
+        if (!g->app_done_ev) AQ_HIP(hipEventCreateWithFlags(&g->app_done_ev, hipEventDisableTiming));
+        if (need > g->cap_app) {
             for (auto *h : g->sh) AQ_HIP(hipStreamSynchronize(h->stream));
             if (g->h_app) AQ_HIP(hipHostFree(g->h_app));
             if (g->d_app) AQ_HIP(hipFree(g->d_app));
-            g->cap_app = std::max(tot, 2 * g->cap_app);
+            g->cap_app = std::max(need, 2 * g->cap_app);
             AQ_HIP(hipHostMalloc((void **)&g->h_app, sizeof(int) * g->cap_app, hipHostMallocDefault));
             AQ_HIP(hipMalloc((void **)&g->d_app, sizeof(int) * g->cap_app));
         }
+        ShardApply *tab = reinterpret_cast<ShardApply *>(g->h_app + toff);
         long long off = 0;
-        for (int j = 0; j < g->n; j++) {
-            for (const auto *v : {&g->grants[(size_t)j], &g->dels[(size_t)j]}) {
-                if (!v->empty()) std::memcpy(g->h_app + off, v->data(), sizeof(int) * v->size());
-                off += (long long)v->size();
-            }
-        }
-        AQ_HIP(hipMemcpyAsync(g->d_app, g->h_app, sizeof(int) * tot, hipMemcpyHostToDevice, h0->stream));
-        AQ_HIP(hipEventRecord(g->app_ev, h0->stream));
-        off = 0;
         for (int j = 0; j < g->n; j++) {
             adlbq_server *h = g->sh[(size_t)j];
             const auto &gr = g->grants[(size_t)j];
             const auto &dl = g->dels[(size_t)j];
-            const int ng = (int)(gr.size() / 2), nd2 = (int)dl.size();
-            if (ng || nd2) {
-                if (h != h0) AQ_HIP(hipStreamWaitEvent(h->stream, g->app_ev, 0));
-                if ((rc = steal_apply_launch(h, ng, g->d_app + off, nd2, g->d_app + off + 2ll * ng))) return rc;
+            if (!gr.empty()) std::memcpy(g->h_app + off, gr.data(), sizeof(int) * gr.size());
+            if (!dl.empty()) std::memcpy(g->h_app + off + gr.size(), dl.data(), sizeof(int) * dl.size());
+            if (!h->d_apply_bad) {  // [bad grants, bad deletes, deleted, settle ticket]
+                AQ_HIP(hipMalloc((void **)&h->d_apply_bad, sizeof(int) * 4));
+                AQ_HIP(hipMemset(h->d_apply_bad, 0, sizeof(int) * 4));
             }
-            off += (long long)gr.size() + nd2;
+            tab[j] = ShardApply{g->d_app + off, g->d_app + off + gr.size(), (int)(gr.size() / 2), (int)dl.size(),
+                                h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_pin, h->d_seq, h->d_cold1,
+                                h->d_apply_bad, h->d_rq_live, h->d_rq_seq, h->d_ctr};
+            if (!gr.empty() || !dl.empty()) wq_changed(h);
+            if (!dl.empty()) h->ctr_stale = true;
+            off += (long long)gr.size() + (long long)dl.size();
         }
+        AQ_HIP(hipMemcpyAsync(g->d_app, g->h_app, sizeof(int) * need, hipMemcpyHostToDevice, h0->stream));
+        AQ_HIP(hipEventRecord(g->app_ev, h0->stream));
+        const int gb = (mg + 255) / 256, db = (md + 255) / 256;
+        k_group_apply<<<dim3(gb + db, g->n), 256, 0, h0->stream>>>(reinterpret_cast<const ShardApply *>(g->d_app + toff),
+                                                                   gb);
+        AQ_HIP(hipGetLastError());
+        AQ_HIP(hipEventRecord(g->app_done_ev, h0->stream));
+        for (int j = 0; j < g->n; j++)
+            if (g->sh[(size_t)j] != h0) AQ_HIP(hipStreamWaitEvent(g->sh[(size_t)j]->stream, g->app_done_ev, 0));
     }
     const auto t3 = clk::now();
     g->ns_copy = std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
@@ -854,39 +935,43 @@ int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g) {
     for (const auto &gr : g->grants) total += (long long)(gr.size() / 2);
     if (!total) return ADLBQ_OK;
     hipSetDevice(g->sh[0]->device);
-    if (3 * total > g->cap_unr) {
+    // the staging is free: the previous round's copy (first shard's stream) completed
+    // before this round's settle returned.  Every shard's triples and a table of
+    // per-shard arguments in one copy, one launch on the first shard's stream
+    adlbq_server *h0 = g->sh[0];
+    const long long toff = (3 * total + 1) & ~1ll;
+    const long long need = toff + (long long)(sizeof(ShardUnres) / sizeof(int)) * g->n;
+    if (need > g->cap_unr) {
         for (auto *h : g->sh) AQ_HIP(hipStreamSynchronize(h->stream));
         if (g->h_unr) AQ_HIP(hipHostFree(g->h_unr));
         if (g->d_unr) AQ_HIP(hipFree(g->d_unr));
-        g->cap_unr = std::max(3 * total, 2 * g->cap_unr);
+        g->cap_unr = std::max(need, 2 * g->cap_unr);
         AQ_HIP(hipHostMalloc((void **)&g->h_unr, sizeof(int) * g->cap_unr, hipHostMallocDefault));
         AQ_HIP(hipMalloc((void **)&g->d_unr, sizeof(int) * g->cap_unr));
     }
-    // the staging is free: the previous round's copy (first shard's stream) completed
-    // before this round's settle returned.  Every shard's triples in one copy; each
-    // shard's kernel behind its event
-    adlbq_server *h0 = g->sh[0];
+    ShardUnres *tab = reinterpret_cast<ShardUnres *>(g->h_unr + toff);
     long long off = 0;
+    int mx = 0;
     for (int j = 0; j < g->n; j++) {
+        adlbq_server *h = g->sh[(size_t)j];
         const auto &gr = g->grants[(size_t)j];
         const int m = (int)(gr.size() / 2);
         int *hb = g->h_unr + off;
         for (int i = 0; i < m; i++) hb[3 * i] = gr[2 * (size_t)i], hb[3 * i + 1] = gr[2 * (size_t)i + 1], hb[3 * i + 2] = -1;
+        tab[j] = ShardUnres{g->d_unr + off, m, h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_pin, h->d_rrec,
+                            h->d_anchor};
+        if (m) wq_changed(h);
+        mx = std::max(mx, m);
         off += 3ll * m;
     }
     if (!g->unr_ev) AQ_HIP(hipEventCreateWithFlags(&g->unr_ev, hipEventDisableTiming));
-    AQ_HIP(hipMemcpyAsync(g->d_unr, g->h_unr, sizeof(int) * (size_t)off, hipMemcpyHostToDevice, h0->stream));
+    AQ_HIP(hipMemcpyAsync(g->d_unr, g->h_unr, sizeof(int) * (size_t)need, hipMemcpyHostToDevice, h0->stream));
+    k_group_unreserve<<<dim3((mx + 255) / 256, g->n), 256, 0, h0->stream>>>(
+        reinterpret_cast<const ShardUnres *>(g->d_unr + toff));
+    AQ_HIP(hipGetLastError());
     AQ_HIP(hipEventRecord(g->unr_ev, h0->stream));
-    off = 0;
-    for (int j = 0; j < g->n; j++) {
-        const int m = (int)(g->grants[(size_t)j].size() / 2);
-        if (!m) continue;
-        adlbq_server *h = g->sh[(size_t)j];
-        if (h != h0) AQ_HIP(hipStreamWaitEvent(h->stream, g->unr_ev, 0));
-        int rc;
-        if ((rc = adlbq_unreserve_batch_device(h, m, g->d_unr + off))) return rc;
-        off += 3ll * m;
-    }
+    for (int j = 0; j < g->n; j++)
+        if (g->sh[(size_t)j] != h0) AQ_HIP(hipStreamWaitEvent(g->sh[(size_t)j]->stream, g->unr_ev, 0));
     return ADLBQ_OK;
 }
 
@@ -944,6 +1029,7 @@ int adlbq_steal_group_destroy(adlbq_steal_group *g) {
     if (g->h_app) hipHostFree(g->h_app);
     if (g->d_app) hipFree(g->d_app);
     if (g->app_ev) hipEventDestroy(g->app_ev);
+    if (g->app_done_ev) hipEventDestroy(g->app_done_ev);
     if (g->unr_ev) hipEventDestroy(g->unr_ev);
     delete g;
     return ADLBQ_OK;

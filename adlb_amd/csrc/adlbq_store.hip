@@ -443,25 +443,6 @@ void host_stage_add(adlbq_server *h, const char *name, std::chrono::steady_clock
 
 // ============================================================================ kernels
 
-// Keep anchor[t] >= prio.  Most calls do not raise it, so the anchor is read
-// first; the lanes of a wave that do raise it agree on one atomic per type
-// (a single device-scope word per type would otherwise serialise them).
-// Every lane of the wave must call it (INT_MIN: nothing to raise).
-__device__ __forceinline__ void raise_anchor(long long *anchor, int t, int prio) {
-    bool up = __hip_atomic_load(anchor + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (long long)prio;
-    while (true) {
-        const unsigned long long b = __ballot(up);
-        if (!b) break;
-        const int leader = __ffsll((long long)b) - 1;
-        const int lt = __shfl(t, leader, 64);
-        int m = (up && t == lt) ? prio : INT_MIN;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-        if (__lane_id() == leader) atomicMax(anchor + lt, (long long)m);
-        if (t == lt) up = false;
-    }
-}
-
 struct PutRec {  // staged by the host per Put
     int slot, prio, meta, seq;
     int answer, len, home, clen;
@@ -802,25 +783,7 @@ __global__ void k_unreserve(int slot, int rank, int seq, int newpin, uint32_t *m
 __global__ void k_unreserve_batch(const int *__restrict__ trip, int n, const long long *__restrict__ seq2slot,
                                   long long nseq, uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
                                   long long *anchor) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int t = 0, up = INT_MIN;
-    if (i < n) {
-        int rank = trip[3 * i], seq = trip[3 * i + 1], np = trip[3 * i + 2];
-        long long slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
-        if (slot >= 0) {
-            // meta, pin and the slot's response record (wqseqno, prio) in one round trip
-            const uint32_t m = meta[slot];
-            const int pn = pin[slot];
-            const int4 r0 = rrec[2 * slot], r1 = rrec[2 * slot + 1];
-            if ((m & M_LIVE) && pn == rank && r0.z == seq) {
-                pin[slot] = np;
-                meta[slot] = m & ~M_PINNED;
-                t = m & M_TYPE;
-                up = r1.w;
-            }
-        }
-    }
-    raise_anchor(anchor, t, up);  // available again: keep the anchor above it
+    unreserve_triple(blockIdx.x * blockDim.x + threadIdx.x, trip, n, seq2slot, nseq, meta, pin, rrec, anchor);
 }
 
 // FA_GET_RESERVED for a batch of (rank, wqseqno) pairs (adlb.c:1347-1381:
