@@ -354,7 +354,14 @@ long long adlbq_stat(adlbq_server *h, const char *name);
  * list in one device-wide radix sort when no list's keys differ in their top
  * 6 bits, 0 always sorts list by list; "segsort_async" = 1 (default) sizes
  * that merged sort from the last landed batch's plan instead of reading the
- * list bounds back (a plan that does not hold leaves the sort to k_rank).
+ * list bounds back (a plan that does not hold leaves the sort to k_rank);
+ * "tindex_delta" = capacity of the delta targeted index that Put batches merge
+ * into (0: every Put batch merges into the main index); "fuse_finalize" = 1
+ * runs the batch's finalize inside the ordered choice's launch (up to 8 types,
+ * up to 65,536 Reserves; default 0); "rank_grid" = k_rank's grid (0 = auto);
+ * "profile_every" = stage events on every n-th batch only (adlbq_stat
+ * "gpu_ns:<stage>"); "hist_variant", "select_chunk", "seg_guess" select
+ * measured-and-rejected kernel variants kept for their parity tests.
  * Results never depend on them; tests lower them to force the other paths. */
 int adlbq_set_param(adlbq_server *h, const char *name, long long value);
 const char *adlbq_last_error(void);
