@@ -346,6 +346,7 @@ struct adlbq_server {
     std::string profile_only;                 // empty: every stage
     std::vector<hipEvent_t> event_pool;
     std::unordered_map<std::string, adlbq::StageTimer> timers;
+    std::unordered_map<std::string, long long> hacc;  // always-on host section time, ns ("hacc:<name>")
     std::chrono::steady_clock::time_point stage_host_t0;
 };
 

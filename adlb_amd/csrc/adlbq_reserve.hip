@@ -3571,8 +3571,10 @@ static int ensure_tindex(adlbq_server *h) {
         // copy of two merges ago has run (its event), so the host never waits for the last one
         const int sl = h->tnew_slot;
         h->tnew_slot ^= 1;
+        const auto w0 = std::chrono::steady_clock::now();
         if (h->tnew_ev[sl]) AQ_HIP(hipEventSynchronize(h->tnew_ev[sl]));
         else AQ_HIP(hipEventCreateWithFlags(&h->tnew_ev[sl], hipEventDisableTiming));
+        h->hacc["tindex_wait"] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
         if (m > h->cap_htnew[sl]) {
             if (h->h_tnewk[sl]) AQ_HIP(hipHostFree(h->h_tnewk[sl]));
             if (h->h_tnewv[sl]) AQ_HIP(hipHostFree(h->h_tnewv[sl]));
@@ -4356,12 +4358,23 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     const auto host_t0 = std::chrono::steady_clock::now();
     h->hint_stamp++;  // landed-snapshot hints are looked up once for this launch
     h->reserve_batches++;
+    using hclk = std::chrono::steady_clock;
+    auto hsec = [&](const char *name, hclk::time_point &t) {  // always-on host section timer
+        const auto now = hclk::now();
+        h->hacc[name] += std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+        t = now;
+    };
+    auto ht = host_t0;
     if ((rc = ensure_req_capacity(h, R))) return rc;
+    hsec("req_cap", ht);
     if ((rc = sync_tables(h))) return rc;
+    hsec("tables", ht);
     if ((rc = ensure_rq_capacity(h, R))) return rc;
+    hsec("rq_cap", ht);
     const int T = h->T;
     const int np = (int)h->open.pages.size();
     if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
+    hsec("scan_cap", ht);
     hipStream_t s = h->stream;
     hipEvent_t ev;
 
@@ -4402,6 +4415,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         const auto ti_t0 = std::chrono::steady_clock::now();
         if (nb < (1 << 20) && (rc = ensure_tindex(h))) return rc;
         host_stage_add(h, "tindex", ti_t0);
+        auto tt = ti_t0;
+        hsec("tindex", tt);
         stage_begin(h, "targeted", &ev);
         if (nb < (1 << 20))
             k_targeted_idx<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_tkeys,
@@ -4414,6 +4429,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                           h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);
         stage_end(h, "targeted", ev);
     }
+    auto st0 = hclk::now();
     if (np > 0 && T > 0 && sort_hint(h)) {
         stage_begin(h, "sort", &ev);
         bool planned = false;
@@ -4422,6 +4438,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         if (!planned && (rc = launch_segsort(h))) return rc;
         stage_end(h, "sort", ev);
     }
+    hsec("sort", st0);
     if (np > 0 && T > 0) {
         stage_begin(h, "rank", &ev);
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
@@ -4524,6 +4541,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     h->ctr_stale = true;
     h->rq_n_upper += R;
     h->rq_next_upper += R;
+    auto t_all = host_t0;
+    hsec("total", t_all);
     return ADLBQ_OK;
 }
 

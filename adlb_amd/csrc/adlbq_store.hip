@@ -304,8 +304,10 @@ int sync_tables(adlbq_server *h) {
                      o_pb = o_af + al(nall), o_pw = o_pb + al(npg), total = o_pw + al(npg);
         const int sl = h->tab_slot;
         h->tab_slot ^= 1;
+        const auto w0 = std::chrono::steady_clock::now();
         if (h->tab_ev[sl]) AQ_HIP(hipEventSynchronize(h->tab_ev[sl]));  // its last copy has left the buffer
         else AQ_HIP(hipEventCreateWithFlags(&h->tab_ev[sl], hipEventDisableTiming));
+        h->hacc["tables_wait"] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
         if ((long long)total > h->cap_htab[sl]) {
             if (h->h_tab[sl]) AQ_HIP(hipHostFree(h->h_tab[sl]));
             h->cap_htab[sl] = std::max((long long)total, 2 * h->cap_htab[sl]);
@@ -2211,6 +2213,10 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         return v;
     }
     if (n == "device_sorted_lists") return h->n_segsort;  // candidate lists given a device-wide sort (cumulative)
+    if (n.rfind("hacc:", 0) == 0) {  // cumulative host time of a section of the reserve call
+        auto it = h->hacc.find(n.substr(5));
+        return it == h->hacc.end() ? 0 : it->second;
+    }
     if (n.rfind("host_ns:", 0) == 0) {  // host time issuing a profiled stage (adlbq_profile_only)
         auto it = h->timers.find(n.substr(8));
         return it == h->timers.end() ? 0 : it->second.host_ns;

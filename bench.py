@@ -667,6 +667,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    HACC = ("req_cap", "tables", "tables_wait", "rq_cap", "scan_cap", "tindex", "tindex_wait", "sort", "total")
+    hacc0 = {k: srv.stat("hacc:" + k) for k in HACC}
     t0 = time.perf_counter()
     host = 0.0
     for k in host_parts:
@@ -713,6 +715,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "host_call_parts_ms": {k: round(v * 1e3 / steps, 3) for k, v in host_parts.items()},
         "stages_ms": stages,
         "stages_host_ms": stages_host,
+        "reserve_host_sections_ms": {k: round((srv.stat("hacc:" + k) - hacc0[k]) / 1e6 / max(nb - W4, 1), 4)
+                                     for k in HACC},
         "scaling": "weak",
     }
     if per_batch:
