@@ -3522,6 +3522,31 @@ static int tindex_ranges(adlbq_server *h, int nb) {
     return ADLBQ_OK;
 }
 
+// Stable merge of two sorted key runs with their values: entry i of a lands at
+// i + |{b < key}|, entry j of b at j + |{a <= key}|.
+__global__ __launch_bounds__(256) void k_merge_sorted(const unsigned long long *__restrict__ ak,
+                                                      const int *__restrict__ av, long long na,
+                                                      const unsigned long long *__restrict__ bk,
+                                                      const int *__restrict__ bv, long long nb,
+                                                      unsigned long long *__restrict__ ok, int *__restrict__ ov) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= na + nb) return;
+    const bool from_a = i < na;
+    const unsigned long long key = from_a ? ak[i] : bk[i - na];
+    const int val = from_a ? av[i] : bv[i - na];
+    const unsigned long long *o = from_a ? bk : ak;
+    long long lo = 0, hi = from_a ? nb : na;
+    while (lo < hi) {  // a: first b >= key; b: first a > key
+        const long long mid = (lo + hi) >> 1;
+        const unsigned long long x = o[mid];
+        if (from_a ? x < key : x <= key) lo = mid + 1;
+        else hi = mid;
+    }
+    const long long pos = (from_a ? i : i - na) + lo;
+    ok[pos] = key;
+    ov[pos] = val;
+}
+
 static int ensure_tindex(adlbq_server *h) {
     if (!h->tindex_dirty) return ADLBQ_OK;
     hipStream_t s = h->stream;
@@ -3593,21 +3618,14 @@ static int ensure_tindex(adlbq_server *h) {
         h->tnew_vals.clear();
         const int G = nb * 64;
         int rc;
-        // sorted runs a, b merged into (ok, ov) (rocprim, stable: a's entries first on equal keys)
+        // sorted runs a, b merged into (ok, ov), stable (a's entries first on equal keys):
+        // every entry finds its output position by one binary search in the other run
         auto merge_into = [&](const unsigned long long *ak, const int *av, long long na, const unsigned long long *bk,
                               const int *bv, long long nbk, unsigned long long *ok, int *ov) -> int {
-            size_t tmp = 0;
-            AQ_HIP(rocprim::merge(nullptr, tmp, ak, bk, ok, av, bv, ov, (size_t)na, (size_t)nbk,
-                                  rocprim::less<unsigned long long>(), s));
-            if (tmp > h->cap_tsort) {
-                AQ_HIP(hipStreamSynchronize(s));
-                if (h->d_tsort) AQ_HIP(hipFree(h->d_tsort));
-                h->cap_tsort = std::max(tmp, 2 * h->cap_tsort);
-                AQ_HIP(hipMalloc(&h->d_tsort, h->cap_tsort));
-            }
-            size_t t2 = h->cap_tsort;
-            AQ_HIP(rocprim::merge(h->d_tsort, t2, ak, bk, ok, av, bv, ov, (size_t)na, (size_t)nbk,
-                                  rocprim::less<unsigned long long>(), s));
+            const long long tot = na + nbk;
+            if (tot > 0)
+                k_merge_sorted<<<(unsigned int)((tot + 255) / 256), 256, 0, s>>>(ak, av, na, bk, bv, nbk, ok, ov);
+            AQ_HIP(hipGetLastError());
             return ADLBQ_OK;
         };
         // the main index's bounds after m2 sorted keys (nk) joined it (m2 = 0: new groups only)
