@@ -356,6 +356,8 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    HACC = ("tables", "rq_cap", "scan_cap", "sort", "total")
+    hacc0 = {k: sum(srv.stat("hacc:" + k) for srv in srvs) for k in HACC}
     t0 = time.perf_counter()
     settled = decided = 0
     for b in range(W3, nb):
@@ -385,6 +387,8 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         "decided_per_step": decided / steps,
         "parts_ms_per_step": ({kk: round(v * 1e3 / (nb - W3), 3) for kk, v in {**parts, **sparts}.items()}
                               if args.c3_parts else None),
+        "reserve_host_sections_ms_per_step": {k: round((sum(srv.stat("hacc:" + k) for srv in srvs) - hacc0[k]) / 1e6
+                                                       / (nb - W3), 4) for k in HACC},
         "scaling": "weak",
     }
     bg, bd = group.check()
