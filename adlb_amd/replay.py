@@ -143,3 +143,30 @@ def replay_many(servers, traces, cap_factor: int = 8):
     if rc:  # -2: an output buffer was too small (the servers have moved on: no retry)
         raise RuntimeError(f"adlbsrv_replay_many: {lib.adlbsrv_replay_error().decode(errors='replace')}")
     return [o[: nout[j]].copy() for j, o in enumerate(outs)], [ncall[j] for j in range(n)]
+
+
+def server_process(trace_path: str, out_path: str, user_types, num_app_ranks: int, num_servers: int, idx: int,
+                   device: int, barrier, q) -> None:
+    """One ADLB server as its own process (the reference runs one per MPI rank):
+    loads its recorded stream, warms a throwaway handle up on a prefix, waits at
+    the barrier with the other servers, replays the whole stream through the C
+    ABI (native driver, adlb_replay.cpp) and reports (idx, t_start, t_end,
+    calls); the outputs go to out_path.  Used by bench.py's config-5 leg."""
+    import time
+    try:
+        tr = np.load(trace_path)
+        with Server(user_types, num_app_ranks, num_servers, idx, max_units=1 << 16, device=device) as tmp:
+            replay_many([tmp], [tr[: min(tr.size, 20000)]])
+        with Server(user_types, num_app_ranks, num_servers, idx, max_units=1 << 16, device=device) as srv:
+            barrier.wait(timeout=300)
+            t0 = time.time()
+            got, calls = replay_many([srv], [tr])
+            t1 = time.time()
+        np.save(out_path, got[0])
+        q.put((idx, t0, t1, int(calls[0]), ""))
+    except Exception as e:  # reported to the parent, which fails the leg
+        try:
+            barrier.abort()
+        except Exception:
+            pass
+        q.put((idx, 0.0, 0.0, 0, f"{type(e).__name__}: {e}"))

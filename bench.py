@@ -79,6 +79,7 @@ def parse():
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 stream measurement")
     ap.add_argument("--config5-only", action="store_true", help="only the config-5 leg")
+    ap.add_argument("--c5-procs", type=int, default=1, help="config 5: also run one server process per shard (1)")
     ap.add_argument("--c5-shards", type=int, default=8, help="config 5: server shards (own event stream each)")
     ap.add_argument("--c5-ranks", type=int, default=512, help="config 5: app ranks per shard")
     ap.add_argument("--c5-rounds", type=int, default=60, help="config 5: stream rounds per shard")
@@ -544,17 +545,67 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
     total = sum(n_ev)
     for srv in srvs:
         srv.close()
+    threads = {"value": total / el if same else None, "seconds": el, "parity": bool(same)}
+    # one process per server (ADLB runs each server as its own MPI process): the
+    # same streams, every server process on this GPU, started together at a barrier
+    procs = None
+    if world == 1 and args.c5_procs:
+        procs = c5_server_processes(traces, expect, A, S, local)
     if world > 1:
         el, total = shards.reduce_step_timing(el, total)
         same = all_ranks_true(same)
+    use_procs = procs is not None and procs.get("parity")
+    value = procs["value"] if use_procs else (total / el if same else None)
+    mode = (f"one server process per shard ({S} processes on this GPU, each its own HIP stream)" if use_procs
+            else "the shards' streams replayed concurrently, one host thread and HIP stream each")
     return {"workload": f"config5: {S * world} server shards x a tsp-style stream ({A} ranks, {nr} rounds each: "
-                        f"{sum(n_ev)} events on this GPU in {sum(n_batches)} calls; the shards' streams replayed "
-                        f"concurrently, one host thread and HIP stream each)",
-            "value": total / el if same else None, "unit": "events/s", "seconds": el, "events": total,
+                        f"{sum(n_ev)} events on this GPU in {sum(n_batches)} calls; {mode})",
+            "value": value, "unit": "events/s", "seconds": procs["seconds"] if use_procs else el, "events": total,
             "events_per_call": round(sum(n_ev) / max(sum(n_batches), 1), 1),
-            "parity": bool(same), "parity_with_oracle": bool(same),
+            "parity": bool(same and (procs is None or procs.get("parity"))),
+            "parity_with_oracle": bool(same and (procs is None or procs.get("parity"))),
+            "threads": threads, "processes": procs,
             "cpu_oracle_events_per_s": sum(n_ev) / cpu_s, "cpu_cores": 1,
             "trace_generation_s": round(gen_s, 1), "scaling": "weak"}
+
+
+def c5_server_processes(traces, expect, A, S, device):
+    """Config 5 with every server shard in its own process (adlb_amd.replay.server_process):
+    events/s from the first start to the last end over all of them, outputs checked
+    against the oracle's."""
+    import multiprocessing as mp
+    import shutil
+    import tempfile
+    from adlb_amd import replay
+    d = tempfile.mkdtemp(prefix="c5procs_", dir="/tmp")
+    try:
+        paths = []
+        for i, tr in enumerate(traces):
+            paths.append((os.path.join(d, f"tr{i}.npy"), os.path.join(d, f"out{i}.npy")))
+            np.save(paths[-1][0], tr)
+        ctx = mp.get_context("spawn")  # this process holds the GPU: no fork
+        barrier, q = ctx.Barrier(len(traces)), ctx.Queue()
+        ps = [ctx.Process(target=replay.server_process,
+                          args=(paths[i][0], paths[i][1], [1, 2], A, S, i, device, barrier, q))
+              for i in range(len(traces))]
+        for p in ps:
+            p.start()
+        res = []
+        for _ in ps:
+            res.append(q.get(timeout=400))
+        for p in ps:
+            p.join(timeout=60)
+        errs = [r[4] for r in res if r[4]]
+        if errs:
+            return {"error": errs[0], "parity": False}
+        res.sort()
+        t0, t1 = min(r[1] for r in res), max(r[2] for r in res)
+        same = all(np.array_equal(np.load(paths[r[0]][1]), expect[r[0]]) for r in res)
+        total = sum(int(sum(a.shape[0] for _, a in replay._runs(tr, 2))) for tr in traces)
+        return {"value": total / (t1 - t0) if same else None, "seconds": t1 - t0, "parity": bool(same),
+                "calls": sum(r[3] for r in res), "per_process_s": [round(r[2] - r[1], 4) for r in res]}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def config4_parity(ec, w, puts, applied, reqs, d_resp, d_pout, b, R, server_rank):

@@ -13,4 +13,4 @@ python3 -c "import json;d=json.loads(open('$O/c4.json').read().strip().splitline
 timeout -k 10 300 python3 bench.py --config3-only --no-pmc --no-cpu > $O/c3.json 2> $O/c3.err || { echo c3 failed; exit 1; }
 python3 -c "import json;d=json.loads(open(\"$O/c3.json\").read().strip().splitlines()[-1])[\"config3\"];print(\"c3\",d[\"ms_per_step\"],d[\"parity\"],d[\"reserve_host_sections_ms_per_step\"])"
 timeout -k 10 300 python3 bench.py --config5-only --no-pmc --no-cpu > $O/c5.json 2> $O/c5.err || { echo c5 failed; exit 1; }
-python3 -c "import json;d=json.loads(open(\"$O/c5.json\").read().strip().splitlines()[-1])[\"config5\"];print(\"c5\",d[\"value\"],d[\"parity\"],d[\"seconds\"])"
+python3 -c "import json;d=json.loads(open(\"$O/c5.json\").read().strip().splitlines()[-1])[\"config5\"];print(\"c5\",d[\"value\"],d[\"parity\"],d[\"seconds\"],d[\"threads\"],d[\"processes\"])"
