@@ -3588,10 +3588,18 @@ static int ensure_tindex(adlbq_server *h) {
             AQ_HIP(hipMalloc((void **)&h->d_tnewk, sizeof(unsigned long long) * h->cap_tnew));
             AQ_HIP(hipMalloc((void **)&h->d_tnewv, sizeof(int) * h->cap_tnew));
         }
+        auto tq0 = std::chrono::steady_clock::now();
+        auto tsec = [&](const char *name) {
+            const auto now = std::chrono::steady_clock::now();
+            h->hacc[name] += std::chrono::duration_cast<std::chrono::nanoseconds>(now - tq0).count();
+            tq0 = now;
+        };
+        h->hacc["ti_keys"] += m;
         std::vector<int> ord((size_t)m);
         for (long long i = 0; i < m; i++) ord[(size_t)i] = (int)i;
         const auto &K = h->tnew_keys;
         std::stable_sort(ord.begin(), ord.end(), [&K](int a, int b) { return K[(size_t)a] < K[(size_t)b]; });
+        tsec("ti_sort");
         // pinned host staging, two buffers used in turn: a buffer is rewritten only once the
         // copy of two merges ago has run (its event), so the host never waits for the last one
         const int sl = h->tnew_slot;
@@ -3616,6 +3624,7 @@ static int ensure_tindex(adlbq_server *h) {
         AQ_HIP(hipEventRecord(h->tnew_ev[sl], s));
         h->tnew_keys.clear();
         h->tnew_vals.clear();
+        tsec("ti_stage");
         const int G = nb * 64;
         int rc;
         // sorted runs a, b merged into (ok, ov), stable (a's entries first on equal keys):
@@ -3675,6 +3684,7 @@ static int ensure_tindex(adlbq_server *h) {
             if (h->tidx_groups != (long long)G && (rc = shift_main(h->d_tnewk, 0, h->tidx_n))) return rc;  // new buckets
             k_tindex_bounds<<<(G + 255) / 256, 256, 0, s>>>(h->d_dkeys, (int)h->tdel_n, G, h->d_dstart, h->d_dend);
             AQ_HIP(hipGetLastError());
+            tsec("ti_delta");
             h->tidx_delta_merges++;
             h->tindex_dirty = false;
             return ADLBQ_OK;

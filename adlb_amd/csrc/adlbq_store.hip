@@ -196,10 +196,12 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
         tighten_rq_bound(h, false);
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
+        h->hacc["rq_waits"] += 1;
         tighten_rq_bound(h, true);
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
     }
+    h->hacc["rq_reclaims"] += 1;
     if (h->rq_cap > 0 && h->d_rq_seq) {  // reclaim the slots of dead entries, then the exact count
         k_rq_reclaim<<<1, 1024, 0, h->stream>>>(h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr);
         AQ_HIP(hipGetLastError());
