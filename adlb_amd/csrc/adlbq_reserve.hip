@@ -3618,6 +3618,7 @@ static int ensure_tindex(adlbq_server *h) {
         if (h->tnew_ev[sl]) AQ_HIP(hipEventSynchronize(h->tnew_ev[sl]));
         else AQ_HIP(hipEventCreateWithFlags(&h->tnew_ev[sl], hipEventDisableTiming));
         h->hacc["tindex_wait"] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+        tsec("ti_wait");
         if (m > h->cap_htnew[sl]) {
             if (h->h_tnewk[sl]) AQ_HIP(hipHostFree(h->h_tnewk[sl]));
             if (h->h_tnewv[sl]) AQ_HIP(hipHostFree(h->h_tnewv[sl]));
@@ -3625,18 +3626,22 @@ static int ensure_tindex(adlbq_server *h) {
             AQ_HIP(hipHostMalloc((void **)&h->h_tnewk[sl], sizeof(unsigned long long) * h->cap_htnew[sl], hipHostMallocDefault));
             AQ_HIP(hipHostMalloc((void **)&h->h_tnewv[sl], sizeof(int) * h->cap_htnew[sl], hipHostMallocDefault));
         }
+        tsec("ti_alloc");
         for (long long i = 0; i < m; i++) {
             h->h_tnewk[sl][i] = K[(size_t)ord[(size_t)i]];
             h->h_tnewv[sl][i] = h->tnew_vals[(size_t)ord[(size_t)i]];
         }
+        tsec("ti_fill");
         // read straight from the pinned buffers by a kernel: a small hipMemcpyAsync from host
         // memory waited for the stream's earlier work (~0.45 ms per config-4 Put batch)
         unsigned long long *dk = nullptr;
         int *dv = nullptr;
         AQ_HIP(hipHostGetDevicePointer((void **)&dk, h->h_tnewk[sl], 0));
         AQ_HIP(hipHostGetDevicePointer((void **)&dv, h->h_tnewv[sl], 0));
+        tsec("ti_devptr");
         k_copy_kv<<<(unsigned int)((m + 255) / 256), 256, 0, s>>>(dk, dv, m, h->d_tnewk, h->d_tnewv);
         AQ_HIP(hipGetLastError());
+        tsec("ti_launch");
         AQ_HIP(hipEventRecord(h->tnew_ev[sl], s));
         h->tnew_keys.clear();
         h->tnew_vals.clear();

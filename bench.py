@@ -722,7 +722,7 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         dist.barrier()
     torch.cuda.synchronize()
     HACC = ("req_cap", "tables", "tables_wait", "rq_cap", "scan_cap", "tindex", "tindex_wait", "ti_keys", "ti_sort",
-            "ti_stage", "ti_delta", "sort", "total")
+            "ti_wait", "ti_alloc", "ti_fill", "ti_devptr", "ti_launch", "ti_stage", "ti_delta", "sort", "total")
     hacc0 = {k: srv.stat("hacc:" + k) for k in HACC}
     t0 = time.perf_counter()
     host = 0.0
