@@ -3622,7 +3622,8 @@ static int ensure_tindex(adlbq_server *h) {
         if (m > h->cap_htnew[sl]) {
             if (h->h_tnewk[sl]) AQ_HIP(hipHostFree(h->h_tnewk[sl]));
             if (h->h_tnewv[sl]) AQ_HIP(hipHostFree(h->h_tnewv[sl]));
-            h->cap_htnew[sl] = std::max(m, 2 * h->cap_htnew[sl]);
+            // generous from the start: a pinned reallocation costs milliseconds and synchronises
+            h->cap_htnew[sl] = std::max<long long>({m, 2 * h->cap_htnew[sl], 1ll << 16});
             AQ_HIP(hipHostMalloc((void **)&h->h_tnewk[sl], sizeof(unsigned long long) * h->cap_htnew[sl], hipHostMallocDefault));
             AQ_HIP(hipHostMalloc((void **)&h->h_tnewv[sl], sizeof(int) * h->cap_htnew[sl], hipHostMallocDefault));
         }

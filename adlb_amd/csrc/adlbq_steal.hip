@@ -883,7 +883,7 @@ static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, 
             for (auto *h : g->sh) AQ_HIP(hipStreamSynchronize(h->stream));
             if (g->h_app) AQ_HIP(hipHostFree(g->h_app));
             if (g->d_app) AQ_HIP(hipFree(g->d_app));
-            g->cap_app = std::max(need, 2 * g->cap_app);
+            g->cap_app = std::max<long long>({need, 2 * g->cap_app, 1ll << 18});
             AQ_HIP(hipHostMalloc((void **)&g->h_app, sizeof(int) * g->cap_app, hipHostMallocDefault));
             AQ_HIP(hipMalloc((void **)&g->d_app, sizeof(int) * g->cap_app));
         }
@@ -945,7 +945,7 @@ int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g) {
         for (auto *h : g->sh) AQ_HIP(hipStreamSynchronize(h->stream));
         if (g->h_unr) AQ_HIP(hipHostFree(g->h_unr));
         if (g->d_unr) AQ_HIP(hipFree(g->d_unr));
-        g->cap_unr = std::max(need, 2 * g->cap_unr);
+        g->cap_unr = std::max<long long>({need, 2 * g->cap_unr, 1ll << 18});
         AQ_HIP(hipHostMalloc((void **)&g->h_unr, sizeof(int) * g->cap_unr, hipHostMallocDefault));
         AQ_HIP(hipMalloc((void **)&g->d_unr, sizeof(int) * g->cap_unr));
     }

@@ -312,7 +312,7 @@ int sync_tables(adlbq_server *h) {
         h->hacc["tables_wait"] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
         if ((long long)total > h->cap_htab[sl]) {
             if (h->h_tab[sl]) AQ_HIP(hipHostFree(h->h_tab[sl]));
-            h->cap_htab[sl] = std::max((long long)total, 2 * h->cap_htab[sl]);
+            h->cap_htab[sl] = std::max<long long>({(long long)total * 2, 2 * h->cap_htab[sl], 1ll << 16});
             AQ_HIP(hipHostMalloc((void **)&h->h_tab[sl], sizeof(int) * h->cap_htab[sl], hipHostMallocDefault));
         }
         if ((long long)total > h->cap_dtab) {
@@ -1363,7 +1363,7 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
         if (h->d_putout) AQ_HIP(hipFree(h->d_putout));
         for (int q = 0; q < 2; q++)
             if (h->h_putrec[q]) AQ_HIP(hipHostFree(h->h_putrec[q]));
-        h->cap_put = std::max(n, 2 * h->cap_put);
+        h->cap_put = std::max({n, 2 * h->cap_put, 1 << 14});
         AQ_HIP(hipMalloc((void **)&h->d_putrec, sizeof(PutRec) * 2 * (size_t)h->cap_put));
         AQ_HIP(hipMalloc((void **)&h->d_putout, sizeof(int) * 3 * (size_t)h->cap_put));
         for (int q = 0; q < 2; q++)

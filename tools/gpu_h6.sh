@@ -1,0 +1,11 @@
+#!/bin/bash
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/h6
+mkdir -p $O
+( while true; do date +%s > $O/heartbeat; sleep 20; done ) &
+HB=$!
+trap "kill $HB" EXIT
+timeout -k 10 300 python3 bench.py --config4-only --no-pmc --no-cpu > $O/c4.json 2> $O/c4.err || { echo failed; tail -5 $O/c4.err; exit 1; }
+python3 -c "import json;d=json.loads(open('$O/c4.json').read().strip().splitlines()[-1])['config4'];print(d['ms_per_step'],d['parity'],d['host_call_parts_ms'],d['reserve_host_sections_ms'],d['stages_ms'])"
+timeout -k 10 300 python3 bench.py --config4-only --no-pmc --no-cpu > $O/c4.json 2> $O/c4.err || { echo failed; tail -5 $O/c4.err; exit 1; }
