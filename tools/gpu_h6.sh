@@ -9,3 +9,5 @@ trap "kill $HB" EXIT
 timeout -k 10 300 python3 bench.py --config4-only --no-pmc --no-cpu > $O/c4.json 2> $O/c4.err || { echo failed; tail -5 $O/c4.err; exit 1; }
 python3 -c "import json;d=json.loads(open('$O/c4.json').read().strip().splitlines()[-1])['config4'];print(d['ms_per_step'],d['parity'],d['host_call_parts_ms'],d['reserve_host_sections_ms'],d['stages_ms'])"
 timeout -k 10 300 python3 bench.py --config4-only --no-pmc --no-cpu > $O/c4.json 2> $O/c4.err || { echo failed; tail -5 $O/c4.err; exit 1; }
+timeout -k 10 300 python3 bench.py --config3-only --no-pmc --no-cpu > $O/c3.json 2> $O/c3.err || { echo c3 failed; exit 1; }
+python3 -c "import json;d=json.loads(open(\"$O/c3.json\").read().strip().splitlines()[-1])[\"config3\"];print(\"c3\",d[\"ms_per_step\"],d[\"parity\"],d[\"reserve_host_sections_ms_per_step\"])"
