@@ -201,7 +201,8 @@ def parity_of(fn) -> dict:
 def all_ranks_true(ok: bool) -> bool:
     import torch
     import torch.distributed as dist
-    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
+    from adlb_amd import shards
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64, device=shards._dev_of(dist.get_backend()))
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
 
@@ -792,8 +793,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ADLB_BENCH_REHEARSE=1: rehearse the multi-rank path on fewer GPUs than ranks
+    # (gloo, ranks folded onto the visible devices); timings then mean nothing
+    rehearse = os.environ.get("ADLB_BENCH_REHEARSE") == "1"
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearse else "nccl")
+    if rehearse:
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
