@@ -505,7 +505,7 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
     and Gets go as one batch each, every other event one call.  The same traces
     replayed by the oracle on one core are the CPU figure.  Reports events/s."""
     import oracle
-    from adlb_amd import replay, synth
+    from adlb_amd import replay, shards, synth
     from adlb_amd.server import Server
     S, A, nr = args.c5_shards, args.c5_ranks, args.c5_rounds
     traces, expect = [], []
