@@ -8,5 +8,5 @@ mkdir -p $O
 HB=$!
 trap "kill $HB" EXIT
 export ADLB_BENCH_REHEARSE=1
-timeout -k 10 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 > $O/bench2.json 2> $O/bench2.err
+timeout -k 10 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --config5-only > $O/bench2.json 2> $O/bench2.err
 rc=$?; echo "rc=$rc"; tail -1 $O/bench2.json | cut -c1-1500; if [ $rc -ne 0 ]; then grep -v "^\s*$" $O/bench2.err | tail -30; fi
