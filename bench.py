@@ -359,6 +359,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         dist.barrier()
     torch.cuda.synchronize()
     HACC = ("tables", "rq_cap", "rq_waits", "rq_reclaims", "scan_cap", "sort", "total")
+    HACC_MS = ("tables", "rq_cap", "scan_cap", "sort", "total")
     hacc0 = {k: sum(srv.stat("hacc:" + k) for srv in srvs) for k in HACC}
     t0 = time.perf_counter()
     settled = decided = 0
@@ -390,7 +391,9 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         "parts_ms_per_step": ({kk: round(v * 1e3 / (nb - W3), 3) for kk, v in {**parts, **sparts}.items()}
                               if args.c3_parts else None),
         "reserve_host_sections_ms_per_step": {k: round((sum(srv.stat("hacc:" + k) for srv in srvs) - hacc0[k]) / 1e6
-                                                       / (nb - W3), 4) for k in HACC},
+                                                       / (nb - W3), 4) for k in HACC if k in HACC_MS},
+        "reserve_host_counts_per_step": {k: round((sum(srv.stat("hacc:" + k) for srv in srvs) - hacc0[k]) / (nb - W3), 3)
+                                         for k in HACC if k not in HACC_MS},
         "scaling": "weak",
     }
     bg, bd = group.check()
