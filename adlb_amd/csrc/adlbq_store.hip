@@ -208,12 +208,15 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
         int rc;
         if ((rc = refresh_counters(h))) return rc;  // synchronises
         need = (long long)h->ctr.rq_n + extra;
-        if (need <= h->rq_cap) return ADLBQ_OK;
+        // enough room left for the batches a host may run ahead: done; otherwise grow
+        // now rather than wait and reclaim again at the next batches (config 3 did
+        // both on half its shards every step)
+        if (need + (long long)adlbq_server::NSNAP * extra <= h->rq_cap) return ADLBQ_OK;
     }
     // room for NSNAP batches of this size in flight at once (76 B per entry),
     // so that the wait above is the snapshot ring's, not a reallocation's
     long long nc = std::max<long long>(need, (long long)h->rq_cap * 2);
-    nc = std::max<long long>(nc, std::min<long long>((long long)(adlbq_server::NSNAP + 1) * extra, RQ_GROW_MAX));
+    nc = std::max<long long>(nc, std::min<long long>(need + (long long)(adlbq_server::NSNAP + 1) * extra, RQ_GROW_MAX));
     nc = std::max<long long>(nc, 1024);
     int rc;
     if ((rc = grow(&h->d_rq_rank, h->rq_cap, nc, h->stream))) return rc;
