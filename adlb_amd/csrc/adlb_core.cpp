@@ -91,6 +91,7 @@ struct adlbsrv {
     adlbq_steal_group *grp = nullptr;
     std::map<std::tuple<int, int, int>, int> tq;  // (app rank, type, server) -> units: the engine's tq, mirrored
     long long grp_rounds = 0, grp_settled = 0, rfr_sent = 0;
+    bool want_sent = false;  // a TAG_SRV_STEAL_WANT went to the master since the last round
     std::vector<int> grp_rows;
 
     int rc(int r, const char *what) {
@@ -115,8 +116,18 @@ struct adlbsrv {
         if (it != tq.end() && --it->second <= 0) tq.erase(it);
     }
     void send_rfr(int donor, int rqseqno, const Parked &p) {
-        // in a steal group the next round answers it, unless the donor holds targeted work for the rank
-        if (grp && !tq_has(p.rank, donor)) return;
+        // in a steal group the next round answers it, unless the donor holds targeted work for the rank;
+        // the engine recorded the SS_RFR as outstanding (rfr_to_rank / rfr_out): clear that now, as
+        // the SS_RFR_RESP that never comes would (adlb.c:1877-1878), so a later check_remote (a
+        // targeted Put for the rank landing elsewhere) does not skip the rank as busy
+        if (grp && !tq_has(p.rank, donor)) {
+            adlbq_rfr_done(q, donor, p.rank);
+            if (!want_sent) {  // ask the master for a round (once per round)
+                want_sent = true;
+                send(master, TAG_SRV_STEAL_WANT, nullptr, 0);
+            }
+            return;
+        }
         rfr_sent++;
         int b[WIRE_RFR] = {rqseqno, p.rank};
         std::memcpy(b + 2, p.types, sizeof(p.types));
@@ -695,9 +706,11 @@ int adlbsrv_group_settle(adlbsrv *s, const int *all, int nproc, int *settled) {
                     std::to_string(bad_d) + " settled Reserve(s) no longer parked");
     s->grp_rounds++;
     s->grp_settled += cnt;
+    s->want_sent = false;
     if (settled) *settled = cnt;
-    // Reserves the round could not reach (past rqcap, or behind an undecided one) wait for the next round
-    return 0;
+    // Reserves the round could not reach (past rqcap, or behind an undecided one) wait for the next
+    // round; those a tq donor can serve get their SS_RFR now (the export cleared every RFR record)
+    return s->check_remote();
 }
 
 long long adlbsrv_group_stat(adlbsrv *s, int which) {

@@ -94,6 +94,7 @@ struct Loop {
     long long exh_sum = 0, exh_prev_sum = -1;
     // steal group
     bool group = false;
+    bool steal_want = false;  // master: some server asked for a round (TAG_SRV_STEAL_WANT)
     std::vector<int> blob, blobs;
 };
 Loop *g_loop = nullptr;
@@ -234,6 +235,7 @@ void serve(Loop *L, double max_malloc) {
     const double exh_int = env_d("ADLB_EXHAUST_INTERVAL", 0.5);  // the reference waits 5 s (adlb.c:490)
     const double ds_int = 10.0;
     const double st_int = env_d("ADLB_STEAL_INTERVAL", 0.01);
+    const double st_idle = env_d("ADLB_STEAL_IDLE_INTERVAL", 0.5);
     const int T = (int)g_types.size();
     double t_qm = MPI_Wtime(), t_exh = MPI_Wtime(), t_ds = MPI_Wtime(), t_st = MPI_Wtime();
     std::vector<int> src, buf, one;
@@ -249,7 +251,10 @@ void serve(Loop *L, double max_malloc) {
             exh_poll(L);
             t_exh = t;
         }
-        if (L->group && g_rank == g_master && t - t_st > st_int) {  // open a steal round
+        // open a steal round when a server asked for one (a parked Reserve has a donor by its
+        // qmstat table), at most every st_int; otherwise only every st_idle as a safety net
+        if (L->group && g_rank == g_master && ((L->steal_want && t - t_st > st_int) || t - t_st > st_idle)) {
+            L->steal_want = false;
             to_servers(L, TAG_SRV_STEAL, nullptr, 0);
             steal_round(L);
             t_st = MPI_Wtime();
@@ -355,6 +360,10 @@ void serve(Loop *L, double max_malloc) {
         case TAG_SRV_STEAL:
             MPI_Recv(nullptr, 0, MPI_BYTE, from, tag, g_all, MPI_STATUS_IGNORE);
             if (L->group) steal_round(L);
+            break;
+        case TAG_SRV_STEAL_WANT:
+            MPI_Recv(nullptr, 0, MPI_BYTE, from, tag, g_all, MPI_STATUS_IGNORE);
+            L->steal_want = true;
             break;
         case TAG_SRV_QMSTAT: {
             std::vector<char> m(sizeof(int) * (2 + (size_t)T) + sizeof(double));

@@ -51,7 +51,8 @@ enum {
     TAG_SRV_DONE = 1105,          /* empty: every local app finalized -> master */
     TAG_SRV_END = 1106,           /* empty: master -> all */
     TAG_SRV_ABORT = 1107,         /* int[12] {code} */
-    TAG_SRV_STEAL = 1108          /* empty: master -> all, open a steal-group round */
+    TAG_SRV_STEAL = 1108,         /* empty: master -> all, open a steal-group round */
+    TAG_SRV_STEAL_WANT = 1109     /* empty: any -> master, a parked Reserve has a donor by the qmstat table */
 };
 
 #define WIRE_IBUF 12   /* IBUF_NUMINTS / IBUF_NUMDBLS, adlb.c:89-90 */

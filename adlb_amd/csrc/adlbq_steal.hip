@@ -675,6 +675,7 @@ struct adlbq_steal_group {
     hipEvent_t app_ev = nullptr;
     hipEvent_t app_done_ev = nullptr;  // after k_group_apply: the other shards' streams wait for it
     hipEvent_t unr_ev = nullptr;  // the grants' SS_UNRESERVE staging copy (first shard's stream)
+    std::vector<hipEvent_t> jev;  // join: the first shard's stream waits for every other shard's stream
     long long ns_copy = 0, ns_merge = 0, ns_apply = 0, nreq_last = 0;  // the last settle's host phases
 };
 
@@ -801,6 +802,24 @@ int adlbq_steal_group_settle_host(adlbq_steal_group *g, const int *h_all, int np
 
 }  // extern "C"
 
+// A one-launch settle step (k_group_apply / k_group_unreserve) runs on the
+// first shard's stream but writes every shard's queue: that stream first waits
+// for the work already enqueued on every other shard's stream.
+static int group_join_streams(adlbq_steal_group *g) {
+    adlbq_server *h0 = g->sh[0];
+    if (g->jev.size() != (size_t)g->n) {
+        g->jev.assign((size_t)g->n, nullptr);
+        for (auto &e : g->jev) AQ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    for (int j = 0; j < g->n; j++) {
+        adlbq_server *h = g->sh[(size_t)j];
+        if (h == h0 || h->stream == h0->stream) continue;
+        AQ_HIP(hipEventRecord(g->jev[(size_t)j], h->stream));
+        AQ_HIP(hipStreamWaitEvent(h0->stream, g->jev[(size_t)j], 0));
+    }
+    return ADLBQ_OK;
+}
+
 // The merge and the local side of it over g->h_all = [nproc][n][blob] (any region order).
 static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, int *n_settled,
                                std::chrono::steady_clock::time_point t0, std::chrono::steady_clock::time_point t1) {
@@ -906,6 +925,7 @@ static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, 
             if (!dl.empty()) h->ctr_stale = true;
             off += (long long)gr.size() + (long long)dl.size();
         }
+        if ((rc = group_join_streams(g))) return rc;
         AQ_HIP(hipMemcpyAsync(g->d_app, g->h_app, sizeof(int) * need, hipMemcpyHostToDevice, h0->stream));
         AQ_HIP(hipEventRecord(g->app_ev, h0->stream));
         const int gb = (mg + 255) / 256, db = (md + 255) / 256;
@@ -965,6 +985,8 @@ int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g) {
         off += 3ll * m;
     }
     if (!g->unr_ev) AQ_HIP(hipEventCreateWithFlags(&g->unr_ev, hipEventDisableTiming));
+    int rc;
+    if ((rc = group_join_streams(g))) return rc;
     AQ_HIP(hipMemcpyAsync(g->d_unr, g->h_unr, sizeof(int) * (size_t)need, hipMemcpyHostToDevice, h0->stream));
     k_group_unreserve<<<dim3((mx + 255) / 256, g->n), 256, 0, h0->stream>>>(
         reinterpret_cast<const ShardUnres *>(g->d_unr + toff));
@@ -1031,6 +1053,7 @@ int adlbq_steal_group_destroy(adlbq_steal_group *g) {
     if (g->app_ev) hipEventDestroy(g->app_ev);
     if (g->app_done_ev) hipEventDestroy(g->app_done_ev);
     if (g->unr_ev) hipEventDestroy(g->unr_ev);
+    for (auto &e : g->jev) hipEventDestroy(e);
     delete g;
     return ADLBQ_OK;
 }

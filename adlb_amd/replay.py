@@ -43,6 +43,18 @@ def _runs(tr: np.ndarray, T: int):
             i += w
 
 
+def event_prefix(tr: np.ndarray, T: int, n_ints: int) -> int:
+    """Length of the longest prefix of whole events with at most n_ints ints
+    (at least the first event): a cut that never splits an event."""
+    i = 0
+    while i < tr.size:
+        w = 1 + nargs(int(tr[i]), T)
+        if i + w > n_ints and i > 0:
+            break
+        i += w
+    return min(i, tr.size)
+
+
 def replay(srv: Server, trace) -> np.ndarray:
     tr = np.ascontiguousarray(np.asarray(trace, dtype=np.int32))
     T = srv.T
@@ -156,7 +168,7 @@ def server_process(trace_path: str, out_path: str, user_types, num_app_ranks: in
     try:
         tr = np.load(trace_path)
         with Server(user_types, num_app_ranks, num_servers, idx, max_units=1 << 16, device=device) as tmp:
-            replay_many([tmp], [tr[: min(tr.size, 20000)]])
+            replay_many([tmp], [tr[: event_prefix(tr, len(user_types), 20000)]])
         with Server(user_types, num_app_ranks, num_servers, idx, max_units=1 << 16, device=device) as srv:
             barrier.wait(timeout=300)
             t0 = time.time()

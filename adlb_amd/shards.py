@@ -286,26 +286,40 @@ class StealGroup:
         multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
         if multi and dist.get_backend(group) != "nccl":
             return self._round_host(group, timing, t0)
-        if multi and self._dblob is None:
+        if not multi:
+            self.export_device(None)
+            t0 = _tick(timing, "export", t0)
+            out = self.settle_device(None, 1)
+            _tick(timing, "merge_apply", t0)
+            return out
+        if self._dblob is None:
             dev = torch.device("cuda", torch.cuda.current_device())
             self._dblob = torch.empty(self.blob_ints, dtype=torch.int32, device=dev)
-            w = dist.get_world_size(group)
-            self._gathered = torch.empty(w * self.blob_ints, dtype=torch.int32, device=dev)
-        _lib.check(self.lib.adlbq_steal_group_export(self.g, self._dblob.data_ptr() if multi else None),
-                   "adlbq_steal_group_export")
-        d_all, nproc = None, 1
-        if multi:
-            # the export runs on the shards' streams: the collective's stream waits for them
-            for s in self.servers:
-                s.sync()
-            dist.all_gather_into_tensor(self._gathered, self._dblob, group=group)
-            torch.cuda.current_stream().synchronize()
-            d_all, nproc = self._gathered.data_ptr(), dist.get_world_size(group)
+            self._gathered = torch.empty(dist.get_world_size(group) * self.blob_ints, dtype=torch.int32, device=dev)
+        self.export_device(self._dblob.data_ptr())
+        # the export runs on the shards' streams: the collective's stream waits for them
+        for s in self.servers:
+            s.sync()
+        dist.all_gather_into_tensor(self._gathered, self._dblob, group=group)
+        torch.cuda.current_stream().synchronize()
         t0 = _tick(timing, "export", t0)
-        nd, ns = ctypes.c_int(), ctypes.c_int()
-        _lib.check(self.lib.adlbq_steal_group_settle(self.g, d_all, nproc, ctypes.byref(nd), ctypes.byref(ns)),
-                   "adlbq_steal_group_settle")
+        out = self.settle_device(self._gathered.data_ptr(), dist.get_world_size(group))
         _tick(timing, "merge_apply", t0)
+        return out
+
+    def export_device(self, d_blob):
+        """The device half of a round's first step: every local shard's export
+        into the device buffer d_blob (blob_ints int32; None: an internal one),
+        enqueued on the shards' streams (adlbq_steal_group_export)."""
+        _lib.check(self.lib.adlbq_steal_group_export(self.g, d_blob), "adlbq_steal_group_export")
+
+    def settle_device(self, d_all, nproc: int):
+        """The settle over the device buffer d_all = [nproc][blob_ints] as
+        all_gather_into_tensor lays the processes' blobs out (None with nproc 1:
+        the last export): adlbq_steal_group_settle.  Returns (decided, settled)."""
+        nd, ns = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.adlbq_steal_group_settle(self.g, d_all, int(nproc), ctypes.byref(nd), ctypes.byref(ns)),
+                   "adlbq_steal_group_settle")
         return nd.value, ns.value
 
     def _round_host(self, group, timing, t0):

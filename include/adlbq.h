@@ -253,8 +253,10 @@ int adlbq_steal_group_responses(adlbq_steal_group *g, int cap, int *out15, int *
 /* the units the local shards pinned in the last settle: rows {local shard j, rank, wqseqno} */
 int adlbq_steal_group_grants(adlbq_steal_group *g, int cap, int *out3, int *count);
 int adlbq_steal_group_check(adlbq_steal_group *g, int *bad_grants, int *bad_deletes);
-/* SS_UNRESERVE (adlb.c:2051-2070) of every unit the last settle granted, on
- * the donors' streams (a benchmark restores its queues this way). */
+/* SS_UNRESERVE (adlb.c:2051-2070) of every unit the last settle granted (a
+ * benchmark restores its queues this way): one launch on the first shard's
+ * stream, after the work already enqueued on every shard's stream; every
+ * other shard's stream waits for it. */
 int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g);
 /* host phase times of the last settle: "copy_ns", "merge_ns", "apply_ns"; "requests" merged */
 long long adlbq_steal_group_stat(adlbq_steal_group *g, const char *name);

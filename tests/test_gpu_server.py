@@ -27,6 +27,7 @@ MIX = os.path.join(ROOT, "tests", "apps", "adlb_mix")
 PUSH = os.path.join(ROOT, "tests", "apps", "adlb_push")
 FCALL = os.path.join(ROOT, "tests", "apps", "adlb_fcall")
 NQ_AMD = os.path.join(ROOT, "oracle", "_ref", "nq_amd")
+TSP_AMD = os.path.join(ROOT, "oracle", "_ref", "tsp_amd")
 MPIRUN = "/opt/conda/bin/mpirun"
 
 
@@ -141,11 +142,16 @@ def test_mix_every_unit_once(np_, ns, n, group):
 
 
 @pytest.mark.gpu
-def test_mix_put_rejection_walk():
+@pytest.mark.parametrize("group", ["0", "1"])
+def test_mix_put_rejection_walk(group):
     """hi_malloc small enough that servers reject puts: the client walks the
     servers (ADLB_PUT_REJECTED hints), targeted units land away from their
-    home server (FA_DID_PUT_AT_REMOTE + tq) and are still all consumed."""
-    out, got, exp = _run_mix(6, ["-nservers", "2", "-n", "100", "-len", "2000", "-hi", "120000"])
+    home server (FA_DID_PUT_AT_REMOTE + tq) and are still all consumed.
+    group "1": with the steal group on, an SS_RFR a park would send to a
+    non-tq donor is suppressed and its engine record cleared, so a targeted
+    Put for that rank landing on another server later still reaches it."""
+    out, got, exp, _ = _run_mix(6, ["-nservers", "2", "-n", "100", "-len", "2000", "-hi", "120000"],
+                                env_extra={"ADLB_STEAL_GROUP": group})
     assert got == exp, out[-2000:]
     rej = [float(ln.split()[-1]) for ln in out.splitlines() if ln.startswith("server")]
     assert rej and sum(rej) > 0, out[-2000:]
@@ -189,3 +195,36 @@ def test_fortran_bindings_live():
     assert line, r.stdout[-2000:]
     v = line[0].split()
     assert (int(v[2]), int(v[4])) == (int(v[6]), int(v[7])), r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", ["0", "1"])
+@pytest.mark.parametrize("np_,ns,name", [(5, 2, "tsp_m10.txt"), (6, 3, "tsp_m11.txt"), (3, 1, "tsp_m9.txt")])
+def test_tsp_relinked(np_, ns, name, group):
+    """The reference's examples/tsp.c compiled unchanged against
+    include/adlb/adlb.h and linked to adlb_amd/libadlb.so (oracle/_ref/tsp_amd):
+    targeted BOUND_UPDT units at prio 999999999 down the app tree
+    (tsp.c:189-193, 251-252), {2, 1} Reserves (157-161), batched work Puts at
+    prio 1 + len (240-241), ended by exhaustion.  Rank 0 must print the bdist
+    the reference build printed on the same matrix, which is also the
+    Held-Karp optimum (tests/golden/gen_tsp.py, tsp_expected.json).  group
+    "1": the node's servers settle parked Reserves by steal rounds."""
+    import json
+    if not os.path.exists(TSP_AMD):
+        pytest.skip("oracle/_ref/tsp_amd not built (needs the reference sources in the build container)")
+    with open(os.path.join(GOLD, "tsp_expected.json")) as f:
+        exp = json.load(f)[name]
+    env = dict(os.environ, ADLB_DEVICE="0", ADLB_STEAL_GROUP=group)
+    with open(os.path.join(GOLD, name)) as f:
+        r = subprocess.run([MPIRUN, "-np", str(np_), TSP_AMD, "-nservers", str(ns)], stdin=f, env=env,
+                           capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"rc={r.returncode}\nstdout:\n{r.stdout[-3000:]}\nstderr:\n{r.stderr[-3000:]}"
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("bdist ")]
+    assert line, r.stdout[-2000:]
+    assert int(line[0].split()[1]) == exp["reference_bdist"] == exp["held_karp"], r.stdout[-2000:]
+    path = [ln for ln in r.stdout.splitlines() if ln.startswith("bpath ")][0].split()[1:]
+    assert sorted(int(c) for c in path[:-1]) == list(range(exp["n"])) and path[0] == path[-1] == "0"
+    with open(os.path.join(GOLD, name)) as f:
+        v = [int(x) for x in f.read().split()]
+    n, d = v[0], v[1:]
+    assert sum(d[int(a) * n + int(b)] for a, b in zip(path[:-1], path[1:])) == exp["held_karp"]

@@ -115,3 +115,75 @@ def test_steal_group_two_processes_vs_oracle(gpu_available):
         assert res[r][1] == "ok", res[r][1]
     assert sum(res[r][2] for r in range(world)) > 0
     assert res[0][3] == res[1][3]          # both processes ran the same rounds
+
+
+def test_steal_group_device_blobs_two_groups_vs_oracle(gpu_available):
+    """The RCCL branch of StealGroup.round without the collective: two
+    StealGroups of two HIP shards each (the shards two GPU processes would
+    hold) export into adjacent halves of ONE device tensor -- exactly the
+    [nproc][blob] layout all_gather_into_tensor delivers -- and each settles
+    over it with nproc = 2 (adlbq_steal_group_export(g, d_blob) ->
+    adlbq_steal_group_settle(g, d_all, 2)).  Settlements, qmstat rows and a
+    follow-up Reserve batch per shard must equal oracle.serial_steal_round and
+    the oracle shards (adlb.c:1802-1933, 3536-3579)."""
+    import torch
+
+    import oracle
+    from adlb_amd import replay, shards, synth
+    from adlb_amd.server import Server
+    from steal_case import build_case
+
+    ws, orcs, resps = build_case(S, N_UNITS, R, SEED, **KW)
+    groups_of = [[0, 1], [2, 3]]
+    srvs = {s: Server(ws[s].user_types, ws[s].num_app_ranks, S, s, max_units=ws[s].n_units) for s in range(S)}
+    grps = [shards.StealGroup([srvs[s] for s in m], K, rqcap=1 << 14) for m in groups_of]
+    try:
+        for s in range(S):
+            out = synth.split_outputs(replay.replay(srvs[s], synth.workload_trace(ws[s])))
+            np.testing.assert_array_equal(np.asarray(out[ws[s].n_units:], np.int32), resps[s])
+        bi = grps[0].blob_ints
+        assert grps[1].blob_ints == bi
+        d_all = torch.full((2 * bi,), -7, dtype=torch.int32, device="cuda:0")
+        got = [[] for _ in grps]
+        nrounds = 0
+        while True:
+            for p, g in enumerate(grps):       # each "process" exports into its slot
+                g.export_device(d_all.data_ptr() + p * bi * 4)
+            for s in srvs.values():            # as StealGroup.round does before the collective
+                s.sync()
+            res = [g.settle_device(d_all.data_ptr(), 2) for g in grps]
+            assert res[0] == res[1], "both processes must decide and settle the same round"
+            for p, g in enumerate(grps):
+                assert g.check() == (0, 0)
+                got[p].append(g.responses())
+            nrounds += 1
+            if res[0][1] == 0:
+                break
+        assert nrounds >= 2
+        exp = oracle.serial_steal_round(orcs, ws[0].num_app_ranks)
+        assert exp.shape[0] > 0
+        for p, m in enumerate(groups_of):
+            gp = np.concatenate(got[p])
+            e = exp[np.isin(exp[:, 0], m)]
+            assert e.shape[0] > 0, f"no settlement lands on group {p}"
+            np.testing.assert_array_equal(gp[np.lexsort((gp[:, 1], gp[:, 0]))], e[np.lexsort((e[:, 1], e[:, 0]))])
+        rng = np.random.default_rng(SEED)
+        for s in range(S):
+            srv, o, w = srvs[s], orcs[s], ws[s]
+            qn, hi = srv.qmstat_row()
+            oq, ohi = o.qmrow()
+            assert qn == oq and hi.tolist() == ohi.tolist()
+            rfr = [[synth.OP_RFRDONE, int(r[11]), int(rk)] for r, rk in zip(resps[s], w.r_rank)
+                   if r[0] == 0 and r[11] >= 0]
+            if rfr:
+                o.replay(np.asarray(rfr, np.int32).ravel())
+            tv = synth.type_vectors(rng, w.user_types, 256)
+            tr = np.concatenate([synth.simple_events(synth.OP_INFO),
+                                 synth.reserve_events(np.arange(256) * S + s, tv, np.zeros(256, np.uint8)),
+                                 synth.simple_events(synth.OP_INFO)])
+            np.testing.assert_array_equal(replay.replay(srv, tr), o.replay(tr))
+    finally:
+        for g in grps:
+            g.close()
+        for srv in srvs.values():
+            srv.close()

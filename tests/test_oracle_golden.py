@@ -49,3 +49,24 @@ def test_own_vs_ref_random_small():
             o.init(w.user_types, w.num_app_ranks)
             outs.append(o.replay(tr))
         assert np.array_equal(outs[0], outs[1])
+
+
+def test_tsp_fixtures_consistent():
+    """tests/golden/tsp_m*.txt are gen_tsp.py's seeded matrices, and the
+    recorded reference bdist (oracle/_ref/tsp under mpirun, tsp.c:262) equals
+    the Held-Karp optimum of each matrix."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import gen_tsp
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(gold, "tsp_expected.json")) as f:
+        exp = json.load(f)
+    assert set(exp) == {f"tsp_m{n}.txt" for n in gen_tsp.SIZES}
+    for name, rec in exp.items():
+        with open(os.path.join(gold, name)) as f:
+            v = np.array(f.read().split(), dtype=np.int64)
+        n = int(v[0])
+        d = v[1:].reshape(n, n)
+        np.testing.assert_array_equal(d, gen_tsp.matrix(n))
+        assert rec["reference_bdist"] == rec["held_karp"] == gen_tsp.held_karp(d)
