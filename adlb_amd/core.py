@@ -26,6 +26,9 @@ SIGNATURES = {
     "adlbsrv_last_error": (ctypes.c_char_p, []),
     "adlbsrv_put_hdr": (c_int, [P, c_int, P, P]),
     "adlbsrv_put_payload": (c_int, [P, c_int, P, P, c_int]),
+    "adlbsrv_put_stage": (c_int, [P, c_int, P, P, c_int]),
+    "adlbsrv_put_flush": (c_int, [P]),
+    "adlbsrv_put_staged": (c_int, [P]),
     "adlbsrv_put_common_hdr": (c_int, [P, c_int, c_int, P]),
     "adlbsrv_put_common_payload": (c_int, [P, c_int, P, c_int]),
     "adlbsrv_batch_done": (c_int, [P, c_int, c_int, c_int]),
@@ -123,6 +126,23 @@ class Core:
         if need.value:
             b = ctypes.create_string_buffer(payload, len(payload))
             self._chk(load().adlbsrv_put_payload(self._h, src, h.ctypes.data, b, len(payload)), "put_payload")
+        return self._take()
+
+    def put_run(self, puts):
+        """A run of FA_PUT_HDRs as libadlb.so's loop drains it: each header
+        checked and acked in turn, the accepted payloads staged, then one
+        engine batch (adlbsrv_put_stage / adlbsrv_put_flush).  puts: [(src,
+        hdr12, payload)]."""
+        lib = load()
+        need = c_int()
+        for src, hdr12, payload in puts:
+            h = _i32(hdr12)
+            self._chk(lib.adlbsrv_put_hdr(self._h, src, h.ctypes.data, ctypes.byref(need)), "put_hdr")
+            if need.value:
+                b = ctypes.create_string_buffer(payload, len(payload))
+                self._chk(lib.adlbsrv_put_stage(self._h, src, h.ctypes.data, b, len(payload)), "put_stage")
+        self._chk(lib.adlbsrv_put_flush(self._h), "put_flush")
+        assert lib.adlbsrv_put_staged(self._h) == 0
         return self._take()
 
     def put_common(self, src: int, common_len: int, payload: bytes):

@@ -52,6 +52,13 @@ struct Held {  // a unit accepted by SS_PUSH_QUERY, until SS_PUSH_HDR / SS_PUSH_
     double t = 0.0;  // the pusher's time stamp (dbls_info_buf[4], adlb.c:2150)
 };
 
+struct Staged {  // an accepted Put whose payload arrived, not yet appended
+    int src = -1;
+    int u[ADLBQ_PUT_INTS];
+    int hdr[WIRE_IBUF];
+    std::vector<char> buf;
+};
+
 struct Parked {
     int rank = -1;
     int types[WIRE_REQ];
@@ -92,6 +99,11 @@ struct adlbsrv {
     std::map<std::tuple<int, int, int>, int> tq;  // (app rank, type, server) -> units: the engine's tq, mirrored
     long long grp_rounds = 0, grp_settled = 0, rfr_sent = 0;
     bool want_sent = false;  // a TAG_SRV_STEAL_WANT went to the master since the last round
+    // staged Puts (adlbsrv_put_stage / _flush): payloads in arrival order, the
+    // exact byte count when staging began and the bytes the staged Puts add
+    std::vector<Staged> staged;
+    double staged_base = 0.0, staged_add = 0.0;
+    std::vector<int> su, so;
     std::vector<int> grp_rows;
 
     int rc(int r, const char *what) {
@@ -223,42 +235,103 @@ int adlbsrv_destroy(adlbsrv *s) {
     return 0;
 }
 
+static int put_reject(adlbsrv *s, int src, int len) {  // adlb.c:908-931 (nothing changed since the byte read)
+    int rej = 0, hint = -1;
+    if (s->rc(adlbq_put_check(s->q, len, s->max_malloc, &rej, &hint), "adlbq_put_check")) return -1;
+    if (!rej) return fail("FA_PUT_HDR: memory check changed its answer");
+    s->num_rejected++;
+    int b[WIRE_IBUF] = {WIRE_PUT_REJECTED, hint, 1};
+    s->send_ints(src, TAG_ACK_AND_RC, b, WIRE_IBUF);
+    return 0;
+}
+
 int adlbsrv_put_hdr(adlbsrv *s, int src, const int *hdr, int *need_payload) {
     *need_payload = 0;
     if (s->nmw) {  // adlb.c:894-901
         s->send_rc(src, TAG_ACK_AND_RC, WIRE_NO_MORE_WORK);
         return 0;
     }
-    int rej = 0, hint = -1;
-    if (s->rc(adlbq_put_check(s->q, hdr[4], s->max_malloc, &rej, &hint), "adlbq_put_check")) return -1;
-    if (rej) {  // adlb.c:908-931
-        s->num_rejected++;
-        int b[WIRE_IBUF] = {WIRE_PUT_REJECTED, hint, 1};
-        s->send_ints(src, TAG_ACK_AND_RC, b, WIRE_IBUF);
-        return 0;
+    const int len = hdr[4];
+    if (!s->staged.empty()) {
+        // curr_bytes_dmalloced after the staged Puts is at most hi (an rq match frees one parked
+        // Reserve's node, adlb.c:1040, so it may be lower)
+        const double hi = s->staged_base + s->staged_add;
+        if (!(hi + len > s->max_malloc)) {  // accepted whatever the staged Puts match
+            s->send_rc(src, TAG_ACK_AND_RC, WIRE_SUCCESS);
+            *need_payload = 1;
+            return 0;
+        }
+        if (adlbsrv_put_flush(s)) return -1;  // undecided, or a rejection: exact, from the appended queue
     }
+    double curr = 0.0, hwm = 0.0;
+    if (s->rc(adlbq_bytes(s->q, &curr, &hwm), "adlbq_bytes")) return -1;
+    if (curr + len > s->max_malloc) return put_reject(s, src, len);  // adlb.c:908-931
+    s->staged_base = curr;
+    s->staged_add = 0.0;
     s->send_rc(src, TAG_ACK_AND_RC, WIRE_SUCCESS);  // adlb.c:960-961
     *need_payload = 1;
     return 0;
 }
 
-int adlbsrv_put_payload(adlbsrv *s, int src, const int *hdr, const void *buf, int len) {
-    // wq_node_create + wq_append, then rq_find_rank_queued_for_type (adlb.c:963-988)
-    const int u[ADLBQ_PUT_INTS] = {hdr[0], hdr[1], hdr[2], hdr[3], hdr[4], hdr[5], hdr[7], hdr[8], hdr[9]};
-    int o[3];
-    if (s->rc(adlbq_put_batch(s->q, 1, u, o), "adlbq_put_batch")) return -1;
+static void put_fields(const int *hdr, int *u) {
+    const int v[ADLBQ_PUT_INTS] = {hdr[0], hdr[1], hdr[2], hdr[3], hdr[4], hdr[5], hdr[7], hdr[8], hdr[9]};
+    std::memcpy(u, v, sizeof v);
+}
+
+// the append's replies (adlb.c:989-1049): the parked Reserve that gets the unit, then the final ack
+static void put_done(adlbsrv *s, int src, const int *hdr, const int *u, const int *o, const char *buf, int len) {
     Unit &unit = s->units[o[0]];
-    unit.buf.assign((const char *)buf, (const char *)buf + (len > 0 ? len : 0));
+    unit.buf.assign(buf, buf + (len > 0 ? len : 0));
     unit.t = now();
-    std::memcpy(unit.fields, u, sizeof u);
+    std::memcpy(unit.fields, u, sizeof(int) * ADLBQ_PUT_INTS);
     unit.has_fields = true;
     s->activity++;
-    if (o[1] >= 0) {  // the parked Reserve gets this unit (adlb.c:989-1042)
+    if (o[1] >= 0) {
         int b[WIRE_IBUF] = {WIRE_SUCCESS, hdr[0], hdr[1], hdr[4], hdr[2], o[0], s->me, hdr[7], hdr[8], hdr[9]};
         s->send_ints(o[1], TAG_RESERVE_RESP, b, WIRE_IBUF);
         s->served(o[2]);
     }
-    s->send_rc(src, TAG_ACK_AND_RC, WIRE_SUCCESS);  // adlb.c:1048-1049
+    s->send_rc(src, TAG_ACK_AND_RC, WIRE_SUCCESS);
+}
+
+int adlbsrv_put_payload(adlbsrv *s, int src, const int *hdr, const void *buf, int len) {
+    // wq_node_create + wq_append, then rq_find_rank_queued_for_type (adlb.c:963-988)
+    if (!s->staged.empty() && adlbsrv_put_flush(s)) return -1;
+    int u[ADLBQ_PUT_INTS], o[3];
+    put_fields(hdr, u);
+    if (s->rc(adlbq_put_batch(s->q, 1, u, o), "adlbq_put_batch")) return -1;
+    put_done(s, src, hdr, u, o, (const char *)buf, len);
+    return 0;
+}
+
+int adlbsrv_put_stage(adlbsrv *s, int src, const int *hdr, const void *buf, int len) {
+    Staged st;
+    st.src = src;
+    put_fields(hdr, st.u);
+    std::memcpy(st.hdr, hdr, sizeof st.hdr);
+    st.buf.assign((const char *)buf, (const char *)buf + (len > 0 ? len : 0));
+    s->staged.push_back(std::move(st));
+    s->staged_add += (double)(24 + 72) + (double)(len > 0 ? len : 0);  // pmalloc + wq_node_create
+    return 0;
+}
+
+int adlbsrv_put_staged(adlbsrv *s) { return (int)s->staged.size(); }
+
+int adlbsrv_put_flush(adlbsrv *s) {
+    const int n = (int)s->staged.size();
+    if (!n) return 0;
+    s->su.resize((size_t)n * ADLBQ_PUT_INTS);
+    s->so.resize(3 * (size_t)n);
+    for (int i = 0; i < n; i++) std::memcpy(&s->su[(size_t)i * ADLBQ_PUT_INTS], s->staged[(size_t)i].u, sizeof(int) * ADLBQ_PUT_INTS);
+    std::vector<Staged> st;
+    st.swap(s->staged);
+    s->staged_add = 0.0;
+    if (s->rc(adlbq_put_batch(s->q, n, s->su.data(), s->so.data()), "adlbq_put_batch")) return -1;
+    for (int i = 0; i < n; i++) {
+        const Staged &p = st[(size_t)i];
+        put_done(s, p.src, p.hdr, &s->su[(size_t)i * ADLBQ_PUT_INTS], &s->so[3 * (size_t)i], p.buf.data(),
+                 (int)p.buf.size());
+    }
     return 0;
 }
 

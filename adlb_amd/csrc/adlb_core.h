@@ -31,6 +31,18 @@ const char *adlbsrv_last_error(void);
  * adlbsrv_put_payload (adlb.c:963-1049). */
 int adlbsrv_put_hdr(adlbsrv *s, int src, const int *hdr12, int *need_payload);
 int adlbsrv_put_payload(adlbsrv *s, int src, const int *hdr12, const void *buf, int len);
+/* Batched Puts (the MPI loop drains a run of waiting FA_PUT_HDRs): _stage
+ * keeps an accepted Put's payload instead of appending it, _flush appends
+ * every staged Put with one adlbq_put_batch (arrival order: the same queue
+ * and rq matches as one at a time) and sends, per Put in order, the
+ * TA_RESERVE_RESP of a matched parked Reserve and the final ack.  While Puts
+ * are staged, adlbsrv_put_hdr's memory check (adlb.c:908) is decided from
+ * exact bounds on the staged Puts' bytes (each adds BYTES_WQ + len and an rq
+ * match frees BYTES_RQ); an undecidable check flushes first.  Every other
+ * handler requires nothing staged (the driver flushes at the end of the run). */
+int adlbsrv_put_stage(adlbsrv *s, int src, const int *hdr12, const void *buf, int len);
+int adlbsrv_put_flush(adlbsrv *s);
+int adlbsrv_put_staged(adlbsrv *s);
 /* FA_PUT_COMMON_HDR / _MSG (adlb.c:1054-1134), FA_PUT_BATCH_DONE (1135-1160),
  * FA_GET_COMMON (1321-1332) */
 int adlbsrv_put_common_hdr(adlbsrv *s, int src, int common_len, int *need_payload);

@@ -236,6 +236,9 @@ void serve(Loop *L, double max_malloc) {
     const double ds_int = 10.0;
     const double st_int = env_d("ADLB_STEAL_INTERVAL", 0.01);
     const double st_idle = env_d("ADLB_STEAL_IDLE_INTERVAL", 0.5);
+    // ADLB_PUT_BATCH=0: every Put appended on its own (the one-at-a-time path, for comparison)
+    const bool put_batching = env_d("ADLB_PUT_BATCH", 1.0) != 0.0;
+    const int put_cap = 4096;
     const int T = (int)g_types.size();
     double t_qm = MPI_Wtime(), t_exh = MPI_Wtime(), t_ds = MPI_Wtime(), t_st = MPI_Wtime();
     std::vector<int> src, buf, one;
@@ -272,14 +275,28 @@ void serve(Loop *L, double max_malloc) {
         const int from = st.MPI_SOURCE, tag = st.MPI_TAG;
         switch (tag) {
         case TAG_PUT_HDR: {
-            int h[WIRE_IBUF], need = 0;
-            recv_ints<WIRE_IBUF>(h, from, tag);
-            check(adlbsrv_put_hdr(g_srv, from, h, &need), "FA_PUT_HDR");
-            if (need) {
-                std::vector<char> p((size_t)std::max(h[4], 0));
-                MPI_Recv(p.data(), h[4], MPI_BYTE, from, TAG_PUT_MSG, g_all, MPI_STATUS_IGNORE);
-                check(adlbsrv_put_payload(g_srv, from, h, p.data(), h[4]), "FA_PUT_MSG");
+            // a run of waiting FA_PUT_HDRs: each acked and its payload received in turn
+            // (adlb.c:891-962), the appends and rq matches as one engine batch (963-1049)
+            int src_put = from, nput = 0;
+            std::vector<char> p;
+            while (true) {
+                int h[WIRE_IBUF], need = 0;
+                recv_ints<WIRE_IBUF>(h, src_put, TAG_PUT_HDR);
+                check(adlbsrv_put_hdr(g_srv, src_put, h, &need), "FA_PUT_HDR");
+                if (need) {
+                    p.resize((size_t)std::max(h[4], 1));
+                    MPI_Recv(p.data(), h[4], MPI_BYTE, src_put, TAG_PUT_MSG, g_all, MPI_STATUS_IGNORE);
+                    if (put_batching) check(adlbsrv_put_stage(g_srv, src_put, h, p.data(), h[4]), "FA_PUT_MSG");
+                    else check(adlbsrv_put_payload(g_srv, src_put, h, p.data(), h[4]), "FA_PUT_MSG");
+                }
+                if (++nput >= put_cap) break;
+                int more = 0;
+                MPI_Status pst;
+                MPI_Iprobe(MPI_ANY_SOURCE, TAG_PUT_HDR, g_all, &more, &pst);
+                if (!more) break;
+                src_put = pst.MPI_SOURCE;
             }
+            check(adlbsrv_put_flush(g_srv), "FA_PUT_MSG (batch)");
             break;
         }
         case TAG_RESERVE:

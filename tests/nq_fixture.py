@@ -77,8 +77,10 @@ def normalise(kind, dest, tag, b):
     return (dest, tag, bytes(b))  # payloads
 
 
-def replay(core, fx: Fixture, batch: bool = True):
-    """Feed the fixture's events to a Core; returns [(kind, dest, tag, bytes)]."""
+def replay(core, fx: Fixture, batch: bool = True, put_batch: bool = False):
+    """Feed the fixture's events to a Core; returns [(kind, dest, tag, bytes)].
+    put_batch: runs of Puts go through Core.put_run as libadlb.so drains them
+    (replies then differ in order across destinations only: compare_per_dest)."""
     out = []
     ev = fx.events
     i = 0
@@ -94,6 +96,14 @@ def replay(core, fx: Fixture, batch: bool = True):
                 r = core.reserve_batch(srcs, np.stack([ints(ev[k][2], 17) for k in range(i, j)]))
             else:
                 r = core.get_batch(srcs, [int(ints(ev[k][2])[0]) for k in range(i, j)])
+            out.extend((kind, d, t, x) for d, t, x in r)
+            i = j
+            continue
+        if kind == "put" and put_batch:
+            j = i + 1
+            while j < len(ev) and ev[j][0] == "put":
+                j += 1
+            r = core.put_run([(ev[k][1], ints(ev[k][2][:48]), ev[k][2][48:]) for k in range(i, j)])
             out.extend((kind, d, t, x) for d, t, x in r)
             i = j
             continue
@@ -139,4 +149,26 @@ def compare(got, exp):
             return f"reply {k}: got {a} expected {b} (caused by {exp[k][0]})"
     if len(g) != len(e):
         return f"{len(g)} replies, expected {len(e)}"
+    return None
+
+
+def compare_per_dest(got, exp):
+    """First mismatch of the reply sequence to some destination, or None: a
+    batched run of Puts reorders replies across destinations only (MPI orders
+    messages per sender-receiver pair)."""
+    def by_dest(x):
+        d = {}
+        for r in x:
+            n = normalise(*r)
+            d.setdefault(n[0], []).append(n)
+        return d
+    g, e = by_dest(got), by_dest(exp)
+    if set(g) != set(e):
+        return f"destinations differ: got {sorted(g)} expected {sorted(e)}"
+    for dest in sorted(e):
+        for k, (a, b) in enumerate(zip(g[dest], e[dest])):
+            if a != b:
+                return f"dest {dest} reply {k}: got {a} expected {b}"
+        if len(g[dest]) != len(e[dest]):
+            return f"dest {dest}: {len(g[dest])} replies, expected {len(e[dest])}"
     return None

@@ -54,6 +54,23 @@ def test_nq_event_stream_replay(name, batch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", [f for f in FIXTURES if f not in REF_UB])
+def test_event_stream_replay_put_runs(name):
+    """The recorded streams with every run of Puts drained the way libadlb.so
+    drains waiting FA_PUT_HDRs (each acked in turn, one engine batch for the
+    appends and rq matches: adlbsrv_put_stage / _flush): every destination
+    receives exactly the reference server's replies in the same order."""
+    from adlb_amd.core import Core
+    from nq_fixture import compare_per_dest
+    fx = Fixture(os.path.join(GOLD, name))
+    with Core(fx.types, fx.A, fx.S, fx.me, max_malloc=fx.max_malloc, device=0) as core:
+        got = replay(core, fx, batch=True, put_batch=True)
+        assert core.num_parked() == 0
+    err = compare_per_dest(got, fx.expected())
+    assert err is None, f"{name}: {err}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("batch", [True, False])
 @pytest.mark.parametrize("name", sorted(REF_UB))
 def test_ref_ub_stream_until_suppressed_rfr(name, batch):
