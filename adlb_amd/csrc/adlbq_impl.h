@@ -211,6 +211,7 @@ struct adlbq_server {
     int cap_req = 0;
     unsigned long long *d_mask = nullptr;
     int *d_tmatch = nullptr, *d_umatch = nullptr;
+    int *d_mslot = nullptr;            // [cap_req] the slot the last reserve batch gave request j (-1: none)
     int *d_reqbuf = nullptr, *d_respbuf = nullptr;  // host-API staging
     int *d_dem = nullptr;              // [T]
     int *d_theta = nullptr;            // [T] threshold bin (-1 none)
@@ -219,7 +220,9 @@ struct adlbq_server {
     int *d_binoff = nullptr;           // [T*NB]
     unsigned int *d_coltot = nullptr;  // [T*NB] column totals (k_thresholds)
     int *d_type_cnt = nullptr;         // [T] k_thresholds arrival counters (zero between batches)
-    int *d_rank_sync = nullptr;        // [ADLBQ_MAX_TYPES + 2] k_rank's in-launch sort: epochs, ticket, timeouts
+    int *d_rank_sync = nullptr;        // [ADLBQ_MAX_TYPES + 6] k_rank's in-launch sort: epochs, ticket, timeouts;
+                                       // then k_chain0's rank grid barrier (arrivals, released epoch), then
+                                       // k_prep_hist's folded-thresholds counters (arrivals, finished roles)
     unsigned int rank_epoch = 0;       // per reserve batch, never 0 once used
     unsigned short *d_gh = nullptr; long long cap_gh = 0;   // [open pages][T*NB]
     unsigned int *d_spec = nullptr; int *d_specn = nullptr; long long cap_spec = 0;  // [open pages][4][SPEC_CAP], [open pages][4]
@@ -314,6 +317,9 @@ struct adlbq_server {
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int fuse_finalize = 0;             // "fuse_finalize": k_finalize inside the final k_chain0 launch (measured even: off)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
+    int fuse_rank = 0;
+    int fold_thresholds = 0;
+    int *d_fold = nullptr;             // k_prep_hist's folded-thresholds arrival counters           // "fold_thresholds": k_thresholds' work in pass 1's last workgroups                 // "fuse_rank": T <= 8, no k_rank launch; k_chain0 ranks when k_select_open did not
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]

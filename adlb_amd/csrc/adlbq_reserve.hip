@@ -438,14 +438,6 @@ __device__ __forceinline__ void hist_page_v0(const HistArgs &a, const int p, uns
 // workgroups [0, nprep) prepare 256 requests each, the rest count one page.
 constexpr int PREP_LDS = (int)sizeof(int) * PREP_BLOCK * PREP_ROW;
 
-template <int TB, int PPB = 1>
-__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha) {
-    static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
-    extern __shared__ unsigned int lds[];
-    if ((int)blockIdx.x < nprep) prep_block<TB>(pa, blockIdx.x, reinterpret_cast<int *>(lds));
-    else if (ha.variant == 0) hist_page_v0(ha, blockIdx.x - nprep, lds);
-    else hist_pages<PPB>(ha, (blockIdx.x - nprep) * PPB, lds);
-}
 
 // The lowest prio in bins 0..th of a type with anchor an (bin_of: exact bins
 // below NBX, then powers of two); no bin (th < 0) cuts above every prio.
@@ -453,6 +445,64 @@ __device__ __forceinline__ long long cut_of(int th, long long an) {
     if (th < 0) return 1ll << 40;
     const long long dmax = bin_hi(th);
     return std::max(an - dmax, (long long)LOWEST + 1);
+}
+
+// Type t's threshold, by wave 0 of the workgroup whose column of type t
+// arrived last (lane b = bin b): the bin where the demand is reached and how
+// many units of it are needed; the next anchor and guessed cut.
+__device__ void type_threshold(const int t, const int *__restrict__ dem, int *theta, int *need, int *candlen,
+                               int *needsort, int *binoff, const unsigned int *coltot, int *type_cnt,
+                               const long long *__restrict__ anchor, long long *__restrict__ anchor_next,
+                               long long *__restrict__ gcut_next, int guess) {
+    const int lane = threadIdx.x & 63;
+    // the last column of type t: wave 0, lane b = bin b (NB == 64), all totals loaded at once
+    static_assert(NB == 64, "one lane per bin");
+    if (lane == 0) type_cnt[t] = 0;  // for the next batch
+    const int d = __hip_atomic_load(dem + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // prep's atomics
+    const long long x = __hip_atomic_load(coltot + t * NB + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long incl = x;  // inclusive prefix over bins
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const long long cum = incl - x;
+    int th = -1, nd = 0, len = 0;
+    if (d > 0) {
+        binoff[t * NB + lane] = (int)cum;
+        const unsigned long long nz = __ballot(x > 0), hit = __ballot(incl >= d);
+        if (nz && lane == 0) {
+            // the live maximum is at most anchor - (smallest distance of the first
+            // non-empty bin): the next batch's anchor (applied when this batch ends)
+            const int bb = __ffsll((long long)nz) - 1;
+            anchor_next[t] = anchor[t] - bin_lo(bb);
+        }
+        if (hit) {
+            th = __ffsll((long long)hit) - 1;
+            const long long cth = __shfl(cum, th, 64), ith = __shfl(incl, th, 64);
+            if (th < NBX) {  // one priority value: the first (d - cum) by wqseqno
+                nd = (int)(d - cth);
+                len = d;
+            } else {         // several values: take the whole bin, sort later
+                nd = INT_MAX;
+                len = (int)ith;
+            }
+        } else {             // fewer available units than demand: take all
+            th = NB - 1;
+            nd = INT_MAX;
+            len = (int)__shfl(incl, 63, 64);
+        }
+    }
+    if (lane == 0) {
+        if (guess && d > 0) {  // next batch's pass-1 guess: this cut less a margin of half its depth
+            const long long an = anchor[t], cut = cut_of(th, an);
+            gcut_next[t] = cut - std::max(2ll, (an - cut) / 2);
+        }
+        theta[t] = th;
+        need[t] = nd;
+        candlen[t] = len;
+        needsort[t] = (th >= NBX && len > 1) ? 1 : 0;
+    }
 }
 
 // ---------------------------------------------------------------- thresholds
@@ -517,54 +567,141 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, lo
     }
     __syncthreads();
     if (!s_last || threadIdx.x >= 64) return;
-    // the last column of type t: wave 0, lane b = bin b (NB == 64), all totals loaded at once
-    static_assert(NB == 64, "one lane per bin");
-    if (lane == 0) type_cnt[t] = 0;  // for the next batch
-    const int d = dem[t];
-    const long long x = __hip_atomic_load(coltot + t * NB + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    long long incl = x;  // inclusive prefix over bins
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    const long long cum = incl - x;
-    int th = -1, nd = 0, len = 0;
-    if (d > 0) {
-        binoff[t * NB + lane] = (int)cum;
-        const unsigned long long nz = __ballot(x > 0), hit = __ballot(incl >= d);
-        if (nz && lane == 0) {
-            // the live maximum is at most anchor - (smallest distance of the first
-            // non-empty bin): the next batch's anchor (applied when this batch ends)
-            const int bb = __ffsll((long long)nz) - 1;
-            anchor_next[t] = anchor[t] - bin_lo(bb);
-        }
-        if (hit) {
-            th = __ffsll((long long)hit) - 1;
-            const long long cth = __shfl(cum, th, 64), ith = __shfl(incl, th, 64);
-            if (th < NBX) {  // one priority value: the first (d - cum) by wqseqno
-                nd = (int)(d - cth);
-                len = d;
-            } else {         // several values: take the whole bin, sort later
-                nd = INT_MAX;
-                len = (int)ith;
+    type_threshold(t, dem, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next,
+                   guess);
+}
+
+// ---------------------------------------------------------------- thresholds folded into pass 1
+// k_thresholds' work done by the last workgroups of k_prep_hist instead of a
+// launch of its own.  Every workgroup (request preparation or page) arrives
+// at one counter once its demand / chunk-sum atomics have completed (each
+// wave's s_waitcnt, then a workgroup barrier, then one agent-scope add: the
+// atomics are the hand-off, read back with sc1 loads -- MI355X_MICROARCH.md,
+// inter-workgroup visibility).  The workgroups holding the last nl tickets
+// wait for every arrival, then role r scans the C / nl columns [r C / nl, ...)
+// (tpc = 256 nl / C threads per column, a run of chunks each): the chunk sums
+// become exclusive prefixes in place, the column totals go out sc1, and the
+// workgroup whose add completes a type's 64 columns finds that type's
+// threshold (type_threshold).  The last role to finish resets the counters.
+struct FoldArgs {
+    int on;            // 0: k_thresholds runs as its own launch
+    int *arrive;       // [nl + 2] arrivals per role group (workgroup b in group b % nl), groups complete, roles done
+    int total, nl;     // workgroups of the launch; roles (C % nl == 0, 4 <= C / nl <= 64)
+    int nchunks;
+    const int *dem;
+    int *theta, *need, *candlen, *needsort, *binoff;
+    unsigned int *coltot;
+    int *type_cnt;
+    const long long *anchor;
+    long long *anchor_next, *gcut_next;
+    int guess;
+    int *fail;         // the batch's failure counter (k_finalize answers ADLB_ERROR when it moved)
+    unsigned int *zcs; // the previous scan's chunk sums, zeroed here: a slice per page workgroup
+    long long zn;
+};
+
+constexpr long long FOLD_WAIT_TICKS = 100ll * 1000 * 1000;  // 1 s at the 100 MHz constant clock
+constexpr int FOLD_MAX_NL = ADLBQ_MAX_TYPES * NB / 8;
+
+__device__ void fold_thresholds(const FoldArgs &f, int T, unsigned int *csum, unsigned int *lds) {
+    // two-level arrival (one counter per role group, then the top counter): a
+    // single counter taking every workgroup's add serialised them (tens of us)
+    __shared__ int s_role;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int g = (int)blockIdx.x % f.nl, ng = (f.total - g + f.nl - 1) / f.nl;
+        const int v = __hip_atomic_fetch_add(f.arrive + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int role = -1;
+        if (v == ng - 1) {  // the group is complete: this workgroup takes its role once every group is
+            __hip_atomic_fetch_add(f.arrive + f.nl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            role = g;
+            const long long t0 = wall_clock64();
+            while (__hip_atomic_load(f.arrive + f.nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < f.nl) {
+                if (wall_clock64() - t0 > FOLD_WAIT_TICKS) {
+                    atomicAdd(f.fail, 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
             }
-        } else {             // fewer available units than demand: take all
-            th = NB - 1;
-            nd = INT_MAX;
-            len = (int)__shfl(incl, 63, 64);
+        }
+        s_role = role;
+    }
+    __syncthreads();
+    const int role = s_role;
+    if (role < 0) return;
+    const int C = T * NB, ncol = C / f.nl, tpc = 256 / ncol;
+    const int c = role * ncol + (int)threadIdx.x / tpc, sub = (int)threadIdx.x % tpc;
+    const int per = (f.nchunks + tpc - 1) / tpc, k0 = min(f.nchunks, sub * per), k1 = min(f.nchunks, k0 + per);
+    // this thread's run of chunks: loads in flight 16 at a time, summed
+    unsigned int sum = 0;
+    for (int k = k0; k < k1; k += 16) {
+        unsigned int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            v[i] = k + i < k1 ? __hip_atomic_load(csum + (long long)(k + i) * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+        for (int i = 0; i < 16; i++) sum += v[i];
+    }
+    // exclusive scan over the tpc threads of the column (consecutive lanes of one wave)
+    unsigned int x = sum;
+    for (int o = 1; o < tpc; o <<= 1) {
+        const unsigned int y = __shfl_up(x, o, tpc);
+        if (sub >= o) x += y;
+    }
+    unsigned int run = x - sum;
+    for (int k = k0; k < k1; k += 16) {  // the chunk sums as exclusive prefixes, in place (read by k_select_open)
+        unsigned int v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            v[i] = k + i < k1 ? __hip_atomic_load(csum + (long long)(k + i) * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+            if (k + i < k1) {
+                csum[(long long)(k + i) * C + c] = run;
+                run += v[i];
+            }
+    }
+    if (sub == tpc - 1) __hip_atomic_store(f.coltot + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int t = (role * ncol) / NB;  // every column of a role is of one type (ncol <= NB)
+    __shared__ int s_last;
+    if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(f.type_cnt + t, ncol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + ncol == NB;
+    __syncthreads();
+    if (s_last && threadIdx.x < 64)
+        type_threshold(t, f.dem, f.theta, f.need, f.candlen, f.needsort, f.binoff, f.coltot, f.type_cnt, f.anchor,
+                       f.anchor_next, f.gcut_next, f.guess);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(f.arrive + role, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // its group is done
+        if (__hip_atomic_fetch_add(f.arrive + f.nl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.nl - 1) {
+            // the last role: every waiter has seen the total
+            __hip_atomic_store(f.arrive + f.nl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(f.arrive + f.nl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (lane == 0) {
-        if (guess && d > 0) {  // next batch's pass-1 guess: this cut less a margin of half its depth
-            const long long an = anchor[t], cut = cut_of(th, an);
-            gcut_next[t] = cut - std::max(2ll, (an - cut) / 2);
+    (void)lds;
+}
+
+// Pass 1 and the request preparation in one launch (they are independent):
+// workgroups [0, nprep) prepare 256 requests each, the rest count one page;
+// with fd.on the last workgroups then do k_thresholds' work.
+template <int TB, int PPB = 1>
+__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd) {
+    static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
+    extern __shared__ unsigned int lds[];
+    if ((int)blockIdx.x < nprep) {
+        prep_block<TB>(pa, blockIdx.x, reinterpret_cast<int *>(lds));
+    } else {
+        if (ha.variant == 0) hist_page_v0(ha, blockIdx.x - nprep, lds);
+        else hist_pages<PPB>(ha, (blockIdx.x - nprep) * PPB, lds);
+        if (fd.on && fd.zn > 0) {  // the previous scan's chunk sums (consumed): zeroed for the scan after this one
+            const long long npb = (long long)gridDim.x - nprep, b = (long long)blockIdx.x - nprep;
+            const long long per = (fd.zn + npb - 1) / npb, z0 = b * per;
+            for (long long i = z0 + threadIdx.x; i < min(fd.zn, z0 + per); i += blockDim.x) fd.zcs[i] = 0u;
         }
-        theta[t] = th;
-        need[t] = nd;
-        candlen[t] = len;
-        needsort[t] = (th >= NBX && len > 1) ? 1 : 0;
     }
+    if (fd.on) fold_thresholds(fd, ha.T, ha.csum, lds);
 }
 
 // ---------------------------------------------------------------- pass 2
@@ -1872,13 +2009,41 @@ __device__ void seg_guesses(const SegGuess &g, int T, const int *soff, const int
     if (tid == 0) g.sg[0] = (int)g.epoch;
 }
 
-__global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict__ candoff,
-                                                    const int *__restrict__ candlen,
-                                                    unsigned long long *ckey,  // sorted in this launch: not restrict
-                                                    unsigned int *__restrict__ crank, unsigned int *__restrict__ csum,
-                                                    long long ncsum, const unsigned long long *__restrict__ mask,
-                                                    const int *__restrict__ tmatch, int R, int *seg_cnt, RankSort rs,
-                                                    LevelRows lr, const DevCounters *ctr, SegGuess sgv) {
+// k_rank's arguments (also carried by k_chain0, which runs the same body when
+// the host skipped the k_rank launch and k_select_open did not rank)
+struct RankArgs {
+    int T;
+    const int *candoff, *candlen;
+    unsigned long long *ckey;  // sorted in this launch: not restrict
+    unsigned int *crank, *csum;
+    long long ncsum;
+    const unsigned long long *mask;
+    const int *tmatch;
+    int R;
+    int *seg_cnt;
+    RankSort rs;
+    LevelRows lr;
+    const DevCounters *ctr;
+    SegGuess sgv;
+};
+
+// The rank work of workgroup bid of nb (RANK_TILE threads).
+__device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const int bid, const int nb) {
+    const int T = ra.T;
+    const int *__restrict__ candoff = ra.candoff;
+    const int *__restrict__ candlen = ra.candlen;
+    unsigned long long *ckey = ra.ckey;
+    unsigned int *__restrict__ crank = ra.crank;
+    unsigned int *__restrict__ csum = ra.csum;
+    const long long ncsum = ra.ncsum;
+    const unsigned long long *__restrict__ mask = ra.mask;
+    const int *__restrict__ tmatch = ra.tmatch;
+    const int R = ra.R;
+    int *seg_cnt = ra.seg_cnt;
+    const RankSort &rs = ra.rs;
+    const LevelRows &lr = ra.lr;
+    const DevCounters *ctr = ra.ctr;
+    const SegGuess &sgv = ra.sgv;
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
     __shared__ unsigned long long span[4][RANK_SPAN];  // also the sort's LDS blocks
     static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * SORT_BLK,
@@ -1886,7 +2051,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     __shared__ unsigned long long s_first, s_last, s_sortmask;
     __shared__ int s_a0[4], s_len[4], s_tk, s_fast;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (rs.fail_test && blockIdx.x == 0 && tid == 0) atomicAdd(rs.sync + ADLBQ_MAX_TYPES + 1, 1);
+    if (rs.fail_test && bid == 0 && tid == 0) atomicAdd(rs.sync + ADLBQ_MAX_TYPES + 1, 1);
     // every input of the prologue in one round of loads: list offsets / lengths,
     // the sort flags, the fast-ranking flag k_select_open left
     if (tid <= T) soff[tid] = candoff[tid];
@@ -1902,7 +2067,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         }
     }
     // the scan's chunk sums are consumed (k_select_open): leave them zeroed for the next batch
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < ncsum; i += (long long)gridDim.x * blockDim.x)
+    for (long long i = (long long)bid * blockDim.x + threadIdx.x; i < ncsum; i += (long long)nb * blockDim.x)
         csum[i] = 0;
     __syncthreads();
     const unsigned long long sortmask = s_sortmask;
@@ -1910,7 +2075,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         const int nsort = __popcll(sortmask);
         if (tid == 0) {
             const int tk = __hip_atomic_fetch_add(rs.sync + ADLBQ_MAX_TYPES, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (tk == (int)gridDim.x - 1)  // every ticket drawn: reset for the next batch
+            if (tk == (int)nb - 1)  // every ticket drawn: reset for the next batch
                 __hip_atomic_store(rs.sync + ADLBQ_MAX_TYPES, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_tk = tk;
         }
@@ -1918,7 +2083,7 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
         // the block with ticket tk sorts the tk-th, (tk + grid)-th, ... type that needs it:
         // the first blocks to run take the work, and a grid smaller than the sort count
         // (the small grid of a rank hint) still sorts every list
-        for (int q = s_tk; q < nsort; q += gridDim.x) {
+        for (int q = s_tk; q < nsort; q += nb) {
             unsigned long long mm = sortmask;
             for (int r = 0; r < q; r++) mm &= mm - 1;
             const int t = __ffsll((long long)mm) - 1;
@@ -1962,8 +2127,8 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
             // eight groups of 64 per wave per step, their loads in flight together (a small grid
             // walks the whole batch: 16 waves over 1,024 groups at 65,536 Reserves)
             constexpr int DU = 8;
-            const int waves = gridDim.x * (RANK_TILE / 64);
-            for (int g0 = blockIdx.x * (RANK_TILE / 64) + w; g0 * 64 < R; g0 += waves * DU) {
+            const int waves = nb * (RANK_TILE / 64);
+            for (int g0 = bid * (RANK_TILE / 64) + w; g0 * 64 < R; g0 += waves * DU) {
                 unsigned long long m[DU];
                 int tmv[DU];
 #pragma unroll
@@ -1991,13 +2156,13 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     }
     __syncthreads();
     if (s_fast) {  // k_select_open ranked the candidates and wrote the level rows
-        if (blockIdx.x == 0 && sgv.sg != nullptr)
+        if (bid == 0 && sgv.sg != nullptr)
             seg_guesses(sgv, T, soff, slen, seg_cnt, R, lr, reinterpret_cast<int *>(&span[0][0]),
                         (int)(sizeof(span) / sizeof(int)));
         return;
     }
-    if (blockIdx.x == 0 && sgv.sg != nullptr && tid == 0) sgv.sg[0] = 0;  // the chain computes its own
-    for (int tile = blockIdx.x; tile < stile[T]; tile += gridDim.x) {
+    if (bid == 0 && sgv.sg != nullptr && tid == 0) sgv.sg[0] = 0;  // the chain computes its own
+    for (int tile = bid; tile < stile[T]; tile += nb) {
         int t = 0;
         while (t + 1 < T && stile[t + 1] <= tile) t++;
         const int i0 = (tile - stile[t]) * RANK_TILE, n = min(RANK_TILE, slen[t] - i0);
@@ -2070,6 +2235,8 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank(int T, const int *__restrict
     }
 }
 
+__global__ __launch_bounds__(RANK_TILE) void k_rank(RankArgs ra) { rank_body(ra, blockIdx.x, gridDim.x); }
+
 // ---------------------------------------------------------------- ordered choice: rounds over segment prefixes
 //
 // Segment s (SEG requests, one wavefront) turns a start state (lane t = head
@@ -2124,6 +2291,10 @@ struct ChainArgs {
     unsigned int sg_epoch;
     int *walked;                     // [nseg] fused finalize: == wepoch for a segment the walk re-solved (or nullptr)
     unsigned int wepoch;
+    // k_chain0 launched with RANK_TILE threads in place of a k_rank launch (T <= 8): rank_bar[2] = grid barrier
+    int rank_fuse;
+    int *rank_bar;
+    RankArgs rk;
 };
 
 // diagnostic phase stamps (100 MHz constant clock), lane 0 of a segment
@@ -2879,6 +3050,7 @@ struct FinArgs {
     const int *needsort;
     int *sortfail;
     int *done;  // fused into k_chain0: [0] = the chain epoch once the choices are final
+    int *mslot;  // [R] out: the slot request j was given, or -1 (adlbq_unreserve_resp_device reads it back)
 };
 
 // k_rank gave up waiting for an in-launch candidate sort: the lists may be
@@ -2895,6 +3067,7 @@ __device__ __forceinline__ bool fin_request(const FinArgs &f, int j, bool failed
     const int rank = rq[0], hang = failed ? 0 : rq[1];
     const int tm = f.tmatch[j], um = f.umatch[j];
     const int slot = failed ? -1 : tm >= 0 ? tm : (um >= 0 ? f.cslot[um] : -1);
+    f.mslot[j] = slot;
     int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
     if (failed) {
         o[0] = -1;  // ADLB_ERROR
@@ -3073,6 +3246,7 @@ __device__ __forceinline__ int fin_seg_store(const FinArgs &f, int s, const FinS
         bool parks = false;
         if (j < f.R) {
             const int sl = failed ? -1 : g.slot[u], hg = failed ? 0 : g.hang[u];
+            f.mslot[j] = sl;
             int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
             if (failed) {
                 o[0] = -1;  // ADLB_ERROR
@@ -3176,14 +3350,64 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, i
     fin_tail(f, total, failed);  // reads other segments' data only through sc1 / atomic loads
 }
 
+// k_chain0 in place of the k_rank launch (T <= 8; RANK_TILE threads per
+// workgroup, every workgroup resident).  When k_select_open ranked every
+// candidate and every type has candidates (the usual case) nothing happens
+// here.  Otherwise every workgroup runs k_rank's body (sorts, ranks, level
+// rows, guess counts), then all meet at a grid barrier: each publishes with an
+// agent-scope release before its arrival, each reads after an agent-scope
+// acquire (MI355X_MICROARCH.md, inter-workgroup visibility), since the chain's
+// waves read what other CUs wrote.  A barrier that does not complete within a
+// second answers the batch ADLB_ERROR (the sort-timeout path).  Wave 0 then
+// goes on with the chain; the others return.
+constexpr long long RANK_BAR_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
+constexpr int RANK_FUSE_MAX_SEG = 256;  // one workgroup per CU: every one resident for the barrier
+
+// All waves of the workgroup: k_rank's body, then the grid barrier.
+__device__ __attribute__((noinline)) void chain_rank_run(const ChainArgs &a) {
+    const RankArgs &ra = a.rk;
+    rank_body(ra, blockIdx.x, gridDim.x);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int v = __hip_atomic_fetch_add(a.rank_bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v == (int)gridDim.x - 1) {  // the last arrival: reset for the next batch, release the others
+            __hip_atomic_store(a.rank_bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.rank_bar + 1, (int)ra.rs.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const long long t0 = wall_clock64();
+            while (__hip_atomic_load(a.rank_bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (int)ra.rs.epoch) {
+                if (wall_clock64() - t0 > RANK_BAR_TICKS) {
+                    atomicAdd(ra.rs.sync + ADLBQ_MAX_TYPES + 1, 1);  // k_finalize answers the batch ADLB_ERROR
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
 // Round 0: every segment from its level guess (lane t = type t's head), then
 // passes 2 .. P in the same launch: segment s waits for segment s-1's end of
 // the previous pass and re-solves (seeded) only if it differs from its own
 // start; finally each segment checks its start against its predecessor's last
 // end.  A launch in which every check holds is the fixed point.
-template <int TB>
-__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
+template <int TB, int NT = 64>  // NT = RANK_TILE: the k_rank launch was skipped (a.rank_fuse)
+__global__ __launch_bounds__(NT) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
                                                int fuse) {
+    __shared__ int s_need;
+    if constexpr (NT > 64) {
+        if (threadIdx.x >= 64) {  // waves 1..3 only help with a rank wave 0 finds missing
+            __syncthreads();
+            if (s_need) chain_rank_run(a);
+            return;
+        }
+    }
     extern __shared__ unsigned int win[];
     const int lane = threadIdx.x, T = a.T, s = blockIdx.x, nseg = a.nseg, P = cp.passes;
     chain_stamp(a, s, 0);
@@ -3207,18 +3431,37 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
     }
     // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
     const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
+    // in place of a k_rank launch: whether k_select_open ranked every candidate and every type has
+    // some (else k_rank's body runs here first), loaded with the rest of the prologue
+    int rk_ns = 0, rk_fast = 1;
+    if constexpr (NT > 64) {
+        rk_ns = lane < T ? a.rk.rs.needsort[lane] : 0;
+        rk_fast = a.rk.ctr->rank_fast;
+    }
     // k_rank's guess for this segment, when it made them (one load instead of the three dependent ones below)
     const bool sg_ok = a.sg != nullptr && a.lv != nullptr && a.sg[0] == (int)a.sg_epoch;
     const int sg_v = (a.sg != nullptr && lane < T) ? a.sg[1 + s * T + lane] : 0;
     int J = 0;  // requests before jb that take an untargeted unit
-    if (!sg_ok) {
+    auto count_J = [&]() {
+        int acc = 0;
         const int nq = jb >> 6;
         int cv[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) cv[u] = u * 64 + lane < nq ? a.seg_cnt[u * 64 + lane] : 0;
 #pragma unroll
-        for (int u = 0; u < 16; u++) J += cv[u];
-        for (int q = 1024 + lane; q < nq; q += 64) J += a.seg_cnt[q];  // batches above 65,536 Reserves
+        for (int u = 0; u < 16; u++) acc += cv[u];
+        for (int q = 1024 + lane; q < nq; q += 64) acc += a.seg_cnt[q];  // batches above 65,536 Reserves
+        return acc;
+    };
+    if (!sg_ok) J = count_J();
+    if constexpr (NT > 64) {
+        const bool need = __ballot(lane < T && (my_len <= 0 || (rk_ns == 1 && my_len > 1))) != 0ull || rk_fast != 1;
+        if (lane == 0) s_need = need ? 1 : 0;
+        __syncthreads();
+        if (need) {  // rare: sorts, ranks, level rows, guess counts first, then the counts again
+            chain_rank_run(a);
+            if (!sg_ok) J = count_J();
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
@@ -3353,7 +3596,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     if (n <= h->cap_req) return ADLBQ_OK;
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
-    void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf,
+    void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_mslot, h->d_reqbuf, h->d_respbuf,
                   h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht,
                   h->d_chcnt, h->d_chE, h->d_chflag, h->d_pmask, h->d_lv, h->d_rtype};
     for (void *p : ps)
@@ -3361,6 +3604,8 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_tmatch, sizeof(int) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_umatch, sizeof(int) * nc));
+    AQ_HIP(hipMalloc((void **)&h->d_mslot, sizeof(int) * nc));
+    AQ_HIP(hipMemsetAsync(h->d_mslot, 0xff, sizeof(int) * nc, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_reqbuf, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
     const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
@@ -3459,6 +3704,24 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     const int npb = (np + ppb - 1) / ppb;
     ha.zper = npb > 0 ? (int)((ha.zn + npb - 1) / npb) : 0;
     const int grid = nprep + (scan ? npb : 0);
+    // k_thresholds folded into pass 1's last workgroups: 8 columns per role (4..64), every role a workgroup
+    FoldArgs fd{};
+    if (scan && h->fold_thresholds && !h->split_prep) {
+        const int C1 = T * NB;
+        int ncol = 8;
+        while (ncol < 64 && C1 / ncol > grid) ncol *= 2;
+        if (C1 / ncol <= grid && C1 % ncol == 0) {
+            const int nchunks = (np + CHUNK - 1) / CHUNK;
+            if (!h->d_fold) {
+                AQ_HIP(hipMalloc((void **)&h->d_fold, sizeof(int) * (FOLD_MAX_NL + 2)));
+                AQ_HIP(hipMemsetAsync(h->d_fold, 0, sizeof(int) * (FOLD_MAX_NL + 2), s));
+            }
+            fd = FoldArgs{C1 / ncol <= FOLD_MAX_NL ? 1 : 0, h->d_fold, grid, C1 / ncol, nchunks, h->d_dem, h->d_theta,
+                          h->d_need, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt,
+                          h->d_anchor, h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0,
+                          h->d_rank_sync + ADLBQ_MAX_TYPES + 1, zcs, ha.zn};
+        }
+    }
     if (grid > 0) {
         // pass 1: the histogram copies, then the four waves' speculative lists
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0,
@@ -3469,23 +3732,26 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             HistArgs hd = ha;
             hd.diag = (h->hist_diag & 0xff) | 2;
             hd.zn = 0;
-            for (int r = 0; r < std::max(1, h->hist_diag >> 8); r++) kph<<<npb, 256, lds, s>>>(pa, 0, hd);
+            for (int r = 0; r < std::max(1, h->hist_diag >> 8); r++) kph<<<npb, 256, lds, s>>>(pa, 0, hd, FoldArgs{});
         }
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
-            kph<<<nprep, 256, lds, s>>>(pa, nprep, ha);
-            kph<<<npb, 256, lds, s>>>(pa, 0, ha);
+            kph<<<nprep, 256, lds, s>>>(pa, nprep, ha, FoldArgs{});
+            kph<<<npb, 256, lds, s>>>(pa, 0, ha, FoldArgs{});
         } else {
-            kph<<<grid, 256, lds, s>>>(pa, nprep, ha);
+            kph<<<grid, 256, lds, s>>>(pa, nprep, ha, fd);
         }
         stage_end(h, "hist", ev);
     }
     if (scan) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
-        stage_begin(h, "thresholds", &ev);
-        k_thresholds<<<C, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
-                                       h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor,
-                                       h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0);
-        stage_end(h, "thresholds", ev);
+        if (!fd.on) {
+            stage_begin(h, "thresholds", &ev);
+            k_thresholds<<<C, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need,
+                                                  h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot,
+                                                  h->d_type_cnt, h->d_anchor, h->d_anchor_next, h->d_gcut_next,
+                                                  nprep > 0 ? 1 : 0);
+            stage_end(h, "thresholds", ev);
+        }
         stage_begin(h, "select", &ev);
         const bool chunked = h->select_chunk && T <= 8;  // one workgroup per chunk of pages
         auto sel = chunked ? (T <= 4 ? k_select_chunk<4> : k_select_chunk<8>)
@@ -4459,6 +4725,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     const auto scan_t0 = std::chrono::steady_clock::now();
     if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) return rc;
     host_stage_add(h, "scan", scan_t0);
+    auto hl = hclk::now();
+    h->hacc["l_scan"] += std::chrono::duration_cast<std::chrono::nanoseconds>(hl - scan_t0).count();
     h->last_scan_units = h->live_units - h->live_targeted;
 
     if (targeted) {
@@ -4489,21 +4757,29 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_end(h, "sort", ev);
     }
     hsec("sort", st0);
+    // T <= 8 with a small enough grid: no k_rank launch, k_chain0 runs its body when needed
+    const int nseg0 = (R + SEG - 1) / SEG;
+    const bool rank_fused = np > 0 && T > 0 && T <= 8 && h->fuse_rank && !h->fuse_finalize && !h->seg_guess &&
+                            !h->rank_grid && nseg0 <= RANK_FUSE_MAX_SEG;
+    RankArgs rka{};
     if (np > 0 && T > 0) {
-        stage_begin(h, "rank", &ev);
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
         const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch,
                           h->sort_fail_test};
         const int warm0 = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
         const SegGuess sgv{(T <= 8 && h->seg_guess) ? h->d_sg : nullptr, (R + SEG - 1) / SEG, warm0, h->rank_epoch};
-        // a small grid when the last landed batch was ranked in k_select_open (every loop is
-        // grid-strided: any grid is correct, the hint only sizes it); chunk sums: zeroed by the next scan
-        k_rank<<<h->rank_grid ? h->rank_grid : rank_hint(h) ? 4 : 1280, RANK_TILE, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, nullptr,
-                                    0, h->d_mask, h->d_tmatch, R,
-                                    h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr,
-                                    sgv);
-        stage_end(h, "rank", ev);
+        // chunk sums: zeroed by the next scan
+        rka = RankArgs{T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, nullptr, 0, h->d_mask, h->d_tmatch, R,
+                       h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr, sgv};
+        if (!rank_fused) {
+            stage_begin(h, "rank", &ev);
+            // a small grid when the last landed batch was ranked in k_select_open (every loop is
+            // grid-strided: any grid is correct, the hint only sizes it)
+            k_rank<<<h->rank_grid ? h->rank_grid : rank_hint(h) ? 4 : 1280, RANK_TILE, 0, s>>>(rka);
+            stage_end(h, "rank", ev);
+        }
     }
+    hsec("l_rank", hl);
     // k_finalize's arguments (its own launch, or fused into the final k_chain0 launch)
     DevCounters *const snap = h->d_snap + h->snap_next;
     h->snap_tag[h->snap_next] = ++h->snap_tags;
@@ -4512,7 +4788,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                      h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
                      h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, T, snap, h->snap_tag[h->snap_next],
                      h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
-                     h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1};
+                     h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot};
     bool fused = false;
     stage_begin(h, "chain", &ev);
     {
@@ -4565,7 +4841,13 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             ca.walked = h->d_chflag + (size_t)CHAIN_MAX_PASSES * ((h->cap_req + SEG - 1) / SEG);
             ca.wepoch = h->chain_epoch;
         }
-        if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
+        if (rank_fused) {
+            ca.rank_fuse = 1;
+            ca.rank_bar = h->d_rank_sync + ADLBQ_MAX_TYPES + 2;
+            ca.rk = rka;
+            if (T <= 4) k_chain0<4, RANK_TILE><<<nseg, RANK_TILE, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
+            else k_chain0<8, RANK_TILE><<<nseg, RANK_TILE, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
+        } else if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
         for (int k = 1; k <= K; k++) {
@@ -4577,9 +4859,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         }
     }
     stage_end(h, "chain", ev);
+    hsec("l_chain", hl);
     stage_begin(h, "finalize", &ev);
     if (!fused) k_finalize<<<(R + 255) / 256, 256, 0, s>>>(fa);
     stage_end(h, "finalize", ev);
+    hsec("l_fin", hl);
     // the lists hold export_extra more per type: a steal export right after this batch gathers them
     h->batch_export_k = (np > 0 && T > 0) ? h->export_extra : 0;
     h->batch_export_R = R;

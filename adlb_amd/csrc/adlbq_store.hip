@@ -917,21 +917,47 @@ __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ page
 
 // SS_UNRESERVE of every unit a reserve batch handed out, read straight from the
 // batch's requests and TA_RESERVE_RESP records (rc 1 = matched, [5] = wqseqno;
-// the new pin is -1, i.e. the unit is available again)
+// the new pin is -1, i.e. the unit is available again).  The slot comes from
+// the last batch's record of what it gave request i (mslot, read with the
+// response: one dependent load level fewer), checked against the unit's
+// wqseqno; responses of another batch fall back to the wqseqno -> slot map.
+// The anchor is raised by a fire-and-forget atomic max per type of the wave
+// (a stale read could only add a harmless one: no load of it first).
 __global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
                                  const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta, int *pin,
-                                 const int4 *__restrict__ rrec, long long *anchor) {
+                                 const int4 *__restrict__ rrec, long long *anchor, const int *__restrict__ mslot,
+                                 int ntypes) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
-    int t = 0, up = INT_MIN;
+    int t = -1, up = INT_MIN;
+    // lane u holds anchor[u] (T <= 64), loaded with the responses: only a unit above it needs an
+    // atomic max (one per type of the wave; every wave adding to one word would serialise them)
+    const long long my_anchor = __lane_id() < ntypes ? __hip_atomic_load(anchor + __lane_id(), __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT) : LLONG_MAX;
     if (i < n) {
         const int rc = resp[(long long)ADLBQ_RESP_INTS * i], seq = resp[(long long)ADLBQ_RESP_INTS * i + 5];
         const int rank = reqs[(long long)ADLBQ_RESERVE_INTS * i];
-        long long slot = (rc == 1 && seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
-        if (slot >= 0) {
-            const uint32_t m = meta[slot];
-            const int pn = pin[slot];
-            const int4 r0 = rrec[2 * slot], r1 = rrec[2 * slot + 1];
-            if ((m & M_LIVE) && pn == rank && r0.z == seq) {
+        const int ms = mslot != nullptr ? mslot[i] : -1;
+        if (rc == 1 && seq > 0 && seq < nseq) {
+            long long slot = ms;
+            uint32_t m = 0;
+            int pn = 0;
+            int4 r0 = make_int4(0, 0, 0, 0), r1 = r0;
+            if (slot >= 0) {
+                m = meta[slot];
+                pn = pin[slot];
+                r0 = rrec[2 * slot];
+                r1 = rrec[2 * slot + 1];
+            }
+            if (slot < 0 || r0.z != seq) {  // not the last batch's record: the map
+                slot = seq2slot[seq];
+                if (slot >= 0) {
+                    m = meta[slot];
+                    pn = pin[slot];
+                    r0 = rrec[2 * slot];
+                    r1 = rrec[2 * slot + 1];
+                }
+            }
+            if (slot >= 0 && (m & M_LIVE) && pn == rank && r0.z == seq) {
                 pin[slot] = -1;
                 meta[slot] = m & ~M_PINNED;
                 t = m & M_TYPE;
@@ -939,7 +965,18 @@ __global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__rest
             }
         }
     }
-    raise_anchor(anchor, t, up);  // available again: keep the anchor above it
+    // available again: keep the anchor above it, one atomic max per distinct type of the wave that rose
+    const long long at = __shfl(my_anchor, t >= 0 ? t : 0, 64);
+    if (t >= 0 && (long long)up <= at) t = -1;
+    for (unsigned long long b = __ballot(t >= 0); b;) {
+        const int leader = __ffsll((long long)b) - 1;
+        const int lt = __shfl(t, leader, 64);
+        int mx = t == lt ? up : INT_MIN;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+        if (__lane_id() == leader) atomicMax(anchor + lt, (long long)mx);
+        b &= ~__ballot(t == lt);
+    }
 }
 
 // update_local_state over the open bucket: count of live unpinned units and per
@@ -1242,8 +1279,8 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMalloc((void **)&h->d_coltot, sizeof(unsigned int) * T1 * NB));
     AQ_HIP(hipMalloc((void **)&h->d_type_cnt, sizeof(int) * T1));
     AQ_HIP(hipMemsetAsync(h->d_type_cnt, 0, sizeof(int) * T1, h->stream));
-    AQ_HIP(hipMalloc((void **)&h->d_rank_sync, sizeof(int) * (ADLBQ_MAX_TYPES + 2)));
-    AQ_HIP(hipMemsetAsync(h->d_rank_sync, 0, sizeof(int) * (ADLBQ_MAX_TYPES + 2), h->stream));
+    AQ_HIP(hipMalloc((void **)&h->d_rank_sync, sizeof(int) * (ADLBQ_MAX_TYPES + 6)));
+    AQ_HIP(hipMemsetAsync(h->d_rank_sync, 0, sizeof(int) * (ADLBQ_MAX_TYPES + 6), h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
     long long pages = std::max<long long>(16, (max_units + PAGE - 1) / PAGE + 16);
@@ -1269,7 +1306,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
                     h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
-                    h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg};
+                    h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg,
+                    h->d_mslot, h->d_fold};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1602,7 +1640,9 @@ int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, con
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
     k_unreserve_resp<<<(n + 255) / 256, 256, 0, h->stream>>>(d_reqs18, d_resp12, n, h->d_seq2slot, h->next_wqseqno,
-                                                             h->d_meta, h->d_pin, h->d_rrec, h->d_anchor);
+                                                             h->d_meta, h->d_pin, h->d_rrec, h->d_anchor,
+                                                             (h->d_mslot && n <= h->cap_req) ? h->d_mslot : nullptr,
+                                                             std::min(h->T, 64));
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
 }
@@ -2137,6 +2177,16 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (n == "fuse_finalize") {
         if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "fuse_finalize must be 0 or 1");
         h->fuse_finalize = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "fold_thresholds") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0 or 1");
+        h->fold_thresholds = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "fuse_rank") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "fuse_rank must be 0 or 1");
+        h->fuse_rank = (int)value;
         return ADLBQ_OK;
     }
     if (n == "rank_grid") {  // test: k_rank's grid (0: sized by the rank hint)

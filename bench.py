@@ -269,6 +269,34 @@ def cpu_baseline(w, budget_s: float, seed: int, cores: int, equal_prio: bool = F
             "host_cpus": {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()}}
 
 
+def cpu_baseline_config(name, jobs, budget_s: float, what: str, units_per_proc: int) -> dict:
+    """CPU baselines of configs 3 and 4 on the GPU box's host (BASELINE.md:
+    configs 2-5 in one table): len(jobs) processes in parallel, each building
+    its queue in the reference's own xq.c (oracle/_ref/libxqref.so) where
+    adlb.c's allocation cap allows, this repo's restatement otherwise, and
+    timing Reserves of the same workload for budget_s seconds.  value =
+    aggregate Reserves/s; ns_per_node as cpu_baseline."""
+    import multiprocessing as mp
+    from oracle.baseline import sample
+    ctx = mp.get_context("spawn")  # this process holds the GPU: no fork
+    with ctx.Pool(len(jobs)) as pool:
+        res = pool.map_async(sample, jobs).get(10 * budget_s + 600)
+    kind = jobs[0][1]
+    rate = sum(r[0] / r[1] for r in res if r[1] > 0)
+    per = [r[1] / max(r[0], 1) / (2.0 * r[2]) * 1e9 for r in res]
+    src = ("oracle/_ref/libxqref.so (the reference's src/xq.c, compiled in the build container)" if kind == "ref"
+           else "oracle/liboracle.so (this repo's restatement of xq.c)")
+    return {"value": rate, "unit": "assignments/s", "cores": len(jobs), "kind": "reference" if kind == "ref" else "port",
+            "reserves_timed": int(sum(r[0] for r in res)), "ns_per_node": round(float(np.median(per)), 3),
+            "units_per_process": units_per_proc, "sample": f"{name}: {what}; {src}; {budget_s:.0f} s each"}
+
+
+def _ref_fits(units: int) -> str:
+    import oracle
+    # adlb.c's max_malloc is 500 MB until ADLB_Server runs (adlb.c:218, 3439-3452): ~150 B per unit with payload
+    return "ref" if oracle.available("ref") and units * 150 < 4.5e8 else "own"
+
+
 def bench_config3(args, torch, dist, world, rank, local, dev):
     """Config 3: c3_servers server shards per GPU (64 over 8
     GPUs), c3_units units each, per-shard type skew so ~10% of the Reserves
@@ -869,10 +897,13 @@ def main():
     d_resp = torch.empty((nb, R, 12), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
+    p_req = [d_reqs[b].data_ptr() for b in range(nb)]  # no tensor views inside the timed loop
+    p_resp = [d_resp[b].data_ptr() for b in range(nb)]
+
     def step(b):
-        srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        srv.reserve_batch_device(R, p_req[b], p_resp[b])
         # SS_UNRESERVE every matched unit, straight from the batch's responses
-        srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        srv.unreserve_resp_device(R, p_req[b], p_resp[b])
 
     for b in range(args.warmup):
         step(b)
@@ -899,10 +930,13 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    HACC_M = ("req_cap", "tables", "rq_cap", "scan_cap", "l_scan", "sort", "l_rank", "l_chain", "l_fin", "total")
+    hacc0 = {k: srv.stat("hacc:" + k) for k in HACC_M}
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
     t_submit = time.perf_counter() - t0  # host time to enqueue the K steps
+    host_sections = {k: round((srv.stat("hacc:" + k) - hacc0[k]) / 1e6 / max(args.steps, 1), 4) for k in HACC_M}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -1007,6 +1041,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps,
         "host_submit_ms_per_step": round(t_submit * 1e3 / args.steps, 4),
+        "reserve_host_sections_ms_per_step": host_sections,
         "host_buffer_path": host_path,
         "higher_is_better": True,
         "scaling": "weak",
@@ -1051,6 +1086,27 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, shards.shard_seed(args.seed, rank),
                                            args.cpu_cores, args.equal_prio)
+        c3 = res.get("config3")
+        if isinstance(c3, dict) and "error" not in c3:
+            # the shard layout: one server process per shard, each shard as the GPU leg builds it
+            S = args.c3_servers * world
+            ncp = min(args.cpu_cores, S)
+            kind = _ref_fits(args.c3_units)
+            jobs = [("config3", kind, j, S, args.c3_units, args.c3_reserves, args.seed, args.cpu_seconds)
+                    for j in range(ncp)]
+            c3["cpu_baseline"] = cpu_baseline_config(
+                "config3", jobs, args.cpu_seconds,
+                f"{ncp} server processes, shards 0..{ncp - 1} of {S} ({args.c3_units} units each, the GPU leg's "
+                f"queues and first Reserve batches; local matching only, no steal round)", args.c3_units)
+        c4 = res.get("config4")
+        if isinstance(c4, dict) and "error" not in c4:
+            kind = _ref_fits(args.c4_units)
+            jobs = [("config4", kind, args.c4_units, args.reserves, shards.shard_seed(args.seed + 40, 0),
+                     args.cpu_seconds)] * args.cpu_cores
+            c4["cpu_baseline"] = cpu_baseline_config(
+                "config4", jobs, args.cpu_seconds,
+                f"{args.cpu_cores} processes x one replica of the {args.c4_units}-unit config-4 queue (80% targeted, "
+                f"32 types; the GPU leg's queue and first Reserve batch, no Puts between Reserves)", args.c4_units)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

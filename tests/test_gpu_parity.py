@@ -73,6 +73,13 @@ CASES = {
     "c4_n200k": lambda: synth.config4(n_units=200_000, n_reserves=8192, n_ranks=256, seed=207),
     "c4_t8_tied": lambda: synth.config4(n_units=100_000, n_types=8, n_reserves=8192, n_ranks=64, seed=208,
                                         prio_hi=4),
+    # T <= 8 with thresholds in multi-priority bins: k_select_open cannot rank, so the chain
+    # launch sorts and ranks in place of k_rank (fuse_rank) behind its grid barrier
+    "c2_t4_wide_prio": lambda: synth.config2(n_units=100_000, n_reserves=16_384, seed=230, prio_hi=1 << 20),
+    "c2_t8_wide_prio": lambda: synth.config2(n_units=100_000, n_types=8, n_reserves=8192, seed=231,
+                                             prio_hi=1 << 16),
+    # a type with no unit at all (config 3's shards): the guess counts are adjusted first
+    "c3_shard_missing_type": lambda: synth.config3_shard(1, 64, 80_000, 4, 8192, seed=232),
 }
 
 
@@ -90,11 +97,13 @@ VARIANTS = {
     "no_seg_guess": {"seg_guess": 0},      # the chain finds its own start guesses
     "all": {"select_chunk": 1, "hist_ppb": 2},
     "fused": {"fuse_finalize": 1},         # k_finalize inside the final k_chain0 launch
+    "rank_fused": {"fuse_rank": 1},        # no k_rank launch: k_chain0 ranks when k_select_open did not (measured slower)
+    "thresholds_folded": {"fold_thresholds": 1},  # k_thresholds' work in pass 1's last workgroups (measured slower)
 }
 
 
 @pytest.mark.parametrize("name", ["c2_n200k_r16k", "c2_eq_n200k_r16k", "c2_mixed_wide_pages", "c2_exhaust",
-                                  "c4_t8_tied", "c2_t1"])
+                                  "c4_t8_tied", "c2_t1", "c2_t4_wide_prio", "c3_shard_missing_type"])
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
 def test_pipeline_variants_vs_oracle(gpu_available, name, variant):
     """The scan and chain variants (adlbq_set_param) give the sequential result."""
