@@ -24,13 +24,11 @@
 //                  unmatched hanging Reserves on rq (FIFO) with their RFR donors
 #include <algorithm>
 #include <climits>
-
-#include <hipcub/hipcub.hpp>
+#include <cstring>
 
 #include "adlbq_donor.h"
 #include "adlbq_impl.h"
-
-#include <rocprim/device/device_merge.hpp>
+#include "adlbq_rsx.h"
 
 using namespace adlbq;
 
@@ -1401,7 +1399,7 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
 // rank's Reserves, in order, against that rank's bucket.  Instead of one scan
 // of the bucket per Reserve, the bucket's units are kept in an index sorted
 // by (bucket, type, prio desc, bucket position asc) -- one stable radix sort,
-// rebuilt only after targeted Puts (k_tindex_keys, hipcub) -- with the range
+// rebuilt only after targeted Puts (k_tindex_keys, rsx_sort_pairs) -- with the range
 // of every (bucket, type) as lower bounds (k_tindex_bounds; after an
 // incremental merge, k_tindex_shift).  A Reserve's best unit is then
 // the best head among its types' ranges: lane t of wave 0 keeps type t's
@@ -4001,10 +3999,7 @@ static int ensure_tindex(adlbq_server *h) {
         return ADLBQ_OK;
     }
     // full build: keys over every slot of every rank-bucket page (holes sort last), one stable sort
-    size_t tmp = 0;
-    hipcub::DoubleBuffer<unsigned long long> dk(h->d_tkeys, h->d_tkeys2);
-    hipcub::DoubleBuffer<int> dv(h->d_tvals, h->d_tvals2);
-    AQ_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, dk, dv, (int)n, 0, TIDX_KEY_BITS, s));
+    const size_t tmp = rsx_temp_bytes(n);
     if (tmp > h->cap_tsort) {
         AQ_HIP(hipStreamSynchronize(s));
         if (h->d_tsort) AQ_HIP(hipFree(h->d_tsort));
@@ -4017,12 +4012,11 @@ static int ensure_tindex(adlbq_server *h) {
     if (npg > 0) {
         k_tindex_keys<<<npg, 256, 0, s>>>(h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill, nb, h->d_prio, h->d_meta,
                                           h->d_tkeys, h->d_tvals);
-        size_t t2 = h->cap_tsort;
-        AQ_HIP(hipcub::DeviceRadixSort::SortPairs(h->d_tsort, t2, dk, dv, (int)n, 0, TIDX_KEY_BITS, s));
-        if (dk.Current() != h->d_tkeys) {  // keep the sorted arrays in d_tkeys / d_tvals
-            std::swap(h->d_tkeys, h->d_tkeys2);
-            std::swap(h->d_tvals, h->d_tvals2);
-        }
+        const int rs = rsx_sort_pairs(h->d_tsort, h->cap_tsort, h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, n, 0,
+                                      TIDX_KEY_BITS, false, s);
+        if (rs) return rs;
+        std::swap(h->d_tkeys, h->d_tkeys2);  // keep the sorted arrays in d_tkeys / d_tvals
+        std::swap(h->d_tvals, h->d_tvals2);
     }
     h->tidx_n = filled;  // the holes sorted past the filled slots
     h->tdel_n = 0;       // every targeted unit is in the main index again
@@ -4054,6 +4048,22 @@ __global__ __launch_bounds__(256) void k_segsort_back(SegList sl, const unsigned
         slot[i] = s2[i];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) needsort[sl.type[q]] = 2;
+}
+
+// short list from + blockIdx.x sorted by one workgroup (sort_type: LDS bitonic
+// blocks, then merges through key2 / slot2), then copied to key2 / slot2, where
+// k_segsort_back takes every sorted list from
+__global__ __launch_bounds__(1024) void k_segsort_short(SegList sl, int from, unsigned long long *key, int *slot,
+                                                        unsigned long long *key2, int *slot2) {
+    __shared__ unsigned long long sk[SORT_BLK];
+    __shared__ int ss[SORT_BLK];
+    const int q = from + blockIdx.x, b = sl.beg[q], n = sl.end[q] - b;
+    sort_type(b, n, key, slot, key2, slot2, sk, ss);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        key2[b + i] = key[b + i];
+        slot2[b + i] = slot[b + i];
+    }
 }
 
 __global__ void k_segsort_bounds(SegList sl, int from, int *sbeg, int *send) {
@@ -4213,18 +4223,17 @@ static int launch_segsort_planned(adlbq_server *h, bool *done) {
                                  h->d_ctr);
     k_merge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_ckey2);
     k_merge_pad<<<std::min(1024, (g_bound + 255) / 256 + 1), 256, 0, s>>>(h->d_plan, g_bound, h->d_ckey2);
-    size_t tmp = 0;
-    AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey2, h->d_ckey3, h->d_cslot,
-                                                        h->d_cslot3, g_bound, lo_hint, 64, s));
+    const size_t tmp = rsx_temp_bytes(g_bound);
     if (tmp > h->cap_ssort) {
         AQ_HIP(hipStreamSynchronize(s));
         if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
         h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
         AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
     }
-    size_t t2 = h->cap_ssort;
-    AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey2, h->d_ckey3, h->d_cslot,
-                                                        h->d_cslot3, g_bound, lo_hint, 64, s));
+    int rc;
+    if ((rc = rsx_sort_pairs(h->d_ssort, h->cap_ssort, h->d_ckey2, h->d_ckey3, h->d_cslot, h->d_cslot3, g_bound, lo_hint,
+                             64, true, s)))
+        return rc;
     k_unmerge_plan<<<dim3(kgx, T), 256, 0, s>>>(h->d_plan, h->d_candoff, h->d_candlen, h->d_kb, h->d_ckey3,
                                                  h->d_cslot3, h->d_ckey, h->d_cslot, h->d_needsort);
     AQ_HIP(hipGetLastError());
@@ -4594,18 +4603,17 @@ static int launch_segsort(adlbq_server *h) {
         if (nsort == 0) return ADLBQ_OK;
         if (ok) {
             if (lo >= LIST_SHIFT) lo = LIST_SHIFT;  // every list is constant: the sort only keeps lists apart
-            size_t tmp = 0;
-            AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey2, h->d_ckey, h->d_cslot,
-                                                                h->d_cslot2, G, lo, 64, s));
+            const size_t tmp = rsx_temp_bytes(G);
             if (tmp > h->cap_ssort) {
                 if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
                 h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
                 AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
             }
             k_merge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_ckey2);
-            size_t t2 = h->cap_ssort;
-            AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey2, h->d_ckey, h->d_cslot,
-                                                                h->d_cslot2, G, lo, 64, s));
+            int rc;
+            if ((rc = rsx_sort_pairs(h->d_ssort, h->cap_ssort, h->d_ckey2, h->d_ckey, h->d_cslot, h->d_cslot2, G, lo,
+                                     64, true, s)))
+                return rc;
             k_unmerge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_kb, h->d_ckey, h->d_cslot2,
                                                         h->d_ckey, h->d_cslot, h->d_needsort);
             AQ_HIP(hipGetLastError());
@@ -4634,35 +4642,23 @@ static int launch_segsort(adlbq_server *h) {
         AQ_HIP(hipMalloc((void **)&h->d_send, sizeof(int) * ADLBQ_MAX_TYPES));
     }
     const int nshort = sl.n - nwide;
-    const int span = nshort > 0 ? sl.end[sl.n - 1] : 0;  // short lists lie below this bound (candoff ascends)
-    size_t tmp = 0, t1 = 0;
-    if (nwide > 0)
-        AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tmp, h->d_ckey, h->d_ckey2, h->d_cslot,
-                                                            h->d_cslot2, maxlen, 0, 64, s));
-    if (nshort > 0) {
-        AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(nullptr, t1, h->d_ckey, h->d_ckey2, h->d_cslot,
-                                                                     h->d_cslot2, span, nshort, h->d_sbeg,
-                                                                     h->d_send, 0, 64, s));
-        tmp = std::max(tmp, t1);
+    if (nwide > 0) {
+        const size_t tmp = rsx_temp_bytes(maxlen);
+        if (tmp > h->cap_ssort) {
+            if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
+            h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
+            AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
+        }
     }
-    if (tmp > h->cap_ssort) {
-        if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
-        h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
-        AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
-    }
-    for (int q = 0; q < nwide; q++) {
+    int rc;
+    for (int q = 0; q < nwide; q++) {  // a device-wide sort of its own per long list
         const int b = sl.beg[q], len = sl.end[q] - b;
-        size_t t2 = h->cap_ssort;
-        AQ_HIP(hipcub::DeviceRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey + b, h->d_ckey2 + b,
-                                                            h->d_cslot + b, h->d_cslot2 + b, len, 0, 64, s));
+        if ((rc = rsx_sort_pairs(h->d_ssort, h->cap_ssort, h->d_ckey + b, h->d_ckey2 + b, h->d_cslot + b,
+                                 h->d_cslot2 + b, len, 0, 64, true, s)))
+            return rc;
     }
-    if (nshort > 0) {
-        k_segsort_bounds<<<1, 64, 0, s>>>(sl, nwide, h->d_sbeg, h->d_send);
-        size_t t2 = h->cap_ssort;
-        AQ_HIP(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(h->d_ssort, t2, h->d_ckey, h->d_ckey2,
-                                                                     h->d_cslot, h->d_cslot2, span, nshort,
-                                                                     h->d_sbeg, h->d_send, 0, 64, s));
-    }
+    if (nshort > 0)  // one workgroup per short list
+        k_segsort_short<<<nshort, 1024, 0, s>>>(sl, nwide, h->d_ckey, h->d_cslot, h->d_ckey2, h->d_cslot2);
     const int gx = std::min((maxlen + 255) / 256, 256);
     k_segsort_back<<<dim3(gx, sl.n), 256, 0, s>>>(sl, h->d_ckey2, h->d_cslot2, h->d_ckey, h->d_cslot, h->d_needsort);
     AQ_HIP(hipGetLastError());
