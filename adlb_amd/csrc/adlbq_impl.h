@@ -74,6 +74,8 @@ struct DevCounters {
     int plan_missed;       // sync-free sorts whose plan did not hold (k_rank sorted in-launch), cumulative
     int plan_phi;          // highest bit of the prio field any candidate list varies in (-1: none)
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
+    int rank_covered;      // ... and every type had candidates: the next batch may skip k_rank (fuse_rank)
+    int pad0;
     int batch_failed;      // batches answered ADLB_ERROR because an in-launch candidate sort gave up (cumulative)
     int rq_next;           // rqseqnos handed out (next_rqseqno - 1, adlb.c:1244)
     int rq_reclaims;       // k_rq_reclaim compactions (cumulative)
@@ -212,6 +214,7 @@ struct adlbq_server {
     unsigned long long *d_mask = nullptr;
     int *d_tmatch = nullptr, *d_umatch = nullptr;
     int *d_mslot = nullptr;            // [cap_req] the slot the last reserve batch gave request j (-1: none)
+    int2 *d_rh = nullptr;              // [cap_req] (rank, hang) of the last batch's requests (k_finalize)
     int *d_reqbuf = nullptr, *d_respbuf = nullptr;  // host-API staging
     int *d_dem = nullptr;              // [T]
     int *d_theta = nullptr;            // [T] threshold bin (-1 none)
@@ -317,9 +320,11 @@ struct adlbq_server {
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int fuse_finalize = 0;             // "fuse_finalize": k_finalize inside the final k_chain0 launch (measured even: off)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
-    int fuse_rank = 0;
-    int fold_thresholds = 0;
-    int *d_fold = nullptr;             // k_prep_hist's folded-thresholds arrival counters           // "fold_thresholds": k_thresholds' work in pass 1's last workgroups                 // "fuse_rank": T <= 8, no k_rank launch; k_chain0 ranks when k_select_open did not
+    int fuse_rank = 1;                 // "fuse_rank": T <= 8, no k_rank launch when the newest landed batch needed
+                                       // none; k_chain0 then ranks itself if this batch's k_select_open did not
+    int fold_thresholds = 0;           // "fold_thresholds": k_thresholds' work in pass 1's last workgroups
+                                       // (measured slower: off)
+    int *d_fold = nullptr;             // k_prep_hist's folded-thresholds arrival counters
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]
@@ -373,6 +378,7 @@ int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
+bool rank_skip_hint(adlbq_server *h);  // ... and every type had candidates (k_rank may be skipped)
 bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi = nullptr);
 inline void wq_changed(adlbq_server *h) { h->batch_export_k = 0; }  // the last batch's lists no longer describe the wq  // newest landed batch's candidate sort plan
 bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper

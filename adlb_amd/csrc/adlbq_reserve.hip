@@ -70,6 +70,7 @@ struct PrepArgs {
     int *tlist;         // [buckets][tcap] request indices, any order
     int tcap;
     int dem_extra;      // candidates listed per type beyond the demand (a steal group's export depth)
+    int2 *rh;           // [R] out: (rank, hang) of each request, compact for k_finalize (or nullptr)
 };
 
 template <int TB>  // TB >= T; TB <= 8: the user types are compared in registers
@@ -109,6 +110,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
     unsigned long long m = 0;
     if (threadIdx.x < nj) {
         tmatch[j] = -1;
+        if (a.rh != nullptr) a.rh[j] = make_int2(rows[threadIdx.x * PREP_ROW], rows[threadIdx.x * PREP_ROW + 1]);
         const int *rt = rows + threadIdx.x * PREP_ROW + 2;
         bool wild = false;
 #pragma unroll
@@ -600,6 +602,7 @@ struct FoldArgs {
 
 constexpr long long FOLD_WAIT_TICKS = 100ll * 1000 * 1000;  // 1 s at the 100 MHz constant clock
 constexpr int FOLD_MAX_NL = ADLBQ_MAX_TYPES * NB / 8;
+constexpr int FOLD_AUTO_PAGES = 1024;
 
 __device__ void fold_thresholds(const FoldArgs &f, int T, unsigned int *csum, unsigned int *lds) {
     // two-level arrival (one counter per role group, then the top counter): a
@@ -954,6 +957,9 @@ __global__ __launch_bounds__(256) void k_select_open(
     }
     if (fast && p == 0 && threadIdx.x == 0) ctr->rank_fast = 1;
     if (!fast && crank != nullptr && p == 0 && threadIdx.x == 0) ctr->rank_fast = 0;
+    // the next batch's hint for skipping k_rank: ranked here, and every type has candidates
+    const bool empty = __ballot(tl && len_l <= 0) != 0ull;
+    if (crank != nullptr && p == 0 && threadIdx.x == 0) ctr->rank_covered = (fast && !empty) ? 1 : 0;
 }
 
 // k_select_open with one workgroup per chunk of CHUNK pages, in order (the
@@ -2025,8 +2031,11 @@ struct RankArgs {
     SegGuess sgv;
 };
 
-// The rank work of workgroup bid of nb (RANK_TILE threads).
+// The rank work of workgroup bid of nb (NT threads: k_rank's NT, or a
+// 64-thread k_chain0 workgroup doing it in place of a skipped k_rank launch).
+template <int NT>
 __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const int bid, const int nb) {
+    constexpr int NW = NT / 64, SROWS = NW > 3 ? NW : 3;  // span: NW search rows, at least the sort's 24 KB
     const int T = ra.T;
     const int *__restrict__ candoff = ra.candoff;
     const int *__restrict__ candlen = ra.candlen;
@@ -2043,11 +2052,11 @@ __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const in
     const DevCounters *ctr = ra.ctr;
     const SegGuess &sgv = ra.sgv;
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
-    __shared__ unsigned long long span[4][RANK_SPAN];  // also the sort's LDS blocks
-    static_assert(sizeof(unsigned long long) * 4 * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * SORT_BLK,
+    __shared__ unsigned long long span[SROWS][RANK_SPAN];  // also the sort's LDS blocks
+    static_assert(sizeof(unsigned long long) * SROWS * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * SORT_BLK,
                   "sort_type's LDS fits in span");
     __shared__ unsigned long long s_first, s_last, s_sortmask;
-    __shared__ int s_a0[4], s_len[4], s_tk, s_fast;
+    __shared__ int s_a0[NW], s_len[NW], s_tk, s_fast;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (rs.fail_test && bid == 0 && tid == 0) atomicAdd(rs.sync + ADLBQ_MAX_TYPES + 1, 1);
     // every input of the prologue in one round of loads: list offsets / lengths,
@@ -2125,8 +2134,8 @@ __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const in
             // eight groups of 64 per wave per step, their loads in flight together (a small grid
             // walks the whole batch: 16 waves over 1,024 groups at 65,536 Reserves)
             constexpr int DU = 8;
-            const int waves = nb * (RANK_TILE / 64);
-            for (int g0 = bid * (RANK_TILE / 64) + w; g0 * 64 < R; g0 += waves * DU) {
+            const int waves = nb * (NT / 64);
+            for (int g0 = bid * (NT / 64) + w; g0 * 64 < R; g0 += waves * DU) {
                 unsigned long long m[DU];
                 int tmv[DU];
 #pragma unroll
@@ -2148,7 +2157,7 @@ __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const in
         int acc = 0;
         for (int t = 0; t < T; t++) {
             stile[t] = acc;
-            acc += (slen[t] + RANK_TILE - 1) / RANK_TILE;
+            acc += (slen[t] + NT - 1) / NT;
         }
         stile[T] = acc;
     }
@@ -2163,7 +2172,7 @@ __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const in
     for (int tile = bid; tile < stile[T]; tile += nb) {
         int t = 0;
         while (t + 1 < T && stile[t + 1] <= tile) t++;
-        const int i0 = (tile - stile[t]) * RANK_TILE, n = min(RANK_TILE, slen[t] - i0);
+        const int i0 = (tile - stile[t]) * NT, n = min(NT, slen[t] - i0);
         const unsigned long long *Lt = ckey + soff[t];
         const unsigned long long key = tid < n ? Lt[i0 + tid] : 0ull;
         if (tid == 0) s_first = key;
@@ -2174,7 +2183,7 @@ __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const in
         int lbv[8];  // per type: candidates ranked before this one (level rows, T <= 8)
 #pragma unroll
         for (int u = 0; u < 8; u++) lbv[u] = u == t ? i0 + tid : 0;
-        for (int r0 = 0; r0 < T; r0 += 4) {  // wave w takes type r0 + w; every wave meets every barrier
+        for (int r0 = 0; r0 < T; r0 += NW) {  // wave w takes type r0 + w; every wave meets every barrier
             const int u = r0 + w;
             int a0 = 0, len = -1;
             if (u < T && u != t && slen[u] > 0) {
@@ -2210,7 +2219,7 @@ __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const in
             }
             __syncthreads();
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < NW; q++) {
                 const int lq = s_len[q], aq = s_a0[q];
                 if (lq < 0 || tid >= n) continue;
                 const int lb = lq <= RANK_SPAN ? lower_bound_key(span[q], lq, key)
@@ -2233,7 +2242,7 @@ __device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const in
     }
 }
 
-__global__ __launch_bounds__(RANK_TILE) void k_rank(RankArgs ra) { rank_body(ra, blockIdx.x, gridDim.x); }
+__global__ __launch_bounds__(RANK_TILE) void k_rank(RankArgs ra) { rank_body<RANK_TILE>(ra, blockIdx.x, gridDim.x); }
 
 // ---------------------------------------------------------------- ordered choice: rounds over segment prefixes
 //
@@ -2289,7 +2298,7 @@ struct ChainArgs {
     unsigned int sg_epoch;
     int *walked;                     // [nseg] fused finalize: == wepoch for a segment the walk re-solved (or nullptr)
     unsigned int wepoch;
-    // k_chain0 launched with RANK_TILE threads in place of a k_rank launch (T <= 8): rank_bar[2] = grid barrier
+    // k_chain0 in place of a skipped k_rank launch (T <= 8): rank_bar[2] = its grid barrier
     int rank_fuse;
     int *rank_bar;
     RankArgs rk;
@@ -3049,6 +3058,7 @@ struct FinArgs {
     int *sortfail;
     int *done;  // fused into k_chain0: [0] = the chain epoch once the choices are final
     int *mslot;  // [R] out: the slot request j was given, or -1 (adlbq_unreserve_resp_device reads it back)
+    const int2 *rh;  // [R] (rank, hang) as prep_block copied them: 8 B per request instead of a 72 B record stride
 };
 
 // k_rank gave up waiting for an in-launch candidate sort: the lists may be
@@ -3061,8 +3071,8 @@ __device__ __forceinline__ bool fin_failed(const FinArgs &f) {
 // Request j (j < R): pin its unit and write its response; true when it parks
 // (words [10], [11] are then left to the park tail).
 __device__ __forceinline__ bool fin_request(const FinArgs &f, int j, bool failed) {
-    const int *rq = f.reqs + (long long)ADLBQ_RESERVE_INTS * j;
-    const int rank = rq[0], hang = failed ? 0 : rq[1];
+    const int2 rk = f.rh[j];
+    const int rank = rk.x, hang = failed ? 0 : rk.y;
     const int tm = f.tmatch[j], um = f.umatch[j];
     const int slot = failed ? -1 : tm >= 0 ? tm : (um >= 0 ? f.cslot[um] : -1);
     f.mslot[j] = slot;
@@ -3219,9 +3229,9 @@ __device__ __forceinline__ void fin_seg_load(const FinArgs &f, int s, FinSeg &g)
     for (int u = 0; u < FIN_U; u++) {
         const int j = j0 + u * 64 + lane;
         const bool in = j < f.R;
-        const int *rq = f.reqs + (long long)ADLBQ_RESERVE_INTS * (in ? j : 0);
-        g.rank[u] = in ? rq[0] : 0;
-        g.hang[u] = in ? rq[1] : 0;
+        const int2 rk = in ? f.rh[j] : make_int2(0, 0);
+        g.rank[u] = rk.x;
+        g.hang[u] = rk.y;
         tm[u] = in ? f.tmatch[j] : -1;
         um[u] = in ? f.umatch[j] : -1;
     }
@@ -3348,23 +3358,21 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, i
     fin_tail(f, total, failed);  // reads other segments' data only through sc1 / atomic loads
 }
 
-// k_chain0 in place of the k_rank launch (T <= 8; RANK_TILE threads per
-// workgroup, every workgroup resident).  When k_select_open ranked every
-// candidate and every type has candidates (the usual case) nothing happens
-// here.  Otherwise every workgroup runs k_rank's body (sorts, ranks, level
-// rows, guess counts), then all meet at a grid barrier: each publishes with an
-// agent-scope release before its arrival, each reads after an agent-scope
-// acquire (MI355X_MICROARCH.md, inter-workgroup visibility), since the chain's
-// waves read what other CUs wrote.  A barrier that does not complete within a
-// second answers the batch ADLB_ERROR (the sort-timeout path).  Wave 0 then
-// goes on with the chain; the others return.
+// k_chain0 in place of a k_rank launch the host skipped (T <= 8; the newest
+// landed batch had k_select_open rank every candidate and every type some).
+// When this batch's flags say so too (the usual case) nothing happens here.
+// Otherwise every workgroup (one wave each) runs k_rank's body, then all meet
+// at a grid barrier: each publishes with an agent-scope release before its
+// arrival, each reads after an agent-scope acquire (MI355X_MICROARCH.md,
+// inter-workgroup visibility), since the chain reads what other CUs wrote.  A
+// barrier that does not complete within a second answers the batch
+// ADLB_ERROR (the sort-timeout path).
 constexpr long long RANK_BAR_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
-constexpr int RANK_FUSE_MAX_SEG = 256;  // one workgroup per CU: every one resident for the barrier
+constexpr int RANK_FUSE_MAX_SEG = 256;  // every workgroup resident for the barrier
 
-// All waves of the workgroup: k_rank's body, then the grid barrier.
 __device__ __attribute__((noinline)) void chain_rank_run(const ChainArgs &a) {
     const RankArgs &ra = a.rk;
-    rank_body(ra, blockIdx.x, gridDim.x);
+    rank_body<64>(ra, blockIdx.x, gridDim.x);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -3395,17 +3403,9 @@ __device__ __attribute__((noinline)) void chain_rank_run(const ChainArgs &a) {
 // the previous pass and re-solves (seeded) only if it differs from its own
 // start; finally each segment checks its start against its predecessor's last
 // end.  A launch in which every check holds is the fixed point.
-template <int TB, int NT = 64>  // NT = RANK_TILE: the k_rank launch was skipped (a.rank_fuse)
-__global__ __launch_bounds__(NT) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
+template <int TB>
+__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
                                                int fuse) {
-    __shared__ int s_need;
-    if constexpr (NT > 64) {
-        if (threadIdx.x >= 64) {  // waves 1..3 only help with a rank wave 0 finds missing
-            __syncthreads();
-            if (s_need) chain_rank_run(a);
-            return;
-        }
-    }
     extern __shared__ unsigned int win[];
     const int lane = threadIdx.x, T = a.T, s = blockIdx.x, nseg = a.nseg, P = cp.passes;
     chain_stamp(a, s, 0);
@@ -3432,7 +3432,7 @@ __global__ __launch_bounds__(NT) void k_chain0(ChainArgs a, ChainPass cp, int pr
     // in place of a k_rank launch: whether k_select_open ranked every candidate and every type has
     // some (else k_rank's body runs here first), loaded with the rest of the prologue
     int rk_ns = 0, rk_fast = 1;
-    if constexpr (NT > 64) {
+    if (TB <= 8 && a.rank_fuse) {
         rk_ns = lane < T ? a.rk.rs.needsort[lane] : 0;
         rk_fast = a.rk.ctr->rank_fast;
     }
@@ -3452,11 +3452,9 @@ __global__ __launch_bounds__(NT) void k_chain0(ChainArgs a, ChainPass cp, int pr
         return acc;
     };
     if (!sg_ok) J = count_J();
-    if constexpr (NT > 64) {
+    if (TB <= 8 && a.rank_fuse) {
         const bool need = __ballot(lane < T && (my_len <= 0 || (rk_ns == 1 && my_len > 1))) != 0ull || rk_fast != 1;
-        if (lane == 0) s_need = need ? 1 : 0;
-        __syncthreads();
-        if (need) {  // rare: sorts, ranks, level rows, guess counts first, then the counts again
+        if (need) {  // the hint did not hold: sorts, ranks, level rows, guess counts first, then the counts again
             chain_rank_run(a);
             if (!sg_ok) J = count_J();
         }
@@ -3594,7 +3592,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     if (n <= h->cap_req) return ADLBQ_OK;
     int nc = std::max(n, std::max(1024, h->cap_req * 2));
     AQ_HIP(hipStreamSynchronize(h->stream));
-    void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_mslot, h->d_reqbuf, h->d_respbuf,
+    void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_mslot, h->d_rh, h->d_reqbuf, h->d_respbuf,
                   h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht,
                   h->d_chcnt, h->d_chE, h->d_chflag, h->d_pmask, h->d_lv, h->d_rtype};
     for (void *p : ps)
@@ -3603,6 +3601,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_tmatch, sizeof(int) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_umatch, sizeof(int) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_mslot, sizeof(int) * nc));
+    AQ_HIP(hipMalloc((void **)&h->d_rh, sizeof(int2) * nc));
     AQ_HIP(hipMemsetAsync(h->d_mslot, 0xff, sizeof(int) * nc, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_reqbuf, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
@@ -3704,7 +3703,9 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     const int grid = nprep + (scan ? npb : 0);
     // k_thresholds folded into pass 1's last workgroups: 8 columns per role (4..64), every role a workgroup
     FoldArgs fd{};
-    if (scan && h->fold_thresholds && !h->split_prep) {
+    // fold_thresholds 1: always; 2: on queues of at most FOLD_AUTO_PAGES pages (a launch saved
+    // weighs more than the folded tail there; measured slower on the 10M-unit metric queue)
+    if (scan && (h->fold_thresholds == 1 || (h->fold_thresholds == 2 && np <= FOLD_AUTO_PAGES)) && !h->split_prep) {
         const int C1 = T * NB;
         int ncol = 8;
         while (ncol < 64 && C1 / ncol > grid) ncol *= 2;
@@ -4691,7 +4692,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hipEvent_t ev;
 
     PrepArgs pa{d_reqs, R, h->d_utypes, T, h->d_mask, h->d_dem, h->d_seg_cnt, h->d_ctr, h->d_tmatch,
-                nullptr, 0, nullptr, nullptr, 0, h->export_extra};
+                nullptr, 0, nullptr, nullptr, 0, h->export_extra, h->d_rh};
     const int nb = (int)h->bucket_ranks.size();
     const bool targeted = h->live_targeted > 0 && nb > 0;
     if (targeted && nb < (1 << 20)) {  // per-bucket Reserve lists for k_targeted_idx
@@ -4756,7 +4757,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     // T <= 8 with a small enough grid: no k_rank launch, k_chain0 runs its body when needed
     const int nseg0 = (R + SEG - 1) / SEG;
     const bool rank_fused = np > 0 && T > 0 && T <= 8 && h->fuse_rank && !h->fuse_finalize && !h->seg_guess &&
-                            !h->rank_grid && nseg0 <= RANK_FUSE_MAX_SEG;
+                            !h->rank_grid && nseg0 <= RANK_FUSE_MAX_SEG && (h->fuse_rank == 2 || rank_skip_hint(h));
     RankArgs rka{};
     if (np > 0 && T > 0) {
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
@@ -4784,7 +4785,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                      h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
                      h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, T, snap, h->snap_tag[h->snap_next],
                      h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
-                     h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot};
+                     h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot, h->d_rh};
     bool fused = false;
     stage_begin(h, "chain", &ev);
     {
@@ -4841,8 +4842,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             ca.rank_fuse = 1;
             ca.rank_bar = h->d_rank_sync + ADLBQ_MAX_TYPES + 2;
             ca.rk = rka;
-            if (T <= 4) k_chain0<4, RANK_TILE><<<nseg, RANK_TILE, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
-            else k_chain0<8, RANK_TILE><<<nseg, RANK_TILE, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
+            if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
+            else k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
         } else if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);

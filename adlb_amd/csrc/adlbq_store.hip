@@ -117,6 +117,11 @@ bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi) {
     return *g > 0;
 }
 
+bool rank_skip_hint(adlbq_server *h) {
+    const int i = newest_landed(h);
+    return i >= 0 && h->h_snap[i].rank_covered == 1;
+}
+
 bool sort_hint(adlbq_server *h) {
     const int i = newest_landed(h);
     // nothing landed yet (the first batches): sort whatever needs it through the
@@ -1307,7 +1312,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
                     h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg,
-                    h->d_mslot, h->d_fold};
+                    h->d_mslot, h->d_fold, h->d_rh};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -2180,12 +2185,13 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         return ADLBQ_OK;
     }
     if (n == "fold_thresholds") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0 or 1");
+        if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0, 1 or 2 (auto)");
         h->fold_thresholds = (int)value;
         return ADLBQ_OK;
     }
     if (n == "fuse_rank") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "fuse_rank must be 0 or 1");
+        // 2 (test hook): skip k_rank whatever the hint, so the chain ranks whenever this batch needs it
+        if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fuse_rank must be 0, 1 or 2");
         h->fuse_rank = (int)value;
         return ADLBQ_OK;
     }

@@ -50,6 +50,8 @@ STAGES = ["hist", "thresholds", "select", "sort", "targeted", "rank", "chain", "
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process unless set (0: HIP's default)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--units", type=int, default=10_000_000)
@@ -76,6 +78,8 @@ def parse():
     ap.add_argument("--c3-warmup", type=int, default=8, help="config 3: untimed steps (rq and export buffers grow)")
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
+    ap.add_argument("--c3-param", action="append", default=[], metavar="NAME=V",
+                    help="config 3: adlbq_set_param on every shard (repeatable)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 stream measurement")
     ap.add_argument("--config5-only", action="store_true", help="only the config-5 leg")
@@ -317,6 +321,9 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         idx = rank * SL + j
         w = synth.config3_shard(idx, S, N, T, R, seed=args.seed)
         srv = Server(w.user_types, w.num_app_ranks, S, idx, max_units=N, device=local)
+        for kv in args.c3_param:
+            k_, v_ = kv.split("=", 1)
+            srv.set_param(k_, int(v_))
         st = torch.cuda.Stream(dev)
         srv.set_stream(st.cuda_stream)
         srv.put_batch(np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1),
@@ -344,8 +351,12 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         def __init__(self, decided, settled):
             self.decided, self.settled = decided, settled
 
+    # device pointers of every (shard, batch) once: no tensor views inside the timed loop
+    p_req = [[d_reqs[j][b].data_ptr() for b in range(nb)] for j in range(len(srvs))]
+    p_resp = [[d_resp[j][b].data_ptr() for b in range(nb)] for j in range(len(srvs))]
+
     def enqueue(j, b):
-        srvs[j].reserve_batch_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
+        srvs[j].reserve_batch_device(R, p_req[j][b], p_resp[j][b])
 
     def step(b, timed_parts=False):
         t0 = time.perf_counter()
@@ -362,7 +373,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         nd, ns = group.round(timing=tm)
         t2 = time.perf_counter()
         for j, srv in enumerate(srvs):
-            srv.unreserve_resp_device(R, d_reqs[j][b].data_ptr(), d_resp[j][b].data_ptr())
+            srv.unreserve_resp_device(R, p_req[j][b], p_resp[j][b])
         group.unreserve_grants()
         if timed_parts:
             for key in ("copy_ns", "merge_ns", "apply_ns"):
@@ -721,15 +732,19 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     host_parts = {"put": 0.0, "reserve": 0.0, "unreserve": 0.0}
     applied = []  # put batches in the order they went in (wqseqnos follow it)
 
+    p_req = [d_reqs[b].data_ptr() for b in range(nb)]  # no tensor views inside the timed loop
+    p_resp = [d_resp[b].data_ptr() for b in range(nb)]
+    p_pout = d_pout.data_ptr() if puts is not None else 0
+
     def step(b):
         t0 = time.perf_counter()
         if puts is not None:  # device-resident results: no host round trip
-            srv.put_batch_device(puts[b], d_pout.data_ptr())
+            srv.put_batch_device(puts[b], p_pout)
             applied.append(b)
         t1 = time.perf_counter()
-        srv.reserve_batch_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        srv.reserve_batch_device(R, p_req[b], p_resp[b])
         t2 = time.perf_counter()
-        srv.unreserve_resp_device(R, d_reqs[b].data_ptr(), d_resp[b].data_ptr())
+        srv.unreserve_resp_device(R, p_req[b], p_resp[b])
         host_parts["put"] += t1 - t0
         host_parts["reserve"] += t2 - t1
         host_parts["unreserve"] += time.perf_counter() - t2
@@ -818,6 +833,10 @@ def main():
     pmc = None
     if world0 == 1 and not args.no_pmc:
         pmc = pmc_traffic(args)  # before this process initialises the GPU
+    # one hardware queue per server shard's stream (HIP's default is 4): config 3's
+    # 8 shards and config 5's 8 streams then run side by side instead of 2 per queue
+    if args.hw_queues > 0 and "GPU_MAX_HW_QUEUES" not in os.environ:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import torch.distributed as dist
 

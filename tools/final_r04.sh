@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 evidence on one MI355X (outputs under gpurun_out/r04/):
 #   final_r04.sh tests   every GPU test + smoke
-#   final_r04.sh sel "<pytest -k expr or file list>"   selected GPU tests
+#   final_r04.sh sel <pytest arguments>   selected GPU tests
 #   final_r04.sh prof    rocprofv3 kernel stats per bench leg + the step timeline
 #   final_r04.sh bench   the default bench
 #   final_r04.sh all     tests, prof, bench
@@ -15,7 +15,8 @@ trap "kill $HB" EXIT
 python -c "import torch" > /dev/null 2>&1
 PART=${1:-all}
 if [ "$PART" = "sel" ]; then
-  timeout -k 10 900 python -u -m pytest $2 -m gpu -v -x --timeout 200 --timeout-method thread > $O/sel.log 2>&1
+  shift
+  timeout -k 10 900 python -u -m pytest "$@" -m gpu -v -x --timeout 200 --timeout-method thread > $O/sel.log 2>&1
   rc=$?; echo "[sel] rc=$rc $(tail -1 $O/sel.log)"
   [ $rc -ne 0 ] && grep -E "FAIL|Error|assert" $O/sel.log | head -30
   exit $rc
