@@ -25,12 +25,14 @@ SIGNATURES = {
     "adlbq_put_batch_device": (c_int, [P, c_int, P, P]),
     "adlbq_reserve_batch": (c_int, [P, c_int, P, P]),
     "adlbq_reserve_batch_device": (c_int, [P, c_int, P, P]),
+    "adlbq_reserve_group_device": (c_int, [P, c_int, P, P, P]),
     "adlbq_get_reserved": (c_int, [P, c_int, c_int, P]),
     "adlbq_get_reserved_batch": (c_int, [P, c_int, P, P]),
     "adlbq_get_reserved_batch_device": (c_int, [P, c_int, P, P]),
     "adlbq_unreserve": (c_int, [P, c_int, c_int, c_int, P]),
     "adlbq_unreserve_batch_device": (c_int, [P, c_int, P]),
     "adlbq_unreserve_resp_device": (c_int, [P, c_int, P, P]),
+    "adlbq_unreserve_resp_group_device": (c_int, [P, c_int, P, P, P]),
     "adlbq_qmstat_row": (c_int, [P, P, P]),
     "adlbq_set_qmstat_row": (c_int, [P, c_int, c_int, c_double, P]),
     "adlbq_check_remote": (c_int, [P, c_int, P, P]),

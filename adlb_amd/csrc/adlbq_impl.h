@@ -22,6 +22,8 @@
 
 #include "adlbq.h"
 
+struct GroupRec;  // adlbq_reserve.hip: a reserve batch's launches recorded for a group launch
+
 namespace adlbq {
 
 // the ordered choice (adlbq_reserve.hip): requests per segment (one wavefront)
@@ -320,11 +322,22 @@ struct adlbq_server {
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int fuse_finalize = 0;             // "fuse_finalize": k_finalize inside the final k_chain0 launch (measured even: off)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
-    int fuse_rank = 1;                 // "fuse_rank": T <= 8, no k_rank launch when the newest landed batch needed
+    int fuse_rank = 0;                 // "fuse_rank": T <= 8, no k_rank launch when the newest landed batch needed
                                        // none; k_chain0 then ranks itself if this batch's k_select_open did not
+                                       // (off: that k_chain0 instance carries k_rank's registers and stack,
+                                       // measured +16 us against the 8 us launch it saves)
     int fold_thresholds = 0;           // "fold_thresholds": k_thresholds' work in pass 1's last workgroups
                                        // (measured slower: off)
     int *d_fold = nullptr;             // k_prep_hist's folded-thresholds arrival counters
+    int group_launch = 1;              // "group_launch": 0 = adlbq_reserve_group_device launches this handle alone
+    ::GroupRec *grec = nullptr;        // non-null: launch_reserve records its launches (adlbq_reserve_group_device)
+    // the group launch's argument tables (kept by the group's first handle): pinned staging x 2, device copy
+    char *h_gtab[2] = {nullptr, nullptr};
+    hipEvent_t gtab_ev[2] = {nullptr, nullptr};
+    char *d_gtab = nullptr;
+    size_t cap_gtab = 0;
+    int gtab_slot = 0;
+    std::vector<hipEvent_t> gjoin;     // one per grouped handle: its stream joins the launch stream
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]
@@ -388,8 +401,27 @@ void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
 // host time since t0 added to stage `name` (profiling only; no events)
 void host_stage_add(adlbq_server *h, const char *name, std::chrono::steady_clock::time_point t0);
 int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
+int group_join(adlbq_server *const *hs, const std::vector<int> &m);     // hs[m[0]]'s stream waits for the members'
+int group_release(adlbq_server *const *hs, const std::vector<int> &m);  // the members' streams wait for hs[m[0]]'s
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail);
 bool launch_export_after(adlbq_server *h, int k, int *d_recs, int *d_nrec, long long *d_navail);
+// the grouped form (adlbq_steal_group_export): one shard's k_export_after arguments, when its last
+// batch's lists serve an export of depth k; EXPORT_GROUP shards per launch, kernel arguments
+struct ExportAfterArgs {
+    int T, k, R;
+    const unsigned char *cht;
+    const int *candoff, *candlen, *cslot, *prio, *seqa;
+    const int4 *cold0, *cold1;
+    int *recs, *nrec;
+    long long *navail;
+    const unsigned int *coltot;
+};
+constexpr int EXPORT_GROUP = 16;
+struct ExportAfterGroup {
+    ExportAfterArgs a[EXPORT_GROUP];
+};
+bool export_after_args(adlbq_server *h, int k, int *d_recs, int *d_nrec, long long *d_navail, ExportAfterArgs *a);
+int launch_export_after_group(const ExportAfterGroup &g, int n, int k, int Tmax, hipStream_t s);
 
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ unsigned long long make_key(int prio, unsigned int order) {

@@ -513,16 +513,16 @@ __device__ void type_threshold(const int t, const int *__restrict__ dem, int *th
 // demand is reached and how many units of it are needed.  Candidate list
 // offsets (the prefix of candlen over types) follow in k_select_open.
 constexpr int TH_THREADS = 256;  // chunks per step of the column scan
-__global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, long long zn, int T, const int *__restrict__ dem, unsigned int *csum,
+__device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn, int T, const int *__restrict__ dem, unsigned int *csum,
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
                                                      int *type_cnt, const long long *__restrict__ anchor,
                                                      long long *__restrict__ anchor_next,
-                                                     long long *__restrict__ gcut_next, int guess) {
+                                                     long long *__restrict__ gcut_next, int guess, const int bid_, const int nbk_) {
     constexpr int NW = TH_THREADS / 64;
     __shared__ unsigned int wsum[NW];
     __shared__ bool s_last;
-    const int c = blockIdx.x, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = bid_, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     unsigned int carry = 0;
     // the first TH_PRE rows' loads all in flight before the first scan step
     constexpr int TH_PRE = 4;
@@ -562,13 +562,22 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, lo
     }
     // the previous scan's chunk sums (consumed): zeroed for the scan after this one, a slice per workgroup
     if (zn > 0) {
-        const long long per = (zn + gridDim.x - 1) / gridDim.x, z0 = (long long)blockIdx.x * per;
+        const long long per = (zn + nbk_ - 1) / nbk_, z0 = (long long)bid_ * per;
         for (long long i = z0 + threadIdx.x; i < min(zn, z0 + per); i += TH_THREADS) zcs[i] = 0u;
     }
     __syncthreads();
     if (!s_last || threadIdx.x >= 64) return;
     type_threshold(t, dem, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next,
                    guess);
+}
+
+__global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, long long zn, int T, const int *__restrict__ dem, unsigned int *csum,
+                                                     int nchunks, int *theta, int *need, int *candlen,
+                                                     int *needsort, int *binoff, unsigned int *coltot,
+                                                     int *type_cnt, const long long *__restrict__ anchor,
+                                                     long long *__restrict__ anchor_next,
+                                                     long long *__restrict__ gcut_next, int guess) {
+    thresholds_body(zcs, zn, T, dem, csum, nchunks, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next, guess, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------- thresholds folded into pass 1
@@ -604,14 +613,14 @@ constexpr long long FOLD_WAIT_TICKS = 100ll * 1000 * 1000;  // 1 s at the 100 MH
 constexpr int FOLD_MAX_NL = ADLBQ_MAX_TYPES * NB / 8;
 constexpr int FOLD_AUTO_PAGES = 1024;
 
-__device__ void fold_thresholds(const FoldArgs &f, int T, unsigned int *csum, unsigned int *lds) {
+__device__ void fold_thresholds(const FoldArgs &f, int T, unsigned int *csum, unsigned int *lds, const int bid) {
     // two-level arrival (one counter per role group, then the top counter): a
     // single counter taking every workgroup's add serialised them (tens of us)
     __shared__ int s_role;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int g = (int)blockIdx.x % f.nl, ng = (f.total - g + f.nl - 1) / f.nl;
+        const int g = bid % f.nl, ng = (f.total - g + f.nl - 1) / f.nl;
         const int v = __hip_atomic_fetch_add(f.arrive + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int role = -1;
         if (v == ng - 1) {  // the group is complete: this workgroup takes its role once every group is
@@ -688,21 +697,26 @@ __device__ void fold_thresholds(const FoldArgs &f, int T, unsigned int *csum, un
 // workgroups [0, nprep) prepare 256 requests each, the rest count one page;
 // with fd.on the last workgroups then do k_thresholds' work.
 template <int TB, int PPB = 1>
-__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd) {
+__device__ __forceinline__ void prep_hist_body(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd, const int bid_, const int nbk_) {
     static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
     extern __shared__ unsigned int lds[];
-    if ((int)blockIdx.x < nprep) {
-        prep_block<TB>(pa, blockIdx.x, reinterpret_cast<int *>(lds));
+    if ((int)bid_ < nprep) {
+        prep_block<TB>(pa, bid_, reinterpret_cast<int *>(lds));
     } else {
-        if (ha.variant == 0) hist_page_v0(ha, blockIdx.x - nprep, lds);
-        else hist_pages<PPB>(ha, (blockIdx.x - nprep) * PPB, lds);
+        if (ha.variant == 0) hist_page_v0(ha, bid_ - nprep, lds);
+        else hist_pages<PPB>(ha, (bid_ - nprep) * PPB, lds);
         if (fd.on && fd.zn > 0) {  // the previous scan's chunk sums (consumed): zeroed for the scan after this one
-            const long long npb = (long long)gridDim.x - nprep, b = (long long)blockIdx.x - nprep;
+            const long long npb = (long long)nbk_ - nprep, b = (long long)bid_ - nprep;
             const long long per = (fd.zn + npb - 1) / npb, z0 = b * per;
             for (long long i = z0 + threadIdx.x; i < min(fd.zn, z0 + per); i += blockDim.x) fd.zcs[i] = 0u;
         }
     }
-    if (fd.on) fold_thresholds(fd, ha.T, ha.csum, lds);
+    if (fd.on) fold_thresholds(fd, ha.T, ha.csum, lds, bid_);
+}
+
+template <int TB, int PPB = 1>
+__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd) {
+    prep_hist_body<TB>(pa, nprep, ha, fd, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------- pass 2
@@ -717,7 +731,7 @@ __global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistA
 //   4. a candidate's rank in its column = that start + the number of equal
 //      columns earlier in the wave's list (64 list entries per step).
 template <int TB>  // TB >= T; the candidates are ranked here only for TB <= RT
-__global__ __launch_bounds__(256) void k_select_open(
+__device__ __forceinline__ void select_open_body(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
     const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
     const int *__restrict__ theta, const int *__restrict__ need,
@@ -726,13 +740,13 @@ __global__ __launch_bounds__(256) void k_select_open(
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
     const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
     const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
-    unsigned char *__restrict__ rtype, int R) {
+    unsigned char *__restrict__ rtype, int R, const int bid_, const int nbk_) {
     constexpr int RT = TB <= RANK_FAST_T ? TB : 1;  // types of the fast ranking
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
     __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES], slen[RT];
     __shared__ int sbo[RT * NB];  // binoff (fast ranking)
-    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = blockIdx.x;
+    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = bid_;
     unsigned int *wc = lds;
     unsigned int *list = lds + 4 * C + w * 1024;
     const long long base = (long long)pages[p] << PAGE_SHIFT;
@@ -960,6 +974,20 @@ __global__ __launch_bounds__(256) void k_select_open(
     // the next batch's hint for skipping k_rank: ranked here, and every type has candidates
     const bool empty = __ballot(tl && len_l <= 0) != 0ull;
     if (crank != nullptr && p == 0 && threadIdx.x == 0) ctr->rank_covered = (fast && !empty) ? 1 : 0;
+}
+
+template <int TB>  // TB >= T; the candidates are ranked here only for TB <= RT
+__global__ __launch_bounds__(256) void k_select_open(
+    const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
+    const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
+    const int *__restrict__ theta, const int *__restrict__ need,
+    const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
+    const int *__restrict__ candlen, int *__restrict__ candoff_out,
+    unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
+    const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
+    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
+    unsigned char *__restrict__ rtype, int R) {
+    select_open_body<TB>(pages, npages, tail_fill, prio, meta, seqa, T, anchor, theta, need, binoff, csum, gh, candlen, candoff_out, ckey, cslot, gcut, spec, specn, pbase, pwide, ctr, crank, lv, rtype, R, blockIdx.x, gridDim.x);
 }
 
 // k_select_open with one workgroup per chunk of CHUNK pages, in order (the
@@ -2034,7 +2062,7 @@ struct RankArgs {
 // The rank work of workgroup bid of nb (NT threads: k_rank's NT, or a
 // 64-thread k_chain0 workgroup doing it in place of a skipped k_rank launch).
 template <int NT>
-__device__ __attribute__((noinline)) void rank_body(const RankArgs &ra, const int bid, const int nb) {
+__device__ __forceinline__ void rank_body(const RankArgs &ra, const int bid, const int nb) {
     constexpr int NW = NT / 64, SROWS = NW > 3 ? NW : 3;  // span: NW search rows, at least the sort's 24 KB
     const int T = ra.T;
     const int *__restrict__ candoff = ra.candoff;
@@ -3176,10 +3204,10 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
     }
 }
 
-__global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
+__device__ __forceinline__ void finalize_body(FinArgs f, const int bid_, const int nbk_) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = bid_ * blockDim.x + threadIdx.x;
     if (threadIdx.x == 0) s_parked = 0;
     const bool failed = fin_failed(f);
     __syncthreads();
@@ -3194,10 +3222,14 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) s_ticket = fin_arrive(f, s_parked, gridDim.x, blockIdx.x);
+    if (threadIdx.x == 0) s_ticket = fin_arrive(f, s_parked, nbk_, bid_);
     __syncthreads();
     if (!(s_ticket & 1ull)) return;
     fin_tail(f, (int)(s_ticket >> 32), failed);
+}
+
+__global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
+    finalize_body(f, blockIdx.x, gridDim.x);
 }
 
 // k_finalize fused into the final k_chain0 launch (every segment one
@@ -3370,16 +3402,16 @@ __device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, i
 constexpr long long RANK_BAR_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
 constexpr int RANK_FUSE_MAX_SEG = 256;  // every workgroup resident for the barrier
 
-__device__ __attribute__((noinline)) void chain_rank_run(const ChainArgs &a) {
+__device__ __attribute__((noinline)) void chain_rank_run(const ChainArgs &a, const int bid, const int nb) {
     const RankArgs &ra = a.rk;
-    rank_body<64>(ra, blockIdx.x, gridDim.x);
+    rank_body<64>(ra, bid, nb);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int v = __hip_atomic_fetch_add(a.rank_bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v == (int)gridDim.x - 1) {  // the last arrival: reset for the next batch, release the others
+        if (v == nb - 1) {  // the last arrival: reset for the next batch, release the others
             __hip_atomic_store(a.rank_bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(a.rank_bar + 1, (int)ra.rs.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
@@ -3403,11 +3435,11 @@ __device__ __attribute__((noinline)) void chain_rank_run(const ChainArgs &a) {
 // the previous pass and re-solves (seeded) only if it differs from its own
 // start; finally each segment checks its start against its predecessor's last
 // end.  A launch in which every check holds is the fixed point.
-template <int TB>
-__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
-                                               int fuse) {
+template <int TB, bool RF = false>
+__device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
+                                               int fuse, const int bid_, const int nbk_) {
     extern __shared__ unsigned int win[];
-    const int lane = threadIdx.x, T = a.T, s = blockIdx.x, nseg = a.nseg, P = cp.passes;
+    const int lane = threadIdx.x, T = a.T, s = bid_, nseg = a.nseg, P = cp.passes;
     chain_stamp(a, s, 0);
     if (s == 0 && lane == 0) *a.clean = 0;
     if constexpr (TB <= 8) win[TB * (SEG + a.warm) + lane] = ~0u;  // seg_solve_small's sentinel row
@@ -3432,7 +3464,7 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
     // in place of a k_rank launch: whether k_select_open ranked every candidate and every type has
     // some (else k_rank's body runs here first), loaded with the rest of the prologue
     int rk_ns = 0, rk_fast = 1;
-    if (TB <= 8 && a.rank_fuse) {
+    if (RF && TB <= 8 && a.rank_fuse) {
         rk_ns = lane < T ? a.rk.rs.needsort[lane] : 0;
         rk_fast = a.rk.ctr->rank_fast;
     }
@@ -3452,10 +3484,11 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
         return acc;
     };
     if (!sg_ok) J = count_J();
-    if (TB <= 8 && a.rank_fuse) {
-        const bool need = __ballot(lane < T && (my_len <= 0 || (rk_ns == 1 && my_len > 1))) != 0ull || rk_fast != 1;
+    if constexpr (RF && TB <= 8) {  // RF: the instances with k_rank's body (its call costs the chain registers)
+        const bool need = a.rank_fuse &&
+                          (__ballot(lane < T && (my_len <= 0 || (rk_ns == 1 && my_len > 1))) != 0ull || rk_fast != 1);
         if (need) {  // the hint did not hold: sorts, ranks, level rows, guess counts first, then the counts again
-            chain_rank_run(a);
+            chain_rank_run(a, s, nseg);
             if (!sg_ok) J = count_J();
         }
     }
@@ -3531,6 +3564,80 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
                                        prefix_next != 0, win);
     chain_stamp(a, s, 5);
     if (fuse) fin_fused(f, a.walked, s, last, cp.epoch, nseg);
+}
+
+template <int TB, bool RF = false>
+__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
+                                               int fuse) {
+    chain0_body<TB, RF>(a, cp, prefix_next, final, f, fuse, blockIdx.x, gridDim.x);
+}
+
+// ---------------------------------------------------------------- one launch per kernel for a group of handles
+// adlbq_reserve_group_device: the reserve batches of several handles (a GPU
+// process's server shards) go as ONE launch per pipeline kernel, grid.y =
+// handle, each handle's arguments in a device table (launch_reserve records
+// them instead of launching: GroupRec).  Blocks past a handle's own grid
+// return at once; every body gets its handle's block index and grid size.
+struct GPrep { PrepArgs pa; int nprep; HistArgs ha; FoldArgs fd; int grid; };
+struct GThr {
+    unsigned int *zcs; long long zn; int T; const int *dem; unsigned int *csum; int nchunks;
+    int *theta, *need, *candlen, *needsort, *binoff; unsigned int *coltot; int *type_cnt;
+    const long long *anchor; long long *anchor_next, *gcut_next; int guess; int grid;
+};
+struct GSel {
+    const int *pages; int npages, tail_fill; const int *prio; const uint32_t *meta; const int *seqa; int T;
+    const long long *anchor; const int *theta, *need, *binoff; const unsigned int *csum; const unsigned short *gh;
+    const int *candlen; int *candoff_out; unsigned long long *ckey; int *cslot; const long long *gcut;
+    const unsigned int *spec; const int *specn, *pbase, *pwide; DevCounters *ctr; unsigned int *crank; int *lv;
+    unsigned char *rtype; int R; int grid;
+};
+struct GRank { RankArgs ra; int grid; };
+struct GChain { ChainArgs a; ChainPass cp; int prefix_next, final, fuse; int grid; FinArgs f; };
+struct GFin { FinArgs f; int grid; };
+
+enum : int { GK_PREP = 1, GK_THR = 2, GK_SEL = 4, GK_RANK = 8, GK_CHAIN = 16, GK_FIN = 32 };
+struct GroupRec {
+    int kinds = 0;  // GK_* recorded
+    int tb = 0;     // the TB of the templated kernels (4 or 8)
+    GPrep prep; GThr thr; GSel sel; GRank rank; GChain chain; GFin fin;
+    size_t lds_prep = 0, lds_sel = 0, lds_chain = 0;
+};
+
+template <int TB>
+__global__ __launch_bounds__(256) void k_prep_hist_g(const GPrep *__restrict__ t) {
+    const GPrep &g = t[blockIdx.y];
+    if ((int)blockIdx.x >= g.grid) return;
+    prep_hist_body<TB>(g.pa, g.nprep, g.ha, g.fd, blockIdx.x, g.grid);
+}
+__global__ __launch_bounds__(TH_THREADS) void k_thresholds_g(const GThr *__restrict__ t) {
+    const GThr &g = t[blockIdx.y];
+    if ((int)blockIdx.x >= g.grid) return;
+    thresholds_body(g.zcs, g.zn, g.T, g.dem, g.csum, g.nchunks, g.theta, g.need, g.candlen, g.needsort, g.binoff,
+                    g.coltot, g.type_cnt, g.anchor, g.anchor_next, g.gcut_next, g.guess, blockIdx.x, g.grid);
+}
+template <int TB>
+__global__ __launch_bounds__(256) void k_select_open_g(const GSel *__restrict__ t) {
+    const GSel &g = t[blockIdx.y];
+    if ((int)blockIdx.x >= g.grid) return;
+    select_open_body<TB>(g.pages, g.npages, g.tail_fill, g.prio, g.meta, g.seqa, g.T, g.anchor, g.theta, g.need,
+                         g.binoff, g.csum, g.gh, g.candlen, g.candoff_out, g.ckey, g.cslot, g.gcut, g.spec, g.specn,
+                         g.pbase, g.pwide, g.ctr, g.crank, g.lv, g.rtype, g.R, blockIdx.x, g.grid);
+}
+__global__ __launch_bounds__(RANK_TILE) void k_rank_g(const GRank *__restrict__ t) {
+    const GRank &g = t[blockIdx.y];
+    if ((int)blockIdx.x >= g.grid) return;
+    rank_body<RANK_TILE>(g.ra, blockIdx.x, g.grid);
+}
+template <int TB, bool RF>
+__global__ __launch_bounds__(64) void k_chain0_g(const GChain *__restrict__ t) {
+    const GChain &g = t[blockIdx.y];
+    if ((int)blockIdx.x >= g.grid) return;
+    chain0_body<TB, RF>(g.a, g.cp, g.prefix_next, g.final, g.f, g.fuse, blockIdx.x, g.grid);
+}
+__global__ __launch_bounds__(256) void k_finalize_g(const GFin *__restrict__ t) {
+    const GFin &g = t[blockIdx.y];
+    if ((int)blockIdx.x >= g.grid) return;
+    finalize_body(g.f, blockIdx.x, g.grid);
 }
 
 // ---------------------------------------------------------------- steal export
@@ -3736,6 +3843,11 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
             kph<<<nprep, 256, lds, s>>>(pa, nprep, ha, FoldArgs{});
             kph<<<npb, 256, lds, s>>>(pa, 0, ha, FoldArgs{});
+        } else if (h->grec) {  // adlbq_reserve_group_device: recorded, launched with the group's
+            h->grec->kinds |= GK_PREP;
+            h->grec->tb = T <= 4 ? 4 : 8;
+            h->grec->prep = GPrep{pa, nprep, ha, fd, grid};
+            h->grec->lds_prep = (size_t)lds;
         } else {
             kph<<<grid, 256, lds, s>>>(pa, nprep, ha, fd);
         }
@@ -3743,7 +3855,12 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     }
     if (scan) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
-        if (!fd.on) {
+        if (!fd.on && h->grec) {
+            h->grec->kinds |= GK_THR;
+            h->grec->thr = GThr{zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
+                                h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor, h->d_anchor_next,
+                                h->d_gcut_next, nprep > 0 ? 1 : 0, C};
+        } else if (!fd.on) {
             stage_begin(h, "thresholds", &ev);
             k_thresholds<<<C, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need,
                                                   h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot,
@@ -3755,6 +3872,15 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         const bool chunked = h->select_chunk && T <= 8;  // one workgroup per chunk of pages
         auto sel = chunked ? (T <= 4 ? k_select_chunk<4> : k_select_chunk<8>)
                            : T <= 4 ? k_select_open<4> : T <= 8 ? k_select_open<8> : k_select_open<64>;
+        if (h->grec && !chunked) {
+            h->grec->kinds |= GK_SEL;
+            h->grec->sel = GSel{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor,
+                                h->d_theta, h->d_need, h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff,
+                                h->d_ckey, h->d_cslot, h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide,
+                                h->d_ctr, (sort || !h->rank_in_select) ? nullptr : h->d_crank,
+                                (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R, np};
+            h->grec->lds_sel = sizeof(unsigned int) * (4 * C + 4 * 1024);
+        } else
         sel<<<chunked ? nchunks : np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
@@ -4666,6 +4792,40 @@ static int launch_segsort(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
+// The kernels a handle recorded (GroupRec), launched one by one on its own stream.
+static int launch_recorded(adlbq_server *h, GroupRec &r) {
+    hipStream_t s = h->stream;
+    const bool t4 = r.tb == 4;
+    if (r.kinds & GK_PREP) {
+        auto kph = t4 ? k_prep_hist<4> : k_prep_hist<8>;
+        kph<<<r.prep.grid, 256, r.lds_prep, s>>>(r.prep.pa, r.prep.nprep, r.prep.ha, r.prep.fd);
+    }
+    if (r.kinds & GK_THR) {
+        const GThr &g = r.thr;
+        k_thresholds<<<g.grid, TH_THREADS, 0, s>>>(g.zcs, g.zn, g.T, g.dem, g.csum, g.nchunks, g.theta, g.need,
+                                                   g.candlen, g.needsort, g.binoff, g.coltot, g.type_cnt, g.anchor,
+                                                   g.anchor_next, g.gcut_next, g.guess);
+    }
+    if (r.kinds & GK_SEL) {
+        const GSel &g = r.sel;
+        auto sel = t4 ? k_select_open<4> : k_select_open<8>;
+        sel<<<g.grid, 256, r.lds_sel, s>>>(g.pages, g.npages, g.tail_fill, g.prio, g.meta, g.seqa, g.T, g.anchor,
+                                           g.theta, g.need, g.binoff, g.csum, g.gh, g.candlen, g.candoff_out, g.ckey,
+                                           g.cslot, g.gcut, g.spec, g.specn, g.pbase, g.pwide, g.ctr, g.crank, g.lv,
+                                           g.rtype, g.R);
+    }
+    if (r.kinds & GK_RANK) k_rank<<<r.rank.grid, RANK_TILE, 0, s>>>(r.rank.ra);
+    if (r.kinds & GK_CHAIN) {
+        const GChain &g = r.chain;
+        auto ch = g.a.rank_fuse ? (t4 ? k_chain0<4, true> : k_chain0<8, true>) : (t4 ? k_chain0<4> : k_chain0<8>);
+        ch<<<g.grid, 64, r.lds_chain, s>>>(g.a, g.cp, g.prefix_next, g.final, g.f, g.fuse);
+    }
+    if (r.kinds & GK_FIN) k_finalize<<<r.fin.grid, 256, 0, s>>>(r.fin.f);
+    r.kinds = 0;
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
 int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
     const auto host_t0 = std::chrono::steady_clock::now();
@@ -4726,7 +4886,16 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     h->hacc["l_scan"] += std::chrono::duration_cast<std::chrono::nanoseconds>(hl - scan_t0).count();
     h->last_scan_units = h->live_units - h->live_targeted;
 
+    // a group member whose batch needs a launch between the recorded ones (the targeted index, a
+    // read-back sort) launches what it recorded on its own stream and leaves the group
+    auto leave_group = [&]() -> int {
+        if (!h->grec) return ADLBQ_OK;
+        const int r2 = launch_recorded(h, *h->grec);
+        h->grec = nullptr;
+        return r2;
+    };
     if (targeted) {
+        if ((rc = leave_group())) return rc;
         const auto ti_t0 = std::chrono::steady_clock::now();
         if (nb < (1 << 20) && (rc = ensure_tindex(h))) return rc;
         host_stage_add(h, "tindex", ti_t0);
@@ -4746,6 +4915,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     auto st0 = hclk::now();
     if (np > 0 && T > 0 && sort_hint(h)) {
+        if ((rc = leave_group())) return rc;
         stage_begin(h, "sort", &ev);
         bool planned = false;
         if ((rc = launch_segsort_radix(h, &planned))) return rc;
@@ -4772,7 +4942,17 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             stage_begin(h, "rank", &ev);
             // a small grid when the last landed batch was ranked in k_select_open (every loop is
             // grid-strided: any grid is correct, the hint only sizes it)
-            k_rank<<<h->rank_grid ? h->rank_grid : rank_hint(h) ? 4 : 1280, RANK_TILE, 0, s>>>(rka);
+            // otherwise one workgroup per tile of the candidates a batch can list at most (the
+            // demand plus the export depth per type): 1,280 workgroups cost ~20 us on small lists
+            const long long tiles = ((long long)R * std::min(T, NREQ) + (long long)T * h->export_extra + RANK_TILE - 1) /
+                                    RANK_TILE;
+            const int rgrid = h->rank_grid ? h->rank_grid : rank_hint(h) ? 4 : (int)std::min(1280ll, std::max(8ll, tiles));
+            if (h->grec) {
+                h->grec->kinds |= GK_RANK;
+                h->grec->rank = GRank{rka, rgrid};
+            } else {
+                k_rank<<<rgrid, RANK_TILE, 0, s>>>(rka);
+            }
             stage_end(h, "rank", ev);
         }
     }
@@ -4842,8 +5022,14 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             ca.rank_fuse = 1;
             ca.rank_bar = h->d_rank_sync + ADLBQ_MAX_TYPES + 2;
             ca.rk = rka;
-            if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
-            else k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
+        }
+        if (h->grec) {  // T <= 8, no round launches, no fused finalize (group_eligible)
+            h->grec->kinds |= GK_CHAIN;
+            h->grec->chain = GChain{ca, cp, mode_of(1), K == 0 ? 1 : 0, 0, nseg, fa};
+            h->grec->lds_chain = lds;
+        } else if (rank_fused) {
+            if (T <= 4) k_chain0<4, true><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
+            else k_chain0<8, true><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
         } else if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
         else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
@@ -4858,7 +5044,12 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     stage_end(h, "chain", ev);
     hsec("l_chain", hl);
     stage_begin(h, "finalize", &ev);
-    if (!fused) k_finalize<<<(R + 255) / 256, 256, 0, s>>>(fa);
+    if (h->grec) {
+        h->grec->kinds |= GK_FIN;
+        h->grec->fin = GFin{fa, (R + 255) / 256};
+    } else if (!fused) {
+        k_finalize<<<(R + 255) / 256, 256, 0, s>>>(fa);
+    }
     stage_end(h, "finalize", ev);
     hsec("l_fin", hl);
     // the lists hold export_extra more per type: a steal export right after this batch gathers them
@@ -4888,15 +5079,16 @@ __device__ __forceinline__ int bytes_eq(unsigned int x, unsigned int t) {
 
 // Grid (T, ceil(k / 256)): block (t, y) counts h_t itself (16 choice bytes per
 // load, four loads in flight) and gathers records [256 y, 256 y + 256) of type t.
-__global__ __launch_bounds__(256) void k_export_after(int T, int k, int R, const unsigned char *__restrict__ cht,
-                                                      const int *__restrict__ candoff, const int *__restrict__ candlen,
-                                                      const int *__restrict__ cslot, const int *__restrict__ prio,
-                                                      const int *__restrict__ seqa, const int4 *__restrict__ cold0,
-                                                      const int4 *__restrict__ cold1, int *__restrict__ recs,
-                                                      int *__restrict__ nrec, long long *__restrict__ navail,
-                                                      const unsigned int *__restrict__ coltot) {
+__device__ __forceinline__ void export_after_body(int T, int k, int R, const unsigned char *__restrict__ cht,
+                                                  const int *__restrict__ candoff, const int *__restrict__ candlen,
+                                                  const int *__restrict__ cslot, const int *__restrict__ prio,
+                                                  const int *__restrict__ seqa, const int4 *__restrict__ cold0,
+                                                  const int4 *__restrict__ cold1, int *__restrict__ recs,
+                                                  int *__restrict__ nrec, long long *__restrict__ navail,
+                                                  const unsigned int *__restrict__ coltot, const int t, const int y,
+                                                  const int ny) {
     __shared__ int s_h[4];
-    const int t = blockIdx.x, y = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned int ut = (unsigned int)t;
     const uint4 *cv = reinterpret_cast<const uint4 *>(cht);
     const int nv = R >> 4;
@@ -4924,7 +5116,7 @@ __global__ __launch_bounds__(256) void k_export_after(int T, int k, int R, const
         if (threadIdx.x == 0) navail[t] = (long long)a - ht;
     }
     const int n = max(0, min(k, candlen[t] - ht)), off = candoff[t] + ht;
-    for (int i = y * blockDim.x + threadIdx.x; i < n; i += gridDim.y * blockDim.x) {
+    for (int i = y * blockDim.x + threadIdx.x; i < n; i += ny * blockDim.x) {
         const int slot = cslot[off + i];
         const int4 c0 = cold0[slot], c1 = cold1[slot];
         int4 *r = reinterpret_cast<int4 *>(recs + ((long long)t * k + i) * 8);
@@ -4932,6 +5124,38 @@ __global__ __launch_bounds__(256) void k_export_after(int T, int k, int R, const
         r[1] = make_int4(c0.x, c0.w, c1.x, c1.y);
     }
     if (y == 0 && threadIdx.x == 0) nrec[t] = n;
+}
+
+__global__ __launch_bounds__(256) void k_export_after(int T, int k, int R, const unsigned char *__restrict__ cht,
+                                                      const int *__restrict__ candoff, const int *__restrict__ candlen,
+                                                      const int *__restrict__ cslot, const int *__restrict__ prio,
+                                                      const int *__restrict__ seqa, const int4 *__restrict__ cold0,
+                                                      const int4 *__restrict__ cold1, int *__restrict__ recs,
+                                                      int *__restrict__ nrec, long long *__restrict__ navail,
+                                                      const unsigned int *__restrict__ coltot) {
+    export_after_body(T, k, R, cht, candoff, candlen, cslot, prio, seqa, cold0, cold1, recs, nrec, navail, coltot,
+                      blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+// adlbq_steal_group_export: the shards' k_export_after as one launch, grid (T, y, shard)
+__global__ __launch_bounds__(256) void k_export_after_g(const ExportAfterGroup g) {
+    const ExportAfterArgs &a = g.a[blockIdx.z];
+    if ((int)blockIdx.x >= a.T) return;
+    export_after_body(a.T, a.k, a.R, a.cht, a.candoff, a.candlen, a.cslot, a.prio, a.seqa, a.cold0, a.cold1, a.recs,
+                      a.nrec, a.navail, a.coltot, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+bool export_after_args(adlbq_server *h, int k, int *d_recs, int *d_nrec, long long *d_navail, ExportAfterArgs *a) {
+    if (h->batch_export_k < k || h->T < 1) return false;
+    *a = ExportAfterArgs{h->T, k, h->batch_export_R, h->d_cht, h->d_candoff, h->d_candlen, h->d_cslot, h->d_prio,
+                         h->d_seq, h->d_cold0, h->d_cold1, d_recs, d_nrec, d_navail, h->d_coltot};
+    return true;
+}
+
+int launch_export_after_group(const ExportAfterGroup &g, int n, int k, int Tmax, hipStream_t s) {
+    k_export_after_g<<<dim3(Tmax, std::min(8, std::max(1, (k + 255) / 256)), n), 256, 0, s>>>(g);
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
 }
 
 // true (and the gather enqueued) when the last reserve batch's lists serve an export of depth k
@@ -4961,6 +5185,120 @@ int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
     return ADLBQ_OK;
 }
 
+
+// ---------------------------------------------------------------- group launch
+// A batch that can be recorded whole: T <= 8 (the 4/8-wide kernels), a
+// non-empty open bucket, no round launches after k_chain0, no diagnostics.
+static bool group_eligible(const adlbq_server *h) {
+    const int K = h->chain_rounds >= 0 ? h->chain_rounds : 0;
+    return h->T > 0 && h->T <= 8 && !h->open.pages.empty() && K == 0 && !h->hist_diag && !h->split_prep &&
+           !h->select_chunk && !h->chain_stamps;
+}
+
+static size_t gt_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// The recorded batches of handles m (same TB) as one launch per kernel on the
+// first handle's stream, which first waits for every member's stream; every
+// member's stream then waits for the last launch.
+static int run_group(adlbq_server *const *hs, std::vector<GroupRec> &rec, const std::vector<int> &m) {
+    adlbq_server *L = hs[m[0]];
+    hipStream_t ls = L->stream;
+    const int k = (int)m.size();
+    int rc;
+    if ((rc = group_join(hs, m))) return rc;
+    const size_t o_thr = gt_align(sizeof(GPrep) * k), o_sel = o_thr + gt_align(sizeof(GThr) * k),
+                 o_rank = o_sel + gt_align(sizeof(GSel) * k), o_chain = o_rank + gt_align(sizeof(GRank) * k),
+                 o_fin = o_chain + gt_align(sizeof(GChain) * k), total = o_fin + gt_align(sizeof(GFin) * k);
+    if (total > L->cap_gtab) {
+        AQ_HIP(hipStreamSynchronize(ls));
+        for (int sl = 0; sl < 2; sl++)
+            if (L->h_gtab[sl]) AQ_HIP(hipHostFree(L->h_gtab[sl]));
+        if (L->d_gtab) AQ_HIP(hipFree(L->d_gtab));
+        L->cap_gtab = std::max<size_t>(total, 1 << 16);
+        for (int sl = 0; sl < 2; sl++)
+            AQ_HIP(hipHostMalloc((void **)&L->h_gtab[sl], L->cap_gtab, hipHostMallocDefault));
+        AQ_HIP(hipMalloc((void **)&L->d_gtab, L->cap_gtab));
+    }
+    // pinned staging in turn: a buffer is refilled once the copy of two groups ago has run
+    const int sl = L->gtab_slot;
+    L->gtab_slot ^= 1;
+    if (L->gtab_ev[sl]) AQ_HIP(hipEventSynchronize(L->gtab_ev[sl]));
+    else AQ_HIP(hipEventCreateWithFlags(&L->gtab_ev[sl], hipEventDisableTiming));
+    char *hb = L->h_gtab[sl];
+    auto *tp = reinterpret_cast<GPrep *>(hb);
+    auto *tt = reinterpret_cast<GThr *>(hb + o_thr);
+    auto *ts = reinterpret_cast<GSel *>(hb + o_sel);
+    auto *tr = reinterpret_cast<GRank *>(hb + o_rank);
+    auto *tc = reinterpret_cast<GChain *>(hb + o_chain);
+    auto *tf = reinterpret_cast<GFin *>(hb + o_fin);
+    int gp = 0, gt = 0, gs = 0, gr = 0, gc = 0, gf = 0;
+    bool rf = false;  // some member ranks inside k_chain0 (the instance with k_rank's body)
+    size_t lp = 0, lsel = 0, lc = 0;
+    for (int j = 0; j < k; j++) {
+        const GroupRec &r = rec[(size_t)m[(size_t)j]];
+        tp[j] = r.prep;
+        tt[j] = r.thr;
+        ts[j] = r.sel;
+        tr[j] = r.rank;
+        tc[j] = r.chain;
+        tf[j] = r.fin;
+        if (!(r.kinds & GK_PREP)) tp[j].grid = 0;
+        if (!(r.kinds & GK_THR)) tt[j].grid = 0;
+        if (!(r.kinds & GK_SEL)) ts[j].grid = 0;
+        if (!(r.kinds & GK_RANK)) tr[j].grid = 0;
+        if (!(r.kinds & GK_CHAIN)) tc[j].grid = 0;
+        if (!(r.kinds & GK_FIN)) tf[j].grid = 0;
+        gp = std::max(gp, tp[j].grid);
+        gt = std::max(gt, tt[j].grid);
+        gs = std::max(gs, ts[j].grid);
+        gr = std::max(gr, tr[j].grid);
+        gc = std::max(gc, tc[j].grid);
+        gf = std::max(gf, tf[j].grid);
+        lp = std::max(lp, r.lds_prep);
+        lsel = std::max(lsel, r.lds_sel);
+        lc = std::max(lc, r.lds_chain);
+        rf = rf || ((r.kinds & GK_CHAIN) && r.chain.a.rank_fuse);
+    }
+    char *d = L->d_gtab;
+    AQ_HIP(hipMemcpyAsync(d, hb, total, hipMemcpyHostToDevice, ls));
+    AQ_HIP(hipEventRecord(L->gtab_ev[sl], ls));
+    const bool t4 = rec[(size_t)m[0]].tb == 4;
+    if (gp) (t4 ? k_prep_hist_g<4> : k_prep_hist_g<8>)<<<dim3(gp, k), 256, lp, ls>>>(reinterpret_cast<const GPrep *>(d));
+    if (gt) k_thresholds_g<<<dim3(gt, k), TH_THREADS, 0, ls>>>(reinterpret_cast<const GThr *>(d + o_thr));
+    if (gs) (t4 ? k_select_open_g<4> : k_select_open_g<8>)<<<dim3(gs, k), 256, lsel, ls>>>(reinterpret_cast<const GSel *>(d + o_sel));
+    if (gr) k_rank_g<<<dim3(gr, k), RANK_TILE, 0, ls>>>(reinterpret_cast<const GRank *>(d + o_rank));
+    if (gc) (rf ? (t4 ? k_chain0_g<4, true> : k_chain0_g<8, true>) : (t4 ? k_chain0_g<4, false> : k_chain0_g<8, false>))
+                <<<dim3(gc, k), 64, lc, ls>>>(reinterpret_cast<const GChain *>(d + o_chain));
+    if (gf) k_finalize_g<<<dim3(gf, k), 256, 0, ls>>>(reinterpret_cast<const GFin *>(d + o_fin));
+    AQ_HIP(hipGetLastError());
+    for (int j : m) rec[(size_t)j].kinds = 0;
+    return group_release(hs, m);
+}
+
+// adlbq_reserve_group_device: every handle's batch recorded (or launched on its
+// own stream when it cannot be), then the recorded ones grouped by TB.
+int launch_group(adlbq_server *const *hs, int n, const int *const *d_reqs, int *const *d_resp, const int *counts) {
+    std::vector<GroupRec> rec((size_t)n);
+    std::vector<int> m4, m8;
+    int rc;
+    for (int i = 0; i < n; i++) {
+        adlbq_server *h = hs[i];
+        if (counts[i] <= 0) continue;
+        const bool g = h->group_launch && group_eligible(h);
+        h->grec = g ? &rec[(size_t)i] : nullptr;
+        rc = launch_reserve(h, counts[i], d_reqs[i], d_resp[i]);
+        h->grec = nullptr;
+        if (rc) return rc;
+        if (rec[(size_t)i].kinds) (rec[(size_t)i].tb == 4 ? m4 : m8).push_back(i);
+    }
+    for (auto *mm : {&m4, &m8}) {
+        if (mm->size() == 1) rc = launch_recorded(hs[(*mm)[0]], rec[(size_t)(*mm)[0]]);
+        else if (mm->size() > 1) rc = run_group(hs, rec, *mm);
+        else rc = ADLBQ_OK;
+        if (rc) return rc;
+    }
+    return ADLBQ_OK;
+}
 }  // namespace adlbq
 
 extern "C" {
@@ -5007,6 +5345,25 @@ int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int 
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
     return launch_reserve(h, n, d_reqs18, d_resp12);
+}
+
+
+// One launch per pipeline kernel for the batches of n handles of one process
+// (its server shards), each handle's stream ordered as if it had run its own.
+int adlbq_reserve_group_device(adlbq_server *const *hs, int n, const int *const *d_reqs18, int *const *d_resp12,
+                               const int *counts) {
+    if (n < 0 || (n && (!hs || !d_reqs18 || !d_resp12 || !counts)))
+        return fail(ADLBQ_ERR_ARG, "adlbq_reserve_group_device");
+    for (int i = 0; i < n; i++) {
+        if (!hs[i] || counts[i] < 0 || (counts[i] && (!d_reqs18[i] || !d_resp12[i])) ||
+            hs[i]->device != hs[0]->device)
+            return fail(ADLBQ_ERR_ARG, "adlbq_reserve_group_device: bad handle, count or pointer, or mixed devices");
+        for (int j = 0; j < i; j++)
+            if (hs[j] == hs[i]) return fail(ADLBQ_ERR_ARG, "adlbq_reserve_group_device: a handle appears twice");
+    }
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(hs[0]->device);
+    return launch_group(hs, n, d_reqs18, d_resp12, counts);
 }
 
 

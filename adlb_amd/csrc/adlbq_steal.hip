@@ -237,10 +237,10 @@ struct RfrReset {  // k_rfr_reset's work, done by k_rq_compact when it runs anyw
     int *rfr_to_rank, A, *rfr_out, nworld, *hdr, idx;
 };
 
-__global__ __launch_bounds__(1024) void k_rq_compact(const int *__restrict__ rq_live, const int *__restrict__ rq_rank,
-                                                     const int *__restrict__ rq_types,
-                                                     const int *__restrict__ rq_seq, const DevCounters *ctr,
-                                                     int cap, int *__restrict__ out, RfrReset rr) {
+__device__ __forceinline__ void rq_compact_body(const int *__restrict__ rq_live, const int *__restrict__ rq_rank,
+                                                const int *__restrict__ rq_types, const int *__restrict__ rq_seq,
+                                                const DevCounters *ctr, int cap, int *__restrict__ out,
+                                                const RfrReset &rr) {
     __shared__ int wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (rr.rfr_to_rank) {
@@ -282,6 +282,29 @@ __global__ __launch_bounds__(1024) void k_rq_compact(const int *__restrict__ rq_
         __syncthreads();
     }
     if (tid == 0) out[0] = base;
+}
+
+__global__ __launch_bounds__(1024) void k_rq_compact(const int *__restrict__ rq_live, const int *__restrict__ rq_rank,
+                                                     const int *__restrict__ rq_types,
+                                                     const int *__restrict__ rq_seq, const DevCounters *ctr,
+                                                     int cap, int *__restrict__ out, RfrReset rr) {
+    rq_compact_body(rq_live, rq_rank, rq_types, rq_seq, ctr, cap, out, rr);
+}
+
+// adlbq_steal_group_export: the shards' k_rq_compact as one launch, one workgroup per shard
+struct RqCompactArgs {
+    const int *rq_live, *rq_rank, *rq_types, *rq_seq;
+    const DevCounters *ctr;
+    int cap;
+    int *out;
+    RfrReset rr;
+};
+struct RqCompactGroup {
+    RqCompactArgs a[EXPORT_GROUP];
+};
+__global__ __launch_bounds__(1024) void k_rq_compact_g(const RqCompactGroup g) {
+    const RqCompactArgs &a = g.a[blockIdx.x];
+    rq_compact_body(a.rq_live, a.rq_rank, a.rq_types, a.rq_seq, a.ctr, a.cap, a.out, a.rr);
 }
 
 // ---------------------------------------------------------------- merge (host)
@@ -660,6 +683,7 @@ int adlbq_rq_delete_batch(adlbq_server *h, int n, const int *rqseqnos, int *foun
 struct adlbq_steal_group {
     std::vector<adlbq_server *> sh;
     int n = 0, k = 0, T = 0, rqcap = 0;
+    int group_launch = 1;       // the export's kernels as one launch for the shards (adlbq_steal_group_set_param)
     long long off_recs = 0, off_nrec = 0, off_nav = 0, off_rq = 0, blob = 0;
     int *d_own = nullptr;       // the local blob when the caller passes none
     int *d_last = nullptr;      // where the last export went
@@ -691,6 +715,7 @@ int adlbq_steal_group_create(adlbq_steal_group **out, adlbq_server **shards, int
     g->sh.assign(shards, shards + n);
     for (int j = 0; j < n; j++) shards[j]->export_extra = std::max(shards[j]->export_extra, k);
     g->n = n, g->k = k, g->T = shards[0]->T, g->rqcap = rqcap;
+    if (const char *e = std::getenv("ADLBQ_STEAL_GROUP_LAUNCH")) g->group_launch = std::atoi(e) != 0;  // A/B runs
     const long long T = g->T;
     g->off_recs = 2;                                  // [0] shard index, [1] pad
     g->off_nrec = g->off_recs + T * k * 8;            // launch_export writes nrec right after the records
@@ -718,14 +743,44 @@ int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
         d_blob = g->d_own;
     }
     g->d_last = d_blob;
+    // shards whose last batch's lists serve the export and that have an rq: both kernels as one
+    // launch each for all of them (grid.z / grid.x = shard), EXPORT_GROUP at a time
+    std::vector<int> m;
+    ExportAfterGroup eg{};
+    RqCompactGroup rg{};
+    int Tmax = 0, rc;
+    auto flush = [&]() -> int {
+        if (m.empty()) return ADLBQ_OK;
+        int r2;
+        if ((r2 = group_join(g->sh.data(), m))) return r2;
+        hipStream_t ls = g->sh[(size_t)m[0]]->stream;
+        if ((r2 = launch_export_after_group(eg, (int)m.size(), g->k, Tmax, ls))) return r2;
+        k_rq_compact_g<<<(unsigned)m.size(), 1024, 0, ls>>>(rg);
+        AQ_HIP(hipGetLastError());
+        if ((r2 = group_release(g->sh.data(), m))) return r2;
+        for (int j : m)
+            if (g->sh[(size_t)j]->stream != g->sh[0]->stream) AQ_HIP(hipEventRecord(g->ev[(size_t)j], g->sh[(size_t)j]->stream));
+        m.clear();
+        Tmax = 0;
+        return ADLBQ_OK;
+    };
     for (int j = 0; j < g->n; j++) {
         adlbq_server *h = g->sh[(size_t)j];
         int *r = d_blob + (size_t)j * g->blob;
         // every SS_RFR of this shard's parks is answered by the round (adlb.c:1877-1878):
         // the reset rides in k_rq_compact (the export reads neither table)
         const RfrReset rr{h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world, r, h->my_idx};
-        int rc;
         long long *nav = reinterpret_cast<long long *>(r + g->off_nav);
+        const size_t q = m.size();
+        if (g->group_launch && g->T && h->rq_cap > 0 && g->rqcap > 0 &&
+            export_after_args(h, g->k, r + g->off_recs, r + g->off_nrec, nav, &eg.a[q])) {
+            rg.a[q] = RqCompactArgs{h->d_rq_live, h->d_rq_rank, h->d_rq_types, h->d_rq_seq, h->d_ctr, g->rqcap,
+                                    r + g->off_rq, rr};
+            Tmax = std::max(Tmax, h->T);
+            m.push_back(j);
+            if (m.size() == (size_t)EXPORT_GROUP && (rc = flush())) return rc;
+            continue;
+        }
         if (g->T && !launch_export_after(h, g->k, r + g->off_recs, r + g->off_nrec, nav) &&
             (rc = launch_export(h, g->k, r + g->off_recs, nav)))
             return rc;
@@ -738,9 +793,9 @@ int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
             AQ_HIP(hipMemsetAsync(r + g->off_rq, 0, sizeof(int), h->stream));
         }
         AQ_HIP(hipGetLastError());
-        AQ_HIP(hipEventRecord(g->ev[(size_t)j], h->stream));
+        if (h->stream != g->sh[0]->stream) AQ_HIP(hipEventRecord(g->ev[(size_t)j], h->stream));
     }
-    return ADLBQ_OK;
+    return flush();
 }
 
 }  // extern "C"
@@ -771,7 +826,8 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
     if ((rc = group_host_cap(g, total))) return rc;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    for (int j = 0; j < g->n; j++) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
+    for (int j = 0; j < g->n; j++)  // shards on the first shard's stream are ordered already (no event)
+        if (g->sh[(size_t)j]->stream != h0->stream) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
     AQ_HIP(hipMemcpyAsync(g->h_all, d_all, sizeof(int) * total, hipMemcpyDeviceToHost, h0->stream));
     AQ_HIP(hipStreamSynchronize(h0->stream));
     return group_settle_staged(g, nproc, n_decided, n_settled, t0, clk::now());
@@ -782,7 +838,8 @@ int adlbq_steal_group_export_host(adlbq_steal_group *g, int *h_blob) {
     int rc;
     if ((rc = adlbq_steal_group_export(g, nullptr))) return rc;
     adlbq_server *h0 = g->sh[0];
-    for (int j = 0; j < g->n; j++) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
+    for (int j = 0; j < g->n; j++)  // shards on the first shard's stream are ordered already (no event)
+        if (g->sh[(size_t)j]->stream != h0->stream) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
     AQ_HIP(hipMemcpyAsync(h_blob, g->d_last, sizeof(int) * g->blob * g->n, hipMemcpyDeviceToHost, h0->stream));
     AQ_HIP(hipStreamSynchronize(h0->stream));
     return ADLBQ_OK;
@@ -934,7 +991,8 @@ static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, 
         AQ_HIP(hipGetLastError());
         AQ_HIP(hipEventRecord(g->app_done_ev, h0->stream));
         for (int j = 0; j < g->n; j++)
-            if (g->sh[(size_t)j] != h0) AQ_HIP(hipStreamWaitEvent(g->sh[(size_t)j]->stream, g->app_done_ev, 0));
+            if (g->sh[(size_t)j]->stream != h0->stream)
+                AQ_HIP(hipStreamWaitEvent(g->sh[(size_t)j]->stream, g->app_done_ev, 0));
     }
     const auto t3 = clk::now();
     g->ns_copy = std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
@@ -993,7 +1051,7 @@ int adlbq_steal_group_unreserve_grants(adlbq_steal_group *g) {
     AQ_HIP(hipGetLastError());
     AQ_HIP(hipEventRecord(g->unr_ev, h0->stream));
     for (int j = 0; j < g->n; j++)
-        if (g->sh[(size_t)j] != h0) AQ_HIP(hipStreamWaitEvent(g->sh[(size_t)j]->stream, g->unr_ev, 0));
+        if (g->sh[(size_t)j]->stream != h0->stream) AQ_HIP(hipStreamWaitEvent(g->sh[(size_t)j]->stream, g->unr_ev, 0));
     return ADLBQ_OK;
 }
 

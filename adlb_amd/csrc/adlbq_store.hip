@@ -928,11 +928,12 @@ __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ page
 // wqseqno; responses of another batch fall back to the wqseqno -> slot map.
 // The anchor is raised by a fire-and-forget atomic max per type of the wave
 // (a stale read could only add a harmless one: no load of it first).
-__global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
-                                 const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta, int *pin,
-                                 const int4 *__restrict__ rrec, long long *anchor, const int *__restrict__ mslot,
-                                 int ntypes) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void unreserve_resp_body(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
+                                                    const long long *__restrict__ seq2slot, long long nseq,
+                                                    uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
+                                                    long long *anchor, const int *__restrict__ mslot, int ntypes,
+                                                    int bid) {
+    int i = bid * blockDim.x + threadIdx.x;
     int t = -1, up = INT_MIN;
     // lane u holds anchor[u] (T <= 64), loaded with the responses: only a unit above it needs an
     // atomic max (one per type of the wave; every wave adding to one word would serialise them)
@@ -983,6 +984,69 @@ __global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__rest
         b &= ~__ballot(t == lt);
     }
 }
+
+__global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
+                                 const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta, int *pin,
+                                 const int4 *__restrict__ rrec, long long *anchor, const int *__restrict__ mslot,
+                                 int ntypes) {
+    unreserve_resp_body(reqs, resp, n, seq2slot, nseq, meta, pin, rrec, anchor, mslot, ntypes, blockIdx.x);
+}
+
+// adlbq_unreserve_resp_group_device: up to UNRES_GROUP shards per launch, blockIdx.y = shard, the
+// arguments in the kernel's own argument block (no table upload)
+constexpr int UNRES_GROUP = 16;
+struct UnresArgs {
+    const int *reqs, *resp;
+    int n;
+    const long long *seq2slot;
+    long long nseq;
+    uint32_t *meta;
+    int *pin;
+    const int4 *rrec;
+    long long *anchor;
+    const int *mslot;
+    int ntypes;
+};
+struct UnresGroup {
+    UnresArgs a[UNRES_GROUP];
+};
+__global__ __launch_bounds__(256) void k_unreserve_resp_g(const UnresGroup g) {
+    const UnresArgs &a = g.a[blockIdx.y];
+    if ((int)blockIdx.x * 256 >= a.n) return;  // whole workgroups return together
+    unreserve_resp_body(a.reqs, a.resp, a.n, a.seq2slot, a.nseq, a.meta, a.pin, a.rrec, a.anchor, a.mslot, a.ntypes,
+                        blockIdx.x);
+}
+
+// Several handles' work as one launch on the first handle's stream (hs[m[0]]):
+// that stream first waits for what every member's stream already holds, and
+// every member's stream then waits for the launch (events kept by the first).
+namespace adlbq {
+int group_join(adlbq_server *const *hs, const std::vector<int> &m) {
+    adlbq_server *L = hs[m[0]];
+    if (L->gjoin.size() < m.size()) {
+        const size_t old = L->gjoin.size();
+        L->gjoin.resize(m.size(), nullptr);
+        for (size_t j = old; j < m.size(); j++) AQ_HIP(hipEventCreateWithFlags(&L->gjoin[j], hipEventDisableTiming));
+    }
+    for (size_t j = 1; j < m.size(); j++) {
+        adlbq_server *h = hs[m[j]];
+        if (h->stream == L->stream) continue;
+        AQ_HIP(hipEventRecord(L->gjoin[j], h->stream));
+        AQ_HIP(hipStreamWaitEvent(L->stream, L->gjoin[j], 0));
+    }
+    return ADLBQ_OK;
+}
+
+int group_release(adlbq_server *const *hs, const std::vector<int> &m) {
+    adlbq_server *L = hs[m[0]];
+    AQ_HIP(hipEventRecord(L->gjoin[0], L->stream));
+    for (size_t j = 1; j < m.size(); j++) {
+        adlbq_server *h = hs[m[j]];
+        if (h->stream != L->stream) AQ_HIP(hipStreamWaitEvent(h->stream, L->gjoin[0], 0));
+    }
+    return ADLBQ_OK;
+}
+}  // namespace adlbq
 
 // update_local_state over the open bucket: count of live unpinned units and per
 // type max prio (strictly above ADLB_LOWEST_PRIO, else LOWEST)
@@ -1333,6 +1397,13 @@ int adlbq_destroy(adlbq_server *h) {
     for (int q = 0; q < 2; q++)
         if (h->put_ev[q]) hipEventDestroy(h->put_ev[q]);
     for (int q = 0; q < 2; q++) {
+        if (h->gtab_ev[q]) hipEventDestroy(h->gtab_ev[q]);
+        if (h->h_gtab[q]) hipHostFree(h->h_gtab[q]);
+    }
+    if (h->d_gtab) hipFree(h->d_gtab);
+    for (hipEvent_t e : h->gjoin)
+        if (e) hipEventDestroy(e);
+    for (int q = 0; q < 2; q++) {
         if (h->tnew_ev[q]) hipEventDestroy(h->tnew_ev[q]);
         if (h->h_tnewk[q]) hipHostFree(h->h_tnewk[q]);
         if (h->h_tnewv[q]) hipHostFree(h->h_tnewv[q]);
@@ -1649,6 +1720,44 @@ int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, con
                                                              (h->d_mslot && n <= h->cap_req) ? h->d_mslot : nullptr,
                                                              std::min(h->T, 64));
     AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
+int adlbq_unreserve_resp_group_device(adlbq_server *const *hs, int n, const int *const *d_reqs18,
+                                      const int *const *d_resp12, const int *counts) {
+    if (n < 0 || (n && (!hs || !d_reqs18 || !d_resp12 || !counts)))
+        return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_group_device");
+    std::vector<int> m;
+    for (int i = 0; i < n; i++) {
+        if (!ok_handle(hs[i]) || counts[i] < 0 || (counts[i] && (!d_reqs18[i] || !d_resp12[i])) ||
+            hs[i]->device != hs[0]->device)
+            return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_group_device: bad handle, count or pointer, or mixed devices");
+        for (int j = 0; j < i; j++)
+            if (hs[j] == hs[i]) return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_group_device: a handle appears twice");
+        wq_changed(hs[i]);
+        if (counts[i] > 0) m.push_back(i);
+    }
+    if (m.empty()) return ADLBQ_OK;
+    hipSetDevice(hs[0]->device);
+    int rc;
+    for (size_t c0 = 0; c0 < m.size(); c0 += UNRES_GROUP) {  // UNRES_GROUP shards per launch (kernel arguments)
+        const std::vector<int> mm(m.begin() + c0, m.begin() + std::min(m.size(), c0 + UNRES_GROUP));
+        UnresGroup g{};
+        int nb = 0;
+        for (size_t j = 0; j < mm.size(); j++) {
+            adlbq_server *h = hs[mm[j]];
+            const int c = counts[mm[j]];
+            g.a[j] = UnresArgs{d_reqs18[mm[j]], d_resp12[mm[j]], c, h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_pin,
+                               h->d_rrec, h->d_anchor, (h->d_mslot && c <= h->cap_req) ? h->d_mslot : nullptr,
+                               std::min(h->T, 64)};
+            nb = std::max(nb, (c + 255) / 256);
+        }
+        adlbq_server *L = hs[mm[0]];
+        if ((rc = group_join(hs, mm))) return rc;
+        k_unreserve_resp_g<<<dim3(nb, (unsigned)mm.size()), 256, 0, L->stream>>>(g);
+        AQ_HIP(hipGetLastError());
+        if ((rc = group_release(hs, mm))) return rc;
+    }
     return ADLBQ_OK;
 }
 
@@ -2187,6 +2296,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (n == "fold_thresholds") {
         if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0, 1 or 2 (auto)");
         h->fold_thresholds = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "group_launch") {
+        if (value < 0 || value > 1) return fail(ADLBQ_ERR_ARG, "group_launch must be 0 or 1");
+        h->group_launch = (int)value;
         return ADLBQ_OK;
     }
     if (n == "fuse_rank") {

@@ -324,3 +324,32 @@ class Server:
     def set_param(self, name: str, value: int) -> None:
         """Tuning knobs of the engine (adlbq_set_param); results never depend on them."""
         _lib.check(self.lib.adlbq_set_param(self.h, name.encode(), int(value)), "adlbq_set_param")
+
+
+class ReserveGroup:
+    """adlbq_reserve_group_device over a fixed set of one process's server
+    shards: every shard's Reserve batch as one launch per pipeline kernel
+    (include/adlbq.h).  pack() builds a call's argument arrays once, so a
+    loop over pre-staged batches does no per-call marshalling."""
+
+    def __init__(self, servers):
+        self.servers = list(servers)
+        self.n = len(self.servers)
+        self.lib = self.servers[0].lib
+        self._hs = (ctypes.c_void_p * self.n)(*[s.h for s in self.servers])
+
+    def pack(self, counts, d_reqs, d_resp):
+        n = self.n
+        if not (len(counts) == len(d_reqs) == len(d_resp) == n):
+            raise ValueError("one count, request pointer and reply pointer per shard")
+        return ((ctypes.c_void_p * n)(*d_reqs), (ctypes.c_void_p * n)(*d_resp), (ctypes.c_int * n)(*counts))
+
+    def reserve_device(self, counts=None, d_reqs=None, d_resp=None, packed=None) -> None:
+        rq, rs, ct = packed if packed is not None else self.pack(counts, d_reqs, d_resp)
+        _lib.check(self.lib.adlbq_reserve_group_device(self._hs, self.n, rq, rs, ct), "adlbq_reserve_group_device")
+
+    def unreserve_resp_device(self, counts=None, d_reqs=None, d_resp=None, packed=None) -> None:
+        """adlbq_unreserve_resp_group_device: SS_UNRESERVE of every unit the shards' batches matched."""
+        rq, rs, ct = packed if packed is not None else self.pack(counts, d_reqs, d_resp)
+        _lib.check(self.lib.adlbq_unreserve_resp_group_device(self._hs, self.n, rq, rs, ct),
+                   "adlbq_unreserve_resp_group_device")

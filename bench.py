@@ -75,6 +75,10 @@ def parse():
     ap.add_argument("--c3-steps", type=int, default=40)
     ap.add_argument("--c3-rqcap", type=int, default=2048, help="config 3: parked Reserves per shard a round considers (~820 park per step)")
     ap.add_argument("--c3-threads", type=int, default=0, help="config 3: enqueue the shards' batches from threads")
+    ap.add_argument("--c3-streams", type=int, default=1,
+                    help="config 3: HIP streams the GPU's shards share (round robin); 0 = one per shard")
+    ap.add_argument("--c3-group", type=int, default=1,
+                    help="config 3: every shard's Reserve batch as one launch per kernel (adlbq_reserve_group_device)")
     ap.add_argument("--c3-warmup", type=int, default=8, help="config 3: untimed steps (rq and export buffers grow)")
     ap.add_argument("--c3-parts", action="store_true", help="config 3: synchronise and time each part of every step")
     ap.add_argument("--config3-only", action="store_true", help="only the config-3 leg (profiling)")
@@ -310,7 +314,7 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     matched and stolen unit so each step sees the same queues.  Reports
     (local + stolen assignments) / s and the steal round's share."""
     from adlb_amd import shards, synth
-    from adlb_amd.server import Server
+    from adlb_amd.server import ReserveGroup, Server
 
     SL, N, R, k = args.c3_servers, args.c3_units, args.c3_reserves, args.c3_k
     S, T = SL * world, 4
@@ -324,7 +328,8 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         for kv in args.c3_param:
             k_, v_ = kv.split("=", 1)
             srv.set_param(k_, int(v_))
-        st = torch.cuda.Stream(dev)
+        nst = args.c3_streams if args.c3_streams > 0 else SL
+        st = streams[j % nst] if j >= nst else torch.cuda.Stream(dev)
         srv.set_stream(st.cuda_stream)
         srv.put_batch(np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1),
                                 np.zeros(N), np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32))
@@ -358,9 +363,15 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     def enqueue(j, b):
         srvs[j].reserve_batch_device(R, p_req[j][b], p_resp[j][b])
 
+    rgroup = ReserveGroup(srvs) if args.c3_group else None
+    packed = ([rgroup.pack([R] * len(srvs), [p_req[j][b] for j in range(len(srvs))],
+                           [p_resp[j][b] for j in range(len(srvs))]) for b in range(nb)] if rgroup else None)
+
     def step(b, timed_parts=False):
         t0 = time.perf_counter()
-        if pool is not None:
+        if rgroup is not None:
+            rgroup.reserve_device(packed=packed[b])
+        elif pool is not None:
             list(pool.map(lambda j: enqueue(j, b), range(len(srvs))))
         else:
             for j in range(len(srvs)):
@@ -372,8 +383,11 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
         tm = sparts if timed_parts else None
         nd, ns = group.round(timing=tm)
         t2 = time.perf_counter()
-        for j, srv in enumerate(srvs):
-            srv.unreserve_resp_device(R, p_req[j][b], p_resp[j][b])
+        if rgroup is not None:
+            rgroup.unreserve_resp_device(packed=packed[b])
+        else:
+            for j, srv in enumerate(srvs):
+                srv.unreserve_resp_device(R, p_req[j][b], p_resp[j][b])
         group.unreserve_grants()
         if timed_parts:
             for key in ("copy_ns", "merge_ns", "apply_ns"):
@@ -419,7 +433,8 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
     steps = nb - W3
     out = {
         "workload": f"config3: {S} server shards ({SL}/GPU) x {N} units, {T} types with one type missing per "
-                    f"shard, {R} Reserves/shard/step (~10% only the missing type), steal round k={k}, rqcap={args.c3_rqcap}",
+                    f"shard, {R} Reserves/shard/step (~10% only the missing type), steal round k={k}, rqcap={args.c3_rqcap}"
+                    + (", the shards' batches as one launch per kernel" if rgroup else ""),
         "value": (local_matched + settled) / el,
         "unit": "assignments/s",
         "ms_per_step": el * 1e3 / steps,

@@ -87,6 +87,18 @@ int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12);
  * (no host synchronisation).  Used when requests are staged in HBM. */
 int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int *d_resp12);
 
+/* adlbq_reserve_batch_device for the local server shards of one process
+ * (handles hs[0..n), distinct, one device; counts[i] Reserves for hs[i]), as
+ * ONE launch per pipeline kernel over all of them (grid.y = shard) on hs[0]'s
+ * stream, which first waits for every shard's stream; every shard's stream
+ * then waits for the last launch.  Results are those of n separate
+ * adlbq_reserve_batch_device calls.  A shard whose batch needs an extra launch
+ * in between (targeted units, a read-back sort) or with T > 8 runs alone on
+ * its stream.  The reference serves each server's Reserves in its own process
+ * (src/adlb.c:1181-1320); this entry is the multi-shard-per-GPU form of it. */
+int adlbq_reserve_group_device(adlbq_server *const *hs, int n, const int *const *d_reqs18, int *const *d_resp12,
+                               const int *counts);
+
 /* FA_GET_RESERVED (src/adlb.c:1347-1381): wq_find_pinned_for_rank(rank, wqseqno)
  * (xq.c:249-264) then wq_delete.  out5 = {rc (1 / -1 not found), work_len,
  * work_type, work_prio, answer_rank}. */
@@ -111,6 +123,12 @@ int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples);
  * out, taken straight from that batch's device-resident reqs18 / resp12 (rows
  * with rc 1): pin_rank = -1, pinned = 0.  Enqueued on the handle's stream. */
 int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12);
+
+/* adlbq_unreserve_resp_device for several handles of one process (distinct,
+ * one device; counts[i] responses of hs[i]) as one launch on hs[0]'s stream,
+ * ordered like adlbq_reserve_group_device. */
+int adlbq_unreserve_resp_group_device(adlbq_server *const *hs, int n, const int *const *d_reqs18,
+                                      const int *const *d_resp12, const int *counts);
 
 /* update_local_state (src/adlb.c:3581-3593): qlen = wq_get_num_unpinned_untargeted
  * (xq.c:298-311), type_hi_prio[t] = wq_get_avail_hi_prio_of_type(user_types[t])

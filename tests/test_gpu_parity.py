@@ -97,7 +97,7 @@ VARIANTS = {
     "no_seg_guess": {"seg_guess": 0},      # the chain finds its own start guesses
     "all": {"select_chunk": 1, "hist_ppb": 2},
     "fused": {"fuse_finalize": 1},         # k_finalize inside the final k_chain0 launch
-    "rank_launch": {"fuse_rank": 0},       # k_rank always as its own launch (default: skipped on the rank hint)
+    "rank_skip": {"fuse_rank": 1},         # k_rank skipped on the rank hint, the chain ranks when the hint fails
     "rank_in_chain": {"fuse_rank": 2},     # k_rank never launched: the chain sorts / ranks behind its grid barrier
     "thresholds_folded": {"fold_thresholds": 1},  # k_thresholds' work in pass 1's last workgroups (measured slower)
 }
