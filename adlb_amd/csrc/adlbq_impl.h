@@ -329,6 +329,16 @@ struct adlbq_server {
     int fold_thresholds = 0;           // "fold_thresholds": k_thresholds' work in pass 1's last workgroups
                                        // (measured slower: off)
     int *d_fold = nullptr;             // k_prep_hist's folded-thresholds arrival counters
+    // the Reserve path of more than ADLBQ_MAX_TYPES types (adlbq_wide.hip): sort buffers and runs
+    unsigned long long *d_wk0 = nullptr, *d_wk1 = nullptr, *d_wekey = nullptr;
+    int *d_wv0 = nullptr, *d_wv1 = nullptr, *d_wflag = nullptr, *d_wrstart = nullptr, *d_whead = nullptr;
+    unsigned int *d_wrkey = nullptr;
+    int *d_wreq = nullptr, *d_wcnt = nullptr;
+    int2 *d_wpages = nullptr;
+    void *d_wtmp = nullptr;
+    long long cap_wn = 0;
+    size_t cap_wtmp = 0;
+    int cap_wreq = 0, cap_wpages = 0;
     int group_launch = 1;              // "group_launch": 0 = adlbq_reserve_group_device launches this handle alone
     ::GroupRec *grec = nullptr;        // non-null: launch_reserve records its launches (adlbq_reserve_group_device)
     // the group launch's argument tables (kept by the group's first handle): pinned staging x 2, device copy
@@ -401,6 +411,7 @@ void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
 // host time since t0 added to stage `name` (profiling only; no events)
 void host_stage_add(adlbq_server *h, const char *name, std::chrono::steady_clock::time_point t0);
 int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
+int wide_choose(adlbq_server *h, int R, const int *d_reqs);  // T > ADLBQ_MAX_TYPES: the batch's choices
 int group_join(adlbq_server *const *hs, const std::vector<int> &m);     // hs[m[0]]'s stream waits for the members'
 int group_release(adlbq_server *const *hs, const std::vector<int> &m);  // the members' streams wait for hs[m[0]]'s
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail);

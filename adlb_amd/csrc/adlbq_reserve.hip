@@ -3033,7 +3033,7 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     // server can be a donor any more (each RFR sets rfr_out), the rest get -1
     // in parallel
     __shared__ int s_hi[ADLBQ_MAX_TYPES * 64], s_tq[4 * DONOR_TQ_LDS], s_tv[64 * NREQ];
-    if (w == 0 && donors && c.S <= 64 && c.n_tq <= DONOR_TQ_LDS) {
+    if (w == 0 && donors && c.S <= 64 && c.T <= ADLBQ_MAX_TYPES && c.n_tq <= DONOR_TQ_LDS) {
         const int k = park_donors_fast(c, reqs, rq_req, n0, np, resp, s_hi, s_tq, s_tv);
         if (lane == 0) s_stop = k;
     } else if (w == 0) {
@@ -4792,6 +4792,42 @@ static int launch_segsort(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
+// k_finalize's arguments for a batch (its own launch, or fused into the final k_chain0 launch)
+static FinArgs fin_args(adlbq_server *h, int R, const int *d_reqs, int *d_resp, DevCounters *snap) {
+    return FinArgs{d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_meta, h->d_pin, h->my_world, d_resp,
+                   h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
+                   h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, h->T, snap, h->snap_tag[h->snap_next],
+                   h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
+                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot, h->d_rh};
+}
+
+// the host side of a batch in flight: its snapshot slot, counts, upper bounds
+static void batch_launched(adlbq_server *h, int R, int export_k) {
+    h->batch_export_k = export_k;
+    h->batch_export_R = R;
+    h->launched_reserves += R;
+    h->snap_at[h->snap_next] = h->launched_reserves;
+    h->snap_next = (h->snap_next + 1) % adlbq_server::NSNAP;
+    h->hint_stamp++;  // a new snapshot slot is in flight: look again next time
+    h->ctr_stale = true;
+    h->rq_n_upper += R;
+    h->rq_next_upper += R;
+}
+
+// More than ADLBQ_MAX_TYPES types: the sorted-runs choice (adlbq_wide.hip), then k_finalize.
+static int launch_reserve_wide(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
+    int rc;
+    if ((rc = wide_choose(h, R, d_reqs))) return rc;
+    DevCounters *const snap = h->d_snap + h->snap_next;
+    h->snap_tag[h->snap_next] = ++h->snap_tags;
+    __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);
+    const FinArgs fa = fin_args(h, R, d_reqs, d_resp, snap);
+    k_finalize<<<(R + 255) / 256, 256, 0, h->stream>>>(fa);
+    AQ_HIP(hipGetLastError());
+    batch_launched(h, R, 0);
+    return ADLBQ_OK;
+}
+
 // The kernels a handle recorded (GroupRec), launched one by one on its own stream.
 static int launch_recorded(adlbq_server *h, GroupRec &r) {
     hipStream_t s = h->stream;
@@ -4844,6 +4880,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hsec("tables", ht);
     if ((rc = ensure_rq_capacity(h, R))) return rc;
     hsec("rq_cap", ht);
+    if (h->T > ADLBQ_MAX_TYPES) return launch_reserve_wide(h, R, d_reqs, d_resp);
     const int T = h->T;
     const int np = (int)h->open.pages.size();
     if ((rc = ensure_scan_capacity(h, std::max(np, 1)))) return rc;
@@ -4961,11 +4998,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     DevCounters *const snap = h->d_snap + h->snap_next;
     h->snap_tag[h->snap_next] = ++h->snap_tags;
     __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);  // not landed until k_finalize stores it
-    const FinArgs fa{d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_meta, h->d_pin, h->my_world, d_resp,
-                     h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
-                     h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, T, snap, h->snap_tag[h->snap_next],
-                     h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
-                     h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot, h->d_rh};
+    const FinArgs fa = fin_args(h, R, d_reqs, d_resp, snap);
     bool fused = false;
     stage_begin(h, "chain", &ev);
     {
@@ -5053,16 +5086,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     stage_end(h, "finalize", ev);
     hsec("l_fin", hl);
     // the lists hold export_extra more per type: a steal export right after this batch gathers them
-    h->batch_export_k = (np > 0 && T > 0) ? h->export_extra : 0;
-    h->batch_export_R = R;
-    h->launched_reserves += R;
-    h->snap_at[h->snap_next] = h->launched_reserves;
-    h->snap_next = (h->snap_next + 1) % adlbq_server::NSNAP;
-    h->hint_stamp++;  // a new snapshot slot is in flight: look again next time
     AQ_HIP(hipGetLastError());
-    h->ctr_stale = true;
-    h->rq_n_upper += R;
-    h->rq_next_upper += R;
+    batch_launched(h, R, (np > 0 && T > 0) ? h->export_extra : 0);
     auto t_all = host_t0;
     hsec("total", t_all);
     return ADLBQ_OK;
@@ -5169,6 +5194,7 @@ bool launch_export_after(adlbq_server *h, int k, int *d_recs, int *d_nrec, long 
 
 // recs8 [T][k][8] then nrec [T] land in d_out, navail [T] in d_navail (device)
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
+    if (h->T > ADLBQ_MAX_TYPES) return fail(ADLBQ_ERR_UNSUPPORTED, "steal export: more than 64 work types");
     wq_changed(h);  // the export scan rebuilds the candidate lists
     int rc;
     if ((rc = sync_tables(h))) return rc;

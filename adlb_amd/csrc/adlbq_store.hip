@@ -1052,7 +1052,7 @@ int group_release(adlbq_server *const *hs, const std::vector<int> &m) {
 // type max prio (strictly above ADLB_LOWEST_PRIO, else LOWEST)
 __global__ void k_qmrow(const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
                         const uint32_t *__restrict__ meta, int T, int *res /* [0]=qlen, [1+t]=max */) {
-    __shared__ int smax[ADLBQ_MAX_TYPES];
+    __shared__ int smax[ADLBQ_MAX_TYPES_WIDE];
     __shared__ int scnt;
     for (int t = threadIdx.x; t < T; t += blockDim.x) smax[t] = LOWEST;
     if (threadIdx.x == 0) scnt = 0;
@@ -1273,7 +1273,10 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     if (!out || ntypes < 0 || (ntypes && !user_types) || num_app_ranks < 0 || num_servers < 1 ||
         my_server_idx < 0 || my_server_idx >= num_servers)
         return fail(ADLBQ_ERR_ARG, "adlbq_create: bad argument");
-    if (ntypes > ADLBQ_MAX_TYPES) return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 64 work types");
+    if (ntypes > ADLBQ_MAX_TYPES_WIDE)
+        return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 255 work types (8-bit type index per slot)");
+    if (ntypes > ADLBQ_MAX_TYPES && num_app_ranks >= (1 << 24) - 2)
+        return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 64 types with 2^24 or more app ranks");
     auto *h = new adlbq_server();
     hipError_t e;
     if (device < 0) {  // one GPU per server shard, round robin over the visible devices
@@ -1350,8 +1353,8 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMemsetAsync(h->d_type_cnt, 0, sizeof(int) * T1, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_rank_sync, sizeof(int) * (ADLBQ_MAX_TYPES + 6)));
     AQ_HIP(hipMemsetAsync(h->d_rank_sync, 0, sizeof(int) * (ADLBQ_MAX_TYPES + 6), h->stream));
-    AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
-    AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES + 16)));
+    AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES_WIDE + 16)));
+    AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES_WIDE + 16)));
     long long pages = std::max<long long>(16, (max_units + PAGE - 1) / PAGE + 16);
     if ((rc = grow_pages(h, (int)std::min<long long>(pages, INT_MAX / PAGE)))) return cleanup(rc);
     if ((rc = ensure_rq_capacity(h, 1024))) return cleanup(rc);
@@ -1376,7 +1379,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
                     h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg,
-                    h->d_mslot, h->d_fold, h->d_rh};
+                    h->d_mslot, h->d_fold, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
+                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1568,8 +1572,9 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
     if (may_match) {
         // one workgroup over the staged rq; too many parked Reserves: the one-wave scan of the whole rq
         if (!h->d_pm_over) AQ_HIP(hipMalloc((void **)&h->d_pm_over, sizeof(int)));
-        AQ_HIP(hipMemsetAsync(h->d_pm_over, h->put_match_block ? 0 : 1, sizeof(int), h->stream));
-        if (h->put_match_block)
+        const bool blk = h->put_match_block && h->T <= ADLBQ_MAX_TYPES;  // its type sets are 64-bit masks
+        AQ_HIP(hipMemsetAsync(h->d_pm_over, blk ? 0 : 1, sizeof(int), h->stream));
+        if (blk)
             k_put_match_blk<<<1, PM_THREADS, 0, h->stream>>>(d_rec, n, h->d_rq_rank, h->d_rq_types, h->d_rq_live,
                                                          h->d_rq_seq, h->d_ctr, h->d_meta, h->d_pin,
                                                          d_out3 ? d_out3 : h->d_putout, h->d_utypes, h->T,

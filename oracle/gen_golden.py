@@ -199,6 +199,35 @@ def bytes_stream(seed=61, n_events=600, kind="ref", hwm=False):
     return np.asarray(ev, np.int32)
 
 
+def wide_cases():
+    """More than 64 work types (get_type_idx, adlb.c:3476-3485; the device's slower
+    sorted-runs path): 100 and 200 types, with exhaustion, parking, Puts that
+    match parked Reserves, wildcards, targeted units and Gets / unreserves."""
+    out = {}
+    w = synth.config2(n_units=3_000, n_types=100, n_reserves=4096, seed=71, prio_hi=64)
+    extra = synth.put_events(synth.config2(n_units=2_000, n_types=100, n_reserves=0, seed=72, prio_hi=64))
+    out["w100_c2_park_puts"] = (w.user_types, w.num_app_ranks, 1, 0,
+                                np.concatenate([synth.workload_trace(w), extra]))
+    w = synth.config4(n_units=20_000, n_types=100, n_reserves=2048, n_ranks=64, seed=73, prio_hi=256)
+    out["w100_c4"] = (w.user_types, w.num_app_ranks, 1, 0, synth.workload_trace(w))
+    # 200 types: one Reserve batch, then Gets and unreserves of some matches, then another batch
+    w = synth.config2(n_units=20_000, n_types=200, n_reserves=2048, seed=74, prio_hi=16)
+    o = oracle.Oracle("ref")
+    o.init(w.user_types, w.num_app_ranks, 2, 1)
+    first = synth.workload_trace(w)
+    outs = synth.split_outputs(o.replay(first))[w.n_units:]
+    back = []
+    for i, (r, x) in enumerate(zip(w.r_rank, outs)):
+        if x[0] == 1 and i % 3 == 0:
+            back.append([U, int(r), int(x[5]), -1])
+        elif x[0] == 1 and i % 3 == 1:
+            back.append([G, int(r), int(x[5])])
+    second = synth.reserve_events(w.r_rank[:1024], w.r_types[:1024], w.r_hang[:1024])
+    tr = np.concatenate([first.ravel()] + [np.asarray(e, np.int32) for e in back] + [second.ravel()])
+    out["w200_get_unreserve"] = (w.user_types, w.num_app_ranks, 2, 1, tr)
+    return out
+
+
 def save(name, user_types, num_app_ranks, num_servers, my_idx, trace):
     o = oracle.Oracle("ref")
     o.init(user_types, num_app_ranks, num_servers, my_idx)
@@ -224,6 +253,9 @@ def main():
         for name, tr in edge_cases().items():
             if name in only:
                 save(name, [0, 1, 2, 3], 8, 1, 0, tr)
+        for name, (ut, a, ns, mi, tr) in wide_cases().items():
+            if name in only:
+                save(name, ut, a, ns, mi, tr)
         return
     save("t14_bytes", [0, 1, 2], 6, 4, 0, bytes_case())
     save("t15_bytes_stream", [0, 1, 2], 16, 3, 1, bytes_stream())
@@ -251,6 +283,8 @@ def main():
     tr = synth.config5_stream(lambda ev: synth.split_outputs(o.replay(ev)), n_rounds=300,
                               n_ranks=64, n_servers=4, seed=51)
     save("c5_stream", [1, 2], 64, 4, 0, tr)
+    for name, (ut, a, ns, mi, tr) in wide_cases().items():
+        save(name, ut, a, ns, mi, tr)
 
 
 if __name__ == "__main__":

@@ -78,6 +78,11 @@ CASES = {
     "c2_t4_wide_prio": lambda: synth.config2(n_units=100_000, n_reserves=16_384, seed=230, prio_hi=1 << 20),
     "c2_t8_wide_prio": lambda: synth.config2(n_units=100_000, n_types=8, n_reserves=8192, seed=231,
                                              prio_hi=1 << 16),
+    # more than 64 types: the sorted-runs Reserve path (adlbq_wide.hip), untargeted and targeted
+    "w100_c2": lambda: synth.config2(n_units=50_000, n_types=100, n_reserves=8192, seed=240, prio_hi=128),
+    "w150_c4": lambda: synth.config4(n_units=50_000, n_types=150, n_reserves=4096, n_ranks=128, seed=241,
+                                     prio_hi=512),
+    "w255_exhaust": lambda: synth.config2(n_units=4_000, n_types=255, n_reserves=6000, seed=242, prio_hi=8),
     # a type with no unit at all (config 3's shards): the guess counts are adjusted first
     "c3_shard_missing_type": lambda: synth.config3_shard(1, 64, 80_000, 4, 8192, seed=232),
 }

@@ -33,7 +33,8 @@ def test_oracle_matches_reference_golden(path):
 def test_golden_set_is_complete():
     names = {os.path.basename(p)[:-4] for p in GOLD}
     for must in ["t01_tie_seqno", "t03_pretargeted", "t06_lowest", "t08_rq_fifo",
-                 "t13_donor", "t16_wild_nonzero", "c2_n20k_r4k", "c2_eqprio_n20k_r4k", "c4_n30k_r2k", "c5_stream"]:
+                 "t13_donor", "t16_wild_nonzero", "c2_n20k_r4k", "c2_eqprio_n20k_r4k", "c4_n30k_r2k", "c5_stream",
+                 "w100_c2_park_puts", "w100_c4", "w200_get_unreserve"]:
         assert must in names
 
 
