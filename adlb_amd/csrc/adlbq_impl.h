@@ -340,6 +340,12 @@ struct adlbq_server {
     size_t cap_wtmp = 0;
     int cap_wreq = 0, cap_wpages = 0;
     int group_launch = 1;              // "group_launch": 0 = adlbq_reserve_group_device launches this handle alone
+    // adlbq_unreserve_reserve_device: the unreserves the next launch_scan puts ahead of pass 1
+    int unres_n = 0;
+    const int *unres_reqs = nullptr, *unres_resp = nullptr;
+    int *d_unres_arrive = nullptr;     // [2] arrival counters, used in turn
+    int unres_par = 0;
+    int fuse_unreserve = 1;            // "fuse_unreserve": 0 = a separate k_unreserve_resp launch
     ::GroupRec *grec = nullptr;        // non-null: launch_reserve records its launches (adlbq_reserve_group_device)
     // the group launch's argument tables (kept by the group's first handle): pinned staging x 2, device copy
     char *h_gtab[2] = {nullptr, nullptr};
@@ -411,7 +417,9 @@ void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
 // host time since t0 added to stage `name` (profiling only; no events)
 void host_stage_add(adlbq_server *h, const char *name, std::chrono::steady_clock::time_point t0);
 int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
+int sync_batch_counters(adlbq_server *h);  // synchronise; h->ctr from the last batch's landed snapshot
 int wide_choose(adlbq_server *h, int R, const int *d_reqs);  // T > ADLBQ_MAX_TYPES: the batch's choices
+int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12);  // k_unreserve_resp
 int group_join(adlbq_server *const *hs, const std::vector<int> &m);     // hs[m[0]]'s stream waits for the members'
 int group_release(adlbq_server *const *hs, const std::vector<int> &m);  // the members' streams wait for hs[m[0]]'s
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail);
@@ -435,6 +443,66 @@ bool export_after_args(adlbq_server *h, int k, int *d_recs, int *d_nrec, long lo
 int launch_export_after_group(const ExportAfterGroup &g, int n, int k, int Tmax, hipStream_t s);
 
 // ---------------------------------------------------------------- device helpers
+// SS_UNRESERVE of every unit a reserve batch handed out (k_unreserve_resp, and
+// the unreserve workgroups of a fused adlbq_unreserve_reserve_device launch)
+__device__ __forceinline__ void unreserve_resp_body(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
+                                                    const long long *__restrict__ seq2slot, long long nseq,
+                                                    uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
+                                                    long long *anchor, const int *__restrict__ mslot, int ntypes,
+                                                    int bid) {
+    int i = bid * blockDim.x + threadIdx.x;
+    int t = -1, up = INT_MIN;
+    // lane u holds anchor[u] (T <= 64), loaded with the responses: only a unit above it needs an
+    // atomic max (one per type of the wave; every wave adding to one word would serialise them)
+    const long long my_anchor = __lane_id() < ntypes ? __hip_atomic_load(anchor + __lane_id(), __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_AGENT) : LLONG_MAX;
+    if (i < n) {
+        const int rc = resp[(long long)ADLBQ_RESP_INTS * i], seq = resp[(long long)ADLBQ_RESP_INTS * i + 5];
+        const int rank = reqs[(long long)ADLBQ_RESERVE_INTS * i];
+        const int ms = mslot != nullptr ? mslot[i] : -1;
+        if (rc == 1 && seq > 0 && seq < nseq) {
+            long long slot = ms;
+            uint32_t m = 0;
+            int pn = 0;
+            int4 r0 = make_int4(0, 0, 0, 0), r1 = r0;
+            if (slot >= 0) {
+                m = meta[slot];
+                pn = pin[slot];
+                r0 = rrec[2 * slot];
+                r1 = rrec[2 * slot + 1];
+            }
+            if (slot < 0 || r0.z != seq) {  // not the last batch's record: the map
+                slot = seq2slot[seq];
+                if (slot >= 0) {
+                    m = meta[slot];
+                    pn = pin[slot];
+                    r0 = rrec[2 * slot];
+                    r1 = rrec[2 * slot + 1];
+                }
+            }
+            if (slot >= 0 && (m & M_LIVE) && pn == rank && r0.z == seq) {
+                pin[slot] = -1;
+                meta[slot] = m & ~M_PINNED;
+                t = m & M_TYPE;
+                up = r1.w;
+            }
+        }
+    }
+    // available again: keep the anchor above it, one atomic max per distinct type of the wave that rose
+    const long long at = __shfl(my_anchor, t >= 0 ? t : 0, 64);
+    if (t >= 0 && (long long)up <= at) t = -1;
+    for (unsigned long long b = __ballot(t >= 0); b;) {
+        const int leader = __ffsll((long long)b) - 1;
+        const int lt = __shfl(t, leader, 64);
+        int mx = t == lt ? up : INT_MIN;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+        if (__lane_id() == leader) atomicMax(anchor + lt, (long long)mx);
+        b &= ~__ballot(t == lt);
+    }
+}
+
+
 __device__ __forceinline__ unsigned long long make_key(int prio, unsigned int order) {
     // larger key == better: priority descending, then `order` ascending
     return ((unsigned long long)((unsigned int)prio ^ 0x80000000u) << 32) |

@@ -270,6 +270,20 @@ int refresh_counters(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
+static void apply_counters(adlbq_server *h);
+
+// After a synchronous reserve batch: the counters its k_finalize copied into
+// the newest snapshot slot (mapped memory, tagged last), no k_ctr_out launch.
+int sync_batch_counters(adlbq_server *h) {
+    const int slot = (h->snap_next + adlbq_server::NSNAP - 1) % adlbq_server::NSNAP;
+    AQ_HIP(hipStreamSynchronize(h->stream));
+    if (__atomic_load_n(&h->h_snap[slot].snap_tag, __ATOMIC_ACQUIRE) != h->snap_tag[slot])
+        return refresh_counters(h);
+    h->ctr = h->h_snap[slot];
+    apply_counters(h);
+    return ADLBQ_OK;
+}
+
 // the host's view after h->ctr has been refreshed
 static void apply_counters(adlbq_server *h) {
     h->ctr_stale = false;
@@ -850,6 +864,61 @@ __global__ void k_get_apply(const int *__restrict__ pairs, int n, long long *seq
     }
 }
 
+// A Get batch of at most 256 in one launch (the synchronous entry's few dozen
+// Gets): claim, barrier, apply, then the counters into mapped memory -- the
+// work of k_get_claim, k_get_apply and k_ctr_out without two launch boundaries.
+__global__ __launch_bounds__(256) void k_get_small(const int *__restrict__ pairs, int n, long long *seq2slot,
+                                                   long long nseq, uint32_t *meta, const int *__restrict__ pin,
+                                                   const int *__restrict__ seqa, const int *__restrict__ prio,
+                                                   const int4 *__restrict__ cold0, const int4 *__restrict__ cold1,
+                                                   int *claim, int *out5, DevCounters *ctr, DevCounters *zctr) {
+    const int i = threadIdx.x;
+    int seq = 0;
+    long long slot = -1;
+    if (i < n) {
+        const int rank = pairs[2 * i];
+        seq = pairs[2 * i + 1];
+        slot = (seq > 0 && seq < nseq) ? seq2slot[seq] : -1;
+        if (slot >= 0 && (meta[slot] & M_LIVE) && pin[slot] == rank && seqa[slot] == seq) atomicMin(&claim[seq], i);
+    }
+    __syncthreads();
+    int ok = 0, tgt = 0;
+    long long freed = 0;
+    if (i < n) {
+        int o[5] = {-1, 0, 0, 0, 0};
+        if (slot >= 0 && __hip_atomic_load(claim + seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == i) {
+            const int4 c0 = cold0[slot], c1 = cold1[slot];
+            o[0] = 1;
+            o[1] = c0.y;
+            o[2] = c1.z;
+            o[3] = prio[slot];
+            o[4] = c0.x;
+            meta[slot] = 0;
+            seq2slot[seq] = -1;
+            claim[seq] = INT_MAX;  // for the next batch
+            ok = 1;
+            tgt = c1.w >= 0;
+            freed = BYTES_WQ + c0.y;
+        }
+#pragma unroll
+        for (int k = 0; k < 5; k++) out5[5 * i + k] = o[k];
+    }
+    const unsigned long long b = __ballot(ok), bt = __ballot(tgt);
+    for (int o = 32; o > 0; o >>= 1) freed += __shfl_xor(freed, o, 64);
+    if ((threadIdx.x & 63) == 0 && b) {
+        atomicAdd((unsigned long long *)&ctr->got, (unsigned long long)__popcll(b));
+        if (bt) atomicAdd((unsigned long long *)&ctr->got_targeted, (unsigned long long)__popcll(bt));
+        atomicAdd((unsigned long long *)&ctr->bytes, (unsigned long long)(-freed));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // every field after the block's atomics (L2 reads), into mapped host memory
+    const int *src = reinterpret_cast<const int *>(ctr);
+    int *dst = reinterpret_cast<int *>(zctr);
+    for (int k = threadIdx.x; k < (int)(sizeof(DevCounters) / 4); k += blockDim.x)
+        dst[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // FA_INFO_NUM_WORK_UNITS (adlb.c:2466-2496) in one pass over every page:
 // max prio of the type (strict >, from LOWEST), units at that max, units of
 // the type.  Blocks publish partials; the last to arrive combines them.
@@ -928,62 +997,6 @@ __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ page
 // wqseqno; responses of another batch fall back to the wqseqno -> slot map.
 // The anchor is raised by a fire-and-forget atomic max per type of the wave
 // (a stale read could only add a harmless one: no load of it first).
-__device__ __forceinline__ void unreserve_resp_body(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
-                                                    const long long *__restrict__ seq2slot, long long nseq,
-                                                    uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
-                                                    long long *anchor, const int *__restrict__ mslot, int ntypes,
-                                                    int bid) {
-    int i = bid * blockDim.x + threadIdx.x;
-    int t = -1, up = INT_MIN;
-    // lane u holds anchor[u] (T <= 64), loaded with the responses: only a unit above it needs an
-    // atomic max (one per type of the wave; every wave adding to one word would serialise them)
-    const long long my_anchor = __lane_id() < ntypes ? __hip_atomic_load(anchor + __lane_id(), __ATOMIC_RELAXED,
-                                                                         __HIP_MEMORY_SCOPE_AGENT) : LLONG_MAX;
-    if (i < n) {
-        const int rc = resp[(long long)ADLBQ_RESP_INTS * i], seq = resp[(long long)ADLBQ_RESP_INTS * i + 5];
-        const int rank = reqs[(long long)ADLBQ_RESERVE_INTS * i];
-        const int ms = mslot != nullptr ? mslot[i] : -1;
-        if (rc == 1 && seq > 0 && seq < nseq) {
-            long long slot = ms;
-            uint32_t m = 0;
-            int pn = 0;
-            int4 r0 = make_int4(0, 0, 0, 0), r1 = r0;
-            if (slot >= 0) {
-                m = meta[slot];
-                pn = pin[slot];
-                r0 = rrec[2 * slot];
-                r1 = rrec[2 * slot + 1];
-            }
-            if (slot < 0 || r0.z != seq) {  // not the last batch's record: the map
-                slot = seq2slot[seq];
-                if (slot >= 0) {
-                    m = meta[slot];
-                    pn = pin[slot];
-                    r0 = rrec[2 * slot];
-                    r1 = rrec[2 * slot + 1];
-                }
-            }
-            if (slot >= 0 && (m & M_LIVE) && pn == rank && r0.z == seq) {
-                pin[slot] = -1;
-                meta[slot] = m & ~M_PINNED;
-                t = m & M_TYPE;
-                up = r1.w;
-            }
-        }
-    }
-    // available again: keep the anchor above it, one atomic max per distinct type of the wave that rose
-    const long long at = __shfl(my_anchor, t >= 0 ? t : 0, 64);
-    if (t >= 0 && (long long)up <= at) t = -1;
-    for (unsigned long long b = __ballot(t >= 0); b;) {
-        const int leader = __ffsll((long long)b) - 1;
-        const int lt = __shfl(t, leader, 64);
-        int mx = t == lt ? up : INT_MIN;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-        if (__lane_id() == leader) atomicMax(anchor + lt, (long long)mx);
-        b &= ~__ballot(t == lt);
-    }
-}
 
 __global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
                                  const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta, int *pin,
@@ -1405,6 +1418,7 @@ int adlbq_destroy(adlbq_server *h) {
         if (h->h_gtab[q]) hipHostFree(h->h_gtab[q]);
     }
     if (h->d_gtab) hipFree(h->d_gtab);
+    if (h->d_unres_arrive) hipFree(h->d_unres_arrive);
     for (hipEvent_t e : h->gjoin)
         if (e) hipEventDestroy(e);
     for (int q = 0; q < 2; q++) {
@@ -1683,8 +1697,16 @@ int adlbq_get_reserved_batch(adlbq_server *h, int n, const int *pairs2, int *out
     if ((rc0 = ensure_zc(h, (long long)n * 7)) || (rc0 = ensure_zctr(h))) return rc0;
     std::memcpy(h->h_zc, pairs2, sizeof(int) * 2 * (size_t)n);
     int rc;
-    if ((rc = launch_get_batch(h, n, h->d_zc, h->d_zc + 2 * (size_t)n))) return rc;
-    k_ctr_out<<<1, 1, 0, h->stream>>>(h->d_ctr, h->d_zctr);
+    if (n <= 256 && (long long)h->next_wqseqno <= h->cap_getclaim) {  // one launch
+        wq_changed(h);
+        k_get_small<<<1, 256, 0, h->stream>>>(h->d_zc, n, h->d_seq2slot, h->next_wqseqno, h->d_meta,
+                                              h->d_pin, h->d_seq, h->d_prio, h->d_cold0, h->d_cold1, h->d_getclaim,
+                                              h->d_zc + 2 * (size_t)n, h->d_ctr, h->d_zctr);
+        h->ctr_stale = true;
+    } else {
+        if ((rc = launch_get_batch(h, n, h->d_zc, h->d_zc + 2 * (size_t)n))) return rc;
+        k_ctr_out<<<1, 1, 0, h->stream>>>(h->d_ctr, h->d_zctr);
+    }
     AQ_HIP(hipGetLastError());
     AQ_HIP(hipStreamSynchronize(h->stream));
     std::memcpy(out5, h->h_zc + 2 * (size_t)n, sizeof(int) * 5 * (size_t)n);
@@ -1714,18 +1736,26 @@ int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, in
     return ADLBQ_OK;
 }
 
-int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12) {
-    if (h) wq_changed(h);
-    if (!ok_handle(h) || n < 0 || (n && (!d_reqs18 || !d_resp12)))
-        return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_device");
-    if (!n) return ADLBQ_OK;
-    hipSetDevice(h->device);
+}  // extern "C"
+namespace adlbq {
+int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12) {
     k_unreserve_resp<<<(n + 255) / 256, 256, 0, h->stream>>>(d_reqs18, d_resp12, n, h->d_seq2slot, h->next_wqseqno,
                                                              h->d_meta, h->d_pin, h->d_rrec, h->d_anchor,
                                                              (h->d_mslot && n <= h->cap_req) ? h->d_mslot : nullptr,
                                                              std::min(h->T, 64));
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
+}
+}  // namespace adlbq
+extern "C" {
+
+int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12) {
+    if (h) wq_changed(h);
+    if (!ok_handle(h) || n < 0 || (n && (!d_reqs18 || !d_resp12)))
+        return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_device");
+    if (!n) return ADLBQ_OK;
+    hipSetDevice(h->device);
+    return launch_unreserve_resp(h, n, d_reqs18, d_resp12);
 }
 
 int adlbq_unreserve_resp_group_device(adlbq_server *const *hs, int n, const int *const *d_reqs18,
@@ -2301,6 +2331,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (n == "fold_thresholds") {
         if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0, 1 or 2 (auto)");
         h->fold_thresholds = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "fuse_unreserve") {
+        if (value < 0 || value > 1) return fail(ADLBQ_ERR_ARG, "fuse_unreserve must be 0 or 1");
+        h->fuse_unreserve = (int)value;
         return ADLBQ_OK;
     }
     if (n == "group_launch") {

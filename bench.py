@@ -4,8 +4,11 @@ One step = one batch of R=65,536 hanging Reserves (config 2 / metric shape:
 4 types, prio ~ U[0,1024), 70% one type / 20% two / 10% wildcard) matched
 against an HBM-resident 10M-unit work queue through the C ABI
 (adlbq_reserve_batch_device), followed by SS_UNRESERVE of every matched unit
-(adlbq_unreserve_batch_device) so each step sees the same queue.  Each step
-uses a different pre-staged request batch.  Inputs are resident in HBM before
+(adlbq_unreserve_resp_device) so each step sees the same queue; by default the
+unreserves go down with the next step's batch (adlbq_unreserve_reserve_device:
+they run in the first workgroups of that batch's first launch, which the scan
+waits for), so K timed steps still hold K batches and K batches' unreserves.
+Each step uses a different pre-staged request batch.  Inputs are resident in HBM before
 the timed region.
 
 Multi-GPU (torchrun, one process per GPU): every rank is an independent ADLB
@@ -86,6 +89,13 @@ def parse():
                     help="config 3: adlbq_set_param on every shard (repeatable)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 stream measurement")
+    ap.add_argument("--fuse-unreserve", type=int, default=1,
+                    help="metric step: the unreserves ride in the next batch's first launch (1) or launch alone (0)")
+    ap.add_argument("--no-wide", action="store_true", help="skip the more-than-64-types leg")
+    ap.add_argument("--wide-only", action="store_true", help="only the more-than-64-types leg")
+    ap.add_argument("--wide-types", type=int, default=100)
+    ap.add_argument("--wide-units", type=int, default=200_000)
+    ap.add_argument("--wide-reserves", type=int, default=4096)
     ap.add_argument("--config5-only", action="store_true", help="only the config-5 leg")
     ap.add_argument("--c5-procs", type=int, default=1, help="config 5: also run one server process per shard (1)")
     ap.add_argument("--c5-shards", type=int, default=8, help="config 5: server shards (own event stream each)")
@@ -151,7 +161,7 @@ def pmc_traffic(args) -> dict | None:
     if prof is None:
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu", "--no-pmc",
-             "--no-config3", "--no-config4", "--no-config5",
+             "--no-config3", "--no-config4", "--no-config5", "--no-wide",
              "--no-profile", "--no-host-path", "--units", str(args.units), "--reserves", str(args.reserves), "--types",
              str(args.types), "--seed", str(args.seed)] + (["--equal-prio"] if args.equal_prio else [])
     out = {}
@@ -665,6 +675,48 @@ def c5_server_processes(traces, expect, A, S, device):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def bench_wide(args, torch, dev):
+    """More than 64 work types (the sorted-runs Reserve path, adlbq_wide.hip):
+    a config-2-shaped queue with args.wide_types types; a step = one Reserve
+    batch + the unreserve of its matches.  The first batch is checked against
+    the oracle (the restatement of xq.c, on the same trace)."""
+    import oracle
+    from adlb_amd import synth
+    from adlb_amd.server import Server
+    N, R, T = args.wide_units, args.wide_reserves, args.wide_types
+    w = synth.config2(n_units=N, n_types=T, n_reserves=R, seed=args.seed + 90, prio_hi=1024)
+    reqs = np.concatenate([w.r_rank[:, None], w.r_hang[:, None].astype(np.int32), w.r_types], axis=1).astype(np.int32)
+    units = np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1), np.zeros(N),
+                      np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32)
+    with Server(w.user_types, w.num_app_ranks, max_units=N) as srv:
+        srv.put_batch(units)
+        d_req = torch.from_numpy(reqs).to(dev)
+        d_resp = torch.empty((R, 12), dtype=torch.int32, device=dev)
+        first = None
+        for _ in range(2):  # warm-up (buffers sized), then the checked batch's answers
+            srv.reserve_batch_device(R, d_req.data_ptr(), d_resp.data_ptr())
+            torch.cuda.synchronize()
+            first = d_resp.cpu().numpy().copy()
+            srv.unreserve_resp_device(R, d_req.data_ptr(), d_resp.data_ptr())
+        torch.cuda.synchronize()
+        steps = 5
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            srv.reserve_batch_device(R, d_req.data_ptr(), d_resp.data_ptr())
+            srv.unreserve_resp_device(R, d_req.data_ptr(), d_resp.data_ptr())
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    o = oracle.Oracle("own")
+    o.init(w.user_types, w.num_app_ranks)
+    exp = np.asarray(synth.split_outputs(o.replay(synth.workload_trace(w)))[N:], np.int32)
+    same = bool(np.array_equal(first[:, :10], exp[:, :10]))
+    matched = int((first[:, 0] == 1).sum())
+    return {"workload": f"{T} work types (sorted-runs path): {N} untargeted units, prio U[0,1024), {R} hanging "
+                        f"Reserves (70/20/10 single/pair/wildcard); step = reserve batch + unreserve",
+            "value": matched * steps / el if same else None, "unit": "assignments/s",
+            "ms_per_step": el * 1e3 / steps, "matched_per_step": matched, "parity": same}
+
+
 def config4_parity(ec, w, puts, applied, reqs, d_resp, d_pout, b, R, server_rank):
     """Batch b (the last timed one) of the config-4 leg against the sequential
     result over the queue it saw: the initial units, then every Put batch in
@@ -878,6 +930,10 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    if args.wide_only:
+        if rank == 0:
+            print(json.dumps({"wide_types": bench_wide(args, torch, dev)}), flush=True)
+        return
     if args.config5_only:
         out = bench_config5(args, torch, dist, world, rank, local, dev)
         if rank == 0:
@@ -934,10 +990,27 @@ def main():
     p_req = [d_reqs[b].data_ptr() for b in range(nb)]  # no tensor views inside the timed loop
     p_resp = [d_resp[b].data_ptr() for b in range(nb)]
 
+    # SS_UNRESERVE every matched unit, straight from the batch's responses: with
+    # --fuse-unreserve (default) it goes down with the next step's batch
+    # (adlbq_unreserve_reserve_device: the unreserve workgroups lead that batch's
+    # first launch), so every step still does one batch + one batch's unreserves
+    pending = []
+
     def step(b):
-        srv.reserve_batch_device(R, p_req[b], p_resp[b])
-        # SS_UNRESERVE every matched unit, straight from the batch's responses
-        srv.unreserve_resp_device(R, p_req[b], p_resp[b])
+        if args.fuse_unreserve and pending:
+            srv.unreserve_reserve_device(R, pending[0][0], pending[0][1], R, p_req[b], p_resp[b])
+            pending.clear()
+        else:
+            srv.reserve_batch_device(R, p_req[b], p_resp[b])
+        if args.fuse_unreserve:
+            pending.append((p_req[b], p_resp[b]))
+        else:
+            srv.unreserve_resp_device(R, p_req[b], p_resp[b])
+
+    def flush_unreserve():
+        if pending:
+            srv.unreserve_resp_device(R, pending[0][0], pending[0][1])
+            pending.clear()
 
     for b in range(args.warmup):
         step(b)
@@ -975,6 +1048,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    flush_unreserve()  # the last batch's unreserves (the first timed step did the warm-up's last)
     matched = int((d_resp[args.warmup:, :, 0] == 1).sum().item())
     if world > 1:
         el, matched = shards.reduce_step_timing(el, matched)
@@ -1117,6 +1191,11 @@ def main():
             res["config5"] = bench_config5(args, torch, dist, world, rank, local, dev)
         except Exception as e:  # reported, not fatal
             res["config5"] = {"error": f"{type(e).__name__}: {e}"}
+    if not args.no_wide:
+        try:
+            res["wide_types"] = bench_wide(args, torch, dev)
+        except Exception as e:  # reported, not fatal
+            res["wide_types"] = {"error": f"{type(e).__name__}: {e}"}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds, shards.shard_seed(args.seed, rank),
                                            args.cpu_cores, args.equal_prio)

@@ -32,7 +32,7 @@ if [ "$PART" = "tests" ] || [ "$PART" = "all" ]; then
 fi
 if [ "$PART" = "prof" ] || [ "$PART" = "all" ]; then
   cd /tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/metric -o metric -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --no-pmc --no-host-path --no-config3 --no-config4 --no-config5 > $O/metric_bench.json 2> $O/metric.err || { echo metric prof failed; tail -5 $O/metric.err; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/metric -o metric -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --no-pmc --no-host-path --no-config3 --no-config4 --no-config5 --no-wide > $O/metric_bench.json 2> $O/metric.err || { echo metric prof failed; tail -5 $O/metric.err; exit 1; }
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c3 -o c3 -- python3 $R/bench.py --config3-only --no-pmc --no-cpu > $O/c3_bench.json 2> $O/c3.err || { echo c3 prof failed; exit 1; }
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4 -o c4 -- python3 $R/bench.py --config4-only --no-pmc --no-cpu > $O/c4_bench.json 2> $O/c4.err || { echo c4 prof failed; exit 1; }
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c5 -o c5 -- python3 $R/bench.py --config5-only --no-pmc --no-cpu > $O/c5_bench.json 2> $O/c5.err || { echo c5 prof failed; exit 1; }
@@ -44,6 +44,6 @@ if [ "$PART" = "bench" ] || [ "$PART" = "all" ]; then
   tail -1 $O/bench_default.json | cut -c1-3000
 fi
 if [ "$PART" = "metric" ]; then
-  timeout -k 10 300 python3 bench.py --no-cpu --no-host-path --no-config3 --no-config4 --no-config5 > $O/metric_only.json 2> $O/metric_only.err || { echo bench failed; tail -20 $O/metric_only.err; exit 1; }
+  timeout -k 10 300 python3 bench.py --no-cpu --no-host-path --no-config3 --no-config4 --no-config5 --no-wide > $O/metric_only.json 2> $O/metric_only.err || { echo bench failed; tail -20 $O/metric_only.err; exit 1; }
   tail -1 $O/metric_only.json | cut -c1-1500
 fi
