@@ -26,7 +26,6 @@ SIGNATURES = {
     "adlbq_reserve_batch": (c_int, [P, c_int, P, P]),
     "adlbq_reserve_batch_device": (c_int, [P, c_int, P, P]),
     "adlbq_reserve_group_device": (c_int, [P, c_int, P, P, P]),
-    "adlbq_unreserve_reserve_device": (c_int, [P, c_int, P, P, c_int, P, P]),
     "adlbq_get_reserved": (c_int, [P, c_int, c_int, P]),
     "adlbq_get_reserved_batch": (c_int, [P, c_int, P, P]),
     "adlbq_get_reserved_batch_device": (c_int, [P, c_int, P, P]),

@@ -340,12 +340,6 @@ struct adlbq_server {
     size_t cap_wtmp = 0;
     int cap_wreq = 0, cap_wpages = 0;
     int group_launch = 1;              // "group_launch": 0 = adlbq_reserve_group_device launches this handle alone
-    // adlbq_unreserve_reserve_device: the unreserves the next launch_scan puts ahead of pass 1
-    int unres_n = 0;
-    const int *unres_reqs = nullptr, *unres_resp = nullptr;
-    int *d_unres_arrive = nullptr;     // [2] arrival counters, used in turn
-    int unres_par = 0;
-    int fuse_unreserve = 1;            // "fuse_unreserve": 0 = a separate k_unreserve_resp launch
     ::GroupRec *grec = nullptr;        // non-null: launch_reserve records its launches (adlbq_reserve_group_device)
     // the group launch's argument tables (kept by the group's first handle): pinned staging x 2, device copy
     char *h_gtab[2] = {nullptr, nullptr};

@@ -165,29 +165,6 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
 // (most units fall in a few far bins) do not serialise one LDS atomic.
 constexpr int HK = 4;
 
-// adlbq_unreserve_reserve_device: the previous batch's SS_UNRESERVE in the
-// first workgroups of this batch's first launch.  They arrive at a counter
-// (agent-scope release); the pass-1 workgroups wait for every arrival
-// (acquire) before they load a page, so the scan sees the queue after the
-// unreserves, as two launches would.  Two counters used in turn: the
-// unreserve workgroups zero the other one (its last batch's launch is over).
-struct UnresPre {
-    int nb;  // workgroups of 256 unreserves (0: none)
-    int n;
-    const int *reqs, *resp;
-    const long long *seq2slot;
-    long long nseq;
-    uint32_t *meta;
-    int *pin;
-    const int4 *rrec;
-    long long *anchor;
-    const int *mslot;
-    int ntypes;
-    int *arrive, *arrive_other;
-    int *fail;  // a timed-out wait: the batch is answered ADLB_ERROR (k_finalize)
-};
-constexpr long long UNRES_WAIT_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock: one second
-
 struct HistArgs {
     const int *pages;
     int npages, tail_fill;
@@ -207,7 +184,6 @@ struct HistArgs {
     int zper;                  // (unused: k_thresholds zeroes the other buffer)
     int variant;               // "hist_variant": 0 the round-2 loop, 1 the rebased one
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
-    UnresPre un;               // the fused unreserves ahead of this launch's roles (nb = 0: none)
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -721,45 +697,12 @@ __device__ void fold_thresholds(const FoldArgs &f, int T, unsigned int *csum, un
 // workgroups [0, nprep) prepare 256 requests each, the rest count one page;
 // with fd.on the last workgroups then do k_thresholds' work.
 template <int TB, int PPB = 1>
-__device__ __forceinline__ void prep_hist_body(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd, int bid_, int nbk_) {
+__device__ __forceinline__ void prep_hist_body(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd, const int bid_, const int nbk_) {
     static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
     extern __shared__ unsigned int lds[];
-    const UnresPre &un = ha.un;
-    if (un.nb > 0) {
-        if (bid_ < un.nb) {  // an unreserve workgroup: 256 SS_UNRESERVEs, then its arrival
-            if (bid_ == 0 && threadIdx.x == 0) *un.arrive_other = 0;
-            unreserve_resp_body(un.reqs, un.resp, un.n, un.seq2slot, un.nseq, un.meta, un.pin, un.rrec, un.anchor,
-                                un.mslot, un.ntypes, bid_);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_fetch_add(un.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            return;
-        }
-        bid_ -= un.nb;
-        nbk_ -= un.nb;
-    }
     if ((int)bid_ < nprep) {
         prep_block<TB>(pa, bid_, reinterpret_cast<int *>(lds));
     } else {
-        if (un.nb > 0) {  // the page's loads only after every unreserve has landed
-            if (threadIdx.x == 0) {
-                const long long t0 = wall_clock64();
-                while (__hip_atomic_load(un.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < un.nb) {
-                    if (wall_clock64() - t0 > UNRES_WAIT_TICKS) {
-                        atomicAdd(un.fail, 1);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-        }
         if (ha.variant == 0) hist_page_v0(ha, bid_ - nprep, lds);
         else hist_pages<PPB>(ha, (bid_ - nprep) * PPB, lds);
         if (fd.on && fd.zn > 0) {  // the previous scan's chunk sums (consumed): zeroed for the scan after this one
@@ -3885,27 +3828,6 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                           h->d_rank_sync + ADLBQ_MAX_TYPES + 1, zcs, ha.zn};
         }
     }
-    int gridu = grid;
-    if (h->unres_n > 0) {  // adlbq_unreserve_reserve_device: the unreserves ride ahead of pass 1 when they can
-        const int nu = h->unres_n;
-        h->unres_n = 0;
-        if (grid > 0 && scan && !fd.on && !h->hist_diag && !h->split_prep) {
-            if (!h->d_unres_arrive) {
-                AQ_HIP(hipMalloc((void **)&h->d_unres_arrive, sizeof(int) * 2));
-                AQ_HIP(hipMemsetAsync(h->d_unres_arrive, 0, sizeof(int) * 2, s));
-            }
-            const int pu = h->unres_par;
-            h->unres_par ^= 1;
-            ha.un = UnresPre{(nu + 255) / 256, nu, h->unres_reqs, h->unres_resp, h->d_seq2slot, h->next_wqseqno,
-                             h->d_meta, h->d_pin, h->d_rrec, h->d_anchor,
-                             (h->d_mslot && nu <= h->cap_req) ? h->d_mslot : nullptr, std::min(h->T, 64),
-                             h->d_unres_arrive + pu, h->d_unres_arrive + (pu ^ 1), h->d_rank_sync + ADLBQ_MAX_TYPES + 1};
-            gridu = grid + ha.un.nb;
-        } else {
-            int rc;
-            if ((rc = launch_unreserve_resp(h, nu, h->unres_reqs, h->unres_resp))) return rc;
-        }
-    }
     if (grid > 0) {
         // pass 1: the histogram copies, then the four waves' speculative lists
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0,
@@ -3924,10 +3846,10 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         } else if (h->grec) {  // adlbq_reserve_group_device: recorded, launched with the group's
             h->grec->kinds |= GK_PREP;
             h->grec->tb = T <= 4 ? 4 : 8;
-            h->grec->prep = GPrep{pa, nprep, ha, fd, gridu};
+            h->grec->prep = GPrep{pa, nprep, ha, fd, grid};
             h->grec->lds_prep = (size_t)lds;
         } else {
-            kph<<<gridu, 256, lds, s>>>(pa, nprep, ha, fd);
+            kph<<<grid, 256, lds, s>>>(pa, nprep, ha, fd);
         }
         stage_end(h, "hist", ev);
     }
@@ -5451,38 +5373,6 @@ int adlbq_reserve_batch_device(adlbq_server *h, int n, const int *d_reqs18, int 
     return launch_reserve(h, n, d_reqs18, d_resp12);
 }
 
-
-// SS_UNRESERVE of the matches of an earlier batch (reqs/resp of nu requests),
-// then a Reserve batch: the unreserves run in the first workgroups of the
-// batch's first launch (UnresPre), or as their own launch when that launch
-// cannot carry them.  The same results as adlbq_unreserve_resp_device then
-// adlbq_reserve_batch_device.
-int adlbq_unreserve_reserve_device(adlbq_server *h, int nu, const int *d_ureqs18, const int *d_uresp12, int n,
-                                   const int *d_reqs18, int *d_resp12) {
-    if (!h || nu < 0 || n < 0 || (nu && (!d_ureqs18 || !d_uresp12)) || (n && (!d_reqs18 || !d_resp12)))
-        return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_reserve_device");
-    hipSetDevice(h->device);
-    int rc;
-    if (nu > 0) {
-        wq_changed(h);
-        if (!n || !h->fuse_unreserve || h->T > ADLBQ_MAX_TYPES) {
-            if ((rc = launch_unreserve_resp(h, nu, d_ureqs18, d_uresp12))) return rc;
-        } else {
-            h->unres_n = nu;  // launch_scan takes them
-            h->unres_reqs = d_ureqs18;
-            h->unres_resp = d_uresp12;
-        }
-    }
-    if (!n) return ADLBQ_OK;
-    rc = launch_reserve(h, n, d_reqs18, d_resp12);
-    if (h->unres_n > 0) {  // not taken (an error path): never drop them
-        const int nu2 = h->unres_n;
-        h->unres_n = 0;
-        const int rc2 = launch_unreserve_resp(h, nu2, h->unres_reqs, h->unres_resp);
-        if (!rc) rc = rc2;
-    }
-    return rc;
-}
 
 // One launch per pipeline kernel for the batches of n handles of one process
 // (its server shards), each handle's stream ordered as if it had run its own.

@@ -1418,7 +1418,6 @@ int adlbq_destroy(adlbq_server *h) {
         if (h->h_gtab[q]) hipHostFree(h->h_gtab[q]);
     }
     if (h->d_gtab) hipFree(h->d_gtab);
-    if (h->d_unres_arrive) hipFree(h->d_unres_arrive);
     for (hipEvent_t e : h->gjoin)
         if (e) hipEventDestroy(e);
     for (int q = 0; q < 2; q++) {
@@ -2331,11 +2330,6 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (n == "fold_thresholds") {
         if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0, 1 or 2 (auto)");
         h->fold_thresholds = (int)value;
-        return ADLBQ_OK;
-    }
-    if (n == "fuse_unreserve") {
-        if (value < 0 || value > 1) return fail(ADLBQ_ERR_ARG, "fuse_unreserve must be 0 or 1");
-        h->fuse_unreserve = (int)value;
         return ADLBQ_OK;
     }
     if (n == "group_launch") {

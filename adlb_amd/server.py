@@ -102,11 +102,6 @@ class Server:
         _lib.check(self.lib.adlbq_reserve_batch_device(self.h, n, d_reqs, d_resp),
                    "adlbq_reserve_batch_device")
 
-    def unreserve_reserve_device(self, nu: int, d_ureqs: int, d_uresp: int, n: int, d_reqs: int, d_resp: int) -> None:
-        """SS_UNRESERVE of an earlier batch's matches, then a Reserve batch, in one launch chain."""
-        _lib.check(self.lib.adlbq_unreserve_reserve_device(self.h, nu, d_ureqs, d_uresp, n, d_reqs, d_resp),
-                   "adlbq_unreserve_reserve_device")
-
     # -- FA_GET_RESERVED / SS_UNRESERVE ---------------------------------------
     def get_reserved(self, rank, wqseqno):
         out = np.empty(5, dtype=np.int32)

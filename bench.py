@@ -4,11 +4,8 @@ One step = one batch of R=65,536 hanging Reserves (config 2 / metric shape:
 4 types, prio ~ U[0,1024), 70% one type / 20% two / 10% wildcard) matched
 against an HBM-resident 10M-unit work queue through the C ABI
 (adlbq_reserve_batch_device), followed by SS_UNRESERVE of every matched unit
-(adlbq_unreserve_resp_device) so each step sees the same queue; by default the
-unreserves go down with the next step's batch (adlbq_unreserve_reserve_device:
-they run in the first workgroups of that batch's first launch, which the scan
-waits for), so K timed steps still hold K batches and K batches' unreserves.
-Each step uses a different pre-staged request batch.  Inputs are resident in HBM before
+(adlbq_unreserve_resp_device) so each step sees the same queue.  Each step
+uses a different pre-staged request batch.  Inputs are resident in HBM before
 the timed region.
 
 Multi-GPU (torchrun, one process per GPU): every rank is an independent ADLB
@@ -89,8 +86,6 @@ def parse():
                     help="config 3: adlbq_set_param on every shard (repeatable)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 stream measurement")
-    ap.add_argument("--fuse-unreserve", type=int, default=1,
-                    help="metric step: the unreserves ride in the next batch's first launch (1) or launch alone (0)")
     ap.add_argument("--no-wide", action="store_true", help="skip the more-than-64-types leg")
     ap.add_argument("--wide-only", action="store_true", help="only the more-than-64-types leg")
     ap.add_argument("--wide-types", type=int, default=100)
@@ -990,27 +985,10 @@ def main():
     p_req = [d_reqs[b].data_ptr() for b in range(nb)]  # no tensor views inside the timed loop
     p_resp = [d_resp[b].data_ptr() for b in range(nb)]
 
-    # SS_UNRESERVE every matched unit, straight from the batch's responses: with
-    # --fuse-unreserve (default) it goes down with the next step's batch
-    # (adlbq_unreserve_reserve_device: the unreserve workgroups lead that batch's
-    # first launch), so every step still does one batch + one batch's unreserves
-    pending = []
-
     def step(b):
-        if args.fuse_unreserve and pending:
-            srv.unreserve_reserve_device(R, pending[0][0], pending[0][1], R, p_req[b], p_resp[b])
-            pending.clear()
-        else:
-            srv.reserve_batch_device(R, p_req[b], p_resp[b])
-        if args.fuse_unreserve:
-            pending.append((p_req[b], p_resp[b]))
-        else:
-            srv.unreserve_resp_device(R, p_req[b], p_resp[b])
-
-    def flush_unreserve():
-        if pending:
-            srv.unreserve_resp_device(R, pending[0][0], pending[0][1])
-            pending.clear()
+        srv.reserve_batch_device(R, p_req[b], p_resp[b])
+        # SS_UNRESERVE every matched unit, straight from the batch's responses
+        srv.unreserve_resp_device(R, p_req[b], p_resp[b])
 
     for b in range(args.warmup):
         step(b)
@@ -1048,7 +1026,6 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    flush_unreserve()  # the last batch's unreserves (the first timed step did the warm-up's last)
     matched = int((d_resp[args.warmup:, :, 0] == 1).sum().item())
     if world > 1:
         el, matched = shards.reduce_step_timing(el, matched)

@@ -125,14 +125,6 @@ int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples);
  * with rc 1): pin_rank = -1, pinned = 0.  Enqueued on the handle's stream. */
 int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12);
 
-/* adlbq_unreserve_resp_device(h, nu, d_ureqs18, d_uresp12) followed by
- * adlbq_reserve_batch_device(h, n, d_reqs18, d_resp12), with the same results:
- * the unreserves run in the first workgroups of the batch's first launch, and
- * the batch's scan waits for them inside that launch instead of behind a
- * launch boundary.  nu = 0 or n = 0: the one call alone. */
-int adlbq_unreserve_reserve_device(adlbq_server *h, int nu, const int *d_ureqs18, const int *d_uresp12, int n,
-                                   const int *d_reqs18, int *d_resp12);
-
 /* adlbq_unreserve_resp_device for several handles of one process (distinct,
  * one device; counts[i] responses of hs[i]) as one launch on hs[0]'s stream,
  * ordered like adlbq_reserve_group_device. */

@@ -545,39 +545,3 @@ def test_put_batch_device_matches_host_variant(gpu_available):
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 
-
-@pytest.mark.parametrize("fuse", [1, 0])
-def test_unreserve_reserve_fused(gpu_available, fuse):
-    """adlbq_unreserve_reserve_device (the previous batch's unreserves in the
-    first workgroups of the next batch's first launch) == the two calls one
-    after the other: every batch after an unreserve of the one before gets the
-    first batch's answers, which equal the oracle's."""
-    import torch
-    w = synth.config2(n_units=100_000, n_reserves=8192, seed=233)
-    reqs = np.concatenate([w.r_rank[:, None], w.r_hang[:, None].astype(np.int32), w.r_types],
-                          axis=1).astype(np.int32)
-    exp = run_oracle(w.user_types, (w.num_app_ranks, 1, 0), np.concatenate(
-        [synth.put_events(w), synth.reserve_events(w.r_rank, w.r_types, w.r_hang)]))
-    exp = np.asarray(synth.split_outputs(exp)[-len(reqs):])
-    with Server(w.user_types, w.num_app_ranks, max_units=w.n_units) as s:
-        s.set_param("fuse_unreserve", fuse)
-        units = np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(w.n_units, -1),
-                          np.zeros(w.n_units), np.full(w.n_units, -1), np.full(w.n_units, -1)],
-                         axis=1).astype(np.int32)
-        s.put_batch(units)
-        R = len(reqs)
-        d_req = torch.from_numpy(reqs).cuda()
-        d_resp = torch.full((4, R, 12), -7, dtype=torch.int32, device="cuda")
-        torch.cuda.synchronize()
-        s.reserve_batch_device(R, d_req.data_ptr(), d_resp[0].data_ptr())
-        for i in range(1, 4):
-            s.unreserve_reserve_device(R, d_req.data_ptr(), d_resp[i - 1].data_ptr(), R, d_req.data_ptr(),
-                                       d_resp[i].data_ptr())
-        s.unreserve_reserve_device(R, d_req.data_ptr(), d_resp[3].data_ptr(), 0, 0, 0)  # unreserves alone
-        s.sync()
-        outs = d_resp.cpu().numpy()
-        assert s.stat("batch_failed") == 0
-    assert (outs[0][:, 0] == 1).all()
-    for o in outs[1:]:
-        assert np.array_equal(o, outs[0])
-    assert np.array_equal(outs[0][:, :10], exp[:, :10])
