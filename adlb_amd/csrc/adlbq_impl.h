@@ -340,6 +340,9 @@ struct adlbq_server {
     size_t cap_wtmp = 0;
     int cap_wreq = 0, cap_wpages = 0;
     int group_launch = 1;              // "group_launch": 0 = adlbq_reserve_group_device launches this handle alone
+    const int *last_reqs = nullptr;    // the last batch's request array and size (its d_rh rows describe it)
+    int last_R = 0;
+    int fin_flat = 512;                // "fin_flat": k_finalize grids up to this size arrive at one counter
     ::GroupRec *grec = nullptr;        // non-null: launch_reserve records its launches (adlbq_reserve_group_device)
     // the group launch's argument tables (kept by the group's first handle): pinned staging x 2, device copy
     char *h_gtab[2] = {nullptr, nullptr};
@@ -443,7 +446,7 @@ __device__ __forceinline__ void unreserve_resp_body(const int *__restrict__ reqs
                                                     const long long *__restrict__ seq2slot, long long nseq,
                                                     uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
                                                     long long *anchor, const int *__restrict__ mslot, int ntypes,
-                                                    int bid) {
+                                                    int bid, const int2 *__restrict__ rh = nullptr) {
     int i = bid * blockDim.x + threadIdx.x;
     int t = -1, up = INT_MIN;
     // lane u holds anchor[u] (T <= 64), loaded with the responses: only a unit above it needs an
@@ -452,7 +455,8 @@ __device__ __forceinline__ void unreserve_resp_body(const int *__restrict__ reqs
                                                                          __HIP_MEMORY_SCOPE_AGENT) : LLONG_MAX;
     if (i < n) {
         const int rc = resp[(long long)ADLBQ_RESP_INTS * i], seq = resp[(long long)ADLBQ_RESP_INTS * i + 5];
-        const int rank = reqs[(long long)ADLBQ_RESERVE_INTS * i];
+        // the last batch's own requests: (rank, hang) compacted by its prep (8 B instead of a 72 B stride)
+        const int rank = rh != nullptr ? rh[i].x : reqs[(long long)ADLBQ_RESERVE_INTS * i];
         const int ms = mslot != nullptr ? mslot[i] : -1;
         if (rc == 1 && seq > 0 && seq < nseq) {
             long long slot = ms;

@@ -922,16 +922,23 @@ __device__ __forceinline__ void select_open_body(
                 cnt[u] = 0;
             }
         }
-        int rank = 0;
-        const int jn = min(n - i0, 64);
-        for (int j = 0; j < jn; j++) {
-            const int cj = __builtin_amdgcn_readlane(col, j);  // lane j's column (no LDS read per step)
-            const int before = j < lane;
-            rank += before & (cj == col);
-            if (fast) {
+        // earlier lanes of this step with a given column: one ballot per column bit, then per
+        // wanted column x the AND of B_b or ~B_b by x's bits (no 64-step walk over the lanes)
+        constexpr int CBITS = TB <= 4 ? 8 : TB <= 8 ? 9 : 12;  // bits of a column index (T * NB columns)
+        unsigned long long cb_[CBITS];
 #pragma unroll
-                for (int u = 0; u < RT; u++) cnt[u] += before & (cj == tcol[u]);
-            }
+        for (int b = 0; b < CBITS; b++) cb_[b] = __ballot((col >> b) & 1);
+        const unsigned long long vm = __ballot(i < n) & lt;
+        auto earlier_in = [&](int x) {
+            unsigned long long m = vm;
+#pragma unroll
+            for (int b = 0; b < CBITS; b++) m &= ((x >> b) & 1) ? cb_[b] : ~cb_[b];
+            return __popcll(m);
+        };
+        const int rank = earlier_in(col);
+        if (fast) {
+#pragma unroll
+            for (int u = 0; u < RT; u++) cnt[u] = tcol[u] >= 0 ? earlier_in(tcol[u]) : 0;
         }
         if (i < n) {
             const unsigned int r = run[col] + rank;
@@ -3087,6 +3094,7 @@ struct FinArgs {
     int *done;  // fused into k_chain0: [0] = the chain epoch once the choices are final
     int *mslot;  // [R] out: the slot request j was given, or -1 (adlbq_unreserve_resp_device reads it back)
     const int2 *rh;  // [R] (rank, hang) as prep_block copied them: 8 B per request instead of a 72 B record stride
+    int flat;        // grids up to this size arrive at one counter ("fin_flat"), larger ones by 8 groups
 };
 
 // k_rank gave up waiting for an in-launch candidate sort: the lists may be
@@ -3135,13 +3143,12 @@ __device__ __forceinline__ bool fin_request(const FinArgs &f, int j, bool failed
     return parks;
 }
 
-constexpr unsigned int FIN_FLAT = 512;  // grids up to this size arrive at one counter
 // Two-level arrival of workgroup bid of nb (8 groups, then one top counter)
 // keeps every counter's atomics to about nb / 8; a count rides in the high
 // half.  One thread; returns (parked in the batch << 32) | 1 for the last.
 __device__ __forceinline__ unsigned long long fin_arrive(const FinArgs &f, int parked, unsigned int nb,
                                                          unsigned int bid) {
-    if (nb <= FIN_FLAT) {  // a small grid: one counter, one returning atomic per workgroup
+    if (nb <= (unsigned int)f.flat) {  // a small grid: one counter, one returning atomic per workgroup
         const unsigned long long top = atomicAdd(&f.ctr->fin_top, ((unsigned long long)parked << 32) | 1ull);
         return (unsigned int)top == nb - 1u ? ((((top >> 32) + (unsigned long long)parked) << 32) | 1ull) : 0ull;
     }
@@ -4798,11 +4805,13 @@ static FinArgs fin_args(adlbq_server *h, int R, const int *d_reqs, int *d_resp, 
                    h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
                    h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, h->T, snap, h->snap_tag[h->snap_next],
                    h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
-                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot, h->d_rh};
+                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot, h->d_rh, h->fin_flat};
 }
 
 // the host side of a batch in flight: its snapshot slot, counts, upper bounds
-static void batch_launched(adlbq_server *h, int R, int export_k) {
+static void batch_launched(adlbq_server *h, int R, int export_k, const int *d_reqs) {
+    h->last_reqs = d_reqs;  // its d_rh rows describe these requests (adlbq_unreserve_resp_device)
+    h->last_R = R;
     h->batch_export_k = export_k;
     h->batch_export_R = R;
     h->launched_reserves += R;
@@ -4824,7 +4833,7 @@ static int launch_reserve_wide(adlbq_server *h, int R, const int *d_reqs, int *d
     const FinArgs fa = fin_args(h, R, d_reqs, d_resp, snap);
     k_finalize<<<(R + 255) / 256, 256, 0, h->stream>>>(fa);
     AQ_HIP(hipGetLastError());
-    batch_launched(h, R, 0);
+    batch_launched(h, R, 0, d_reqs);
     return ADLBQ_OK;
 }
 
@@ -5087,7 +5096,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     hsec("l_fin", hl);
     // the lists hold export_extra more per type: a steal export right after this batch gathers them
     AQ_HIP(hipGetLastError());
-    batch_launched(h, R, (np > 0 && T > 0) ? h->export_extra : 0);
+    batch_launched(h, R, (np > 0 && T > 0) ? h->export_extra : 0, d_reqs);
     auto t_all = host_t0;
     hsec("total", t_all);
     return ADLBQ_OK;

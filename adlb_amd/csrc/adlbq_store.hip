@@ -1001,8 +1001,14 @@ __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ page
 __global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
                                  const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta, int *pin,
                                  const int4 *__restrict__ rrec, long long *anchor, const int *__restrict__ mslot,
-                                 int ntypes) {
-    unreserve_resp_body(reqs, resp, n, seq2slot, nseq, meta, pin, rrec, anchor, mslot, ntypes, blockIdx.x);
+                                 int ntypes, const int2 *__restrict__ rh) {
+    unreserve_resp_body(reqs, resp, n, seq2slot, nseq, meta, pin, rrec, anchor, mslot, ntypes, blockIdx.x, rh);
+}
+
+// The last batch's compacted (rank, hang) rows when the unreserve is of that batch's own requests
+// (k_finalize read the same rows), else none (the ranks come from the request records).
+static const int2 *unres_rh(const adlbq_server *h, const int *d_reqs18, int n) {
+    return (h->d_rh && d_reqs18 == h->last_reqs && n == h->last_R) ? h->d_rh : nullptr;
 }
 
 // adlbq_unreserve_resp_group_device: up to UNRES_GROUP shards per launch, blockIdx.y = shard, the
@@ -1019,6 +1025,7 @@ struct UnresArgs {
     long long *anchor;
     const int *mslot;
     int ntypes;
+    const int2 *rh;
 };
 struct UnresGroup {
     UnresArgs a[UNRES_GROUP];
@@ -1027,7 +1034,7 @@ __global__ __launch_bounds__(256) void k_unreserve_resp_g(const UnresGroup g) {
     const UnresArgs &a = g.a[blockIdx.y];
     if ((int)blockIdx.x * 256 >= a.n) return;  // whole workgroups return together
     unreserve_resp_body(a.reqs, a.resp, a.n, a.seq2slot, a.nseq, a.meta, a.pin, a.rrec, a.anchor, a.mslot, a.ntypes,
-                        blockIdx.x);
+                        blockIdx.x, a.rh);
 }
 
 // Several handles' work as one launch on the first handle's stream (hs[m[0]]):
@@ -1741,7 +1748,7 @@ int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int
     k_unreserve_resp<<<(n + 255) / 256, 256, 0, h->stream>>>(d_reqs18, d_resp12, n, h->d_seq2slot, h->next_wqseqno,
                                                              h->d_meta, h->d_pin, h->d_rrec, h->d_anchor,
                                                              (h->d_mslot && n <= h->cap_req) ? h->d_mslot : nullptr,
-                                                             std::min(h->T, 64));
+                                                             std::min(h->T, 64), unres_rh(h, d_reqs18, n));
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
 }
@@ -1783,7 +1790,7 @@ int adlbq_unreserve_resp_group_device(adlbq_server *const *hs, int n, const int 
             const int c = counts[mm[j]];
             g.a[j] = UnresArgs{d_reqs18[mm[j]], d_resp12[mm[j]], c, h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_pin,
                                h->d_rrec, h->d_anchor, (h->d_mslot && c <= h->cap_req) ? h->d_mslot : nullptr,
-                               std::min(h->T, 64)};
+                               std::min(h->T, 64), unres_rh(h, d_reqs18[mm[j]], c)};
             nb = std::max(nb, (c + 255) / 256);
         }
         adlbq_server *L = hs[mm[0]];
@@ -2330,6 +2337,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (n == "fold_thresholds") {
         if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0, 1 or 2 (auto)");
         h->fold_thresholds = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "fin_flat") {
+        if (value < 0 || value > (1 << 20)) return fail(ADLBQ_ERR_ARG, "fin_flat out of range");
+        h->fin_flat = (int)value;
         return ADLBQ_OK;
     }
     if (n == "group_launch") {
