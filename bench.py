@@ -87,6 +87,8 @@ def parse():
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 stream measurement")
     ap.add_argument("--no-wide", action="store_true", help="skip the more-than-64-types leg")
+    ap.add_argument("--diag-same-batch", action="store_true",
+                    help="diagnostic: every metric step on the same request / response buffers (cache residency)")
     ap.add_argument("--wide-only", action="store_true", help="only the more-than-64-types leg")
     ap.add_argument("--wide-types", type=int, default=100)
     ap.add_argument("--wide-units", type=int, default=200_000)
@@ -984,6 +986,9 @@ def main():
 
     p_req = [d_reqs[b].data_ptr() for b in range(nb)]  # no tensor views inside the timed loop
     p_resp = [d_resp[b].data_ptr() for b in range(nb)]
+    if args.diag_same_batch:  # diagnostic only (never a reported number): every step on batch 0's buffers
+        p_req = [p_req[0]] * nb
+        p_resp = [p_resp[0]] * nb
 
     def step(b):
         srv.reserve_batch_device(R, p_req[b], p_resp[b])
