@@ -119,3 +119,39 @@ def test_group_rejects_bad_arguments(gpu_available):
         with pytest.raises(_lib.AdlbqError):
             ReserveGroup([a]).reserve_device([64], [0], [r.data_ptr()])
         ReserveGroup([a]).reserve_device([0], [0], [0])  # nothing to do
+
+
+def test_group_many_small_shards(gpu_available):
+    """40 small shards in one group (the argument tables outgrow their first
+    allocation; grid.y = 40): every shard's answers equal its own sequential
+    run's, over two batches."""
+    import torch
+    from adlb_amd.server import ReserveGroup, Server
+
+    S, N, R = 40, 2_000, 512
+    specs = [(synth.config3_shard(s, S, N, 4, R, seed=300 + s, prio_hi=32, p_remote=0.1), s) for s in range(S)]
+    exp = [_oracle_resps(w, S, s) for w, s in specs]
+    srvs, d_req, d_resp = [], [], []
+    st = torch.cuda.Stream()
+    try:
+        for w, s in specs:
+            srv = Server(w.user_types, w.num_app_ranks, S, s, max_units=N)
+            srvs.append(srv)
+            srv.set_stream(st.cuda_stream)  # one shared stream, as the bench runs them
+            srv.put_batch(_units(w))
+            reqs = np.concatenate([w.r_rank[:, None], w.r_hang[:, None].astype(np.int32), w.r_types],
+                                  axis=1).astype(np.int32)
+            d_req.append(torch.from_numpy(reqs).cuda())
+            d_resp.append(torch.full((R, 12), -7, dtype=torch.int32, device="cuda"))
+        torch.cuda.synchronize()
+        grp = ReserveGroup(srvs)
+        for lo, hi in ((0, R // 2), (R // 2, R)):
+            grp.reserve_device([hi - lo] * S, [d.data_ptr() + lo * 18 * 4 for d in d_req],
+                               [d.data_ptr() + lo * 12 * 4 for d in d_resp])
+        torch.cuda.synchronize()
+        for j, (w, s) in enumerate(specs):
+            assert np.array_equal(d_resp[j].cpu().numpy()[:, :10], exp[j][:, :10]), f"shard {s}"
+    finally:
+        torch.cuda.synchronize()
+        for srv in srvs:
+            srv.close()
