@@ -688,6 +688,11 @@ struct adlbq_steal_group {
     int *d_own = nullptr;       // the local blob when the caller passes none
     int *d_last = nullptr;      // where the last export went
     int *h_all = nullptr;       // pinned copy of the gathered blobs
+    // one process: the export written straight into mapped pinned memory (no copy before the merge)
+    int *h_map = nullptr, *d_map = nullptr;
+    long long cap_map = 0;
+    bool last_mapped = false;
+    int zero_copy = 1;          // ADLBQ_STEAL_ZERO_COPY=0: device blob + one copy (A/B runs)
     long long cap_h = 0;
     std::vector<hipEvent_t> ev;
     std::vector<int> reqs, out3, resp;  // merge scratch; resp [m][15] of the last settle
@@ -716,6 +721,7 @@ int adlbq_steal_group_create(adlbq_steal_group **out, adlbq_server **shards, int
     for (int j = 0; j < n; j++) shards[j]->export_extra = std::max(shards[j]->export_extra, k);
     g->n = n, g->k = k, g->T = shards[0]->T, g->rqcap = rqcap;
     if (const char *e = std::getenv("ADLBQ_STEAL_GROUP_LAUNCH")) g->group_launch = std::atoi(e) != 0;  // A/B runs
+    if (const char *e = std::getenv("ADLBQ_STEAL_ZERO_COPY")) g->zero_copy = std::atoi(e) != 0;
     const long long T = g->T;
     g->off_recs = 2;                                  // [0] shard index, [1] pad
     g->off_nrec = g->off_recs + T * k * 8;            // launch_export writes nrec right after the records
@@ -738,7 +744,20 @@ long long adlbq_steal_group_blob_ints(adlbq_steal_group *g) { return g ? g->blob
 int adlbq_steal_group_export(adlbq_steal_group *g, int *d_blob) {
     if (!g) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_export");
     hipSetDevice(g->sh[0]->device);
-    if (!d_blob) {
+    g->last_mapped = false;
+    if (!d_blob && g->zero_copy) {  // the merge reads the kernels' stores where they landed
+        const long long need = g->blob * g->n;
+        if (need > g->cap_map) {
+            for (auto *h : g->sh) AQ_HIP(hipStreamSynchronize(h->stream));
+            if (g->h_map) AQ_HIP(hipHostFree(g->h_map));
+            g->h_map = g->d_map = nullptr;
+            AQ_HIP(hipHostMalloc((void **)&g->h_map, sizeof(int) * need, hipHostMallocMapped));
+            AQ_HIP(hipHostGetDevicePointer((void **)&g->d_map, g->h_map, 0));
+            g->cap_map = need;
+        }
+        d_blob = g->d_map;
+        g->last_mapped = true;
+    } else if (!d_blob) {
         if (!g->d_own) AQ_HIP(hipMalloc((void **)&g->d_own, sizeof(int) * g->blob * g->n));
         d_blob = g->d_own;
     }
@@ -810,7 +829,7 @@ static int group_host_cap(adlbq_steal_group *g, long long total) {
     return ADLBQ_OK;
 }
 
-static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, int *n_settled,
+static int group_settle_staged(adlbq_steal_group *g, const int *all, int nproc, int *n_decided, int *n_settled,
                                std::chrono::steady_clock::time_point t0, std::chrono::steady_clock::time_point t1);
 
 extern "C" {
@@ -819,18 +838,24 @@ int adlbq_steal_group_settle(adlbq_steal_group *g, const int *d_all, int nproc, 
     if (!g || nproc < 1 || (nproc > 1 && !d_all)) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle");
     adlbq_server *h0 = g->sh[0];
     hipSetDevice(h0->device);
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    if (!d_all && nproc == 1 && g->last_mapped) {  // the export landed in mapped memory: no copy
+        for (int j = 0; j < g->n; j++)
+            if (g->sh[(size_t)j]->stream != h0->stream) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
+        AQ_HIP(hipStreamSynchronize(h0->stream));
+        return group_settle_staged(g, g->h_map, 1, n_decided, n_settled, t0, clk::now());
+    }
     if (!d_all) d_all = g->d_last;
     if (!d_all) return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle: no export");
     const long long total = g->blob * g->n * nproc;
     int rc;
     if ((rc = group_host_cap(g, total))) return rc;
-    using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
     for (int j = 0; j < g->n; j++)  // shards on the first shard's stream are ordered already (no event)
         if (g->sh[(size_t)j]->stream != h0->stream) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
     AQ_HIP(hipMemcpyAsync(g->h_all, d_all, sizeof(int) * total, hipMemcpyDeviceToHost, h0->stream));
     AQ_HIP(hipStreamSynchronize(h0->stream));
-    return group_settle_staged(g, nproc, n_decided, n_settled, t0, clk::now());
+    return group_settle_staged(g, g->h_all, nproc, n_decided, n_settled, t0, clk::now());
 }
 
 int adlbq_steal_group_export_host(adlbq_steal_group *g, int *h_blob) {
@@ -840,6 +865,11 @@ int adlbq_steal_group_export_host(adlbq_steal_group *g, int *h_blob) {
     adlbq_server *h0 = g->sh[0];
     for (int j = 0; j < g->n; j++)  // shards on the first shard's stream are ordered already (no event)
         if (g->sh[(size_t)j]->stream != h0->stream) AQ_HIP(hipStreamWaitEvent(h0->stream, g->ev[(size_t)j], 0));
+    if (g->last_mapped) {  // already in host memory
+        AQ_HIP(hipStreamSynchronize(h0->stream));
+        std::memcpy(h_blob, g->h_map, sizeof(int) * g->blob * g->n);
+        return ADLBQ_OK;
+    }
     AQ_HIP(hipMemcpyAsync(h_blob, g->d_last, sizeof(int) * g->blob * g->n, hipMemcpyDeviceToHost, h0->stream));
     AQ_HIP(hipStreamSynchronize(h0->stream));
     return ADLBQ_OK;
@@ -854,7 +884,7 @@ int adlbq_steal_group_settle_host(adlbq_steal_group *g, const int *h_all, int np
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     std::memcpy(g->h_all, h_all, sizeof(int) * total);
-    return group_settle_staged(g, nproc, n_decided, n_settled, t0, clk::now());
+    return group_settle_staged(g, g->h_all, nproc, n_decided, n_settled, t0, clk::now());
 }
 
 }  // extern "C"
@@ -877,8 +907,8 @@ static int group_join_streams(adlbq_steal_group *g) {
     return ADLBQ_OK;
 }
 
-// The merge and the local side of it over g->h_all = [nproc][n][blob] (any region order).
-static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, int *n_settled,
+// The merge and the local side of it over all = [nproc][n][blob] (any region order).
+static int group_settle_staged(adlbq_steal_group *g, const int *all, int nproc, int *n_decided, int *n_settled,
                                std::chrono::steady_clock::time_point t0, std::chrono::steady_clock::time_point t1) {
     using clk = std::chrono::steady_clock;
     adlbq_server *h0 = g->sh[0];
@@ -890,7 +920,7 @@ static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, 
     // regions in shard order (regions may come in any order) give it directly
     std::vector<int> reg_of((size_t)S, -1);
     for (int r = 0; r < nreg; r++) {
-        const int *b = g->h_all + (size_t)r * g->blob;
+        const int *b = all + (size_t)r * g->blob;
         const int idx = b[0];
         if (idx < 0 || idx >= S || reg_of[(size_t)idx] >= 0)
             return fail(ADLBQ_ERR_ARG, "adlbq_steal_group_settle: bad or repeated shard index");
@@ -900,7 +930,7 @@ static int group_settle_staged(adlbq_steal_group *g, int nproc, int *n_decided, 
     g->reqs.clear();
     for (int idx = 0; idx < S; idx++) {
         if (reg_of[(size_t)idx] < 0) continue;
-        const int *rq = g->h_all + (size_t)reg_of[(size_t)idx] * g->blob + g->off_rq;
+        const int *rq = all + (size_t)reg_of[(size_t)idx] * g->blob + g->off_rq;
         const int c = std::min(rq[0], g->rqcap);  // entries past rqcap wait for the next round
         const size_t o = g->reqs.size();
         g->reqs.resize(o + 19 * (size_t)c);
@@ -1104,6 +1134,7 @@ int adlbq_steal_group_destroy(adlbq_steal_group *g) {
     for (auto &e : g->ev) hipEventDestroy(e);
     if (g->d_own) hipFree(g->d_own);
     if (g->h_all) hipHostFree(g->h_all);
+    if (g->h_map) hipHostFree(g->h_map);
     if (g->h_unr) hipHostFree(g->h_unr);
     if (g->d_unr) hipFree(g->d_unr);
     if (g->h_app) hipHostFree(g->h_app);
