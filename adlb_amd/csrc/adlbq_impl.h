@@ -77,7 +77,7 @@ struct DevCounters {
     int plan_phi;          // highest bit of the prio field any candidate list varies in (-1: none)
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
     int rank_covered;      // ... and every type had candidates: the next batch may skip k_rank (fuse_rank)
-    int pad0;
+    int kr_fail;           // batches whose keyrank failed over to k_rank (cumulative)
     int batch_failed;      // batches answered ADLB_ERROR because an in-launch candidate sort gave up (cumulative)
     int rq_next;           // rqseqnos handed out (next_rqseqno - 1, adlb.c:1244)
     int rq_reclaims;       // k_rq_reclaim compactions (cumulative)
@@ -351,6 +351,11 @@ struct adlbq_server {
     size_t cap_gtab = 0;
     int gtab_slot = 0;
     std::vector<hipEvent_t> gjoin;     // one per grouped handle: its stream joins the launch stream
+    // keyrank (adlbq_keyrank.hip): 8 < T <= 64, the candidates binned and ranked in one global order
+    char *d_kr = nullptr; long long cap_kr = 0;
+    int keyrank = 1;                   // "keyrank": 0 = the per-list sort + k_rank
+    int kr_bin_max = 1024;             // "keyrank_bin_max": a larger digit bin fails the batch over to k_rank
+    long long n_keyrank = 0, kr_fail_seen = 0, kr_skip_until = 0;
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]
@@ -415,7 +420,9 @@ void stage_end(adlbq_server *h, const char *name, hipEvent_t ev);
 void host_stage_add(adlbq_server *h, const char *name, std::chrono::steady_clock::time_point t0);
 int launch_reserve(adlbq_server *h, int n, const int *d_reqs, int *d_resp);
 int sync_batch_counters(adlbq_server *h);  // synchronise; h->ctr from the last batch's landed snapshot
-int wide_choose(adlbq_server *h, int R, const int *d_reqs);  // T > ADLBQ_MAX_TYPES: the batch's choices
+int wide_choose(adlbq_server *h, int R, const int *d_reqs);
+int launch_keyrank(adlbq_server *h, int R);  // 8 < T <= 64: lists sorted and ranked (k_kr_*)
+bool keyrank_hint(adlbq_server *h);         // no failed keyrank landed recently  // T > ADLBQ_MAX_TYPES: the batch's choices
 int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12);  // k_unreserve_resp
 int group_join(adlbq_server *const *hs, const std::vector<int> &m);     // hs[m[0]]'s stream waits for the members'
 int group_release(adlbq_server *const *hs, const std::vector<int> &m);  // the members' streams wait for hs[m[0]]'s

@@ -4960,7 +4960,14 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_end(h, "targeted", ev);
     }
     auto st0 = hclk::now();
-    if (np > 0 && T > 0 && sort_hint(h)) {
+    // 8 < T <= 64: every list sorted and ranked by one binning of the keys (k_rank's tile work skipped)
+    const bool kr = np > 0 && T > RANK_FAST_T && T <= ADLBQ_MAX_TYPES && h->keyrank && keyrank_hint(h);
+    if (kr) {
+        if ((rc = leave_group())) return rc;
+        stage_begin(h, "sort", &ev);
+        if ((rc = launch_keyrank(h, R))) return rc;
+        stage_end(h, "sort", ev);
+    } else if (np > 0 && T > 0 && sort_hint(h)) {
         if ((rc = leave_group())) return rc;
         stage_begin(h, "sort", &ev);
         bool planned = false;
@@ -4992,7 +4999,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             // demand plus the export depth per type): 1,280 workgroups cost ~20 us on small lists
             const long long tiles = ((long long)R * std::min(T, NREQ) + (long long)T * h->export_extra + RANK_TILE - 1) /
                                     RANK_TILE;
-            const int rgrid = h->rank_grid ? h->rank_grid : rank_hint(h) ? 4 : (int)std::min(1280ll, std::max(8ll, tiles));
+            // (keyrank: k_rank's tiles run only when the batch failed over)
+            const int rgrid = h->rank_grid ? h->rank_grid
+                              : kr           ? 64
+                              : (T <= RANK_FAST_T && rank_hint(h)) ? 4
+                                                                    : (int)std::min(1280ll, std::max(8ll, tiles));
             if (h->grec) {
                 h->grec->kinds |= GK_RANK;
                 h->grec->rank = GRank{rka, rgrid};

@@ -122,6 +122,16 @@ bool rank_skip_hint(adlbq_server *h) {
     return i >= 0 && h->h_snap[i].rank_covered == 1;
 }
 
+// keyrank unless a landed batch failed it over lately (then 64 batches on the sort + k_rank path)
+bool keyrank_hint(adlbq_server *h) {
+    const int i = newest_landed(h);
+    if (i >= 0 && h->h_snap[i].kr_fail > h->kr_fail_seen) {
+        h->kr_fail_seen = h->h_snap[i].kr_fail;
+        h->kr_skip_until = h->reserve_batches + 64;
+    }
+    return h->reserve_batches >= h->kr_skip_until;
+}
+
 bool sort_hint(adlbq_server *h) {
     const int i = newest_landed(h);
     // nothing landed yet (the first batches): sort whatever needs it through the
@@ -1400,7 +1410,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
                     h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg,
                     h->d_mslot, h->d_fold, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
-                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp};
+                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -2339,6 +2349,16 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->fold_thresholds = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "keyrank") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "keyrank must be 0 or 1");
+        h->keyrank = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "keyrank_bin_max") {
+        if (value < 0 || value > (1 << 24)) return fail(ADLBQ_ERR_ARG, "keyrank_bin_max out of range");
+        h->kr_bin_max = (int)value;
+        return ADLBQ_OK;
+    }
     if (n == "fin_flat") {
         if (value < 0 || value > (1 << 20)) return fail(ADLBQ_ERR_ARG, "fin_flat out of range");
         h->fin_flat = (int)value;
@@ -2441,6 +2461,11 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n.rfind("host_ns:", 0) == 0) {  // host time issuing a profiled stage (adlbq_profile_only)
         auto it = h->timers.find(n.substr(8));
         return it == h->timers.end() ? 0 : it->second.host_ns;
+    }
+    if (n == "keyrank") return h->n_keyrank;               // batches ranked by keyrank (cumulative)
+    if (n == "keyrank_failed") {                             // ... that failed over to k_rank, as of the newest landed batch
+        refresh_counters(h);
+        return h->ctr.kr_fail;
     }
     if (n == "sort_radix") return h->n_sort_radix;         // planned sorts issued as the list-stable radix sort
     if (n == "sort_async") return h->n_sort_async;         // merged sorts planned from the last landed batch (cumulative)

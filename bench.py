@@ -871,7 +871,8 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "targeted_index": {"merges": srv.stat("tindex_merges"), "rebuilds": srv.stat("tindex_rebuilds")},
         "candidate_sort": {"planned": srv.stat("sort_async"), "planned_radix": srv.stat("sort_radix"),
                            "plan_missed": srv.stat("sort_async_bad"),
-                           "device_sorted_lists": srv.stat("device_sorted_lists")},
+                           "device_sorted_lists": srv.stat("device_sorted_lists"),
+                           "keyrank": srv.stat("keyrank"), "keyrank_failed": srv.stat("keyrank_failed")},
         "value": matched / el if par["parity"] else None,
         **par,
         "unit": "assignments/s",

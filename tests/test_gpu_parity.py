@@ -34,7 +34,8 @@ def run_abi(ut, cfg, trace, max_units=1 << 16, params=None, stats=None):
         assert s.stat("sort_timeouts") == 0, "k_rank timed out waiting for an in-launch sort"
         if stats is not None:
             stats.update({k: s.stat(k) for k in ("chain_passes", "chain_recomputed", "chain_fallback",
-                                                 "chain_timeouts", "spec_lists", "rank_fast")})
+                                                 "chain_timeouts", "spec_lists", "rank_fast", "keyrank",
+                                                 "keyrank_failed")})
         return out
 
 
@@ -83,6 +84,10 @@ CASES = {
     "w150_c4": lambda: synth.config4(n_units=50_000, n_types=150, n_reserves=4096, n_ranks=128, seed=241,
                                      prio_hi=512),
     "w255_exhaust": lambda: synth.config2(n_units=4_000, n_types=255, n_reserves=6000, seed=242, prio_hi=8),
+    # 8 < T <= 64 (keyrank): keys varying only in the bucket position, and over the whole int32 range
+    "c2_t16_eq": lambda: synth.config2(n_units=100_000, n_types=16, n_reserves=8192, seed=233, equal_prio=True),
+    "c2_t32_extreme": lambda: synth.config2(n_units=100_000, n_types=32, n_reserves=8192, seed=234, wide_frac=0.05,
+                                            wide_range=(-(1 << 31), (1 << 31) - 1)),
     # a type with no unit at all (config 3's shards): the guess counts are adjusted first
     "c3_shard_missing_type": lambda: synth.config3_shard(1, 64, 80_000, 4, 8192, seed=232),
 }
@@ -129,8 +134,38 @@ def test_rank_small_grid_sorts_every_list(gpu_available, name, grid):
     w = CASES[name]()
     tr = synth.workload_trace(w)
     cfg = (w.num_app_ranks, 1, 0)
-    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units, params={"rank_grid": grid, "segsort_wide": 1 << 30})
+    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units,
+                  params={"rank_grid": grid, "segsort_wide": 1 << 30, "keyrank": 0})
     assert_same(got, run_oracle(w.user_types, cfg, tr))
+
+
+KEYRANK_MODES = {
+    "on": {},
+    "off": {"keyrank": 0},            # per-list sort + k_rank's searches
+    "failover": {"keyrank_bin_max": 0},  # every binning fails over: k_rank sorts and ranks in its launch
+}
+
+
+@pytest.mark.parametrize("name", ["c4_n200k", "c2_t64_wide", "c2_t16_eq", "c2_t32_extreme"])
+@pytest.mark.parametrize("mode", sorted(KEYRANK_MODES))
+def test_keyrank_vs_oracle(gpu_available, name, mode):
+    """8 < T <= 64: the lists sorted and ranked by one binning of the keys
+    (adlbq_keyrank.hip), the sort + k_rank path, and a binning that fails over
+    to k_rank inside the batch all give the sequential result."""
+    w = CASES[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    st = {}
+    got = run_abi(w.user_types, cfg, tr, max_units=w.n_units, params=KEYRANK_MODES[mode], stats=st)
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
+    if mode == "on":
+        # c2_t32_extreme: a few prios at the ends of the int32 range put the bulk of the keys
+        # into one digit bin, so its first batch fails over (by design) and later ones skip keyrank
+        assert st["keyrank"] >= 1 and (st["keyrank_failed"] == 0 or name == "c2_t32_extreme"), st
+    elif mode == "off":
+        assert st["keyrank"] == 0, st
+    else:
+        assert st["keyrank_failed"] >= 1, st
 
 
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
@@ -263,7 +298,8 @@ def _exact_full(w, batches=1, stats=None, params=()):
                 s.unreserve_batch_device(m.size, trip.data_ptr())
                 s.sync()
         if stats is not None:
-            for k in ("device_sorted_lists", "sort_timeouts", "sort_radix", "sort_async_bad"):
+            for k in ("device_sorted_lists", "sort_timeouts", "sort_radix", "sort_async_bad", "keyrank",
+                      "keyrank_failed"):
                 stats[k] = s.stat(k)
         return first
 
@@ -295,7 +331,8 @@ def test_config4_2m_exact(gpu_available, merged, wide, rounds, radix):
     w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
     stats = {}
     _exact_full(w, batches=4, stats=stats, params=[("segsort_merged", merged), ("segsort_wide", wide),
-                                                       ("chain_rounds", rounds), ("segsort_radix", radix)])
+                                                       ("chain_rounds", rounds), ("segsort_radix", radix),
+                                                       ("keyrank", 0)])
     if merged or wide == 256:
         assert stats["device_sorted_lists"] > 0, "the device-wide list sort did not run"
     if merged and radix:
@@ -303,13 +340,30 @@ def test_config4_2m_exact(gpu_available, merged, wide, rounds, radix):
     assert stats["sort_timeouts"] == 0
 
 
+@pytest.mark.parametrize("rounds", [-1, 0])
+def test_config4_2m_keyrank_exact(gpu_available, rounds):
+    """Four config-4 batches (32 types, thresholds in multi-prio bins) through
+    keyrank: every batch binned and ranked without a failover."""
+    w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
+    stats = {}
+    _exact_full(w, batches=4, stats=stats, params=[("chain_rounds", rounds)])
+    assert stats["keyrank"] == 4 and stats["keyrank_failed"] == 0 and stats["sort_timeouts"] == 0, stats
+
+
 def test_full_size_config4_exact(gpu_available):
     """Config 4 at its BASELINE size (10M units, 80% targeted over 1024 ranks,
-    32 Zipf types, 65,536 Reserves of 1-4 types): two batches, the second with
-    the candidate lists sorted before the rank pass."""
+    32 Zipf types, 65,536 Reserves of 1-4 types): three batches through keyrank."""
     w = synth.config4(n_units=10_000_000, n_reserves=65_536, n_ranks=1024, seed=10)
     stats = {}
     _exact_full(w, batches=3, stats=stats)
+    assert stats["sort_timeouts"] == 0 and stats["keyrank"] >= 3 and stats["keyrank_failed"] == 0, stats
+
+
+def test_full_size_config4_sort_path_exact(gpu_available):
+    """The same through the per-list sort + k_rank path (keyrank off)."""
+    w = synth.config4(n_units=10_000_000, n_reserves=65_536, n_ranks=1024, seed=10)
+    stats = {}
+    _exact_full(w, batches=3, stats=stats, params=[("keyrank", 0)])
     assert stats["sort_timeouts"] == 0 and stats["sort_radix"] >= 1, stats
 
 
