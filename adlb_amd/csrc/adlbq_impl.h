@@ -356,6 +356,7 @@ struct adlbq_server {
     int keyrank = 1;                   // "keyrank": 0 = the per-list sort + k_rank
     int kr_bin_max = 1024;             // "keyrank_bin_max": a larger digit bin fails the batch over to k_rank
     long long n_keyrank = 0, kr_fail_seen = 0, kr_skip_until = 0;
+    int kr_par = 0;                    // parity of keyrank's chunk-count rows
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]
