@@ -78,6 +78,8 @@ struct DevCounters {
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
     int rank_covered;      // ... and every type had candidates: the next batch may skip k_rank (fuse_rank)
     int kr_fail;           // batches whose keyrank failed over to k_rank (cumulative)
+    int kr_why;            // the last keyrank failover: 1 more candidates than its buffers, 2 a bin over kr_bin_max
+    int kr_maxbin;         // the largest digit bin of the last keyrank batch (diagnostic)
     int batch_failed;      // batches answered ADLB_ERROR because an in-launch candidate sort gave up (cumulative)
     int rq_next;           // rqseqnos handed out (next_rqseqno - 1, adlb.c:1244)
     int rq_reclaims;       // k_rq_reclaim compactions (cumulative)
@@ -356,6 +358,8 @@ struct adlbq_server {
     int keyrank = 1;                   // "keyrank": 0 = the per-list sort + k_rank
     int kr_bin_max = 1024;             // "keyrank_bin_max": a larger digit bin fails the batch over to k_rank
     long long n_keyrank = 0, kr_fail_seen = 0, kr_skip_until = 0;
+    int *d_arrive = nullptr; long long cap_arrive = 0;  // pass 1: pages of each chunk counted (hist_arrive)
+    int hist_arrive = 1;               // "hist_arrive": a chunk's last page sums its chunk (0: an atomic per column)
     int kr_par = 0;                    // parity of keyrank's chunk-count rows
     int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror

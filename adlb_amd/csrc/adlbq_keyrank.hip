@@ -41,7 +41,8 @@ namespace adlbq {
 
 constexpr int KR_BINS = 1 << 16, KR_CHUNK = 1024, KR_TY = 64;  // KR_TY: count row stride (T <= 64)
 constexpr int KR_COARSE = KR_BINS / 256;                        // 256 groups of 256 bins (k_kr_scan's workgroups)
-constexpr int KR_RANK_PER = 1024;                               // positions per k_kr_rank workgroup
+constexpr int KR_RANK_PER = 256;                                // positions per k_kr_rank workgroup (one per thread)
+constexpr int KR_SLACK = 256;                                   // ... and keys staged on either side
 
 struct KrArgs {
     int T;
@@ -120,15 +121,35 @@ __global__ __launch_bounds__(256) void k_kr_hist(KrArgs a) {
         a.flag[0] = G > a.cap ? 1 : 0;
         a.ctr->plan_g = G;     // sizes the next batch's buffers
         a.ctr->rank_fast = 0;  // k_kr_write sets it once the ranks are in
+        a.ctr->kr_maxbin = 0;
     }
     if (G > a.cap) return;
     const KrDigit s = kr_shape(a);
     lc[tid] = 0;
     __syncthreads();
-    for (int i = blockIdx.x * blockDim.x + tid; i < G; i += gridDim.x * blockDim.x) {
-        const int d = kr_digit(a.ckey[i], s);
-        a.tslot[i] = atomicAdd(&a.bins[d], 1);
-        atomicAdd(&lc[d >> 8], 1);
+    const int lane = tid & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    // consecutive candidates of a list mostly share a digit: one atomic per distinct digit of a
+    // wave (its lanes' places follow the leader's), as many LDS adds for the group counts
+    for (int i0 = blockIdx.x * blockDim.x; i0 < G; i0 += gridDim.x * blockDim.x) {
+        const int i = i0 + tid;
+        const bool valid = i < G;
+        const int d = valid ? kr_digit(a.ckey[i], s) : 0;
+        unsigned long long pe = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            const unsigned long long bb = __ballot((d >> b) & 1);
+            pe &= ((d >> b) & 1) ? bb : ~bb;
+        }
+        const bool lead = valid && (pe & lt) == 0ull;
+        int base = 0;
+        if (lead) {
+            const int n = __popcll(pe);
+            base = atomicAdd(&a.bins[d], n);
+            atomicAdd(&lc[d >> 8], n);
+        }
+        base = __shfl(base, valid ? __ffsll((long long)pe) - 1 : 0, 64);
+        if (valid) a.tslot[i] = base + __popcll(pe & lt);
     }
     __syncthreads();
     if (lc[tid]) atomicAdd(&a.coarse[tid], lc[tid]);
@@ -141,14 +162,16 @@ __global__ __launch_bounds__(256) void k_kr_scan(KrArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = blockIdx.x;
     int base = tid < g ? a.coarse[tid] : 0;
     const int c = a.bins[g * 256 + tid];
-    if (c > a.bin_max) a.flag[0] = 1;  // every later launch returns at once; k_kr_write still cleans up
-    int x = c;
+    if (c > a.bin_max) a.flag[0] = 2;  // every later launch returns at once; k_kr_write still cleans up
+    int x = c, mx = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const int y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
         base += __shfl_xor(base, o, 64);
+        mx = max(mx, __shfl_xor(mx, o, 64));
     }
+    if (lane == 0 && mx > 0) atomicMax(&a.ctr->kr_maxbin, mx);
     __shared__ int bsum[4];
     if (lane == 63) wsum[w] = x;
     if (lane == 0) bsum[w] = base;
@@ -174,6 +197,7 @@ __global__ __launch_bounds__(256) void k_kr_scatter(KrArgs a) {
 // the (chunk, type) counts of chunks c0 - 1 .. c0 + 2 are gathered in LDS first
 __global__ __launch_bounds__(256) void k_kr_rank(KrArgs a) {
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], lc[4][KR_TY];
+    __shared__ unsigned long long skey[KR_RANK_PER + 2 * KR_SLACK];
     if (a.flag[0]) return;
     const int T = a.T, tid = threadIdx.x;
     if (tid <= T) soff[tid] = a.candoff[tid];
@@ -182,12 +206,23 @@ __global__ __launch_bounds__(256) void k_kr_rank(KrArgs a) {
     const int G = soff[T];
     const int c0 = (blockIdx.x * KR_RANK_PER) / KR_CHUNK - 1;
     for (int p0 = blockIdx.x * KR_RANK_PER; p0 < G; p0 += gridDim.x * KR_RANK_PER) {
+        // the keys of positions [p0 - KR_SLACK, p0 + KR_RANK_PER + KR_SLACK) in LDS: the bins of
+        // the block's positions, unless one reaches further
+        const int l0 = p0 - KR_SLACK, l1 = min(G, p0 + KR_RANK_PER + KR_SLACK);
+        __syncthreads();
+        for (int q = max(0, l0) + tid; q < l1; q += 256) skey[q - l0] = a.tkey[q];
+        __syncthreads();
         for (int p = p0 + tid; p < min(G, p0 + KR_RANK_PER); p += 256) {
-            const unsigned long long k = a.tkey[p];
+            const unsigned long long k = skey[p - l0];
             const int d = kr_digit(k, s);
             const int bs = a.bins[d], be = d == KR_BINS - 1 ? G : a.bins[d + 1];
             int r = bs;
-            for (int q = bs; q < be; q++) r += a.tkey[q] > k ? 1 : 0;
+            if (bs >= l0 && be <= l1) {
+#pragma unroll 4
+                for (int q = bs; q < be; q++) r += skey[q - l0] > k ? 1 : 0;
+            } else {
+                for (int q = bs; q < be; q++) r += a.tkey[q] > k ? 1 : 0;
+            }
             const int i = a.tidx[p];
             int lo = 0, hi = T - 1;  // the last list starting at or before i
             while (lo < hi) {
@@ -219,7 +254,10 @@ __global__ __launch_bounds__(KR_CHUNK) void k_kr_write(KrArgs a) {
     for (long long k = gt; k < a.nccnt; k += gs) a.ccnt_next[k] = 0;
     const bool failed = a.flag[0] != 0;
     if (blockIdx.x == 0 && tid == 0) {
-        if (failed) a.ctr->kr_fail += 1;
+        if (failed) {
+            a.ctr->kr_fail += 1;
+            a.ctr->kr_why = a.flag[0];
+        }
         else a.ctr->rank_fast = 1;  // k_rank: the ranks are in, only its bookkeeping is left
     }
     if (failed) return;
@@ -233,6 +271,7 @@ __global__ __launch_bounds__(KR_CHUNK) void k_kr_write(KrArgs a) {
     for (int c = blockIdx.x; c < nch; c += gridDim.x) {
         {  // per type: candidates of the earlier chunks (thread = type lane x 16 parts)
             int sum = 0;
+#pragma unroll 8
             for (int q = w; q < c; q += 16) sum += a.ccnt[(long long)q * KR_TY + lane];
             spre[w][lane] = sum;
             wcnt[w][lane] = 0;

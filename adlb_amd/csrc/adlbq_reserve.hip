@@ -184,6 +184,8 @@ struct HistArgs {
     int zper;                  // (unused: k_thresholds zeroes the other buffer)
     int variant;               // "hist_variant": 0 the round-2 loop, 1 the rebased one
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
+    int *arrive;               // [chunks] pages of the chunk counted so far (its last page sums the chunk), or
+                               // nullptr: every page adds its row to the chunk sums with atomics
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -315,14 +317,63 @@ __device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const
         if (k * 64 + lane < nl) sp[k * 64 + lane] = wl[k * 64 + lane];
     if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     if (!(a.diag & 2)) {
-        unsigned int *cs = a.csum + (long long)(p / CHUNK) * C;
+        const int ck = p / CHUNK;
+        unsigned int *cs = a.csum + (long long)ck * C;
         unsigned short *g = a.gh + (long long)p * C;
-        for (int c = threadIdx.x; c < C; c += blockDim.x) {
-            unsigned int v = 0;
+        if (a.arrive == nullptr) {
+            for (int c = threadIdx.x; c < C; c += blockDim.x) {
+                unsigned int v = 0;
 #pragma unroll
-            for (int k = 0; k < HK; k++) v += hist[c * HK + k];
-            g[c] = (unsigned short)v;
-            if (v) atomicAdd(&cs[c], v);
+                for (int k = 0; k < HK; k++) v += hist[c * HK + k];
+                g[c] = (unsigned short)v;
+                if (v) atomicAdd(&cs[c], v);
+            }
+        } else {
+            // The row goes out written through (agent-scope stores, two columns a word), and the
+            // chunk's last page to arrive sums the chunk's rows into its chunk sums with agent-scope
+            // loads (another XCD's L2 may hold stale lines of those rows): one atomic per page
+            // instead of one per non-zero column (~500 per page at 32 types)
+            unsigned int *g32 = reinterpret_cast<unsigned int *>(g);  // C is even (NB = 64)
+            for (int c2 = threadIdx.x; c2 < C / 2; c2 += blockDim.x) {
+                unsigned int v0 = 0, v1 = 0;
+#pragma unroll
+                for (int k = 0; k < HK; k++) {
+                    v0 += hist[(2 * c2) * HK + k];
+                    v1 += hist[(2 * c2 + 1) * HK + k];
+                }
+                __hip_atomic_store(g32 + c2, (v1 << 16) | (v0 & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __shared__ int s_last;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const int n = min(CHUNK, a.npages - ck * CHUNK);
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                const int old = __hip_atomic_fetch_add(a.arrive + ck, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_last = old == n - 1;
+                if (old == n - 1) __hip_atomic_store(a.arrive + ck, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            if (s_last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                const unsigned int *r32 = reinterpret_cast<const unsigned int *>(a.gh + (long long)ck * CHUNK * C);
+                for (int c2 = threadIdx.x; c2 < C / 2; c2 += blockDim.x) {
+                    unsigned int w[CHUNK];
+#pragma unroll
+                    for (int q = 0; q < CHUNK; q++)
+                        w[q] = q < n ? __hip_atomic_load(r32 + (long long)q * (C / 2) + c2, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0u;
+                    unsigned int v0 = 0, v1 = 0;
+#pragma unroll
+                    for (int q = 0; q < CHUNK; q++) {
+                        v0 += w[q] & 0xffffu;
+                        v1 += w[q] >> 16;
+                    }
+                    __hip_atomic_store(cs + 2 * c2, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(cs + 2 * c2 + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
     }
 }
@@ -3758,6 +3809,12 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         AQ_HIP(hipMalloc((void **)&h->d_gh, sizeof(unsigned short) * h->cap_gh));
 
     }
+    if (nchunks + 1 > h->cap_arrive) {  // pass 1's per-chunk arrival counters (each chunk's last page resets its own)
+        if (h->d_arrive) AQ_HIP(hipFree(h->d_arrive));
+        h->cap_arrive = std::max(nchunks + 1, 2 * h->cap_arrive);
+        AQ_HIP(hipMalloc((void **)&h->d_arrive, sizeof(int) * h->cap_arrive));
+        AQ_HIP(hipMemsetAsync(h->d_arrive, 0, sizeof(int) * h->cap_arrive, h->stream));
+    }
     if (need_cs > h->cap_csum) {
         if (h->d_csum) AQ_HIP(hipFree(h->d_csum));
         h->cap_csum = std::max(need_cs, 2 * h->cap_csum);
@@ -3811,6 +3868,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         h->csum_used[par ^ 1] = 0;
         h->csum_par = par ^ 1;
     }
+    ha.arrive = h->hist_arrive ? h->d_arrive : nullptr;
     const int ppb = 1;  // pages per pass-1 workgroup
     const int npb = (np + ppb - 1) / ppb;
     ha.zper = npb > 0 ? (int)((ha.zn + npb - 1) / npb) : 0;
@@ -4349,6 +4407,8 @@ static int launch_segsort_planned(adlbq_server *h, bool *done) {
         AQ_HIP(hipMalloc((void **)&h->d_cslot3, sizeof(int) * h->cap_c3));
     }
     if (!h->d_plan) AQ_HIP(hipMalloc((void **)&h->d_plan, sizeof(int) * 4));
+    // (a plan can land from a keyrank batch that failed over, before any read-back sort allocated this)
+    if (!h->d_kb) AQ_HIP(hipMalloc((void **)&h->d_kb, sizeof(unsigned long long) * 2 * ADLBQ_MAX_TYPES));
     const int kgx = 16;
     AQ_HIP(hipMemsetAsync(h->d_kb, 0, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
     AQ_HIP(hipMemsetAsync(h->d_kb + ADLBQ_MAX_TYPES, 0xff, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));

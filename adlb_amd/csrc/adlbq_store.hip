@@ -1410,7 +1410,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
                     h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg,
                     h->d_mslot, h->d_fold, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
-                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr};
+                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr, h->d_arrive};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -2349,6 +2349,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->fold_thresholds = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "hist_arrive") {
+        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "hist_arrive must be 0 or 1");
+        h->hist_arrive = (int)value;
+        return ADLBQ_OK;
+    }
     if (n == "keyrank") {
         if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "keyrank must be 0 or 1");
         h->keyrank = (int)value;
@@ -2466,6 +2471,10 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n == "keyrank_failed") {                             // ... that failed over to k_rank, as of the newest landed batch
         refresh_counters(h);
         return h->ctr.kr_fail;
+    }
+    if (n == "keyrank_why" || n == "keyrank_maxbin") {  // the last failover's reason; the last batch's largest bin
+        refresh_counters(h);
+        return n == "keyrank_why" ? h->ctr.kr_why : h->ctr.kr_maxbin;
     }
     if (n == "sort_radix") return h->n_sort_radix;         // planned sorts issued as the list-stable radix sort
     if (n == "sort_async") return h->n_sort_async;         // merged sorts planned from the last landed batch (cumulative)

@@ -872,7 +872,9 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
         "candidate_sort": {"planned": srv.stat("sort_async"), "planned_radix": srv.stat("sort_radix"),
                            "plan_missed": srv.stat("sort_async_bad"),
                            "device_sorted_lists": srv.stat("device_sorted_lists"),
-                           "keyrank": srv.stat("keyrank"), "keyrank_failed": srv.stat("keyrank_failed")},
+                           "keyrank": srv.stat("keyrank"), "keyrank_failed": srv.stat("keyrank_failed"),
+                           "keyrank_why": srv.stat("keyrank_why"), "keyrank_maxbin": srv.stat("keyrank_maxbin"),
+                           "candidates": srv.stat("candidates")},
         "value": matched / el if par["parity"] else None,
         **par,
         "unit": "assignments/s",
