@@ -106,6 +106,22 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
         }
     }
     __syncthreads();
+    // larger T: the user types sorted (value, then declared index) for a binary search per slot,
+    // and the slots outside [smallest, largest] type (the -2 padding) rejected at once
+    __shared__ int sv[ADLBQ_MAX_TYPES], si[ADLBQ_MAX_TYPES];
+    if constexpr (TB > 8) {
+        if (threadIdx.x < T) {
+            const int v = su[threadIdx.x];
+            int r = 0;
+            for (int u = 0; u < T; u++) {
+                const int x = su[u];
+                r += (x < v || (x == v && u < (int)threadIdx.x)) ? 1 : 0;
+            }
+            sv[r] = v;
+            si[r] = threadIdx.x;
+        }
+        __syncthreads();
+    }
     const int j = j0 + threadIdx.x;
     unsigned long long m = 0;
     if (threadIdx.x < nj) {
@@ -121,12 +137,14 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
 #pragma unroll
                 for (int t = 0; t < TB; t++) m |= (uok[t] && v == ur[t]) ? (1ull << t) : 0ull;
             } else {
-                if (v == -1) continue;
-                for (int t = 0; t < T; t++)
-                    if (su[t] == v) {  // get_type_idx: first declared match
-                        m |= 1ull << t;
-                        break;
-                    }
+                if (v == -1 || T == 0 || v < sv[0] || v > sv[T - 1]) continue;
+                int lo = 0, hi = T - 1;  // first sorted entry >= v: the first declared match (get_type_idx)
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sv[mid] < v) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (sv[lo] == v) m |= 1ull << si[lo];
             }
         }
         if (wild) m = T >= 64 ? ~0ull : ((1ull << T) - 1);
