@@ -1633,7 +1633,8 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                                                       const int *__restrict__ tend, TDelta dl, int T, const uint32_t *meta,
                                                       const unsigned long long *__restrict__ mask,
                                                       const int *__restrict__ reqs, int R, int *tmatch, int *seg_cnt,
-                                                      int *tcnt, const int *__restrict__ tlist, int tcap) {
+                                                      int *tcnt, const int *__restrict__ tlist, int tcap,
+                                                      int tdiag) {
     __shared__ int sreq[TGT_REQ];                   // the batch's Reserves in arrival order
     __shared__ unsigned long long smk[TGT_REQ];     // their type masks
     __shared__ unsigned long long ckey[TGT_CACHE];  // cached heads: inverted prio << 32 | position in the bucket
@@ -1711,6 +1712,7 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
         }
         __syncthreads();
         if (n == 0) break;
+        if (tdiag & 1) break;  // diagnostic ("targeted_diag" 1): the request lists only (wrong results)
         for (int k = tid; k < n; k += blockDim.x) smk[k] = mask[sreq[k]];
         if (tid < 64) {
             dem[tid] = 0;
@@ -1865,6 +1867,7 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
             if (k <= cut[ty[q]]) atomicAdd(&ccnt[ty[q]], 1);  // the valid prefix of the merged cache
         }
         __syncthreads();
+        if (tdiag & 2) break;  // diagnostic ("targeted_diag" 2): lists and cache fill only (wrong results)
         // ---- serve the Reserves in order (wave 0): lane t holds type t's head
         // (and the one after it) in registers; per Reserve a scalar loop over
         // its types compares the heads (readlane), the winner's lane advances
@@ -5031,7 +5034,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                                               h->d_tvals, h->d_tstart, h->d_tend,
                                               TDelta{h->d_dkeys, h->d_dvals, h->d_dstart, h->d_dend, (int)h->tdel_n},
                                               T, h->d_meta, h->d_mask, d_reqs, R,
-                                              h->d_tmatch, h->d_seg_cnt, h->d_tcnt, h->d_tlist, h->tcap);
+                                              h->d_tmatch, h->d_seg_cnt, h->d_tcnt, h->d_tlist, h->tcap,
+                                              h->targeted_diag);
         else
             k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
                                           h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);

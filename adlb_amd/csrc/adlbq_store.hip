@@ -2349,6 +2349,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->fold_thresholds = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "targeted_diag") {
+        h->targeted_diag = (int)value;
+        return ADLBQ_OK;
+    }
     if (n == "hist_arrive") {
         if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "hist_arrive must be 0 or 1");
         h->hist_arrive = (int)value;
