@@ -110,6 +110,7 @@ VARIANTS = {
     "rank_skip": {"fuse_rank": 1},         # k_rank skipped on the rank hint, the chain ranks when the hint fails
     "rank_in_chain": {"fuse_rank": 2},     # k_rank never launched: the chain sorts / ranks behind its grid barrier
     "thresholds_folded": {"fold_thresholds": 1},  # k_thresholds' work in pass 1's last workgroups (measured slower)
+    "hist_atomics": {"hist_arrive": 0},    # pass 1's chunk sums by an atomic per column (not by the chunk's last page)
 }
 
 
