@@ -359,6 +359,7 @@ struct adlbq_server {
     int kr_bin_max = 1024;             // "keyrank_bin_max": a larger digit bin fails the batch over to k_rank
     long long n_keyrank = 0, kr_fail_seen = 0, kr_skip_until = 0;
     int *d_arrive = nullptr; long long cap_arrive = 0;  // pass 1: pages of each chunk counted (hist_arrive)
+    int rq_wait_sync = 1;              // "rq_wait_sync": rq backpressure by stream sync (0: spin on the oldest snapshot, measured slower)
     int targeted_diag = 0;             // diagnostic ("targeted_diag"): parts of k_targeted_idx skipped (wrong results)
     int hist_arrive = 1;               // "hist_arrive": a chunk's last page sums its chunk (0: an atomic per column)
     int kr_par = 0;                    // parity of keyrank's chunk-count rows

@@ -93,6 +93,25 @@ void tighten_rq_bound(adlbq_server *h, bool wait_oldest) {
     }
 }
 
+// Wait (host spin on the mapped snapshot, no HIP call: the stream keeps its
+// queued batches) until the oldest batch still in flight has landed its
+// counter snapshot.  False when none is in flight, or after ~2 s (the caller
+// then synchronises the stream).
+static bool wait_oldest_snapshot(adlbq_server *h) {
+    const int N = adlbq_server::NSNAP;
+    for (int k = 0; k < N; k++) {
+        const int i = (h->snap_next + k) % N;  // the ring from its oldest slot
+        if (!h->snap_at[i] || h->snap_tag[i] == 0 || snap_landed(h, i)) continue;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (!snap_landed(h, i)) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) return false;
+        }
+        h->hint_stamp++;
+        return true;
+    }
+    return false;
+}
+
 // Upper bound of the parked Reserves alive now, from the newest landed batch
 // snapshot plus every Reserve launched after it (no synchronisation).
 long long rq_live_upper(adlbq_server *h) {
@@ -212,6 +231,13 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
         h->hacc["rq_waits"] += 1;
+        // the oldest batches in flight first, one at a time (a stream synchronisation would
+        // drain the queue and leave the GPU idle while the host issues the next batch)
+        while (!h->rq_wait_sync && wait_oldest_snapshot(h)) {
+            tighten_rq_bound(h, false);
+            need = h->rq_n_upper + extra;
+            if (need <= h->rq_cap) return ADLBQ_OK;
+        }
         tighten_rq_bound(h, true);
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
@@ -2347,6 +2373,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     if (n == "fold_thresholds") {
         if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0, 1 or 2 (auto)");
         h->fold_thresholds = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "rq_wait_sync") {  // 1: rq backpressure synchronises the stream (the round-3 form)
+        h->rq_wait_sync = value ? 1 : 0;
         return ADLBQ_OK;
     }
     if (n == "targeted_diag") {
