@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                     const unsigned long long m = readlane64(mv, kk);
                     // a type whose cache ran dry walks before it competes (uniform loop over such types)
                     const unsigned long long dry = __ballot(tl && hk == ~0ull && hd >= cn && (gn < ge || dn < de)) & m;
-                    if (dry && ((dry >> lane) & 1ull)) walk(hk, hs);
+                    if (dry && ((dry >> lane) & 1ull) && !(tdiag & 4)) walk(hk, hs);  // diag 4: no walks
                     unsigned long long best = ~0ull;
                     int bt = -1;
                     for (unsigned long long mm = m; mm; mm &= mm - 1) {

@@ -3,7 +3,7 @@
 export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/r04tdiag
 mkdir -p $O
-for d in 0 1 2; do
+for d in ${DIAGS:-0 1 2}; do
   timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/p$d -o run -- python3 bench.py --config4-only --no-cpu --no-pmc --c4-param targeted_diag=$d > $O/b$d.json 2> $O/b$d.err || { tail -5 $O/b$d.err; exit 1; }
   f=$(find $O/p$d -name "*kernel_trace.csv" | head -1)
   python3 - "$f" $d <<'PY'
