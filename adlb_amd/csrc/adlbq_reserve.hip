@@ -4082,10 +4082,30 @@ static int ensure_tindex(adlbq_server *h) {
             tq0 = now;
         };
         h->hacc["ti_keys"] += m;
-        std::vector<int> ord((size_t)m);
-        for (long long i = 0; i < m; i++) ord[(size_t)i] = (int)i;
         const auto &K = h->tnew_keys;
-        std::stable_sort(ord.begin(), ord.end(), [&K](int a, int b) { return K[(size_t)a] < K[(size_t)b]; });
+        // stable LSD radix sort of the new keys' indices, 8-bit digits, only the digits the
+        // keys differ in (a comparison sort of ~1,600 keys cost ~48 us of the config-4 step)
+        std::vector<int> ord((size_t)m), ord2((size_t)m);
+        for (long long i = 0; i < m; i++) ord[(size_t)i] = (int)i;
+        {
+            unsigned long long vor = 0, vand = ~0ull;
+            for (long long i = 0; i < m; i++) {
+                vor |= K[(size_t)i];
+                vand &= K[(size_t)i];
+            }
+            const unsigned long long vary = vor ^ vand;
+            for (int sh = 0; sh < 64; sh += 8) {
+                if (((vary >> sh) & 0xffull) == 0) continue;
+                int cnt[257] = {0};
+                for (long long i = 0; i < m; i++) cnt[((K[(size_t)ord[(size_t)i]] >> sh) & 0xff) + 1]++;
+                for (int d = 0; d < 256; d++) cnt[d + 1] += cnt[d];
+                for (long long i = 0; i < m; i++) {
+                    const int x = ord[(size_t)i];
+                    ord2[(size_t)cnt[(K[(size_t)x] >> sh) & 0xff]++] = x;
+                }
+                ord.swap(ord2);
+            }
+        }
         tsec("ti_sort");
         // pinned host staging, two buffers used in turn: a buffer is rewritten only once the
         // copy of two merges ago has run (its event), so the host never waits for the last one
