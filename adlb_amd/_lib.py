@@ -37,6 +37,7 @@ SIGNATURES = {
     "adlbq_set_qmstat_row": (c_int, [P, c_int, c_int, c_double, P]),
     "adlbq_check_remote": (c_int, [P, c_int, P, P]),
     "adlbq_rfr_done": (c_int, [P, c_int, c_int]),
+    "adlbq_rfr_done_batch": (c_int, [P, c_int, P]),
     "adlbq_tq_add": (c_int, [P, c_int, c_int, c_int]),
     "adlbq_rq_delete": (c_int, [P, c_int, P]),
     "adlbq_tq_dec": (c_int, [P, c_int, c_int, c_int]),

@@ -127,13 +127,24 @@ struct adlbsrv {
         auto it = tq.find(std::make_tuple(rank, type, server));
         if (it != tq.end() && --it->second <= 0) tq.erase(it);
     }
+    // SS_RFRs a steal group leaves to its next round: their engine records (rfr_to_rank /
+    // rfr_out) are cleared together by flush_rfr_cleared, one launch for all of them
+    std::vector<int> rfr_cleared;
+    int flush_rfr_cleared() {
+        const int n = (int)rfr_cleared.size() / 2;
+        if (!n) return 0;
+        const int r = adlbq_rfr_done_batch(q, n, rfr_cleared.data());
+        rfr_cleared.clear();
+        return rc(r, "adlbq_rfr_done_batch");
+    }
     void send_rfr(int donor, int rqseqno, const Parked &p) {
         // in a steal group the next round answers it, unless the donor holds targeted work for the rank;
-        // the engine recorded the SS_RFR as outstanding (rfr_to_rank / rfr_out): clear that now, as
-        // the SS_RFR_RESP that never comes would (adlb.c:1877-1878), so a later check_remote (a
-        // targeted Put for the rank landing elsewhere) does not skip the rank as busy
+        // the engine recorded the SS_RFR as outstanding (rfr_to_rank / rfr_out): clear that before the
+        // next engine call, as the SS_RFR_RESP that never comes would (adlb.c:1877-1878), so a later
+        // check_remote (a targeted Put for the rank landing elsewhere) does not skip the rank as busy
         if (grp && !tq_has(p.rank, donor)) {
-            adlbq_rfr_done(q, donor, p.rank);
+            rfr_cleared.push_back(donor);
+            rfr_cleared.push_back(p.rank);
             if (!want_sent) {  // ask the master for a round (once per round)
                 want_sent = true;
                 send(master, TAG_SRV_STEAL_WANT, nullptr, 0);
@@ -160,6 +171,7 @@ struct adlbsrv {
     }
     // check_remote_work_for_queued_apps (adlb.c:3536-3579)
     int check_remote() {
+        if (flush_rfr_cleared()) return -1;
         int cnt = 0;
         const int cap = (int)parked.size();
         if (!cap) return 0;
@@ -169,7 +181,7 @@ struct adlbsrv {
             auto it = parked.find(crem[3 * i]);
             if (it != parked.end()) send_rfr(crem[3 * i + 2], crem[3 * i], it->second);
         }
-        return 0;
+        return flush_rfr_cleared();
     }
     // answer every parked Reserve with code, FIFO order (adlb.c:1412-1442, 1639-1649)
     int drain_rq(int code) {
@@ -311,7 +323,7 @@ int adlbsrv_put_stage(adlbsrv *s, int src, const int *hdr, const void *buf, int 
     std::memcpy(st.hdr, hdr, sizeof st.hdr);
     st.buf.assign((const char *)buf, (const char *)buf + (len > 0 ? len : 0));
     s->staged.push_back(std::move(st));
-    s->staged_add += (double)(24 + 72) + (double)(len > 0 ? len : 0);  // pmalloc + wq_node_create
+    s->staged_add += (double)ADLBQ_BYTES_WQ + (double)(len > 0 ? len : 0);  // pmalloc + wq_node_create
     return 0;
 }
 
@@ -437,7 +449,7 @@ int adlbsrv_reserve_batch(adlbsrv *s, int n, const int *src, const int *bufs17) 
             if (r[11] >= 0) s->send_rfr(r[11], r[10], p);
         }
     }
-    return 0;
+    return s->flush_rfr_cleared();
 }
 
 int adlbsrv_get_batch(adlbsrv *s, int n, const int *src, const int *wqseqno) {

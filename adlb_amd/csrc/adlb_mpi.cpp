@@ -37,6 +37,7 @@
 #include <vector>
 
 #include "adlb/adlb.h"
+#include "adlbq.h"
 #include "adlb_core.h"
 #include "adlb_wire.h"
 
@@ -238,7 +239,8 @@ void serve(Loop *L, double max_malloc) {
     const double st_idle = env_d("ADLB_STEAL_IDLE_INTERVAL", 0.5);
     // ADLB_PUT_BATCH=0: every Put appended on its own (the one-at-a-time path, for comparison)
     const bool put_batching = env_d("ADLB_PUT_BATCH", 1.0) != 0.0;
-    const int put_cap = 4096;
+    const int put_cap = std::max(1, (int)env_d("ADLB_PUT_RUN_CAP", 256));
+    const double put_run_s = env_d("ADLB_PUT_RUN_US", 200.0) * 1e-6;
     const int T = (int)g_types.size();
     double t_qm = MPI_Wtime(), t_exh = MPI_Wtime(), t_ds = MPI_Wtime(), t_st = MPI_Wtime();
     std::vector<int> src, buf, one;
@@ -276,8 +278,14 @@ void serve(Loop *L, double max_malloc) {
         switch (tag) {
         case TAG_PUT_HDR: {
             // a run of waiting FA_PUT_HDRs: each acked and its payload received in turn
-            // (adlb.c:891-962), the appends and rq matches as one engine batch (963-1049)
+            // (adlb.c:891-962), the appends and rq matches as one engine batch (963-1049).
+            // The run holds back its Puts' final acks and the Reserves they match, so it is
+            // short: at most put_cap Puts or put_run_s of wall time, and it ends at the first
+            // waiting message that is not a Put.  The next header is taken only when an
+            // any-tag probe returns it, i.e. it is its source's oldest waiting message, so
+            // every app's messages are still handled in the order it sent them.
             int src_put = from, nput = 0;
+            const double t_run = MPI_Wtime();
             std::vector<char> p;
             while (true) {
                 int h[WIRE_IBUF], need = 0;
@@ -289,11 +297,11 @@ void serve(Loop *L, double max_malloc) {
                     if (put_batching) check(adlbsrv_put_stage(g_srv, src_put, h, p.data(), h[4]), "FA_PUT_MSG");
                     else check(adlbsrv_put_payload(g_srv, src_put, h, p.data(), h[4]), "FA_PUT_MSG");
                 }
-                if (++nput >= put_cap) break;
+                if (++nput >= put_cap || MPI_Wtime() - t_run > put_run_s) break;
                 int more = 0;
                 MPI_Status pst;
-                MPI_Iprobe(MPI_ANY_SOURCE, TAG_PUT_HDR, g_all, &more, &pst);
-                if (!more) break;
+                MPI_Iprobe(MPI_ANY_SOURCE, MPI_ANY_TAG, g_all, &more, &pst);
+                if (!more || pst.MPI_TAG != TAG_PUT_HDR) break;
                 src_put = pst.MPI_SOURCE;
             }
             check(adlbsrv_put_flush(g_srv), "FA_PUT_MSG (batch)");
@@ -570,6 +578,10 @@ int ADLBP_Server(double hi_malloc, double periodic_logging_time) {
         MPI_Comm_free(&node);
         const char *sg = getenv("ADLB_STEAL_GROUP");
         want = sg && *sg ? atoi(sg) != 0 : nn == g_S;
+        // the merge's type sets are 64-bit masks (adlbq_steal_group_export): a server of more
+        // types keeps the reference's SS_RFR steals (adlb.c:1280-1308), whatever was asked for.
+        // Every server declared the same types (ADLB_Init), so this agrees on all of them.
+        if (T > ADLBQ_MAX_TYPES) want = 0;
     }
     int all_want = 0;
     MPI_Allreduce(&want, &all_want, 1, MPI_INT, MPI_MIN, g_srvcomm);

@@ -51,9 +51,8 @@ constexpr uint32_t M_PINNED = 1u << 9;
 constexpr int M_OFF_SHIFT = 10;
 constexpr long long M_OFF_RANGE = 1ll << 22;
 constexpr int NREQ = ADLBQ_REQ_TYPES;
-// the reference's allocation sizes on LP64 (xq.h:8-79): xq_node_t 24 B + wq_struct_t 72 B per
-// unit (plus its payload), + rq_struct_t 80 B per parked Reserve, + tq_struct_t 16 B per tq entry
-constexpr long long BYTES_WQ = 24 + 72, BYTES_RQ = 24 + 80, BYTES_TQ = 24 + 16;
+// the reference's allocation sizes (include/adlbq.h: ADLBQ_BYTES_*)
+constexpr long long BYTES_WQ = ADLBQ_BYTES_WQ, BYTES_RQ = ADLBQ_BYTES_RQ, BYTES_TQ = ADLBQ_BYTES_TQ;
 
 
 // device-side scalar counters shared by kernels and read back lazily by the host
@@ -76,7 +75,7 @@ struct DevCounters {
     int plan_missed;       // sync-free sorts whose plan did not hold (k_rank sorted in-launch), cumulative
     int plan_phi;          // highest bit of the prio field any candidate list varies in (-1: none)
     int rank_fast;         // the last scan ranked its candidates in k_select_open (every threshold in an exact bin)
-    int rank_covered;      // ... and every type had candidates: the next batch may skip k_rank (fuse_rank)
+    int rank_covered;      // ... and every type had candidates (diagnostic)
     int kr_fail;           // batches whose keyrank failed over to k_rank (cumulative)
     int kr_why;            // the last keyrank failover: 1 more candidates than its buffers, 2 a bin over kr_bin_max
     int kr_maxbin;         // the largest digit bin of the last keyrank batch (diagnostic)
@@ -190,7 +189,7 @@ struct adlbq_server {
     long long rq_next_upper = 0;   // ... and on rq_next
     // rq_n snapshots written by k_finalize into mapped host memory at the end of
     // each reserve batch, so the rq capacity bound tightens without a sync
-    static constexpr int NSNAP = 8;
+    static constexpr int NSNAP = 32;  // reserve batches the host may run ahead of the device (rq bound)
     adlbq::DevCounters *h_snap = nullptr;   // [NSNAP] pinned, device-visible
     unsigned long long snap_tag[NSNAP] = {};  // the tag k_finalize stores last into that snapshot (0: unused)
     unsigned long long snap_tags = 0;          // tags handed out
@@ -241,9 +240,6 @@ struct adlbq_server {
     unsigned int *d_crank = nullptr;   // packed global rank << 6 | type, per candidate
     int *d_seg_cnt = nullptr;          // [R/64] chain: untargeted-capable requests per 64 requests
     unsigned long long *d_pmask = nullptr;  // [R/64] k_finalize: ballots of the requests that park
-    int *d_sg = nullptr;               // [1 + nseg * 8] k_rank's per-segment start guesses for the chain (T <= 8)
-    int seg_guess = 0;                 // "seg_guess": k_rank makes them (0: every chain segment finds its own;
-                                       // measured: k_rank +7 us for -0.5 us of chain, so off by default)
     int *d_lv = nullptr;               // [R][T] k_rank: level rows for the chain's guess (T <= 8)
     unsigned char *d_rtype = nullptr;
     int *d_pm_over = nullptr;          // k_put_match_blk: the staged rq overflowed
@@ -279,8 +275,8 @@ struct adlbq_server {
     int tnew_slot = 0;
     // segmented radix sort of the multi-prio-bin candidate lists (launched
     // when the newest landed batch needed one; k_rank sorts otherwise)
-    int *d_sbeg = nullptr, *d_send = nullptr; void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort
-    // launch_segsort's sync-free path: sorted merged keys / slots land here, the plan (valid, G, lo) on the device
+    void *d_ssort = nullptr; size_t cap_ssort = 0;  // launch_segsort
+    // launch_segsort_radix: the lists copied aside (keys / slots), the plan (valid, G, lo) on the device
     unsigned long long *d_ckey3 = nullptr; int *d_cslot3 = nullptr; long long cap_c3 = 0; int *d_plan = nullptr;
     // the candidate radix sort (rsort_*): 32-bit keys + indices, ping-pong; per-(digit, tile) counts; per-list OR / AND
     unsigned int *d_rs = nullptr; long long cap_rs = 0; int *d_rs_cnt = nullptr; long long cap_rs_cnt = 0;
@@ -289,10 +285,7 @@ struct adlbq_server {
     // kernels read and write directly, and a mapped copy of the counters
     int *h_zc = nullptr, *d_zc = nullptr; long long cap_zc = 0;
     adlbq::DevCounters *h_zctr = nullptr, *d_zctr = nullptr;
-    int segsort_radix = 1;             // "segsort_radix": the hand-written list-stable radix sort in the sync-free plan
     long long n_sort_radix = 0;
-    int segsort_async = 1;             // "segsort_async": plan the merged sort from the last landed batch (no sync)
-    long long n_sort_async = 0;
     long long n_segsort = 0;                          // lists given a device-wide sort (cumulative)
     long long ssort_items = 0;
     // ordered choice (k_chain0 / k_chainr): per segment start used and delta, the
@@ -309,10 +302,6 @@ struct adlbq_server {
     int chain_passes = 0;              // round 0's in-launch passes, 0 = auto (adlbq_set_param "chain_passes")
     int chain_rounds = -1;             // round launches after round 0, -1 = auto ("chain_rounds")
     int put_match_block = 1, put_always_match = 0;  // diagnostics ("put_match_block", "put_always_match")
-    int hist_variant = 0;              // pass 1: 0 the round-2 loop, 1 the rebased loop ("hist_variant")
-    int select_chunk = 0;              // pass 2: one workgroup per chunk of CHUNK pages (T <= 8) ("select_chunk")
-    int hist_ppb = 1;                  // pass-1 pages per workgroup, 1 or 2 (T <= 8) ("hist_ppb")
-    int hist_diag = 0;                 // diagnostic ("hist_diag"): parts of pass 1 skipped (wrong results)
     int split_prep = 0;                // diagnostic ("split_prep"): request preparation and pass 1 as two launches
     int rank_in_select = 1;            // k_select_open ranks the candidates when it can ("rank_in_select")
     int sort_fail_test = 0;            // test hook ("sort_fail_test"): the error path of a failed sort wait
@@ -320,17 +309,8 @@ struct adlbq_server {
     unsigned long long *d_stamps = nullptr; int cap_stamps = 0, n_stamps = 0;
     int chain_warm = -1;               // round-0 warm-up requests (T <= 8), -1 = auto ("chain_warm")
     long long chain_modes = -1;        // bit k-1: round k uses prefix starts, -1 = auto ("chain_modes")
-    int segsort_merged = 1;            // one merged sort of every list when the keys allow ("segsort_merged")
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
-    int fuse_finalize = 0;             // "fuse_finalize": k_finalize inside the final k_chain0 launch (measured even: off)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
-    int fuse_rank = 0;                 // "fuse_rank": T <= 8, no k_rank launch when the newest landed batch needed
-                                       // none; k_chain0 then ranks itself if this batch's k_select_open did not
-                                       // (off: that k_chain0 instance carries k_rank's registers and stack,
-                                       // measured +16 us against the 8 us launch it saves)
-    int fold_thresholds = 0;           // "fold_thresholds": k_thresholds' work in pass 1's last workgroups
-                                       // (measured slower: off)
-    int *d_fold = nullptr;             // k_prep_hist's folded-thresholds arrival counters
     // the Reserve path of more than ADLBQ_MAX_TYPES types (adlbq_wide.hip): sort buffers and runs
     unsigned long long *d_wk0 = nullptr, *d_wk1 = nullptr, *d_wekey = nullptr;
     int *d_wv0 = nullptr, *d_wv1 = nullptr, *d_wflag = nullptr, *d_wrstart = nullptr, *d_whead = nullptr;
@@ -358,12 +338,9 @@ struct adlbq_server {
     int keyrank = 1;                   // "keyrank": 0 = the per-list sort + k_rank
     int kr_bin_max = 1024;             // "keyrank_bin_max": a larger digit bin fails the batch over to k_rank
     long long n_keyrank = 0, kr_fail_seen = 0, kr_skip_until = 0;
-    int *d_arrive = nullptr; long long cap_arrive = 0;  // pass 1: pages of each chunk counted (hist_arrive)
     int rq_wait_sync = 1;              // "rq_wait_sync": rq backpressure by stream sync (0: spin on the oldest snapshot, measured slower)
     int targeted_diag = 0;             // diagnostic ("targeted_diag"): parts of k_targeted_idx skipped (wrong results)
-    int hist_arrive = 1;               // "hist_arrive": a chunk's last page sums its chunk (0: an atomic per column)
     int kr_par = 0;                    // parity of keyrank's chunk-count rows
-    int segsort_wide = 16384;          // list length from which a list gets a device-wide sort ("segsort_wide")
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]
     long long *d_navail = nullptr;                       // [T]
@@ -416,7 +393,6 @@ int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
-bool rank_skip_hint(adlbq_server *h);  // ... and every type had candidates (k_rank may be skipped)
 bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi = nullptr);
 inline void wq_changed(adlbq_server *h) { h->batch_export_k = 0; }  // the last batch's lists no longer describe the wq  // newest landed batch's candidate sort plan
 bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper

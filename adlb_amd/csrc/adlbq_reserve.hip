@@ -177,6 +177,26 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
 }
 
 // ---------------------------------------------------------------- pass 1
+// The far bins, lumped (T <= 8).  With guessed cuts gc below the anchors an,
+// the units deeper than twice the deepest guessed depth are counted per type in
+// registers (one LDS add per wave and type at the end) into the last bin of
+// their type instead of with one LDS atomic each into their own bin.  The
+// thresholds lie above the cuts whenever the guesses hold; when one does not,
+// that type's lump is a multi-priority bin like any other (its units are listed
+// and sorted).  Pass 1 and pass 2 bin by the same rule: a unit in bin
+// batch_lump_bin or deeper belongs to bin NB - 1 of its type (NB: nothing lumped).
+// Lane t holds type t's anchor and cut; every lane of the wave calls it.
+__device__ __forceinline__ int batch_lump_bin(int T, bool tl, long long an, long long gc) {
+#ifdef ADLBQ_NO_LUMP
+    return NB;
+#endif
+    int v = -1;  // a type without a guess (or with an empty one) does not vote
+    if (T <= 8 && tl && gc != LLONG_MAX && gc <= an && an - gc < (1ll << 30)) v = bin_of(2 * (an - gc) + 2) + 1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return (v < 0 || v >= NB - 1) ? NB : v;
+}
+
 // One workgroup per page: each wave owns a quarter of the page and issues all
 // of its loads (8 x 16 B per lane) before counting.  The histogram is kept in
 // HK lane-interleaved copies so that lanes hitting the same (type, bin) column
@@ -196,14 +216,9 @@ struct HistArgs {
     unsigned int *spec;      // [npages][4][SPEC_CAP] per wave: (column << 12 | slot-in-page), slot order
     int *specn;              // [npages][4] entries found (> SPEC_CAP: overflowed, not usable)
     const int *pbase, *pwide;  // per page id: packed-offset base, wide flag
-    int diag;                  // diagnostic ("hist_diag", wrong results): bit 0 no lists, 1 no epilogue, 2 no counts
-    unsigned int *zcs;         // the other chunk-sum buffer (the previous scan's): zeroed here, a slice per workgroup
+    unsigned int *zcs;         // the other chunk-sum buffer (the previous scan's): k_thresholds zeroes it
     long long zn;
-    int zper;                  // (unused: k_thresholds zeroes the other buffer)
-    int variant;               // "hist_variant": 0 the round-2 loop, 1 the rebased one
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
-    int *arrive;               // [chunks] pages of the chunk counted so far (its last page sums the chunk), or
-                               // nullptr: every page adds its row to the chunk sums with atomics
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -236,230 +251,21 @@ __device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const
     }
 }
 
-// A quarter page of the scan columns as stored: meta (4 B per unit), and the
-// prio column only on a wide page (a narrow page's prios are pb + meta >> 10).
-__device__ __forceinline__ void load_quarter_raw(const int *__restrict__ prio, const uint32_t *__restrict__ meta,
-                                                 const int *__restrict__ pbase, const int *__restrict__ pwide,
-                                                 int pg, int fill, int w, int4 (&pv)[4], uint4 (&mv)[4], int &wide,
-                                                 int &pb) {
-    const int lane = threadIdx.x & 63;
-    const long long base = (long long)pg << PAGE_SHIFT;
-    const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
-    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
-    wide = pwide[pg];
-    pb = pbase[pg];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int idx = (w * 4 + k) * 64 + lane;
-        mv[k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
-    }
-    if (wide) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int idx = (w * 4 + k) * 64 + lane;
-            pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
-        }
-    }
-}
-
-// Page p's counts from its loaded quarter (pv, mv): histogram (hist zeroed and
-// sag staged before the barrier the caller ran), speculative lists, per-page
-// row and chunk sums.
-// Per unit: off = the prio relative to the page base (narrow: meta >> 10; wide:
-// the prio itself, pb = 0); sagp[t] = {anchor - pb, cut - pb} and lowrel =
-// LOWEST - pb were rebased for this page, so the distance, the cut test and
-// the availability test need no per-unit prio reconstruction.  Every unit's
-// sagp read is issued before any is used; columns and counts are branch-free.
-template <bool NARROW>
-__device__ __forceinline__ void hist_count(const HistArgs &a, const int p, const int4 (&pv)[4], const uint4 (&mv)[4],
-                                           const int2 *sagp, int lowrel,
-                                           unsigned int *__restrict__ hist /* [C][HK] */,
-                                           unsigned int *__restrict__ slist /* [4][SPEC_CAP] */) {
-    const int T = a.T;
-    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    unsigned int *my = hist + (lane % HK);
-    // units at or above the guessed cut go to this wave's speculative list, in
-    // slot order: k_select_open reads the list instead of the page when the
-    // guess holds (every real cut at or above it) and the list did not overflow.
-    // The list is built in LDS and written out once at the end: a global store
-    // inside the loop would make every later wait on the loads wait for it too
-    unsigned int *wl = slist + w * SPEC_CAP;
-    int sn = 0;
-    int2 ag[4][4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-#pragma unroll
-        for (int q = 0; q < 4; q++) ag[k][q] = sagp[min((int)(mm[q] & M_TYPE), T - 1)];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int pw[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
-        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-        int col[4];
-        bool in[4], av[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int off = NARROW ? (int)(mm[q] >> M_OFF_SHIFT) : pw[q];
-            av[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && off > lowrel;
-            // no branch: an unavailable unit gets some in-range column and adds 0 to it
-            const int t = av[q] ? (int)(mm[q] & M_TYPE) : 0;
-            const unsigned int d = av[q] ? (unsigned int)ag[k][q].x - (unsigned int)off : 0u;  // distance < 2^32
-            col[q] = t * NB + bin_of32(d);
-            in[q] = av[q] && off >= ag[k][q].y;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++) atomicAdd(&my[col[q] * HK], av[q] ? 1u : 0u);
-        // the few units at or above the cut, appended in slot order (lane-major, then q)
-        // by a scalar walk over the set bits: no per-lane position arithmetic
-        const unsigned long long B[4] = {__ballot(in[0]), __ballot(in[1]), __ballot(in[2]), __ballot(in[3])};
-        for (unsigned long long any = B[0] | B[1] | B[2] | B[3]; any; any &= any - 1) {
-            const int l = __ffsll((long long)any) - 1;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if ((B[q] >> l) & 1ull) {
-                    const int cq = __builtin_amdgcn_readlane(col[q], l);
-                    if (lane == 0 && sn < SPEC_CAP)
-                        wl[sn] = ((unsigned int)cq << 12) | (unsigned int)((w * 4 + k) * 256 + l * 4 + q);
-                    sn++;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // the wave's list out to global memory (coalesced), then the page's column row and chunk sums
-    unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
-    const int nl = min(sn, SPEC_CAP);
-#pragma unroll
-    for (int k = 0; k < SPEC_CAP / 64; k++)
-        if (k * 64 + lane < nl) sp[k * 64 + lane] = wl[k * 64 + lane];
-    if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
-    if (!(a.diag & 2)) {
-        const int ck = p / CHUNK;
-        unsigned int *cs = a.csum + (long long)ck * C;
-        unsigned short *g = a.gh + (long long)p * C;
-        if (a.arrive == nullptr) {
-            for (int c = threadIdx.x; c < C; c += blockDim.x) {
-                unsigned int v = 0;
-#pragma unroll
-                for (int k = 0; k < HK; k++) v += hist[c * HK + k];
-                g[c] = (unsigned short)v;
-                if (v) atomicAdd(&cs[c], v);
-            }
-        } else {
-            // The row goes out written through (agent-scope stores, two columns a word), and the
-            // chunk's last page to arrive sums the chunk's rows into its chunk sums with agent-scope
-            // loads (another XCD's L2 may hold stale lines of those rows): one atomic per page
-            // instead of one per non-zero column (~500 per page at 32 types)
-            unsigned int *g32 = reinterpret_cast<unsigned int *>(g);  // C is even (NB = 64)
-            for (int c2 = threadIdx.x; c2 < C / 2; c2 += blockDim.x) {
-                unsigned int v0 = 0, v1 = 0;
-#pragma unroll
-                for (int k = 0; k < HK; k++) {
-                    v0 += hist[(2 * c2) * HK + k];
-                    v1 += hist[(2 * c2 + 1) * HK + k];
-                }
-                __hip_atomic_store(g32 + c2, (v1 << 16) | (v0 & 0xffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __shared__ int s_last;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            const int n = min(CHUNK, a.npages - ck * CHUNK);
-            if (threadIdx.x == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                const int old = __hip_atomic_fetch_add(a.arrive + ck, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_last = old == n - 1;
-                if (old == n - 1) __hip_atomic_store(a.arrive + ck, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
-            if (s_last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                const unsigned int *r32 = reinterpret_cast<const unsigned int *>(a.gh + (long long)ck * CHUNK * C);
-                for (int c2 = threadIdx.x; c2 < C / 2; c2 += blockDim.x) {
-                    unsigned int w[CHUNK];
-#pragma unroll
-                    for (int q = 0; q < CHUNK; q++)
-                        w[q] = q < n ? __hip_atomic_load(r32 + (long long)q * (C / 2) + c2, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                     : 0u;
-                    unsigned int v0 = 0, v1 = 0;
-#pragma unroll
-                    for (int q = 0; q < CHUNK; q++) {
-                        v0 += w[q] & 0xffffu;
-                        v1 += w[q] >> 16;
-                    }
-                    __hip_atomic_store(cs + 2 * c2, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(cs + 2 * c2 + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-        }
-    }
-}
-
-// Every type is counted, demand or not: k_thresholds ignores the columns of a
-// type without demand; the next scan's pass 1 zeroes this one's chunk sums.  PPB pages per
-// workgroup, every page's loads issued before the first is counted.
-template <int PPB>
-__device__ __forceinline__ void hist_pages(const HistArgs &a, const int p0, unsigned int *__restrict__ hist) {
-    static_assert(PPB == 1, "one page per workgroup (two measured slower)");
-    __shared__ int2 sagp[ADLBQ_MAX_TYPES];
-    const int C = a.T * NB, w = threadIdx.x >> 6;
-    int4 pv[4];
-    uint4 mv[4];
-    int wide = 0, pb = 0;
-    // every load issued before anything waits: the page, then the per-type
-    // anchor / cut (staged in LDS before the barrier, so that wait covers all)
-    const int p = p0;
-    load_quarter_raw(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p],
-                     p == a.npages - 1 ? a.tail_fill : PAGE, w, pv, mv, wide, pb);
-    const int tt = threadIdx.x;
-    long long an = 0, gc = 0;
-    if (tt < a.T) {
-        an = __builtin_nontemporal_load(a.anchor + tt);
-        gc = __builtin_nontemporal_load(a.gcut + tt);
-    }
-    if (a.diag & 8) {  // diagnostic: the loads alone (one store of their sum per wave, so they are kept)
-        unsigned int acc = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) acc += mv[k].x + mv[k].y + mv[k].z + mv[k].w;
-        if (acc == 0x9e3779b9u) a.specn[0] = (int)acc;  // practically never taken
-        return;
-    }
-    // this page's rebased constants: a narrow page's units carry prio - pb (wide: pb = 0)
-    const long long base = wide ? 0 : pb;
-    auto clampi = [](long long v) { return (int)std::max(std::min(v, (long long)INT_MAX), (long long)INT_MIN); };
-    const int lowrel = clampi((long long)LOWEST - base);
-    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-    if (tt < a.T) sagp[tt] = make_int2((int)((unsigned int)an - (unsigned int)base), clampi(gc - base));
-    __syncthreads();
-    if (wide) hist_count<false>(a, p, pv, mv, sagp, lowrel, hist, hist + C * HK);
-    else hist_count<true>(a, p, pv, mv, sagp, lowrel, hist, hist + C * HK);
-}
-
-// Pass 1, variant 0 ("hist_variant" 0): the round-2 form (per-unit anchor /
-// cut from LDS, list stores in the loop); kept beside the rebased form below
-// for measurement.
-__device__ __forceinline__ void hist_page_v0(const HistArgs &a, const int p, unsigned int *__restrict__ hist /* [C][HK] */) {
-    __shared__ int2 sag[ADLBQ_MAX_TYPES];
-    const int *__restrict__ prio = a.prio;
-    const uint32_t *__restrict__ meta = a.meta;
-    const int T = a.T, npages = a.npages, tail_fill = a.tail_fill;
-    const long long *__restrict__ anchor = a.anchor;
-    unsigned short *__restrict__ gh = a.gh;
-    unsigned int *__restrict__ csum = a.csum;
-    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int fill = (p == npages - 1) ? tail_fill : PAGE;
-    int4 pv[4];
-    uint4 mv[4];
-    load_quarter(prio, meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p], fill, w, pv, mv);
-    for (int t = threadIdx.x; t < T; t += blockDim.x) {
-        sag[t] = make_int2((int)anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
-    }
-    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-    __syncthreads();
+// Pass 1 over one page (four waves, a quarter page each): per (type, bin)
+// column the available units (LDS copies, then the page's row and the chunk
+// sums), and in each wave's list the units at or above the guessed cut, in
+// slot order.  LUMP (T <= 8): units in bin lb or deeper are counted in
+// registers, 8 bits per type, and added to bin NB - 1 of their type once per
+// wave (batch_lump_bin).
+template <bool LUMP>
+__device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, const int4 (&pv)[4],
+                                               const uint4 (&mv)[4], const int2 *sag, const int lb,
+                                               unsigned int *__restrict__ hist /* [C][HK] */) {
+    const int T = a.T, C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     unsigned int *my = hist + (lane % HK);
     unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
     const unsigned long long lt = lanemask_lt();
+    unsigned long long lumpc = 0ull;
     int sn = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -472,9 +278,15 @@ __device__ __forceinline__ void hist_page_v0(const HistArgs &a, const int p, uns
             const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
             const int t = mm[q] & M_TYPE;
             const int2 ag = sag[t];
-            col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
+            const int bn = bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
+            col[q] = t * NB + bn;
             in[q] = av && pr[q] >= ag.y;
-            if (av) atomicAdd(&my[col[q] * HK], 1u);
+            if constexpr (LUMP) {
+                if (av && bn < lb) atomicAdd(&my[col[q] * HK], 1u);
+                lumpc += (av && bn >= lb) ? (1ull << (8 * (t & 7))) : 0ull;
+            } else {
+                if (av) atomicAdd(&my[col[q] * HK], 1u);
+            }
         }
         const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
                                  b3 = __ballot(in[3]);
@@ -490,10 +302,18 @@ __device__ __forceinline__ void hist_page_v0(const HistArgs &a, const int p, uns
         }
         sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
     }
+    if constexpr (LUMP) {
+        for (int u = 0; u < T; u++) {
+            unsigned int c = (unsigned int)(lumpc >> (8 * u)) & 0xffu;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+            if (lane == 0 && c) atomicAdd(&hist[(u * NB + NB - 1) * HK], c);
+        }
+    }
     if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
-    unsigned int *cs = csum + (long long)(p / CHUNK) * C;
-    unsigned short *g = gh + (long long)p * C;
+    unsigned int *cs = a.csum + (long long)(p / CHUNK) * C;
+    unsigned short *g = a.gh + (long long)p * C;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         unsigned int v = 0;
 #pragma unroll
@@ -501,6 +321,28 @@ __device__ __forceinline__ void hist_page_v0(const HistArgs &a, const int p, uns
         g[c] = (unsigned short)v;
         if (v) atomicAdd(&cs[c], v);
     }
+}
+
+__device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist) {
+    __shared__ int2 sag[ADLBQ_MAX_TYPES];
+    __shared__ int s_lb;
+    const int T = a.T, C = T * NB, w = threadIdx.x >> 6;
+    const int fill = (p == a.npages - 1) ? a.tail_fill : PAGE;
+    int4 pv[4];
+    uint4 mv[4];
+    load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p], fill, w, pv, mv);
+    if (threadIdx.x < 64) {  // wave 0 holds every type (T <= 64): anchors, cuts, the batch's lump bin
+        const int t = threadIdx.x;
+        const long long an = t < T ? a.anchor[t] : 0, gc = t < T ? a.gcut[t] : 0;
+        if (t < T) sag[t] = make_int2((int)an, (int)std::max(std::min(gc, (long long)INT_MAX), (long long)INT_MIN));
+        const int lb = batch_lump_bin(T, t < T, an, gc);
+        if (t == 0) s_lb = lb;
+    }
+    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
+    const int lb = s_lb;
+    if (lb < NB) hist_page_body<true>(a, p, pv, mv, sag, lb, hist);
+    else hist_page_body<false>(a, p, pv, mv, sag, lb, hist);
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
@@ -649,143 +491,22 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, lo
     thresholds_body(zcs, zn, T, dem, csum, nchunks, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next, guess, blockIdx.x, gridDim.x);
 }
 
-// ---------------------------------------------------------------- thresholds folded into pass 1
-// k_thresholds' work done by the last workgroups of k_prep_hist instead of a
-// launch of its own.  Every workgroup (request preparation or page) arrives
-// at one counter once its demand / chunk-sum atomics have completed (each
-// wave's s_waitcnt, then a workgroup barrier, then one agent-scope add: the
-// atomics are the hand-off, read back with sc1 loads -- MI355X_MICROARCH.md,
-// inter-workgroup visibility).  The workgroups holding the last nl tickets
-// wait for every arrival, then role r scans the C / nl columns [r C / nl, ...)
-// (tpc = 256 nl / C threads per column, a run of chunks each): the chunk sums
-// become exclusive prefixes in place, the column totals go out sc1, and the
-// workgroup whose add completes a type's 64 columns finds that type's
-// threshold (type_threshold).  The last role to finish resets the counters.
-struct FoldArgs {
-    int on;            // 0: k_thresholds runs as its own launch
-    int *arrive;       // [nl + 2] arrivals per role group (workgroup b in group b % nl), groups complete, roles done
-    int total, nl;     // workgroups of the launch; roles (C % nl == 0, 4 <= C / nl <= 64)
-    int nchunks;
-    const int *dem;
-    int *theta, *need, *candlen, *needsort, *binoff;
-    unsigned int *coltot;
-    int *type_cnt;
-    const long long *anchor;
-    long long *anchor_next, *gcut_next;
-    int guess;
-    int *fail;         // the batch's failure counter (k_finalize answers ADLB_ERROR when it moved)
-    unsigned int *zcs; // the previous scan's chunk sums, zeroed here: a slice per page workgroup
-    long long zn;
-};
-
-constexpr long long FOLD_WAIT_TICKS = 100ll * 1000 * 1000;  // 1 s at the 100 MHz constant clock
-constexpr int FOLD_MAX_NL = ADLBQ_MAX_TYPES * NB / 8;
-constexpr int FOLD_AUTO_PAGES = 1024;
-
-__device__ void fold_thresholds(const FoldArgs &f, int T, unsigned int *csum, unsigned int *lds, const int bid) {
-    // two-level arrival (one counter per role group, then the top counter): a
-    // single counter taking every workgroup's add serialised them (tens of us)
-    __shared__ int s_role;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's atomics have completed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int g = bid % f.nl, ng = (f.total - g + f.nl - 1) / f.nl;
-        const int v = __hip_atomic_fetch_add(f.arrive + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int role = -1;
-        if (v == ng - 1) {  // the group is complete: this workgroup takes its role once every group is
-            __hip_atomic_fetch_add(f.arrive + f.nl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            role = g;
-            const long long t0 = wall_clock64();
-            while (__hip_atomic_load(f.arrive + f.nl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < f.nl) {
-                if (wall_clock64() - t0 > FOLD_WAIT_TICKS) {
-                    atomicAdd(f.fail, 1);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        s_role = role;
-    }
-    __syncthreads();
-    const int role = s_role;
-    if (role < 0) return;
-    const int C = T * NB, ncol = C / f.nl, tpc = 256 / ncol;
-    const int c = role * ncol + (int)threadIdx.x / tpc, sub = (int)threadIdx.x % tpc;
-    const int per = (f.nchunks + tpc - 1) / tpc, k0 = min(f.nchunks, sub * per), k1 = min(f.nchunks, k0 + per);
-    // this thread's run of chunks: loads in flight 16 at a time, summed
-    unsigned int sum = 0;
-    for (int k = k0; k < k1; k += 16) {
-        unsigned int v[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            v[i] = k + i < k1 ? __hip_atomic_load(csum + (long long)(k + i) * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-        for (int i = 0; i < 16; i++) sum += v[i];
-    }
-    // exclusive scan over the tpc threads of the column (consecutive lanes of one wave)
-    unsigned int x = sum;
-    for (int o = 1; o < tpc; o <<= 1) {
-        const unsigned int y = __shfl_up(x, o, tpc);
-        if (sub >= o) x += y;
-    }
-    unsigned int run = x - sum;
-    for (int k = k0; k < k1; k += 16) {  // the chunk sums as exclusive prefixes, in place (read by k_select_open)
-        unsigned int v[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            v[i] = k + i < k1 ? __hip_atomic_load(csum + (long long)(k + i) * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-            if (k + i < k1) {
-                csum[(long long)(k + i) * C + c] = run;
-                run += v[i];
-            }
-    }
-    if (sub == tpc - 1) __hip_atomic_store(f.coltot + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const int t = (role * ncol) / NB;  // every column of a role is of one type (ncol <= NB)
-    __shared__ int s_last;
-    if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(f.type_cnt + t, ncol, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + ncol == NB;
-    __syncthreads();
-    if (s_last && threadIdx.x < 64)
-        type_threshold(t, f.dem, f.theta, f.need, f.candlen, f.needsort, f.binoff, f.coltot, f.type_cnt, f.anchor,
-                       f.anchor_next, f.gcut_next, f.guess);
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(f.arrive + role, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // its group is done
-        if (__hip_atomic_fetch_add(f.arrive + f.nl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == f.nl - 1) {
-            // the last role: every waiter has seen the total
-            __hip_atomic_store(f.arrive + f.nl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(f.arrive + f.nl + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    (void)lds;
-}
-
 // Pass 1 and the request preparation in one launch (they are independent):
-// workgroups [0, nprep) prepare 256 requests each, the rest count one page;
-// with fd.on the last workgroups then do k_thresholds' work.
-template <int TB, int PPB = 1>
-__device__ __forceinline__ void prep_hist_body(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd, const int bid_, const int nbk_) {
+// workgroups [0, nprep) prepare 256 requests each, the rest count one page.
+template <int TB>
+__device__ __forceinline__ void prep_hist_body(PrepArgs pa, int nprep, HistArgs ha, const int bid_) {
     static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
     extern __shared__ unsigned int lds[];
     if ((int)bid_ < nprep) {
         prep_block<TB>(pa, bid_, reinterpret_cast<int *>(lds));
     } else {
-        if (ha.variant == 0) hist_page_v0(ha, bid_ - nprep, lds);
-        else hist_pages<PPB>(ha, (bid_ - nprep) * PPB, lds);
-        if (fd.on && fd.zn > 0) {  // the previous scan's chunk sums (consumed): zeroed for the scan after this one
-            const long long npb = (long long)nbk_ - nprep, b = (long long)bid_ - nprep;
-            const long long per = (fd.zn + npb - 1) / npb, z0 = b * per;
-            for (long long i = z0 + threadIdx.x; i < min(fd.zn, z0 + per); i += blockDim.x) fd.zcs[i] = 0u;
-        }
+        hist_page(ha, bid_ - nprep, lds);
     }
-    if (fd.on) fold_thresholds(fd, ha.T, ha.csum, lds, bid_);
 }
 
-template <int TB, int PPB = 1>
-__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha, FoldArgs fd) {
-    prep_hist_body<TB>(pa, nprep, ha, fd, blockIdx.x, gridDim.x);
+template <int TB>
+__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha) {
+    prep_hist_body<TB>(pa, nprep, ha, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- pass 2
@@ -843,6 +564,7 @@ __device__ __forceinline__ void select_open_body(
 #pragma unroll
     for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
     const long long cut_l = cut_of(th_l, an_l);
+    const int lumpb = batch_lump_bin(T, tl, an_l, gc_l);  // pass 1's lumped far bins: bin NB - 1 from there on
     const bool use_spec = __ballot(th_l >= 0 && gc_l > cut_l) == 0 && sn <= SPEC_CAP;  // wave-uniform
     int4 pv[4];
     uint4 mv[4];
@@ -933,7 +655,8 @@ __device__ __forceinline__ void select_open_body(
         for (int q = 0; q < 4; q++) {
             if (cnd[q]) {
                 const int t = mm[q] & M_TYPE;
-                const int col = t * NB + bin_of(sanc[t] - pr[q]);
+                const int bq = bin_of(sanc[t] - pr[q]);
+                const int col = t * NB + (bq >= lumpb ? NB - 1 : bq);
                 atomicAdd(&wc[w * C + col], 1u);
                 list[pos++] = ((unsigned int)col << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
             }
@@ -1064,273 +787,6 @@ __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
     unsigned char *__restrict__ rtype, int R) {
     select_open_body<TB>(pages, npages, tail_fill, prio, meta, seqa, T, anchor, theta, need, binoff, csum, gh, candlen, candoff_out, ckey, cslot, gcut, spec, specn, pbase, pwide, ctr, crank, lv, rtype, R, blockIdx.x, gridDim.x);
-}
-
-// k_select_open with one workgroup per chunk of CHUNK pages, in order (the
-// chunk's prefix is its row alone; each page's column counts carry into the
-// next; the next page's speculative list is loaded while the current one is
-// ranked).  Option "select_chunk" (T <= 8).
-template <int TB, int PPB = CHUNK>  // TB >= T; the candidates are ranked here only for TB <= RT
-__global__ __launch_bounds__(256) void k_select_chunk(
-    const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
-    const uint32_t *__restrict__ meta, const int *__restrict__ seqa, int T, const long long *__restrict__ anchor,
-    const int *__restrict__ theta, const int *__restrict__ need,
-    const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
-    const int *__restrict__ candlen, int *__restrict__ candoff_out,
-    unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
-    const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
-    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
-    unsigned char *__restrict__ rtype, int R) {
-    static_assert(PPB == CHUNK, "a workgroup takes one whole chunk");
-    constexpr int RT = TB <= RANK_FAST_T ? TB : 1;  // types of the fast ranking
-    extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
-    __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
-    __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES], slen[RT];
-    __shared__ int sbo[RT * NB];  // binoff (fast ranking)
-    const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int pfirst = blockIdx.x * PPB, plast = min(npages, pfirst + PPB);
-    unsigned int *wc = lds;
-    unsigned int *list = lds + 4 * C + w * 1024;
-    // Pass 1's speculative list of this wave's quarter is usable when it did
-    // not overflow and, for every type with demand, the guessed cut is at or
-    // below the real one (lane t checks type t; T <= 64): then the list holds
-    // every candidate and the page's columns are not read again.
-    // All of the prologue's loads are issued together: lane t's type-t
-    // parameters, the first list (read whether or not it is used) and, below,
-    // the page prefix rows.
-    const bool tl = lane < T;
-    const int th_l = tl ? theta[lane] : -1, nd_l = tl ? need[lane] : 0, len_l = tl ? candlen[lane] : 0;
-    const long long an_l = tl ? anchor[lane] : 0, gc_l = tl ? gcut[lane] : 0;
-    int sn = specn[(long long)pfirst * 4 + w];
-    // binoff for the fast ranking (T <= 8: at most two columns per thread), in flight with the rest
-    int bo_r[2];
-#pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const int c = threadIdx.x + q * 256;
-        bo_r[q] = (TB <= RANK_FAST_T && crank != nullptr && c < C) ? binoff[c] : 0;
-    }
-    unsigned int se[SPEC_CAP / 64];
-    {
-        const unsigned int *__restrict__ sp = spec + ((long long)pfirst * 4 + w) * SPEC_CAP;
-#pragma unroll
-        for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
-    }
-    const long long cut_l = cut_of(th_l, an_l);
-    const bool guess_ok = __ballot(th_l >= 0 && gc_l > cut_l) == 0;  // wave-uniform, the same in every wave
-    // rank of the first page's first unit in each of the thread's columns (only
-    // columns at or below a threshold): the chunk's exclusive prefix
-    // (k_thresholds) plus the counts of the chunk's earlier pages (hist_count);
-    // then carried from page to page
-    constexpr int CPT = (TB * NB + 255) / 256;  // columns per thread, at most
-    unsigned int ppv[CPT];
-    const int p0 = (pfirst / CHUNK) * CHUNK;
-#pragma unroll
-    for (int r = 0; r < CPT; r++) {
-        const int c = threadIdx.x + r * 256;
-        ppv[r] = 0;
-        if (r * 256 >= C) break;
-        const int thc = __shfl(th_l, (c / NB) & 63, 64);
-        if (c < C && (c % NB) <= thc) {
-            unsigned int v = csum[(long long)(pfirst / CHUNK) * C + c];
-            if (PPB == 1) {
-                unsigned short g[CHUNK - 1];
-#pragma unroll
-                for (int q = 0; q < CHUNK - 1; q++)
-                    g[q] = p0 + q < pfirst ? gh[(long long)(p0 + q) * C + c] : (unsigned short)0;
-#pragma unroll
-                for (int q = 0; q < CHUNK - 1; q++) v += g[q];
-            }
-            ppv[r] = v;
-        }
-    }
-    if (w == 0 && tl) {
-        sanc[lane] = an_l;
-        sth[lane] = th_l;
-        sneed[lane] = nd_l;
-        scut[lane] = cut_l;
-        if (lane < RT) slen[lane] = len_l;
-    }
-    // ranks computed here (k_rank then skips its tiles) when every threshold
-    // lies in an exact bin: every candidate list is then in (prio desc,
-    // position asc) order by construction, and a unit of another type u with
-    // the same prio precedes this one iff it lies earlier in the open bucket
-    const bool fast = TB <= RANK_FAST_T && crank != nullptr && __ballot(tl && th_l >= NBX) == 0;
-    if (fast)  // binoff (only read for the types with demand, the ones k_thresholds wrote it for)
-#pragma unroll
-        for (int q = 0; q < 2; q++)
-            if (threadIdx.x + q * 256 < C) sbo[threadIdx.x + q * 256] = bo_r[q];
-    if (threadIdx.x < 64) {  // candidate list offsets: exclusive prefix of candlen over types
-        const int len = len_l;
-        int x = len;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o, 64);
-            if (threadIdx.x >= o) x += y;
-        }
-        if (threadIdx.x < T) soff[threadIdx.x] = x - len;
-        if (blockIdx.x == 0 && threadIdx.x < T) candoff_out[threadIdx.x] = x - len;
-        if (blockIdx.x == 0 && threadIdx.x == T - 1) candoff_out[T] = x;
-    }
-    const unsigned long long lt = lanemask_lt();
-    for (int p = pfirst; p < plast; p++) {
-        const long long base = (long long)pages[p] << PAGE_SHIFT;
-        const int fill = (p == npages - 1) ? tail_fill : PAGE;
-        const bool use_spec = guess_ok && sn <= SPEC_CAP;  // wave-uniform
-        int4 pv[4];
-        uint4 mv[4];
-        if (!use_spec) load_quarter(prio, meta, pbase, pwide, pages[p], fill, w, pv, mv);
-        if (p == 0 && threadIdx.x == 0) ctr->spec_page0 = use_spec ? 1 : 0;
-        for (int c = threadIdx.x; c < 4 * C; c += blockDim.x) wc[c] = 0;
-        __syncthreads();
-        int n = 0;  // this wave's candidates so far (uniform)
-        if (use_spec) {  // filter the list: entries in bins up to the type's threshold
-#pragma unroll
-            for (int k = 0; k < SPEC_CAP / 64; k++) {
-                if (k * 64 >= sn) break;
-                const unsigned int e = se[k];
-                const int col = (int)(e >> 12), ct = col / NB;
-                const bool c = k * 64 + lane < sn && col - ct * NB <= sth[ct];
-                const unsigned long long b = __ballot(c);
-                if (c) {
-                    list[n + __popcll(b & lt)] = e;
-                    atomicAdd(&wc[w * C + col], 1u);
-                }
-                n += __popcll(b);
-            }
-        } else
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
-            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-            bool cnd[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                cnd[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && (long long)pr[q] >= scut[mm[q] & M_TYPE];
-            const unsigned long long b0 = __ballot(cnd[0]), b1 = __ballot(cnd[1]), b2 = __ballot(cnd[2]),
-                                     b3 = __ballot(cnd[3]);
-            if (!(b0 | b1 | b2 | b3)) continue;
-            int pos = n + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (cnd[q]) {
-                    const int t = mm[q] & M_TYPE;
-                    const int col = t * NB + bin_of(sanc[t] - pr[q]);
-                    atomicAdd(&wc[w * C + col], 1u);
-                    list[pos++] = ((unsigned int)col << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
-                }
-            }
-            n += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
-        }
-        // the next page's list, in flight while this page is ranked
-        if (PPB > 1 && p + 1 < plast) {
-            sn = specn[(long long)(p + 1) * 4 + w];
-            const unsigned int *__restrict__ sp = spec + ((long long)(p + 1) * 4 + w) * SPEC_CAP;
-#pragma unroll
-            for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < CPT; r++) {
-            const int c = threadIdx.x + r * 256;
-            if (c < C && (c % NB) <= sth[c / NB]) {
-                unsigned int run = ppv[r];
-#pragma unroll
-                for (int v = 0; v < 4; v++) {
-                    const unsigned int x = wc[v * C + c];
-                    wc[v * C + c] = run;
-                    run += x;
-                }
-                ppv[r] = run;  // the next page's prefix
-            }
-        }
-        __syncthreads();
-        unsigned int *run = wc + w * C;
-        // the fast ranking's per-type constants, uniform over the wave (from LDS once)
-        long long an_u[RT];
-        int th_u[RT], nd_u[RT], len_u[RT];
-        if (fast) {
-#pragma unroll
-            for (int u = 0; u < RT; u++) {
-                const bool ok = u < T;
-                an_u[u] = ok ? sanc[u] : 0;
-                th_u[u] = ok ? sth[u] : -1;
-                nd_u[u] = ok ? sneed[u] : 0;
-                len_u[u] = ok ? slen[u] : 0;
-            }
-        }
-        for (int i0 = 0; i0 < n; i0 += 64) {
-            const int i = i0 + lane;
-            const unsigned int e = i < n ? list[i] : 0u;
-            const int col = (int)(e >> 12), so = (int)(e & (PAGE - 1));
-            // key order = (prio desc, position in the open bucket asc): the bucket
-            // holds its units in wqseqno order, so this is the reference's order.
-            // An exact bin fixes the prio (anchor - bin); only a multi-prio bin reads it.
-            const int ct = col / NB, cb = col - ct * NB;
-            const int pr = i >= n ? 0 : cb < NBX ? (int)(sanc[ct] - cb) : prio[base + so];
-            const unsigned int bpos = ((unsigned int)p << PAGE_SHIFT) | (unsigned int)so;
-            // fast ranking: per type u, the column holding prio pr (exact bins at
-            // or below u's threshold), else -1 (u has no unit of prio pr among its
-            // candidates: all of them are better, or none)
-            int tcol[RT], cnt[RT];
-            if (fast) {
-#pragma unroll
-                for (int u = 0; u < RT; u++) {
-                    const long long bu = an_u[u] - (long long)pr;
-                    tcol[u] = (bu >= 0 && bu <= th_u[u]) ? u * NB + (int)bu : -1;
-                    cnt[u] = 0;
-                }
-            }
-            int rank = 0;
-            const int jn = min(n - i0, 64);
-            for (int j = 0; j < jn; j++) {
-                const int cj = __builtin_amdgcn_readlane(col, j);  // lane j's column (no LDS read per step)
-                const int before = j < lane;
-                rank += before & (cj == col);
-                if (fast) {
-#pragma unroll
-                    for (int u = 0; u < RT; u++) cnt[u] += before & (cj == tcol[u]);
-                }
-            }
-            if (i < n) {
-                const unsigned int r = run[col] + rank;
-                const int t = col / NB, b = col - t * NB;
-                if (b < sth[t] || b >= NBX || (int)r < sneed[t]) {  // exact threshold bin: its first `need` only
-                    const long long at = (long long)soff[t] + binoff[col] + r;
-                    ckey[at] = make_key(pr, bpos);
-                    cslot[at] = (int)(base + so);
-                    if (fast) {
-                        // global rank: per type u, its candidates better than this one
-                        int lb[RT], g = 0;
-#pragma unroll
-                        for (int u = 0; u < RT; u++) {
-                            lb[u] = 0;
-                            if (tcol[u] >= 0) {
-                                int c = (int)run[tcol[u]] + cnt[u];  // units of prio pr earlier in the bucket
-                                if (tcol[u] - u * NB == th_u[u]) c = min(c, nd_u[u]);  // the threshold bin's first `need`
-                                lb[u] = sbo[tcol[u]] + c;
-                            } else if (an_u[u] >= (long long)pr) {
-                                lb[u] = len_u[u];  // every candidate of u is better
-                            }
-                            g += lb[u];
-                        }
-                        crank[at] = ((unsigned int)g << 6) | (unsigned int)t;
-                        if (lv != nullptr && g < R) rtype[g] = (unsigned char)t;
-                        // level rows, sampled every LV_STEP ranks (rtype completes them between samples)
-                        if (lv != nullptr && (g & (LV_STEP - 1)) == 0 && g < R)
-#pragma unroll
-                            for (int u = 0; u < RT; u++)
-                                if (u < T) lv[(long long)(g / LV_STEP) * T + u] = lb[u];
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (i < n) atomicAdd(&run[col], 1u);  // after every lane of the step has read run[]
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (PPB > 1) __syncthreads();  // the next page reuses wc and the lists
-    }
-    if (fast && blockIdx.x == 0 && threadIdx.x == 0) ctr->rank_fast = 1;
-    if (!fast && crank != nullptr && blockIdx.x == 0 && threadIdx.x == 0) ctr->rank_fast = 0;
 }
 
 // ---------------------------------------------------------------- per-type sort (multi-priority bins only)
@@ -2043,85 +1499,7 @@ struct RankSort {
     int fail_test;  // adlbq_set_param("sort_fail_test"): count one timed-out wait (tests the error path)
 };
 
-// The chain's round-0 start guesses, one per segment (T <= 8, ranks from
-// k_select_open): the level state after J untargeted choices, J = requests
-// before the segment's first (warm-up) request that can take an untargeted
-// unit -- what k_chain0 would otherwise find itself with three dependent
-// loads.  Block 0 of k_rank, and only when no request's count was adjusted in
-// this launch (every type has candidates); sg[0] = epoch marks them valid.
-struct SegGuess {
-    int *sg;            // [1 + nseg * T]
-    int nseg, warm;
-    unsigned int epoch;
-};
-
-__device__ void seg_guesses(const SegGuess &g, int T, const int *soff, const int *slen, const int *seg_cnt, int R,
-                            const LevelRows &lr, int *pre /* LDS scratch */, int cap) {
-    const int tid = threadIdx.x, nq = (R + 63) / 64;
-    bool ok = lr.lv != nullptr && T <= 8 && nq + 1 <= cap;
-    for (int t = 0; t < T && ok; t++) ok = slen[t] > 0;  // else k_rank drops requests from seg_cnt
-    if (!ok) {
-        if (tid == 0) g.sg[0] = 0;
-        return;
-    }
-    // exclusive prefix of seg_cnt: thread tid sums a contiguous run, then a block scan of the runs
-    __shared__ int wtot[RANK_TILE / 64];
-    const int per = (nq + blockDim.x - 1) / blockDim.x, q0 = tid * per;
-    int run = 0;
-    for (int q = q0; q < min(nq, q0 + per); q++) run += seg_cnt[q];
-    int x = run;
-    const int lane = tid & 63, w = tid >> 6;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wtot[w] = x;
-    __syncthreads();
-    int acc = x - run;
-    for (int q = 0; q < w; q++) acc += wtot[q];
-    for (int q = q0; q < min(nq, q0 + per); q++) {
-        pre[q] = acc;
-        acc += seg_cnt[q];
-    }
-    if (q0 < nq && q0 + per >= nq) pre[nq] = acc;  // the thread whose run ends the array
-    __syncthreads();
-    const int G = soff[T];
-    for (int s = tid; s < g.nseg; s += blockDim.x) {
-        const int jb = max(0, s * SEG - g.warm);
-        const int J = pre[min(jb >> 6, nq)];
-        const int Js = J & ~(LV_STEP - 1);
-        int extra[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (J > 0 && J < G) {  // type bytes of ranks [Js, J): four 16-byte loads (Js is 64-aligned)
-            const uint4 *rt4 = reinterpret_cast<const uint4 *>(lr.rtype + Js);
-            uint4 v4[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) v4[q] = rt4[q];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const unsigned int wd[4] = {v4[q].x, v4[q].y, v4[q].z, v4[q].w};
-#pragma unroll
-                for (int b = 0; b < 16; b++) {
-                    const int tt = (int)((wd[b >> 2] >> (8 * (b & 3))) & 0xffu);
-                    const bool in = Js + q * 16 + b < J;
-#pragma unroll
-                    for (int u = 0; u < 8; u++) extra[u] += (in && tt == u) ? 1 : 0;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            if (u >= T) break;
-            const int gs = J == 0 ? 0 : J >= G ? slen[u] : min(slen[u], (Js ? lr.lv[(long long)(Js / LV_STEP) * T + u] : 0) + extra[u]);
-            g.sg[1 + s * T + u] = gs;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) g.sg[0] = (int)g.epoch;
-}
-
-// k_rank's arguments (also carried by k_chain0, which runs the same body when
-// the host skipped the k_rank launch and k_select_open did not rank)
+// k_rank's arguments
 struct RankArgs {
     int T;
     const int *candoff, *candlen;
@@ -2135,11 +1513,9 @@ struct RankArgs {
     RankSort rs;
     LevelRows lr;
     const DevCounters *ctr;
-    SegGuess sgv;
 };
 
-// The rank work of workgroup bid of nb (NT threads: k_rank's NT, or a
-// 64-thread k_chain0 workgroup doing it in place of a skipped k_rank launch).
+// The rank work of workgroup bid of nb (NT threads).
 template <int NT>
 __device__ __forceinline__ void rank_body(const RankArgs &ra, const int bid, const int nb) {
     constexpr int NW = NT / 64, SROWS = NW > 3 ? NW : 3;  // span: NW search rows, at least the sort's 24 KB
@@ -2157,7 +1533,6 @@ __device__ __forceinline__ void rank_body(const RankArgs &ra, const int bid, con
     const RankSort &rs = ra.rs;
     const LevelRows &lr = ra.lr;
     const DevCounters *ctr = ra.ctr;
-    const SegGuess &sgv = ra.sgv;
     __shared__ int soff[ADLBQ_MAX_TYPES + 1], slen[ADLBQ_MAX_TYPES], stile[ADLBQ_MAX_TYPES + 1];
     __shared__ unsigned long long span[SROWS][RANK_SPAN];  // also the sort's LDS blocks
     static_assert(sizeof(unsigned long long) * SROWS * RANK_SPAN >= (sizeof(unsigned long long) + sizeof(int)) * SORT_BLK,
@@ -2269,13 +1644,7 @@ __device__ __forceinline__ void rank_body(const RankArgs &ra, const int bid, con
         stile[T] = acc;
     }
     __syncthreads();
-    if (s_fast) {  // k_select_open ranked the candidates and wrote the level rows
-        if (bid == 0 && sgv.sg != nullptr)
-            seg_guesses(sgv, T, soff, slen, seg_cnt, R, lr, reinterpret_cast<int *>(&span[0][0]),
-                        (int)(sizeof(span) / sizeof(int)));
-        return;
-    }
-    if (bid == 0 && sgv.sg != nullptr && tid == 0) sgv.sg[0] = 0;  // the chain computes its own
+    if (s_fast) return;  // k_select_open ranked the candidates and wrote the level rows
     for (int tile = bid; tile < stile[T]; tile += nb) {
         int t = 0;
         while (t + 1 < T && stile[t + 1] <= tile) t++;
@@ -2401,14 +1770,6 @@ struct ChainArgs {
     const int *lv;                   // [R][T] k_rank's level rows (T <= 8), else nullptr
     const unsigned char *rtype;      // [R] type index of the candidate at each global rank (with lv)
     unsigned long long *stamps;      // [nseg][8] s_memrealtime per phase (diagnostic build of the run), or nullptr
-    const int *sg;                   // k_rank's start guesses (SegGuess), valid when sg[0] == sg_epoch; or nullptr
-    unsigned int sg_epoch;
-    int *walked;                     // [nseg] fused finalize: == wepoch for a segment the walk re-solved (or nullptr)
-    unsigned int wepoch;
-    // k_chain0 in place of a skipped k_rank launch (T <= 8): rank_bar[2] = its grid barrier
-    int rank_fuse;
-    int *rank_bar;
-    RankArgs rk;
 };
 
 // diagnostic phase stamps (100 MHz constant clock), lane 0 of a segment
@@ -2864,7 +2225,6 @@ __device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, i
                     __builtin_amdgcn_wave_barrier();  // win is refilled
                     st = seg_solve<TB>(a, q, q * SEG, st, win, true, true, 0, my_off, my_len, rec, rounds_w);
                     redo++;
-                    if (a.walked != nullptr && lane == 0) st_sc1(a.walked + q, (int)a.wepoch);
                 } else {
                     st += dq[i];
                 }
@@ -3163,7 +2523,6 @@ struct FinArgs {
     const int4 *rrec;
     const int *needsort;
     int *sortfail;
-    int *done;  // fused into k_chain0: [0] = the chain epoch once the choices are final
     int *mslot;  // [R] out: the slot request j was given, or -1 (adlbq_unreserve_resp_device reads it back)
     const int2 *rh;  // [R] (rank, hang) as prep_block copied them: 8 B per request instead of a 72 B record stride
     int flat;        // grids up to this size arrive at one counter ("fin_flat"), larger ones by 8 groups
@@ -3311,212 +2670,14 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
     finalize_body(f, blockIdx.x, gridDim.x);
 }
 
-// k_finalize fused into the final k_chain0 launch (every segment one
-// workgroup, all of them resident: the host fuses only small grids).  The
-// launch's last arriver has the exact choices once its walk is done and
-// publishes the chain epoch; every other segment waits for it, then
-// finalizes its own SEG requests (their loads issued together, the three
-// dependent levels umatch -> cslot -> record one after the other), and the
-// last of those arrivals runs the batch tail.  The wait is bounded (one second
-// of wall clock): a segment that gives up answers ADLB_ERROR, never a guess.
-constexpr int FUSE_MAX_SEG = 256;                       // 65,536 Reserves
-constexpr long long FIN_WAIT_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
-
-// The finalize of segment s's SEG requests by one wave: the loads (issued
-// together, the three dependent levels umatch -> cslot -> record one after
-// the other), then the pins, replies and park ballots; the store half returns
-// how many park.  Reads umatch with plain loads: only the wave that last wrote
-// those choices (the segment's own, or the walker) may load them.
-constexpr int FIN_U = SEG / 64;
-struct FinSeg {
-    int rank[FIN_U], hang[FIN_U], slot[FIN_U];
-    int4 c0[FIN_U], c1[FIN_U];
-};
-
-__device__ __forceinline__ void fin_seg_load(const FinArgs &f, int s, FinSeg &g) {
-    const int lane = threadIdx.x, j0 = s * SEG;
-    int tm[FIN_U], um[FIN_U];
-#pragma unroll
-    for (int u = 0; u < FIN_U; u++) {
-        const int j = j0 + u * 64 + lane;
-        const bool in = j < f.R;
-        const int2 rk = in ? f.rh[j] : make_int2(0, 0);
-        g.rank[u] = rk.x;
-        g.hang[u] = rk.y;
-        tm[u] = in ? f.tmatch[j] : -1;
-        um[u] = in ? f.umatch[j] : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < FIN_U; u++) g.slot[u] = tm[u] >= 0 ? tm[u] : (um[u] >= 0 ? f.cslot[um[u]] : -1);
-#pragma unroll
-    for (int u = 0; u < FIN_U; u++) {
-        g.c0[u] = g.slot[u] >= 0 ? f.rrec[2ll * g.slot[u]] : make_int4(0, 0, 0, 0);
-        g.c1[u] = g.slot[u] >= 0 ? f.rrec[2ll * g.slot[u] + 1] : make_int4(0, 0, 0, 0);
-    }
-}
-
-__device__ __forceinline__ int fin_seg_store(const FinArgs &f, int s, const FinSeg &g, bool failed) {
-    const int lane = threadIdx.x, j0 = s * SEG;
-    int parked = 0;
-#pragma unroll
-    for (int u = 0; u < FIN_U; u++) {
-        const int j = j0 + u * 64 + lane;
-        if (j0 + u * 64 >= f.R) break;
-        bool parks = false;
-        if (j < f.R) {
-            const int sl = failed ? -1 : g.slot[u], hg = failed ? 0 : g.hang[u];
-            f.mslot[j] = sl;
-            int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
-            if (failed) {
-                o[0] = -1;  // ADLB_ERROR
-            } else if (sl >= 0) {
-                f.pin[sl] = g.rank[u];  // adlb.c:1210-1212
-                if (g.rank[u] >= 0)
-                    __hip_atomic_fetch_or(f.meta + sl, M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                o[0] = 1;
-                o[1] = g.c1[u].z;
-                o[2] = g.c1[u].w;
-                o[3] = g.c0[u].y;
-                o[4] = g.c0[u].x;
-                o[5] = g.c0[u].z;
-                o[6] = f.my_world;
-                o[7] = g.c0[u].w;
-                o[8] = g.c1[u].x;
-                o[9] = g.c1[u].y;
-            } else if (!hg) {
-                o[0] = -2;  // NO_CURR_WORK
-            }
-            parks = sl < 0 && hg;
-            int *out = f.resp + (long long)ADLBQ_RESP_INTS * j;
-#pragma unroll
-            for (int i = 0; i < 10; i++) out[i] = o[i];
-            if (!parks) {
-                out[10] = -1;
-                out[11] = -1;
-            }
-        }
-        const unsigned long long pb = __ballot(parks);
-        if (lane == 0) __hip_atomic_store(f.pmask + ((j0 >> 6) + u), pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        parked += __popcll(pb);
-    }
-    __builtin_amdgcn_s_waitcnt(0);  // the segment's stores have landed before it arrives
-    return parked;
-}
-
-// One arrival for segment s (wave-uniform result: the batch's parked count, or -1 when not last).
-__device__ __forceinline__ int fin_seg_arrive(const FinArgs &f, int s, int parked, int nseg) {
-    unsigned long long tk = 0;
-    if (threadIdx.x == 0) tk = fin_arrive(f, parked, (unsigned int)nseg, (unsigned int)s);
-    const unsigned int lo = __builtin_amdgcn_readfirstlane((unsigned int)tk),
-                       hi = __builtin_amdgcn_readfirstlane((unsigned int)(tk >> 32));
-    return (lo & 1u) ? (int)hi : -1;
-}
-
-// k_finalize fused into the final k_chain0 launch (every segment one
-// workgroup; the host fuses only grids small enough to be resident at once,
-// since each segment waits here).  Choices are read only by the wave that
-// wrote them last: per-XCD L2s are not coherent, and a segment's own plain
-// stores stay in its XCD's L2.  So the launch's last arriver finalizes the
-// segments its walk re-solved (flagged in `walked`), then publishes the
-// chain epoch; every other segment waits for it and, unless walked,
-// finalizes itself.  The last of the nseg arrivals runs the batch tail.  The
-// wait is bounded (one second of wall clock): a segment that gives up answers
-// ADLB_ERROR, never a guess.
-__device__ __forceinline__ void fin_fused(const FinArgs &f, const int *walked, int s, bool last, unsigned int epoch,
-                                          int nseg) {
-    const int lane = threadIdx.x;
-    int total = -1;
-    bool failed = fin_failed(f);
-    FinSeg mine;
-    if (last) {
-        for (int q0 = 0; q0 < nseg; q0 += 64) {
-            const bool w = q0 + lane < nseg && ld_sc1(walked + q0 + lane) == (int)epoch;
-            for (unsigned long long b = __ballot(w); b; b &= b - 1) {
-                const int q = q0 + __ffsll((long long)b) - 1;
-                FinSeg g;
-                fin_seg_load(f, q, g);
-                const int t = fin_seg_arrive(f, q, fin_seg_store(f, q, g, failed), nseg);
-                if (t >= 0) total = t;
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chain counters went out sc1
-        if (lane == 0) st_sc1(f.done, (int)epoch);
-    } else {
-        fin_seg_load(f, s, mine);  // speculative: used only if the walk leaves this segment alone
-        int ok = 0;
-        if (lane == 0) {
-            const long long t0 = wall_clock64();
-            while (true) {
-                if (ld_sc1(f.done) == (int)epoch) {
-                    ok = 1;
-                    break;
-                }
-                if (wall_clock64() - t0 > FIN_WAIT_TICKS) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        if (!__builtin_amdgcn_readfirstlane(ok)) {
-            if (lane == 0) atomicAdd(&f.ctr->chain_timeouts, 1);
-            failed = true;
-        }
-    }
-    if (ld_sc1(walked + s) != (int)epoch) {  // not re-solved by the walk: this wave holds the choices
-        if (last) fin_seg_load(f, s, mine);
-        const int t = fin_seg_arrive(f, s, fin_seg_store(f, s, mine, failed), nseg);
-        if (t >= 0) total = t;
-    }
-    if (total < 0) return;
-    fin_tail(f, total, failed);  // reads other segments' data only through sc1 / atomic loads
-}
-
-// k_chain0 in place of a k_rank launch the host skipped (T <= 8; the newest
-// landed batch had k_select_open rank every candidate and every type some).
-// When this batch's flags say so too (the usual case) nothing happens here.
-// Otherwise every workgroup (one wave each) runs k_rank's body, then all meet
-// at a grid barrier: each publishes with an agent-scope release before its
-// arrival, each reads after an agent-scope acquire (MI355X_MICROARCH.md,
-// inter-workgroup visibility), since the chain reads what other CUs wrote.  A
-// barrier that does not complete within a second answers the batch
-// ADLB_ERROR (the sort-timeout path).
-constexpr long long RANK_BAR_TICKS = 100ll * 1000 * 1000;  // 100 MHz constant clock
-constexpr int RANK_FUSE_MAX_SEG = 256;  // every workgroup resident for the barrier
-
-__device__ __attribute__((noinline)) void chain_rank_run(const ChainArgs &a, const int bid, const int nb) {
-    const RankArgs &ra = a.rk;
-    rank_body<64>(ra, bid, nb);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int v = __hip_atomic_fetch_add(a.rank_bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v == nb - 1) {  // the last arrival: reset for the next batch, release the others
-            __hip_atomic_store(a.rank_bar, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.rank_bar + 1, (int)ra.rs.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            const long long t0 = wall_clock64();
-            while (__hip_atomic_load(a.rank_bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (int)ra.rs.epoch) {
-                if (wall_clock64() - t0 > RANK_BAR_TICKS) {
-                    atomicAdd(ra.rs.sync + ADLBQ_MAX_TYPES + 1, 1);  // k_finalize answers the batch ADLB_ERROR
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
-
 // Round 0: every segment from its level guess (lane t = type t's head), then
 // passes 2 .. P in the same launch: segment s waits for segment s-1's end of
 // the previous pass and re-solves (seeded) only if it differs from its own
 // start; finally each segment checks its start against its predecessor's last
 // end.  A launch in which every check holds is the fixed point.
-template <int TB, bool RF = false>
-__device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
-                                               int fuse, const int bid_, const int nbk_) {
+template <int TB>
+__device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefix_next, int final, const int bid_,
+                                            const int nbk_) {
     extern __shared__ unsigned int win[];
     const int lane = threadIdx.x, T = a.T, s = bid_, nseg = a.nseg, P = cp.passes;
     chain_stamp(a, s, 0);
@@ -3540,43 +2701,20 @@ __device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefi
     }
     // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
     const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
-    // in place of a k_rank launch: whether k_select_open ranked every candidate and every type has
-    // some (else k_rank's body runs here first), loaded with the rest of the prologue
-    int rk_ns = 0, rk_fast = 1;
-    if (RF && TB <= 8 && a.rank_fuse) {
-        rk_ns = lane < T ? a.rk.rs.needsort[lane] : 0;
-        rk_fast = a.rk.ctr->rank_fast;
-    }
-    // k_rank's guess for this segment, when it made them (one load instead of the three dependent ones below)
-    const bool sg_ok = a.sg != nullptr && a.lv != nullptr && a.sg[0] == (int)a.sg_epoch;
-    const int sg_v = (a.sg != nullptr && lane < T) ? a.sg[1 + s * T + lane] : 0;
     int J = 0;  // requests before jb that take an untargeted unit
-    auto count_J = [&]() {
-        int acc = 0;
+    {
         const int nq = jb >> 6;
         int cv[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) cv[u] = u * 64 + lane < nq ? a.seg_cnt[u * 64 + lane] : 0;
 #pragma unroll
-        for (int u = 0; u < 16; u++) acc += cv[u];
-        for (int q = 1024 + lane; q < nq; q += 64) acc += a.seg_cnt[q];  // batches above 65,536 Reserves
-        return acc;
-    };
-    if (!sg_ok) J = count_J();
-    if constexpr (RF && TB <= 8) {  // RF: the instances with k_rank's body (its call costs the chain registers)
-        const bool need = a.rank_fuse &&
-                          (__ballot(lane < T && (my_len <= 0 || (rk_ns == 1 && my_len > 1))) != 0ull || rk_fast != 1);
-        if (need) {  // the hint did not hold: sorts, ranks, level rows, guess counts first, then the counts again
-            chain_rank_run(a, s, nseg);
-            if (!sg_ok) J = count_J();
-        }
+        for (int u = 0; u < 16; u++) J += cv[u];
+        for (int q = 1024 + lane; q < nq; q += 64) J += a.seg_cnt[q];  // batches above 65,536 Reserves
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
     int guess;
-    if (sg_ok) {
-        guess = sg_v;
-    } else if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
+    if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
         const int G = __builtin_amdgcn_readlane(my_off, T);
         // the row at the sampled rank below J, the rest spread in proportion to the list lengths
         const int Js = J & ~(LV_STEP - 1);
@@ -3639,16 +2777,13 @@ __device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefi
     }
     if (timeouts && lane == 0) atomicAdd(&a.ctr->chain_timeouts, timeouts);
     chain_stamp(a, s, 4);
-    const bool last = chain_arrive<TB>(a, s, start, end - start, solves, bad, rounds, 0, P, final != 0,
-                                       prefix_next != 0, win);
+    chain_arrive<TB>(a, s, start, end - start, solves, bad, rounds, 0, P, final != 0, prefix_next != 0, win);
     chain_stamp(a, s, 5);
-    if (fuse) fin_fused(f, a.walked, s, last, cp.epoch, nseg);
 }
 
-template <int TB, bool RF = false>
-__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final, FinArgs f,
-                                               int fuse) {
-    chain0_body<TB, RF>(a, cp, prefix_next, final, f, fuse, blockIdx.x, gridDim.x);
+template <int TB>
+__global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final) {
+    chain0_body<TB>(a, cp, prefix_next, final, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------- one launch per kernel for a group of handles
@@ -3657,7 +2792,7 @@ __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int pr
 // handle, each handle's arguments in a device table (launch_reserve records
 // them instead of launching: GroupRec).  Blocks past a handle's own grid
 // return at once; every body gets its handle's block index and grid size.
-struct GPrep { PrepArgs pa; int nprep; HistArgs ha; FoldArgs fd; int grid; };
+struct GPrep { PrepArgs pa; int nprep; HistArgs ha; int grid; };
 struct GThr {
     unsigned int *zcs; long long zn; int T; const int *dem; unsigned int *csum; int nchunks;
     int *theta, *need, *candlen, *needsort, *binoff; unsigned int *coltot; int *type_cnt;
@@ -3671,7 +2806,7 @@ struct GSel {
     unsigned char *rtype; int R; int grid;
 };
 struct GRank { RankArgs ra; int grid; };
-struct GChain { ChainArgs a; ChainPass cp; int prefix_next, final, fuse; int grid; FinArgs f; };
+struct GChain { ChainArgs a; ChainPass cp; int prefix_next, final; int grid; };
 struct GFin { FinArgs f; int grid; };
 
 enum : int { GK_PREP = 1, GK_THR = 2, GK_SEL = 4, GK_RANK = 8, GK_CHAIN = 16, GK_FIN = 32 };
@@ -3686,7 +2821,7 @@ template <int TB>
 __global__ __launch_bounds__(256) void k_prep_hist_g(const GPrep *__restrict__ t) {
     const GPrep &g = t[blockIdx.y];
     if ((int)blockIdx.x >= g.grid) return;
-    prep_hist_body<TB>(g.pa, g.nprep, g.ha, g.fd, blockIdx.x, g.grid);
+    prep_hist_body<TB>(g.pa, g.nprep, g.ha, blockIdx.x);
 }
 __global__ __launch_bounds__(TH_THREADS) void k_thresholds_g(const GThr *__restrict__ t) {
     const GThr &g = t[blockIdx.y];
@@ -3707,11 +2842,11 @@ __global__ __launch_bounds__(RANK_TILE) void k_rank_g(const GRank *__restrict__ 
     if ((int)blockIdx.x >= g.grid) return;
     rank_body<RANK_TILE>(g.ra, blockIdx.x, g.grid);
 }
-template <int TB, bool RF>
+template <int TB>
 __global__ __launch_bounds__(64) void k_chain0_g(const GChain *__restrict__ t) {
     const GChain &g = t[blockIdx.y];
     if ((int)blockIdx.x >= g.grid) return;
-    chain0_body<TB, RF>(g.a, g.cp, g.prefix_next, g.final, g.f, g.fuse, blockIdx.x, g.grid);
+    chain0_body<TB>(g.a, g.cp, g.prefix_next, g.final, blockIdx.x, g.grid);
 }
 __global__ __launch_bounds__(256) void k_finalize_g(const GFin *__restrict__ t) {
     const GFin &g = t[blockIdx.y];
@@ -3798,7 +2933,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_chD, sizeof(int) * 2 * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chLP, sizeof(int) * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chE, sizeof(int) * CHAIN_MAX_PASSES * nseg * T1));
-    // [CHAIN_MAX_PASSES][nseg] hand-off flags, then [nseg] the fused finalize's walked segments
+    // [CHAIN_MAX_PASSES][nseg] hand-off flags
     AQ_HIP(hipMalloc((void **)&h->d_chflag, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg));
     AQ_HIP(hipMemsetAsync(h->d_chflag, 0, sizeof(int) * (CHAIN_MAX_PASSES + 1) * nseg, h->stream));  // epochs start at 1
     AQ_HIP(hipMalloc((void **)&h->d_chGT, sizeof(int) * CH_GROUPS * T1));
@@ -3811,9 +2946,6 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMemsetAsync(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 1), h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_lv, sizeof(int) * 8 * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_rtype, (size_t)nc + 64));
-    if (h->d_sg) AQ_HIP(hipFree(h->d_sg));
-    AQ_HIP(hipMalloc((void **)&h->d_sg, sizeof(int) * (1 + 8 * nseg)));
-    AQ_HIP(hipMemsetAsync(h->d_sg, 0, sizeof(int), h->stream));
     h->cap_req = nc;
     return ADLBQ_OK;
 }
@@ -3829,12 +2961,6 @@ static int ensure_scan_capacity(adlbq_server *h, int npages) {
         h->cap_gh = std::max(need_gh, 2 * h->cap_gh);
         AQ_HIP(hipMalloc((void **)&h->d_gh, sizeof(unsigned short) * h->cap_gh));
 
-    }
-    if (nchunks + 1 > h->cap_arrive) {  // pass 1's per-chunk arrival counters (each chunk's last page resets its own)
-        if (h->d_arrive) AQ_HIP(hipFree(h->d_arrive));
-        h->cap_arrive = std::max(nchunks + 1, 2 * h->cap_arrive);
-        AQ_HIP(hipMalloc((void **)&h->d_arrive, sizeof(int) * h->cap_arrive));
-        AQ_HIP(hipMemsetAsync(h->d_arrive, 0, sizeof(int) * h->cap_arrive, h->stream));
     }
     if (need_cs > h->cap_csum) {
         if (h->d_csum) AQ_HIP(hipFree(h->d_csum));
@@ -3882,71 +3008,41 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     const int par = h->csum_par;
     unsigned int *csum = h->d_csum + (long long)par * h->cap_csum, *zcs = h->d_csum + (long long)(par ^ 1) * h->cap_csum;
     HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
-                      h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, 0, zcs, h->csum_used[par ^ 1],
-                      0, h->hist_variant, pg0};
+                h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, zcs, h->csum_used[par ^ 1], pg0};
     if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
         h->csum_used[par] = (long long)((np + CHUNK - 1) / CHUNK) * C;
         h->csum_used[par ^ 1] = 0;
         h->csum_par = par ^ 1;
     }
-    ha.arrive = h->hist_arrive ? h->d_arrive : nullptr;
-    const int ppb = 1;  // pages per pass-1 workgroup
-    const int npb = (np + ppb - 1) / ppb;
-    ha.zper = npb > 0 ? (int)((ha.zn + npb - 1) / npb) : 0;
+    const int npb = np;  // one page per pass-1 workgroup
     const int grid = nprep + (scan ? npb : 0);
-    // k_thresholds folded into pass 1's last workgroups: 8 columns per role (4..64), every role a workgroup
-    FoldArgs fd{};
-    // fold_thresholds 1: always; 2: on queues of at most FOLD_AUTO_PAGES pages (a launch saved
-    // weighs more than the folded tail there; measured slower on the 10M-unit metric queue)
-    if (scan && (h->fold_thresholds == 1 || (h->fold_thresholds == 2 && np <= FOLD_AUTO_PAGES)) && !h->split_prep) {
-        const int C1 = T * NB;
-        int ncol = 8;
-        while (ncol < 64 && C1 / ncol > grid) ncol *= 2;
-        if (C1 / ncol <= grid && C1 % ncol == 0) {
-            const int nchunks = (np + CHUNK - 1) / CHUNK;
-            if (!h->d_fold) {
-                AQ_HIP(hipMalloc((void **)&h->d_fold, sizeof(int) * (FOLD_MAX_NL + 2)));
-                AQ_HIP(hipMemsetAsync(h->d_fold, 0, sizeof(int) * (FOLD_MAX_NL + 2), s));
-            }
-            fd = FoldArgs{C1 / ncol <= FOLD_MAX_NL ? 1 : 0, h->d_fold, grid, C1 / ncol, nchunks, h->d_dem, h->d_theta,
-                          h->d_need, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt,
-                          h->d_anchor, h->d_anchor_next, h->d_gcut_next, nprep > 0 ? 1 : 0,
-                          h->d_rank_sync + ADLBQ_MAX_TYPES + 1, zcs, ha.zn};
-        }
-    }
     if (grid > 0) {
         // pass 1: the histogram copies, then the four waves' speculative lists
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0,
                                       scan ? sizeof(unsigned int) * (HK * C + 4 * SPEC_CAP) : 0);
         stage_begin(h, "hist", &ev);
         auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
-        if (h->hist_diag && scan) {  // diagnostic: extra passes 1 (no epilogue) with parts skipped, before the real one
-            HistArgs hd = ha;
-            hd.diag = (h->hist_diag & 0xff) | 2;
-            hd.zn = 0;
-            for (int r = 0; r < std::max(1, h->hist_diag >> 8); r++) kph<<<npb, 256, lds, s>>>(pa, 0, hd, FoldArgs{});
-        }
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
-            kph<<<nprep, 256, lds, s>>>(pa, nprep, ha, FoldArgs{});
-            kph<<<npb, 256, lds, s>>>(pa, 0, ha, FoldArgs{});
+            kph<<<nprep, 256, lds, s>>>(pa, nprep, ha);
+            kph<<<npb, 256, lds, s>>>(pa, 0, ha);
         } else if (h->grec) {  // adlbq_reserve_group_device: recorded, launched with the group's
             h->grec->kinds |= GK_PREP;
             h->grec->tb = T <= 4 ? 4 : 8;
-            h->grec->prep = GPrep{pa, nprep, ha, fd, grid};
+            h->grec->prep = GPrep{pa, nprep, ha, grid};
             h->grec->lds_prep = (size_t)lds;
         } else {
-            kph<<<grid, 256, lds, s>>>(pa, nprep, ha, fd);
+            kph<<<grid, 256, lds, s>>>(pa, nprep, ha);
         }
         stage_end(h, "hist", ev);
     }
     if (scan) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
-        if (!fd.on && h->grec) {
+        if (h->grec) {
             h->grec->kinds |= GK_THR;
             h->grec->thr = GThr{zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                 h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor, h->d_anchor_next,
                                 h->d_gcut_next, nprep > 0 ? 1 : 0, C};
-        } else if (!fd.on) {
+        } else {
             stage_begin(h, "thresholds", &ev);
             k_thresholds<<<C, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need,
                                                   h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot,
@@ -3955,10 +3051,8 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             stage_end(h, "thresholds", ev);
         }
         stage_begin(h, "select", &ev);
-        const bool chunked = h->select_chunk && T <= 8;  // one workgroup per chunk of pages
-        auto sel = chunked ? (T <= 4 ? k_select_chunk<4> : k_select_chunk<8>)
-                           : T <= 4 ? k_select_open<4> : T <= 8 ? k_select_open<8> : k_select_open<64>;
-        if (h->grec && !chunked) {
+        auto sel = T <= 4 ? k_select_open<4> : T <= 8 ? k_select_open<8> : k_select_open<64>;
+        if (h->grec) {
             h->grec->kinds |= GK_SEL;
             h->grec->sel = GSel{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor,
                                 h->d_theta, h->d_need, h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff,
@@ -3967,7 +3061,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                                 (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R, np};
             h->grec->lds_sel = sizeof(unsigned int) * (4 * C + 4 * 1024);
         } else
-        sel<<<chunked ? nchunks : np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
+        sel<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
             h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr,
@@ -4299,26 +3393,8 @@ __global__ __launch_bounds__(1024) void k_segsort_short(SegList sl, int from, un
     }
 }
 
-__global__ void k_segsort_bounds(SegList sl, int from, int *sbeg, int *send) {
-    const int q = from + threadIdx.x;
-    if (q >= sl.n) return;
-    sbeg[q - from] = sl.beg[q];
-    send[q - from] = sl.end[q];
-}
-
-// Multi-prio-bin candidate lists sorted before k_rank (64-bit keys,
-// descending).  The list bounds are read back first (one stream sync).  When
-// no list's keys differ in their top 6 bits (k_keybits), every list is sorted
-// by ONE device-wide radix sort over all candidates, the type index in those
-// bits and only the bits some list varies in sorted ("segsort_merged", the
-// default).  Otherwise lists
-// of at least segsort_wide entries get a device-wide radix sort each, spread
-// over every CU, the shorter ones share one segmented sort (a block per
-// list).  One segmented sort over every list ran the few large ones in one
-// block each: 2.8 ms of a config-4 step.
-// Per-type OR / AND of the candidate keys (kb[t] = OR, kb[64 + t] = AND):
-// the bits a list's keys differ in, so launch_segsort can sort every list in
-// one device-wide radix sort with the list index in constant top bits.
+// Per-type OR / AND of the candidate keys (kb[t] = OR, kb[64 + t] = AND): the
+// bits a list's keys differ in (the sync-free radix sort's plan, k_sort_plan).
 __global__ __launch_bounds__(256) void k_keybits(const int *__restrict__ candoff, const int *__restrict__ candlen,
                                                  const unsigned long long *__restrict__ key,
                                                  unsigned long long *kb) {
@@ -4340,43 +3416,11 @@ __global__ __launch_bounds__(256) void k_keybits(const int *__restrict__ candoff
     }
 }
 
-constexpr int LIST_SHIFT = 58;  // list index bits of a merged sort key (T <= 64)
-constexpr unsigned long long LIST_LOW = (1ull << LIST_SHIFT) - 1;
+constexpr int LIST_SHIFT = 58;  // a list whose keys vary at or above this bit cannot be planned
 
-// key -> (63 - t) << 58 | low bits: a descending sort keeps type t's list at
-// its own offsets, in preference order
-__global__ __launch_bounds__(256) void k_merge_keys(const int *__restrict__ candoff, const int *__restrict__ candlen,
-                                                    const unsigned long long *__restrict__ key,
-                                                    unsigned long long *mkey) {
-    const int t = blockIdx.y, b = candoff[t], e = b + candlen[t];
-    const unsigned long long top = (unsigned long long)(63 - t) << LIST_SHIFT;
-    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x)
-        mkey[i] = top | (key[i] & LIST_LOW);
-}
-
-// sorted merged keys back, with each list's constant top bits; needsort 2
-__global__ __launch_bounds__(256) void k_unmerge_keys(const int *__restrict__ candoff,
-                                                      const int *__restrict__ candlen,
-                                                      const unsigned long long *__restrict__ kb,
-                                                      const unsigned long long *mkey,  // may be `key`
-                                                      const int *__restrict__ s2, unsigned long long *key, int *slot,
-                                                      int *needsort) {
-    const int t = blockIdx.y, b = candoff[t], e = b + candlen[t];
-    const unsigned long long top = kb[ADLBQ_MAX_TYPES + t] & ~LIST_LOW;
-    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x) {
-        key[i] = top | (mkey[i] & LIST_LOW);
-        slot[i] = s2[i];
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && needsort[t] == 1) needsort[t] = 2;
-}
-
-// The merged sort without a host read-back: the host sizes it from the last
-// landed batch's plan (G_bound candidates, key bits from lo_hint up); this
-// kernel checks the plan against this batch (every list's keys constant in the
-// top bits, G <= G_bound, no key varying below lo_hint) and records this
-// batch's own figures for the next one.  If the plan does not hold,
-// k_unmerge_plan leaves the lists alone and k_rank sorts them inside its launch
-// (needsort stays 1), so a stale plan costs time, never results.
+// A read-back sort's figures for the next batch's sync-free radix sort
+// (launch_segsort_radix): candidates in all, lowest key bit any list varies
+// in, highest prio-field bit.
 __global__ void k_sort_plan(int T, const int *__restrict__ candoff, const int *__restrict__ candlen,
                             const int *__restrict__ needsort, const unsigned long long *__restrict__ kb, int g_bound,
                             int lo_hint, int *plan, DevCounters *ctr) {
@@ -4402,79 +3446,6 @@ __global__ void k_sort_plan(int T, const int *__restrict__ candoff, const int *_
         ctr->plan_g = G;
         ctr->plan_lo = ok ? lo : 0;
     }
-}
-
-// merged keys of every list (k_merge_keys), and sentinel keys (0: last in a
-// descending sort) from G up to the planned bound
-__global__ __launch_bounds__(256) void k_merge_pad(const int *__restrict__ plan, int g_bound,
-                                                   unsigned long long *mkey) {
-    for (int i = plan[1] + blockIdx.x * blockDim.x + threadIdx.x; i < g_bound; i += gridDim.x * blockDim.x)
-        mkey[i] = 0ull;
-}
-
-__global__ __launch_bounds__(256) void k_unmerge_plan(const int *__restrict__ plan, const int *__restrict__ candoff,
-                                                      const int *__restrict__ candlen,
-                                                      const unsigned long long *__restrict__ kb,
-                                                      const unsigned long long *__restrict__ mkey,
-                                                      const int *__restrict__ s2, unsigned long long *key, int *slot,
-                                                      int *needsort) {
-    if (!plan[0]) return;  // k_rank sorts the lists that need it
-    const int t = blockIdx.y, b = candoff[t], e = b + candlen[t];
-    const unsigned long long top = kb[ADLBQ_MAX_TYPES + t] & ~LIST_LOW;
-    for (int i = b + blockIdx.x * blockDim.x + threadIdx.x; i < e; i += gridDim.x * blockDim.x) {
-        key[i] = top | (mkey[i] & LIST_LOW);
-        slot[i] = s2[i];
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && needsort[t] == 1) needsort[t] = 2;
-}
-
-// the sync-free merged sort (see k_sort_plan); false when no plan has landed yet
-static int launch_segsort_planned(adlbq_server *h, bool *done) {
-    *done = false;
-    int g_last = 0, lo_last = 0;
-    if (!h->segsort_merged || !h->segsort_async || !plan_hint(h, &g_last, &lo_last)) return ADLBQ_OK;
-    const int T = h->T;
-    hipStream_t s = h->stream;
-    const long long gb = std::min<long long>(h->cap_cand, (long long)g_last + g_last / 4 + 4096);
-    const int g_bound = (int)gb;
-    const int lo_hint = std::max(0, (lo_last & ~7) - 8);  // a digit of margin; lower bits cost a pass each
-    if (gb > h->cap_c3) {
-        AQ_HIP(hipStreamSynchronize(s));
-        if (h->d_ckey3) AQ_HIP(hipFree(h->d_ckey3));
-        if (h->d_cslot3) AQ_HIP(hipFree(h->d_cslot3));
-        h->cap_c3 = std::max(gb, h->cap_cand / 4);
-        h->cap_c3 = std::min(h->cap_c3, h->cap_cand);
-        AQ_HIP(hipMalloc((void **)&h->d_ckey3, sizeof(unsigned long long) * h->cap_c3));
-        AQ_HIP(hipMalloc((void **)&h->d_cslot3, sizeof(int) * h->cap_c3));
-    }
-    if (!h->d_plan) AQ_HIP(hipMalloc((void **)&h->d_plan, sizeof(int) * 4));
-    // (a plan can land from a keyrank batch that failed over, before any read-back sort allocated this)
-    if (!h->d_kb) AQ_HIP(hipMalloc((void **)&h->d_kb, sizeof(unsigned long long) * 2 * ADLBQ_MAX_TYPES));
-    const int kgx = 16;
-    AQ_HIP(hipMemsetAsync(h->d_kb, 0, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
-    AQ_HIP(hipMemsetAsync(h->d_kb + ADLBQ_MAX_TYPES, 0xff, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
-    k_keybits<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_kb);
-    k_sort_plan<<<1, 64, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_needsort, h->d_kb, g_bound, lo_hint, h->d_plan,
-                                 h->d_ctr);
-    k_merge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_ckey2);
-    k_merge_pad<<<std::min(1024, (g_bound + 255) / 256 + 1), 256, 0, s>>>(h->d_plan, g_bound, h->d_ckey2);
-    const size_t tmp = rsx_temp_bytes(g_bound);
-    if (tmp > h->cap_ssort) {
-        AQ_HIP(hipStreamSynchronize(s));
-        if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
-        h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
-        AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
-    }
-    int rc;
-    if ((rc = rsx_sort_pairs(h->d_ssort, h->cap_ssort, h->d_ckey2, h->d_ckey3, h->d_cslot, h->d_cslot3, g_bound, lo_hint,
-                             64, true, s)))
-        return rc;
-    k_unmerge_plan<<<dim3(kgx, T), 256, 0, s>>>(h->d_plan, h->d_candoff, h->d_candlen, h->d_kb, h->d_ckey3,
-                                                 h->d_cslot3, h->d_ckey, h->d_cslot, h->d_needsort);
-    AQ_HIP(hipGetLastError());
-    h->n_sort_async++;
-    *done = true;
-    return ADLBQ_OK;
 }
 
 // ---------------------------------------------------------------- list-stable radix sort
@@ -4741,7 +3712,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(RsArgs a, int pass, i
 static int launch_segsort_radix(adlbq_server *h, bool *done) {
     *done = false;
     int g_last = 0, lo_last = 0, phi_last = -1;
-    if (!h->segsort_radix || !h->segsort_async || !plan_hint(h, &g_last, &lo_last, &phi_last)) return ADLBQ_OK;
+    if (!plan_hint(h, &g_last, &lo_last, &phi_last)) return ADLBQ_OK;
     const int T = h->T;
     if (T < 1 || T > ADLBQ_MAX_TYPES) return ADLBQ_OK;
     const int tb = T > 1 ? 32 - __builtin_clz((unsigned int)(T - 1)) : 0;
@@ -4794,75 +3765,41 @@ static int launch_segsort_radix(adlbq_server *h, bool *done) {
         std::swap(I0, I1);
     }
     AQ_HIP(hipGetLastError());
-    h->n_sort_async++;
     h->n_sort_radix++;
     *done = true;
     return ADLBQ_OK;
 }
 
+// The lists of multi-priority thresholds sorted after a read-back of their
+// bounds (no plan from a landed batch yet): each long list by a device-wide
+// radix sort of its own, the short ones one workgroup each.  The keys' varying
+// bits are recorded (k_keybits, k_sort_plan) for the next batch's sync-free
+// radix sort.
+constexpr int SEGSORT_WIDE = 16384;  // a list this long or longer gets a device-wide sort of its own
+
 static int launch_segsort(adlbq_server *h) {
     const int T = h->T;
     hipStream_t s = h->stream;
     if (!h->d_kb) AQ_HIP(hipMalloc((void **)&h->d_kb, sizeof(unsigned long long) * 2 * ADLBQ_MAX_TYPES));
-    const int kgx = 16;  // blocks per list of the key passes
-    if (h->segsort_merged) {
-        AQ_HIP(hipMemsetAsync(h->d_kb, 0, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
-        AQ_HIP(hipMemsetAsync(h->d_kb + ADLBQ_MAX_TYPES, 0xff, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
-        k_keybits<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_kb);
-        // this batch's plan figures for the next batch's sync-free path (plan[0] unused here)
-        if (!h->d_plan) AQ_HIP(hipMalloc((void **)&h->d_plan, sizeof(int) * 4));
-        k_sort_plan<<<1, 64, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_needsort, h->d_kb, 0, 64, h->d_plan, h->d_ctr);
-        AQ_HIP(hipGetLastError());
-    }
+    const int kgx = 16;  // blocks per list of the key pass
+    AQ_HIP(hipMemsetAsync(h->d_kb, 0, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
+    AQ_HIP(hipMemsetAsync(h->d_kb + ADLBQ_MAX_TYPES, 0xff, sizeof(unsigned long long) * ADLBQ_MAX_TYPES, s));
+    k_keybits<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_kb);
+    if (!h->d_plan) AQ_HIP(hipMalloc((void **)&h->d_plan, sizeof(int) * 4));
+    k_sort_plan<<<1, 64, 0, s>>>(T, h->d_candoff, h->d_candlen, h->d_needsort, h->d_kb, 0, 64, h->d_plan, h->d_ctr);
+    AQ_HIP(hipGetLastError());
     std::vector<int> hb(3 * (size_t)T + 1);
-    std::vector<unsigned long long> kb(2 * ADLBQ_MAX_TYPES);
     AQ_HIP(hipMemcpyAsync(hb.data(), h->d_candoff, sizeof(int) * (T + 1), hipMemcpyDeviceToHost, s));
     AQ_HIP(hipMemcpyAsync(hb.data() + T + 1, h->d_candlen, sizeof(int) * T, hipMemcpyDeviceToHost, s));
     AQ_HIP(hipMemcpyAsync(hb.data() + 2 * T + 1, h->d_needsort, sizeof(int) * T, hipMemcpyDeviceToHost, s));
-    if (h->segsort_merged)
-        AQ_HIP(hipMemcpyAsync(kb.data(), h->d_kb, sizeof(unsigned long long) * 2 * ADLBQ_MAX_TYPES,
-                              hipMemcpyDeviceToHost, s));
     AQ_HIP(hipStreamSynchronize(s));
-    if (h->segsort_merged) {
-        // one sort of every list when no list's keys differ in the top bits
-        const int G = hb[T];
-        int nsort = 0, lo = 64;
-        bool ok = G > 1;
-        for (int t = 0; t < T && ok; t++) {
-            if (hb[T + 1 + t] == 0) continue;
-            const unsigned long long diff = kb[t] ^ kb[ADLBQ_MAX_TYPES + t];
-            ok = (diff >> LIST_SHIFT) == 0;
-            if (diff) lo = std::min(lo, __builtin_ctzll(diff));
-            nsort += hb[2 * T + 1 + t] == 1 && hb[T + 1 + t] > 1;
-        }
-        if (nsort == 0) return ADLBQ_OK;
-        if (ok) {
-            if (lo >= LIST_SHIFT) lo = LIST_SHIFT;  // every list is constant: the sort only keeps lists apart
-            const size_t tmp = rsx_temp_bytes(G);
-            if (tmp > h->cap_ssort) {
-                if (h->d_ssort) AQ_HIP(hipFree(h->d_ssort));
-                h->cap_ssort = std::max(tmp, 2 * h->cap_ssort);
-                AQ_HIP(hipMalloc(&h->d_ssort, h->cap_ssort));
-            }
-            k_merge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_ckey, h->d_ckey2);
-            int rc;
-            if ((rc = rsx_sort_pairs(h->d_ssort, h->cap_ssort, h->d_ckey2, h->d_ckey, h->d_cslot, h->d_cslot2, G, lo,
-                                     64, true, s)))
-                return rc;
-            k_unmerge_keys<<<dim3(kgx, T), 256, 0, s>>>(h->d_candoff, h->d_candlen, h->d_kb, h->d_ckey, h->d_cslot2,
-                                                        h->d_ckey, h->d_cslot, h->d_needsort);
-            AQ_HIP(hipGetLastError());
-            h->n_segsort += nsort;
-            return ADLBQ_OK;
-        }
-    }
     // wide lists first, then the short ones
     SegList sl{};
     int maxlen = 0, nwide = 0;
     for (int pass = 0; pass < 2; pass++)
         for (int t = 0; t < T; t++) {
             const int off = hb[t], len = hb[T + 1 + t], ns = hb[2 * T + 1 + t];
-            if (ns != 1 || len < 2 || (len >= h->segsort_wide) != (pass == 0)) continue;
+            if (ns != 1 || len < 2 || (len >= SEGSORT_WIDE) != (pass == 0)) continue;
             sl.type[sl.n] = t;
             sl.beg[sl.n] = off;
             sl.end[sl.n] = off + len;
@@ -4872,10 +3809,6 @@ static int launch_segsort(adlbq_server *h) {
         }
     if (sl.n == 0) return ADLBQ_OK;
     h->n_segsort += nwide;
-    if (!h->d_sbeg) {
-        AQ_HIP(hipMalloc((void **)&h->d_sbeg, sizeof(int) * ADLBQ_MAX_TYPES));
-        AQ_HIP(hipMalloc((void **)&h->d_send, sizeof(int) * ADLBQ_MAX_TYPES));
-    }
     const int nshort = sl.n - nwide;
     if (nwide > 0) {
         const size_t tmp = rsx_temp_bytes(maxlen);
@@ -4900,13 +3833,13 @@ static int launch_segsort(adlbq_server *h) {
     return ADLBQ_OK;
 }
 
-// k_finalize's arguments for a batch (its own launch, or fused into the final k_chain0 launch)
+// k_finalize's arguments for a batch
 static FinArgs fin_args(adlbq_server *h, int R, const int *d_reqs, int *d_resp, DevCounters *snap) {
     return FinArgs{d_reqs, R, h->d_tmatch, h->d_umatch, h->d_cslot, h->d_meta, h->d_pin, h->my_world, d_resp,
                    h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
                    h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, h->T, snap, h->snap_tag[h->snap_next],
                    h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
-                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_chclean + 1, h->d_mslot, h->d_rh, h->fin_flat};
+                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_mslot, h->d_rh, h->fin_flat};
 }
 
 // the host side of a batch in flight: its snapshot slot, counts, upper bounds
@@ -4944,7 +3877,7 @@ static int launch_recorded(adlbq_server *h, GroupRec &r) {
     const bool t4 = r.tb == 4;
     if (r.kinds & GK_PREP) {
         auto kph = t4 ? k_prep_hist<4> : k_prep_hist<8>;
-        kph<<<r.prep.grid, 256, r.lds_prep, s>>>(r.prep.pa, r.prep.nprep, r.prep.ha, r.prep.fd);
+        kph<<<r.prep.grid, 256, r.lds_prep, s>>>(r.prep.pa, r.prep.nprep, r.prep.ha);
     }
     if (r.kinds & GK_THR) {
         const GThr &g = r.thr;
@@ -4963,8 +3896,7 @@ static int launch_recorded(adlbq_server *h, GroupRec &r) {
     if (r.kinds & GK_RANK) k_rank<<<r.rank.grid, RANK_TILE, 0, s>>>(r.rank.ra);
     if (r.kinds & GK_CHAIN) {
         const GChain &g = r.chain;
-        auto ch = g.a.rank_fuse ? (t4 ? k_chain0<4, true> : k_chain0<8, true>) : (t4 ? k_chain0<4> : k_chain0<8>);
-        ch<<<g.grid, 64, r.lds_chain, s>>>(g.a, g.cp, g.prefix_next, g.final, g.f, g.fuse);
+        (t4 ? k_chain0<4> : k_chain0<8>)<<<g.grid, 64, r.lds_chain, s>>>(g.a, g.cp, g.prefix_next, g.final);
     }
     if (r.kinds & GK_FIN) k_finalize<<<r.fin.grid, 256, 0, s>>>(r.fin.f);
     r.kinds = 0;
@@ -5074,26 +4006,19 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_begin(h, "sort", &ev);
         bool planned = false;
         if ((rc = launch_segsort_radix(h, &planned))) return rc;
-        if (!planned && (rc = launch_segsort_planned(h, &planned))) return rc;
         if (!planned && (rc = launch_segsort(h))) return rc;
         stage_end(h, "sort", ev);
     }
     hsec("sort", st0);
-    // T <= 8 with a small enough grid: no k_rank launch, k_chain0 runs its body when needed
-    const int nseg0 = (R + SEG - 1) / SEG;
-    const bool rank_fused = np > 0 && T > 0 && T <= 8 && h->fuse_rank && !h->fuse_finalize && !h->seg_guess &&
-                            !h->rank_grid && nseg0 <= RANK_FUSE_MAX_SEG && (h->fuse_rank == 2 || rank_skip_hint(h));
     RankArgs rka{};
     if (np > 0 && T > 0) {
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
         const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch,
                           h->sort_fail_test};
-        const int warm0 = T <= 8 ? (h->chain_warm >= 0 ? h->chain_warm : CHAIN_WARM) : 0;
-        const SegGuess sgv{(T <= 8 && h->seg_guess) ? h->d_sg : nullptr, (R + SEG - 1) / SEG, warm0, h->rank_epoch};
         // chunk sums: zeroed by the next scan
         rka = RankArgs{T, h->d_candoff, h->d_candlen, h->d_ckey, h->d_crank, nullptr, 0, h->d_mask, h->d_tmatch, R,
-                       h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr, sgv};
-        if (!rank_fused) {
+                       h->d_seg_cnt, rs, LevelRows{T <= 8 ? h->d_lv : nullptr, R, h->d_rtype}, h->d_ctr};
+        {
             stage_begin(h, "rank", &ev);
             // a small grid when the last landed batch was ranked in k_select_open (every loop is
             // grid-strided: any grid is correct, the hint only sizes it)
@@ -5116,12 +4041,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         }
     }
     hsec("l_rank", hl);
-    // k_finalize's arguments (its own launch, or fused into the final k_chain0 launch)
+    // k_finalize's arguments
     DevCounters *const snap = h->d_snap + h->snap_next;
     h->snap_tag[h->snap_next] = ++h->snap_tags;
     __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);  // not landed until k_finalize stores it
     const FinArgs fa = fin_args(h, R, d_reqs, d_resp, snap);
-    bool fused = false;
     stage_begin(h, "chain", &ev);
     {
         const int nseg = (R + SEG - 1) / SEG;
@@ -5140,8 +4064,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, warm, gs, h->d_candoff, h->d_candlen, h->d_crank,
                      h->d_umatch, h->d_cht, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chS + nsT, h->d_chD + nsT,
                      h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_chcnt, h->d_ctr,
-                     (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr,
-                     (T <= 8 && np > 0 && h->seg_guess) ? h->d_sg : nullptr, h->rank_epoch, nullptr, 0u};
+                     (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr};
         if (h->chain_stamps) {
             if (nseg > h->cap_stamps) {
                 AQ_HIP(hipStreamSynchronize(s));
@@ -5166,28 +4089,13 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         else if (T <= 8) lds = sizeof(unsigned int) * (8 * (SEG + warm) + 64) + 9 * (SEG + warm);
         else lds = sizeof(unsigned int) * T * SEG + sizeof(TypeRec) * ADLBQ_MAX_TYPES;
         auto mode_of = [&](int k) { return (k >= 1 && k <= K) ? (int)(((unsigned long long)modes >> (k - 1)) & 1ull) : 0; };
-        // the finalize rides in k_chain0 when that launch is the final one and its
-        // grid is small enough to be resident at once (each segment waits there)
-        fused = h->fuse_finalize && K == 0 && T <= 8 && nseg <= FUSE_MAX_SEG;
-        if (fused) {
-            ca.walked = h->d_chflag + (size_t)CHAIN_MAX_PASSES * ((h->cap_req + SEG - 1) / SEG);
-            ca.wepoch = h->chain_epoch;
-        }
-        if (rank_fused) {
-            ca.rank_fuse = 1;
-            ca.rank_bar = h->d_rank_sync + ADLBQ_MAX_TYPES + 2;
-            ca.rk = rka;
-        }
-        if (h->grec) {  // T <= 8, no round launches, no fused finalize (group_eligible)
+        if (h->grec) {  // T <= 8, no round launches (group_eligible)
             h->grec->kinds |= GK_CHAIN;
-            h->grec->chain = GChain{ca, cp, mode_of(1), K == 0 ? 1 : 0, 0, nseg, fa};
+            h->grec->chain = GChain{ca, cp, mode_of(1), K == 0 ? 1 : 0, nseg};
             h->grec->lds_chain = lds;
-        } else if (rank_fused) {
-            if (T <= 4) k_chain0<4, true><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
-            else k_chain0<8, true><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
-        } else if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
-        else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, fused);
-        else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0, fa, 0);
+        } else if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
+        else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
+        else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
         for (int k = 1; k <= K; k++) {
             flip(k);
             const int mode = mode_of(k), pn = mode_of(k + 1);
@@ -5202,7 +4110,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if (h->grec) {
         h->grec->kinds |= GK_FIN;
         h->grec->fin = GFin{fa, (R + 255) / 256};
-    } else if (!fused) {
+    } else {
         k_finalize<<<(R + 255) / 256, 256, 0, s>>>(fa);
     }
     stage_end(h, "finalize", ev);
@@ -5339,8 +4247,8 @@ int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail) {
 // non-empty open bucket, no round launches after k_chain0, no diagnostics.
 static bool group_eligible(const adlbq_server *h) {
     const int K = h->chain_rounds >= 0 ? h->chain_rounds : 0;
-    return h->T > 0 && h->T <= 8 && !h->open.pages.empty() && K == 0 && !h->hist_diag && !h->split_prep &&
-           !h->select_chunk && !h->chain_stamps;
+    return h->T > 0 && h->T <= 8 && !h->open.pages.empty() && K == 0 && !h->split_prep &&
+           !h->chain_stamps;
 }
 
 static size_t gt_align(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -5380,7 +4288,6 @@ static int run_group(adlbq_server *const *hs, std::vector<GroupRec> &rec, const 
     auto *tc = reinterpret_cast<GChain *>(hb + o_chain);
     auto *tf = reinterpret_cast<GFin *>(hb + o_fin);
     int gp = 0, gt = 0, gs = 0, gr = 0, gc = 0, gf = 0;
-    bool rf = false;  // some member ranks inside k_chain0 (the instance with k_rank's body)
     size_t lp = 0, lsel = 0, lc = 0;
     for (int j = 0; j < k; j++) {
         const GroupRec &r = rec[(size_t)m[(size_t)j]];
@@ -5405,7 +4312,6 @@ static int run_group(adlbq_server *const *hs, std::vector<GroupRec> &rec, const 
         lp = std::max(lp, r.lds_prep);
         lsel = std::max(lsel, r.lds_sel);
         lc = std::max(lc, r.lds_chain);
-        rf = rf || ((r.kinds & GK_CHAIN) && r.chain.a.rank_fuse);
     }
     char *d = L->d_gtab;
     AQ_HIP(hipMemcpyAsync(d, hb, total, hipMemcpyHostToDevice, ls));
@@ -5415,8 +4321,7 @@ static int run_group(adlbq_server *const *hs, std::vector<GroupRec> &rec, const 
     if (gt) k_thresholds_g<<<dim3(gt, k), TH_THREADS, 0, ls>>>(reinterpret_cast<const GThr *>(d + o_thr));
     if (gs) (t4 ? k_select_open_g<4> : k_select_open_g<8>)<<<dim3(gs, k), 256, lsel, ls>>>(reinterpret_cast<const GSel *>(d + o_sel));
     if (gr) k_rank_g<<<dim3(gr, k), RANK_TILE, 0, ls>>>(reinterpret_cast<const GRank *>(d + o_rank));
-    if (gc) (rf ? (t4 ? k_chain0_g<4, true> : k_chain0_g<8, true>) : (t4 ? k_chain0_g<4, false> : k_chain0_g<8, false>))
-                <<<dim3(gc, k), 64, lc, ls>>>(reinterpret_cast<const GChain *>(d + o_chain));
+    if (gc) (t4 ? k_chain0_g<4> : k_chain0_g<8>)<<<dim3(gc, k), 64, lc, ls>>>(reinterpret_cast<const GChain *>(d + o_chain));
     if (gf) k_finalize_g<<<dim3(gf, k), 256, 0, ls>>>(reinterpret_cast<const GFin *>(d + o_fin));
     AQ_HIP(hipGetLastError());
     for (int j : m) rec[(size_t)j].kinds = 0;

@@ -136,11 +136,6 @@ bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi) {
     return *g > 0;
 }
 
-bool rank_skip_hint(adlbq_server *h) {
-    const int i = newest_landed(h);
-    return i >= 0 && h->h_snap[i].rank_covered == 1;
-}
-
 // keyrank unless a landed batch failed it over lately (then 64 batches on the sort + k_rank path)
 bool keyrank_hint(adlbq_server *h) {
     const int i = newest_landed(h);
@@ -1432,11 +1427,11 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv, h->d_rtype, h->d_pm_over,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
-                    h->d_sbeg, h->d_send, h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
+                    h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
-                    h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend, h->d_sg,
-                    h->d_mslot, h->d_fold, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
-                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr, h->d_arrive};
+                    h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend,
+                    h->d_mslot, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
+                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1933,6 +1928,33 @@ int adlbq_rfr_done(adlbq_server *h, int from_server_rank, int for_rank) {
     return ADLBQ_OK;
 }
 
+// adlbq_rfr_done for up to RFR_BATCH pairs, in order, by one thread
+constexpr int RFR_BATCH = 32;
+struct RfrPairs {
+    int n;
+    int v[2 * RFR_BATCH];
+};
+__global__ void k_rfr_done_batch(RfrPairs p, int *rfr_to_rank, int A, int *rfr_out, int nworld) {
+    for (int k = 0; k < p.n; k++) {
+        const int srv = p.v[2 * k], rank = p.v[2 * k + 1];
+        if (rank >= 0 && rank < A) rfr_to_rank[rank] = -1;
+        if (srv >= 0 && srv < nworld) rfr_out[srv] = 0;
+    }
+}
+
+int adlbq_rfr_done_batch(adlbq_server *h, int n, const int *pairs) {
+    if (!ok_handle(h) || n < 0 || (n && !pairs)) return fail(ADLBQ_ERR_ARG, "adlbq_rfr_done_batch");
+    hipSetDevice(h->device);
+    for (int k0 = 0; k0 < n; k0 += RFR_BATCH) {
+        RfrPairs p{};
+        p.n = std::min(RFR_BATCH, n - k0);
+        memcpy(p.v, pairs + 2 * k0, sizeof(int) * 2 * p.n);
+        k_rfr_done_batch<<<1, 1, 0, h->stream>>>(p, h->d_rfr_to_rank, h->A, h->d_rfr_out, h->num_world);
+    }
+    AQ_HIP(hipGetLastError());
+    return ADLBQ_OK;
+}
+
 int adlbq_tq_add(adlbq_server *h, int app_rank, int work_type, int server_rank) {
     if (!ok_handle(h)) return fail(ADLBQ_ERR_ARG, "adlbq_tq_add");
     for (size_t i = 0; i + 3 < h->tq.size(); i += 4)
@@ -2277,29 +2299,9 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->profile_every = (int)std::max(1ll, value);
         return ADLBQ_OK;
     }
-    if (n == "seg_guess") {
-        h->seg_guess = value ? 1 : 0;
-        return ADLBQ_OK;
-    }
     if (n == "tindex_delta") {  // delta index capacity (0: merge every Put batch into the main index)
         if (value < 0 || value > (1ll << 26)) return fail(ADLBQ_ERR_ARG, "adlbq_set_param: tindex_delta");
         h->tdel_max = value;
-        return ADLBQ_OK;
-    }
-    if (n == "hist_variant") {
-        h->hist_variant = value ? 1 : 0;
-        return ADLBQ_OK;
-    }
-    if (n == "select_chunk") {
-        h->select_chunk = value ? 1 : 0;
-        return ADLBQ_OK;
-    }
-    if (n == "hist_ppb") {
-        h->hist_ppb = value == 2 ? 2 : 1;
-        return ADLBQ_OK;
-    }
-    if (n == "hist_diag") {
-        h->hist_diag = (int)value;
         return ADLBQ_OK;
     }
     if (n == "split_prep") {
@@ -2340,11 +2342,6 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_rounds = (int)value;
         return ADLBQ_OK;
     }
-    if (n == "segsort_async") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "segsort_async must be 0 or 1");
-        h->segsort_async = (int)value;
-        return ADLBQ_OK;
-    }
     if (n == "chain_warm") {
         if (value != -1 && (value < 0 || value > CHAIN_WARM || value % SEG != 0))
             return fail(ADLBQ_ERR_ARG, "chain_warm must be -1 (auto) or a multiple of the segment up to CHAIN_WARM");
@@ -2355,37 +2352,12 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->chain_modes = value;
         return ADLBQ_OK;
     }
-    if (n == "segsort_radix") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "segsort_radix must be 0 or 1");
-        h->segsort_radix = (int)value;
-        return ADLBQ_OK;
-    }
-    if (n == "segsort_merged") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "segsort_merged must be 0 or 1");
-        h->segsort_merged = (int)value;
-        return ADLBQ_OK;
-    }
-    if (n == "fuse_finalize") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "fuse_finalize must be 0 or 1");
-        h->fuse_finalize = (int)value;
-        return ADLBQ_OK;
-    }
-    if (n == "fold_thresholds") {
-        if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fold_thresholds must be 0, 1 or 2 (auto)");
-        h->fold_thresholds = (int)value;
-        return ADLBQ_OK;
-    }
     if (n == "rq_wait_sync") {  // 1: rq backpressure synchronises the stream (the round-3 form)
         h->rq_wait_sync = value ? 1 : 0;
         return ADLBQ_OK;
     }
     if (n == "targeted_diag") {
         h->targeted_diag = (int)value;
-        return ADLBQ_OK;
-    }
-    if (n == "hist_arrive") {
-        if (value != 0 && value != 1) return fail(ADLBQ_ERR_ARG, "hist_arrive must be 0 or 1");
-        h->hist_arrive = (int)value;
         return ADLBQ_OK;
     }
     if (n == "keyrank") {
@@ -2408,20 +2380,9 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->group_launch = (int)value;
         return ADLBQ_OK;
     }
-    if (n == "fuse_rank") {
-        // 2 (test hook): skip k_rank whatever the hint, so the chain ranks whenever this batch needs it
-        if (value < 0 || value > 2) return fail(ADLBQ_ERR_ARG, "fuse_rank must be 0, 1 or 2");
-        h->fuse_rank = (int)value;
-        return ADLBQ_OK;
-    }
     if (n == "rank_grid") {  // test: k_rank's grid (0: sized by the rank hint)
         if (value < 0 || value > 4096) return fail(ADLBQ_ERR_ARG, "rank_grid must be in [0, 4096]");
         h->rank_grid = (int)value;
-        return ADLBQ_OK;
-    }
-    if (n == "segsort_wide") {
-        if (value < 2 || value > (1ll << 30)) return fail(ADLBQ_ERR_ARG, "segsort_wide must be in [2, 2^30]");
-        h->segsort_wide = (int)value;
         return ADLBQ_OK;
     }
     return fail(ADLBQ_ERR_ARG, "adlbq_set_param: unknown parameter");
@@ -2511,7 +2472,6 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         return n == "keyrank_why" ? h->ctr.kr_why : h->ctr.kr_maxbin;
     }
     if (n == "sort_radix") return h->n_sort_radix;         // planned sorts issued as the list-stable radix sort
-    if (n == "sort_async") return h->n_sort_async;         // merged sorts planned from the last landed batch (cumulative)
     if (n == "sort_async_bad") {  // ... whose plan did not hold (k_rank sorted them), as of the newest landed batch
         refresh_counters(h);
         return h->ctr.plan_missed;

@@ -126,11 +126,6 @@ def parse():
                     help="metric leg: any adlbq_set_param (diagnostics), repeatable")
     ap.add_argument("--c4-chain-stats", action="store_true",
                     help="config 4: after the timed region, replay each batch alone and report its chain counters")
-    ap.add_argument("--c4-segsort-async", type=int, default=None,
-                    help="config 4: adlbq 'segsort_async' (1: candidate sort planned from the last batch, no sync)")
-    ap.add_argument("--c4-segsort-wide", type=int, default=None,
-                    help="config 4: sort list by list (no merged sort); length from which a list gets a device-wide "
-                         "sort (adlbq 'segsort_wide')")
     return ap.parse_args()
 
 
@@ -595,7 +590,7 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
     srvs = [Server([1, 2], A, S * world, rank * S + s_, max_units=1 << 16, device=local) for s_ in range(S)]
     # warm-up: a short stream on a throwaway handle (kernels loaded, buffers sized)
     with Server([1, 2], A, S * world, rank * S, max_units=1 << 16, device=local) as tmp:
-        replay.replay(tmp, traces[0][: min(traces[0].size, 20000)])
+        replay.replay(tmp, traces[0][: replay.event_prefix(traces[0], 2, 20000)])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -765,11 +760,6 @@ def bench_config4(args, torch, dist, world, rank, local, dev):
     for kv in args.c4_param:
         k_, v_ = kv.split("=", 1)
         srv.set_param(k_, int(v_))
-    if args.c4_segsort_async is not None:
-        srv.set_param("segsort_async", args.c4_segsort_async)
-    if args.c4_segsort_wide is not None:
-        srv.set_param("segsort_merged", 0)
-        srv.set_param("segsort_wide", args.c4_segsort_wide)
     srv.put_batch(np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1),
                             np.zeros(N), np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32))
     rng = np.random.default_rng(args.seed + 41 + rank)

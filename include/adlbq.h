@@ -151,6 +151,10 @@ int adlbq_check_remote(adlbq_server *h, int cap, int *out3, int *count);
 
 /* SS_RFR_RESP bookkeeping (src/adlb.c:1877-1878). */
 int adlbq_rfr_done(adlbq_server *h, int from_server_rank, int for_rank);
+/* The same for n SS_RFRs at once, pairs[2k] = from_server_rank, pairs[2k+1] =
+ * for_rank, applied in order by one launch per 32 pairs (a steal group's server
+ * clears the records of every SS_RFR it leaves to the next round together). */
+int adlbq_rfr_done_batch(adlbq_server *h, int n, const int *pairs);
 
 /* FA_DID_PUT_AT_REMOTE's tq update (src/adlb.c:1167-1178); the caller then
  * runs adlbq_check_remote like adlb.c:1179. */
@@ -306,6 +310,13 @@ int adlbq_push_take(adlbq_server *h, int wqseqno, int *out10);
 int adlbq_push_commit(adlbq_server *h, int wqseqno, int *out3);
 /* Pushee, SS_PUSH_DEL (adlb.c:2353-2360): the held unit is removed. */
 int adlbq_push_discard(adlbq_server *h, int wqseqno, int *found);
+
+/* The reference's allocation sizes on LP64 (xq.h:8-79): xq_node_t 24 B + wq_struct_t 72 B per
+ * work unit (plus its payload), + rq_struct_t 80 B per parked Reserve, + tq_struct_t 16 B per
+ * tq entry.  The handle's byte count adds exactly these (callers that bound it must too). */
+#define ADLBQ_BYTES_WQ (24 + 72)
+#define ADLBQ_BYTES_RQ (24 + 80)
+#define ADLBQ_BYTES_TQ (24 + 16)
 
 /* ---- byte accounting (SURVEY hard part 5; adlb.c:3419-3474).  The handle
  * keeps the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced for the

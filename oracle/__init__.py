@@ -35,6 +35,7 @@ OP_PUT, OP_RESERVE, OP_GET, OP_UNRESERVE, OP_QMROW, OP_SETROW = 1, 2, 3, 4, 5, 6
 OP_CHECKREM, OP_RFRDONE, OP_TQADD, OP_PUSHSEL, OP_INFO, OP_RQDEL, OP_INFOTYPE = 7, 8, 9, 10, 11, 12, 13
 OP_RFR, OP_RQLIST, OP_BYTES, OP_PUTCHECK, OP_HWM = 14, 15, 16, 17, 18
 OP_PUSHACCEPT, OP_PUSHTAKE, OP_PUSHCOMMIT, OP_PUSHDEL = 19, 20, 21, 22
+OP_ROUND = 23  # a steal round of the server group (gen_config5): outstanding RFR records cleared
 
 
 def build(ref: bool = False) -> None:
@@ -172,7 +173,7 @@ def event_nargs(op: int, ntypes: int) -> int:
             OP_SETROW: 3 + ntypes, OP_CHECKREM: 0, OP_RFRDONE: 2, OP_TQADD: 3,
             OP_PUSHSEL: 1, OP_INFO: 0, OP_RQDEL: 1, OP_INFOTYPE: 1, OP_RFR: 18, OP_RQLIST: 0,
             OP_BYTES: 0, OP_PUTCHECK: 2, OP_HWM: 0, OP_PUSHACCEPT: 9, OP_PUSHTAKE: 1, OP_PUSHCOMMIT: 1,
-            OP_PUSHDEL: 1}[op]
+            OP_PUSHDEL: 1, OP_ROUND: 0}[op]
 
 
 def output_bound(tr: np.ndarray, ntypes: int) -> int:
@@ -190,3 +191,54 @@ def output_bound(tr: np.ndarray, ntypes: int) -> int:
         n_res += op == OP_RESERVE
         n_chk += op in (OP_CHECKREM, OP_TQADD)
     return 1024 + n_ev * (2 + max(12, ntypes + 1)) + n_chk * (1 + 3 * n_res)
+
+
+def gen_config5(n_shards: int = 8, n_ranks: int = 4096, n_events: int = 10_000_000, round_every: int = 10_000,
+                k: int = 64, q0: int = 512, seed: int = 5, seed_units: int = 256) -> dict:
+    """The config-5 stream at SURVEY §8(d)'s shape (oracle/gen_c5.c): per shard
+    its event trace (a steal round = ORC_OP_ROUND at the same place in every
+    shard's trace) and the oracle's outputs; the steals of every round
+    {shard, rqseqno, rank, TA_RESERVE_RESP[12]} in serial order, and how many
+    each round made; the generator's wall time (the oracle's CPU work)."""
+    path = os.path.join(HERE, "libgen5.so")
+    if not os.path.exists(path) or not os.path.exists(LIBS["own"]):
+        subprocess.run(["make", "-s", "-C", HERE, "liboracle.so", "libgen5.so"], check=True)
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    lib.c5_new.restype = ctypes.c_void_p
+    lib.c5_new.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                           ctypes.c_ulonglong]
+    lib.c5_error.restype = ctypes.c_char_p
+    lib.c5_error.argtypes = [ctypes.c_void_p]
+    lib.c5_run.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_long, ctypes.c_int]
+    for f in ("c5_events", "c5_rounds", "c5_stopped"):
+        getattr(lib, f).restype = ctypes.c_long
+        getattr(lib, f).argtypes = [ctypes.c_void_p]
+    lib.c5_seconds.restype = ctypes.c_double
+    lib.c5_seconds.argtypes = [ctypes.c_void_p]
+    pp = ctypes.POINTER(ctypes.POINTER(ctypes.c_int))
+    for f in ("c5_trace", "c5_out"):
+        getattr(lib, f).restype = ctypes.c_long
+        getattr(lib, f).argtypes = [ctypes.c_void_p, ctypes.c_int, pp]
+    for f in ("c5_steals", "c5_round_nsteal"):
+        getattr(lib, f).restype = ctypes.c_long
+        getattr(lib, f).argtypes = [ctypes.c_void_p, pp]
+    lib.c5_free.argtypes = [ctypes.c_void_p]
+    g = lib.c5_new(LIBS["own"].encode(), n_shards, n_ranks, k, q0, seed)
+    try:
+        if lib.c5_run(g, n_events, round_every, seed_units) != 0:
+            raise RuntimeError("gen_c5: " + lib.c5_error(g).decode())
+
+        def arr(f, *a, cols=1):
+            p = ctypes.POINTER(ctypes.c_int)()
+            n = f(g, *a, ctypes.byref(p))
+            return np.ctypeslib.as_array(p, shape=(n * cols,)).copy().reshape(-1, cols) if n else \
+                np.zeros((0, cols), np.int32)
+
+        return {"traces": [arr(lib.c5_trace, s).ravel() for s in range(n_shards)],
+                "outputs": [arr(lib.c5_out, s).ravel() for s in range(n_shards)],
+                "steals": arr(lib.c5_steals, cols=15), "round_nsteal": arr(lib.c5_round_nsteal).ravel(),
+                "events": lib.c5_events(g), "rounds": lib.c5_rounds(g), "stopped": lib.c5_stopped(g),
+                "seconds": lib.c5_seconds(g), "n_shards": n_shards, "n_ranks": n_ranks, "k": k,
+                "user_types": [1, 2]}
+    finally:
+        lib.c5_free(g)

@@ -11,6 +11,8 @@ fixture under tests/golden/:
   nq_np6_n9_s2_r5.npz  ... server rank 5
   mix_np6_s2_r{4,5}.npz, mix_np7_s3_r{4,5,6}.npz   tests/apps/adlb_mix.c on the reference
                        library: steals, targeted work, a common-prefix batch
+  mix_np6_s2_t100_r{4,5}.npz   the same with 100 declared work types (-ntypes 100): the
+                       engine's >64-type path and SS_RFR steals
 
 Fixture = the server's inbound events in the order its loop handled them and
 every reply it sent, attributed to the event that caused it:
@@ -25,7 +27,7 @@ time-triggered exhaustion answer (adlb.c:757-772) becomes an `exhausted`
 event of its own.
 
 Run in the build container (needs /root/reference and /opt/conda's MPICH):
-  python oracle/gen_nq.py
+  python oracle/gen_nq.py [case ...]     (no case: all of them)
 """
 from __future__ import annotations
 
@@ -136,15 +138,34 @@ def run_case(np_, args, servers, name, exe="nq", types=NQ_TYPES, max_malloc=NQ_M
         return found
 
 
+MIX_TYPES = [11, 22, 33, 44]
+
+
+def mix_types(k):
+    """tests/apps/adlb_mix.c's declared types for -ntypes k"""
+    return MIX_TYPES + [1000 + i for i in range(4, k)]
+
+
+CASES = {
+    "nq_np4_n8": lambda: run_case(4, ["-n", "8", "-q"], [3], "nq_np4_n8"),
+    "nq_np6_n9_s2": lambda: run_case(6, ["-n", "9", "-q", "-nservers", "2"], [4, 5], "nq_np6_n9_s2"),
+    # tests/apps/adlb_mix.c: steals (SS_RFR / SS_RFR_RESP / SS_UNRESERVE), targeted units,
+    # a common-prefix batch, Ireserve and info queries (types 11, 22, 33, 44; hi 1e8)
+    "mix_np6_s2": lambda: run_case(6, ["-nservers", "2", "-n", "200"], [4, 5], "mix_np6_s2", "mix", MIX_TYPES,
+                                   100000000),
+    "mix_np7_s3": lambda: run_case(7, ["-nservers", "3", "-n", "150"], [4, 5, 6], "mix_np7_s3", "mix", MIX_TYPES,
+                                   100000000),
+    # 100 declared types (more than the 64-bit type masks hold)
+    "mix_np6_s2_t100": lambda: run_case(6, ["-nservers", "2", "-n", "120", "-ntypes", "100"], [4, 5],
+                                        "mix_np6_s2_t100", "mix", mix_types(100), 100000000),
+}
+
+
 def main():
     if not os.path.isdir("/root/reference/src"):
         sys.exit("needs the reference sources (build container only)")
-    run_case(4, ["-n", "8", "-q"], [3], "nq_np4_n8")
-    run_case(6, ["-n", "9", "-q", "-nservers", "2"], [4, 5], "nq_np6_n9_s2")
-    # tests/apps/adlb_mix.c: steals (SS_RFR / SS_RFR_RESP / SS_UNRESERVE), targeted units,
-    # a common-prefix batch, Ireserve and info queries (types 11, 22, 33, 44; hi 1e8)
-    run_case(6, ["-nservers", "2", "-n", "200"], [4, 5], "mix_np6_s2", "mix", [11, 22, 33, 44], 100000000)
-    run_case(7, ["-nservers", "3", "-n", "150"], [4, 5, 6], "mix_np7_s3", "mix", [11, 22, 33, 44], 100000000)
+    for name in sys.argv[1:] or list(CASES):
+        CASES[name]()
 
 
 if __name__ == "__main__":

@@ -164,6 +164,7 @@ int orc_event_nargs(int op, int ntypes)
     case ORC_OP_PUSHTAKE: return 1;
     case ORC_OP_PUSHCOMMIT: return 1;
     case ORC_OP_PUSHDEL: return 1;
+    case ORC_OP_ROUND: return 0;
     default: return -1;
     }
 }
@@ -485,6 +486,14 @@ long orc_replay(const int *tr, long ntrace, int *out, long outcap)
                 o[2] = for_rank;
                 n = 3;
             }
+            break;
+        }
+        case ORC_OP_ROUND: {
+            for (int i = 0; i < S.num_world; i++)
+                S.rfr_out[i] = 0;
+            for (int i = 0; i < S.num_app_ranks; i++)
+                S.rfr_to_rank[i] = -1;
+            n = 0;
             break;
         }
         case ORC_OP_RQLIST: {

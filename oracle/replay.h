@@ -37,6 +37,9 @@ enum {
     ORC_OP_PUSHTAKE = 20,   /* wqseqno                                          -> [ok, type, prio, len, answer, target, home, clen, csrv, cseq] SS_PUSH_QUERY_RESP at the pusher (2179-2222) */
     ORC_OP_PUSHCOMMIT = 21, /* wqseqno                                          -> [found, matched_rank, matched_rqseqno] SS_PUSH_HDR at the pushee (2232-2340) */
     ORC_OP_PUSHDEL = 22,    /* wqseqno                                          -> [found] SS_PUSH_DEL at the pushee (2353-2360) */
+    /* a steal round of the server group starts here (oracle/gen_c5.c): every outstanding RFR record
+     * is cleared, as the SS_RFR_RESPs the round replaces would (adlb.c:1877-1878) -> [] */
+    ORC_OP_ROUND = 23,
 };
 
 /* TA_RESERVE_RESP layout (adlb.c:1213-1222), plus two slots this build uses

@@ -15,6 +15,10 @@
  * With -hi small, servers reject puts (PUT_REJECTED walk, puts of targeted
  * work away from the target's server: FA_DID_PUT_AT_REMOTE and the tq).
  *
+ * With -ntypes K (K > 4) the servers declare K work types: the four above and
+ * K - 4 more that no unit carries (K > 64: the engine's sorted-runs Reserve
+ * path, and SS_RFR steals instead of the steal group's merge).
+ *
  * Output (rank 0): "adlb_mix: units U sum S expect U' S'"; U == U' and
  * S == S' whatever the schedule.
  */
@@ -41,23 +45,28 @@ static int check(const int *w, int nw, int type) {
 }
 
 int main(int argc, char **argv) {
-    int nservers = 2, n = 200, len = 64, ndbatch = 8;
+    int nservers = 2, n = 200, len = 64, ndbatch = 8, ntypes = 4;
     double hi = 1e8;
     for (int i = 1; i < argc; i++) {
         if (!strcmp(argv[i], "-nservers")) nservers = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-n")) n = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-len")) len = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-hi")) hi = atof(argv[++i]);
+        else if (!strcmp(argv[i], "-ntypes")) ntypes = atoi(argv[++i]);
     }
+    if (ntypes < 4) ntypes = 4;
     len = (len / 4 < 4 ? 4 : len / 4) * 4;
     const int nw = len / 4;
-    int types[4] = {TA, TB, TC, TD}, am_server, am_debug;
+    /* the four carried types first, then declared-only ones (values below 10010: adlb.c:343-356) */
+    int *types = malloc(sizeof(int) * (size_t)ntypes), am_server, am_debug;
+    types[0] = TA, types[1] = TB, types[2] = TC, types[3] = TD;
+    for (int k = 4; k < ntypes; k++) types[k] = 1000 + k;
     MPI_Comm app_comm;
     MPI_Init(&argc, &argv);
     int world, rank;
     MPI_Comm_size(MPI_COMM_WORLD, &world);
     MPI_Comm_rank(MPI_COMM_WORLD, &rank);
-    if (ADLB_Init(nservers, 0, 0, 4, types, &am_server, &am_debug, &app_comm) != ADLB_SUCCESS) MPI_Abort(MPI_COMM_WORLD, 1);
+    if (ADLB_Init(nservers, 0, 0, ntypes, types, &am_server, &am_debug, &app_comm) != ADLB_SUCCESS) MPI_Abort(MPI_COMM_WORLD, 1);
     if (am_server) {
         ADLB_Server(hi, 0.0);
         double hwm = 0, nrej = 0, pfrom = 0, pto = 0;
@@ -139,6 +148,7 @@ int main(int argc, char **argv) {
     if (rank == 0) printf("adlb_mix: units %lld sum %lld expect %d %lld\n", all[0], all[1], expect_units, expect_sum);
     free(w);
     free(buf);
+    free(types);
     ADLB_Finalize();
     MPI_Finalize();
     return 0;

@@ -45,8 +45,7 @@ def _oracle_resps(w, S, s):
     return np.asarray(out[w.n_units:], dtype=np.int32)
 
 
-@pytest.mark.parametrize("params", [{}, {"fuse_rank": 1}, {"fuse_rank": 2}, {"fold_thresholds": 1}],
-                         ids=["default", "rank_skip", "rank_in_chain", "folded"])
+@pytest.mark.parametrize("params", [{}, {"rank_in_select": 0}], ids=["default", "rank_in_k_rank"])
 def test_group_matches_sequential(gpu_available, params):
     import torch
     from adlb_amd.server import ReserveGroup, Server

@@ -90,7 +90,8 @@ def _stream(seed, rounds, n_res, n_put, ut, A):
 
 def test_rq_slots_reclaimed_vs_oracle(gpu_available):
     ut, A = np.arange(3, dtype=np.int32), 4096
-    tr = _stream(11, rounds=40, n_res=2048, n_put=2000, ut=ut, A=A)
+    # batches of 512: the rq headroom a host may run ahead by (NSNAP batches) stays far below the parks
+    tr = _stream(11, rounds=160, n_res=512, n_put=500, ut=ut, A=A)
     with Server(ut, A, max_units=1 << 16) as s:
         got = replay.replay(s, tr)
         parks = s.stat("rq_next")

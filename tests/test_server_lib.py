@@ -79,7 +79,10 @@ def test_nq_fixture_consistent(name):
     if fx.S == 1:
         assert len(handed) == gets
     assert kinds.count("exhausted") == 1
-    assert fx.types.tolist() in ([1000, 2000, 3000], [11, 22, 33, 44])
+    t = fx.types.tolist()
+    # nq's types, adlb_mix's four, or adlb_mix -ntypes 100 (the four, then declared-only 1004 ...)
+    assert t in ([1000, 2000, 3000], [11, 22, 33, 44]) or (t[:4] == [11, 22, 33, 44] and
+                                                            t[4:] == [1000 + k for k in range(4, len(t))])
 
 
 def test_mix_fixtures_cover_the_steal_paths():
@@ -89,3 +92,5 @@ def test_mix_fixtures_cover_the_steal_paths():
     assert {"rfr", "rfr_resp", "common_hdr", "batch_done", "get_common", "info", "qmstat"} <= kinds
     fails = [e for f in fx for e in f.events if e[0] == "rfr_resp" and int(np.frombuffer(e[2][:4], np.int32)[0]) != 1]
     assert fails, "no failed SS_RFR_RESP recorded"
+    many = [f for f in fx if len(f.types) > 64]
+    assert many and any(e[0] == "rfr_resp" for f in many for e in f.events), "no >64-type steal recorded"

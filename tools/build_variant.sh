@@ -7,7 +7,7 @@ name=$1; shift
 D=$(cd "$(dirname "$0")/.." && pwd)
 O=$D/adlb_amd/variants/$name
 mkdir -p $O
-for f in adlbq_store adlbq_reserve adlbq_steal adlbq_rsx; do
+for f in adlbq_store adlbq_reserve adlbq_steal adlbq_rsx adlbq_wide adlbq_keyrank; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$D/include "$@" -c $D/adlb_amd/csrc/$f.hip -o $O/$f.o &
 done
 wait
