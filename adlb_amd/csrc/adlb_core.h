@@ -119,6 +119,17 @@ typedef struct adlbq_server adlbq_server;
 int adlbsrv_replay_many(adlbq_server **hs, int n, int ntypes, const int *const *traces, const long long *lens,
                         int *const *outs, const long long *caps, long long *nouts, long long *ncalls);
 const char *adlbsrv_replay_error(void);
+/* Config 5 at its SURVEY shape (oracle/gen_c5.c): S shards' traces with steal
+ * rounds (event 23 at the same place in every trace).  Between rounds each
+ * shard's Puts / Reserves / Gets go down as device-side batches from its own
+ * host thread (inputs staged in HBM first, outputs left there: no
+ * synchronisation per call); a round runs adlbq_steal_group_export + _settle
+ * over all S shards (export depth k, rqcap parked Reserves per shard) and its
+ * responses are appended to steals (rows of 15).  outs[j] receives the replay
+ * layout; *seconds the wall time of the replay (staging excluded). */
+int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
+                          int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
+                          int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls);
 
 /* state for the driver */
 int adlbsrv_num_parked(adlbsrv *s);     /* rq->count */

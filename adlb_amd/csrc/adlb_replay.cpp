@@ -14,8 +14,13 @@
 // where 8 server shards of one GPU each replay their own stream.
 #include "adlb_core.h"
 
+#include <hip/hip_runtime_api.h>
+
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -28,7 +33,7 @@ enum {
     OP_PUT = 1, OP_RESERVE = 2, OP_GET = 3, OP_UNRESERVE = 4, OP_QMROW = 5, OP_SETROW = 6, OP_CHECKREM = 7,
     OP_RFRDONE = 8, OP_TQADD = 9, OP_PUSHSEL = 10, OP_INFO = 11, OP_RQDEL = 12, OP_INFOTYPE = 13,
     OP_BYTES = 16, OP_PUTCHECK = 17, OP_HWM = 18, OP_PUSHACCEPT = 19, OP_PUSHTAKE = 20, OP_PUSHCOMMIT = 21,
-    OP_PUSHDEL = 22
+    OP_PUSHDEL = 22, OP_ROUND = 23
 };
 
 int nargs(int op, int T) {
@@ -37,7 +42,7 @@ int nargs(int op, int T) {
     case OP_RESERVE: return ADLBQ_RESERVE_INTS;
     case OP_GET: case OP_RFRDONE: case OP_PUTCHECK: return 2;
     case OP_UNRESERVE: case OP_TQADD: return 3;
-    case OP_QMROW: case OP_CHECKREM: case OP_INFO: case OP_BYTES: case OP_HWM: return 0;
+    case OP_QMROW: case OP_CHECKREM: case OP_INFO: case OP_BYTES: case OP_HWM: case OP_ROUND: return 0;
     case OP_SETROW: return 3 + T;
     case OP_PUSHSEL: case OP_RQDEL: case OP_INFOTYPE: case OP_PUSHTAKE: case OP_PUSHCOMMIT: case OP_PUSHDEL: return 1;
     default: return -1;
@@ -214,6 +219,48 @@ struct Replayer {
     }
 };
 
+
+// ---------------------------------------------------------------- config 5 at its SURVEY shape
+// S shards' traces with steal rounds (OP_ROUND at the same place in every
+// trace; oracle/gen_c5.c).  Between rounds every shard's Puts, Reserves and
+// Gets go down as device-side batches on its own stream from its own host
+// thread, their inputs staged in HBM beforehand and their outputs left in HBM:
+// nothing waits for a batch to finish (no synchronisation per call; the
+// engine's counter snapshots land in mapped memory).  A qmstat row is read
+// back where the trace asks for it.  At a round every thread stops; one thread
+// runs the steal group's export and settle over all shards (the merge on the
+// host, the grants and rq deletions enqueued on the shards' streams) and
+// collects the responses; then every thread goes on.
+struct RCall {
+    int op, n;
+    long long in, dout, hout;  // input offset (ints), device output offset, host output offset (QMROW)
+    const int *x;              // the event's arguments (single events)
+};
+
+struct RShard {
+    adlbq_server *h = nullptr;
+    std::vector<RCall> calls;
+    std::vector<int> hin;        // reserve records (18) and get pairs (2), in call order
+    std::vector<int> put;        // put records (9), in call order (host: adlbq_put_batch_device stages them)
+    std::vector<int> hqm;        // QMROW outputs
+    int *din = nullptr, *dout = nullptr;
+    long long nout_dev = 0;
+    std::string err;
+    long long ncalls = 0;
+};
+
+namespace {
+int out_ints(int op, int T) {
+    switch (op) {
+    case OP_PUT: return 3;
+    case OP_RESERVE: return ADLBQ_RESP_INTS;
+    case OP_GET: return 5;
+    case OP_QMROW: return 1 + T;
+    default: return 0;
+    }
+}
+}  // namespace
+
 thread_local std::string g_rerr;
 
 }  // namespace
@@ -258,6 +305,203 @@ int adlbsrv_replay_many(adlbq_server **hs, int n, int ntypes, const int *const *
         }
     }
     return 0;
+}
+
+
+int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
+                          int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
+                          int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls) {
+    if (!hs || S < 1 || !traces || !lens || !outs || !caps || !nouts || !steals || !nsteals) {
+        g_rerr = "adlbsrv_replay_rounds: bad argument";
+        return -1;
+    }
+    const int T = ntypes;
+    std::vector<RShard> sh((size_t)S);
+    long long nround = -1;
+    // ---- untimed: the calls, their staged inputs (HBM) and output space
+    for (int j = 0; j < S; j++) {
+        RShard &r = sh[(size_t)j];
+        r.h = hs[j];
+        const int *tr = traces[j];
+        const long long n = lens[j];
+        long long i = 0, rounds = 0, hq = 0;
+        while (i < n) {
+            const int op = tr[i], w = 1 + nargs(op, T);
+            if (w <= 0 || i + w > n) {
+                g_rerr = "shard " + std::to_string(j) + ": bad event at " + std::to_string(i);
+                return -1;
+            }
+            RCall c{op, 1, 0, 0, 0, tr + i + 1};
+            if (op == OP_PUT || op == OP_RESERVE || op == OP_GET) {
+                long long e = i;
+                while (e + w <= n && tr[e] == op) e += w;
+                c.n = (int)((e - i) / w);
+                std::vector<int> &dst = op == OP_PUT ? r.put : r.hin;
+                c.in = (long long)dst.size();
+                for (long long q = i; q < e; q += w) dst.insert(dst.end(), tr + q + 1, tr + q + w);
+                c.dout = r.nout_dev;
+                r.nout_dev += (long long)c.n * out_ints(op, T);
+                i = e;
+            } else {
+                if (op != OP_QMROW && op != OP_SETROW && op != OP_ROUND) {
+                    g_rerr = "shard " + std::to_string(j) + ": event " + std::to_string(op) + " is not part of the rounds replay";
+                    return -1;
+                }
+                if (op == OP_QMROW) {
+                    c.hout = hq;
+                    hq += 1 + T;
+                }
+                rounds += op == OP_ROUND;
+                i += w;
+            }
+            r.calls.push_back(c);
+        }
+        r.hqm.assign((size_t)std::max(hq, 1ll), 0);
+        if (nround < 0) nround = rounds;
+        if (rounds != nround) {
+            g_rerr = "the traces do not hold the same number of rounds";
+            return -1;
+        }
+        if (hipMalloc((void **)&r.din, sizeof(int) * std::max<size_t>(r.hin.size(), 1)) != hipSuccess ||
+            hipMalloc((void **)&r.dout, sizeof(int) * std::max<long long>(r.nout_dev, 1)) != hipSuccess ||
+            hipMemcpy(r.din, r.hin.data(), sizeof(int) * r.hin.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            g_rerr = "adlbsrv_replay_rounds: device staging";
+            return -1;
+        }
+    }
+    adlbq_steal_group *g = nullptr;
+    if (adlbq_steal_group_create(&g, hs, S, k, rqcap)) {
+        g_rerr = std::string("adlbq_steal_group_create: ") + adlbq_last_error();
+        return -1;
+    }
+    // ---- timed: the shards' threads, meeting at every round
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long long gen = 0;
+    bool failed = false;
+    long long ns = 0;
+    std::string gerr;
+    std::vector<int> resp;
+    auto round_barrier = [&](bool ok) {  // every thread; the last one in runs the round
+        std::unique_lock<std::mutex> lk(mu);
+        if (!ok) failed = true;
+        const long long my = gen;
+        if (++arrived == S) {
+            if (!failed) {
+                int dec = 0, set = 0, cnt = 0;
+                if (adlbq_steal_group_export(g, nullptr) || adlbq_steal_group_settle(g, nullptr, 1, &dec, &set)) {
+                    gerr = std::string("steal round: ") + adlbq_last_error();
+                    failed = true;
+                } else {
+                    resp.resize((size_t)15 * (set + 16));
+                    if (adlbq_steal_group_responses(g, set + 16, resp.data(), &cnt)) {
+                        gerr = std::string("steal round responses: ") + adlbq_last_error();
+                        failed = true;
+                    } else {
+                        for (int q = 0; q < cnt && ns < steal_cap; q++, ns++)
+                            std::memcpy(steals + 15 * ns, resp.data() + 15 * q, sizeof(int) * 15);
+                        if (cnt && ns >= steal_cap) {
+                            gerr = "steal output full";
+                            failed = true;
+                        }
+                    }
+                }
+            }
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != my; });
+        }
+        return !failed;
+    };
+    auto work = [&](int j) {
+        RShard &r = sh[(size_t)j];
+        adlbq_server *h = r.h;
+        bool ok = true;
+        for (const RCall &c : r.calls) {
+            if (!ok) {
+                if (c.op == OP_ROUND) round_barrier(false);
+                continue;
+            }
+            r.ncalls++;
+            int rc = 0;
+            switch (c.op) {
+            case OP_PUT: rc = adlbq_put_batch_device(h, c.n, r.put.data() + c.in, r.dout + c.dout); break;
+            case OP_RESERVE: rc = adlbq_reserve_batch_device(h, c.n, r.din + c.in, r.dout + c.dout); break;
+            case OP_GET: rc = adlbq_get_reserved_batch_device(h, c.n, r.din + c.in, r.dout + c.dout); break;
+            case OP_QMROW: rc = adlbq_qmstat_row(h, &r.hqm[(size_t)c.hout], &r.hqm[(size_t)c.hout + 1]); break;
+            case OP_SETROW: rc = adlbq_set_qmstat_row(h, c.x[0], c.x[1], (double)c.x[2], c.x + 3); break;
+            case OP_ROUND: ok = round_barrier(true); continue;
+            }
+            if (rc) {
+                r.err = std::string("call ") + std::to_string(c.op) + ": " + adlbq_last_error();
+                ok = false;
+            }
+        }
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    {
+        std::vector<std::thread> th;
+        for (int j = 0; j < S; j++) th.emplace_back(work, j);
+        for (auto &t : th) t.join();
+    }
+    // every shard's device work has finished (the engine's batches run on its streams)
+    for (int j = 0; j < S; j++) {
+        double c0, c1;
+        if (adlbq_bytes(hs[j], &c0, &c1)) failed = true;  // synchronises the shard's stream
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+    *nsteals = ns;
+    adlbq_steal_group_destroy(g);
+    // ---- untimed: outputs back, in the replay layout
+    int rc = 0;
+    for (int j = 0; j < S && !rc; j++) {
+        RShard &r = sh[(size_t)j];
+        if (ncalls) ncalls[j] = r.ncalls;
+        if (!r.err.empty()) {
+            g_rerr = "shard " + std::to_string(j) + ": " + r.err;
+            rc = -1;
+            break;
+        }
+        std::vector<int> dv((size_t)std::max<long long>(r.nout_dev, 1));
+        if (hipMemcpy(dv.data(), r.dout, sizeof(int) * r.nout_dev, hipMemcpyDeviceToHost) != hipSuccess) {
+            g_rerr = "output copy";
+            rc = -1;
+            break;
+        }
+        Out o{outs[j], caps[j]};
+        for (const RCall &c : r.calls) {
+            const int oi = out_ints(c.op, T);
+            if (c.op == OP_PUT || c.op == OP_RESERVE || c.op == OP_GET) {
+                for (int e = 0; e < c.n; e++) {
+                    o.put(oi);
+                    for (int q = 0; q < oi; q++) o.put(dv[(size_t)(c.dout + (long long)e * oi + q)]);
+                }
+            } else if (c.op == OP_QMROW) {
+                o.put(oi);
+                for (int q = 0; q < oi; q++) o.put(r.hqm[(size_t)c.hout + q]);
+            } else {
+                o.put(0);
+            }
+        }
+        nouts[j] = o.n;
+        if (o.over) {
+            g_rerr = "shard " + std::to_string(j) + ": output buffer too small";
+            rc = -2;
+        }
+    }
+    for (auto &r : sh) {
+        if (r.din) hipFree(r.din);
+        if (r.dout) hipFree(r.dout);
+    }
+    if (!rc && (failed || !gerr.empty())) {
+        g_rerr = gerr.empty() ? "a shard failed" : gerr;
+        rc = -1;
+    }
+    return rc;
 }
 
 }  // extern "C"

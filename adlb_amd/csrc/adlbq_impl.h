@@ -306,6 +306,8 @@ struct adlbq_server {
     int rank_in_select = 1;            // k_select_open ranks the candidates when it can ("rank_in_select")
     int sort_fail_test = 0;            // test hook ("sort_fail_test"): the error path of a failed sort wait
     int chain_stamps = 0;              // diagnostic: phase stamps of the first chain launch ("chain_stamps")
+    int kstamps = 0;                   // diagnostic ("kernel_stamps"): per-workgroup phase stamps of passes 1 and 2
+    unsigned long long *d_kst = nullptr; int cap_kst = 0, n_kst = 0;
     unsigned long long *d_stamps = nullptr; int cap_stamps = 0, n_stamps = 0;
     int chain_warm = -1;               // round-0 warm-up requests (T <= 8), -1 = auto ("chain_warm")
     long long chain_modes = -1;        // bit k-1: round k uses prefix starts, -1 = auto ("chain_modes")

@@ -177,31 +177,17 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
 }
 
 // ---------------------------------------------------------------- pass 1
-// The far bins, lumped (T <= 8).  With guessed cuts gc below the anchors an,
-// the units deeper than twice the deepest guessed depth are counted per type in
-// registers (one LDS add per wave and type at the end) into the last bin of
-// their type instead of with one LDS atomic each into their own bin.  The
-// thresholds lie above the cuts whenever the guesses hold; when one does not,
-// that type's lump is a multi-priority bin like any other (its units are listed
-// and sorted).  Pass 1 and pass 2 bin by the same rule: a unit in bin
-// batch_lump_bin or deeper belongs to bin NB - 1 of its type (NB: nothing lumped).
-// Lane t holds type t's anchor and cut; every lane of the wave calls it.
-__device__ __forceinline__ int batch_lump_bin(int T, bool tl, long long an, long long gc) {
-#ifdef ADLBQ_NO_LUMP
-    return NB;
-#endif
-    int v = -1;  // a type without a guess (or with an empty one) does not vote
-    if (T <= 8 && tl && gc != LLONG_MAX && gc <= an && an - gc < (1ll << 30)) v = bin_of(2 * (an - gc) + 2) + 1;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return (v < 0 || v >= NB - 1) ? NB : v;
-}
-
 // One workgroup per page: each wave owns a quarter of the page and issues all
 // of its loads (8 x 16 B per lane) before counting.  The histogram is kept in
 // HK lane-interleaved copies so that lanes hitting the same (type, bin) column
 // (most units fall in a few far bins) do not serialise one LDS atomic.
 constexpr int HK = 4;
+
+// diagnostic ("kernel_stamps"): per workgroup, the constant clock (100 MHz) at
+// phase boundaries of pass 1 / pass 2, [workgroup][4]
+__device__ __forceinline__ void kstamp(unsigned long long *kst, int bid, int ph) {
+    if (kst != nullptr && threadIdx.x == 0) kst[(long long)bid * 4 + ph] = __builtin_amdgcn_s_memrealtime();
+}
 
 struct HistArgs {
     const int *pages;
@@ -219,6 +205,7 @@ struct HistArgs {
     unsigned int *zcs;         // the other chunk-sum buffer (the previous scan's): k_thresholds zeroes it
     long long zn;
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
+    unsigned long long *kst = nullptr;  // diagnostic stamps, or nullptr
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -254,23 +241,44 @@ __device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const
 // Pass 1 over one page (four waves, a quarter page each): per (type, bin)
 // column the available units (LDS copies, then the page's row and the chunk
 // sums), and in each wave's list the units at or above the guessed cut, in
-// slot order.  LUMP (T <= 8): units in bin lb or deeper are counted in
-// registers, 8 bits per type, and added to bin NB - 1 of their type once per
-// wave (batch_lump_bin).
-template <bool LUMP>
-__device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, const int4 (&pv)[4],
-                                               const uint4 (&mv)[4], const int2 *sag, const int lb,
-                                               unsigned int *__restrict__ hist /* [C][HK] */) {
+// slot order.  NARROW: the page's prios are its base plus the offsets packed
+// into meta, so only the meta column is loaded and held (the wide form holds
+// the prio column as well: 16 more registers).
+template <bool NARROW>
+__device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, const int pg, const int fill,
+                                               const int2 *sag, unsigned int *__restrict__ hist /* [C][HK] */) {
     const int T = a.T, C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long long base = (long long)pg << PAGE_SHIFT;
+    const uint4 *M4 = reinterpret_cast<const uint4 *>(a.meta + base);
+    const int4 *P4 = reinterpret_cast<const int4 *>(a.prio + base);
+    uint4 mv[4];
+    int4 pv[NARROW ? 1 : 4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int idx = (w * 4 + k) * 64 + lane;
+        mv[k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+        if constexpr (!NARROW) pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
+    }
+    const int pb = NARROW ? a.pbase[pg] : 0;
+    __syncthreads();  // sag and the zeroed histogram (the caller's stores) are visible
+    if (a.kst) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        kstamp(a.kst, p, 1);
+    }
     unsigned int *my = hist + (lane % HK);
     unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
     const unsigned long long lt = lanemask_lt();
-    unsigned long long lumpc = 0ull;
     int sn = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
         const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+        int pr[4];
+        if constexpr (NARROW) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) pr[q] = pb + (int)(mm[q] >> M_OFF_SHIFT);
+        } else {
+            pr[0] = pv[k].x, pr[1] = pv[k].y, pr[2] = pv[k].z, pr[3] = pv[k].w;
+        }
         int col[4];
         bool in[4];
 #pragma unroll
@@ -278,15 +286,9 @@ __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, c
             const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
             const int t = mm[q] & M_TYPE;
             const int2 ag = sag[t];
-            const int bn = bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
-            col[q] = t * NB + bn;
+            col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
             in[q] = av && pr[q] >= ag.y;
-            if constexpr (LUMP) {
-                if (av && bn < lb) atomicAdd(&my[col[q] * HK], 1u);
-                lumpc += (av && bn >= lb) ? (1ull << (8 * (t & 7))) : 0ull;
-            } else {
-                if (av) atomicAdd(&my[col[q] * HK], 1u);
-            }
+            if (av) atomicAdd(&my[col[q] * HK], 1u);
         }
         const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
                                  b3 = __ballot(in[3]);
@@ -302,16 +304,9 @@ __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, c
         }
         sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
     }
-    if constexpr (LUMP) {
-        for (int u = 0; u < T; u++) {
-            unsigned int c = (unsigned int)(lumpc >> (8 * u)) & 0xffu;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-            if (lane == 0 && c) atomicAdd(&hist[(u * NB + NB - 1) * HK], c);
-        }
-    }
     if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
+    kstamp(a.kst, p, 2);
     unsigned int *cs = a.csum + (long long)(p / CHUNK) * C;
     unsigned short *g = a.gh + (long long)p * C;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -321,28 +316,24 @@ __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, c
         g[c] = (unsigned short)v;
         if (v) atomicAdd(&cs[c], v);
     }
+    if (a.kst) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        kstamp(a.kst, p, 3);
+    }
 }
 
 __device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist) {
     __shared__ int2 sag[ADLBQ_MAX_TYPES];
-    __shared__ int s_lb;
-    const int T = a.T, C = T * NB, w = threadIdx.x >> 6;
+    const int T = a.T, C = T * NB;
+    const int pg = a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
     const int fill = (p == a.npages - 1) ? a.tail_fill : PAGE;
-    int4 pv[4];
-    uint4 mv[4];
-    load_quarter(a.prio, a.meta, a.pbase, a.pwide, a.pg0 >= 0 ? a.pg0 + p : a.pages[p], fill, w, pv, mv);
-    if (threadIdx.x < 64) {  // wave 0 holds every type (T <= 64): anchors, cuts, the batch's lump bin
-        const int t = threadIdx.x;
-        const long long an = t < T ? a.anchor[t] : 0, gc = t < T ? a.gcut[t] : 0;
-        if (t < T) sag[t] = make_int2((int)an, (int)std::max(std::min(gc, (long long)INT_MAX), (long long)INT_MIN));
-        const int lb = batch_lump_bin(T, t < T, an, gc);
-        if (t == 0) s_lb = lb;
-    }
+    kstamp(a.kst, p, 0);
+    const int wide = a.pwide[pg];
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+        sag[t] = make_int2((int)a.anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
     for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-    __syncthreads();
-    const int lb = s_lb;
-    if (lb < NB) hist_page_body<true>(a, p, pv, mv, sag, lb, hist);
-    else hist_page_body<false>(a, p, pv, mv, sag, lb, hist);
+    if (wide) hist_page_body<false>(a, p, pg, fill, sag, hist);
+    else hist_page_body<true>(a, p, pg, fill, sag, hist);
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
@@ -530,8 +521,9 @@ __device__ __forceinline__ void select_open_body(
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
     const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
     const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
-    unsigned char *__restrict__ rtype, int R, const int bid_, const int nbk_) {
+    unsigned char *__restrict__ rtype, int R, const int bid_, const int nbk_, unsigned long long *kst = nullptr) {
     constexpr int RT = TB <= RANK_FAST_T ? TB : 1;  // types of the fast ranking
+    kstamp(kst, bid_, 0);
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
     __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES], slen[RT];
@@ -564,7 +556,6 @@ __device__ __forceinline__ void select_open_body(
 #pragma unroll
     for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
     const long long cut_l = cut_of(th_l, an_l);
-    const int lumpb = batch_lump_bin(T, tl, an_l, gc_l);  // pass 1's lumped far bins: bin NB - 1 from there on
     const bool use_spec = __ballot(th_l >= 0 && gc_l > cut_l) == 0 && sn <= SPEC_CAP;  // wave-uniform
     int4 pv[4];
     uint4 mv[4];
@@ -622,6 +613,7 @@ __device__ __forceinline__ void select_open_body(
         if (p == 0 && threadIdx.x == T - 1) candoff_out[T] = x;
     }
     __syncthreads();
+    kstamp(kst, bid_, 1);
     int n = 0;  // this wave's candidates so far (uniform)
     const unsigned long long lt = lanemask_lt();
     if (use_spec) {  // filter the list: entries in bins up to the type's threshold
@@ -655,8 +647,7 @@ __device__ __forceinline__ void select_open_body(
         for (int q = 0; q < 4; q++) {
             if (cnd[q]) {
                 const int t = mm[q] & M_TYPE;
-                const int bq = bin_of(sanc[t] - pr[q]);
-                const int col = t * NB + (bq >= lumpb ? NB - 1 : bq);
+                const int col = t * NB + bin_of(sanc[t] - pr[q]);
                 atomicAdd(&wc[w * C + col], 1u);
                 list[pos++] = ((unsigned int)col << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
             }
@@ -678,6 +669,7 @@ __device__ __forceinline__ void select_open_body(
         }
     }
     __syncthreads();
+    kstamp(kst, bid_, 2);
     unsigned int *run = wc + w * C;
     // the fast ranking's per-type constants, uniform over the wave (from LDS once)
     long long an_u[RT];
@@ -773,6 +765,10 @@ __device__ __forceinline__ void select_open_body(
     // the next batch's hint for skipping k_rank: ranked here, and every type has candidates
     const bool empty = __ballot(tl && len_l <= 0) != 0ull;
     if (crank != nullptr && p == 0 && threadIdx.x == 0) ctr->rank_covered = (fast && !empty) ? 1 : 0;
+    if (kst) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        kstamp(kst, bid_, 3);
+    }
 }
 
 template <int TB>  // TB >= T; the candidates are ranked here only for TB <= RT
@@ -785,8 +781,8 @@ __global__ __launch_bounds__(256) void k_select_open(
     unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
     const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
     const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
-    unsigned char *__restrict__ rtype, int R) {
-    select_open_body<TB>(pages, npages, tail_fill, prio, meta, seqa, T, anchor, theta, need, binoff, csum, gh, candlen, candoff_out, ckey, cslot, gcut, spec, specn, pbase, pwide, ctr, crank, lv, rtype, R, blockIdx.x, gridDim.x);
+    unsigned char *__restrict__ rtype, int R, unsigned long long *kst) {
+    select_open_body<TB>(pages, npages, tail_fill, prio, meta, seqa, T, anchor, theta, need, binoff, csum, gh, candlen, candoff_out, ckey, cslot, gcut, spec, specn, pbase, pwide, ctr, crank, lv, rtype, R, blockIdx.x, gridDim.x, kst);
 }
 
 // ---------------------------------------------------------------- per-type sort (multi-priority bins only)
@@ -2950,6 +2946,23 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     return ADLBQ_OK;
 }
 
+// diagnostic ("kernel_stamps"): the stamp rows of pass 1 (which 0) or pass 2 (1) of the next batch, or nullptr
+static unsigned long long *kst_for(adlbq_server *h, int n, int which) {
+    if (!h->kstamps || n <= 0) return nullptr;
+    if (n > h->cap_kst) {
+        hipStreamSynchronize(h->stream);
+        if (h->d_kst) hipFree(h->d_kst);
+        h->cap_kst = n;
+        if (hipMalloc((void **)&h->d_kst, sizeof(unsigned long long) * 8 * n) != hipSuccess) {
+            h->d_kst = nullptr;
+            h->cap_kst = 0;
+            return nullptr;
+        }
+    }
+    h->n_kst = n;
+    return h->d_kst + (size_t)which * 4 * n;
+}
+
 static int ensure_scan_capacity(adlbq_server *h, int npages) {
     const long long C = (long long)std::max(h->T, 1) * NB;
     const long long need_gh = (long long)npages * C, nchunks = (npages + CHUNK - 1) / CHUNK;
@@ -3009,6 +3022,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     unsigned int *csum = h->d_csum + (long long)par * h->cap_csum, *zcs = h->d_csum + (long long)(par ^ 1) * h->cap_csum;
     HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
                 h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, zcs, h->csum_used[par ^ 1], pg0};
+    ha.kst = kst_for(h, np, 0);
     if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
         h->csum_used[par] = (long long)((np + CHUNK - 1) / CHUNK) * C;
         h->csum_used[par ^ 1] = 0;
@@ -3065,7 +3079,8 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,
             h->d_need, h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot,
             h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr,
-            (sort || !h->rank_in_select) ? nullptr : h->d_crank, (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R);
+            (sort || !h->rank_in_select) ? nullptr : h->d_crank, (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R,
+            kst_for(h, np, 1));
         stage_end(h, "select", ev);
         if (sort) {  // a reserve batch sorts inside k_rank
             stage_begin(h, "sort", &ev);
@@ -3891,7 +3906,7 @@ static int launch_recorded(adlbq_server *h, GroupRec &r) {
         sel<<<g.grid, 256, r.lds_sel, s>>>(g.pages, g.npages, g.tail_fill, g.prio, g.meta, g.seqa, g.T, g.anchor,
                                            g.theta, g.need, g.binoff, g.csum, g.gh, g.candlen, g.candoff_out, g.ckey,
                                            g.cslot, g.gcut, g.spec, g.specn, g.pbase, g.pwide, g.ctr, g.crank, g.lv,
-                                           g.rtype, g.R);
+                                           g.rtype, g.R, nullptr);
     }
     if (r.kinds & GK_RANK) k_rank<<<r.rank.grid, RANK_TILE, 0, s>>>(r.rank.ra);
     if (r.kinds & GK_CHAIN) {

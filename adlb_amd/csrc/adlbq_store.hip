@@ -1424,7 +1424,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_mask, h->d_tmatch, h->d_umatch, h->d_reqbuf, h->d_respbuf, h->d_dem, h->d_theta,
                     h->d_need, h->d_candoff, h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_rank_sync, h->d_gh, h->d_csum,
                     h->d_ckey, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_crank, h->d_result,
-                    h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
+                    h->d_kst, h->d_putrec, h->d_putout, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht, h->d_chcnt, h->d_chE, h->d_chflag, h->d_stamps, h->d_export,
                     h->d_navail, h->d_rqx, h->d_apply, h->d_apply_bad, h->d_pmask, h->d_lv, h->d_rtype, h->d_pm_over,
                     h->d_tkeys, h->d_tkeys2, h->d_tvals, h->d_tvals2, h->d_tstart, h->d_tend, h->d_tsort,
                     h->d_ssort, h->d_kb, h->d_getclaim, h->d_getbuf, h->d_info, h->d_crem,
@@ -2320,6 +2320,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->put_always_match = value ? 1 : 0;
         return ADLBQ_OK;
     }
+    if (n == "kernel_stamps") {
+        h->kstamps = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "chain_stamps") {
         h->chain_stamps = value ? 1 : 0;
         return ADLBQ_OK;
@@ -2393,6 +2397,31 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     hipSetDevice(h->device);
     if (refresh_counters(h)) return -1;
     std::string n(name);
+    if (n.rfind("kst_", 0) == 0 && h->d_kst && h->n_kst > 0) {
+        // diagnostic: "kst_{hist,sel}_{1,2,3}" = median over workgroups of (stamp K - stamp 0) in ns,
+        // "kst_{hist,sel}_start" = the spread of the start stamps, "kst_{hist,sel}_span" = first start to last end
+        const int which = n.compare(4, 4, "hist") == 0 ? 0 : 1;
+        const std::string what = n.substr(which == 0 ? 9 : 8);
+        std::vector<unsigned long long> st(4 * (size_t)h->n_kst);
+        if (hipMemcpy(st.data(), h->d_kst + (size_t)which * 4 * h->n_kst, sizeof(unsigned long long) * st.size(),
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+        unsigned long long s0 = ~0ull, s1 = 0, e1 = 0;
+        std::vector<long long> d;
+        const int k = (what.size() == 1) ? what[0] - '0' : 0;
+        for (int i = 0; i < h->n_kst; i++) {
+            const unsigned long long *r = &st[4 * (size_t)i];
+            s0 = std::min(s0, r[0]);
+            s1 = std::max(s1, r[0]);
+            e1 = std::max(e1, r[3]);
+            if (k >= 1 && k <= 3 && r[k] >= r[0]) d.push_back((long long)(r[k] - r[0]) * 10);
+        }
+        if (what == "start") return (long long)(s1 - s0) * 10;
+        if (what == "span") return (long long)(e1 - s0) * 10;
+        if (d.empty()) return -1;
+        std::sort(d.begin(), d.end());
+        return d[d.size() / 2];
+    }
     if (n == "chain_rounds") return h->ctr.chain_rounds;
     if (n == "chain_passes") return h->ctr.chain_passes;
     if (n == "chain_recomputed") return h->ctr.chain_recomputed;

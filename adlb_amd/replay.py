@@ -157,6 +157,38 @@ def replay_many(servers, traces, cap_factor: int = 8):
     return [o[: nout[j]].copy() for j, o in enumerate(outs)], [ncall[j] for j in range(n)]
 
 
+def replay_rounds(servers, traces, k: int, rqcap: int, steal_cap: int = 1 << 22):
+    """Config 5 at its SURVEY shape (adlb_replay.cpp, adlbsrv_replay_rounds): the
+    shards' traces with steal rounds (event 23 in every trace), device-side
+    batches between the rounds from one host thread per shard, one steal-group
+    round (export depth k, rqcap parked Reserves per shard) at each marker.
+    Returns (outputs per shard, steals (n, 15), seconds, calls per shard)."""
+    import ctypes
+
+    from . import core
+    lib = core.load()
+    n = len(servers)
+    trs = [np.ascontiguousarray(np.asarray(t, dtype=np.int32)) for t in traces]
+    outs = [np.empty(2 * t.size + (1 << 20), np.int32) for t in trs]
+    steals = np.empty((steal_cap, 15), np.int32)
+    PA = ctypes.c_void_p * n
+    LA = ctypes.c_longlong * n
+    hs = PA(*[s.h.value if hasattr(s.h, "value") else s.h for s in servers])
+    tp = PA(*[t.ctypes.data for t in trs])
+    lens = LA(*[t.size for t in trs])
+    op = PA(*[o.ctypes.data for o in outs])
+    caps = LA(*[o.size for o in outs])
+    nout, ncall = LA(), LA()
+    nst = ctypes.c_longlong()
+    sec = ctypes.c_double()
+    rc = lib.adlbsrv_replay_rounds(hs, n, servers[0].T, tp, lens, k, rqcap, op, caps, nout, steals.ctypes.data,
+                                   steal_cap, ctypes.byref(nst), ctypes.byref(sec), ncall)
+    if rc:
+        raise RuntimeError(f"adlbsrv_replay_rounds: {lib.adlbsrv_replay_error().decode(errors='replace')}")
+    return ([o[: nout[j]].copy() for j, o in enumerate(outs)], steals[: nst.value].copy(), sec.value,
+            [ncall[j] for j in range(n)])
+
+
 def server_process(trace_path: str, out_path: str, user_types, num_app_ranks: int, num_servers: int, idx: int,
                    device: int, barrier, q) -> None:
     """One ADLB server as its own process (the reference runs one per MPI rank):
