@@ -63,6 +63,7 @@ SIGNATURES = {
     "adlbsrv_group_settle": (c_int, [P, P, c_int, P]),
     "adlbsrv_group_stat": (ctypes.c_longlong, [P, c_int]),
     "adlbsrv_replay_many": (c_int, [P, c_int, c_int, P, P, P, P, P, P]),
+    "adlbsrv_replay_prof": (None, [P]),
     "adlbsrv_replay_rounds": (c_int, [P, c_int, c_int, P, P, c_int, c_int, P, P, P, P, ctypes.c_longlong, P, P, P]),
     "adlbsrv_replay_error": (ctypes.c_char_p, []),
 }

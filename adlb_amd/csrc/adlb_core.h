@@ -130,6 +130,7 @@ const char *adlbsrv_replay_error(void);
 int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
                           int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
                           int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls);
+void adlbsrv_replay_prof(double *out8);
 
 /* state for the driver */
 int adlbsrv_num_parked(adlbsrv *s);     /* rq->count */

@@ -262,12 +262,23 @@ int out_ints(int op, int T) {
 }  // namespace
 
 thread_local std::string g_rerr;
+// host seconds of the last rounds replay, summed over the shards' threads:
+// put, reserve, get, qmstat rows, set rows, waiting at the round barrier, the round itself
+double g_rprof[8];
+std::mutex g_rprof_mu;
 
 }  // namespace
 
 extern "C" {
 
 const char *adlbsrv_replay_error(void) { return g_rerr.c_str(); }
+
+// host seconds of the last adlbsrv_replay_rounds, summed over its threads: put,
+// reserve, get, qmstat row, set row, round barrier (waiting + the round), the
+// rounds alone (the last arriver's work), wall
+void adlbsrv_replay_prof(double *out8) {
+    for (int q = 0; q < 8; q++) out8[q] = g_rprof[q];
+}
 
 int adlbsrv_replay_many(adlbq_server **hs, int n, int ntypes, const int *const *traces, const long long *lens,
                         int *const *outs, const long long *caps, long long *nouts, long long *ncalls) {
@@ -383,11 +394,13 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
     long long ns = 0;
     std::string gerr;
     std::vector<int> resp;
+    double round_s = 0.0;
     auto round_barrier = [&](bool ok) {  // every thread; the last one in runs the round
         std::unique_lock<std::mutex> lk(mu);
         if (!ok) failed = true;
         const long long my = gen;
         if (++arrived == S) {
+            const auto r0 = std::chrono::steady_clock::now();
             if (!failed) {
                 int dec = 0, set = 0, cnt = 0;
                 if (adlbq_steal_group_export(g, nullptr) || adlbq_steal_group_settle(g, nullptr, 1, &dec, &set)) {
@@ -408,6 +421,7 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
                     }
                 }
             }
+            round_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - r0).count();
             arrived = 0;
             gen++;
             cv.notify_all();
@@ -416,10 +430,13 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
         }
         return !failed;
     };
+    for (double &v : g_rprof) v = 0.0;
     auto work = [&](int j) {
         RShard &r = sh[(size_t)j];
         adlbq_server *h = r.h;
         bool ok = true;
+        double prof[8] = {0};
+        using clk = std::chrono::steady_clock;
         for (const RCall &c : r.calls) {
             if (!ok) {
                 if (c.op == OP_ROUND) round_barrier(false);
@@ -427,19 +444,26 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
             }
             r.ncalls++;
             int rc = 0;
+            const auto c0 = clk::now();
+            const int slot = c.op == OP_PUT ? 0 : c.op == OP_RESERVE ? 1 : c.op == OP_GET ? 2 : c.op == OP_QMROW ? 3
+                             : c.op == OP_SETROW ? 4 : 5;
             switch (c.op) {
             case OP_PUT: rc = adlbq_put_batch_device(h, c.n, r.put.data() + c.in, r.dout + c.dout); break;
             case OP_RESERVE: rc = adlbq_reserve_batch_device(h, c.n, r.din + c.in, r.dout + c.dout); break;
             case OP_GET: rc = adlbq_get_reserved_batch_device(h, c.n, r.din + c.in, r.dout + c.dout); break;
             case OP_QMROW: rc = adlbq_qmstat_row(h, &r.hqm[(size_t)c.hout], &r.hqm[(size_t)c.hout + 1]); break;
             case OP_SETROW: rc = adlbq_set_qmstat_row(h, c.x[0], c.x[1], (double)c.x[2], c.x + 3); break;
-            case OP_ROUND: ok = round_barrier(true); continue;
+            case OP_ROUND: ok = round_barrier(true); break;
             }
+            prof[slot] += std::chrono::duration<double>(clk::now() - c0).count();
+            if (c.op == OP_ROUND) continue;
             if (rc) {
                 r.err = std::string("call ") + std::to_string(c.op) + ": " + adlbq_last_error();
                 ok = false;
             }
         }
+        std::lock_guard<std::mutex> lk(g_rprof_mu);
+        for (int q = 0; q < 6; q++) g_rprof[q] += prof[q];
     };
     const auto t0 = std::chrono::steady_clock::now();
     {
@@ -454,6 +478,8 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
     }
     const auto t1 = std::chrono::steady_clock::now();
     if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+    g_rprof[6] = round_s;
+    g_rprof[7] = std::chrono::duration<double>(t1 - t0).count();
     *nsteals = ns;
     adlbq_steal_group_destroy(g);
     // ---- untimed: outputs back, in the replay layout

@@ -51,7 +51,6 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long v, i
 // conflicts).  Each wave also writes its chain segment's count of requests
 // with a non-empty type set (the chain's level guess), tmatch starts at -1,
 // and block 0 resets the chain's per-batch counters.
-constexpr int PREP_ROW = ADLBQ_RESERVE_INTS + 1;
 
 struct PrepArgs {
     const int *reqs;
@@ -74,7 +73,7 @@ struct PrepArgs {
 };
 
 template <int TB>  // TB >= T; TB <= 8: the user types are compared in registers
-__device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int *__restrict__ rows) {
+__device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk) {
     __shared__ int su[ADLBQ_MAX_TYPES], sd[ADLBQ_MAX_TYPES];
     const int *__restrict__ reqs = a.reqs, *__restrict__ utypes = a.utypes;
     const int R = a.R, T = a.T;
@@ -82,10 +81,18 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
     int *dem = a.dem, *__restrict__ seg_cnt = a.seg_cnt, *__restrict__ tmatch = a.tmatch;
     DevCounters *ctr = a.ctr;
     const int j0 = blk * PREP_BLOCK, nj = min(PREP_BLOCK, R - j0);
-    const int *src = reqs + (long long)ADLBQ_RESERVE_INTS * j0;
-    for (int i = threadIdx.x; i < nj * ADLBQ_RESERVE_INTS; i += PREP_BLOCK) {
-        const int r = i / ADLBQ_RESERVE_INTS, c = i - r * ADLBQ_RESERVE_INTS;
-        rows[r * PREP_ROW + c] = src[i];
+    // this thread's request record, straight into registers (9 x 8 B: a record is 72 B,
+    // so every record is 8-B aligned; the wave's loads cover one contiguous 4.6 KB run)
+    static_assert(ADLBQ_RESERVE_INTS == 18, "record layout");
+    int row[ADLBQ_RESERVE_INTS];
+    if ((int)threadIdx.x < nj) {
+        const int2 *src = reinterpret_cast<const int2 *>(reqs + (long long)ADLBQ_RESERVE_INTS * (j0 + threadIdx.x));
+#pragma unroll
+        for (int i = 0; i < ADLBQ_RESERVE_INTS / 2; i++) {
+            const int2 v = src[i];
+            row[2 * i] = v.x;
+            row[2 * i + 1] = v.y;
+        }
     }
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         su[t] = utypes[t];
@@ -126,8 +133,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
     unsigned long long m = 0;
     if (threadIdx.x < nj) {
         tmatch[j] = -1;
-        if (a.rh != nullptr) a.rh[j] = make_int2(rows[threadIdx.x * PREP_ROW], rows[threadIdx.x * PREP_ROW + 1]);
-        const int *rt = rows + threadIdx.x * PREP_ROW + 2;
+        if (a.rh != nullptr) a.rh[j] = make_int2(row[0], row[1]);
+        const int *rt = row + 2;
         bool wild = false;
 #pragma unroll
         for (int i = 0; i < NREQ; i++) {
@@ -150,7 +157,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
         if (wild) m = T >= 64 ? ~0ull : ((1ull << T) - 1);
         mask[j] = m;
         if (a.tlist != nullptr && m) {  // the Reserve's rank owns targeted units: list it under that bucket
-            const int r = rows[threadIdx.x * PREP_ROW];
+            const int r = row[0];
             const int b = (r >= 0 && r < a.A) ? a.rank2b[r] : -1;
             if (b >= 0) {
                 const int k = atomicAdd(&a.tcnt[b], 1);
@@ -182,6 +189,11 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk, int
 // HK lane-interleaved copies so that lanes hitting the same (type, bin) column
 // (most units fall in a few far bins) do not serialise one LDS atomic.
 constexpr int HK = 4;
+
+// lanes below this one with their bit set in m
+__device__ __forceinline__ unsigned int mbcnt64(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned int)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)m, 0u));
+}
 
 // diagnostic ("kernel_stamps"): per workgroup, the constant clock (100 MHz) at
 // phase boundaries of pass 1 / pass 2, [workgroup][4]
@@ -238,15 +250,51 @@ __device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const
     }
 }
 
+// The far bins, lumped (T <= 8).  With a guessed cut gc below its anchor an,
+// a type's units in bin lump_bin(an, gc) or deeper -- deeper than about twice
+// the guessed depth -- all belong to the type's last bin NB - 1, and pass 1
+// counts them per type with one ballot per type instead of binning each one.
+// When the guess holds, every threshold lies above the lump; when it does not,
+// the lump is a multi-priority bin like any other (listed, then sorted).
+// Pass 1, k_thresholds and pass 2 bin by this same rule.  NB: nothing lumped.
+__host__ __device__ __forceinline__ int lump_bin(long long an, long long gc) {
+    if (gc == LLONG_MAX || gc > an || an - gc >= (1ll << 30)) return NB;
+    long long d = 2 * (an - gc) + 2;
+    int b;  // bin_of(d), host and device
+    if (d < NBX) b = (int)d;
+    else {
+        int o = 0;
+        while ((d >> (o + 1)) != 0) o++;
+        b = o < OCT_H ? NBX + 2 * (o - 5) + (int)((d >> (o - 1)) & 1) : NBX + NBH + (o - OCT_H);
+        if (b > NB - 1) b = NB - 1;
+    }
+    return b + 1 >= NB - 1 ? NB : b + 1;
+}
+
 // Pass 1 over one page (four waves, a quarter page each): per (type, bin)
 // column the available units (LDS copies, then the page's row and the chunk
-// sums), and in each wave's list the units at or above the guessed cut, in
-// slot order.  NARROW: the page's prios are its base plus the offsets packed
-// into meta, so only the meta column is loaded and held (the wide form holds
-// the prio column as well: 16 more registers).
-template <bool NARROW>
+// sums), and each wave's speculative list, in slot order.  NARROW: the page's
+// prios are its base plus the offsets packed into meta, so only the meta
+// column is loaded (the wide form holds the prio column as well).
+//   LUMP (T <= 8): a unit is near when it lies above its type's lump
+//   (lump_bin), and the list is every near unit.  On a narrow page a unit is
+//   classified through an LDS table indexed by the low ten bits of its meta
+//   (status, type): {far cut in the page's offsets, counter increment}; an
+//   unavailable unit's entry {INT_MAX, 0} makes it far and uncounted.  A far
+//   unit adds to 8-bit per-type counters in a register (four types each); a
+//   near one (a few per wave when the guess holds) is staged in LDS, then
+//   binned one per lane.  Should a wave's near units overflow the list, they
+//   are binned from the registers and the list is marked unusable.  A wide
+//   page bins every unit, its far ones into the lump.
+//   Otherwise (T > 8) every unit is binned and the list holds the units at or
+//   above the guessed cut.
+constexpr int HIST_TAB = 1024;  // LUMP table entries (10 meta bits), 2 words each
+
+template <bool NARROW, bool LUMP, int TB>
 __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, const int pg, const int fill,
-                                               const int2 *sag, unsigned int *__restrict__ hist /* [C][HK] */) {
+                                               unsigned int *__restrict__ hist /* [C][HK], stage, table */,
+                                               const uint4 *pre) {
+    __shared__ int sanc[ADLBQ_MAX_TYPES], scv[ADLBQ_MAX_TYPES], slb[ADLBQ_MAX_TYPES];
     const int T = a.T, C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const long long base = (long long)pg << PAGE_SHIFT;
     const uint4 *M4 = reinterpret_cast<const uint4 *>(a.meta + base);
@@ -256,11 +304,32 @@ __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, c
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int idx = (w * 4 + k) * 64 + lane;
-        mv[k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+        mv[k] = pre != nullptr ? pre[k] : idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
         if constexpr (!NARROW) pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
     }
     const int pb = NARROW ? a.pbase[pg] : 0;
-    __syncthreads();  // sag and the zeroed histogram (the caller's stores) are visible
+    // the table path needs every offset above LOWEST (a base above it)
+    const bool fast = NARROW && LUMP && pb > LOWEST;
+    unsigned int *stg = hist + HK * C + w * 2 * SPEC_CAP;  // near units: (type << 12 | slot), prio
+    uint2 *tab = reinterpret_cast<uint2 *>(hist + HK * C + 8 * SPEC_CAP);
+    if ((int)threadIdx.x < 4 * T) {
+        const int t = (int)threadIdx.x % T, st = (int)threadIdx.x / T;  // status: bit 0 LIVE, bit 1 PINNED
+        const long long an = a.anchor[t], gc = a.gcut[t];
+        const int lb = LUMP ? lump_bin(an, gc) : NB;
+        const long long fc = lb < NB ? an - bin_lo(lb) - pb : (long long)INT_MIN;  // far: value <= fc
+        const int fci = (int)std::max(std::min(fc, (long long)INT_MAX), (long long)INT_MIN);
+        if (st == 0) {
+            sanc[t] = (int)an;
+            slb[t] = lb;
+            scv[t] = LUMP ? fci : (int)std::max(std::min(gc, (long long)INT_MAX), (long long)INT_MIN);
+        }
+        if (fast)
+            tab[(st << 8) | t] = st == 1 ? make_uint2((unsigned int)fci, 1u << (8 * (t & 3)))
+                                         : make_uint2((unsigned int)INT_MAX, 0u);
+    }
+    if (fast && threadIdx.x == 0) tab[0] = make_uint2((unsigned int)INT_MAX, 0u);  // slots past the fill (meta 0)
+    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+    __syncthreads();
     if (a.kst) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         kstamp(a.kst, p, 1);
@@ -269,40 +338,153 @@ __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, c
     unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
     const unsigned long long lt = lanemask_lt();
     int sn = 0;
+    if (LUMP && fast) {
+        unsigned int c0 = 0u, c1 = 0u;  // far units per type, 8 bits each: types 0-3, 4-7
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-        int pr[4];
-        if constexpr (NARROW) {
+        for (int k = 0; k < 4; k++) {
+            __builtin_amdgcn_sched_barrier(0);  // one quarter's table reads at a time (registers)
+            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+            uint2 e[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) pr[q] = pb + (int)(mm[q] >> M_OFF_SHIFT);
-        } else {
-            pr[0] = pv[k].x, pr[1] = pv[k].y, pr[2] = pv[k].z, pr[3] = pv[k].w;
+            for (int q = 0; q < 4; q++) e[q] = tab[mm[q] & 0x3ffu];
+            unsigned long long b[4];
+            bool ne[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const bool far = (int)(mm[q] >> M_OFF_SHIFT) <= (int)e[q].x;
+                ne[q] = !far;
+                if constexpr (TB <= 4) {
+                    c0 += far ? e[q].y : 0u;
+                } else {
+                    const bool hi = (mm[q] & 4u) != 0u;
+                    c0 += (far && !hi) ? e[q].y : 0u;
+                    c1 += (far && hi) ? e[q].y : 0u;
+                }
+                b[q] = __builtin_amdgcn_ballot_w64(!far);
+            }
+            if (!(b[0] | b[1] | b[2] | b[3])) continue;
+            int pos = sn + (int)mbcnt64(b[0]) + (int)mbcnt64(b[1]) + (int)mbcnt64(b[2]) + (int)mbcnt64(b[3]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (ne[q]) {
+                    if (pos < SPEC_CAP) {
+                        stg[pos] = ((mm[q] & M_TYPE) << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+                        stg[SPEC_CAP + pos] = (unsigned int)(pb + (int)(mm[q] >> M_OFF_SHIFT));
+                    }
+                    pos++;
+                }
+            }
+            sn += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
         }
-        int col[4];
-        bool in[4];
+        if (sn <= SPEC_CAP) {  // the staged near units: binned one per lane, listed with their columns
+            __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
+            for (int i = lane; i < sn; i += 64) {
+                const unsigned int ev = stg[i];
+                const int t = (int)(ev >> 12), pr = (int)stg[SPEC_CAP + i];
+                const int col = t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)pr);
+                atomicAdd(&my[col * HK], 1u);
+                sp[i] = ((unsigned int)col << 12) | (ev & (PAGE - 1));
+            }
+        } else {  // overflow (no usable guess): the near units binned from the registers, no list
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
-            const int t = mm[q] & M_TYPE;
-            const int2 ag = sag[t];
-            col[q] = t * NB + bin_of32((unsigned int)ag.x - (unsigned int)pr[q]);  // distance < 2^32
-            in[q] = av && pr[q] >= ag.y;
-            if (av) atomicAdd(&my[col[q] * HK], 1u);
-        }
-        const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
-                                 b3 = __ballot(in[3]);
-        if (!(b0 | b1 | b2 | b3)) continue;
-        int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+            for (int k = 0; k < 4; k++) {
+                uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            if (in[q]) {
-                if (pos < SPEC_CAP)
-                    sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
-                pos++;
+                for (int q = 0; q < 4; q++) asm volatile("" : "+v"(mm[q]));  // recomputed here, not kept live from above
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int off = (int)(mm[q] >> M_OFF_SHIFT);
+                    if (off > (int)tab[mm[q] & 0x3ffu].x) {
+                        const int t = mm[q] & M_TYPE;
+                        atomicAdd(&my[(t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)(pb + off))) * HK], 1u);
+                    }
+                }
             }
         }
-        sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+        // the far counts: 16-bit lanes of the even and odd bytes, summed over the wave
+        unsigned int f[4] = {c0 & 0x00ff00ffu, (c0 >> 8) & 0x00ff00ffu, c1 & 0x00ff00ffu, (c1 >> 8) & 0x00ff00ffu};
+#pragma unroll
+        for (int i = 0; i < (TB <= 4 ? 2 : 4); i++)
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) f[i] += __shfl_xor(f[i], o, 64);
+        if (lane == 0)
+#pragma unroll
+            for (int u = 0; u < TB; u++) {
+                // type u: word (u >> 2) * 2 + (u & 1), half (u >> 1) & 1
+                const unsigned int v = (f[(u >> 2) * 2 + (u & 1)] >> (16 * ((u >> 1) & 1))) & 0xffffu;
+                if (u < T && v) atomicAdd(&hist[(u * NB + NB - 1) * HK], v);
+            }
+    } else if (LUMP) {  // a wide page (or a base at LOWEST): every unit binned, the far ones into the lump
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+            int pr[4];
+            if constexpr (NARROW) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) pr[q] = pb + (int)(mm[q] >> M_OFF_SHIFT);
+            } else {
+                pr[0] = pv[k].x, pr[1] = pv[k].y, pr[2] = pv[k].z, pr[3] = pv[k].w;
+            }
+            int col[4];
+            bool ne[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
+                const int t = mm[q] & M_TYPE;
+                const int bq = bin_of32((unsigned int)sanc[t] - (unsigned int)pr[q]);
+                ne[q] = av && bq < slb[t];
+                col[q] = t * NB + (ne[q] ? bq : NB - 1);
+                if (av) atomicAdd(&my[col[q] * HK], 1u);
+            }
+            const unsigned long long b0 = __ballot(ne[0]), b1 = __ballot(ne[1]), b2 = __ballot(ne[2]),
+                                     b3 = __ballot(ne[3]);
+            if (!(b0 | b1 | b2 | b3)) continue;
+            int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (ne[q]) {
+                    if (pos < SPEC_CAP)
+                        sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+                    pos++;
+                }
+            }
+            sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+            int pr[4];
+            if constexpr (NARROW) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) pr[q] = pb + (int)(mm[q] >> M_OFF_SHIFT);
+            } else {
+                pr[0] = pv[k].x, pr[1] = pv[k].y, pr[2] = pv[k].z, pr[3] = pv[k].w;
+            }
+            int col[4];
+            bool in[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
+                const int t = mm[q] & M_TYPE;
+                col[q] = t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)pr[q]);  // distance < 2^32
+                in[q] = av && pr[q] >= scv[t];
+                if (av) atomicAdd(&my[col[q] * HK], 1u);
+            }
+            const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
+                                     b3 = __ballot(in[3]);
+            if (!(b0 | b1 | b2 | b3)) continue;
+            int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (in[q]) {
+                    if (pos < SPEC_CAP)
+                        sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+                    pos++;
+                }
+            }
+            sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+        }
     }
     if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
@@ -322,23 +504,62 @@ __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, c
     }
 }
 
-__device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist) {
-    __shared__ int2 sag[ADLBQ_MAX_TYPES];
-    const int T = a.T, C = T * NB;
+template <int TB>
+__device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist,
+                                          const uint4 *pre) {
     const int pg = a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
     const int fill = (p == a.npages - 1) ? a.tail_fill : PAGE;
     kstamp(a.kst, p, 0);
-    const int wide = a.pwide[pg];
-    for (int t = threadIdx.x; t < T; t += blockDim.x)
-        sag[t] = make_int2((int)a.anchor[t], (int)std::max(std::min(a.gcut[t], (long long)INT_MAX), (long long)INT_MIN));
-    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
-    if (wide) hist_page_body<false>(a, p, pg, fill, sag, hist);
-    else hist_page_body<true>(a, p, pg, fill, sag, hist);
+    if (a.pwide[pg]) hist_page_body<false, (TB <= 8), TB>(a, p, pg, fill, hist, pre);
+    else hist_page_body<true, (TB <= 8), TB>(a, p, pg, fill, hist, pre);
+}
+
+// HIST_PP pages per pass-1 workgroup: the later pages' meta loads are issued
+// before the first page is counted and arrive while it is.  Measured at the
+// metric size (r05): 2 pages per workgroup 22.5 us against 19.5 for one (the
+// workgroups' start ramp stretches under the heavier load flood), so one.
+#ifndef ADLBQ_HIST_PP
+#define ADLBQ_HIST_PP 1
+#endif
+// (T <= 8, the table path; a larger T bins every unit and keeps one page per workgroup)
+__host__ __device__ constexpr int hist_pp(int TB) { return TB <= 8 ? ADLBQ_HIST_PP : 1; }
+#ifndef ADLBQ_HIST_WAVES
+#define ADLBQ_HIST_WAVES 6  // waves per SIMD k_prep_hist<4> is compiled for (<= 80 VGPRs, no spill)
+#endif
+__host__ __device__ constexpr int hist_waves(int TB) {
+    return ADLBQ_HIST_PP == 1 ? 1 : TB <= 4 ? ADLBQ_HIST_WAVES : TB <= 8 ? 5 : 1;
+}
+
+template <int TB>
+__device__ __forceinline__ void hist_pages(const HistArgs &a, const int q, unsigned int *__restrict__ hist) {
+    constexpr int HIST_PP = hist_pp(TB);
+    const int p0 = q * HIST_PP, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint4 nb[HIST_PP > 1 ? HIST_PP - 1 : 1][4];
+#pragma unroll
+    for (int i = 1; i < HIST_PP; i++) {
+        const int p = p0 + i;
+        const bool ok = p < a.npages;
+        const int pg = !ok ? 0 : a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
+        const int fill = !ok ? 0 : (p == a.npages - 1) ? a.tail_fill : PAGE;
+        const uint4 *M4 = reinterpret_cast<const uint4 *>(a.meta + ((long long)pg << PAGE_SHIFT));
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int idx = (w * 4 + k) * 64 + lane;
+            nb[i - 1][k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+        }
+    }
+    hist_page<TB>(a, p0, hist, nullptr);
+#pragma unroll
+    for (int i = 1; i < HIST_PP; i++) {
+        if (p0 + i >= a.npages) break;
+        __syncthreads();  // the previous page's histogram is read out
+        hist_page<TB>(a, p0 + i, hist, nb[i - 1]);
+    }
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
 // workgroups [0, nprep) prepare 256 requests each, the rest count one page.
-constexpr int PREP_LDS = (int)sizeof(int) * PREP_BLOCK * PREP_ROW;
+constexpr int PREP_LDS = 0;  // the request records go straight to registers
 
 
 // The lowest prio in bins 0..th of a type with anchor an (bin_of: exact bins
@@ -355,7 +576,8 @@ __device__ __forceinline__ long long cut_of(int th, long long an) {
 __device__ void type_threshold(const int t, const int *__restrict__ dem, int *theta, int *need, int *candlen,
                                int *needsort, int *binoff, const unsigned int *coltot, int *type_cnt,
                                const long long *__restrict__ anchor, long long *__restrict__ anchor_next,
-                               long long *__restrict__ gcut_next, int guess) {
+                               long long *__restrict__ gcut_next, int guess, const long long *__restrict__ gcut,
+                               int T) {
     const int lane = threadIdx.x & 63;
     // the last column of type t: wave 0, lane b = bin b (NB == 64), all totals loaded at once
     static_assert(NB == 64, "one lane per bin");
@@ -377,7 +599,9 @@ __device__ void type_threshold(const int t, const int *__restrict__ dem, int *th
             // the live maximum is at most anchor - (smallest distance of the first
             // non-empty bin): the next batch's anchor (applied when this batch ends)
             const int bb = __ffsll((long long)nz) - 1;
-            anchor_next[t] = anchor[t] - bin_lo(bb);
+            // a lump (T <= 8) starts at its lump bin
+            const int lb = (T <= 8 && bb == NB - 1) ? lump_bin(anchor[t], gcut[t]) : NB;
+            anchor_next[t] = anchor[t] - bin_lo(lb < NB ? lb : bb);
         }
         if (hit) {
             th = __ffsll((long long)hit) - 1;
@@ -420,7 +644,8 @@ __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn,
                                                      int *needsort, int *binoff, unsigned int *coltot,
                                                      int *type_cnt, const long long *__restrict__ anchor,
                                                      long long *__restrict__ anchor_next,
-                                                     long long *__restrict__ gcut_next, int guess, const int bid_, const int nbk_) {
+                                                     long long *__restrict__ gcut_next, int guess,
+                                                     const long long *__restrict__ gcut, const int bid_, const int nbk_) {
     constexpr int NW = TH_THREADS / 64;
     __shared__ unsigned int wsum[NW];
     __shared__ bool s_last;
@@ -470,7 +695,7 @@ __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn,
     __syncthreads();
     if (!s_last || threadIdx.x >= 64) return;
     type_threshold(t, dem, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next,
-                   guess);
+                   guess, gcut, T);
 }
 
 __global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, long long zn, int T, const int *__restrict__ dem, unsigned int *csum,
@@ -478,8 +703,9 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, lo
                                                      int *needsort, int *binoff, unsigned int *coltot,
                                                      int *type_cnt, const long long *__restrict__ anchor,
                                                      long long *__restrict__ anchor_next,
-                                                     long long *__restrict__ gcut_next, int guess) {
-    thresholds_body(zcs, zn, T, dem, csum, nchunks, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next, guess, blockIdx.x, gridDim.x);
+                                                     long long *__restrict__ gcut_next, int guess,
+                                                     const long long *__restrict__ gcut) {
+    thresholds_body(zcs, zn, T, dem, csum, nchunks, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next, guess, gcut, blockIdx.x, gridDim.x);
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
@@ -489,14 +715,14 @@ __device__ __forceinline__ void prep_hist_body(PrepArgs pa, int nprep, HistArgs 
     static_assert(PREP_BLOCK == 256, "one launch shape for both roles");
     extern __shared__ unsigned int lds[];
     if ((int)bid_ < nprep) {
-        prep_block<TB>(pa, bid_, reinterpret_cast<int *>(lds));
+        prep_block<TB>(pa, bid_);
     } else {
-        hist_page(ha, bid_ - nprep, lds);
+        hist_pages<TB>(ha, bid_ - nprep, lds);
     }
 }
 
 template <int TB>
-__global__ __launch_bounds__(256) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha) {
+__global__ __launch_bounds__(256, hist_waves(TB)) void k_prep_hist(PrepArgs pa, int nprep, HistArgs ha) {
     prep_hist_body<TB>(pa, nprep, ha, blockIdx.x);
 }
 
@@ -527,6 +753,7 @@ __device__ __forceinline__ void select_open_body(
     extern __shared__ unsigned int lds[];  // wc[4][C], then list[4][1024]
     __shared__ long long sanc[ADLBQ_MAX_TYPES], scut[ADLBQ_MAX_TYPES];
     __shared__ int sth[ADLBQ_MAX_TYPES], sneed[ADLBQ_MAX_TYPES], soff[ADLBQ_MAX_TYPES], slen[RT];
+    __shared__ int slb[TB <= 8 ? TB : 1];  // pass 1's lump bins (T <= 8)
     __shared__ int sbo[RT * NB];  // binoff (fast ranking)
     const int C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63, p = bid_;
     unsigned int *wc = lds;
@@ -556,11 +783,20 @@ __device__ __forceinline__ void select_open_body(
 #pragma unroll
     for (int k = 0; k < SPEC_CAP / 64; k++) se[k] = sp[k * 64 + lane];
     const long long cut_l = cut_of(th_l, an_l);
-    const bool use_spec = __ballot(th_l >= 0 && gc_l > cut_l) == 0 && sn <= SPEC_CAP;  // wave-uniform
+    // T <= 8: the list holds every unit above its type's lump, usable when no
+    // threshold lies in a lump; otherwise every unit at or above the guessed cut
+    const int lb_l = (TB <= 8 && tl) ? lump_bin(an_l, gc_l) : NB;
+    const bool use_spec = (TB <= 8 ? __ballot(th_l >= 0 && th_l >= lb_l) : __ballot(th_l >= 0 && gc_l > cut_l)) == 0 &&
+                          sn <= SPEC_CAP;  // wave-uniform
     int4 pv[4];
     uint4 mv[4];
     if (!use_spec) load_quarter(prio, meta, pbase, pwide, pages[p], fill, w, pv, mv);
-    if (p == 0 && threadIdx.x == 0) ctr->spec_page0 = use_spec ? 1 : 0;
+    // diagnostic: 1 used; else -(entries) when the list overflowed, or -100000 - (a type whose threshold passed the list)
+    if (p == 0 && threadIdx.x < 64) {
+        const unsigned long long bad = TB <= 8 ? __ballot(th_l >= 0 && th_l >= lb_l) : __ballot(th_l >= 0 && gc_l > cut_l);
+        if (threadIdx.x == 0)
+            ctr->spec_page0 = use_spec ? 1 : sn > SPEC_CAP ? -sn : -100000 - (bad ? __ffsll((long long)bad) - 1 : 99);
+    }
     // rank of this page's first unit in each of the thread's columns (only
     // columns at or below a threshold): the chunk's exclusive prefix
     // (k_thresholds) plus the counts of the chunk's earlier pages (hist_page)
@@ -589,6 +825,7 @@ __device__ __forceinline__ void select_open_body(
         sneed[lane] = nd_l;
         scut[lane] = cut_l;
         if (lane < RT) slen[lane] = len_l;
+        if (TB <= 8 && lane < TB) slb[lane] = lb_l;
     }
     // ranks computed here (k_rank then skips its tiles) when every threshold
     // lies in an exact bin: every candidate list is then in (prio desc,
@@ -647,7 +884,8 @@ __device__ __forceinline__ void select_open_body(
         for (int q = 0; q < 4; q++) {
             if (cnd[q]) {
                 const int t = mm[q] & M_TYPE;
-                const int col = t * NB + bin_of(sanc[t] - pr[q]);
+                const int bq = bin_of(sanc[t] - pr[q]);
+                const int col = t * NB + ((TB <= 8 && bq >= slb[t]) ? NB - 1 : bq);  // pass 1's lump
                 atomicAdd(&wc[w * C + col], 1u);
                 list[pos++] = ((unsigned int)col << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
             }
@@ -1438,9 +1676,6 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
 //     walks the segments in order from the exact prefix and recomputes only
 //     those whose start still differs (adversarial inputs; tests force it).
 
-__device__ __forceinline__ unsigned int mbcnt64(unsigned long long m) {
-    return __builtin_amdgcn_mbcnt_hi((unsigned int)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)m, 0u));
-}
 
 __device__ __forceinline__ unsigned long long wave_or_u64(unsigned long long v) {
 #pragma unroll
@@ -2792,7 +3027,7 @@ struct GPrep { PrepArgs pa; int nprep; HistArgs ha; int grid; };
 struct GThr {
     unsigned int *zcs; long long zn; int T; const int *dem; unsigned int *csum; int nchunks;
     int *theta, *need, *candlen, *needsort, *binoff; unsigned int *coltot; int *type_cnt;
-    const long long *anchor; long long *anchor_next, *gcut_next; int guess; int grid;
+    const long long *anchor; long long *anchor_next, *gcut_next; int guess; int grid; const long long *gcut;
 };
 struct GSel {
     const int *pages; int npages, tail_fill; const int *prio; const uint32_t *meta; const int *seqa; int T;
@@ -2814,7 +3049,7 @@ struct GroupRec {
 };
 
 template <int TB>
-__global__ __launch_bounds__(256) void k_prep_hist_g(const GPrep *__restrict__ t) {
+__global__ __launch_bounds__(256, hist_waves(TB) > 1 ? 5 : 1) void k_prep_hist_g(const GPrep *__restrict__ t) {
     const GPrep &g = t[blockIdx.y];
     if ((int)blockIdx.x >= g.grid) return;
     prep_hist_body<TB>(g.pa, g.nprep, g.ha, blockIdx.x);
@@ -2823,7 +3058,7 @@ __global__ __launch_bounds__(TH_THREADS) void k_thresholds_g(const GThr *__restr
     const GThr &g = t[blockIdx.y];
     if ((int)blockIdx.x >= g.grid) return;
     thresholds_body(g.zcs, g.zn, g.T, g.dem, g.csum, g.nchunks, g.theta, g.need, g.candlen, g.needsort, g.binoff,
-                    g.coltot, g.type_cnt, g.anchor, g.anchor_next, g.gcut_next, g.guess, blockIdx.x, g.grid);
+                    g.coltot, g.type_cnt, g.anchor, g.anchor_next, g.gcut_next, g.guess, g.gcut, blockIdx.x, g.grid);
 }
 template <int TB>
 __global__ __launch_bounds__(256) void k_select_open_g(const GSel *__restrict__ t) {
@@ -2950,8 +3185,8 @@ int ensure_req_capacity(adlbq_server *h, int n) {
 static unsigned long long *kst_for(adlbq_server *h, int n, int which) {
     if (!h->kstamps || n <= 0) return nullptr;
     if (n > h->cap_kst) {
-        hipStreamSynchronize(h->stream);
-        if (h->d_kst) hipFree(h->d_kst);
+        (void)hipStreamSynchronize(h->stream);
+        if (h->d_kst) (void)hipFree(h->d_kst);
         h->cap_kst = n;
         if (hipMalloc((void **)&h->d_kst, sizeof(unsigned long long) * 8 * n) != hipSuccess) {
             h->d_kst = nullptr;
@@ -3028,12 +3263,12 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
         h->csum_used[par ^ 1] = 0;
         h->csum_par = par ^ 1;
     }
-    const int npb = np;  // one page per pass-1 workgroup
+    const int pp = hist_pp(T <= 8 ? 8 : 64), npb = (np + pp - 1) / pp;  // pages per pass-1 workgroup
     const int grid = nprep + (scan ? npb : 0);
     if (grid > 0) {
         // pass 1: the histogram copies, then the four waves' speculative lists
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0,
-                                      scan ? sizeof(unsigned int) * (HK * C + 4 * SPEC_CAP) : 0);
+                                      scan ? sizeof(unsigned int) * (HK * C + 8 * SPEC_CAP + (T <= 8 ? 2 * HIST_TAB : 0)) : 0);
         stage_begin(h, "hist", &ev);
         auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
@@ -3055,13 +3290,13 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             h->grec->kinds |= GK_THR;
             h->grec->thr = GThr{zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                 h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor, h->d_anchor_next,
-                                h->d_gcut_next, nprep > 0 ? 1 : 0, C};
+                                h->d_gcut_next, nprep > 0 ? 1 : 0, C, h->d_gcut};
         } else {
             stage_begin(h, "thresholds", &ev);
             k_thresholds<<<C, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need,
                                                   h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot,
                                                   h->d_type_cnt, h->d_anchor, h->d_anchor_next, h->d_gcut_next,
-                                                  nprep > 0 ? 1 : 0);
+                                                  nprep > 0 ? 1 : 0, h->d_gcut);
             stage_end(h, "thresholds", ev);
         }
         stage_begin(h, "select", &ev);
@@ -3898,7 +4133,7 @@ static int launch_recorded(adlbq_server *h, GroupRec &r) {
         const GThr &g = r.thr;
         k_thresholds<<<g.grid, TH_THREADS, 0, s>>>(g.zcs, g.zn, g.T, g.dem, g.csum, g.nchunks, g.theta, g.need,
                                                    g.candlen, g.needsort, g.binoff, g.coltot, g.type_cnt, g.anchor,
-                                                   g.anchor_next, g.gcut_next, g.guess);
+                                                   g.anchor_next, g.gcut_next, g.guess, g.gcut);
     }
     if (r.kinds & GK_SEL) {
         const GSel &g = r.sel;

@@ -2417,6 +2417,14 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
             if (k >= 1 && k <= 3 && r[k] >= r[0]) d.push_back((long long)(r[k] - r[0]) * 10);
         }
         if (what == "start") return (long long)(s1 - s0) * 10;
+        if (what.rfind("startp", 0) == 0 || what.rfind("endp", 0) == 0) {  // percentile of the starts / ends
+            const bool st0 = what[0] == 's';
+            const int pc = std::atoi(what.c_str() + (st0 ? 6 : 4));
+            std::vector<long long> v;
+            for (int i = 0; i < h->n_kst; i++) v.push_back((long long)(st[4 * (size_t)i + (st0 ? 0 : 3)] - s0) * 10);
+            std::sort(v.begin(), v.end());
+            return v[std::min(v.size() - 1, v.size() * (size_t)pc / 100)];
+        }
         if (what == "span") return (long long)(e1 - s0) * 10;
         if (d.empty()) return -1;
         std::sort(d.begin(), d.end());

@@ -189,6 +189,19 @@ def replay_rounds(servers, traces, k: int, rqcap: int, steal_cap: int = 1 << 22)
             [ncall[j] for j in range(n)])
 
 
+def last_rounds_prof() -> dict:
+    """Host seconds of the last replay_rounds, summed over the shards' threads
+    (adlb_replay.cpp adlbsrv_replay_prof): per call kind, the round barrier
+    (waiting + the round), the rounds alone, and the wall time."""
+    import ctypes
+
+    from . import core
+    v = (ctypes.c_double * 8)()
+    core.load().adlbsrv_replay_prof(v)
+    return dict(zip(("put", "reserve", "get", "qmrow", "setrow", "barrier", "rounds", "wall"),
+                    [round(x, 4) for x in v]))
+
+
 def server_process(trace_path: str, out_path: str, user_types, num_app_ranks: int, num_servers: int, idx: int,
                    device: int, barrier, q) -> None:
     """One ADLB server as its own process (the reference runs one per MPI rank):

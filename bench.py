@@ -94,10 +94,12 @@ def parse():
     ap.add_argument("--wide-units", type=int, default=200_000)
     ap.add_argument("--wide-reserves", type=int, default=4096)
     ap.add_argument("--config5-only", action="store_true", help="only the config-5 leg")
-    ap.add_argument("--c5-procs", type=int, default=1, help="config 5: also run one server process per shard (1)")
-    ap.add_argument("--c5-shards", type=int, default=8, help="config 5: server shards (own event stream each)")
-    ap.add_argument("--c5-ranks", type=int, default=512, help="config 5: app ranks per shard")
-    ap.add_argument("--c5-rounds", type=int, default=60, help="config 5: stream rounds per shard")
+    ap.add_argument("--c5-shards", type=int, default=8, help="config 5: server shards (one steal group)")
+    ap.add_argument("--c5-ranks", type=int, default=4096, help="config 5: app ranks")
+    ap.add_argument("--c5-events", type=int, default=10_000_000, help="config 5: events over all shards")
+    ap.add_argument("--c5-round-every", type=int, default=10_000, help="config 5: events between steal rounds")
+    ap.add_argument("--c5-k", type=int, default=64, help="config 5: steal export depth per (shard, type)")
+    ap.add_argument("--c5-q0", type=int, default=128, help="config 5: generator's target queue depth")
     ap.add_argument("--config4-only", action="store_true", help="only the config-4 leg (profiling)")
     ap.add_argument("--c4-units", type=int, default=10_000_000, help="config 4: units (80%% targeted)")
     ap.add_argument("--c4-steps", type=int, default=5)
@@ -122,6 +124,7 @@ def parse():
     ap.add_argument("--chain-warm", type=int, default=None, help="metric leg: adlbq 'chain_warm' (0, 256, 512)")
     ap.add_argument("--c4-param", action="append", default=[], metavar="NAME=V",
                     help="config-4 leg: any adlbq_set_param (diagnostics), repeatable")
+    ap.add_argument("--kernel-stamps", action="store_true", help="diagnostic: phase stamps of passes 1 and 2 (us)")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
                     help="metric leg: any adlbq_set_param (diagnostics), repeatable")
     ap.add_argument("--c4-chain-stats", action="store_true",
@@ -553,118 +556,69 @@ def zipf_type_sets(rng, n_types, R, lo=1, hi=4):
 
 
 def bench_config5(args, torch, dist, world, rank, local, dev):
-    """Config 5: tsp.c-style branch-and-bound streams.  Each of
-    c5_shards servers has its own stream (synth.config5_stream: work Puts with
-    prio 1+len, targeted bound updates at prio 999999999, Reserves {2, 1} / {1}
-    / wildcard, Gets, unreserves, and every few rounds the qmstat rows, a
-    check_remote, tq updates, RFR completions, push choice and info queries).
-    The streams react to outcomes, so they are recorded first with the oracle
-    as the server (untimed; the GPU must give the same outcomes, checked), then
-    replayed through the C ABI in the timed region: consecutive Puts, Reserves
-    and Gets go as one batch each, every other event one call.  The same traces
-    replayed by the oracle on one core are the CPU figure.  Reports events/s."""
+    """Config 5 at its SURVEY §8(d) shape: S server shards serving tsp.c-style
+    branch-and-bound streams (oracle/gen_c5.c: work Puts at prio 1+len, bound
+    updates at prio 999999999 targeted to their home shard, Reserves {2, 1} /
+    {1} / wildcard that mostly hang, Gets on the holding shard), ~c5_events
+    events in all, and every c5_round_every events a qmstat snapshot exchange
+    and a steal round over all shards (SS_RFR, adlb.c:1802-1933).  The streams
+    react to outcomes and steals, so they are recorded first with the oracle as
+    every shard (untimed; the C generator); the engine then serves them through
+    adlbsrv_replay_rounds (adlb_replay.cpp): one host thread and HIP stream per
+    shard issuing device-side batches with no host sync per call, one
+    steal-group round (export depth c5_k) at each marker.  Every output and
+    every steal is checked against the oracle's.  Reports events/s; the CPU
+    figure is the oracle serving the same stream (generator in the loop)."""
     import oracle
-    from adlb_amd import replay, shards, synth
+    from adlb_amd import replay, shards
     from adlb_amd.server import Server
-    S, A, nr = args.c5_shards, args.c5_ranks, args.c5_rounds
-    traces, expect = [], []
+    S, A = args.c5_shards, args.c5_ranks
+    kw = dict(n_shards=S, n_ranks=A, round_every=args.c5_round_every, k=args.c5_k, q0=args.c5_q0)
     t0 = time.perf_counter()
-    for s_ in range(S):
-        idx = rank * S + s_
-        o = oracle.Oracle("own", private=True)
-        o.init([1, 2], A, S * world, idx)
-        tr = synth.config5_stream(lambda ev: synth.split_outputs(o.replay(ev)), n_ranks=A, n_rounds=nr,
-                                  n_servers=S * world, my_idx=idx, seed=args.seed + 17 * idx,
-                                  n_seed_units=4 * A)
-        traces.append(np.ascontiguousarray(tr, dtype=np.int32))
+    d = oracle.gen_config5(n_events=args.c5_events, seed=args.seed + 101 * rank, **kw)
     gen_s = time.perf_counter() - t0
-    n_ev = [sum(a.shape[0] for _, a in replay._runs(tr, 2)) for tr in traces]
-    n_batches = [sum(1 for _ in replay._runs(tr, 2)) for tr in traces]
-    # CPU: the oracle replaying the recorded streams (one core)
-    t0 = time.perf_counter()
-    for s_, tr in enumerate(traces):
-        o = oracle.Oracle("own", private=True)
-        o.init([1, 2], A, S * world, rank * S + s_)
-        expect.append(o.replay(tr))
-    cpu_s = time.perf_counter() - t0
-    srvs = [Server([1, 2], A, S * world, rank * S + s_, max_units=1 << 16, device=local) for s_ in range(S)]
-    # warm-up: a short stream on a throwaway handle (kernels loaded, buffers sized)
-    with Server([1, 2], A, S * world, rank * S, max_units=1 << 16, device=local) as tmp:
-        replay.replay(tmp, traces[0][: replay.event_prefix(traces[0], 2, 20000)])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    # every shard's stream at once: one host thread and HIP stream per shard (adlb_replay.cpp)
-    got, _calls = replay.replay_many(srvs, traces)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    same = all(np.array_equal(g, e) for g, e in zip(got, expect))
-    total = sum(n_ev)
-    for srv in srvs:
-        srv.close()
-    threads = {"value": total / el if same else None, "seconds": el, "parity": bool(same)}
-    # one process per server (ADLB runs each server as its own MPI process): the
-    # same streams, every server process on this GPU, started together at a barrier
-    procs = None
-    if world == 1 and args.c5_procs:
-        procs = c5_server_processes(traces, expect, A, S, local)
+    warm = oracle.gen_config5(n_events=min(args.c5_events, 100_000), seed=args.seed + 7 + 101 * rank, **kw)
+
+    def run(dd):
+        srvs = [Server(dd["user_types"], A, S, s_, max_units=1 << 16, device=local) for s_ in range(S)]
+        try:
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            w0 = time.perf_counter()
+            got, steals, sec, calls = replay.replay_rounds(srvs, dd["traces"], k=args.c5_k, rqcap=A)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            return got, steals, sec, calls, time.perf_counter() - w0
+        finally:
+            for s_ in srvs:
+                s_.close()
+
+    run(warm)  # kernels loaded, pools sized
+    got, steals, sec, calls, wall = run(d)
+    same = all(np.array_equal(g, e) for g, e in zip(got, d["outputs"]))
+    st_key = lambda a: np.sort(np.ascontiguousarray(a).view([("", a.dtype)] * 15), axis=0)
+    same_steals = steals.shape == d["steals"].shape and np.array_equal(st_key(steals), st_key(d["steals"]))
+    ok = bool(same and same_steals)
+    total = int(d["events"])
+    el = sec
     if world > 1:
         el, total = shards.reduce_step_timing(el, total)
-        same = all_ranks_true(same)
-    use_procs = False  # measured slower than the threaded replay (r03: 1.5e6 vs 2.2e6 events/s): reported beside it
-    value = procs["value"] if use_procs else (total / el if same else None)
-    mode = (f"one server process per shard ({S} processes on this GPU, each its own HIP stream)" if use_procs
-            else "the shards' streams replayed concurrently, one host thread and HIP stream each")
-    return {"workload": f"config5: {S * world} server shards x a tsp-style stream ({A} ranks, {nr} rounds each: "
-                        f"{sum(n_ev)} events on this GPU in {sum(n_batches)} calls; {mode})",
-            "value": value, "unit": "events/s", "seconds": procs["seconds"] if use_procs else el, "events": total,
-            "events_per_call": round(sum(n_ev) / max(sum(n_batches), 1), 1),
-            "parity": bool(same), "parity_with_oracle": bool(same),
-            "threads": threads, "processes": procs,
-            "cpu_oracle_events_per_s": sum(n_ev) / cpu_s, "cpu_cores": 1,
-            "trace_generation_s": round(gen_s, 1), "scaling": "weak"}
-
-
-def c5_server_processes(traces, expect, A, S, device):
-    """Config 5 with every server shard in its own process (adlb_amd.replay.server_process):
-    events/s from the first start to the last end over all of them, outputs checked
-    against the oracle's."""
-    import multiprocessing as mp
-    import shutil
-    import tempfile
-    from adlb_amd import replay
-    d = tempfile.mkdtemp(prefix="c5procs_", dir="/tmp")
-    try:
-        paths = []
-        for i, tr in enumerate(traces):
-            paths.append((os.path.join(d, f"tr{i}.npy"), os.path.join(d, f"out{i}.npy")))
-            np.save(paths[-1][0], tr)
-        ctx = mp.get_context("spawn")  # this process holds the GPU: no fork
-        barrier, q = ctx.Barrier(len(traces)), ctx.Queue()
-        ps = [ctx.Process(target=replay.server_process,
-                          args=(paths[i][0], paths[i][1], [1, 2], A, S, i, device, barrier, q))
-              for i in range(len(traces))]
-        for p in ps:
-            p.start()
-        res = []
-        for _ in ps:
-            res.append(q.get(timeout=400))
-        for p in ps:
-            p.join(timeout=60)
-        errs = [r[4] for r in res if r[4]]
-        if errs:
-            return {"error": errs[0], "parity": False}
-        res.sort()
-        t0, t1 = min(r[1] for r in res), max(r[2] for r in res)
-        same = all(np.array_equal(np.load(paths[r[0]][1]), expect[r[0]]) for r in res)
-        total = sum(int(sum(a.shape[0] for _, a in replay._runs(tr, 2))) for tr in traces)
-        return {"value": total / (t1 - t0) if same else None, "seconds": t1 - t0, "parity": bool(same),
-                "calls": sum(r[3] for r in res), "per_process_s": [round(r[2] - r[1], 4) for r in res]}
-    finally:
-        shutil.rmtree(d, ignore_errors=True)
+        ok = all_ranks_true(ok)
+    return {"workload": f"config5: {S} server shards x tsp-style streams ({A} app ranks, {int(d['events'])} events, "
+                        f"a qmstat exchange + steal round every {args.c5_round_every} events: {int(d['rounds'])} rounds, "
+                        f"{d['steals'].shape[0]} steals, {int(d['stopped'])} stopped at export depth {args.c5_k}) "
+                        f"per GPU; one host thread + HIP stream per shard, no host sync per call",
+            "value": total / el if ok else None, "unit": "events/s", "seconds": el,
+            "wall_incl_staging_s": round(wall, 4), "events": total, "calls": int(sum(calls)),
+            "events_per_call": round(int(d["events"]) / max(int(sum(calls)), 1), 2),
+            "host_seconds": replay.last_rounds_prof(),
+            "parity": ok, "parity_outputs": bool(same), "parity_steals": bool(same_steals),
+            "cpu_oracle_events_per_s": int(d["events"]) / gen_s, "cpu_cores": 1,
+            "cpu_note": "the oracle (oracle/be_own.c) serving all shards' streams and steal rounds on one core, "
+                        "with the stream generator in the loop (gen_c5.c)",
+            "scaling": "weak"}
 
 
 def bench_wide(args, torch, dev):
@@ -1085,6 +1039,17 @@ def main():
         phases = {f"phase{k}": (srv.stat(f"chain_phase{k}"), srv.stat(f"chain_phase{k}_max")) for k in range(1, 8)}
         phases["clock_mhz_pass1"] = srv.stat("chain_phase2_mhz")
         srv.set_param("chain_stamps", 0)
+    if args.kernel_stamps:
+        # diagnostic: per-workgroup phase stamps of pass 1 (hist) and pass 2 (select) of one batch
+        srv.set_param("kernel_stamps", 1)
+        step(1)
+        torch.cuda.synchronize()
+        phases = dict(phases or {})
+        for w in ("hist", "sel"):
+            phases[w] = {k: srv.stat(f"kst_{w}_{k}") / 1000.0 for k in ("1", "2", "3", "start", "span")}
+            phases[w]["startp"] = [srv.stat(f"kst_{w}_startp{q}") / 1000.0 for q in (10, 25, 50, 75, 90, 99)]
+            phases[w]["endp"] = [srv.stat(f"kst_{w}_endp{q}") / 1000.0 for q in (10, 25, 50, 75, 90, 99)]
+        srv.set_param("kernel_stamps", 0)
     live = srv.last_scan_units()
     # algorithmic bytes per launch: SURVEY §8(d)'s 16 B per live
     # unit for the open-bucket scan (hist + select together), 20 B per Reserve

@@ -14,6 +14,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 k = {s: v["ms"] for s, v in d["kernels_ms"].items()}
 print(f"{sys.argv[2]:12s} ms/step {d['ms_per_step']:.4f} parity {d['parity']} kernels {k}")
+if d.get("chain_phases_ns"): print("   stamps", {w: d["chain_phases_ns"][w] for w in ("hist", "sel") if w in d["chain_phases_ns"]})
 PY
 done
 done
