@@ -313,6 +313,15 @@ struct adlbq_server {
     long long chain_modes = -1;        // bit k-1: round k uses prefix starts, -1 = auto ("chain_modes")
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
+    // dead open pages (no LIVE unit; full, never the tail): found by k_page_dead in the background
+    // (flags in mapped host memory, applied once its event has passed), then reused by Puts
+    std::vector<int> free_pages;
+    int *h_pdead = nullptr; long long cap_pdead = 0; int pdead_np = 0; bool pdead_pending = false;
+    hipEvent_t pdead_ev = nullptr; long long pdead_last = -1000000, pages_recycled = 0;
+    int recycle_pages = 1;             // "recycle_pages": 0 = keep every page (the old behaviour)
+    int small_pages = 4;               // "small_pages": an open bucket of at most this many pages and a batch of
+    int small_r = 1024;                //   at most "small_r" Reserves take the one-workgroup choice (0: never)
+    long long small_batches = 0;       // reserve batches served by it (stat "small_batches")
     // the Reserve path of more than ADLBQ_MAX_TYPES types (adlbq_wide.hip): sort buffers and runs
     unsigned long long *d_wk0 = nullptr, *d_wk1 = nullptr, *d_wekey = nullptr;
     int *d_wv0 = nullptr, *d_wv1 = nullptr, *d_wflag = nullptr, *d_wrstart = nullptr, *d_whead = nullptr;
@@ -390,6 +399,8 @@ int hip_fail(hipError_t e, const char *where);
 
 int ensure_req_capacity(adlbq_server *h, int n);
 int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
+void recycle_apply(adlbq_server *h);       // drop the dead open pages a finished k_page_dead found
+int recycle_launch(adlbq_server *h);       // look for dead open pages in the background (when worth it)
 int ensure_zc(adlbq_server *h, long long n);  // mapped pinned staging of >= n ints (h_zc / d_zc)
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);

@@ -2401,8 +2401,8 @@ __device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, i
             }
     }
     const unsigned long long totu =
-        ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned int)(tot >> 32)) << 32) |
-        __builtin_amdgcn_readfirstlane((unsigned int)tot);
+        ((unsigned long long)(unsigned int)__builtin_amdgcn_readfirstlane((int)(tot >> 32)) << 32) |
+        (unsigned long long)(unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)tot);  // no sign extension
     const int nbad = (int)((totu >> 20) & CNT20), nsolved = (int)(totu >> 40);
     const bool clean = nbad == 0;  // every start equals its predecessor's end
     if (lane == 0) {
@@ -4107,6 +4107,146 @@ static void batch_launched(adlbq_server *h, int R, int export_k, const int *d_re
     h->rq_next_upper += R;
 }
 
+// ---------------------------------------------------------------- small queues: one workgroup
+// An open bucket of at most SMALL_UNITS units and a batch of at most
+// SMALL_R Reserves: the request preparation (unless a targeted phase needs it
+// first), then the whole untargeted choice in one workgroup -- the available
+// units gathered and sorted by (type, prio desc, position asc) in LDS, then
+// the serial dictatorship in request order on one wave (lane t holds type t's
+// list head; a Reserve takes the least head among its types), the same rule
+// as xq.c:190-247 / adlb.c:1199-1317 that the batch pipeline evaluates in
+// parallel.  Writes umatch / cslot for k_finalize (cslot[j] = request j's unit).
+constexpr int SMALL_UNITS = 4 * PAGE, SMALL_R = 1024;  // 140 KB of LDS
+
+struct SmallArgs {
+    PrepArgs pa;
+    int prep;  // 1: prepare the requests here (no targeted phase)
+    const int *pages;
+    int npages, tail_fill;
+    const int *prio;
+    const uint32_t *meta;
+    int T, R;
+    int *umatch, *cslot, *needsort;
+    const int *tmatch;
+    const unsigned long long *mask;
+};
+
+// sort key, ascending = better within a type: type (7 bits), prio descending, position ascending
+__device__ __forceinline__ unsigned long long small_key(int t, int pr, unsigned int pos) {
+    return ((unsigned long long)t << 56) | ((unsigned long long)(~((unsigned int)pr ^ 0x80000000u)) << 24) |
+           (unsigned long long)pos;
+}
+
+template <int TB>
+__global__ __launch_bounds__(256) void k_reserve_small(SmallArgs a) {
+    extern __shared__ unsigned long long skey[];  // [m] keys, then R masks, then R targeted flags
+    __shared__ int s_n, s_start[ADLBQ_MAX_TYPES], s_end[ADLBQ_MAX_TYPES];
+    const int tid = threadIdx.x, lane = tid & 63, T = a.T, R = a.R;
+    if (a.prep) {
+        const int nprep = (R + PREP_BLOCK - 1) / PREP_BLOCK;
+        for (int b = 0; b < nprep; b++) {
+            prep_block<TB>(a.pa, b);
+            __syncthreads();
+        }
+    }
+    if (tid == 0) s_n = 0;
+    if (tid < ADLBQ_MAX_TYPES) s_start[tid] = s_end[tid] = 0;
+    if (tid < T) a.needsort[tid] = 0;  // k_finalize reports needsort_last from it
+    __syncthreads();
+    // the available units, appended in any order (they are sorted next)
+    const int nslots = a.npages > 0 ? (a.npages - 1) * PAGE + a.tail_fill : 0;
+    for (int i0 = 0; i0 < nslots; i0 += 256) {
+        const int i = i0 + tid;
+        unsigned long long k = 0ull;
+        bool av = false;
+        if (i < nslots) {
+            const int p = i >> PAGE_SHIFT, so = i & (PAGE - 1);
+            const long long slot = ((long long)a.pages[p] << PAGE_SHIFT) | so;
+            const uint32_t m = a.meta[slot];
+            const int pr = a.prio[slot];
+            av = (m & (M_LIVE | M_PINNED)) == M_LIVE && pr > LOWEST;
+            k = small_key((int)(m & M_TYPE), pr, (unsigned int)i);
+        }
+        const unsigned long long b = __ballot(av);
+        int base = 0;
+        if (lane == 0 && b) base = atomicAdd(&s_n, __popcll(b));
+        base = __shfl(base, 0, 64);
+        if (av) skey[base + mbcnt64(b)] = k;
+    }
+    __syncthreads();
+    const int n = s_n;
+    int mpow = 1;
+    while (mpow < n) mpow <<= 1;
+    for (int i = n + tid; i < mpow; i += 256) skey[i] = ~0ull;
+    unsigned long long *smask = skey + SMALL_UNITS;
+    int *stm = reinterpret_cast<int *>(smask + SMALL_R);
+    for (int j = tid; j < R; j += 256) {  // written by this launch's prep or earlier kernels: sc1 loads
+        smask[j] = __hip_atomic_load(a.mask + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stm[j] = __hip_atomic_load(a.tmatch + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    // bitonic sort, ascending
+    for (int k = 2; k <= mpow; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = tid; i < mpow; i += 256) {
+                const int x = i ^ jj;
+                if (x > i) {
+                    const unsigned long long u = skey[i], v = skey[x];
+                    const bool up = (i & k) == 0;
+                    if ((u > v) == up) {
+                        skey[i] = v;
+                        skey[x] = u;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // each type's run
+    for (int i = tid; i < n; i += 256) {
+        const int t = (int)(skey[i] >> 56);
+        if (i == 0 || (int)(skey[i - 1] >> 56) != t) s_start[t] = i;
+        if (i == n - 1 || (int)(skey[i + 1] >> 56) != t) s_end[t] = i + 1;
+    }
+    __syncthreads();
+    if (tid >= 64) return;
+    // the serial dictatorship: lane t = type t, its head and the one after (the next head in flight)
+    const bool tl = lane < T;
+    const int e = tl ? s_end[lane] : 0;
+    int h = tl ? s_start[lane] : 0;
+    unsigned long long cur = h < e ? skey[h] : ~0ull, nxt = h + 1 < e ? skey[h + 1] : ~0ull;
+    int tp = 1;
+    while (tp < T) tp <<= 1;
+    for (int j = 0; j < R; j++) {
+        const unsigned long long mk = stm[j] >= 0 ? 0ull : smask[j];
+        // compared across types without the type field: prio descending, position ascending
+        // (an exhausted list's head is ~0: no candidate)
+        const unsigned long long c =
+            (tl && cur != ~0ull && ((mk >> lane) & 1ull)) ? (cur & ((1ull << 56) - 1)) : ~0ull;
+        unsigned long long best = c;
+        for (int o = 1; o < tp; o <<= 1) best = min(best, (unsigned long long)__shfl_xor(best, o, 64));
+        best = ((unsigned long long)(unsigned int)__builtin_amdgcn_readfirstlane((int)(best >> 32)) << 32) |
+               (unsigned long long)(unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)best);  // lane 0's
+        if (best != ~0ull) {
+            const unsigned long long w = __ballot(tl && c == best);
+            if (lane == __ffsll((long long)w) - 1) {
+                h++;
+                cur = nxt;
+                nxt = h + 1 < e ? skey[h + 1] : ~0ull;
+            }
+            if (lane == 0) {
+                const unsigned int pos = (unsigned int)(best & 0xffffffu);
+                const int p = (int)(pos >> PAGE_SHIFT);
+                const bool ok = p < a.npages;  // always (a gathered unit's position); never index past the list
+                a.cslot[j] = ok ? (a.pages[p] << PAGE_SHIFT) | (int)(pos & (PAGE - 1)) : -1;
+                a.umatch[j] = ok ? j : -1;
+            }
+        } else if (lane == 0) {
+            a.umatch[j] = -1;
+        }
+    }
+}
+
 // More than ADLBQ_MAX_TYPES types: the sorted-runs choice (adlbq_wide.hip), then k_finalize.
 static int launch_reserve_wide(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
@@ -4168,7 +4308,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     auto ht = host_t0;
     if ((rc = ensure_req_capacity(h, R))) return rc;
     hsec("req_cap", ht);
+    recycle_apply(h);
     if ((rc = sync_tables(h))) return rc;
+    if ((rc = recycle_launch(h))) return rc;
     hsec("tables", ht);
     if ((rc = ensure_rq_capacity(h, R))) return rc;
     hsec("rq_cap", ht);
@@ -4209,7 +4351,19 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     host_stage_add(h, "pre", host_t0);
     const auto scan_t0 = std::chrono::steady_clock::now();
-    if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) return rc;
+    // a small open bucket and batch: one workgroup chooses (k_reserve_small), no scan
+    const bool small = !h->grec && T > 0 && R <= std::min(h->small_r, SMALL_R) && np <= h->small_pages &&
+                       (long long)np * PAGE <= SMALL_UNITS;
+    if (small) {
+        if (targeted) {  // the targeted phase reads the prepared requests first
+            const int nprep = (R + PREP_BLOCK - 1) / PREP_BLOCK;
+            HistArgs none{};
+            auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
+            kph<<<nprep, 256, 0, s>>>(pa, nprep, none);
+        }
+    } else if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) {
+        return rc;
+    }
     host_stage_add(h, "scan", scan_t0);
     auto hl = hclk::now();
     h->hacc["l_scan"] += std::chrono::duration_cast<std::chrono::nanoseconds>(hl - scan_t0).count();
@@ -4242,6 +4396,27 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
                                           h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);
         stage_end(h, "targeted", ev);
+    }
+    if (small) {
+        const SmallArgs sa{pa, targeted ? 0 : 1, h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, R,
+                           h->d_umatch, h->d_cslot, h->d_needsort, h->d_tmatch, h->d_mask};
+        const size_t lds = sizeof(unsigned long long) * (SMALL_UNITS + SMALL_R) + sizeof(int) * SMALL_R;
+        stage_begin(h, "small", &ev);
+        if (T <= 4) k_reserve_small<4><<<1, 256, lds, s>>>(sa);
+        else if (T <= 8) k_reserve_small<8><<<1, 256, lds, s>>>(sa);
+        else k_reserve_small<64><<<1, 256, lds, s>>>(sa);
+        stage_end(h, "small", ev);
+        h->small_batches++;
+        DevCounters *const snap = h->d_snap + h->snap_next;
+        h->snap_tag[h->snap_next] = ++h->snap_tags;
+        __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);
+        const FinArgs fa = fin_args(h, R, d_reqs, d_resp, snap);
+        stage_begin(h, "finalize", &ev);
+        k_finalize<<<(R + 255) / 256, 256, 0, s>>>(fa);
+        stage_end(h, "finalize", ev);
+        AQ_HIP(hipGetLastError());
+        batch_launched(h, R, 0, d_reqs);  // no candidate lists for a steal export to reuse
+        return ADLBQ_OK;
     }
     auto st0 = hclk::now();
     // 8 < T <= 64: every list sorted and ranked by one binning of the keys (k_rank's tile work skipped)

@@ -343,6 +343,76 @@ static int upload(T **dptr, int *cap, const std::vector<T> &v, hipStream_t s) {
     return ADLBQ_OK;
 }
 
+// ---------------------------------------------------------------- dead open pages
+// Pages are append-only: a long-running server's open bucket keeps every page a
+// Put ever filled, and each scan and table upload pays for the dead ones.  A
+// full page (never the tail) with no LIVE unit stays dead -- units become LIVE
+// only by a Put into the tail page -- so it can leave the bucket (the others
+// keep their relative order, which is the bucket order) and be reused by
+// later Puts.  k_page_dead flags them, one workgroup per page, into mapped
+// host memory; the flags are applied by a later reserve call once the kernel's
+// event has passed, never waited for.
+__global__ __launch_bounds__(256) void k_page_dead(const int *__restrict__ pages, int n,
+                                                   const uint32_t *__restrict__ meta, int *flags) {
+    __shared__ int live;
+    const int p = blockIdx.x;
+    if (threadIdx.x == 0) live = 0;
+    __syncthreads();
+    const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + ((long long)pages[p] << PAGE_SHIFT));
+    uint32_t o = 0u;
+    for (int i = threadIdx.x; i < PAGE / 4; i += 256) {
+        const uint4 v = M4[i];
+        o |= v.x | v.y | v.z | v.w;
+    }
+    if (o & M_LIVE) live = 1;  // every writer stores 1
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + p, live ? 0 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void recycle_apply(adlbq_server *h) {
+    if (!h->pdead_pending || hipEventQuery(h->pdead_ev) != hipSuccess) return;
+    h->pdead_pending = false;
+    std::vector<int> &op = h->open.pages;
+    const int n = std::min<int>(h->pdead_np, (int)op.size() - 1);  // pages that were full when flagged
+    int w = 0, dropped = 0;
+    for (int i = 0; i < (int)op.size(); i++) {
+        if (i < n && __atomic_load_n(h->h_pdead + i, __ATOMIC_ACQUIRE) == 1) {
+            h->free_pages.push_back(op[(size_t)i]);
+            dropped++;
+            continue;
+        }
+        op[(size_t)w++] = op[(size_t)i];
+    }
+    op.resize((size_t)w);
+    if (dropped) {
+        h->tables_dirty = true;
+        h->batch_export_k = 0;  // the last batch's candidate lists hold bucket positions of the old list
+        h->pages_recycled += dropped;
+    }
+}
+
+int recycle_launch(adlbq_server *h) {
+    const int np = (int)h->open.pages.size();
+    if (!h->recycle_pages || h->pdead_pending || np < 4 || h->reserve_batches - h->pdead_last < 16) return ADLBQ_OK;
+    const long long live_open = h->live_units - h->live_targeted;  // an upper bound (Gets land later)
+    if (live_open * 2 >= (long long)(np - 1) * PAGE) return ADLBQ_OK;  // mostly live: nothing to drop
+    if (np - 1 > h->cap_pdead) {
+        if (h->h_pdead) AQ_HIP(hipHostFree(h->h_pdead));
+        h->cap_pdead = std::max<long long>(np, 2 * h->cap_pdead);
+        AQ_HIP(hipHostMalloc((void **)&h->h_pdead, sizeof(int) * h->cap_pdead, hipHostMallocDefault));
+    }
+    if (!h->pdead_ev) AQ_HIP(hipEventCreateWithFlags(&h->pdead_ev, hipEventDisableTiming));
+    int *dflags = nullptr;
+    AQ_HIP(hipHostGetDevicePointer((void **)&dflags, h->h_pdead, 0));
+    k_page_dead<<<np - 1, 256, 0, h->stream>>>(h->d_open_pages, np - 1, h->d_meta, dflags);
+    AQ_HIP(hipGetLastError());
+    AQ_HIP(hipEventRecord(h->pdead_ev, h->stream));
+    h->pdead_pending = true;
+    h->pdead_np = np - 1;
+    h->pdead_last = h->reserve_batches;
+    return ADLBQ_OK;
+}
+
 int sync_tables(adlbq_server *h) {
     if (h->tables_dirty || h->pinfo_dirty) {
         // every page table in one pinned staging buffer and one copy: the open pages,
@@ -1445,6 +1515,8 @@ int adlbq_destroy(adlbq_server *h) {
     if (h->h_steal) hipHostFree(h->h_steal);
     if (h->h_apply) hipHostFree(h->h_apply);
     if (h->h_crem) hipHostFree(h->h_crem);
+    if (h->h_pdead) hipHostFree(h->h_pdead);
+    if (h->pdead_ev) hipEventDestroy(h->pdead_ev);
     for (int q = 0; q < 2; q++)
         if (h->h_putrec[q]) hipHostFree(h->h_putrec[q]);
     if (h->d_tnewk) hipFree(h->d_tnewk);
@@ -1554,12 +1626,21 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
             b = &h->rankb[bk];
         }
         if (b->pages.empty() || b->tail_fill == PAGE) {
-            if (h->n_pages == h->cap_pages && (rc = grow_pages(h, h->n_pages + 1))) return rc;
-            b->pages.push_back(h->n_pages++);
-            b->tail_fill = 0;
             // the page's packed-offset base: its first prio less half the range
-            h->page_base.push_back((int)std::max((long long)u[1] - M_OFF_RANGE / 2, (long long)INT_MIN));
-            h->page_wide.push_back(0);
+            const int pbase = (int)std::max((long long)u[1] - M_OFF_RANGE / 2, (long long)INT_MIN);
+            if (!h->free_pages.empty()) {  // a recycled dead page (every slot is written before it is read)
+                const int pg = h->free_pages.back();
+                h->free_pages.pop_back();
+                b->pages.push_back(pg);
+                h->page_base[(size_t)pg] = pbase;
+                h->page_wide[(size_t)pg] = 0;
+            } else {
+                if (h->n_pages == h->cap_pages && (rc = grow_pages(h, h->n_pages + 1))) return rc;
+                b->pages.push_back(h->n_pages++);
+                h->page_base.push_back(pbase);
+                h->page_wide.push_back(0);
+            }
+            b->tail_fill = 0;
             h->pinfo_dirty = true;
         }
         h->tables_dirty = true;
@@ -2384,6 +2465,20 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->group_launch = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "recycle_pages") {
+        h->recycle_pages = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
+    if (n == "small_pages") {  // the one-workgroup choice: largest open bucket (pages), 0 = off
+        if (value < 0 || value > 4) return fail(ADLBQ_ERR_ARG, "small_pages must be in [0, 4]");
+        h->small_pages = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "small_r") {  // ... and largest batch
+        if (value < 0 || value > 1024) return fail(ADLBQ_ERR_ARG, "small_r must be in [0, 1024]");
+        h->small_r = (int)value;
+        return ADLBQ_OK;
+    }
     if (n == "rank_grid") {  // test: k_rank's grid (0: sized by the rank hint)
         if (value < 0 || value > 4096) return fail(ADLBQ_ERR_ARG, "rank_grid must be in [0, 4096]");
         h->rank_grid = (int)value;
@@ -2430,6 +2525,10 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         std::sort(d.begin(), d.end());
         return d[d.size() / 2];
     }
+    if (n == "small_batches") return h->small_batches;
+    if (n == "pages_recycled") return h->pages_recycled;
+    if (n == "open_pages") return (long long)h->open.pages.size();
+    if (n == "pages_total") return h->n_pages;
     if (n == "chain_rounds") return h->ctr.chain_rounds;
     if (n == "chain_passes") return h->ctr.chain_passes;
     if (n == "chain_recomputed") return h->ctr.chain_recomputed;

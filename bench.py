@@ -578,6 +578,7 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
     d = oracle.gen_config5(n_events=args.c5_events, seed=args.seed + 101 * rank, **kw)
     gen_s = time.perf_counter() - t0
     warm = oracle.gen_config5(n_events=min(args.c5_events, 100_000), seed=args.seed + 7 + 101 * rank, **kw)
+    c5_stats = {}
 
     def run(dd):
         srvs = [Server(dd["user_types"], A, S, s_, max_units=1 << 16, device=local) for s_ in range(S)]
@@ -590,7 +591,13 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
-            return got, steals, sec, calls, time.perf_counter() - w0
+            wall_s = time.perf_counter() - w0
+            # reserve batches served by the one-workgroup choice, and the host sections of the reserve call (ms)
+            c5_stats.clear()
+            c5_stats["small_batches"] = sum(s_.stat("small_batches") for s_ in srvs)
+            for sec_name in ("total", "tindex", "l_scan", "l_rank", "l_chain", "l_fin", "tables", "sort"):
+                c5_stats["host_ms_" + sec_name] = round(sum(s_.stat("hacc:" + sec_name) for s_ in srvs) / 1e6, 1)
+            return got, steals, sec, calls, wall_s
         finally:
             for s_ in srvs:
                 s_.close()
@@ -614,6 +621,7 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
             "wall_incl_staging_s": round(wall, 4), "events": total, "calls": int(sum(calls)),
             "events_per_call": round(int(d["events"]) / max(int(sum(calls)), 1), 2),
             "host_seconds": replay.last_rounds_prof(),
+            "engine": dict(c5_stats),
             "parity": ok, "parity_outputs": bool(same), "parity_steals": bool(same_steals),
             "cpu_oracle_events_per_s": int(d["events"]) / gen_s, "cpu_cores": 1,
             "cpu_note": "the oracle (oracle/be_own.c) serving all shards' streams and steal rounds on one core, "

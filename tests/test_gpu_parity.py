@@ -61,10 +61,92 @@ def assert_same(got, exp):
     assert bad.size == 0, f"first mismatch at output int {bad[0]}: got {got[bad[0]]} expected {exp[bad[0]]}"
 
 
+# small open buckets and batches take the one-workgroup choice by default
+# (k_reserve_small); "pipeline" turns it off so that the batch pipeline is
+# checked on the same small cases
+ENGINES = {"default": {}, "pipeline": {"small_pages": 0}}
+
+
+@pytest.mark.parametrize("engine", sorted(ENGINES))
 @pytest.mark.parametrize("path", GOLD, ids=[os.path.basename(p)[:-4] for p in GOLD])
-def test_golden(gpu_available, path):
+def test_golden(gpu_available, path, engine):
     d = np.load(path, allow_pickle=False)
-    assert_same(run_abi(d["user_types"], d["cfg"], d["trace"]), d["expected"])
+    assert_same(run_abi(d["user_types"], d["cfg"], d["trace"], params=ENGINES[engine]), d["expected"])
+
+
+SMALL = {
+    "s_c2_t4": lambda: synth.config2(n_units=16_000, n_reserves=1024, seed=601),
+    "s_c2_t1_eq": lambda: synth.config2(n_units=3_000, n_types=1, n_reserves=1000, seed=602, equal_prio=True),
+    "s_c2_exhaust": lambda: synth.config2(n_units=500, n_reserves=1000, seed=603, prio_hi=8),
+    "s_c2_exhaust_nohang": lambda: synth.config2(n_units=500, n_reserves=1000, seed=604, hang=0),
+    "s_c2_t8_extreme": lambda: synth.config2(n_units=8_000, n_types=8, n_reserves=1024, seed=605, wide_frac=0.1,
+                                             wide_range=(-(1 << 31), (1 << 31) - 1)),
+    "s_c2_t64": lambda: synth.config2(n_units=5_000, n_types=64, n_reserves=1024, seed=606, prio_hi=64),
+    "s_c4_targeted": lambda: synth.config4(n_units=6_000, n_reserves=1024, n_ranks=64, seed=607, prio_hi=16),
+    "s_c4_t8_tied": lambda: synth.config4(n_units=4_000, n_types=8, n_reserves=1024, n_ranks=32, seed=608, prio_hi=4),
+    "s_r1": lambda: synth.config2(n_units=500, n_reserves=1, seed=609),
+}
+
+
+@pytest.mark.parametrize("engine", sorted(ENGINES))
+@pytest.mark.parametrize("name", sorted(SMALL))
+def test_small_queue_vs_oracle(gpu_available, name, engine):
+    """Small open buckets (at most four pages) and batches (at most 1024): the
+    one-workgroup choice and the batch pipeline both give the oracle's result."""
+    w = SMALL[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    with Server(w.user_types, *cfg, max_units=w.n_units) as s:
+        for k, v in ENGINES[engine].items():
+            s.set_param(k, v)
+        got = replay.replay(s, tr)
+        used = s.stat("small_batches")
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
+    assert (used > 0) == (engine == "default"), used
+
+
+@pytest.mark.parametrize("recycle", [1, 0])
+def test_dead_pages_recycled_vs_oracle(gpu_available, recycle):
+    """A long stream on a small queue: rounds of Puts, Reserve batches and Gets
+    of every match leave whole pages dead; they leave the open bucket in the
+    background (k_page_dead) and later Puts reuse them.  The results equal the
+    oracle's with and without recycling, and the bucket stays small."""
+    rng = np.random.default_rng(71)
+    ut, A = [3, 5, 7], 256
+    o = oracle.Oracle("own")
+    o.init(ut, A, 1, 0)
+    trace, exp = [], []
+
+    def step(ev):
+        ev = np.asarray(ev, dtype=np.int32).ravel()
+        out = o.replay(ev)
+        trace.append(ev)
+        exp.append(out)
+        return synth.split_outputs(out)
+
+    for rnd in range(40):
+        puts = [[synth.OP_PUT, int(rng.choice(ut)), int(rng.integers(0, 50)), 0, -1, 8, -1, 0, -1, -1]
+                for _ in range(3000)]
+        step(puts)
+        for b in range(3):  # nearly every unit is taken and got: the round's pages die
+            R = 1000
+            ranks = rng.integers(0, A, size=R)
+            types = np.full((R, 16), -2, np.int32)
+            types[:, 0] = rng.choice(ut + [-1, -1, -1], size=R)
+            outs = step(synth.reserve_events(ranks, types, np.zeros(R, np.int32)))
+            gets = [[synth.OP_GET, int(r), int(x[5])] for r, x in zip(ranks, outs) if x[0] == 1]
+            if gets:
+                step(gets)
+    st = {}
+    with Server(ut, A, 1, 0, max_units=1 << 17) as s:
+        s.set_param("recycle_pages", recycle)
+        got = replay.replay(s, np.concatenate(trace))
+        st = {k: s.stat(k) for k in ("pages_recycled", "open_pages", "pages_total")}
+    assert_same(got, np.concatenate(exp))
+    if recycle:
+        assert st["pages_recycled"] > 0 and st["pages_total"] <= 12, st
+    else:
+        assert st["pages_recycled"] == 0, st
 
 
 CASES = {
