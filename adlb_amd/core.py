@@ -61,6 +61,8 @@ SIGNATURES = {
     "adlbsrv_group_blob_ints": (ctypes.c_longlong, [P]),
     "adlbsrv_group_export": (c_int, [P, P]),
     "adlbsrv_group_settle": (c_int, [P, P, c_int, P]),
+    "adlbsrv_group_export_device": (c_int, [P, P]),
+    "adlbsrv_group_settle_device": (c_int, [P, P, c_int, P]),
     "adlbsrv_group_stat": (ctypes.c_longlong, [P, c_int]),
     "adlbsrv_replay_many": (c_int, [P, c_int, c_int, P, P, P, P, P, P]),
     "adlbsrv_replay_prof": (None, [P]),

@@ -756,13 +756,33 @@ int adlbsrv_group_export(adlbsrv *s, int *blob) {
     return s->rc(adlbq_steal_group_export_host(s->grp, blob), "adlbq_steal_group_export_host");
 }
 
+int adlbsrv_group_export_device(adlbsrv *s, int *d_blob) {
+    if (!s->grp) return fail("adlbsrv_group_export_device: no steal group");
+    return s->rc(adlbq_steal_group_export(s->grp, d_blob), "adlbq_steal_group_export");
+}
+
+static int group_settle_common(adlbsrv *s, int *settled);
+
 int adlbsrv_group_settle(adlbsrv *s, const int *all, int nproc, int *settled) {
     // the round's SS_RFR_RESP successes (adlb.c:1877-1948) for this server's
     // parked Reserves, and its donor side (1807-1827) for the others'
     if (!s->grp) return fail("adlbsrv_group_settle: no steal group");
-    int nd = 0, won = 0, cnt = 0;
+    int nd = 0, won = 0;
     if (s->rc(adlbq_steal_group_settle_host(s->grp, all, nproc, &nd, &won), "adlbq_steal_group_settle_host"))
         return -1;
+    return group_settle_common(s, settled);
+}
+
+int adlbsrv_group_settle_device(adlbsrv *s, const int *d_all, int nproc, int *settled) {
+    // the blobs all-gathered in device memory (RCCL): the engine copies them to pinned memory once
+    if (!s->grp) return fail("adlbsrv_group_settle_device: no steal group");
+    int nd = 0, won = 0;
+    if (s->rc(adlbq_steal_group_settle(s->grp, d_all, nproc, &nd, &won), "adlbq_steal_group_settle")) return -1;
+    return group_settle_common(s, settled);
+}
+
+static int group_settle_common(adlbsrv *s, int *settled) {
+    int cnt = 0;
     if (s->rc(adlbq_steal_group_responses(s->grp, 0, nullptr, &cnt), "adlbq_steal_group_responses")) return -1;
     s->grp_rows.resize(15 * (size_t)cnt);
     if (cnt && s->rc(adlbq_steal_group_responses(s->grp, cnt, s->grp_rows.data(), &cnt), "adlbq_steal_group_responses"))

@@ -107,6 +107,10 @@ int adlbsrv_group_create(adlbsrv *s, int k, int rqcap);
 long long adlbsrv_group_blob_ints(adlbsrv *s);
 int adlbsrv_group_export(adlbsrv *s, int *blob);
 int adlbsrv_group_settle(adlbsrv *s, const int *all, int nproc, int *settled);
+/* the same with the blobs in device memory (d_blob: _blob_ints ints; d_all: [nproc][blob],
+ * all-gathered by RCCL between the server processes) */
+int adlbsrv_group_export_device(adlbsrv *s, int *d_blob);
+int adlbsrv_group_settle_device(adlbsrv *s, const int *d_all, int nproc, int *settled);
 long long adlbsrv_group_stat(adlbsrv *s, int which);
 
 /* A native server-loop driver for recorded event streams (adlb_replay.cpp):

@@ -25,7 +25,14 @@
 // the units it donates.  A server takes no other message between its export
 // and its settle, so the merge sees every queue as it is applied.
 // ADLB_STEAL_GROUP=0 keeps the reference's SS_RFR protocol.
+// ADLB_STEAL_RCCL=1: the blobs stay in device memory and are all-gathered by
+// RCCL (one server per GPU; the ncclUniqueId goes out by MPI_Bcast among the
+// servers); if any server cannot join the communicator, every server keeps
+// the host all-gather.
 #include <mpi.h>
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -99,6 +106,56 @@ struct Loop {
     std::vector<int> blob, blobs;
 };
 Loop *g_loop = nullptr;
+
+// the steal round's device all-gather (ADLB_STEAL_RCCL)
+struct Rccl {
+    ncclComm_t comm = nullptr;
+    int *d_blob = nullptr, *d_all = nullptr;
+    hipStream_t st = nullptr;
+} g_rccl;
+
+// collective over the servers: true when every server joined the communicator
+bool rccl_init(size_t blob_ints) {
+    int me = 0, ok = 1;
+    MPI_Comm_rank(g_srvcomm, &me);
+    ncclUniqueId id;
+    memset(&id, 0, sizeof id);
+    if (me == 0 && ncclGetUniqueId(&id) != ncclSuccess) ok = 0;
+    MPI_Bcast(&id, (int)sizeof id, MPI_BYTE, 0, g_srvcomm);
+    int all = 0;
+    MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, g_srvcomm);
+    if (!all) return false;
+    int dev = 0;
+    ok = hipGetDevice(&dev) == hipSuccess && hipStreamCreate(&g_rccl.st) == hipSuccess &&
+         hipMalloc((void **)&g_rccl.d_blob, sizeof(int) * blob_ints) == hipSuccess &&
+         hipMalloc((void **)&g_rccl.d_all, sizeof(int) * blob_ints * (size_t)g_S) == hipSuccess;
+    // every server calls the collective init (a failed allocation joins and leaves after)
+    if (ncclCommInitRank(&g_rccl.comm, g_S, id, me) != ncclSuccess) {
+        g_rccl.comm = nullptr;
+        ok = 0;
+    }
+    MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, g_srvcomm);
+    if (!all) {
+        if (g_rccl.comm) ncclCommDestroy(g_rccl.comm);
+        g_rccl.comm = nullptr;
+        if (g_rccl.d_blob) (void)hipFree(g_rccl.d_blob);
+        if (g_rccl.d_all) (void)hipFree(g_rccl.d_all);
+        if (g_rccl.st) (void)hipStreamDestroy(g_rccl.st);
+        g_rccl = Rccl{};
+        if (me == 0) fprintf(stderr, "%06d: ADLB_STEAL_RCCL: RCCL unavailable, host all-gather kept\n", g_rank);
+        return false;
+    }
+    return true;
+}
+
+void rccl_fini() {
+    if (!g_rccl.comm) return;
+    ncclCommDestroy(g_rccl.comm);
+    (void)hipFree(g_rccl.d_blob);
+    (void)hipFree(g_rccl.d_all);
+    (void)hipStreamDestroy(g_rccl.st);
+    g_rccl = Rccl{};
+}
 
 bool is_server_rank(int r) { return r >= g_master && r < g_master + g_S; }
 
@@ -199,6 +256,17 @@ void exh_poll(Loop *L) {
 
 // one steal round: export, all-gather among the servers, settle (no other message in between)
 void steal_round(Loop *L) {
+    if (g_rccl.comm) {  // device blobs, RCCL all-gather
+        const size_t n = L->blob.size();
+        check(adlbsrv_group_export_device(g_srv, g_rccl.d_blob), "steal round export (device)");
+        if (hipDeviceSynchronize() != hipSuccess ||
+            ncclAllGather(g_rccl.d_blob, g_rccl.d_all, n, ncclInt32, g_rccl.comm, g_rccl.st) != ncclSuccess ||
+            hipStreamSynchronize(g_rccl.st) != hipSuccess)
+            die("steal round: RCCL all-gather failed");
+        int settled = 0;
+        check(adlbsrv_group_settle_device(g_srv, g_rccl.d_all, g_S, &settled), "steal round settle (device)");
+        return;
+    }
     check(adlbsrv_group_export(g_srv, L->blob.data()), "steal round export");
     const int n = (int)L->blob.size();
     MPI_Allgather(L->blob.data(), n, MPI_INT, L->blobs.data(), n, MPI_INT, g_srvcomm);
@@ -582,6 +650,10 @@ int ADLBP_Server(double hi_malloc, double periodic_logging_time) {
         // types keeps the reference's SS_RFR steals (adlb.c:1280-1308), whatever was asked for.
         // Every server declared the same types (ADLB_Init), so this agrees on all of them.
         if (T > ADLBQ_MAX_TYPES) want = 0;
+    } else {
+        // one server: a steal group only when asked for (the round path exercised, nothing to steal)
+        const char *sg = getenv("ADLB_STEAL_GROUP");
+        want = sg && *sg && atoi(sg) != 0 && T <= ADLBQ_MAX_TYPES;
     }
     int all_want = 0;
     MPI_Allreduce(&want, &all_want, 1, MPI_INT, MPI_MIN, g_srvcomm);
@@ -591,6 +663,8 @@ int ADLBP_Server(double hi_malloc, double periodic_logging_time) {
         L.group = true;
         L.blob.assign((size_t)adlbsrv_group_blob_ints(g_srv), 0);
         L.blobs.assign(L.blob.size() * (size_t)g_S, 0);
+        if (env_d("ADLB_STEAL_RCCL", 0.0) != 0.0 && rccl_init(L.blob.size()) && getenv("ADLB_STEAL_REPORT"))
+            fprintf(stderr, "%06d: RCCL all-gather of the steal blobs on (%d servers)\n", g_rank, g_S);
     }
     g_loop = &L;
     if (L.my_apps == 0 && g_rank != g_master) emit(&L, g_master, TAG_SRV_DONE, nullptr, 0);
@@ -599,6 +673,7 @@ int ADLBP_Server(double hi_malloc, double periodic_logging_time) {
     if (L.group && getenv("ADLB_STEAL_REPORT"))
         fprintf(stderr, "%06d: steal group: %lld rounds, %lld Reserves settled by the merge, %lld SS_RFR sent\n", g_rank,
                 adlbsrv_group_stat(g_srv, 0), adlbsrv_group_stat(g_srv, 1), adlbsrv_group_stat(g_srv, 2));
+    rccl_fini();
     g_loop = nullptr;
     return ADLB_SUCCESS;
 }

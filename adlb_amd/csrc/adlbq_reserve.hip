@@ -85,7 +85,8 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk) {
     // so every record is 8-B aligned; the wave's loads cover one contiguous 4.6 KB run)
     static_assert(ADLBQ_RESERVE_INTS == 18, "record layout");
     int row[ADLBQ_RESERVE_INTS];
-    if ((int)threadIdx.x < nj) {
+    const bool mine = (int)threadIdx.x < nj;  // (a larger block's threads past PREP_BLOCK idle: nj <= PREP_BLOCK)
+    if (mine) {
         const int2 *src = reinterpret_cast<const int2 *>(reqs + (long long)ADLBQ_RESERVE_INTS * (j0 + threadIdx.x));
 #pragma unroll
         for (int i = 0; i < ADLBQ_RESERVE_INTS / 2; i++) {
@@ -131,7 +132,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk) {
     }
     const int j = j0 + threadIdx.x;
     unsigned long long m = 0;
-    if (threadIdx.x < nj) {
+    if (mine) {
         tmatch[j] = -1;
         if (a.rh != nullptr) a.rh[j] = make_int2(row[0], row[1]);
         const int *rt = row + 2;
@@ -166,7 +167,7 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk) {
         }
     }
     const unsigned long long nz = __ballot(m != 0ull);
-    if ((threadIdx.x & 63) == 0 && j < R) seg_cnt[j >> 6] = __popcll(nz);  // per 64 requests
+    if ((threadIdx.x & 63) == 0 && j < R && (int)threadIdx.x < PREP_BLOCK) seg_cnt[j >> 6] = __popcll(nz);  // per 64 requests
     if constexpr (TB <= 8) {  // per-type demand: one LDS add per wave and type
 #pragma unroll
         for (int t = 0; t < TB; t++) {
@@ -4137,8 +4138,10 @@ __device__ __forceinline__ unsigned long long small_key(int t, int pr, unsigned 
            (unsigned long long)pos;
 }
 
+constexpr int SMALL_THREADS = 1024;
+
 template <int TB>
-__global__ __launch_bounds__(256) void k_reserve_small(SmallArgs a) {
+__global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
     extern __shared__ unsigned long long skey[];  // [m] keys, then R masks, then R targeted flags
     __shared__ int s_n, s_start[ADLBQ_MAX_TYPES], s_end[ADLBQ_MAX_TYPES];
     const int tid = threadIdx.x, lane = tid & 63, T = a.T, R = a.R;
@@ -4153,42 +4156,54 @@ __global__ __launch_bounds__(256) void k_reserve_small(SmallArgs a) {
     if (tid < ADLBQ_MAX_TYPES) s_start[tid] = s_end[tid] = 0;
     if (tid < T) a.needsort[tid] = 0;  // k_finalize reports needsort_last from it
     __syncthreads();
-    // the available units, appended in any order (they are sorted next)
+    // the available units, appended in any order (they are sorted next); every load in flight first
     const int nslots = a.npages > 0 ? (a.npages - 1) * PAGE + a.tail_fill : 0;
-    for (int i0 = 0; i0 < nslots; i0 += 256) {
-        const int i = i0 + tid;
-        unsigned long long k = 0ull;
-        bool av = false;
+    constexpr int GPT = SMALL_UNITS / SMALL_THREADS;
+    uint32_t gm[GPT];
+    int gp[GPT];
+#pragma unroll
+    for (int g = 0; g < GPT; g++) {
+        const int i = g * SMALL_THREADS + tid;
+        gm[g] = 0u;
+        gp[g] = LOWEST;
         if (i < nslots) {
-            const int p = i >> PAGE_SHIFT, so = i & (PAGE - 1);
-            const long long slot = ((long long)a.pages[p] << PAGE_SHIFT) | so;
-            const uint32_t m = a.meta[slot];
-            const int pr = a.prio[slot];
-            av = (m & (M_LIVE | M_PINNED)) == M_LIVE && pr > LOWEST;
-            k = small_key((int)(m & M_TYPE), pr, (unsigned int)i);
+            const long long slot = ((long long)a.pages[i >> PAGE_SHIFT] << PAGE_SHIFT) | (i & (PAGE - 1));
+            gm[g] = a.meta[slot];
+            gp[g] = a.prio[slot];
         }
+    }
+    unsigned long long gk[GPT];  // this thread's units' keys, ~0 when not available
+#pragma unroll
+    for (int g = 0; g < GPT; g++) {
+        const int i = g * SMALL_THREADS + tid;
+        const bool av = (gm[g] & (M_LIVE | M_PINNED)) == M_LIVE && gp[g] > LOWEST;
+        gk[g] = av ? small_key((int)(gm[g] & M_TYPE), gp[g], (unsigned int)i) : ~0ull;
+    }
+    unsigned long long *smask = skey + SMALL_UNITS;
+    int *stm = reinterpret_cast<int *>(smask + SMALL_R);
+    for (int j = tid; j < R; j += SMALL_THREADS) {  // written by this launch's prep or earlier kernels: sc1 loads
+        stm[j] = __hip_atomic_load(a.tmatch + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        smask[j] = __hip_atomic_load(a.mask + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int g = 0; g < GPT; g++) {
+        const bool av = gk[g] != ~0ull;
         const unsigned long long b = __ballot(av);
         int base = 0;
         if (lane == 0 && b) base = atomicAdd(&s_n, __popcll(b));
         base = __shfl(base, 0, 64);
-        if (av) skey[base + mbcnt64(b)] = k;
+        if (av) skey[base + mbcnt64(b)] = gk[g];
     }
     __syncthreads();
     const int n = s_n;
     int mpow = 1;
     while (mpow < n) mpow <<= 1;
-    for (int i = n + tid; i < mpow; i += 256) skey[i] = ~0ull;
-    unsigned long long *smask = skey + SMALL_UNITS;
-    int *stm = reinterpret_cast<int *>(smask + SMALL_R);
-    for (int j = tid; j < R; j += 256) {  // written by this launch's prep or earlier kernels: sc1 loads
-        smask[j] = __hip_atomic_load(a.mask + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        stm[j] = __hip_atomic_load(a.tmatch + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int i = n + tid; i < mpow; i += SMALL_THREADS) skey[i] = ~0ull;
     __syncthreads();
     // bitonic sort, ascending
     for (int k = 2; k <= mpow; k <<= 1) {
         for (int jj = k >> 1; jj > 0; jj >>= 1) {
-            for (int i = tid; i < mpow; i += 256) {
+            for (int i = tid; i < mpow; i += SMALL_THREADS) {
                 const int x = i ^ jj;
                 if (x > i) {
                     const unsigned long long u = skey[i], v = skey[x];
@@ -4203,13 +4218,70 @@ __global__ __launch_bounds__(256) void k_reserve_small(SmallArgs a) {
         }
     }
     // each type's run
-    for (int i = tid; i < n; i += 256) {
+    for (int i = tid; i < n; i += SMALL_THREADS) {
         const int t = (int)(skey[i] >> 56);
         if (i == 0 || (int)(skey[i - 1] >> 56) != t) s_start[t] = i;
         if (i == n - 1 || (int)(skey[i + 1] >> 56) != t) s_end[t] = i + 1;
     }
     __syncthreads();
     if (tid >= 64) return;
+    constexpr unsigned long long KM = (1ull << 56) - 1;  // key without the type field
+    auto uni = [](unsigned long long x) {  // a wave-uniform value into scalar registers
+        return ((unsigned long long)(unsigned int)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+               (unsigned long long)(unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)x);
+    };
+    if constexpr (TB <= 8) {
+        // T <= 8: every type's head, and the two after it (loads in flight), held uniformly: a
+        // Reserve is a few scalar compares, no cross-lane step
+        unsigned long long c0[TB], c1[TB], c2[TB];
+        int hp[TB], he[TB];
+#pragma unroll
+        for (int q = 0; q < TB; q++) {
+            hp[q] = q < T ? s_start[q] : 0;
+            he[q] = q < T ? s_end[q] : 0;
+            c0[q] = hp[q] < he[q] ? uni(skey[hp[q]]) : ~0ull;
+            c1[q] = hp[q] + 1 < he[q] ? uni(skey[hp[q] + 1]) : ~0ull;
+            c2[q] = hp[q] + 2 < he[q] ? uni(skey[hp[q] + 2]) : ~0ull;
+        }
+        unsigned long long mreg = 0ull;  // lane l: request j0 + l's mask (0: matched in the targeted phase)
+        for (int j = 0; j < R; j++) {
+            if ((j & 63) == 0) {
+                const int jl = j + lane;
+                mreg = jl < R && stm[jl] < 0 ? smask[jl] : 0ull;
+            }
+            const unsigned long long mk =
+                ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(mreg >> 32), j & 63) << 32) |
+                (unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)mreg, j & 63);
+            unsigned long long best = ~0ull;
+            int bq = -1;
+#pragma unroll
+            for (int q = 0; q < TB; q++)
+                if (((mk >> q) & 1ull) && c0[q] != ~0ull && (c0[q] & KM) < best) {
+                    best = c0[q] & KM;
+                    bq = q;
+                }
+            if (bq >= 0) {
+#pragma unroll
+                for (int q = 0; q < TB; q++)
+                    if (q == bq) {
+                        hp[q]++;
+                        c0[q] = c1[q];
+                        c1[q] = c2[q];
+                        c2[q] = hp[q] + 2 < he[q] ? uni(skey[hp[q] + 2]) : ~0ull;
+                    }
+                if (lane == 0) {
+                    const unsigned int pos = (unsigned int)(best & 0xffffffu);
+                    const int p = (int)(pos >> PAGE_SHIFT);
+                    const bool ok = p < a.npages;
+                    a.cslot[j] = ok ? (a.pages[p] << PAGE_SHIFT) | (int)(pos & (PAGE - 1)) : -1;
+                    a.umatch[j] = ok ? j : -1;
+                }
+            } else if (lane == 0) {
+                a.umatch[j] = -1;
+            }
+        }
+        return;
+    }
     // the serial dictatorship: lane t = type t, its head and the one after (the next head in flight)
     const bool tl = lane < T;
     const int e = tl ? s_end[lane] : 0;
@@ -4217,8 +4289,15 @@ __global__ __launch_bounds__(256) void k_reserve_small(SmallArgs a) {
     unsigned long long cur = h < e ? skey[h] : ~0ull, nxt = h + 1 < e ? skey[h + 1] : ~0ull;
     int tp = 1;
     while (tp < T) tp <<= 1;
+    unsigned long long mreg = 0ull;  // lane l: request j0 + l's mask (0: matched in the targeted phase)
     for (int j = 0; j < R; j++) {
-        const unsigned long long mk = stm[j] >= 0 ? 0ull : smask[j];
+        if ((j & 63) == 0) {
+            const int jl = j + lane;
+            mreg = jl < R && stm[jl] < 0 ? smask[jl] : 0ull;
+        }
+        const unsigned long long mk =
+            ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(mreg >> 32), j & 63) << 32) |
+            (unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)mreg, j & 63);
         // compared across types without the type field: prio descending, position ascending
         // (an exhausted list's head is ~0: no candidate)
         const unsigned long long c =
@@ -4402,9 +4481,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                            h->d_umatch, h->d_cslot, h->d_needsort, h->d_tmatch, h->d_mask};
         const size_t lds = sizeof(unsigned long long) * (SMALL_UNITS + SMALL_R) + sizeof(int) * SMALL_R;
         stage_begin(h, "small", &ev);
-        if (T <= 4) k_reserve_small<4><<<1, 256, lds, s>>>(sa);
-        else if (T <= 8) k_reserve_small<8><<<1, 256, lds, s>>>(sa);
-        else k_reserve_small<64><<<1, 256, lds, s>>>(sa);
+        if (T <= 4) k_reserve_small<4><<<1, SMALL_THREADS, lds, s>>>(sa);
+        else if (T <= 8) k_reserve_small<8><<<1, SMALL_THREADS, lds, s>>>(sa);
+        else k_reserve_small<64><<<1, SMALL_THREADS, lds, s>>>(sa);
         stage_end(h, "small", ev);
         h->small_batches++;
         DevCounters *const snap = h->d_snap + h->snap_next;

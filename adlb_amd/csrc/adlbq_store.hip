@@ -677,7 +677,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                                                               const int *__restrict__ rq_seq,
                                                               DevCounters *ctr, uint32_t *meta, int *pin, int *out3,
                                                               const int *__restrict__ utypes, int T, int *over) {
-    __shared__ int s_rank[PM_CAP], s_k[PM_CAP];
+    __shared__ int s_rank[PM_CAP], s_k[PM_CAP], s_res[PM_CAP];
+    __shared__ int s_ml, s_rbig;
+    // ranks with a parked entry (ranks below PM_RBITS; s_rbig: a larger one is parked): a targeted Put
+    // whose rank has none skips the scan
+    constexpr int PM_RBITS = 1 << 16;
+    __shared__ unsigned int s_rbits[PM_RBITS / 32];
     __shared__ unsigned long long s_mask[PM_CAP];
     __shared__ int s_wmin[PM_WAVES], s_cnt[PM_WAVES], s_tot;
     __shared__ long long s_wsum[PM_WAVES], s_wpk[PM_WAVES];
@@ -685,7 +690,8 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int head = ctr->rq_head, nrq = ctr->rq_n;
     for (int t = tid; t < T; t += PM_THREADS) s_ut[t] = utypes[t];
-    if (tid == 0) s_tot = 0;
+    for (int q = tid; q < PM_RBITS / 32; q += PM_THREADS) s_rbits[q] = 0u;
+    if (tid == 0) s_tot = 0, s_rbig = 0;
     __syncthreads();
     // stage the live entries in FIFO order (compaction in chunks of 1024)
     for (int c0 = head; c0 < nrq; c0 += PM_THREADS) {
@@ -711,9 +717,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                         break;
                     }
             }
-            s_rank[pos] = rq_rank[k];
+            const int rk = rq_rank[k];
+            s_rank[pos] = rk;
             s_mask[pos] = wild ? ~0ull : m;
             s_k[pos] = k;
+            if (rk >= 0 && rk < PM_RBITS) atomicOr(&s_rbits[rk >> 5], 1u << (rk & 31));
+            else s_rbig = 1;
         }
         __syncthreads();
         if (tid == 0) {
@@ -728,17 +737,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
         if (tid == 0) *over = 1;
         return;
     }
-    // block-wide minimum of v (every thread gets it); two barriers
-    auto block_min = [&](int v) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-        if (lane == 0) s_wmin[w] = v;
+    auto s_mlive_sync = [&](int v, int wv) {  // wave 0's count of live entries, to every thread
+        if (wv == 0 && lane == 0) s_ml = v;
         __syncthreads();
-        int b = INT_MAX;
-#pragma unroll
-        for (int q = 0; q < PM_WAVES; q++) b = min(b, s_wmin[q]);
+        const int x = s_ml;
         __syncthreads();
-        return b;
+        return x;
     };
     int mlive = m, nmatch = 0;
     long long run = 0, peak = LLONG_MIN;  // running byte delta before the chunk; peak over the batch
@@ -754,46 +758,58 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
             if (i < nc) u[q] = r[c0 + i];
             bit[q] = i < nc ? 1ull << (u[q].meta & (int)M_TYPE) : 0ull;
         }
-        if (mlive > 0 && mlive <= nc) {
-            // entry side: each live entry in FIFO order takes the first compatible Put still free
-            for (int e = 0; e < m && mlive > 0; e++) {
-                const int rk = s_rank[e];
-                if (rk == INT_MIN) continue;  // taken (uniform: written before the last barrier)
-                const unsigned long long em = s_mask[e];
-                int best = INT_MAX;
-#pragma unroll
-                for (int q = 0; q < PM_PER; q++)
-                    if (best == INT_MAX && res[q] < 0 && (em & bit[q]) && (u[q].target == -1 || u[q].target == rk))
-                        best = tid * PM_PER + q;
-                const int b = block_min(best);
-                if (b != INT_MAX) {
-                    if (b / PM_PER == tid) res[b % PM_PER] = e;
-                    if (tid == 0) s_rank[e] = INT_MIN;
-                    mlive--;
+        if (mlive > 0) {
+            // One wave takes the Puts in order (adlb.c:1020-1040 per Put): each takes the first free
+            // compatible entry in FIFO order, found 64 entries per step (s_rank[e] == INT_MIN: taken).
+            // Lane t keeps a lower bound for type t: the entries before it holding type t are all
+            // taken, so an untargeted Put of type t starts there and moves it past its match.
+            if (w == 0) {
+                int tptr = 0;
+                int pty = 0, ptg = -1;  // lane l: Put c0 + i0 + l's type and target (64 Puts per load)
+                for (int i = 0; i < nc; i++) {
+                    if ((i & 63) == 0) {
+                        const int il = i + lane;
+                        pty = il < nc ? (r[c0 + il].meta & (int)M_TYPE) : 0;
+                        ptg = il < nc ? r[c0 + il].target : -1;
+                    }
+                    int found = -1;
+                    if (mlive > 0) {
+                        const int t = __builtin_amdgcn_readlane(pty, i & 63);
+                        const int tg = __builtin_amdgcn_readlane(ptg, i & 63);
+                        const unsigned long long pb = 1ull << t;
+                        const int e0 = __builtin_amdgcn_readlane(tptr, t);
+                        // a targeted Put whose rank has no parked entry: no scan
+                        const bool none = tg >= 0 && !s_rbig && (tg >= PM_RBITS || !((s_rbits[tg >> 5] >> (tg & 31)) & 1u));
+                        for (int base = none ? m : e0; base < m; base += 64) {
+                            const int e = base + lane;
+                            bool hit = false;
+                            if (e < m) {
+                                const int rk = s_rank[e];
+                                hit = rk != INT_MIN && (s_mask[e] & pb) && (tg == -1 || tg == rk);
+                            }
+                            const unsigned long long hb = __ballot(hit);
+                            if (hb) {
+                                found = base + __ffsll((long long)hb) - 1;
+                                break;
+                            }
+                        }
+                        if (found >= 0) {
+                            if (lane == 0) s_rank[found] = INT_MIN;
+                            mlive--;
+                        }
+                        if (tg == -1 && lane == t) tptr = found >= 0 ? found + 1 : m;
+                        __builtin_amdgcn_wave_barrier();  // one wave's LDS operations stay in order
+                    }
+                    if (lane == 0) s_res[i] = found;
                 }
-                __syncthreads();
             }
-        } else if (mlive > 0) {
-            // Put side: each Put in order takes the first compatible entry still free
-            for (int i = 0; i < nc && mlive > 0; i++) {
-                const PutRec ui = r[c0 + i];
-                const unsigned long long pb = 1ull << (ui.meta & (int)M_TYPE);
-                int best = INT_MAX;
+            __syncthreads();
 #pragma unroll
-                for (int e = 0; e < PM_PER; e++) {
-                    const int j = tid * PM_PER + e;  // each thread owns PM_PER consecutive entries: its first hit wins
-                    if (best == INT_MAX && j < m && s_rank[j] != INT_MIN && (s_mask[j] & pb) &&
-                        (ui.target == -1 || ui.target == s_rank[j]))
-                        best = j;
-                }
-                const int b = block_min(best);
-                if (b != INT_MAX) {
-                    if (i / PM_PER == tid) res[i % PM_PER] = b;
-                    if (tid == 0) s_rank[b] = INT_MIN;
-                    mlive--;
-                }
-                __syncthreads();
+            for (int q = 0; q < PM_PER; q++) {
+                const int i = tid * PM_PER + q;
+                if (i < nc) res[q] = s_res[i];
             }
+            mlive = s_mlive_sync(mlive, w);
         }
         // results, pins, and the byte deltas of this thread's Puts in order
         long long acc = 0, pk = LLONG_MIN;

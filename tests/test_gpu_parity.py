@@ -85,6 +85,10 @@ SMALL = {
     "s_c4_targeted": lambda: synth.config4(n_units=6_000, n_reserves=1024, n_ranks=64, seed=607, prio_hi=16),
     "s_c4_t8_tied": lambda: synth.config4(n_units=4_000, n_types=8, n_reserves=1024, n_ranks=32, seed=608, prio_hi=4),
     "s_r1": lambda: synth.config2(n_units=500, n_reserves=1, seed=609),
+    # at most 256 Reserves: block minima over the units in registers instead of the sort
+    "s_c2_r200_t8": lambda: synth.config2(n_units=12_000, n_types=8, n_reserves=200, seed=610, prio_hi=4),
+    "s_c4_r256": lambda: synth.config4(n_units=9_000, n_reserves=256, n_ranks=32, seed=611, prio_hi=8),
+    "s_c2_r256_exhaust": lambda: synth.config2(n_units=100, n_reserves=256, seed=612, prio_hi=3),
 }
 
 

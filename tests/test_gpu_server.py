@@ -248,6 +248,22 @@ def test_tsp_relinked(np_, ns, name, group):
 
 
 @pytest.mark.gpu
+def test_mix_steal_group_rccl_one_server():
+    """ADLB_STEAL_RCCL=1: the steal rounds export into device memory and the
+    blobs go through an RCCL all-gather (ncclUniqueId by MPI_Bcast among the
+    servers).  The one-GPU box holds one server (RCCL wants a GPU per rank), so
+    the round has nothing to steal, but its whole path runs: communicator,
+    device export, all-gather, device settle -- and every unit is consumed once."""
+    out, got, exp, err = _run_mix(3, ["-nservers", "1", "-n", "150"],
+                                  env_extra={"ADLB_STEAL_GROUP": "1", "ADLB_STEAL_RCCL": "1",
+                                             "ADLB_STEAL_IDLE_INTERVAL": "0.002", "ADLB_STEAL_REPORT": "1"})
+    assert got == exp, out[-2000:]
+    assert "RCCL all-gather of the steal blobs on (1 servers)" in err, err[-2000:]
+    rep = _steal_report(err)
+    assert rep and rep[0][0] > 0, err[-2000:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("np_,ns", [(6, 2), (7, 3)])
 def test_mix_many_types_every_unit_once(np_, ns):
     """100 declared work types through the relinked library with the steal group
