@@ -86,6 +86,10 @@ struct DevCounters {
     // structures this handle replaces, plus what the caller adds (adlbq_bytes_adjust)
     long long bytes, bytes_hwm;
     long long got, got_targeted;  // units removed by device-side Get batches (folded into the host counts)
+    // diagnostic sums (stat "diag<k>"): k_reserve_small units gathered, Reserves, constant-clock
+    // ticks to the sorted runs and of the serial choice, launches; k_put_match_blk staged rq
+    // entries, ticks of the staging and of the matching
+    long long diag[8];
     // in a batch snapshot (mapped host memory): the batch's tag, stored after every other
     // field has been written back; the host reads the snapshot once the tag matches
     unsigned long long snap_tag;
@@ -318,7 +322,8 @@ struct adlbq_server {
     std::vector<int> free_pages;
     int *h_pdead = nullptr; long long cap_pdead = 0; int pdead_np = 0; bool pdead_pending = false;
     hipEvent_t pdead_ev = nullptr; long long pdead_last = -1000000, pages_recycled = 0;
-    int recycle_pages = 1;             // "recycle_pages": 0 = keep every page (the old behaviour)
+    int recycle_pages = 1;
+    int rq_compact_calls = 0; long long rq_compactions = 0;  // background rq compaction (maybe_compact_rq)             // "recycle_pages": 0 = keep every page (the old behaviour)
     int small_pages = 4;               // "small_pages": an open bucket of at most this many pages and a batch of
     int small_r = 1024;                //   at most "small_r" Reserves take the one-workgroup choice (0: never)
     long long small_batches = 0;       // reserve batches served by it (stat "small_batches")
@@ -401,6 +406,7 @@ int ensure_req_capacity(adlbq_server *h, int n);
 int sync_tables(adlbq_server *h);          // page tables, anchors, qmstat, tq -> device
 void recycle_apply(adlbq_server *h);       // drop the dead open pages a finished k_page_dead found
 int recycle_launch(adlbq_server *h);       // look for dead open pages in the background (when worth it)
+void maybe_compact_rq(adlbq_server *h);    // compact a thinned-out rq in the background
 int ensure_zc(adlbq_server *h, long long n);  // mapped pinned staging of >= n ints (h_zc / d_zc)
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);

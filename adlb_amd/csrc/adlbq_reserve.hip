@@ -4130,6 +4130,7 @@ struct SmallArgs {
     int *umatch, *cslot, *needsort;
     const int *tmatch;
     const unsigned long long *mask;
+    DevCounters *ctr;
 };
 
 // sort key, ascending = better within a type: type (7 bits), prio descending, position ascending
@@ -4156,6 +4157,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
     if (tid < ADLBQ_MAX_TYPES) s_start[tid] = s_end[tid] = 0;
     if (tid < T) a.needsort[tid] = 0;  // k_finalize reports needsort_last from it
     __syncthreads();
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     // the available units, appended in any order (they are sorted next); every load in flight first
     const int nslots = a.npages > 0 ? (a.npages - 1) * PAGE + a.tail_fill : 0;
     constexpr int GPT = SMALL_UNITS / SMALL_THREADS;
@@ -4225,6 +4227,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
     }
     __syncthreads();
     if (tid >= 64) return;
+    const unsigned long long t_sorted = __builtin_amdgcn_s_memrealtime();
     constexpr unsigned long long KM = (1ull << 56) - 1;  // key without the type field
     auto uni = [](unsigned long long x) {  // a wave-uniform value into scalar registers
         return ((unsigned long long)(unsigned int)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
@@ -4244,22 +4247,31 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
             c2[q] = hp[q] + 2 < he[q] ? uni(skey[hp[q] + 2]) : ~0ull;
         }
         unsigned long long mreg = 0ull;  // lane l: request j0 + l's mask (0: matched in the targeted phase)
-        for (int j = 0; j < R; j++) {
+        int um_l = -1, cs_l = -1;         // lane l: request j0 + l's results, stored once per 64
+        unsigned int live = 0u;           // types whose list is not exhausted (uniform)
+#pragma unroll
+        for (int q = 0; q < TB; q++) live |= c0[q] != ~0ull ? (1u << q) : 0u;
+        int j = 0;
+        for (; j < R && live; j++) {
             if ((j & 63) == 0) {
                 const int jl = j + lane;
                 mreg = jl < R && stm[jl] < 0 ? smask[jl] : 0ull;
+                um_l = -1;
+                cs_l = -1;
             }
             const unsigned long long mk =
                 ((unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(mreg >> 32), j & 63) << 32) |
                 (unsigned long long)(unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)mreg, j & 63);
             unsigned long long best = ~0ull;
             int bq = -1;
+            if (mk & live) {
 #pragma unroll
-            for (int q = 0; q < TB; q++)
-                if (((mk >> q) & 1ull) && c0[q] != ~0ull && (c0[q] & KM) < best) {
-                    best = c0[q] & KM;
-                    bq = q;
-                }
+                for (int q = 0; q < TB; q++)
+                    if (((mk >> q) & 1ull) && c0[q] != ~0ull && (c0[q] & KM) < best) {
+                        best = c0[q] & KM;
+                        bq = q;
+                    }
+            }
             if (bq >= 0) {
 #pragma unroll
                 for (int q = 0; q < TB; q++)
@@ -4268,17 +4280,31 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
                         c0[q] = c1[q];
                         c1[q] = c2[q];
                         c2[q] = hp[q] + 2 < he[q] ? uni(skey[hp[q] + 2]) : ~0ull;
+                        if (c0[q] == ~0ull) live &= ~(1u << q);
                     }
-                if (lane == 0) {
-                    const unsigned int pos = (unsigned int)(best & 0xffffffu);
-                    const int p = (int)(pos >> PAGE_SHIFT);
-                    const bool ok = p < a.npages;
-                    a.cslot[j] = ok ? (a.pages[p] << PAGE_SHIFT) | (int)(pos & (PAGE - 1)) : -1;
-                    a.umatch[j] = ok ? j : -1;
+                const unsigned int pos = (unsigned int)(best & 0xffffffu);
+                const int p = (int)(pos >> PAGE_SHIFT);
+                if ((j & 63) == lane && p < a.npages) {
+                    cs_l = (a.pages[p] << PAGE_SHIFT) | (int)(pos & (PAGE - 1));
+                    um_l = j;
                 }
-            } else if (lane == 0) {
-                a.umatch[j] = -1;
             }
+            if ((j & 63) == 63 || j == R - 1 || !live) {  // this block of 64 Reserves' results
+                const int jl = (j & ~63) + lane;
+                if (jl <= j) {
+                    a.umatch[jl] = um_l;
+                    a.cslot[jl] = cs_l;
+                }
+            }
+        }
+        for (int jl = j + lane; jl < R; jl += 64) a.umatch[jl] = -1;  // every list exhausted: no unit left
+        if (lane == 0) {  // diagnostic sums
+            const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+            atomicAdd((unsigned long long *)&a.ctr->diag[0], (unsigned long long)n);
+            atomicAdd((unsigned long long *)&a.ctr->diag[1], (unsigned long long)R);
+            atomicAdd((unsigned long long *)&a.ctr->diag[2], t_sorted - t_start);
+            atomicAdd((unsigned long long *)&a.ctr->diag[3], t_end - t_sorted);
+            atomicAdd((unsigned long long *)&a.ctr->diag[4], 1ull);
         }
         return;
     }
@@ -4388,6 +4414,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if ((rc = ensure_req_capacity(h, R))) return rc;
     hsec("req_cap", ht);
     recycle_apply(h);
+    maybe_compact_rq(h);
     if ((rc = sync_tables(h))) return rc;
     if ((rc = recycle_launch(h))) return rc;
     hsec("tables", ht);
@@ -4478,7 +4505,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     if (small) {
         const SmallArgs sa{pa, targeted ? 0 : 1, h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, R,
-                           h->d_umatch, h->d_cslot, h->d_needsort, h->d_tmatch, h->d_mask};
+                           h->d_umatch, h->d_cslot, h->d_needsort, h->d_tmatch, h->d_mask, h->d_ctr};
         const size_t lds = sizeof(unsigned long long) * (SMALL_UNITS + SMALL_R) + sizeof(int) * SMALL_R;
         stage_begin(h, "small", &ev);
         if (T <= 4) k_reserve_small<4><<<1, SMALL_THREADS, lds, s>>>(sa);

@@ -209,6 +209,21 @@ __global__ __launch_bounds__(1024) void k_rq_reclaim(int *rq_rank, int *rq_types
 
 __global__ void k_set_rq_next(DevCounters *ctr, int v) { ctr->rq_next = v; }
 
+// Parked Reserves come and go while the oldest stay: the live entries thin out
+// over a long rq, and every Put batch's match stages the whole of it (from
+// rq_head).  When the last landed counters show mostly dead slots, compact in
+// the background (stream-ordered, nothing waits; the host's rq bounds stay
+// upper bounds), at most once per RQ_COMPACT_EVERY calls.
+constexpr int RQ_COMPACT_EVERY = 32;
+void maybe_compact_rq(adlbq_server *h) {
+    if (!h->d_rq_seq || h->rq_cap <= 0 || ++h->rq_compact_calls < RQ_COMPACT_EVERY) return;
+    const long long span = (long long)h->ctr.rq_n - h->ctr.rq_head;
+    if (span <= 2ll * h->ctr.rq_live + 4096) return;
+    h->rq_compact_calls = 0;
+    h->rq_compactions++;
+    k_rq_reclaim<<<1, 1024, 0, h->stream>>>(h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr);
+}
+
 int ensure_rq_capacity(adlbq_server *h, int extra) {
     if ((h->ctr_stale ? h->rq_next_upper : (long long)h->ctr.rq_next) + extra > INT_MAX) {
         int rc;
@@ -671,6 +686,7 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
 // running sum just after a Put's allocation (adlb.c:933, 963, 1040).  *over = 1
 // when the live entries exceed PM_CAP (the caller then runs k_put_match).
 constexpr int PM_CAP = 4096, PM_THREADS = 1024, PM_PER = PM_CAP / PM_THREADS, PM_WAVES = PM_THREADS / 64;
+constexpr int PM_REG = 4;  // entries per lane of the register-resident match (<= 256 parked)
 __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__restrict__ r, int n,
                                                               const int *__restrict__ rq_rank,
                                                               const int *__restrict__ rq_types, int *rq_live,
@@ -688,6 +704,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
     __shared__ long long s_wsum[PM_WAVES], s_wpk[PM_WAVES];
     __shared__ int s_ut[ADLBQ_MAX_TYPES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     const int head = ctr->rq_head, nrq = ctr->rq_n;
     for (int t = tid; t < T; t += PM_THREADS) s_ut[t] = utypes[t];
     for (int q = tid; q < PM_RBITS / 32; q += PM_THREADS) s_rbits[q] = 0u;
@@ -733,6 +750,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
         __syncthreads();
     }
     const int m = s_tot;
+    const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
     if (m > PM_CAP) {  // too many parked Reserves for the staging: the caller falls back
         if (tid == 0) *over = 1;
         return;
@@ -763,7 +781,56 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
             // compatible entry in FIFO order, found 64 entries per step (s_rank[e] == INT_MIN: taken).
             // Lane t keeps a lower bound for type t: the entries before it holding type t are all
             // taken, so an untargeted Put of type t starts there and moves it past its match.
-            if (w == 0) {
+            if (w == 0 && m <= PM_REG * 64) {
+                // at most 256 entries: lane l holds entries l, l + 64, ... in registers, their taken
+                // bits in four uniform words; a Put is PM_REG ballots, no memory access
+                int erk[PM_REG];
+                unsigned long long emk[PM_REG], taken[PM_REG];
+#pragma unroll
+                for (int q = 0; q < PM_REG; q++) {
+                    const int e = q * 64 + lane;
+                    erk[q] = e < m ? s_rank[e] : INT_MIN;
+                    emk[q] = e < m ? s_mask[e] : 0ull;
+                    taken[q] = __ballot(e < m && erk[q] == INT_MIN);  // taken by an earlier chunk
+                }
+                int pty = 0, ptg = -1, res_l = -1;  // lane l: Put i0 + l's type, target, result
+                int i = 0;
+                for (; i < nc && mlive > 0; i++) {
+                    if ((i & 63) == 0) {
+                        const int il = i + lane;
+                        pty = il < nc ? (r[c0 + il].meta & (int)M_TYPE) : 0;
+                        ptg = il < nc ? r[c0 + il].target : -1;
+                        res_l = -1;
+                    }
+                    const int t = __builtin_amdgcn_readlane(pty, i & 63);
+                    const int tg = __builtin_amdgcn_readlane(ptg, i & 63);
+                    int found = -1;
+#pragma unroll
+                    for (int q = 0; q < PM_REG; q++) {
+                        if (found >= 0) break;
+                        const bool hit = ((emk[q] >> t) & 1ull) && (tg == -1 || tg == erk[q]) &&
+                                         !((taken[q] >> lane) & 1ull) && erk[q] != INT_MIN;
+                        const unsigned long long hb = __ballot(hit);
+                        if (hb) {
+                            const int b = __ffsll((long long)hb) - 1;
+                            found = q * 64 + b;
+                            taken[q] |= 1ull << b;
+                        }
+                    }
+                    if (found >= 0) mlive--;
+                    if ((i & 63) == lane) res_l = found;
+                    if ((i & 63) == 63 || i == nc - 1 || mlive == 0) {  // this block of 64 Puts' results
+                        const int il = (i & ~63) + lane;
+                        if (il <= i) s_res[il] = res_l;
+                    }
+                }
+                for (int il = i + lane; il < nc; il += 64) s_res[il] = -1;  // every entry taken
+#pragma unroll
+                for (int q = 0; q < PM_REG; q++) {  // the taken entries, for the later chunks
+                    const int e = q * 64 + lane;
+                    if (e < m && ((taken[q] >> lane) & 1ull)) s_rank[e] = INT_MIN;
+                }
+            } else if (w == 0) {
                 int tptr = 0;
                 int pty = 0, ptg = -1;  // lane l: Put c0 + i0 + l's type and target (64 Puts per load)
                 for (int i = 0; i < nc; i++) {
@@ -810,6 +877,11 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                 if (i < nc) res[q] = s_res[i];
             }
             mlive = s_mlive_sync(mlive, w);
+            if (tid == 0 && c0 == 0) {  // diagnostic sums (first chunk)
+                atomicAdd((unsigned long long *)&ctr->diag[5], (unsigned long long)m);
+                atomicAdd((unsigned long long *)&ctr->diag[6], t_staged - t_start);
+                atomicAdd((unsigned long long *)&ctr->diag[7], __builtin_amdgcn_s_memrealtime() - t_staged);
+            }
         }
         // results, pins, and the byte deltas of this thread's Puts in order
         long long acc = 0, pk = LLONG_MIN;
@@ -1608,6 +1680,7 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
     if (h) wq_changed(h);
     if (n == 0) return ADLBQ_OK;
     hipSetDevice(h->device);
+    maybe_compact_rq(h);
     for (int i = 0; i < n; i++)
         if (type_index(h, units9[9 * i]) < 0) return fail(ADLBQ_ERR_TYPE, "adlbq_put_batch: undeclared work type");
     int rc;
@@ -2543,6 +2616,13 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     }
     if (n == "small_batches") return h->small_batches;
     if (n == "pages_recycled") return h->pages_recycled;
+    if (n == "rq_compactions") return h->rq_compactions;
+    if (n.rfind("diag", 0) == 0 && n.size() == 5 && n[4] >= '0' && n[4] <= '7') {
+        h->ctr_stale = true;
+        int rc;
+        if ((rc = refresh_counters(h))) return rc;
+        return h->ctr.diag[n[4] - '0'];
+    }
     if (n == "open_pages") return (long long)h->open.pages.size();
     if (n == "pages_total") return h->n_pages;
     if (n == "chain_rounds") return h->ctr.chain_rounds;

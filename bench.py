@@ -595,6 +595,13 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
             # reserve batches served by the one-workgroup choice, and the host sections of the reserve call (ms)
             c5_stats.clear()
             c5_stats["small_batches"] = sum(s_.stat("small_batches") for s_ in srvs)
+            dg = [sum(s_.stat(f"diag{k}") for s_ in srvs) for k in range(8)]
+            c5_stats["small_units_per_call"] = round(dg[0] / max(dg[4], 1), 1)
+            c5_stats["small_reserves_per_call"] = round(dg[1] / max(dg[4], 1), 1)
+            c5_stats["small_us_to_sorted"] = round(dg[2] / max(dg[4], 1) / 100, 2)  # 100 MHz constant clock
+            c5_stats["small_us_serial"] = round(dg[3] / max(dg[4], 1) / 100, 2)
+            c5_stats["putmatch_calls_with_parked"] = "see diag5-7"
+            c5_stats["putmatch_diag"] = dg[5:]
             for sec_name in ("total", "tindex", "l_scan", "l_rank", "l_chain", "l_fin", "tables", "sort"):
                 c5_stats["host_ms_" + sec_name] = round(sum(s_.stat("hacc:" + sec_name) for s_ in srvs) / 1e6, 1)
             return got, steals, sec, calls, wall_s
