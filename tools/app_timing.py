@@ -8,6 +8,9 @@ same host, with the answer checked on every run.  libadlb.so variants: Put
 batching on / off (ADLB_PUT_BATCH) and the steal group off / on
 (ADLB_STEAL_GROUP).
 
+The deep-queue case (tests/apps/adlb_deep.c) is matching-dominated: every unit
+is queued before the first Reserve, and `app_time` is its Reserve/Get phase.
+
 nq and tsp both end by exhaustion, which the reference detects after a 5 s
 quiet qmstat ring (adlb.c:490, 754-785) and libadlb.so after two 0.5 s polls,
 so the wall times are dominated by that detection delay; nq also prints its
@@ -42,9 +45,20 @@ def run(binary, np_, args, stdin=None, env_extra=None, timeout=600):
     return el, r.stdout
 
 
+def deep_ok(n):
+    def ok(out):
+        ln = [x for x in out.splitlines() if x.startswith("adlb_deep:")]
+        if not ln:
+            return False
+        v = ln[0].split()
+        return v[2] == v[6] == str(n) and v[4] == v[7]
+    return ok
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--only", default="", help="run only the cases whose name starts with this")
     args = ap.parse_args()
     with open(os.path.join(GOLD, "tsp_expected.json")) as f:
         tsp_exp = json.load(f)
@@ -55,7 +69,12 @@ def main():
          lambda out: "found 2680 solutions" in out),
         ("tsp 11 cities, 2 servers, 3 apps", "tsp", 5, ["-nservers", "2"], os.path.join(GOLD, "tsp_m11.txt"),
          lambda out: f"bdist {tsp_exp['tsp_m11.txt']['reference_bdist']}" in out),
+        # matching-dominated: every unit queued before any Reserve (tests/apps/adlb_deep.c); the
+        # reference scans its xq list per Reserve, the engine matches the waiting Reserves together
+        ("deep queue 40000 units, 1 server, 4 apps", "deep", 5, ["-n", "40000"], None, deep_ok(40000)),
+        ("deep queue 100000 units, 1 server, 8 apps", "deep", 9, ["-n", "100000"], None, deep_ok(100000)),
     ]
+    cases = [c for c in cases if c[0].startswith(args.only)]
     variants = [("reference", "_plain", None),
                 ("libadlb.so", "_amd", {"ADLB_PUT_BATCH": "1", "ADLB_STEAL_GROUP": "0"}),
                 ("libadlb.so, one engine call per Put", "_amd", {"ADLB_PUT_BATCH": "0", "ADLB_STEAL_GROUP": "0"}),
@@ -65,6 +84,8 @@ def main():
         row = {"case": name, "np": np_, "args": a, "seconds": {}}
         for vname, suffix, env in variants:
             b = os.path.join(REF, app + suffix)
+            if app == "deep" and suffix == "_amd":
+                b = os.path.join(ROOT, "tests", "apps", "adlb_deep")
             if not os.path.exists(b):
                 row["seconds"][vname] = None
                 continue
@@ -74,7 +95,7 @@ def main():
                 if not ok(out):
                     raise RuntimeError(f"{vname} {name}: wrong answer\n{out[-1500:]}")
                 ts.append(round(el, 3))
-                m = [ln for ln in out.splitlines() if "solutions, time" in ln]
+                m = [ln for ln in out.splitlines() if "solutions, time" in ln or ln.startswith("adlb_deep:")]
                 if m:
                     at.append(float(m[0].split()[-1]))
             row["seconds"][vname] = {"min": min(ts), "all": ts}
