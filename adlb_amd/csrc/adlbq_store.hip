@@ -213,12 +213,15 @@ __global__ void k_set_rq_next(DevCounters *ctr, int v) { ctr->rq_next = v; }
 // over a long rq, and every Put batch's match stages the whole of it (from
 // rq_head).  When the last landed counters show mostly dead slots, compact in
 // the background (stream-ordered, nothing waits; the host's rq bounds stay
-// upper bounds), at most once per RQ_COMPACT_EVERY calls.
-constexpr int RQ_COMPACT_EVERY = 32;
+// upper bounds), at most once per RQ_COMPACT_EVERY calls, and before the rq fills (a
+// full rq reclaims synchronously: config 3 did every fifth step).
+constexpr int RQ_COMPACT_EVERY = 4;
 void maybe_compact_rq(adlbq_server *h) {
     if (!h->d_rq_seq || h->rq_cap <= 0 || ++h->rq_compact_calls < RQ_COMPACT_EVERY) return;
+    // (the last landed counters: a compaction since shows as a shorter span only once it lands)
     const long long span = (long long)h->ctr.rq_n - h->ctr.rq_head;
-    if (span <= 2ll * h->ctr.rq_live + 4096) return;
+    if (span <= 2ll * h->ctr.rq_live + 4096 && span * 2 <= h->rq_cap) return;
+    if (span <= h->ctr.rq_live + 256) return;  // nothing much to reclaim
     h->rq_compact_calls = 0;
     h->rq_compactions++;
     k_rq_reclaim<<<1, 1024, 0, h->stream>>>(h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr);

@@ -72,7 +72,7 @@ def main():
         # matching-dominated: every unit queued before any Reserve (tests/apps/adlb_deep.c); the
         # reference scans its xq list per Reserve, the engine matches the waiting Reserves together
         ("deep queue 40000 units, 1 server, 4 apps", "deep", 5, ["-n", "40000"], None, deep_ok(40000)),
-        ("deep queue 100000 units, 1 server, 8 apps", "deep", 9, ["-n", "100000"], None, deep_ok(100000)),
+        ("deep queue 20000 units, 1 server, 8 apps", "deep", 9, ["-n", "20000"], None, deep_ok(20000)),
     ]
     cases = [c for c in cases if c[0].startswith(args.only)]
     variants = [("reference", "_plain", None),
