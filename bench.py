@@ -600,8 +600,10 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
             c5_stats["small_reserves_per_call"] = round(dg[1] / max(dg[4], 1), 1)
             c5_stats["small_us_to_sorted"] = round(dg[2] / max(dg[4], 1) / 100, 2)  # 100 MHz constant clock
             c5_stats["small_us_serial"] = round(dg[3] / max(dg[4], 1) / 100, 2)
-            c5_stats["putmatch_calls_with_parked"] = "see diag5-7"
-            c5_stats["putmatch_diag"] = dg[5:]
+            # k_put_match_blk over the run (first chunk of each batch with something parked)
+            c5_stats["put_match_staged_entries"] = dg[5]
+            c5_stats["put_match_stage_ms"] = round(dg[6] / 1e5, 1)
+            c5_stats["put_match_match_ms"] = round(dg[7] / 1e5, 1)
             for sec_name in ("total", "tindex", "l_scan", "l_rank", "l_chain", "l_fin", "tables", "sort"):
                 c5_stats["host_ms_" + sec_name] = round(sum(s_.stat("hacc:" + sec_name) for s_ in srvs) / 1e6, 1)
             return got, steals, sec, calls, wall_s
