@@ -322,8 +322,9 @@ struct adlbq_server {
     std::vector<int> free_pages;
     int *h_pdead = nullptr; long long cap_pdead = 0; int pdead_np = 0; bool pdead_pending = false;
     hipEvent_t pdead_ev = nullptr; long long pdead_last = -1000000, pages_recycled = 0;
-    int recycle_pages = 1;
-    int rq_compact_calls = 0; long long rq_compactions = 0;  // background rq compaction (maybe_compact_rq)             // "recycle_pages": 0 = keep every page (the old behaviour)
+    int recycle_pages = 1;             // "recycle_pages": 0 = keep every page (the old behaviour)
+    int select_wave = 1;               // "select_wave": pass 2 with one wave per page (T <= 8); 0 = four
+    int rq_compact_calls = 0; long long rq_compactions = 0;  // background rq compaction (maybe_compact_rq)
     int small_pages = 4;               // "small_pages": an open bucket of at most this many pages and a batch of
     int small_r = 1024;                //   at most "small_r" Reserves take the one-workgroup choice (0: never)
     long long small_batches = 0;       // reserve batches served by it (stat "small_batches")

@@ -1010,6 +1010,263 @@ __device__ __forceinline__ void select_open_body(
     }
 }
 
+// Pass 2 with one wave per page (T <= 8): the page's four quarter lists in
+// slot order, one after the other, against one running count per column
+// (the page's prefix, then each list's candidates as they are ranked).  With
+// 64-thread workgroups every page is resident at once (2,442 pages at the
+// metric size against ~4,000 such workgroups), where k_select_open's
+// four-wave workgroups ran in two rounds (82 VGPRs, 20 KB of LDS each).
+// Results as k_select_open's.
+#ifndef ADLBQ_SELW_GATE
+#define ADLBQ_SELW_GATE 1  // k_select_wave reads a column's page prefix only at or below its threshold
+#endif
+template <int TB>
+__global__ __launch_bounds__(64) void k_select_wave(
+    const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
+    const uint32_t *__restrict__ meta, int T, const long long *__restrict__ anchor,
+    const int *__restrict__ theta, const int *__restrict__ need,
+    const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
+    const int *__restrict__ candlen, int *__restrict__ candoff_out,
+    unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
+    const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
+    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
+    unsigned char *__restrict__ rtype, int R,
+    unsigned long long *kst) {
+    static_assert(TB <= 8 && TB <= RANK_FAST_T, "one wave per page: T <= 8");
+    constexpr int RT = TB;
+    constexpr int CPL = TB * NB / 64;  // columns per lane
+    extern __shared__ unsigned int lds[];  // run[C], then list[1024]
+    __shared__ long long sanc[TB], scut[TB];
+    __shared__ int sth[TB], sneed[TB], soff[TB], slen[TB], slb[TB];
+    __shared__ int sbo[TB * NB];
+    const int C = T * NB, lane = threadIdx.x, p = blockIdx.x;
+    kstamp(kst, p, 0);
+    unsigned int *run = lds;
+    unsigned int *list = lds + C;
+    const long long base = (long long)pages[p] << PAGE_SHIFT;
+    const int fill = (p == npages - 1) ? tail_fill : PAGE;
+    const bool tl = lane < T;
+    const int th_l = tl ? theta[lane] : -1, nd_l = tl ? need[lane] : 0, len_l = tl ? candlen[lane] : 0;
+    const long long an_l = tl ? anchor[lane] : 0, gc_l = tl ? gcut[lane] : 0;
+    int sn[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) sn[q] = specn[(long long)p * 4 + q];
+    int bo_r[CPL];
+#pragma unroll
+    for (int r = 0; r < CPL; r++) {
+        const int c = lane + r * 64;
+        bo_r[r] = (crank != nullptr && c < C) ? binoff[c] : 0;
+    }
+    unsigned int se[4][SPEC_CAP / 64];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int k = 0; k < SPEC_CAP / 64; k++) se[q][k] = spec[((long long)p * 4 + q) * SPEC_CAP + k * 64 + lane];
+    const long long cut_l = cut_of(th_l, an_l);
+    const int lb_l = tl ? lump_bin(an_l, gc_l) : NB;
+    const bool lists_ok = __ballot(th_l >= 0 && th_l >= lb_l) == 0;  // no threshold in a lump
+    if (p == 0 && lane == 0) ctr->spec_page0 = lists_ok && sn[0] <= SPEC_CAP ? 1 : sn[0] > SPEC_CAP ? -sn[0] : -100000;
+    // the page's first rank in each column at or below its threshold: the chunk's
+    // exclusive prefix plus the counts of the chunk's earlier pages
+    unsigned int ppv[CPL];
+    const int p0 = (p / CHUNK) * CHUNK;
+#pragma unroll
+    for (int r = 0; r < CPL; r++) {
+        const int c = lane + r * 64;
+        ppv[r] = 0;
+        const int thc = __shfl(th_l, (c / NB) & 63, 64);
+        const bool use = c < C && (c % NB) <= thc;
+        if (ADLBQ_SELW_GATE ? use : c < C) {  // ungated: the loads need not wait for theta
+            unsigned int v = csum[(long long)(p / CHUNK) * C + c];
+            unsigned short g[CHUNK - 1];
+#pragma unroll
+            for (int q = 0; q < CHUNK - 1; q++) g[q] = p0 + q < p ? gh[(long long)(p0 + q) * C + c] : (unsigned short)0;
+#pragma unroll
+            for (int q = 0; q < CHUNK - 1; q++) v += g[q];
+            ppv[r] = use ? v : 0u;
+        }
+    }
+    if (tl) {
+        sanc[lane] = an_l;
+        sth[lane] = th_l;
+        sneed[lane] = nd_l;
+        scut[lane] = cut_l;
+        slen[lane] = len_l;
+        slb[lane] = lb_l;
+    }
+    const bool fast = crank != nullptr && __ballot(tl && th_l >= NBX) == 0;
+#pragma unroll
+    for (int r = 0; r < CPL; r++) {
+        const int c = lane + r * 64;
+        if (c < C) {
+            run[c] = ppv[r];
+            if (fast) sbo[c] = bo_r[r];
+        }
+    }
+    {  // candidate list offsets: exclusive prefix of candlen over types
+        int x = len_l;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (tl) soff[lane] = x - len_l;
+        if (p == 0 && tl) candoff_out[lane] = x - len_l;
+        if (p == 0 && lane == T - 1) candoff_out[T] = x;
+    }
+    __syncthreads();
+    kstamp(kst, p, 1);
+    long long an_u[RT];
+    int th_u[RT], nd_u[RT], len_u[RT];
+#pragma unroll
+    for (int u = 0; u < RT; u++) {
+        const bool ok = u < T;
+        an_u[u] = ok ? sanc[u] : 0;
+        th_u[u] = ok ? sth[u] : -1;
+        nd_u[u] = ok ? sneed[u] : 0;
+        len_u[u] = ok ? slen[u] : 0;
+    }
+    const unsigned long long lt = lanemask_lt();
+    // The quarters' candidates in slot order, listed together and ranked in one
+    // go when they are pass 1's lists (at most 4 * SPEC_CAP entries; typically
+    // one 64-wide step for the page), a quarter read again ranked on its own.
+    int n = 0, w = 0;
+#pragma unroll 1
+    while (true) {
+        bool rank_now = w == 4;
+        if (w < 4) {
+            int snw = sn[0];
+#pragma unroll
+            for (int q = 1; q < 4; q++)
+                if (w == q) snw = sn[q];
+            const bool sp = lists_ok && snw <= SPEC_CAP;
+            if (!sp && n > 0) {
+                rank_now = true;  // rank what is listed before the quarter is read again
+            } else if (sp) {  // pass 1's list, filtered by the thresholds
+#pragma unroll
+                for (int k = 0; k < SPEC_CAP / 64; k++) {
+                    if (k * 64 >= snw) break;
+                    unsigned int e = se[0][k];
+#pragma unroll
+                    for (int q = 1; q < 4; q++)
+                        if (w == q) e = se[q][k];
+                    const int col = (int)(e >> 12), ct = col / NB;
+                    const bool c = k * 64 + lane < snw && col - ct * NB <= sth[ct];
+                    const unsigned long long b = __ballot(c);
+                    if (c) list[n + __popcll(b & lt)] = e;
+                    n += __popcll(b);
+                }
+            } else {  // the quarter's columns read again
+                int4 pv[4];
+                uint4 mv[4];
+                load_quarter(prio, meta, pbase, pwide, pages[p], fill, w, pv, mv);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int pr[4] = {pv[k].x, pv[k].y, pv[k].z, pv[k].w};
+                    const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+                    bool cnd[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        cnd[q] = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && (long long)pr[q] >= scut[mm[q] & M_TYPE];
+                    const unsigned long long b0 = __ballot(cnd[0]), b1 = __ballot(cnd[1]), b2 = __ballot(cnd[2]),
+                                             b3 = __ballot(cnd[3]);
+                    if (!(b0 | b1 | b2 | b3)) continue;
+                    int pos = n + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        if (cnd[q]) {
+                            const int t = mm[q] & M_TYPE;
+                            const int bq = bin_of(sanc[t] - pr[q]);
+                            const int col = t * NB + (bq >= slb[t] ? NB - 1 : bq);  // pass 1's lump
+                            list[pos++] = ((unsigned int)col << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+                        }
+                    }
+                    n += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+                }
+            }
+            if (!rank_now) {
+                w++;
+                rank_now = !sp || w == 4;
+            }
+        }
+        if (!rank_now) continue;
+        if (w == 4) kstamp(kst, p, 2);
+        __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations complete in order
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            const unsigned int e = i < n ? list[i] : 0u;
+            const int col = (int)(e >> 12), so = (int)(e & (PAGE - 1));
+            const int ct = col / NB, cb = col - ct * NB;
+            const int pr = i >= n ? 0 : cb < NBX ? (int)(sanc[ct] - cb) : prio[base + so];
+            const unsigned int bpos = ((unsigned int)p << PAGE_SHIFT) | (unsigned int)so;
+            int tcol[RT], cnt[RT];
+            if (fast) {
+#pragma unroll
+                for (int u = 0; u < RT; u++) {
+                    const long long bu = an_u[u] - (long long)pr;
+                    tcol[u] = (bu >= 0 && bu <= th_u[u]) ? u * NB + (int)bu : -1;
+                    cnt[u] = 0;
+                }
+            }
+            constexpr int CBITS = TB <= 4 ? 8 : 9;  // bits of a column index (T * NB columns)
+            unsigned long long cb_[CBITS];
+#pragma unroll
+            for (int b = 0; b < CBITS; b++) cb_[b] = __ballot((col >> b) & 1);
+            const unsigned long long vm = __ballot(i < n) & lt;
+            auto earlier_in = [&](int x) {
+                unsigned long long m = vm;
+#pragma unroll
+                for (int b = 0; b < CBITS; b++) m &= ((x >> b) & 1) ? cb_[b] : ~cb_[b];
+                return __popcll(m);
+            };
+            const int rank = earlier_in(col);
+            if (fast) {
+#pragma unroll
+                for (int u = 0; u < RT; u++) cnt[u] = tcol[u] >= 0 ? earlier_in(tcol[u]) : 0;
+            }
+            if (i < n) {
+                const unsigned int r = run[col] + rank;
+                const int t = col / NB, b = col - t * NB;
+                if (b < sth[t] || b >= NBX || (int)r < sneed[t]) {  // exact threshold bin: its first `need` only
+                    const long long at = (long long)soff[t] + binoff[col] + r;
+                    ckey[at] = make_key(pr, bpos);
+                    cslot[at] = (int)(base + so);
+                    if (fast) {
+                        int lb[RT], g = 0;
+#pragma unroll
+                        for (int u = 0; u < RT; u++) {
+                            lb[u] = 0;
+                            if (tcol[u] >= 0) {
+                                int c = (int)run[tcol[u]] + cnt[u];
+                                if (tcol[u] - u * NB == th_u[u]) c = min(c, nd_u[u]);
+                                lb[u] = sbo[tcol[u]] + c;
+                            } else if (an_u[u] >= (long long)pr) {
+                                lb[u] = len_u[u];
+                            }
+                            g += lb[u];
+                        }
+                        crank[at] = ((unsigned int)g << 6) | (unsigned int)t;
+                        if (lv != nullptr && g < R) rtype[g] = (unsigned char)t;
+                        if (lv != nullptr && (g & (LV_STEP - 1)) == 0 && g < R)
+#pragma unroll
+                            for (int u = 0; u < RT; u++)
+                                if (u < T) lv[(long long)(g / LV_STEP) * T + u] = lb[u];
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (i < n) atomicAdd(&run[col], 1u);  // after every lane of the step has read run[]
+            __builtin_amdgcn_wave_barrier();
+        }
+        n = 0;
+        if (w == 4) break;
+    }
+    kstamp(kst, p, 3);
+    if (p == 0 && lane == 0) ctr->rank_fast = fast ? 1 : 0;
+    const bool empty = __ballot(tl && len_l <= 0) != 0ull;
+    if (crank != nullptr && p == 0 && lane == 0) ctr->rank_covered = (fast && !empty) ? 1 : 0;
+}
+
 template <int TB>  // TB >= T; the candidates are ranked here only for TB <= RT
 __global__ __launch_bounds__(256) void k_select_open(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
@@ -3310,6 +3567,13 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                                 h->d_ctr, (sort || !h->rank_in_select) ? nullptr : h->d_crank,
                                 (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R, np};
             h->grec->lds_sel = sizeof(unsigned int) * (4 * C + 4 * 1024);
+        } else if (T <= 8 && h->select_wave) {
+            auto selw = T <= 4 ? k_select_wave<4> : k_select_wave<8>;
+            selw<<<np, 64, sizeof(unsigned int) * (C + 1024), s>>>(
+                h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_theta, h->d_need,
+                h->d_binoff, csum, h->d_gh, h->d_candlen, h->d_candoff, h->d_ckey, h->d_cslot, h->d_gcut, h->d_spec,
+                h->d_specn, h->d_pbase, h->d_pwide, h->d_ctr, (sort || !h->rank_in_select) ? nullptr : h->d_crank,
+                !sort ? h->d_lv : nullptr, h->d_rtype, R, kst_for(h, np, 1));
         } else
         sel<<<np, 256, sizeof(unsigned int) * (4 * C + 4 * 1024), s>>>(
             h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_seq, T, h->d_anchor, h->d_theta,

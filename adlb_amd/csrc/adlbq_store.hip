@@ -2557,6 +2557,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->group_launch = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "select_wave") {
+        h->select_wave = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "recycle_pages") {
         h->recycle_pages = value ? 1 : 0;
         return ADLBQ_OK;

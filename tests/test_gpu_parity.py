@@ -200,6 +200,7 @@ VARIANTS = {
     "default": {},
     "rank_in_k_rank": {"rank_in_select": 0},  # k_rank ranks every candidate (k_select_open does not)
     "split_prep": {"split_prep": 1},          # request preparation and pass 1 as two launches
+    "select_four_waves": {"select_wave": 0},  # pass 2 with four waves per page (k_select_open) for T <= 8
 }
 
 
