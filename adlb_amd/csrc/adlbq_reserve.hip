@@ -272,135 +272,188 @@ __host__ __device__ __forceinline__ int lump_bin(long long an, long long gc) {
     return b + 1 >= NB - 1 ? NB : b + 1;
 }
 
-// Pass 1 over one page (four waves, a quarter page each): per (type, bin)
-// column the available units (LDS copies, then the page's row and the chunk
-// sums), and each wave's speculative list, in slot order.  NARROW: the page's
-// prios are its base plus the offsets packed into meta, so only the meta
-// column is loaded (the wide form holds the prio column as well).
+// Pass 1 over one page: per (type, bin) column the available units (LDS
+// copies, then the page's row and the chunk sums), and a speculative list per
+// quarter page, in slot order.  QW quarters per wave: 1 (four waves per page)
+// or 2 (two waves per page, two pages per workgroup: every page of the metric
+// queue resident at once, where four-wave pages ran in two rounds).  NARROW:
+// the page's prios are its base plus the offsets packed into meta, so only the
+// meta column is loaded (the wide form holds the prio column as well).
 //   LUMP (T <= 8): a unit is near when it lies above its type's lump
 //   (lump_bin), and the list is every near unit.  On a narrow page a unit is
-//   classified through an LDS table indexed by the low ten bits of its meta
-//   (status, type): {far cut in the page's offsets, counter increment}; an
-//   unavailable unit's entry {INT_MAX, 0} makes it far and uncounted.  A far
-//   unit adds to 8-bit per-type counters in a register (four types each); a
-//   near one (a few per wave when the guess holds) is staged in LDS, then
-//   binned one per lane.  Should a wave's near units overflow the list, they
-//   are binned from the registers and the list is marked unusable.  A wide
-//   page bins every unit, its far ones into the lump.
+//   classified through an LDS table indexed by its meta's status and type
+//   bits: {far cut in the page's offsets, counter increment}; an unavailable
+//   unit's entry {INT_MAX, 0} makes it far and uncounted.  A far unit adds to
+//   8-bit per-type counters in a register (four types each); a near one (a
+//   few per wave when the guess holds) is staged in LDS, then binned one per
+//   lane.  Should a quarter's near units overflow the list, they are binned
+//   from the registers and the list is marked unusable.  A wide page bins
+//   every unit, its far ones into the lump.
 //   Otherwise (T > 8) every unit is binned and the list holds the units at or
 //   above the guessed cut.
-constexpr int HIST_TAB = 1024;  // LUMP table entries (10 meta bits), 2 words each
+#ifndef ADLBQ_HIST_PPW
+#define ADLBQ_HIST_PPW 2  // pages per pass-1 workgroup at T <= 8: 1 (four waves each), 2 or 4
+#endif
+#ifndef ADLBQ_HIST_PRE2
+#define ADLBQ_HIST_PRE2 0  // pairs at T <= 4: the second quarter's loads up front too (six waves per SIMD)
+#endif
+constexpr int HIST_TAB = 32;  // LUMP table entries: status (meta bits 8-9) x type (bits 0-2), 2 words each
+__device__ __forceinline__ unsigned int tab_idx(uint32_t m) { return ((m >> 5) & 0x18u) | (m & 7u); }
+// LDS words of one page's pass-1 state: histogram copies, staged near units, table
+__host__ __device__ constexpr int hist_page_words(int C, bool lump) {
+    return HK * C + 8 * SPEC_CAP + (lump ? 2 * HIST_TAB : 0);
+}
 
-template <bool NARROW, bool LUMP, int TB>
+template <bool NARROW, bool LUMP, int TB, int QW>
 __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, const int pg, const int fill,
                                                unsigned int *__restrict__ hist /* [C][HK], stage, table */,
-                                               const uint4 *pre) {
+                                               const bool valid) {
+    static_assert(QW == 1 || ((QW == 2 || QW == 4) && LUMP), "several quarters per wave: T <= 8");
+    constexpr int NT = 256 / QW;  // threads per page
     __shared__ int sanc[ADLBQ_MAX_TYPES], scv[ADLBQ_MAX_TYPES], slb[ADLBQ_MAX_TYPES];
-    const int T = a.T, C = T * NB, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int tid = (int)threadIdx.x & (NT - 1);
+    const int T = a.T, C = T * NB, wv = tid >> 6, lane = tid & 63;
     const long long base = (long long)pg << PAGE_SHIFT;
     const uint4 *M4 = reinterpret_cast<const uint4 *>(a.meta + base);
     const int4 *P4 = reinterpret_cast<const int4 *>(a.prio + base);
-    uint4 mv[4];
-    int4 pv[NARROW ? 1 : 4];
+    // a narrow page's first quarter of meta, loaded before the table is set up;
+    // a second quarter (QW 2) at the top of its turn of the quarter loop (with
+    // every page resident, the first quarters' loads already keep HBM busy; both
+    // at once would not fit the registers of six waves per SIMD).  A wide page
+    // loads per quarter.
+    uint4 cur[4];
+    auto load_meta = [&](int w) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int idx = (w * 4 + k) * 64 + lane;
-        mv[k] = pre != nullptr ? pre[k] : idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
-        if constexpr (!NARROW) pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
-    }
+        for (int k = 0; k < 4; k++) {
+            const int idx = (w * 4 + k) * 64 + lane;
+            cur[k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    if (NARROW) load_meta(wv * QW);
+    // PRE: the next quarter's loads in flight while a quarter is counted (nxt)
+    constexpr bool PRE = QW > 1 && (QW == 4 || (ADLBQ_HIST_PRE2 && TB <= 4));
+    uint4 nxt[PRE ? 4 : 1];
+    auto load_next = [&](int w) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int idx = (w * 4 + k) * 64 + lane;
+            nxt[k] = NARROW && idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    if constexpr (PRE) load_next(wv * QW + 1);
     const int pb = NARROW ? a.pbase[pg] : 0;
     // the table path needs every offset above LOWEST (a base above it)
     const bool fast = NARROW && LUMP && pb > LOWEST;
-    unsigned int *stg = hist + HK * C + w * 2 * SPEC_CAP;  // near units: (type << 12 | slot), prio
     uint2 *tab = reinterpret_cast<uint2 *>(hist + HK * C + 8 * SPEC_CAP);
-    if ((int)threadIdx.x < 4 * T) {
-        const int t = (int)threadIdx.x % T, st = (int)threadIdx.x / T;  // status: bit 0 LIVE, bit 1 PINNED
+    if (tid < 4 * T) {
+        const int t = tid % T, st = tid / T;  // status: bit 0 LIVE, bit 1 PINNED
         const long long an = a.anchor[t], gc = a.gcut[t];
         const int lb = LUMP ? lump_bin(an, gc) : NB;
         const long long fc = lb < NB ? an - bin_lo(lb) - pb : (long long)INT_MIN;  // far: value <= fc
         const int fci = (int)std::max(std::min(fc, (long long)INT_MAX), (long long)INT_MIN);
-        if (st == 0) {
+        if (st == 0) {  // (both pages of a workgroup write the same values)
             sanc[t] = (int)an;
             slb[t] = lb;
             scv[t] = LUMP ? fci : (int)std::max(std::min(gc, (long long)INT_MAX), (long long)INT_MIN);
         }
         if (fast)
-            tab[(st << 8) | t] = st == 1 ? make_uint2((unsigned int)fci, 1u << (8 * (t & 3)))
+            tab[(st << 3) | t] = st == 1 ? make_uint2((unsigned int)fci, 1u << (8 * (t & 3)))
                                          : make_uint2((unsigned int)INT_MAX, 0u);
     }
-    if (fast && threadIdx.x == 0) tab[0] = make_uint2((unsigned int)INT_MAX, 0u);  // slots past the fill (meta 0)
-    for (int c = threadIdx.x; c < C * HK; c += blockDim.x) hist[c] = 0;
+    if (fast && tid == 0) tab[0] = make_uint2((unsigned int)INT_MAX, 0u);  // slots past the fill (meta 0)
+    for (int c = tid; c < C * HK; c += NT) hist[c] = 0;
     __syncthreads();
     if (a.kst) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        kstamp(a.kst, p, 1);
+        if (valid && tid == 0) a.kst[(long long)p * 4 + 1] = __builtin_amdgcn_s_memrealtime();
     }
     unsigned int *my = hist + (lane % HK);
-    unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
     const unsigned long long lt = lanemask_lt();
-    int sn = 0;
     if (LUMP && fast) {
-        unsigned int c0 = 0u, c1 = 0u;  // far units per type, 8 bits each: types 0-3, 4-7
+        unsigned int c0 = 0u, c1 = 0u;  // far units per type, 8 bits each: types 0-3, 4-7 (<= 32 per lane)
+#pragma unroll 1
+        for (int qq = 0; qq < QW; qq++) {
+            const int w = wv * QW + qq;
+            if constexpr (PRE) {
+                if (qq > 0) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            __builtin_amdgcn_sched_barrier(0);  // one quarter's table reads at a time (registers)
-            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-            uint2 e[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) e[q] = tab[mm[q] & 0x3ffu];
-            unsigned long long b[4];
-            bool ne[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const bool far = (int)(mm[q] >> M_OFF_SHIFT) <= (int)e[q].x;
-                ne[q] = !far;
-                if constexpr (TB <= 4) {
-                    c0 += far ? e[q].y : 0u;
-                } else {
-                    const bool hi = (mm[q] & 4u) != 0u;
-                    c0 += (far && !hi) ? e[q].y : 0u;
-                    c1 += (far && hi) ? e[q].y : 0u;
+                    for (int j = 0; j < 4; j++) cur[j] = nxt[j];
+                    if (qq + 1 < QW) load_next(w + 1);
                 }
-                b[q] = __builtin_amdgcn_ballot_w64(!far);
+            } else if (qq > 0) {
+                load_meta(w);
             }
-            if (!(b[0] | b[1] | b[2] | b[3])) continue;
-            int pos = sn + (int)mbcnt64(b[0]) + (int)mbcnt64(b[1]) + (int)mbcnt64(b[2]) + (int)mbcnt64(b[3]);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (ne[q]) {
-                    if (pos < SPEC_CAP) {
-                        stg[pos] = ((mm[q] & M_TYPE) << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
-                        stg[SPEC_CAP + pos] = (unsigned int)(pb + (int)(mm[q] >> M_OFF_SHIFT));
-                    }
-                    pos++;
-                }
-            }
-            sn += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
-        }
-        if (sn <= SPEC_CAP) {  // the staged near units: binned one per lane, listed with their columns
-            __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
-            for (int i = lane; i < sn; i += 64) {
-                const unsigned int ev = stg[i];
-                const int t = (int)(ev >> 12), pr = (int)stg[SPEC_CAP + i];
-                const int col = t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)pr);
-                atomicAdd(&my[col * HK], 1u);
-                sp[i] = ((unsigned int)col << 12) | (ev & (PAGE - 1));
-            }
-        } else {  // overflow (no usable guess): the near units binned from the registers, no list
+            // per-lane values recomputed in each turn, not hoisted out of the loop (registers)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            unsigned int *myq = hist + (ln % HK);
+            unsigned int *stg = hist + HK * C + w * 2 * SPEC_CAP;  // near units: (type << 12 | slot), prio
+            unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
+            int sn = 0;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
+                __builtin_amdgcn_sched_barrier(0);  // one sixteenth's table reads at a time (registers)
+                const uint32_t mm[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+                uint2 e[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++) asm volatile("" : "+v"(mm[q]));  // recomputed here, not kept live from above
+                for (int q = 0; q < 4; q++) e[q] = tab[tab_idx(mm[q])];
+                unsigned long long b[4];
+                bool ne[4];
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const int off = (int)(mm[q] >> M_OFF_SHIFT);
-                    if (off > (int)tab[mm[q] & 0x3ffu].x) {
-                        const int t = mm[q] & M_TYPE;
-                        atomicAdd(&my[(t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)(pb + off))) * HK], 1u);
+                    const bool far = (int)(mm[q] >> M_OFF_SHIFT) <= (int)e[q].x;
+                    ne[q] = !far;
+                    if constexpr (TB <= 4) {
+                        c0 += far ? e[q].y : 0u;
+                    } else {
+                        const bool hi = (mm[q] & 4u) != 0u;
+                        c0 += (far && !hi) ? e[q].y : 0u;
+                        c1 += (far && hi) ? e[q].y : 0u;
+                    }
+                    b[q] = __builtin_amdgcn_ballot_w64(!far);
+                }
+                asm volatile("" : "+v"(c0), "+v"(c1));  // summed here, not deferred (registers)
+                if (!(b[0] | b[1] | b[2] | b[3])) continue;
+                int pos = sn + (int)mbcnt64(b[0]) + (int)mbcnt64(b[1]) + (int)mbcnt64(b[2]) + (int)mbcnt64(b[3]);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (ne[q]) {
+                        if (pos < SPEC_CAP) {
+                            stg[pos] = ((mm[q] & M_TYPE) << 12) | (unsigned int)((w * 4 + k) * 256 + ln * 4 + q);
+                            stg[SPEC_CAP + pos] = (unsigned int)(pb + (int)(mm[q] >> M_OFF_SHIFT));
+                        }
+                        pos++;
+                    }
+                }
+                sn += __popcll(b[0]) + __popcll(b[1]) + __popcll(b[2]) + __popcll(b[3]);
+            }
+            if (sn <= SPEC_CAP) {  // the staged near units: binned one per lane, listed with their columns
+                __builtin_amdgcn_wave_barrier();  // one wave's LDS ops complete in order
+                for (int i = ln; i < sn; i += 64) {
+                    const unsigned int ev = stg[i];
+                    const int t = (int)(ev >> 12), pr = (int)stg[SPEC_CAP + i];
+                    const int col = t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)pr);
+                    atomicAdd(&myq[col * HK], 1u);
+                    sp[i] = ((unsigned int)col << 12) | (ev & (PAGE - 1));
+                }
+            } else {  // overflow (no usable guess): the near units binned from the registers, no list
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    __builtin_amdgcn_sched_barrier(0);  // a sixteenth at a time (registers)
+                    uint32_t mm[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+#pragma unroll
+                    for (int q = 0; q < 4; q++) asm volatile("" : "+v"(mm[q]));  // recomputed here, not kept live from above
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int off = (int)(mm[q] >> M_OFF_SHIFT);
+                        if (off > (int)tab[tab_idx(mm[q])].x) {
+                            const int t = mm[q] & M_TYPE;
+                            atomicAdd(&myq[(t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)(pb + off))) * HK], 1u);
+                        }
                     }
                 }
             }
+            if (valid && ln == 0) a.specn[(long long)p * 4 + w] = sn;
         }
         // the far counts: 16-bit lanes of the even and odd bytes, summed over the wave
         unsigned int f[4] = {c0 & 0x00ff00ffu, (c0 >> 8) & 0x00ff00ffu, c1 & 0x00ff00ffu, (c1 >> 8) & 0x00ff00ffu};
@@ -415,147 +468,117 @@ __device__ __forceinline__ void hist_page_body(const HistArgs &a, const int p, c
                 const unsigned int v = (f[(u >> 2) * 2 + (u & 1)] >> (16 * ((u >> 1) & 1))) & 0xffffu;
                 if (u < T && v) atomicAdd(&hist[(u * NB + NB - 1) * HK], v);
             }
-    } else if (LUMP) {  // a wide page (or a base at LOWEST): every unit binned, the far ones into the lump
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-            int pr[4];
-            if constexpr (NARROW) {
-#pragma unroll
-                for (int q = 0; q < 4; q++) pr[q] = pb + (int)(mm[q] >> M_OFF_SHIFT);
-            } else {
-                pr[0] = pv[k].x, pr[1] = pv[k].y, pr[2] = pv[k].z, pr[3] = pv[k].w;
-            }
-            int col[4];
-            bool ne[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
-                const int t = mm[q] & M_TYPE;
-                const int bq = bin_of32((unsigned int)sanc[t] - (unsigned int)pr[q]);
-                ne[q] = av && bq < slb[t];
-                col[q] = t * NB + (ne[q] ? bq : NB - 1);
-                if (av) atomicAdd(&my[col[q] * HK], 1u);
-            }
-            const unsigned long long b0 = __ballot(ne[0]), b1 = __ballot(ne[1]), b2 = __ballot(ne[2]),
-                                     b3 = __ballot(ne[3]);
-            if (!(b0 | b1 | b2 | b3)) continue;
-            int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (ne[q]) {
-                    if (pos < SPEC_CAP)
-                        sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
-                    pos++;
-                }
-            }
-            sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
-        }
     } else {
+#pragma unroll 1
+        for (int qq = 0; qq < QW; qq++) {
+            const int w = wv * QW + qq;
+            unsigned int *__restrict__ sp = a.spec + ((long long)p * 4 + w) * SPEC_CAP;
+            int sn = 0;
+            int4 pv[NARROW ? 1 : 4];
+            if constexpr (!NARROW) {
+                load_meta(w);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t mm[4] = {mv[k].x, mv[k].y, mv[k].z, mv[k].w};
-            int pr[4];
-            if constexpr (NARROW) {
+                for (int k = 0; k < 4; k++) {
+                    const int idx = (w * 4 + k) * 64 + lane;
+                    pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
+                }
+            } else if (qq > 0) {
+                if constexpr (PRE) {
 #pragma unroll
-                for (int q = 0; q < 4; q++) pr[q] = pb + (int)(mm[q] >> M_OFF_SHIFT);
-            } else {
-                pr[0] = pv[k].x, pr[1] = pv[k].y, pr[2] = pv[k].z, pr[3] = pv[k].w;
-            }
-            int col[4];
-            bool in[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
-                const int t = mm[q] & M_TYPE;
-                col[q] = t * NB + bin_of32((unsigned int)sanc[t] - (unsigned int)pr[q]);  // distance < 2^32
-                in[q] = av && pr[q] >= scv[t];
-                if (av) atomicAdd(&my[col[q] * HK], 1u);
-            }
-            const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
-                                     b3 = __ballot(in[3]);
-            if (!(b0 | b1 | b2 | b3)) continue;
-            int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (in[q]) {
-                    if (pos < SPEC_CAP)
-                        sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
-                    pos++;
+                    for (int j = 0; j < 4; j++) cur[j] = nxt[j];
+                    if (qq + 1 < QW) load_next(w + 1);
+                } else {
+                    load_meta(w);
                 }
             }
-            sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t mm[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+                int pr[4];
+                if constexpr (NARROW) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) pr[q] = pb + (int)(mm[q] >> M_OFF_SHIFT);
+                } else {
+                    pr[0] = pv[k].x, pr[1] = pv[k].y, pr[2] = pv[k].z, pr[3] = pv[k].w;
+                }
+                int col[4];
+                bool in[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const bool av = (mm[q] & (M_LIVE | M_PINNED)) == M_LIVE && pr[q] > LOWEST;
+                    const int t = mm[q] & M_TYPE;
+                    const int bq = bin_of32((unsigned int)sanc[t] - (unsigned int)pr[q]);  // distance < 2^32
+                    if constexpr (LUMP) {  // a wide page (or a base at LOWEST): the far ones into the lump
+                        in[q] = av && bq < slb[t];
+                        col[q] = t * NB + (in[q] ? bq : NB - 1);
+                    } else {
+                        in[q] = av && pr[q] >= scv[t];
+                        col[q] = t * NB + bq;
+                    }
+                    if (av) atomicAdd(&my[col[q] * HK], 1u);
+                }
+                const unsigned long long b0 = __ballot(in[0]), b1 = __ballot(in[1]), b2 = __ballot(in[2]),
+                                         b3 = __ballot(in[3]);
+                if (!(b0 | b1 | b2 | b3)) continue;
+                int pos = sn + __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (in[q]) {
+                        if (pos < SPEC_CAP)
+                            sp[pos] = ((unsigned int)col[q] << 12) | (unsigned int)((w * 4 + k) * 256 + lane * 4 + q);
+                        pos++;
+                    }
+                }
+                sn += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+            }
+            if (valid && lane == 0) a.specn[(long long)p * 4 + w] = sn;
         }
     }
-    if (lane == 0) a.specn[(long long)p * 4 + w] = sn;
     __syncthreads();
-    kstamp(a.kst, p, 2);
-    unsigned int *cs = a.csum + (long long)(p / CHUNK) * C;
-    unsigned short *g = a.gh + (long long)p * C;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        unsigned int v = 0;
+    if (valid && a.kst && tid == 0) a.kst[(long long)p * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+    if (valid) {
+        unsigned int *cs = a.csum + (long long)(p / CHUNK) * C;
+        unsigned short *g = a.gh + (long long)p * C;
+        for (int c = tid; c < C; c += NT) {
+            unsigned int v = 0;
 #pragma unroll
-        for (int k = 0; k < HK; k++) v += hist[c * HK + k];
-        g[c] = (unsigned short)v;
-        if (v) atomicAdd(&cs[c], v);
+            for (int k = 0; k < HK; k++) v += hist[c * HK + k];
+            g[c] = (unsigned short)v;
+            if (v) atomicAdd(&cs[c], v);
+        }
     }
     if (a.kst) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        kstamp(a.kst, p, 3);
+        if (valid && tid == 0) a.kst[(long long)p * 4 + 3] = __builtin_amdgcn_s_memrealtime();
     }
 }
 
-template <int TB>
-__device__ __forceinline__ void hist_page(const HistArgs &a, const int p, unsigned int *__restrict__ hist,
-                                          const uint4 *pre) {
-    const int pg = a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
-    const int fill = (p == a.npages - 1) ? a.tail_fill : PAGE;
-    kstamp(a.kst, p, 0);
-    if (a.pwide[pg]) hist_page_body<false, (TB <= 8), TB>(a, p, pg, fill, hist, pre);
-    else hist_page_body<true, (TB <= 8), TB>(a, p, pg, fill, hist, pre);
-}
-
-// HIST_PP pages per pass-1 workgroup: the later pages' meta loads are issued
-// before the first page is counted and arrive while it is.  Measured at the
-// metric size (r05): 2 pages per workgroup 22.5 us against 19.5 for one (the
-// workgroups' start ramp stretches under the heavier load flood), so one.
-#ifndef ADLBQ_HIST_PP
-#define ADLBQ_HIST_PP 1
-#endif
-// (T <= 8, the table path; a larger T bins every unit and keeps one page per workgroup)
-__host__ __device__ constexpr int hist_pp(int TB) { return TB <= 8 ? ADLBQ_HIST_PP : 1; }
+// Pass 1's shape for T <= TB: two pages per workgroup (two waves each) for
+// T <= 8 (ADLBQ_HIST_PPW); otherwise one page (four waves).
+__host__ __device__ constexpr int hist_pp(int TB) { return TB <= 8 ? ADLBQ_HIST_PPW : 1; }
+// minimum waves per SIMD k_prep_hist is compiled for: for the pairs eight at
+// T <= 4 (<= 64 VGPRs), six at T <= 8 (<= 80), so that 2,442 pages and the
+// request preparation fit at once
 #ifndef ADLBQ_HIST_WAVES
-#define ADLBQ_HIST_WAVES 6  // waves per SIMD k_prep_hist<4> is compiled for (<= 80 VGPRs, no spill)
+#define ADLBQ_HIST_WAVES 8
 #endif
 __host__ __device__ constexpr int hist_waves(int TB) {
-    return ADLBQ_HIST_PP == 1 ? 1 : TB <= 4 ? ADLBQ_HIST_WAVES : TB <= 8 ? 5 : 1;
+    return hist_pp(TB) == 1 ? 1 : hist_pp(TB) == 4 ? 4 : TB <= 4 && !ADLBQ_HIST_PRE2 ? ADLBQ_HIST_WAVES : 6;
 }
 
 template <int TB>
 __device__ __forceinline__ void hist_pages(const HistArgs &a, const int q, unsigned int *__restrict__ hist) {
-    constexpr int HIST_PP = hist_pp(TB);
-    const int p0 = q * HIST_PP, w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint4 nb[HIST_PP > 1 ? HIST_PP - 1 : 1][4];
-#pragma unroll
-    for (int i = 1; i < HIST_PP; i++) {
-        const int p = p0 + i;
-        const bool ok = p < a.npages;
-        const int pg = !ok ? 0 : a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
-        const int fill = !ok ? 0 : (p == a.npages - 1) ? a.tail_fill : PAGE;
-        const uint4 *M4 = reinterpret_cast<const uint4 *>(a.meta + ((long long)pg << PAGE_SHIFT));
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int idx = (w * 4 + k) * 64 + lane;
-            nb[i - 1][k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
-        }
-    }
-    hist_page<TB>(a, p0, hist, nullptr);
-#pragma unroll
-    for (int i = 1; i < HIST_PP; i++) {
-        if (p0 + i >= a.npages) break;
-        __syncthreads();  // the previous page's histogram is read out
-        hist_page<TB>(a, p0 + i, hist, nb[i - 1]);
-    }
+    constexpr int PP = hist_pp(TB);
+    const int half = (int)threadIdx.x / (256 / PP);  // the workgroup's page
+    const int p = q * PP + half;
+    const bool valid = p < a.npages;  // the last workgroup's second page may not exist (it still takes the barriers)
+    const int pv = valid ? p : a.npages - 1;
+    const int pg = a.pg0 >= 0 ? a.pg0 + pv : a.pages[pv];
+    const int fill = !valid ? 0 : (p == a.npages - 1) ? a.tail_fill : PAGE;
+    unsigned int *h = hist + half * hist_page_words(a.T * NB, TB <= 8);
+    if (valid && a.kst && (threadIdx.x & (256 / PP - 1)) == 0) a.kst[(long long)p * 4] = __builtin_amdgcn_s_memrealtime();
+    if (a.pwide[pg]) hist_page_body<false, (TB <= 8), TB, PP>(a, p, pg, fill, h, valid);
+    else hist_page_body<true, (TB <= 8), TB, PP>(a, p, pg, fill, h, valid);
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
@@ -1017,6 +1040,9 @@ __device__ __forceinline__ void select_open_body(
 // metric size against ~4,000 such workgroups), where k_select_open's
 // four-wave workgroups ran in two rounds (82 VGPRs, 20 KB of LDS each).
 // Results as k_select_open's.
+#ifndef ADLBQ_SELW_LAZY
+#define ADLBQ_SELW_LAZY 1  // k_select_wave reads a list's second 64 entries only when it has them
+#endif
 #ifndef ADLBQ_SELW_GATE
 #define ADLBQ_SELW_GATE 1  // k_select_wave reads a column's page prefix only at or below its threshold
 #endif
@@ -1059,9 +1085,7 @@ __global__ __launch_bounds__(64) void k_select_wave(
     }
     unsigned int se[4][SPEC_CAP / 64];
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int k = 0; k < SPEC_CAP / 64; k++) se[q][k] = spec[((long long)p * 4 + q) * SPEC_CAP + k * 64 + lane];
+    for (int q = 0; q < 4; q++) se[q][0] = spec[((long long)p * 4 + q) * SPEC_CAP + lane];
     const long long cut_l = cut_of(th_l, an_l);
     const int lb_l = tl ? lump_bin(an_l, gc_l) : NB;
     const bool lists_ok = __ballot(th_l >= 0 && th_l >= lb_l) == 0;  // no threshold in a lump
@@ -1086,6 +1110,13 @@ __global__ __launch_bounds__(64) void k_select_wave(
             ppv[r] = use ? v : 0u;
         }
     }
+    // the lists' further entries: read when the list is that long (rarely; a list is
+    // typically a few dozen entries at the metric size)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int k = 1; k < SPEC_CAP / 64; k++)
+            se[q][k] = (!ADLBQ_SELW_LAZY || sn[q] > k * 64) ? spec[((long long)p * 4 + q) * SPEC_CAP + k * 64 + lane] : 0u;
     if (tl) {
         sanc[lane] = an_l;
         sth[lane] = th_l;
@@ -3526,7 +3557,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     if (grid > 0) {
         // pass 1: the histogram copies, then the four waves' speculative lists
         const int lds = (int)std::max(nprep > 0 ? (size_t)PREP_LDS : 0,
-                                      scan ? sizeof(unsigned int) * (HK * C + 8 * SPEC_CAP + (T <= 8 ? 2 * HIST_TAB : 0)) : 0);
+                                      scan ? sizeof(unsigned int) * pp * hist_page_words(C, T <= 8) : 0);
         stage_begin(h, "hist", &ev);
         auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
         if (h->split_prep && nprep > 0 && scan) {  // diagnostic: the two roles as two launches
