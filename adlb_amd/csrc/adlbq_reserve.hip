@@ -656,13 +656,19 @@ __device__ void type_threshold(const int t, const int *__restrict__ dem, int *th
 }
 
 // ---------------------------------------------------------------- thresholds
-// One workgroup per (type, bin) column: block scan of the column's chunk sums
-// (exclusive prefix in place, read by k_select_open) and its total.  The
-// column that arrives last for its type (agent-scope counter; totals published
-// write-through and read back the same way) finds the bin where the type's
-// demand is reached and how many units of it are needed.  Candidate list
-// offsets (the prefix of candlen over types) follow in k_select_open.
-constexpr int TH_THREADS = 256;  // chunks per step of the column scan
+// One workgroup per (row tile, type): TH_ROWS chunk rows of the type's NB
+// columns (lane = column, four waves of 16 rows; every load a 256-byte row
+// segment).  The tile's exclusive prefix goes back into the chunk sums in
+// place, its column totals to the tile area after them (csum + nchunks * C,
+// [nrt][C], agent-scope stores).  The tile of a type that arrives last (one
+// counter per type) turns the tile totals into their exclusive prefix in place
+// (k_select_open / k_select_wave add it), writes the column totals, and finds
+// the bin where the type's demand is reached and how many units of it are
+// needed.  Candidate list offsets (the prefix of candlen over types) follow in
+// pass 2.
+constexpr int TH_THREADS = 256;
+constexpr int TH_ROWS = 64;  // chunk rows per tile (16 per wave)
+__host__ __device__ constexpr int th_tiles(int nchunks) { return (nchunks + TH_ROWS - 1) / TH_ROWS; }
 __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn, int T, const int *__restrict__ dem, unsigned int *csum,
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
@@ -670,47 +676,37 @@ __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn,
                                                      long long *__restrict__ anchor_next,
                                                      long long *__restrict__ gcut_next, int guess,
                                                      const long long *__restrict__ gcut, const int bid_, const int nbk_) {
-    constexpr int NW = TH_THREADS / 64;
-    __shared__ unsigned int wsum[NW];
+    static_assert(NB == 64 && TH_THREADS == 256 && TH_ROWS == 64, "lane = column, four waves of 16 rows");
+    __shared__ unsigned int wsum[4][64];
     __shared__ bool s_last;
-    const int c = bid_, t = c / NB, C = T * NB, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    unsigned int carry = 0;
-    // the first TH_PRE rows' loads all in flight before the first scan step
-    constexpr int TH_PRE = 4;
-    unsigned int pre_v[TH_PRE];
+    const int nrt = th_tiles(nchunks), C = T * NB;
+    const int rt = bid_ % nrt, t = bid_ / nrt, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = t * NB + lane;
+    unsigned int *tile = csum + (long long)nchunks * C;
+    const int r0 = rt * TH_ROWS + w * 16;
+    unsigned int v[16];
 #pragma unroll
-    for (int q = 0; q < TH_PRE; q++) {
-        const int k = q * TH_THREADS + threadIdx.x;
-        pre_v[q] = k < nchunks ? csum[(long long)k * C + c] : 0u;
+    for (int i = 0; i < 16; i++) v[i] = r0 + i < nchunks ? csum[(long long)(r0 + i) * C + c] : 0u;
+    unsigned int run = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) run += v[i];
+    wsum[w][lane] = run;
+    __syncthreads();
+    unsigned int x = 0;
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+        if (q < w) x += wsum[q][lane];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        if (r0 + i < nchunks) csum[(long long)(r0 + i) * C + c] = x;
+        x += v[i];
     }
-    for (int k0 = 0; k0 < nchunks; k0 += TH_THREADS) {
-        const int k = k0 + threadIdx.x;
-        const int q0 = k0 / TH_THREADS;
-        unsigned int v = 0u;
-#pragma unroll
-        for (int q = 0; q < TH_PRE; q++)
-            if (q == q0) v = pre_v[q];
-        if (q0 >= TH_PRE) v = k < nchunks ? csum[(long long)k * C + c] : 0u;
-        unsigned int x = v;  // block inclusive scan
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const unsigned int y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[w] = x;
-        __syncthreads();
-        unsigned int pre = carry;
-        for (int q = 0; q < w; q++) pre += wsum[q];
-        if (k < nchunks) csum[(long long)k * C + c] = pre + x - v;
-#pragma unroll
-        for (int q = 0; q < NW; q++) carry += wsum[q];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(coltot + c, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w == 3) {  // x: the tile's column total
+        __hip_atomic_store(tile + (long long)rt * C + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = atomicAdd(&type_cnt[t], 1) == NB - 1;
     }
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&type_cnt[t], 1) == nrt - 1;
     // the previous scan's chunk sums (consumed): zeroed for the scan after this one, a slice per workgroup
     if (zn > 0) {
         const long long per = (zn + nbk_ - 1) / nbk_, z0 = (long long)bid_ * per;
@@ -718,6 +714,21 @@ __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn,
     }
     __syncthreads();
     if (!s_last || threadIdx.x >= 64) return;
+    unsigned int tot = 0;
+    for (int r0 = 0; r0 < nrt; r0 += 8) {  // eight tiles' loads in flight at a time
+        unsigned int y[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            y[i] = r0 + i < nrt ? __hip_atomic_load(tile + (long long)(r0 + i) * C + c, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                : 0u;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            if (r0 + i < nrt) tile[(long long)(r0 + i) * C + c] = tot;  // exclusive prefix over the tiles, read by pass 2
+            tot += y[i];
+        }
+    }
+    __hip_atomic_store(coltot + c, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     type_threshold(t, dem, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next,
                    guess, gcut, T);
 }
@@ -834,7 +845,8 @@ __device__ __forceinline__ void select_open_body(
         if (r * 256 >= C) break;
         const int thc = __shfl(th_l, (c / NB) & 63, 64);
         if (c < C && (c % NB) <= thc) {
-            unsigned int v = csum[(long long)(p / CHUNK) * C + c];
+            const int nch = (npages + CHUNK - 1) / CHUNK;  // the tile prefixes follow the chunk sums
+            unsigned int v = csum[(long long)(p / CHUNK) * C + c] + csum[(long long)(nch + p / CHUNK / TH_ROWS) * C + c];
             unsigned short g[CHUNK - 1];
 #pragma unroll
             for (int q = 0; q < CHUNK - 1; q++) g[q] = p0 + q < p ? gh[(long long)(p0 + q) * C + c] : (unsigned short)0;
@@ -1101,7 +1113,8 @@ __global__ __launch_bounds__(64) void k_select_wave(
         const int thc = __shfl(th_l, (c / NB) & 63, 64);
         const bool use = c < C && (c % NB) <= thc;
         if (ADLBQ_SELW_GATE ? use : c < C) {  // ungated: the loads need not wait for theta
-            unsigned int v = csum[(long long)(p / CHUNK) * C + c];
+            const int nch = (npages + CHUNK - 1) / CHUNK;  // the tile prefixes follow the chunk sums
+            unsigned int v = csum[(long long)(p / CHUNK) * C + c] + csum[(long long)(nch + p / CHUNK / TH_ROWS) * C + c];
             unsigned short g[CHUNK - 1];
 #pragma unroll
             for (int q = 0; q < CHUNK - 1; q++) g[q] = p0 + q < p ? gh[(long long)(p0 + q) * C + c] : (unsigned short)0;
@@ -3490,7 +3503,8 @@ static unsigned long long *kst_for(adlbq_server *h, int n, int which) {
 static int ensure_scan_capacity(adlbq_server *h, int npages) {
     const long long C = (long long)std::max(h->T, 1) * NB;
     const long long need_gh = (long long)npages * C, nchunks = (npages + CHUNK - 1) / CHUNK;
-    const long long need_cs = std::max(1ll, nchunks) * C, need_cand = (long long)npages * PAGE;
+    const long long need_cs = (std::max(1ll, nchunks) + th_tiles((int)std::max(1ll, nchunks))) * C,
+                    need_cand = (long long)npages * PAGE;
     if (need_gh > h->cap_gh || need_cs > h->cap_csum || need_cand > h->cap_cand || (long long)npages * 4 > h->cap_spec)
         AQ_HIP(hipStreamSynchronize(h->stream));
     if (need_gh > h->cap_gh) {
@@ -3548,7 +3562,8 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                 h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, zcs, h->csum_used[par ^ 1], pg0};
     ha.kst = kst_for(h, np, 0);
     if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
-        h->csum_used[par] = (long long)((np + CHUNK - 1) / CHUNK) * C;
+        const int nch = (np + CHUNK - 1) / CHUNK;
+        h->csum_used[par] = (long long)(nch + th_tiles(nch)) * C;  // the chunk sums and the tile area
         h->csum_used[par ^ 1] = 0;
         h->csum_par = par ^ 1;
     }
@@ -3579,10 +3594,10 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             h->grec->kinds |= GK_THR;
             h->grec->thr = GThr{zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen,
                                 h->d_needsort, h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor, h->d_anchor_next,
-                                h->d_gcut_next, nprep > 0 ? 1 : 0, C, h->d_gcut};
+                                h->d_gcut_next, nprep > 0 ? 1 : 0, th_tiles(nchunks) * T, h->d_gcut};
         } else {
             stage_begin(h, "thresholds", &ev);
-            k_thresholds<<<C, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need,
+            k_thresholds<<<th_tiles(nchunks) * T, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need,
                                                   h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot,
                                                   h->d_type_cnt, h->d_anchor, h->d_anchor_next, h->d_gcut_next,
                                                   nprep > 0 ? 1 : 0, h->d_gcut);
