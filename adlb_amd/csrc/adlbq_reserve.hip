@@ -3068,12 +3068,12 @@ __device__ __forceinline__ bool fin_failed(const FinArgs &f) {
     return __hip_atomic_load(f.sortfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
 
-// Request j (j < R): pin its unit and write its response; true when it parks
-// (words [10], [11] are then left to the park tail).
-__device__ __forceinline__ bool fin_request(const FinArgs &f, int j, bool failed) {
-    const int2 rk = f.rh[j];
+// Request j (j < R): pin its unit and write its response (rk, tm, um: its
+// rh, tmatch and umatch entries, loaded by finalize_body).  A request that
+// parks (no unit, hang) leaves words [10], [11] to the park tail.  Every
+// writer of umatch gives a unit (cslot) with it: um >= 0 means slot >= 0.
+__device__ __forceinline__ void fin_request(const FinArgs &f, int j, bool failed, int2 rk, int tm, int um) {
     const int rank = rk.x, hang = failed ? 0 : rk.y;
-    const int tm = f.tmatch[j], um = f.umatch[j];
     const int slot = failed ? -1 : tm >= 0 ? tm : (um >= 0 ? f.cslot[um] : -1);
     f.mslot[j] = slot;
     int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
@@ -3104,7 +3104,6 @@ __device__ __forceinline__ bool fin_request(const FinArgs &f, int j, bool failed
         out[10] = -1;
         out[11] = -1;
     }
-    return parks;
 }
 
 // Two-level arrival of workgroup bid of nb (8 groups, then one top counter)
@@ -3175,15 +3174,26 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
     }
 }
 
+// Which requests park is known from tmatch / umatch alone: the park mask is
+// published and the workgroup arrives first, then the units are pinned and the
+// responses written (their loads and stores overlap the arrival, and the last
+// workgroup's tail -- which reads only the park mask -- overlaps theirs).
 __device__ __forceinline__ void finalize_body(FinArgs f, const int bid_, const int nbk_) {
     __shared__ int s_parked;
     __shared__ unsigned long long s_ticket;
     const int j = bid_ * blockDim.x + threadIdx.x;
     if (threadIdx.x == 0) s_parked = 0;
     const bool failed = fin_failed(f);
+    int2 rk = make_int2(-1, 0);
+    int tm = -1, um = -1;
+    if (j < f.R) {
+        rk = f.rh[j];
+        tm = f.tmatch[j];
+        um = f.umatch[j];
+    }
     __syncthreads();
     if (j < f.R) {
-        const bool parks = fin_request(f, j, failed);
+        const bool parks = !failed && rk.y && tm < 0 && um < 0;
         const unsigned long long pb = __ballot(parks);
         if ((threadIdx.x & 63) == 0) {
             // published for the last workgroup's park (write-through, drained before the arrival below)
@@ -3194,6 +3204,7 @@ __device__ __forceinline__ void finalize_body(FinArgs f, const int bid_, const i
     }
     __syncthreads();
     if (threadIdx.x == 0) s_ticket = fin_arrive(f, s_parked, nbk_, bid_);
+    if (j < f.R) fin_request(f, j, failed, rk, tm, um);
     __syncthreads();
     if (!(s_ticket & 1ull)) return;
     fin_tail(f, (int)(s_ticket >> 32), failed);
