@@ -134,7 +134,7 @@ def parse():
 
 # stage (adlbq_profile_read name) -> kernel symbol of that launch
 KERNEL_OF = {"hist": "k_prep_hist", "thresholds": "k_thresholds",
-             "select": "k_select_open", "sort": "k_keybits + merged hipcub radix sort",
+             "select": "k_select_wave", "sort": "k_keybits + merged hipcub radix sort",
              "targeted": "k_targeted_idx", "rank": "k_rank", "chain": "k_chain0", "finalize": "k_finalize"}
 
 
@@ -188,9 +188,12 @@ def pmc_traffic(args) -> dict | None:
 def traffic_of(pmc, stage):
     if not pmc:
         return None
-    want = KERNEL_OF[stage]
-    hits = [v for k, v in pmc.items() if k == want or k.startswith(want + "_small<") or k.startswith(want + "<")]
-    return round(hits[0]) if len(hits) == 1 else None
+    # the select stage is k_select_wave (T <= 8), else k_select_open
+    for want in (KERNEL_OF[stage], "k_select_open") if stage == "select" else (KERNEL_OF[stage],):
+        hits = [v for k, v in pmc.items() if k == want or k.startswith(want + "_small<") or k.startswith(want + "<")]
+        if len(hits) == 1:
+            return round(hits[0])
+    return None
 
 
 def _exact_check():
@@ -1119,7 +1122,7 @@ def main():
                    "units_per_shard": N, "reserves_per_step": R, "parallelism": f"shards{world}"},
         "roofline": roofline,
         "roofline_scan": roof(alg["scan"], scan_ms, sum(scan_tr) if scan_tr and None not in scan_tr else None,
-                              "k_prep_hist + k_select_open (time includes the request preparation)") if scan_ms else None,
+                              "k_prep_hist + k_select_wave (time includes the request preparation)") if scan_ms else None,
         "roofline_batch": roof(alg["batch"], batch_ms, None, "all reserve-batch kernels"),
         "kernels_ms": kernels,
         "chain_last_batch": {k: srv.stat("chain_" + k) for k in ("rounds", "passes", "recomputed", "fallback",
