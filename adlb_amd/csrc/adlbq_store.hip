@@ -2637,6 +2637,22 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     if (n == "chain_recomputed") return h->ctr.chain_recomputed;
     if (n == "chain_fallback") return h->ctr.chain_fallback;
     if (n == "chain_timeouts") return h->ctr.chain_timeouts;
+    if ((n == "chain_start_spread" || n == "chain_end_abs") && h->d_stamps && h->n_stamps > 0) {
+        // diagnostic, ns: the spread of the segments' first stamps, and the latest stamp of any
+        // segment after the earliest first stamp
+        std::vector<unsigned long long> st(8 * (size_t)h->n_stamps);
+        if (hipMemcpy(st.data(), h->d_stamps, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+        unsigned long long lo = ~0ull, hi0 = 0, hi = 0;
+        for (int q = 0; q < h->n_stamps; q++) {
+            if (!st[8 * q]) continue;
+            lo = std::min(lo, st[8 * q]);
+            hi0 = std::max(hi0, st[8 * q]);
+            for (int k = 1; k < 8; k++) hi = std::max(hi, st[8 * q + k]);
+        }
+        if (lo == ~0ull) return 0;
+        return (long long)((n == "chain_start_spread" ? hi0 : hi) - lo) * 10;
+    }
     if (n.rfind("chain_phase", 0) == 0 && h->d_stamps && h->n_stamps > 0) {
         // diagnostic: "chain_phaseK" = median over segments of (stamp K - stamp 0)
         // in ns; "chain_phaseK_max" = the largest; K = 1..7 (0 where unstamped)

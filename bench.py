@@ -52,8 +52,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process unless set (0: HIP's default)")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--units", type=int, default=10_000_000)
     ap.add_argument("--reserves", type=int, default=65_536)
     ap.add_argument("--types", type=int, default=4)
@@ -64,7 +64,7 @@ def parse():
                     help="CPU baseline processes (the GPU box's CPU share is 16 per GPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-stage HIP event timing")
-    ap.add_argument("--profile-every", type=int, default=4,
+    ap.add_argument("--profile-every", type=int, default=10,
                     help="timed region: HIP events around the dominant kernel on every n-th batch")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-config3", action="store_true", help="skip the config-3 steal-round measurement")
@@ -1058,6 +1058,8 @@ def main():
         torch.cuda.synchronize()
         phases = {f"phase{k}": (srv.stat(f"chain_phase{k}"), srv.stat(f"chain_phase{k}_max")) for k in range(1, 8)}
         phases["clock_mhz_pass1"] = srv.stat("chain_phase2_mhz")
+        phases["start_spread"] = srv.stat("chain_start_spread")
+        phases["end_abs"] = srv.stat("chain_end_abs")
         srv.set_param("chain_stamps", 0)
     if args.kernel_stamps:
         # diagnostic: per-workgroup phase stamps of pass 1 (hist) and pass 2 (select) of one batch
