@@ -2724,7 +2724,12 @@ __device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, i
     const int my_off = lane <= T ? ld_sc1(a.candoff + lane) : 0, my_len = lane < T ? ld_sc1(a.candlen + lane) : 0;
     // ---- walk: every segment before the first inconsistent one (start !=
     // predecessor's end) is exact; from there on, in order, re-solve each
-    // segment whose start differs from the running exact start
+    // segment whose start differs from its exact start.  Only the inconsistent
+    // segments and the successors of re-solved ones can differ: a consistent
+    // segment after an exact one is exact (its start is that one's end).  So the
+    // walk finds the inconsistent segments 64 at a time (lane = segment) and
+    // visits those, plus the successor of a re-solve whose new end differs from
+    // the successor's start, instead of stepping through every segment.
     int redo = 0, rounds_w = 0;
     int first = nseg;
     for (int c0 = 0; c0 < nseg && first == nseg; c0 += 64) {
@@ -2737,29 +2742,36 @@ __device__ __forceinline__ bool chain_arrive(const ChainArgs a, int s, int sv, i
         const unsigned long long bb = __ballot(bad);
         if (bb) first = c0 + __ffsll((long long)bb) - 1;
     }
-    if (first < nseg) {
-        int st = (lane < T && first > 0) ? ld_sc1(a.S + (first - 1) * T + lane) + ld_sc1(a.D + (first - 1) * T + lane)
-                                         : 0;
-        constexpr int AHEAD = 8;  // S and D of the next segments in flight
-        for (int q0 = first; q0 < nseg; q0 += AHEAD) {
-            int sq[AHEAD], dq[AHEAD];
-#pragma unroll
-            for (int i = 0; i < AHEAD; i++) {
-                const bool ok = lane < T && q0 + i < nseg;
-                sq[i] = ok ? ld_sc1(a.S + (q0 + i) * T + lane) : 0;
-                dq[i] = ok ? ld_sc1(a.D + (q0 + i) * T + lane) : 0;
-            }
-#pragma unroll
-            for (int i = 0; i < AHEAD; i++) {
-                const int q = q0 + i;
-                if (q >= nseg) break;
-                if (__ballot(lane < T && sq[i] != st)) {
-                    int rec;
-                    __builtin_amdgcn_wave_barrier();  // win is refilled
-                    st = seg_solve<TB>(a, q, q * SEG, st, win, true, true, 0, my_off, my_len, rec, rounds_w);
-                    redo++;
-                } else {
-                    st += dq[i];
+    int last_redo = -2, new_end = 0, carry = 0;
+    for (int c0 = first & ~63; c0 < nseg; c0 += 64) {
+        const int q = c0 + lane;
+        bool bad = false;
+        if (q < nseg && q > 0 && q >= first)
+            for (int t = 0; t < T; t++)
+                bad |= ld_sc1(a.S + q * T + t) != ld_sc1(a.S + (q - 1) * T + t) + ld_sc1(a.D + (q - 1) * T + t);
+        unsigned long long bm = __ballot(bad) | (unsigned long long)carry;
+        carry = 0;
+        while (bm) {
+            const int i = __ffsll((long long)bm) - 1;
+            bm &= bm - 1;
+            const int qq = c0 + i;
+            // the exact start: the re-solved predecessor's new end, else its recorded end
+            const int st = lane >= T || qq == 0 ? 0
+                           : last_redo == qq - 1
+                               ? new_end
+                               : ld_sc1(a.S + (qq - 1) * T + lane) + ld_sc1(a.D + (qq - 1) * T + lane);
+            const int sq = lane < T ? ld_sc1(a.S + qq * T + lane) : 0;
+            if (!__ballot(lane < T && sq != st)) continue;
+            int rec;
+            __builtin_amdgcn_wave_barrier();  // win is refilled
+            new_end = seg_solve<TB>(a, qq, qq * SEG, st, win, true, true, 0, my_off, my_len, rec, rounds_w);
+            last_redo = qq;
+            redo++;
+            if (qq + 1 < nseg) {  // the successor, if it started elsewhere
+                const int s1 = lane < T ? ld_sc1(a.S + (qq + 1) * T + lane) : 0;
+                if (__ballot(lane < T && s1 != new_end)) {
+                    if (i < 63) bm |= 1ull << (i + 1);
+                    else carry = 1;
                 }
             }
         }
