@@ -323,6 +323,8 @@ struct adlbq_server {
     int *h_pdead = nullptr; long long cap_pdead = 0; int pdead_np = 0; bool pdead_pending = false;
     hipEvent_t pdead_ev = nullptr; long long pdead_last = -1000000, pages_recycled = 0;
     int recycle_pages = 1;             // "recycle_pages": 0 = keep every page (the old behaviour)
+    int reserve_one = 1;               // "reserve_one": a one-Reserve batch on a large open bucket in one launch
+    unsigned long long *d_onepart = nullptr; int cap_onepart = 0; long long one_batches = 0;
     int select_wave = 1;               // "select_wave": pass 2 with one wave per page (T <= 8); 0 = four
     int rq_compact_calls = 0; long long rq_compactions = 0;  // background rq compaction (maybe_compact_rq)
     int small_pages = 4;               // "small_pages": an open bucket of at most this many pages and a batch of
@@ -410,6 +412,7 @@ int recycle_launch(adlbq_server *h);       // look for dead open pages in the ba
 void maybe_compact_rq(adlbq_server *h);    // compact a thinned-out rq in the background
 int ensure_zc(adlbq_server *h, long long n);  // mapped pinned staging of >= n ints (h_zc / d_zc)
 int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
+bool wait_last_snapshot(adlbq_server *h);  // spin until the last batch's snapshot lands (no HIP call)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)

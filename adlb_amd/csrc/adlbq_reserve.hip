@@ -3226,6 +3226,147 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
     finalize_body(f, blockIdx.x, gridDim.x);
 }
 
+// ---------------------------------------------------------------- one Reserve against a large open bucket
+// A batch of one Reserve (T <= 8, no targeted units, an open bucket too large
+// for k_reserve_small) in one launch instead of the seven of the pipeline.
+// Every workgroup takes two pages (256 threads, 32 units each, all loads in
+// flight) and finds each type's best available unit by (prio desc, bucket
+// position asc) -- wq_find_hi_prio's order (xq.c:190-217), the pipeline's key;
+// the per-type minima go out write-through and the workgroup arrives.  The
+// last workgroup prepares the request (prep_block), takes the best head among
+// its types, and finalizes it as k_finalize would (pin, response, park,
+// counters, snapshot).
+struct OneArgs {
+    PrepArgs pa;
+    const int *pages; int npages, tail_fill;
+    const int *prio; const uint32_t *meta; const int *pbase, *pwide;
+    int T;
+    unsigned long long *part;  // [grid][8] per-type minima
+    int *arrive;               // [9] arrival counters: eight groups, then the top (the last workgroup resets them)
+    int *umatch, *cslot;
+    FinArgs f;
+};
+template <int TB>
+__global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
+    static_assert(TB <= 8, "T <= 8");
+    __shared__ unsigned long long smin[4][8];
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    unsigned long long kmin[TB];
+#pragma unroll
+    for (int u = 0; u < TB; u++) kmin[u] = ~0ull;
+    {
+        // groups of 4 units: this workgroup's two pages hold 2 x 1024; thread tid takes g = tid + 256 i
+        uint4 mv[8];
+        int4 pv[8];
+        int pb[2], wide[2], pg[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int p = 2 * blockIdx.x + h;
+            pg[h] = p < a.npages ? a.pages[p] : -1;
+            pb[h] = pg[h] >= 0 ? a.pbase[pg[h]] : 0;
+            wide[h] = pg[h] >= 0 ? a.pwide[pg[h]] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
+            const int fill = p == a.npages - 1 ? a.tail_fill : PAGE;
+            const bool ok = pg[h] >= 0 && gi * 4 < fill;
+            const long long base = (long long)(ok ? pg[h] : 0) << PAGE_SHIFT;
+            mv[i] = ok ? reinterpret_cast<const uint4 *>(a.meta + base)[gi] : make_uint4(0, 0, 0, 0);
+            pv[i] = ok && wide[h] ? reinterpret_cast<const int4 *>(a.prio + base)[gi] : make_int4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
+            const uint32_t mm[4] = {mv[i].x, mv[i].y, mv[i].z, mv[i].w};
+            const int pw[4] = {pv[i].x, pv[i].y, pv[i].z, pv[i].w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int pr = wide[h] ? pw[q] : pb[h] + (int)(mm[q] >> M_OFF_SHIFT);
+                if ((mm[q] & (M_LIVE | M_PINNED)) != M_LIVE || pr <= LOWEST) continue;
+                const int t = (int)(mm[q] & M_TYPE);
+                const unsigned long long key = ((unsigned long long)(~((unsigned int)pr ^ 0x80000000u)) << 32) |
+                                               ((unsigned long long)(unsigned int)p << PAGE_SHIFT) |
+                                               (unsigned long long)(gi * 4 + q);
+#pragma unroll
+                for (int u = 0; u < TB; u++)
+                    if (t == u) kmin[u] = min(kmin[u], key);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < TB; u++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) kmin[u] = min(kmin[u], (unsigned long long)__shfl_xor((long long)kmin[u], o, 64));
+        if (lane == 0) smin[w][u] = kmin[u];
+    }
+    __syncthreads();
+    if (tid < TB) {
+        const unsigned long long m = min(min(smin[0][tid], smin[1][tid]), min(smin[2][tid], smin[3][tid]));
+        __hip_atomic_store(a.part + (long long)blockIdx.x * 8 + tid, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) {  // two-level arrival: eight group counters, then the top one (a.arrive[8])
+        const unsigned int nb = gridDim.x, g = blockIdx.x & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
+        int last = 0;
+        if ((unsigned int)atomicAdd(a.arrive + g, 1) == ng - 1u)
+            last = (unsigned int)atomicAdd(a.arrive + 8, 1) == ngroups - 1u;
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (tid <= 8) a.arrive[tid] = 0;  // for the next launch (kernel boundary in between)
+#ifdef ADLBQ_ONE_DIAG  // timing diagnostic only (wrong results): the scan and the arrival alone
+    return;
+#endif
+    // ---- the last workgroup: the request, every workgroup's minima, the choice, its finalize
+    prep_block<TB>(a.pa, 0);
+    unsigned long long gm[TB];
+#pragma unroll
+    for (int u = 0; u < TB; u++) gm[u] = ~0ull;
+    for (int b = tid; b < (int)gridDim.x; b += 256)
+#pragma unroll
+        for (int u = 0; u < TB; u++)
+            gm[u] = min(gm[u], (unsigned long long)__hip_atomic_load(
+                                   (long long *)(a.part + (long long)b * 8 + u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+    for (int u = 0; u < TB; u++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) gm[u] = min(gm[u], (unsigned long long)__shfl_xor((long long)gm[u], o, 64));
+    }
+    __syncthreads();  // prep_block's outputs, and smin free again
+    if (lane == 0)
+#pragma unroll
+        for (int u = 0; u < TB; u++) smin[w][u] = gm[u];
+    __syncthreads();
+    const FinArgs &f = a.f;
+    if (tid == 0) {
+        const unsigned long long m = a.pa.mask[0];
+        unsigned long long best = ~0ull;
+#pragma unroll
+        for (int u = 0; u < TB; u++) {
+            const unsigned long long k = min(min(smin[0][u], smin[1][u]), min(smin[2][u], smin[3][u]));
+            if (u < a.T && ((m >> u) & 1ull)) best = min(best, k);
+        }
+        int um = -1;
+        if (best != ~0ull) {
+            const int p = (int)((best >> PAGE_SHIFT) & 0xfffffu), sl = (int)(best & (PAGE - 1));
+            a.cslot[0] = (a.pages[p] << PAGE_SHIFT) | sl;
+            um = 0;
+        }
+        a.umatch[0] = um;
+        const int2 rk = f.rh[0];
+        const bool parks = rk.y && um < 0;
+        __hip_atomic_store(f.pmask, parks ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fin_request(f, 0, false, rk, -1, um);
+        s_last = parks ? 1 : 0;
+    }
+    __syncthreads();
+    fin_tail(f, s_last, false);
+}
+
 // Round 0: every segment from its level guess (lane t = type t's head), then
 // passes 2 .. P in the same launch: segment s waits for segment s-1's end of
 // the previous pass and re-solves (seeded) only if it differs from its own
@@ -4793,6 +4934,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     // a small open bucket and batch: one workgroup chooses (k_reserve_small), no scan
     const bool small = !h->grec && T > 0 && R <= std::min(h->small_r, SMALL_R) && np <= h->small_pages &&
                        (long long)np * PAGE <= SMALL_UNITS;
+    // one Reserve against a larger open bucket, no targeted units: one launch (k_reserve_one)
+    const bool one = !small && !h->grec && T > 0 && T <= 8 && R == 1 && !targeted && h->live_targeted == 0 &&
+                     h->reserve_one && np > 0;
     if (small) {
         if (targeted) {  // the targeted phase reads the prepared requests first
             const int nprep = (R + PREP_BLOCK - 1) / PREP_BLOCK;
@@ -4800,7 +4944,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             auto kph = T <= 4 ? k_prep_hist<4> : T <= 8 ? k_prep_hist<8> : k_prep_hist<64>;
             kph<<<nprep, 256, 0, s>>>(pa, nprep, none);
         }
-    } else if ((rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) {
+    } else if (!one && (rc = launch_scan(h, pa, (R + PREP_BLOCK - 1) / PREP_BLOCK, false, R))) {
         return rc;
     }
     host_stage_add(h, "scan", scan_t0);
@@ -4835,6 +4979,31 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             k_targeted<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_rank_fill,
                                           h->d_prio, h->d_meta, h->d_mask, d_reqs, R, h->d_tmatch, h->d_seg_cnt);
         stage_end(h, "targeted", ev);
+    }
+    if (one) {
+        const int grid = (np + 1) / 2;
+        if (grid > h->cap_onepart) {
+            AQ_HIP(hipStreamSynchronize(s));
+            if (h->d_onepart) AQ_HIP(hipFree(h->d_onepart));
+            h->cap_onepart = std::max(grid, 2 * h->cap_onepart);
+            // [16] arrival counters (ints), then [grid][8] per-type minima
+            AQ_HIP(hipMalloc((void **)&h->d_onepart, sizeof(unsigned long long) * 8 * (h->cap_onepart + 2)));
+            AQ_HIP(hipMemsetAsync(h->d_onepart, 0, sizeof(unsigned long long) * 16, s));
+        }
+        DevCounters *const snap = h->d_snap + h->snap_next;
+        h->snap_tag[h->snap_next] = ++h->snap_tags;
+        __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);
+        const OneArgs oa{pa, h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_pbase, h->d_pwide, T,
+                         h->d_onepart + 16, reinterpret_cast<int *>(h->d_onepart), h->d_umatch, h->d_cslot,
+                         fin_args(h, R, d_reqs, d_resp, snap)};
+        stage_begin(h, "one", &ev);
+        if (T <= 4) k_reserve_one<4><<<grid, 256, 0, s>>>(oa);
+        else k_reserve_one<8><<<grid, 256, 0, s>>>(oa);
+        stage_end(h, "one", ev);
+        h->one_batches++;
+        AQ_HIP(hipGetLastError());
+        batch_launched(h, R, 0, d_reqs);  // no candidate lists for a steal export to reuse
+        return ADLBQ_OK;
     }
     if (small) {
         const SmallArgs sa{pa, targeted ? 0 : 1, h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, R,
@@ -5242,8 +5411,13 @@ int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12) 
         const size_t ni = (size_t)ADLBQ_RESERVE_INTS * n, no = (size_t)ADLBQ_RESP_INTS * n;
         if ((rc = ensure_zc(h, (long long)(ni + no)))) return rc;
         std::memcpy(h->h_zc, reqs18, sizeof(int) * ni);
+        const long long one0 = h->one_batches;
         if ((rc = launch_reserve(h, n, h->d_zc, h->d_zc + ni))) return rc;
-        if ((rc = sync_batch_counters(h))) return rc;  // synchronises
+        // k_reserve_one: its one finishing wave stores the response, then the snapshot and last its
+        // tag (system-scope release): the landed tag is the batch's end, no stream synchronisation
+        if (h->one_batches == one0 || !wait_last_snapshot(h)) {
+            if ((rc = sync_batch_counters(h))) return rc;  // synchronises
+        }
         std::memcpy(resp12, h->h_zc + ni, sizeof(int) * no);
         return batch_outcome(h, failed0);
     }

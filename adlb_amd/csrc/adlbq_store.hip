@@ -323,6 +323,19 @@ static void apply_counters(adlbq_server *h);
 
 // After a synchronous reserve batch: the counters its k_finalize copied into
 // the newest snapshot slot (mapped memory, tagged last), no k_ctr_out launch.
+// Spin (host, mapped memory) until the last launched batch's snapshot tag lands, then take its
+// counters as sync_batch_counters does; false after ~2 s (the caller synchronises instead).
+bool wait_last_snapshot(adlbq_server *h) {
+    const int slot = (h->snap_next + adlbq_server::NSNAP - 1) % adlbq_server::NSNAP;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&h->h_snap[slot].snap_tag, __ATOMIC_ACQUIRE) != h->snap_tag[slot])
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) return false;
+    h->ctr = h->h_snap[slot];
+    apply_counters(h);
+    h->hint_stamp++;
+    return true;
+}
+
 int sync_batch_counters(adlbq_server *h) {
     const int slot = (h->snap_next + adlbq_server::NSNAP - 1) % adlbq_server::NSNAP;
     AQ_HIP(hipStreamSynchronize(h->stream));
@@ -1592,7 +1605,8 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_ckey3, h->d_cslot3, h->d_plan, h->d_rs, h->d_rs_cnt, h->d_rs_acc,
                     h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend,
                     h->d_mslot, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
-                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr};
+                    h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr,
+                    h->d_onepart};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -2557,6 +2571,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->group_launch = (int)value;
         return ADLBQ_OK;
     }
+    if (n == "reserve_one") {
+        h->reserve_one = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "select_wave") {
         h->select_wave = value ? 1 : 0;
         return ADLBQ_OK;
@@ -2684,6 +2702,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         return mx ? d.back() : d[d.size() / 2];
     }
     if (n == "parked") return h->ctr.n_parked_last;
+    if (n == "one_batches") return h->one_batches;  // one-Reserve batches through k_reserve_one
     if (n == "rq_cap") return h->rq_cap;  // rq slots allocated
     if (n == "rq_slots") {                // rq slots in use, and rqseqnos handed out / compactions
         refresh_counters(h);

@@ -669,3 +669,58 @@ def test_put_batch_device_matches_host_variant(gpu_available):
     for a, b in zip(*outs):
         np.testing.assert_array_equal(a, b)
 
+
+
+ONE = {
+    "one_c2_t4": lambda: synth.config2(n_units=30_000, n_reserves=300, seed=701),
+    "one_c2_t8_wide": lambda: synth.config2(n_units=25_000, n_types=8, n_reserves=300, seed=702, wide_frac=0.2,
+                                            wide_range=(-(1 << 31), (1 << 31) - 1)),
+    "one_c2_t1_eq": lambda: synth.config2(n_units=20_000, n_types=1, n_reserves=300, seed=703, equal_prio=True),
+    "one_c2_t3_tied": lambda: synth.config2(n_units=24_000, n_types=3, n_reserves=300, seed=704, prio_hi=3),
+}
+
+
+@pytest.mark.parametrize("engine", ["one", "pipeline"])
+@pytest.mark.parametrize("name", sorted(ONE))
+def test_single_reserve_batches_vs_oracle(gpu_available, name, engine):
+    """Batches of one Reserve on an open bucket larger than the one-workgroup
+    path takes: k_reserve_one (one launch) and the pipeline both give the
+    oracle's result, Reserve after Reserve (an INFO ends every batch)."""
+    w = ONE[name]()
+    parts = [synth.put_events(w)]
+    for j in range(w.r_rank.size):
+        parts.append(synth.reserve_events(w.r_rank[j:j + 1], w.r_types[j:j + 1], w.r_hang[j:j + 1]))
+        parts.append(synth.simple_events(synth.OP_INFO))
+    tr = np.concatenate(parts)
+    cfg = (w.num_app_ranks, 1, 0)
+    with Server(w.user_types, *cfg, max_units=w.n_units) as s:
+        if engine == "pipeline":
+            s.set_param("reserve_one", 0)
+        got = replay.replay(s, tr)
+        used = s.stat("one_batches")
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
+    assert (used == w.r_rank.size) == (engine == "one"), used
+
+
+def test_single_reserve_exhaustion_parks_vs_oracle(gpu_available):
+    """One-Reserve batches past the end of the queue: the last ones find nothing
+    and park (hang) or answer NO_CURR_WORK, as the oracle does."""
+    w = synth.config2(n_units=20_100, n_types=2, n_reserves=40, seed=705, prio_hi=5)
+    parts = [synth.put_events(w)]
+    # take nearly everything in one batch first, then single Reserves run the queue dry
+    big = 20_080
+    rng = np.random.default_rng(706)
+    tv = synth.type_vectors(rng, w.user_types, big)
+    parts.append(synth.reserve_events(np.arange(big) % w.num_app_ranks, tv, np.ones(big, np.uint8)))
+    parts.append(synth.simple_events(synth.OP_INFO))
+    for j in range(w.r_rank.size):
+        parts.append(synth.reserve_events(w.r_rank[j:j + 1], w.r_types[j:j + 1], w.r_hang[j:j + 1]))
+        parts.append(synth.simple_events(synth.OP_INFO))
+    tr = np.concatenate(parts)
+    cfg = (w.num_app_ranks, 1, 0)
+    with Server(w.user_types, *cfg, max_units=w.n_units) as s:
+        s.set_param("recycle_pages", 0)  # the emptied pages stay open: the bucket stays above four pages
+        got = replay.replay(s, tr)
+        used = s.stat("one_batches")
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
+    assert used == w.r_rank.size, used
