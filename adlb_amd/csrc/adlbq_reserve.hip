@@ -3239,6 +3239,7 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
 struct OneArgs {
     PrepArgs pa;
     const int *pages; int npages, tail_fill;
+    int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
     const int *prio; const uint32_t *meta; const int *pbase, *pwide;
     int T;
     unsigned long long *part;  // [grid][8] per-type minima
@@ -3263,7 +3264,7 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int p = 2 * blockIdx.x + h;
-            pg[h] = p < a.npages ? a.pages[p] : -1;
+            pg[h] = p >= a.npages ? -1 : a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
             pb[h] = pg[h] >= 0 ? a.pbase[pg[h]] : 0;
             wide[h] = pg[h] >= 0 ? a.pwide[pg[h]] : 0;
         }
@@ -3281,6 +3282,10 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
             const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
             const uint32_t mm[4] = {mv[i].x, mv[i].y, mv[i].z, mv[i].w};
             const int pw[4] = {pv[i].x, pv[i].y, pv[i].z, pv[i].w};
+#ifdef ADLBQ_ONE_MEMONLY  // timing diagnostic only (wrong results): the loads without the comparisons
+            kmin[0] ^= (unsigned long long)(mm[0] ^ mm[1] ^ mm[2] ^ mm[3] ^ pw[0]);
+            continue;
+#endif
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int pr = wide[h] ? pw[q] : pb[h] + (int)(mm[q] >> M_OFF_SHIFT);
@@ -4993,7 +4998,10 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         DevCounters *const snap = h->d_snap + h->snap_next;
         h->snap_tag[h->snap_next] = ++h->snap_tags;
         __atomic_store_n(&h->h_snap[h->snap_next].snap_tag, 0ull, __ATOMIC_RELEASE);
-        const OneArgs oa{pa, h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, h->d_pbase, h->d_pwide, T,
+        int pg0 = h->open.pages[0];
+        for (int i = 1; i < np && pg0 >= 0; i++)
+            if (h->open.pages[(size_t)i] != pg0 + i) pg0 = -1;
+        const OneArgs oa{pa, h->d_open_pages, np, h->open.tail_fill, pg0, h->d_prio, h->d_meta, h->d_pbase, h->d_pwide, T,
                          h->d_onepart + 16, reinterpret_cast<int *>(h->d_onepart), h->d_umatch, h->d_cslot,
                          fin_args(h, R, d_reqs, d_resp, snap)};
         stage_begin(h, "one", &ev);
