@@ -4937,11 +4937,11 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     host_stage_add(h, "pre", host_t0);
     const auto scan_t0 = std::chrono::steady_clock::now();
     // a small open bucket and batch: one workgroup chooses (k_reserve_small), no scan
-    const bool small = !h->grec && T > 0 && R <= std::min(h->small_r, SMALL_R) && np <= h->small_pages &&
+    // one Reserve, no targeted units: one launch (k_reserve_one), whatever the bucket's size (k_reserve_small
+    // sorts every live unit of its pages, ~260 us at 10K units)
+    const bool one = !h->grec && T > 0 && T <= 8 && R == 1 && h->live_targeted == 0 && h->reserve_one && np > 0;
+    const bool small = !one && !h->grec && T > 0 && R <= std::min(h->small_r, SMALL_R) && np <= h->small_pages &&
                        (long long)np * PAGE <= SMALL_UNITS;
-    // one Reserve against a larger open bucket, no targeted units: one launch (k_reserve_one)
-    const bool one = !small && !h->grec && T > 0 && T <= 8 && R == 1 && !targeted && h->live_targeted == 0 &&
-                     h->reserve_one && np > 0;
     if (small) {
         if (targeted) {  // the targeted phase reads the prepared requests first
             const int nprep = (R + PREP_BLOCK - 1) / PREP_BLOCK;

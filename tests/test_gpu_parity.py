@@ -64,7 +64,7 @@ def assert_same(got, exp):
 # small open buckets and batches take the one-workgroup choice by default
 # (k_reserve_small); "pipeline" turns it off so that the batch pipeline is
 # checked on the same small cases
-ENGINES = {"default": {}, "pipeline": {"small_pages": 0}}
+ENGINES = {"default": {}, "pipeline": {"small_pages": 0, "reserve_one": 0}}
 
 
 @pytest.mark.parametrize("engine", sorted(ENGINES))
@@ -104,7 +104,7 @@ def test_small_queue_vs_oracle(gpu_available, name, engine):
         for k, v in ENGINES[engine].items():
             s.set_param(k, v)
         got = replay.replay(s, tr)
-        used = s.stat("small_batches")
+        used = s.stat("small_batches") + s.stat("one_batches")  # (a one-Reserve batch takes k_reserve_one)
     assert_same(got, run_oracle(w.user_types, cfg, tr))
     assert (used > 0) == (engine == "default"), used
 
