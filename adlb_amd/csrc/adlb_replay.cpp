@@ -247,6 +247,13 @@ struct RShard {
     long long nout_dev = 0;
     std::string err;
     long long ncalls = 0;
+    RShard() = default;
+    RShard(const RShard &) = delete;
+    RShard &operator=(const RShard &) = delete;
+    ~RShard() {  // every return path of adlbsrv_replay_rounds, early errors included
+        if (din) (void)hipFree(din);
+        if (dout) (void)hipFree(dout);
+    }
 };
 
 namespace {
@@ -518,10 +525,6 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
             g_rerr = "shard " + std::to_string(j) + ": output buffer too small";
             rc = -2;
         }
-    }
-    for (auto &r : sh) {
-        if (r.din) hipFree(r.din);
-        if (r.dout) hipFree(r.dout);
     }
     if (!rc && (failed || !gerr.empty())) {
         g_rerr = gerr.empty() ? "a shard failed" : gerr;

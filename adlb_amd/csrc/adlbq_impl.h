@@ -50,6 +50,16 @@ constexpr uint32_t M_PINNED = 1u << 9;
 // within 2^22 of the base): the scans then read 4 B per unit, not 8
 constexpr int M_OFF_SHIFT = 10;
 constexpr long long M_OFF_RANGE = 1ll << 22;
+// More than ADLBQ_MAX_TYPES_WIDE (255) types (get_type_idx has no bound, adlb.c:3476-3485): such a
+// server's pages are all wide (prio read from the prio column), so bits 10..31 carry the type
+// index's bits above the low eight.  vw = the server has more than 255 types.
+constexpr int VW_TYPES = ADLBQ_MAX_TYPES_WIDE;
+__host__ __device__ __forceinline__ int meta_type(uint32_t m, int vw) {
+    return (int)(m & M_TYPE) | (vw ? (int)(m >> M_OFF_SHIFT) << 8 : 0);
+}
+__host__ __device__ __forceinline__ uint32_t meta_of_type(int ti, int vw) {
+    return vw ? ((uint32_t)ti & M_TYPE) | ((uint32_t)(ti >> 8) << M_OFF_SHIFT) : (uint32_t)ti;
+}
 constexpr int NREQ = ADLBQ_REQ_TYPES;
 // the reference's allocation sizes (include/adlbq.h: ADLBQ_BYTES_*)
 constexpr long long BYTES_WQ = ADLBQ_BYTES_WQ, BYTES_RQ = ADLBQ_BYTES_RQ, BYTES_TQ = ADLBQ_BYTES_TQ;
@@ -80,6 +90,8 @@ struct DevCounters {
     int kr_why;            // the last keyrank failover: 1 more candidates than its buffers, 2 a bin over kr_bin_max
     int kr_maxbin;         // the largest digit bin of the last keyrank batch (diagnostic)
     int batch_failed;      // batches answered ADLB_ERROR because an in-launch candidate sort gave up (cumulative)
+    int bound_faults;      // choices whose bucket position lay outside the page list (cumulative; the batch
+                           // is answered ADLB_ERROR, never indexed past the list)
     int rq_next;           // rqseqnos handed out (next_rqseqno - 1, adlb.c:1244)
     int rq_reclaims;       // k_rq_reclaim compactions (cumulative)
     // the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced (adlb.c:3419-3474) over the
@@ -327,13 +339,17 @@ struct adlbq_server {
     unsigned long long *d_onepart = nullptr; int cap_onepart = 0; long long one_batches = 0;
     int select_wave = 1;               // "select_wave": pass 2 with one wave per page (T <= 8); 0 = four
     int rq_compact_calls = 0; long long rq_compactions = 0;  // background rq compaction (maybe_compact_rq)
+    long long rq_reclaims_launched = 0;  // k_rq_reclaim launches (DevCounters::rq_reclaims counts the landed ones)
     int small_pages = 4;               // "small_pages": an open bucket of at most this many pages and a batch of
     int small_r = 1024;                //   at most "small_r" Reserves take the one-workgroup choice (0: never)
+    int bound_inject = 0;              // "bound_inject" (test only): the next small / one-Reserve choice is told a
+                                       //   position past the page list (the fault path of DESIGN.md §9)
     long long small_batches = 0;       // reserve batches served by it (stat "small_batches")
     // the Reserve path of more than ADLBQ_MAX_TYPES types (adlbq_wide.hip): sort buffers and runs
     unsigned long long *d_wk0 = nullptr, *d_wk1 = nullptr, *d_wekey = nullptr;
     int *d_wv0 = nullptr, *d_wv1 = nullptr, *d_wflag = nullptr, *d_wrstart = nullptr, *d_whead = nullptr;
-    unsigned int *d_wrkey = nullptr;
+    unsigned long long *d_wrkey = nullptr;  // run keys: (target rank or A) << type bits | type index
+    int2 *d_utsorted = nullptr; int n_utsorted = 0;  // > 255 types: (value, first declared index) by value
     int *d_wreq = nullptr, *d_wcnt = nullptr;
     int2 *d_wpages = nullptr;
     void *d_wtmp = nullptr;

@@ -3080,6 +3080,17 @@ __device__ __forceinline__ bool fin_failed(const FinArgs &f) {
     return __hip_atomic_load(f.sortfail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
 
+// A chosen unit's bucket position must lie inside the open bucket's page list:
+// every gathered position does.  One that does not is counted and fails the
+// whole batch (k_finalize answers ADLB_ERROR, pins and parks nothing) instead of
+// indexing past the list.  (The r05 fault on this path)
+__device__ __forceinline__ bool pos_in_list(unsigned int pos, int npages, DevCounters *ctr, int *fail) {
+    if ((int)(pos >> PAGE_SHIFT) < npages) return true;
+    atomicAdd(&ctr->bound_faults, 1);
+    __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+}
+
 // Request j (j < R): pin its unit and write its response (rk, tm, um: its
 // rh, tmatch and umatch entries, loaded by finalize_body).  A request that
 // parks (no unit, hang) leaves words [10], [11] to the park tail.  Every
@@ -3246,6 +3257,7 @@ struct OneArgs {
     int *arrive;               // [9] arrival counters: eight groups, then the top (the last workgroup resets them)
     int *umatch, *cslot;
     FinArgs f;
+    int inject;  // test only: the choice is told a position past the page list
 };
 template <int TB>
 __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
@@ -3314,14 +3326,18 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
     }
     __syncthreads();
     if (tid == 0) {  // two-level arrival: eight group counters, then the top one (a.arrive[8])
+        // release: this workgroup's minima (and, through the group counter, its group's) are visible
+        // to whoever observes the arrival; the last workgroup acquires below before reading a.part
         const unsigned int nb = gridDim.x, g = blockIdx.x & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
         int last = 0;
-        if ((unsigned int)atomicAdd(a.arrive + g, 1) == ng - 1u)
-            last = (unsigned int)atomicAdd(a.arrive + 8, 1) == ngroups - 1u;
+        if ((unsigned int)__hip_atomic_fetch_add(a.arrive + g, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ng - 1u)
+            last = (unsigned int)__hip_atomic_fetch_add(a.arrive + 8, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                   ngroups - 1u;
         s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's minima before they are read
     if (tid <= 8) a.arrive[tid] = 0;  // for the next launch (kernel boundary in between)
 #ifdef ADLBQ_ONE_DIAG  // timing diagnostic only (wrong results): the scan and the arrival alone
     return;
@@ -3356,20 +3372,25 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
             if (u < a.T && ((m >> u) & 1ull)) best = min(best, k);
         }
         int um = -1;
+        bool bad = false;
         if (best != ~0ull) {
-            const int p = (int)((best >> PAGE_SHIFT) & 0xfffffu), sl = (int)(best & (PAGE - 1));
-            a.cslot[0] = (a.pages[p] << PAGE_SHIFT) | sl;
-            um = 0;
+            const int p = a.inject ? a.npages : (int)((best >> PAGE_SHIFT) & 0xfffffu), sl = (int)(best & (PAGE - 1));
+            if (pos_in_list((unsigned int)p << PAGE_SHIFT, a.npages, f.ctr, f.sortfail)) {
+                a.cslot[0] = (a.pages[p] << PAGE_SHIFT) | sl;
+                um = 0;
+            } else {
+                bad = true;  // answered ADLB_ERROR below; fin_tail resets the flag
+            }
         }
         a.umatch[0] = um;
         const int2 rk = f.rh[0];
-        const bool parks = rk.y && um < 0;
+        const bool parks = !bad && rk.y && um < 0;
         __hip_atomic_store(f.pmask, parks ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fin_request(f, 0, false, rk, -1, um);
-        s_last = parks ? 1 : 0;
+        fin_request(f, 0, bad, rk, -1, um);
+        s_last = (parks ? 1 : 0) | (bad ? 2 : 0);
     }
     __syncthreads();
-    fin_tail(f, s_last, false);
+    fin_tail(f, s_last & 1, (s_last & 2) != 0);
 }
 
 // Round 0: every segment from its level guess (lane t = type t's head), then
@@ -4610,7 +4631,10 @@ struct SmallArgs {
     const int *tmatch;
     const unsigned long long *mask;
     DevCounters *ctr;
+    int *sortfail;  // set: k_finalize answers the batch ADLB_ERROR (a choice outside the page list)
+    int inject;     // test only: the first choice is told a position past the page list
 };
+
 
 // sort key, ascending = better within a type: type (7 bits), prio descending, position ascending
 __device__ __forceinline__ unsigned long long small_key(int t, int pr, unsigned int pos) {
@@ -4761,10 +4785,10 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
                         c2[q] = hp[q] + 2 < he[q] ? uni(skey[hp[q] + 2]) : ~0ull;
                         if (c0[q] == ~0ull) live &= ~(1u << q);
                     }
-                const unsigned int pos = (unsigned int)(best & 0xffffffu);
-                const int p = (int)(pos >> PAGE_SHIFT);
-                if ((j & 63) == lane && p < a.npages) {
-                    cs_l = (a.pages[p] << PAGE_SHIFT) | (int)(pos & (PAGE - 1));
+                const unsigned int pos =
+                    (a.inject && j == 0) ? (unsigned int)a.npages << PAGE_SHIFT : (unsigned int)(best & 0xffffffu);
+                if ((j & 63) == lane && pos_in_list(pos, a.npages, a.ctr, a.sortfail)) {
+                    cs_l = (a.pages[pos >> PAGE_SHIFT] << PAGE_SHIFT) | (int)(pos & (PAGE - 1));
                     um_l = j;
                 }
             }
@@ -4819,10 +4843,10 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
                 nxt = h + 1 < e ? skey[h + 1] : ~0ull;
             }
             if (lane == 0) {
-                const unsigned int pos = (unsigned int)(best & 0xffffffu);
-                const int p = (int)(pos >> PAGE_SHIFT);
-                const bool ok = p < a.npages;  // always (a gathered unit's position); never index past the list
-                a.cslot[j] = ok ? (a.pages[p] << PAGE_SHIFT) | (int)(pos & (PAGE - 1)) : -1;
+                const unsigned int pos =
+                    (a.inject && j == 0) ? (unsigned int)a.npages << PAGE_SHIFT : (unsigned int)(best & 0xffffffu);
+                const bool ok = pos_in_list(pos, a.npages, a.ctr, a.sortfail);
+                a.cslot[j] = ok ? (a.pages[pos >> PAGE_SHIFT] << PAGE_SHIFT) | (int)(pos & (PAGE - 1)) : -1;
                 a.umatch[j] = ok ? j : -1;
             }
         } else if (lane == 0) {
@@ -5003,7 +5027,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             if (h->open.pages[(size_t)i] != pg0 + i) pg0 = -1;
         const OneArgs oa{pa, h->d_open_pages, np, h->open.tail_fill, pg0, h->d_prio, h->d_meta, h->d_pbase, h->d_pwide, T,
                          h->d_onepart + 16, reinterpret_cast<int *>(h->d_onepart), h->d_umatch, h->d_cslot,
-                         fin_args(h, R, d_reqs, d_resp, snap)};
+                         fin_args(h, R, d_reqs, d_resp, snap), h->bound_inject};
+        h->bound_inject = 0;
         stage_begin(h, "one", &ev);
         if (T <= 4) k_reserve_one<4><<<grid, 256, 0, s>>>(oa);
         else k_reserve_one<8><<<grid, 256, 0, s>>>(oa);
@@ -5014,8 +5039,13 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         return ADLBQ_OK;
     }
     if (small) {
+        // what the kernel assumes: the page list it reads is the one uploaded, candidates fit d_cslot
+        if (h->tables_dirty || h->pinfo_dirty || (long long)R > h->cap_cand)
+            return fail(ADLBQ_ERR_DEVICE, "k_reserve_small: stale page tables or candidate buffers (internal)");
         const SmallArgs sa{pa, targeted ? 0 : 1, h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, R,
-                           h->d_umatch, h->d_cslot, h->d_needsort, h->d_tmatch, h->d_mask, h->d_ctr};
+                           h->d_umatch, h->d_cslot, h->d_needsort, h->d_tmatch, h->d_mask, h->d_ctr,
+                           h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->bound_inject};
+        h->bound_inject = 0;
         const size_t lds = sizeof(unsigned long long) * (SMALL_UNITS + SMALL_R) + sizeof(int) * SMALL_R;
         stage_begin(h, "small", &ev);
         if (T <= 4) k_reserve_small<4><<<1, SMALL_THREADS, lds, s>>>(sa);
@@ -5403,8 +5433,10 @@ constexpr int RESERVE_ZC_MAX = 512;  // host-buffer batches up to this size go z
 // batch ADLB_ERROR (a device-side wait gave up; nothing was pinned or parked).
 static int batch_outcome(adlbq_server *h, int failed_before) {
     if (h->ctr.batch_failed != failed_before)
-        return fail(ADLBQ_ERR_DEVICE, "adlbq_reserve_batch: an in-launch candidate sort did not finish in time; "
-                                      "the batch was answered ADLB_ERROR and left the queues unchanged");
+        return fail(ADLBQ_ERR_DEVICE, ("adlbq_reserve_batch: an in-launch candidate sort did not finish in time, "
+                                       "or a choice lay outside the page list (stat bound_faults = " +
+                                       std::to_string(h->ctr.bound_faults) +
+                                       "); the batch was answered ADLB_ERROR and left the queues unchanged").c_str());
     return ADLBQ_OK;
 }
 

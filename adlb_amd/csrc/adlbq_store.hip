@@ -218,12 +218,21 @@ __global__ void k_set_rq_next(DevCounters *ctr, int v) { ctr->rq_next = v; }
 constexpr int RQ_COMPACT_EVERY = 4;
 void maybe_compact_rq(adlbq_server *h) {
     if (!h->d_rq_seq || h->rq_cap <= 0 || ++h->rq_compact_calls < RQ_COMPACT_EVERY) return;
-    // (the last landed counters: a compaction since shows as a shorter span only once it lands)
-    const long long span = (long long)h->ctr.rq_n - h->ctr.rq_head;
-    if (span <= 2ll * h->ctr.rq_live + 4096 && span * 2 <= h->rq_cap) return;
-    if (span <= h->ctr.rq_live + 256) return;  // nothing much to reclaim
+    // the newest counters the host has: the synchronised copy, or -- while batches are in
+    // flight (device-side entry points never synchronise) -- the newest landed batch snapshot
+    const DevCounters *v = &h->ctr;
+    if (h->ctr_stale) {
+        const int i = newest_landed(h);
+        if (i >= 0 && h->h_snap[i].rq_reclaims >= v->rq_reclaims) v = &h->h_snap[i];
+    }
+    // a compaction launched earlier that this view does not show yet: its effect is unknown, wait for it
+    if (v->rq_reclaims < h->rq_reclaims_launched) return;
+    const long long span = (long long)v->rq_n - v->rq_head;
+    if (span <= 2ll * v->rq_live + 4096 && span * 2 <= h->rq_cap) return;
+    if (span <= v->rq_live + 256) return;  // nothing much to reclaim
     h->rq_compact_calls = 0;
     h->rq_compactions++;
+    h->rq_reclaims_launched++;
     k_rq_reclaim<<<1, 1024, 0, h->stream>>>(h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr);
 }
 
@@ -257,6 +266,7 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
     }
     h->hacc["rq_reclaims"] += 1;
     if (h->rq_cap > 0 && h->d_rq_seq) {  // reclaim the slots of dead entries, then the exact count
+        h->rq_reclaims_launched++;
         k_rq_reclaim<<<1, 1024, 0, h->stream>>>(h->d_rq_rank, h->d_rq_types, h->d_rq_live, h->d_rq_seq, h->d_ctr);
         AQ_HIP(hipGetLastError());
         int rc;
@@ -716,7 +726,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
     constexpr int PM_RBITS = 1 << 16;
     __shared__ unsigned int s_rbits[PM_RBITS / 32];
     __shared__ unsigned long long s_mask[PM_CAP];
-    __shared__ int s_wmin[PM_WAVES], s_cnt[PM_WAVES], s_tot;
+    __shared__ int s_cnt[PM_WAVES], s_tot;
     __shared__ long long s_wsum[PM_WAVES], s_wpk[PM_WAVES];
     __shared__ int s_ut[ADLBQ_MAX_TYPES];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1129,7 +1139,7 @@ __global__ __launch_bounds__(256) void k_get_small(const int *__restrict__ pairs
 // the type.  Blocks publish partials; the last to arrive combines them.
 __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ pages, const int *__restrict__ fills,
                                                     int npages, const int *__restrict__ prio,
-                                                    const uint32_t *__restrict__ meta, int tidx, int *part,
+                                                    const uint32_t *__restrict__ meta, int tidx, int vw, int *part,
                                                     int *res) {
     __shared__ int smx[4], scm[4], scn[4];
     __shared__ bool s_last;
@@ -1138,7 +1148,7 @@ __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ page
         const long long base = (long long)pages[p] << PAGE_SHIFT;
         for (int o = threadIdx.x; o < fills[p]; o += blockDim.x) {
             const uint32_t m = meta[base + o];
-            if ((m & M_LIVE) && (int)(m & M_TYPE) == tidx) {
+            if ((m & M_LIVE) && meta_type(m, vw) == tidx) {
                 const int pr = prio[base + o];
                 cn++;
                 if (pr > mx) {
@@ -1279,7 +1289,9 @@ __global__ void k_qmrow(const int *__restrict__ pages, int npages, int tail_fill
                         const uint32_t *__restrict__ meta, int T, int *res /* [0]=qlen, [1+t]=max */) {
     __shared__ int smax[ADLBQ_MAX_TYPES_WIDE];
     __shared__ int scnt;
-    for (int t = threadIdx.x; t < T; t += blockDim.x) smax[t] = LOWEST;
+    const int vw = T > VW_TYPES;  // more than 255 types: the maxima go straight to res (global atomics)
+    if (!vw)
+        for (int t = threadIdx.x; t < T; t += blockDim.x) smax[t] = LOWEST;
     if (threadIdx.x == 0) scnt = 0;
     __syncthreads();
     int cnt = 0;
@@ -1293,13 +1305,17 @@ __global__ void k_qmrow(const int *__restrict__ pages, int npages, int tail_fill
         if ((m & (M_LIVE | M_PINNED)) == M_LIVE) {
             cnt++;
             int pr = prio[s];
-            if (pr > LOWEST) atomicMax(&smax[m & M_TYPE], pr);
+            if (pr > LOWEST) {
+                if (vw) atomicMax(&res[1 + meta_type(m, 1)], pr);
+                else atomicMax(&smax[m & M_TYPE], pr);
+            }
         }
     }
     atomicAdd(&scnt, cnt);
     __syncthreads();
-    for (int t = threadIdx.x; t < T; t += blockDim.x)
-        if (smax[t] > LOWEST) atomicMax(&res[1 + t], smax[t]);
+    if (!vw)
+        for (int t = threadIdx.x; t < T; t += blockDim.x)
+            if (smax[t] > LOWEST) atomicMax(&res[1 + t], smax[t]);
     if (threadIdx.x == 0) atomicAdd(&res[0], scnt);
 }
 
@@ -1498,8 +1514,8 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     if (!out || ntypes < 0 || (ntypes && !user_types) || num_app_ranks < 0 || num_servers < 1 ||
         my_server_idx < 0 || my_server_idx >= num_servers)
         return fail(ADLBQ_ERR_ARG, "adlbq_create: bad argument");
-    if (ntypes > ADLBQ_MAX_TYPES_WIDE)
-        return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 255 work types (8-bit type index per slot)");
+    if (ntypes > ADLBQ_MAX_TYPES_VWIDE)
+        return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 2^22 work types");
     if (ntypes > ADLBQ_MAX_TYPES && num_app_ranks >= (1 << 24) - 2)
         return fail(ADLBQ_ERR_UNSUPPORTED, "adlbq_create: more than 64 types with 2^24 or more app ranks");
     auto *h = new adlbq_server();
@@ -1578,8 +1594,19 @@ int adlbq_create(adlbq_server **out, int ntypes, const int *user_types, int num_
     AQ_HIP(hipMemsetAsync(h->d_type_cnt, 0, sizeof(int) * T1, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_rank_sync, sizeof(int) * (ADLBQ_MAX_TYPES + 6)));
     AQ_HIP(hipMemsetAsync(h->d_rank_sync, 0, sizeof(int) * (ADLBQ_MAX_TYPES + 6), h->stream));
-    AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (ADLBQ_MAX_TYPES_WIDE + 16)));
-    AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (ADLBQ_MAX_TYPES_WIDE + 16)));
+    AQ_HIP(hipMalloc((void **)&h->d_result, sizeof(int) * (std::max(ntypes, ADLBQ_MAX_TYPES_WIDE) + 16)));
+    AQ_HIP(hipHostMalloc((void **)&h->h_result, sizeof(int) * (std::max(ntypes, ADLBQ_MAX_TYPES_WIDE) + 16)));
+    if (ntypes > VW_TYPES) {  // the wide path's (value, first declared index) table, sorted by value
+        std::vector<std::pair<int, int>> vs;
+        for (int i = 0; i < ntypes; i++) vs.emplace_back(user_types[i], i);
+        std::stable_sort(vs.begin(), vs.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+        std::vector<int2> tab;
+        for (size_t i = 0; i < vs.size(); i++)
+            if (i == 0 || vs[i].first != vs[i - 1].first) tab.push_back(make_int2(vs[i].first, vs[i].second));
+        h->n_utsorted = (int)tab.size();
+        AQ_HIP(hipMalloc((void **)&h->d_utsorted, sizeof(int2) * tab.size()));
+        AQ_HIP(hipMemcpy(h->d_utsorted, tab.data(), sizeof(int2) * tab.size(), hipMemcpyHostToDevice));
+    }
     long long pages = std::max<long long>(16, (max_units + PAGE - 1) / PAGE + 16);
     if ((rc = grow_pages(h, (int)std::min<long long>(pages, INT_MAX / PAGE)))) return cleanup(rc);
     if ((rc = ensure_rq_capacity(h, 1024))) return cleanup(rc);
@@ -1606,7 +1633,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend,
                     h->d_mslot, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
                     h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr,
-                    h->d_onepart};
+                    h->d_onepart, h->d_utsorted};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -1756,11 +1783,12 @@ static int put_impl(adlbq_server *h, int n, const int *units9, int *out3, int *d
         PutRec &r = rec[i];
         r.slot = (int)slot;
         r.prio = u[1];
-        r.meta = ti | (int)M_LIVE;
+        const bool vw = h->T > VW_TYPES;  // the offset field holds the type index's high bits
+        r.meta = (int)meta_of_type(ti, vw) | (int)M_LIVE;
         {
             const int pg = b->pages.back();
             const long long off = (long long)u[1] - h->page_base[pg];
-            if (off >= 0 && off < M_OFF_RANGE) r.meta |= (int)((unsigned int)off << M_OFF_SHIFT);
+            if (!vw && off >= 0 && off < M_OFF_RANGE) r.meta |= (int)((unsigned int)off << M_OFF_SHIFT);
             else if (!h->page_wide[pg]) {
                 h->page_wide[pg] = 1;
                 h->pinfo_dirty = true;
@@ -2410,7 +2438,8 @@ int adlbq_info_type(adlbq_server *h, int work_type, int *max_prio, int *num_max_
     }
     if (npages) {
         k_info_fused<<<std::min(npages, IB), 256, 0, h->stream>>>(h->d_all_pages, h->d_all_fill, npages, h->d_prio,
-                                                                  h->d_meta, it->second, h->d_info, h->d_result);
+                                                                  h->d_meta, it->second, h->T > VW_TYPES ? 1 : 0,
+                                                                  h->d_info, h->d_result);
     } else {
         int init[3] = {LOWEST, 0, 0};
         AQ_HIP(hipMemcpyAsync(h->d_result, init, sizeof(init), hipMemcpyHostToDevice, h->stream));
@@ -2583,6 +2612,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->recycle_pages = value ? 1 : 0;
         return ADLBQ_OK;
     }
+    if (n == "bound_inject") {
+        h->bound_inject = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "small_pages") {  // the one-workgroup choice: largest open bucket (pages), 0 = off
         if (value < 0 || value > 4) return fail(ADLBQ_ERR_ARG, "small_pages must be in [0, 4]");
         h->small_pages = (int)value;
@@ -2604,8 +2637,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
 long long adlbq_stat(adlbq_server *h, const char *name) {
     if (!h || !name) return -1;
     hipSetDevice(h->device);
-    if (refresh_counters(h)) return -1;
     std::string n(name);
+    // host-side section timers need no device counters: no launch, no synchronisation
+    const bool host_only = n.rfind("hacc:", 0) == 0 || n.rfind("host_ns:", 0) == 0;
+    if (!host_only && refresh_counters(h)) return -1;
     if (n.rfind("kst_", 0) == 0 && h->d_kst && h->n_kst > 0) {
         // diagnostic: "kst_{hist,sel}_{1,2,3}" = median over workgroups of (stamp K - stamp 0) in ns,
         // "kst_{hist,sel}_start" = the spread of the start stamps, "kst_{hist,sel}_span" = first start to last end
@@ -2750,6 +2785,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         refresh_counters(h);
         return h->ctr.plan_missed;
     }
+    if (n == "bound_faults") return h->ctr.bound_faults;
     if (n == "sort_timeouts" || n == "batch_failed") {  // batches answered ADLB_ERROR because k_rank's wait
         refresh_counters(h);                                // for an in-launch sort gave up (0 unless broken)
         return h->ctr.batch_failed;

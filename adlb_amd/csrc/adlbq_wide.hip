@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void k_wide_gather(const int2 *__restrict__ pa
 // the next sort key of every entry: 1 = prio descending, 2 = run key (target rank or A, type index)
 __global__ __launch_bounds__(256) void k_wide_key(int n, int stage, const int *__restrict__ val,
                                                   const int *__restrict__ prio, const uint32_t *__restrict__ meta,
-                                                  const int4 *__restrict__ cold1, int A,
+                                                  const int4 *__restrict__ cold1, int A, int sh, int vw,
                                                   unsigned long long *__restrict__ key) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_wide_key(int n, int stage, const int *_
     } else {
         const int tg = cold1[s].w;
         const unsigned int tk = tg < 0 ? (unsigned int)A : tg < A ? (unsigned int)tg : (unsigned int)A + 1u;
-        key[i] = ((unsigned long long)tk << 8) | (meta[s] & M_TYPE);
+        key[i] = ((unsigned long long)tk << sh) | (unsigned long long)meta_type(meta[s], vw);
     }
 }
 
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_wide_ekey(int n, const int *__restrict_
 // one workgroup: the runs (key, start, head) in order, and rstart[nr] = n; cnt[1] = nr
 __global__ __launch_bounds__(1024) void k_wide_runs(int n, const int *__restrict__ flag,
                                                     const unsigned long long *__restrict__ rk,
-                                                    unsigned int *__restrict__ rkey, int *__restrict__ rstart,
+                                                    unsigned long long *__restrict__ rkey, int *__restrict__ rstart,
                                                     int *__restrict__ head, int *__restrict__ cnt) {
     __shared__ int wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(1024) void k_wide_runs(int n, const int *__restrict
         }
         if (f) {
             const int r = pre + __popcll(b & ((1ull << lane) - 1ull));
-            rkey[r] = (unsigned int)rk[i];
+            rkey[r] = rk[i];
             rstart[r] = i;
             head[r] = i;
         }
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(1024) void k_wide_runs(int n, const int *__restrict
     }
 }
 
-__device__ __forceinline__ int lower_bound_u32(const unsigned int *a, int n, unsigned int x) {
+__device__ __forceinline__ int lower_bound_u64(const unsigned long long *a, int n, unsigned long long x) {
     int lo = 0, hi = n;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -126,12 +126,14 @@ __device__ __forceinline__ int lower_bound_u32(const unsigned int *a, int n, uns
 // choice looks at -- of its own rank (targeted) and of A (untargeted): one run
 // per listed type, or the rank's whole range of runs for a -1 anywhere
 __global__ __launch_bounds__(256) void k_wide_prep(const int *__restrict__ reqs, int R, const int *__restrict__ utypes,
-                                                   int T, int A, const unsigned int *__restrict__ rkey,
+                                                   int T, int A, const unsigned long long *__restrict__ rkey,
                                                    const int *__restrict__ cnt, int *__restrict__ wreq,
                                                    int2 *__restrict__ rh, int *__restrict__ tmatch,
-                                                   int *__restrict__ umatch) {
+                                                   int *__restrict__ umatch, int sh,
+                                                   const int2 *__restrict__ utsorted, int nut) {
     __shared__ int s_ut[ADLBQ_MAX_TYPES_WIDE];
-    for (int t = threadIdx.x; t < T; t += blockDim.x) s_ut[t] = utypes[t];
+    if (!utsorted)
+        for (int t = threadIdx.x; t < T; t += blockDim.x) s_ut[t] = utypes[t];
     __syncthreads();
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R) return;
@@ -147,6 +149,16 @@ __global__ __launch_bounds__(256) void k_wide_prep(const int *__restrict__ reqs,
         const int v = q[2 + e];
         wild |= v == -1;
         if (v < 0) continue;
+        if (utsorted) {  // more than 255 types: binary search in (value, first declared index) by value
+            int lo = 0, hi = nut;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (utsorted[mid].x < v) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < nut && utsorted[lo].x == v) idx[ni++] = utsorted[lo].y;
+            continue;
+        }
         for (int t = 0; t < T; t++)
             if (s_ut[t] == v) {  // get_type_idx: the first declared match
                 idx[ni++] = t;
@@ -157,18 +169,18 @@ __global__ __launch_bounds__(256) void k_wide_prep(const int *__restrict__ reqs,
     for (int side = 0; side < 2; side++) {
         int *oo = o + (side ? 18 : 2);
         const bool valid = side ? true : (rank >= 0 && rank < A);
-        const unsigned int tk = side ? (unsigned int)A : (unsigned int)rank;
+        const unsigned long long tk = side ? (unsigned long long)A : (unsigned long long)rank;
         int c = 0;
         if (!valid) {
             c = 0;
         } else if (wild) {
-            oo[0] = lower_bound_u32(rkey, nr, tk << 8);
-            oo[1] = lower_bound_u32(rkey, nr, (tk + 1u) << 8);
+            oo[0] = lower_bound_u64(rkey, nr, tk << sh);
+            oo[1] = lower_bound_u64(rkey, nr, (tk + 1ull) << sh);
             c = -1;
         } else {
             for (int e = 0; e < ni; e++) {
-                const unsigned int k = (tk << 8) | (unsigned int)idx[e];
-                const int r = lower_bound_u32(rkey, nr, k);
+                const unsigned long long k = (tk << sh) | (unsigned long long)idx[e];
+                const int r = lower_bound_u64(rkey, nr, k);
                 if (r < nr && rkey[r] == k) oo[c++] = r;
             }
         }
@@ -246,7 +258,7 @@ static int wide_cap(adlbq_server *h, long long n, int R, int npg) {
         AQ_HIP(hipMalloc((void **)&h->d_wv1, sizeof(int) * c));
         AQ_HIP(hipMalloc((void **)&h->d_wekey, sizeof(unsigned long long) * c));
         AQ_HIP(hipMalloc((void **)&h->d_wflag, sizeof(int) * c));
-        AQ_HIP(hipMalloc((void **)&h->d_wrkey, sizeof(unsigned int) * (c + 1)));
+        AQ_HIP(hipMalloc((void **)&h->d_wrkey, sizeof(unsigned long long) * (c + 1)));
         AQ_HIP(hipMalloc((void **)&h->d_wrstart, sizeof(int) * (c + 1)));
         AQ_HIP(hipMalloc((void **)&h->d_whead, sizeof(int) * (c + 1)));
         h->cap_wtmp = rsx_temp_bytes(c);
@@ -295,17 +307,23 @@ int wide_choose(adlbq_server *h, int R, const int *d_reqs) {
     if ((rc = rsx_sort_pairs(h->d_wtmp, h->cap_wtmp, h->d_wk0, h->d_wk1, h->d_wv0, h->d_wv1, n, 0, 32, false, s)))
         return rc;
     const unsigned nb = (unsigned)std::max(1, (n + 255) / 256);
-    if (n > 0) k_wide_key<<<nb, 256, 0, s>>>(n, 1, h->d_wv1, h->d_prio, h->d_meta, h->d_cold1, h->A, h->d_wk0);
+    // run key: (target rank, or A for untargeted, or A + 1) above the type index's sh bits
+    const int vw = h->T > VW_TYPES ? 1 : 0;
+    int sh = 8, tb = 1;
+    while ((1ll << sh) < h->T) sh++;
+    while ((1ll << tb) < (long long)h->A + 2) tb++;
+    if (n > 0) k_wide_key<<<nb, 256, 0, s>>>(n, 1, h->d_wv1, h->d_prio, h->d_meta, h->d_cold1, h->A, sh, vw, h->d_wk0);
     if ((rc = rsx_sort_pairs(h->d_wtmp, h->cap_wtmp, h->d_wk0, h->d_wk1, h->d_wv1, h->d_wv0, n, 0, 32, false, s)))
         return rc;
-    if (n > 0) k_wide_key<<<nb, 256, 0, s>>>(n, 2, h->d_wv0, h->d_prio, h->d_meta, h->d_cold1, h->A, h->d_wk0);
-    if ((rc = rsx_sort_pairs(h->d_wtmp, h->cap_wtmp, h->d_wk0, h->d_wk1, h->d_wv0, h->d_wv1, n, 0, 40, false, s)))
+    if (n > 0) k_wide_key<<<nb, 256, 0, s>>>(n, 2, h->d_wv0, h->d_prio, h->d_meta, h->d_cold1, h->A, sh, vw, h->d_wk0);
+    if ((rc = rsx_sort_pairs(h->d_wtmp, h->cap_wtmp, h->d_wk0, h->d_wk1, h->d_wv0, h->d_wv1, n, 0, sh + tb, false, s)))
         return rc;
     if (n > 0)
         k_wide_ekey<<<nb, 256, 0, s>>>(n, h->d_wv1, h->d_prio, h->d_seq, h->d_wk1, h->d_wekey, h->d_wflag);
     k_wide_runs<<<1, 1024, 0, s>>>(n, h->d_wflag, h->d_wk1, h->d_wrkey, h->d_wrstart, h->d_whead, h->d_wcnt);
     k_wide_prep<<<(R + 255) / 256, 256, 0, s>>>(d_reqs, R, h->d_utypes, h->T, h->A, h->d_wrkey, h->d_wcnt, h->d_wreq,
-                                                h->d_rh, h->d_tmatch, h->d_umatch);
+                                                h->d_rh, h->d_tmatch, h->d_umatch, sh, vw ? h->d_utsorted : nullptr,
+                                                h->n_utsorted);
     k_wide_choose<<<1, 256, 0, s>>>(h->d_wreq, R, h->d_wrstart, h->d_whead, h->d_wekey, h->d_wv1, h->d_tmatch);
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;

@@ -989,15 +989,22 @@ def main():
     torch.cuda.synchronize()
     HACC_M = ("req_cap", "tables", "rq_cap", "scan_cap", "l_scan", "sort", "l_rank", "l_chain", "l_fin", "total")
     hacc0 = {k: srv.stat("hacc:" + k) for k in HACC_M}
+    t_enq = []
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
+        t_enq.append(time.perf_counter())
     t_submit = time.perf_counter() - t0  # host time to enqueue the K steps
-    host_sections = {k: round((srv.stat("hacc:" + k) - hacc0[k]) / 1e6 / max(args.steps, 1), 4) for k in HACC_M}
     torch.cuda.synchronize()
+    t_sync = time.perf_counter()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    host_sections = {k: round((srv.stat("hacc:" + k) - hacc0[k]) / 1e6 / max(args.steps, 1), 4) for k in HACC_M}
+    # where the timed region's host time went: the first step's enqueue, the rest, the final wait
+    enqueue_ms = {"first": round((t_enq[0] - t0) * 1e3, 4) if t_enq else None,
+                  "rest_per_step": round((t_enq[-1] - t_enq[0]) * 1e3 / max(len(t_enq) - 1, 1), 4) if t_enq else None,
+                  "sync_wait": round((t_sync - t_enq[-1]) * 1e3, 4) if t_enq else None}
     matched = int((d_resp[args.warmup:, :, 0] == 1).sum().item())
     if world > 1:
         el, matched = shards.reduce_step_timing(el, matched)
@@ -1111,6 +1118,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el * 1e3 / args.steps,
         "host_submit_ms_per_step": round(t_submit * 1e3 / args.steps, 4),
+        "timed_region_host_ms": enqueue_ms,
         "reserve_host_sections_ms_per_step": host_sections,
         "host_buffer_path": host_path,
         "higher_is_better": True,

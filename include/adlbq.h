@@ -32,12 +32,13 @@ extern "C" {
 #define ADLBQ_ERR_HIP           -2   /* HIP runtime failure (message via adlbq_last_error) */
 #define ADLBQ_ERR_NOMEM         -3
 #define ADLBQ_ERR_TYPE          -4   /* work type not declared at create (ADLBP_Put aborts: adlb.c:2762) */
-#define ADLBQ_ERR_UNSUPPORTED   -5   /* e.g. more than ADLBQ_MAX_TYPES_WIDE types, or a steal export over 64 */
+#define ADLBQ_ERR_UNSUPPORTED   -5   /* e.g. more than ADLBQ_MAX_TYPES_VWIDE types, or a steal export over 64 */
 #define ADLBQ_ERR_DEVICE        -6   /* a device-side wait gave up: the batch was answered ADLB_ERROR
                                         (-1 in word 0 of every reply), nothing pinned or parked */
 
 #define ADLBQ_MAX_TYPES          64  /* request type sets are 64-bit masks on the device */
 #define ADLBQ_MAX_TYPES_WIDE    255  /* more types than 64: a correct, slower Reserve path (adlbq_wide.hip) */
+#define ADLBQ_MAX_TYPES_VWIDE  (1 << 22) /* more than 255: the same path, every page wide (type index bits in meta) */
 #define ADLBQ_REQ_TYPES          16  /* REQ_TYPE_VECT_SZ, src/xq.h:37 */
 #define ADLBQ_RESP_INTS          12  /* TA_RESERVE_RESP int[12], src/adlb.c:1213-1222 */
 #define ADLBQ_PUT_INTS            9

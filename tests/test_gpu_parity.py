@@ -153,6 +153,24 @@ def test_dead_pages_recycled_vs_oracle(gpu_available, recycle):
         assert st["pages_recycled"] == 0, st
 
 
+def _sparse_types(w, seed):
+    """The workload with its declared type values spread over [0, 10010) (the reference's DBG arrays
+    index by value below 10010, adlb.c:343-356), shuffled, and one value declared twice at the end
+    (get_type_idx keeps the first index, adlb.c:3476-3485)."""
+    rng = np.random.default_rng(seed)
+    T = len(w.user_types)
+    vals = rng.choice(10010, size=T, replace=False).astype(np.int32)
+    remap = {int(a): int(b) for a, b in zip(w.user_types, vals)}
+    w.u_type = vals[np.searchsorted(w.user_types, w.u_type)]
+    rt = w.r_types.copy()
+    m = rt >= 0
+    rt[m] = vals[np.searchsorted(w.user_types, rt[m])]
+    w.r_types = rt
+    w.user_types = np.concatenate([vals, vals[:1]])
+    assert len(remap) == T
+    return w
+
+
 CASES = {
     "c2_n200k_r16k": lambda: synth.config2(n_units=200_000, n_reserves=16_384, seed=201),
     "c2_eq_n200k_r16k": lambda: synth.config2(n_units=200_000, n_reserves=16_384, seed=202, equal_prio=True),
@@ -179,6 +197,13 @@ CASES = {
     "w150_c4": lambda: synth.config4(n_units=50_000, n_types=150, n_reserves=4096, n_ranks=128, seed=241,
                                      prio_hi=512),
     "w255_exhaust": lambda: synth.config2(n_units=4_000, n_types=255, n_reserves=6000, seed=242, prio_hi=8),
+    # more than 255 types (get_type_idx has no bound, adlb.c:3476-3485): the type index's high bits in
+    # meta, every page wide; declared values spread out, shuffled and repeated (first declared index wins)
+    "w300_c2": lambda: synth.config2(n_units=60_000, n_types=300, n_reserves=8192, seed=243, prio_hi=256),
+    "w300_c4": lambda: synth.config4(n_units=60_000, n_types=300, n_reserves=4096, n_ranks=128, seed=244,
+                                     prio_hi=512),
+    "w1000_sparse": lambda: _sparse_types(synth.config2(n_units=40_000, n_types=1000, n_reserves=6000, seed=245,
+                                                        prio_hi=64), seed=246),
     # 8 < T <= 64 (keyrank): keys varying only in the bucket position, and over the whole int32 range
     "c2_t16_eq": lambda: synth.config2(n_units=100_000, n_types=16, n_reserves=8192, seed=233, equal_prio=True),
     "c2_t32_extreme": lambda: synth.config2(n_units=100_000, n_types=32, n_reserves=8192, seed=234, wide_frac=0.05,
@@ -724,3 +749,45 @@ def test_single_reserve_exhaustion_parks_vs_oracle(gpu_available):
         used = s.stat("one_batches")
     assert_same(got, run_oracle(w.user_types, cfg, tr))
     assert used == w.r_rank.size, used
+
+
+@pytest.mark.parametrize("T", [4, 8])
+def test_one_and_pipeline_batches_interleaved_vs_oracle(gpu_available, T):
+    """k_reserve_one (one-Reserve batches) alternating with pipeline batches of
+    ~1024 Reserves and Put batches on an open bucket of more than 10 pages: the
+    state one path leaves for the other (anchors, guessed cuts, the landed
+    snapshot's plan / keyrank / rank hints) never changes a result."""
+    rng = np.random.default_rng(80 + T)
+    ut, A = np.arange(T, dtype=np.int32), 2048
+    o = oracle.Oracle("own")
+    o.init(ut, A, 1, 0)
+    trace, exp = [], []
+
+    def step(ev):
+        ev = np.asarray(ev, dtype=np.int32).ravel()
+        out = o.replay(ev)
+        trace.append(ev)
+        exp.append(out)
+        return synth.split_outputs(out)
+
+    def puts(n):
+        return [[synth.OP_PUT, int(rng.choice(ut)), int(rng.integers(0, 200)), 0, -1, 8, -1, 0, -1, -1]
+                for _ in range(n)]
+
+    def reserves(R):
+        ranks = rng.integers(0, A, size=R)
+        return ranks, step(synth.reserve_events(ranks, synth.type_vectors(rng, ut, R), np.ones(R, np.uint8)))
+
+    step(puts(50_000))  # 13 pages
+    for rnd in range(30):
+        for R in (1, 1024, 1, 1, 700, 1):
+            ranks, outs = reserves(R)
+            if rnd % 3 == 2:  # Gets of some matches: units leave the bucket
+                gets = [[synth.OP_GET, int(r), int(x[5])] for r, x in zip(ranks, outs) if x[0] == 1][::2]
+                if gets:
+                    step(gets)
+        step(puts(int(rng.integers(200, 1500))))
+    with Server(ut, A, 1, 0, max_units=1 << 17) as s:
+        got = replay.replay(s, np.concatenate(trace))
+        assert s.stat("one_batches") > 0
+    assert_same(got, np.concatenate(exp))

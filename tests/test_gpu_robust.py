@@ -113,3 +113,31 @@ def test_rqseqno_overflow_is_nomem(gpu_available):
         with pytest.raises(AdlbqError, match="rc=-3"):
             s.reserve_batch([[4, 1, 1] + [-2] * 15] * 64)     # could take rqseqnos past INT_MAX
         assert s.stat("rq_next") == (1 << 31) - 1 - 50
+
+
+@pytest.mark.parametrize("path,n_units,n_res", [("small", 9_000, 700), ("one", 30_000, 1)])
+def test_choice_outside_page_list_is_an_error(gpu_available, path, n_units, n_res):
+    """The round-5 fault: a choice of the one-workgroup paths
+    (k_reserve_small, k_reserve_one) whose bucket position lies past the open
+    bucket's page list.  It is driven directly ("bound_inject" tells the next
+    choice such a position): the batch is answered ADLB_ERROR and counted
+    (stat bound_faults), the synchronous entry returns ADLBQ_ERR_DEVICE, nothing
+    is pinned or parked, and the same batch then answers as the oracle does."""
+    w = synth.config2(n_units=n_units, n_reserves=n_res, seed=303)
+    reqs = _reqs18(w)
+    with Server(w.user_types, w.num_app_ranks, max_units=w.n_units) as s:
+        s.put_batch(_units9(w))
+        s.set_param("bound_inject", 1)
+        with pytest.raises(AdlbqError, match="rc=-6"):
+            s.reserve_batch(reqs)
+        assert s.stat("bound_faults") == 1
+        assert s.stat("batch_failed") == 1
+        assert s.info()[2] == 0                 # nothing parked
+        assert s.stat(path + "_batches") == 1   # the path under test took the batch
+        got = s.reserve_batch(reqs)             # the flag is one-shot: the same batch, now correct
+        assert s.stat("bound_faults") == 1
+    o = oracle.Oracle("own")
+    o.init(w.user_types, w.num_app_ranks)
+    o.replay(synth.put_events(w))
+    exp = synth.split_outputs(o.replay(synth.reserve_events(w.r_rank, w.r_types, w.r_hang)))
+    np.testing.assert_array_equal(got, np.asarray(exp, np.int32))

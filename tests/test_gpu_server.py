@@ -264,15 +264,16 @@ def test_mix_steal_group_rccl_one_server():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("np_,ns", [(6, 2), (7, 3)])
-def test_mix_many_types_every_unit_once(np_, ns):
-    """100 declared work types through the relinked library with the steal group
+@pytest.mark.parametrize("np_,ns,nt", [(6, 2, 100), (7, 3, 100), (6, 2, 300)])
+def test_mix_many_types_every_unit_once(np_, ns, nt):
+    """100 (and 300: more than 255, no bound as in get_type_idx, adlb.c:3476-3485) declared work types
+    through the relinked library with the steal group
     left at its default: the engine serves the Reserves on its >64-type path and
     the servers steal by the reference's SS_RFR round trips (the steal group's
     merge holds type sets as 64-bit masks, so every server turns it off at once);
     every unit is consumed exactly once.  The reference's own 100-type stream of
     the 2-server case (mix_np6_s2_t100_r*) replays reply for reply above."""
-    out, got, exp, err = _run_mix(np_, ["-nservers", str(ns), "-n", "120", "-ntypes", "100"],
+    out, got, exp, err = _run_mix(np_, ["-nservers", str(ns), "-n", "120", "-ntypes", str(nt)],
                                   env_extra={"ADLB_STEAL_REPORT": "1"})
     assert got == exp, out[-2000:]
     assert _steal_report(err) == [], err[-2000:]
