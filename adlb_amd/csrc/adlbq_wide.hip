@@ -189,7 +189,8 @@ __global__ __launch_bounds__(256) void k_wide_prep(const int *__restrict__ reqs,
 }
 
 // the requests strictly in order, one workgroup: thread i looks at the i-th
-// run of the request's side, a block max of the heads' keys picks the unit
+// run of the request's side (a wildcard: runs i, i + 256, ...), a block max of
+// the heads' keys picks the unit
 __global__ __launch_bounds__(256) void k_wide_choose(const int *__restrict__ wreq, int R, const int *__restrict__ rstart,
                                                      int *head, const unsigned long long *__restrict__ ekey,
                                                      const int *__restrict__ val, int *__restrict__ tmatch) {
@@ -204,16 +205,17 @@ __global__ __launch_bounds__(256) void k_wide_choose(const int *__restrict__ wre
         for (int side = 0; side < 2 && chosen < 0; side++) {
             const int c = s_row[side];
             const int *oo = s_row + (side ? 18 : 2);
-            int r = -1;
-            if (c < 0) r = oo[0] + tid < oo[1] ? oo[0] + tid : -1;
-            else if (tid < c) r = oo[tid];
-            unsigned long long k = 0;
-            int hd = 0;
-            if (r >= 0) {
-                hd = __hip_atomic_load(head + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (hd < rstart[r + 1]) k = ekey[hd];
+            unsigned long long k = 0;  // the best head this thread sees (keys are unique, 0 = none)
+            int kr = -1;
+            auto look = [&](int r) {
+                const int hd = __hip_atomic_load(head + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (hd < rstart[r + 1] && ekey[hd] > k) k = ekey[hd], kr = r;
+            };
+            if (c < 0) {  // a wildcard: every run of the side, 256 at a time (more than 255 types: more runs)
+                for (int r = oo[0] + tid; r < oo[1]; r += 256) look(r);
+            } else if (tid < c) {
+                look(oo[tid]);
             }
-            int kr = r;
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
                 const unsigned long long k2 = __shfl_xor(k, o, 64);
