@@ -67,6 +67,8 @@ SIGNATURES = {
     "adlbsrv_replay_many": (c_int, [P, c_int, c_int, P, P, P, P, P, P]),
     "adlbsrv_replay_prof": (None, [P]),
     "adlbsrv_replay_rounds": (c_int, [P, c_int, c_int, P, P, c_int, c_int, P, P, P, P, ctypes.c_longlong, P, P, P]),
+    "adlbsrv_replay_rounds2": (c_int, [P, c_int, c_int, P, P, c_int, c_int, P, P, P, P, ctypes.c_longlong, P, P, P,
+                                       c_int, P]),
     "adlbsrv_replay_error": (ctypes.c_char_p, []),
 }
 

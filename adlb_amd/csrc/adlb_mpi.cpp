@@ -25,14 +25,19 @@
 // the units it donates.  A server takes no other message between its export
 // and its settle, so the merge sees every queue as it is applied.
 // ADLB_STEAL_GROUP=0 keeps the reference's SS_RFR protocol.
-// ADLB_STEAL_RCCL=1: the blobs stay in device memory and are all-gathered by
-// RCCL (one server per GPU; the ncclUniqueId goes out by MPI_Bcast among the
-// servers); if any server cannot join the communicator, every server keeps
-// the host all-gather.
+// Steal transport: when every server of the group owns a distinct GPU (PCI
+// bus ids all-gathered at startup), the blobs stay in device memory and are
+// all-gathered by RCCL over xGMI (the ncclUniqueId goes out by MPI_Bcast among
+// the servers); otherwise, or if any server cannot load librccl (dlopen, so a
+// relinked application needs RCCL only where it is used) or join the
+// communicator, every server keeps the host MPI_Allgather.
+// ADLB_STEAL_RCCL=0 forces MPI_Allgather, =1 tries RCCL even on a shared GPU.
+// ADLB_STEAL_REPORT prints the transport chosen.
 #include <mpi.h>
 
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
-#include <rccl/rccl.h>
+#include <rccl/rccl.h>  // types only: the entry points come from dlopen (rccl_load)
 
 #include <algorithm>
 #include <cstdarg>
@@ -107,22 +112,67 @@ struct Loop {
 };
 Loop *g_loop = nullptr;
 
-// the steal round's device all-gather (ADLB_STEAL_RCCL)
+// the steal round's device all-gather (RCCL)
 struct Rccl {
     ncclComm_t comm = nullptr;
     int *d_blob = nullptr, *d_all = nullptr;
     hipStream_t st = nullptr;
 } g_rccl;
 
-// collective over the servers: true when every server joined the communicator
+// librccl's entry points, loaded on first use
+struct RcclApi {
+    void *lib = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+} g_nccl;
+
+bool rccl_load() {
+    if (g_nccl.lib) return true;
+    for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1", "/opt/rocm/lib/librccl.so"})
+        if ((g_nccl.lib = dlopen(name, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!g_nccl.lib) return false;
+    g_nccl.get_unique_id = (decltype(g_nccl.get_unique_id))dlsym(g_nccl.lib, "ncclGetUniqueId");
+    g_nccl.comm_init_rank = (decltype(g_nccl.comm_init_rank))dlsym(g_nccl.lib, "ncclCommInitRank");
+    g_nccl.all_gather = (decltype(g_nccl.all_gather))dlsym(g_nccl.lib, "ncclAllGather");
+    g_nccl.comm_destroy = (decltype(g_nccl.comm_destroy))dlsym(g_nccl.lib, "ncclCommDestroy");
+    if (!g_nccl.get_unique_id || !g_nccl.comm_init_rank || !g_nccl.all_gather || !g_nccl.comm_destroy) {
+        dlclose(g_nccl.lib);
+        g_nccl = RcclApi{};
+        return false;
+    }
+    return true;
+}
+
+// collective over the servers: do they all own a GPU of their own (distinct PCI bus ids)?
+bool servers_distinct_gpus() {
+    char bus[64];
+    memset(bus, 0, sizeof bus);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, dev) != hipSuccess)
+        snprintf(bus, sizeof bus, "unknown:%d", g_rank);  // no id: treated as a GPU of its own
+    std::vector<char> all((size_t)g_S * sizeof bus);
+    MPI_Allgather(bus, (int)sizeof bus, MPI_CHAR, all.data(), (int)sizeof bus, MPI_CHAR, g_srvcomm);
+    for (int a = 0; a < g_S; a++)
+        for (int b = a + 1; b < g_S; b++)
+            if (!strncmp(&all[(size_t)a * sizeof bus], &all[(size_t)b * sizeof bus], sizeof bus)) return false;
+    return true;
+}
+
+// collective over the servers: true when every server loaded RCCL and joined the communicator
 bool rccl_init(size_t blob_ints) {
-    int me = 0, ok = 1;
+    int me = 0, ok = rccl_load() ? 1 : 0, all = 0;
     MPI_Comm_rank(g_srvcomm, &me);
+    MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, g_srvcomm);
+    if (!all) {
+        if (me == 0) fprintf(stderr, "%06d: RCCL: librccl not loadable, host all-gather kept\n", g_rank);
+        return false;
+    }
     ncclUniqueId id;
     memset(&id, 0, sizeof id);
-    if (me == 0 && ncclGetUniqueId(&id) != ncclSuccess) ok = 0;
+    if (me == 0 && g_nccl.get_unique_id(&id) != ncclSuccess) ok = 0;
     MPI_Bcast(&id, (int)sizeof id, MPI_BYTE, 0, g_srvcomm);
-    int all = 0;
     MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, g_srvcomm);
     if (!all) return false;
     int dev = 0;
@@ -130,19 +180,19 @@ bool rccl_init(size_t blob_ints) {
          hipMalloc((void **)&g_rccl.d_blob, sizeof(int) * blob_ints) == hipSuccess &&
          hipMalloc((void **)&g_rccl.d_all, sizeof(int) * blob_ints * (size_t)g_S) == hipSuccess;
     // every server calls the collective init (a failed allocation joins and leaves after)
-    if (ncclCommInitRank(&g_rccl.comm, g_S, id, me) != ncclSuccess) {
+    if (g_nccl.comm_init_rank(&g_rccl.comm, g_S, id, me) != ncclSuccess) {
         g_rccl.comm = nullptr;
         ok = 0;
     }
     MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_MIN, g_srvcomm);
     if (!all) {
-        if (g_rccl.comm) ncclCommDestroy(g_rccl.comm);
+        if (g_rccl.comm) g_nccl.comm_destroy(g_rccl.comm);
         g_rccl.comm = nullptr;
         if (g_rccl.d_blob) (void)hipFree(g_rccl.d_blob);
         if (g_rccl.d_all) (void)hipFree(g_rccl.d_all);
         if (g_rccl.st) (void)hipStreamDestroy(g_rccl.st);
         g_rccl = Rccl{};
-        if (me == 0) fprintf(stderr, "%06d: ADLB_STEAL_RCCL: RCCL unavailable, host all-gather kept\n", g_rank);
+        if (me == 0) fprintf(stderr, "%06d: RCCL: communicator unavailable, host all-gather kept\n", g_rank);
         return false;
     }
     return true;
@@ -150,7 +200,7 @@ bool rccl_init(size_t blob_ints) {
 
 void rccl_fini() {
     if (!g_rccl.comm) return;
-    ncclCommDestroy(g_rccl.comm);
+    g_nccl.comm_destroy(g_rccl.comm);
     (void)hipFree(g_rccl.d_blob);
     (void)hipFree(g_rccl.d_all);
     (void)hipStreamDestroy(g_rccl.st);
@@ -260,7 +310,7 @@ void steal_round(Loop *L) {
         const size_t n = L->blob.size();
         check(adlbsrv_group_export_device(g_srv, g_rccl.d_blob), "steal round export (device)");
         if (hipDeviceSynchronize() != hipSuccess ||
-            ncclAllGather(g_rccl.d_blob, g_rccl.d_all, n, ncclInt32, g_rccl.comm, g_rccl.st) != ncclSuccess ||
+            g_nccl.all_gather(g_rccl.d_blob, g_rccl.d_all, n, ncclInt32, g_rccl.comm, g_rccl.st) != ncclSuccess ||
             hipStreamSynchronize(g_rccl.st) != hipSuccess)
             die("steal round: RCCL all-gather failed");
         int settled = 0;
@@ -663,8 +713,19 @@ int ADLBP_Server(double hi_malloc, double periodic_logging_time) {
         L.group = true;
         L.blob.assign((size_t)adlbsrv_group_blob_ints(g_srv), 0);
         L.blobs.assign(L.blob.size() * (size_t)g_S, 0);
-        if (env_d("ADLB_STEAL_RCCL", 0.0) != 0.0 && rccl_init(L.blob.size()) && getenv("ADLB_STEAL_REPORT"))
-            fprintf(stderr, "%06d: RCCL all-gather of the steal blobs on (%d servers)\n", g_rank, g_S);
+        // the transport: RCCL when every server owns a GPU of its own (or when forced), else MPI_Allgather
+        const char *rv = getenv("ADLB_STEAL_RCCL");
+        const int mode = rv && *rv ? atoi(rv) : -1;  // -1: automatic
+        const bool distinct = servers_distinct_gpus();  // collective
+        int try_rccl = mode == 0 ? 0 : (mode > 0 || distinct) ? 1 : 0, all_try = 0;
+        MPI_Allreduce(&try_rccl, &all_try, 1, MPI_INT, MPI_MIN, g_srvcomm);
+        const bool on = all_try && rccl_init(L.blob.size());  // collective
+        if (getenv("ADLB_STEAL_REPORT")) {
+            if (on) fprintf(stderr, "%06d: RCCL all-gather of the steal blobs on (%d servers)\n", g_rank, g_S);
+            fprintf(stderr, "%06d: steal transport: %s\n", g_rank,
+                    on ? "rccl" : mode == 0 ? "mpi (ADLB_STEAL_RCCL=0)" : !distinct && mode < 0 ? "mpi (servers share a GPU)"
+                                                                                    : "mpi (RCCL unavailable)");
+        }
     }
     g_loop = &L;
     if (L.my_apps == 0 && g_rank != g_master) emit(&L, g_master, TAG_SRV_DONE, nullptr, 0);

@@ -17,7 +17,9 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <climits>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -245,6 +247,13 @@ struct RShard {
     std::vector<int> hqm;        // QMROW outputs
     int *din = nullptr, *dout = nullptr;
     long long nout_dev = 0;
+    // closed loop: every output lands in mapped host memory (hout, dout its device address) and the
+    // Gets' pairs are written there at run time (hgin, dgin), from the replies that have landed
+    int *hout = nullptr, *hgin = nullptr, *dgin = nullptr;
+    size_t cursor = 0;           // the next call whose replies are not delivered yet
+    long long waits = 0;         // Get calls that had to wait for a reply to land
+    double wait_s = 0.0;
+    long long mismatch = 0;      // replies whose wqseqno differs from the recorded Get's
     std::string err;
     long long ncalls = 0;
     RShard() = default;
@@ -252,9 +261,19 @@ struct RShard {
     RShard &operator=(const RShard &) = delete;
     ~RShard() {  // every return path of adlbsrv_replay_rounds, early errors included
         if (din) (void)hipFree(din);
-        if (dout) (void)hipFree(dout);
+        if (hout) (void)hipHostFree(hout);
+        else if (dout) (void)hipFree(dout);
+        if (hgin) (void)hipHostFree(hgin);
     }
 };
+
+// a word of mapped host memory the device writes once (INT_MIN until then)
+inline int landed(const int *p) {
+    int v;
+    while ((v = __atomic_load_n(p, __ATOMIC_ACQUIRE)) == INT_MIN) {
+    }
+    return v;
+}
 
 namespace {
 int out_ints(int op, int T) {
@@ -326,13 +345,32 @@ int adlbsrv_replay_many(adlbq_server **hs, int n, int ntypes, const int *const *
 }
 
 
+// closed: a shard issues a Get only once the reply it depends on has landed (its Reserve's
+// TA_RESERVE_RESP, the Put that matched its parked Reserve, or the steal round's answer), with the
+// wqseqno taken from that reply, as a live server's app does (tsp.c:157-162); the replies land in
+// mapped host memory and are polled there (no stream synchronisation).  cl_stats (may be null):
+// {Get calls that waited, seconds waited, replies whose wqseqno differs from the recorded Get's}.
+int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
+                           int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
+                           int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls,
+                           int closed, double *cl_stats);
+
 int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
                           int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
                           int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls) {
+    return adlbsrv_replay_rounds2(hs, S, ntypes, traces, lens, k, rqcap, outs, caps, nouts, steals, steal_cap, nsteals,
+                                  seconds, ncalls, 0, nullptr);
+}
+
+int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
+                           int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
+                           int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls,
+                           int closed, double *cl_stats) {
     if (!hs || S < 1 || !traces || !lens || !outs || !caps || !nouts || !steals || !nsteals) {
         g_rerr = "adlbsrv_replay_rounds: bad argument";
         return -1;
     }
+    int A = 0;  // app ranks (closed loop: a reply slot per rank)
     const int T = ntypes;
     std::vector<RShard> sh((size_t)S);
     long long nround = -1;
@@ -381,12 +419,36 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
             return -1;
         }
         if (hipMalloc((void **)&r.din, sizeof(int) * std::max<size_t>(r.hin.size(), 1)) != hipSuccess ||
-            hipMalloc((void **)&r.dout, sizeof(int) * std::max<long long>(r.nout_dev, 1)) != hipSuccess ||
             hipMemcpy(r.din, r.hin.data(), sizeof(int) * r.hin.size(), hipMemcpyHostToDevice) != hipSuccess) {
             g_rerr = "adlbsrv_replay_rounds: device staging";
             return -1;
         }
+        if (!closed) {
+            if (hipMalloc((void **)&r.dout, sizeof(int) * std::max<long long>(r.nout_dev, 1)) != hipSuccess) {
+                g_rerr = "adlbsrv_replay_rounds: device staging";
+                return -1;
+            }
+        } else {
+            const size_t no = (size_t)std::max<long long>(r.nout_dev, 1), ni = std::max<size_t>(r.hin.size(), 1);
+            if (hipHostMalloc((void **)&r.hout, sizeof(int) * no, hipHostMallocMapped) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&r.dout, r.hout, 0) != hipSuccess ||
+                hipHostMalloc((void **)&r.hgin, sizeof(int) * ni, hipHostMallocMapped) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&r.dgin, r.hgin, 0) != hipSuccess) {
+                g_rerr = "adlbsrv_replay_rounds: mapped staging";
+                return -1;
+            }
+            for (size_t q = 0; q < no; q++) r.hout[q] = INT_MIN;  // every reply word is polled until written
+            for (long long q = 0; q < n;) {  // the largest rank any event names
+                const int op = tr[q], w2 = 1 + nargs(op, T);
+                if (op == OP_RESERVE || op == OP_GET) A = std::max(A, tr[q + 1] + 1);
+                q += w2;
+            }
+        }
     }
+    // closed loop: the reply each rank holds (its wqseqno; 0: none), written by the thread of the
+    // shard that answered (or the round, under its barrier), read by the thread whose shard holds the unit
+    std::vector<std::atomic<int>> held((size_t)std::max(A, 1));
+    for (auto &x : held) x.store(0, std::memory_order_relaxed);
     adlbq_steal_group *g = nullptr;
     if (adlbq_steal_group_create(&g, hs, S, k, rqcap)) {
         g_rerr = std::string("adlbq_steal_group_create: ") + adlbq_last_error();
@@ -419,8 +481,12 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
                         gerr = std::string("steal round responses: ") + adlbq_last_error();
                         failed = true;
                     } else {
-                        for (int q = 0; q < cnt && ns < steal_cap; q++, ns++)
+                        for (int q = 0; q < cnt && ns < steal_cap; q++, ns++) {
                             std::memcpy(steals + 15 * ns, resp.data() + 15 * q, sizeof(int) * 15);
+                            const int *row = resp.data() + 15 * q;  // {shard, rqseqno, rank, resp[12]}
+                            if (closed && row[3] == 1 && row[2] >= 0 && row[2] < A)
+                                held[(size_t)row[2]].store(row[3 + 5], std::memory_order_relaxed);
+                        }
                         if (cnt && ns >= steal_cap) {
                             gerr = "steal output full";
                             failed = true;
@@ -454,10 +520,54 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
             const auto c0 = clk::now();
             const int slot = c.op == OP_PUT ? 0 : c.op == OP_RESERVE ? 1 : c.op == OP_GET ? 2 : c.op == OP_QMROW ? 3
                              : c.op == OP_SETROW ? 4 : 5;
+            const int *gin = r.din + c.in;
+            if (closed && c.op == OP_GET) {
+                // every Get's reply: deliver the replies of earlier calls in order until it is held
+                const size_t ci = (size_t)(&c - r.calls.data());
+                bool waited = false;
+                const auto w0 = clk::now();
+                for (int e = 0; e < c.n && ok; e++) {
+                    const int rank = c.x[3 * e], want = c.x[3 * e + 1];  // the recorded {op, rank, wqseqno}
+                    while (held[(size_t)rank].load(std::memory_order_relaxed) == 0 && r.cursor < ci) {
+                        const RCall &d = r.calls[r.cursor++];
+                        if (d.op == OP_RESERVE) {
+                            for (int q = 0; q < d.n; q++) {
+                                const int *o = r.hout + d.dout + (long long)q * ADLBQ_RESP_INTS;
+                                if (__atomic_load_n(o, __ATOMIC_ACQUIRE) == INT_MIN) waited = true;
+                                if (landed(o) == 1)  // TA_RESERVE_RESP success: the rank holds [5]
+                                    held[(size_t)r.hin[(size_t)(d.in + (long long)q * ADLBQ_RESERVE_INTS)]].store(
+                                        landed(o + 5), std::memory_order_relaxed);
+                            }
+                        } else if (d.op == OP_PUT) {
+                            for (int q = 0; q < d.n; q++) {
+                                const int *o = r.hout + d.dout + 3ll * q;
+                                if (__atomic_load_n(o + 1, __ATOMIC_ACQUIRE) == INT_MIN) waited = true;
+                                const int mr = landed(o + 1);  // a parked Reserve matched: its rank holds [0]
+                                if (mr >= 0 && mr < A) held[(size_t)mr].store(landed(o), std::memory_order_relaxed);
+                            }
+                        }
+                    }
+                    const int got = held[(size_t)rank].exchange(0, std::memory_order_relaxed);
+                    if (got == 0) {
+                        r.err = "closed loop: a Get whose reply never arrived (rank " + std::to_string(rank) + ")";
+                        ok = false;
+                        break;
+                    }
+                    r.mismatch += got != want;
+                    r.hgin[(size_t)(c.in + 2ll * e)] = rank;
+                    r.hgin[(size_t)(c.in + 2ll * e + 1)] = got;
+                }
+                if (!ok) continue;
+                if (waited) {
+                    r.waits++;
+                    r.wait_s += std::chrono::duration<double>(clk::now() - w0).count();
+                }
+                gin = r.dgin + c.in;
+            }
             switch (c.op) {
             case OP_PUT: rc = adlbq_put_batch_device(h, c.n, r.put.data() + c.in, r.dout + c.dout); break;
             case OP_RESERVE: rc = adlbq_reserve_batch_device(h, c.n, r.din + c.in, r.dout + c.dout); break;
-            case OP_GET: rc = adlbq_get_reserved_batch_device(h, c.n, r.din + c.in, r.dout + c.dout); break;
+            case OP_GET: rc = adlbq_get_reserved_batch_device(h, c.n, gin, r.dout + c.dout); break;
             case OP_QMROW: rc = adlbq_qmstat_row(h, &r.hqm[(size_t)c.hout], &r.hqm[(size_t)c.hout + 1]); break;
             case OP_SETROW: rc = adlbq_set_qmstat_row(h, c.x[0], c.x[1], (double)c.x[2], c.x + 3); break;
             case OP_ROUND: ok = round_barrier(true); break;
@@ -500,7 +610,9 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
             break;
         }
         std::vector<int> dv((size_t)std::max<long long>(r.nout_dev, 1));
-        if (hipMemcpy(dv.data(), r.dout, sizeof(int) * r.nout_dev, hipMemcpyDeviceToHost) != hipSuccess) {
+        if (r.hout) {
+            std::memcpy(dv.data(), r.hout, sizeof(int) * r.nout_dev);
+        } else if (hipMemcpy(dv.data(), r.dout, sizeof(int) * r.nout_dev, hipMemcpyDeviceToHost) != hipSuccess) {
             g_rerr = "output copy";
             rc = -1;
             break;
@@ -524,6 +636,14 @@ int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const
         if (o.over) {
             g_rerr = "shard " + std::to_string(j) + ": output buffer too small";
             rc = -2;
+        }
+    }
+    if (cl_stats) {
+        cl_stats[0] = cl_stats[1] = cl_stats[2] = 0.0;
+        for (const auto &r : sh) {
+            cl_stats[0] += (double)r.waits;
+            cl_stats[1] += r.wait_s;
+            cl_stats[2] += (double)r.mismatch;
         }
     }
     if (!rc && (failed || !gerr.empty())) {

@@ -329,6 +329,11 @@ struct adlbq_server {
     long long chain_modes = -1;        // bit k-1: round k uses prefix starts, -1 = auto ("chain_modes")
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
+    int fuse_rank_chain = 1;           // "fuse_rank_chain": k_rank's blocks in the chain's launch (T <= 8)
+    unsigned long long rank_arrivals = 0;  // rank blocks launched in k_rank_chain0 so far (their counter's target)
+    int *d_jpref = nullptr;            // [cap_req / 64 + 1] exclusive prefix of seg_cnt (k_thresholds' extra workgroup)
+    bool jpref_ok = false;             // this batch's k_thresholds wrote d_jpref
+    bool open_all_narrow = false;      // every page of the open bucket is narrow (sync_tables)
     // dead open pages (no LIVE unit; full, never the tail): found by k_page_dead in the background
     // (flags in mapped host memory, applied once its event has passed), then reused by Puts
     std::vector<int> free_pages;

@@ -219,6 +219,7 @@ struct HistArgs {
     long long zn;
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
     unsigned long long *kst = nullptr;  // diagnostic stamps, or nullptr
+    int all_narrow = 0;        // every open page is narrow (packed offsets): pwide is not read
 };
 
 // A quarter page (16 units per lane) of the scan columns.  A narrow page's
@@ -577,7 +578,8 @@ __device__ __forceinline__ void hist_pages(const HistArgs &a, const int q, unsig
     const int fill = !valid ? 0 : (p == a.npages - 1) ? a.tail_fill : PAGE;
     unsigned int *h = hist + half * hist_page_words(a.T * NB, TB <= 8);
     if (valid && a.kst && (threadIdx.x & (256 / PP - 1)) == 0) a.kst[(long long)p * 4] = __builtin_amdgcn_s_memrealtime();
-    if (a.pwide[pg]) hist_page_body<false, (TB <= 8), TB, PP>(a, p, pg, fill, h, valid);
+    // every open page narrow (the host's count): no dependent load of the flag before the meta loads
+    if (!a.all_narrow && a.pwide[pg]) hist_page_body<false, (TB <= 8), TB, PP>(a, p, pg, fill, h, valid);
     else hist_page_body<true, (TB <= 8), TB, PP>(a, p, pg, fill, h, valid);
 }
 
@@ -733,14 +735,49 @@ __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn,
                    guess, gcut, T);
 }
 
+// The exclusive prefix of seg_cnt per 64 requests (jp[q] = requests before 64 q that may take an
+// untargeted unit): the chain's level guess reads one word instead of summing up to 1,024 (one
+// dependent load round fewer in its prologue).  One workgroup of TH_THREADS.
+__device__ __forceinline__ void seg_prefix(const int *__restrict__ seg_cnt, int nq, int *jp) {
+    __shared__ int wtot[TH_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int base = 0;
+    for (int q0 = 0; q0 < nq; q0 += TH_THREADS) {
+        const int q = q0 + tid;
+        const int v = q < nq ? seg_cnt[q] : 0;
+        int x = v;  // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wtot[w] = x;
+        __syncthreads();
+        int pre = base;
+        for (int k = 0; k < w; k++) pre += wtot[k];
+        if (q < nq) jp[q] = pre + x - v;
+        int tot = 0;
+        for (int k = 0; k < TH_THREADS / 64; k++) tot += wtot[k];
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) jp[nq] = base;
+}
+
 __global__ __launch_bounds__(TH_THREADS) void k_thresholds(unsigned int *zcs, long long zn, int T, const int *__restrict__ dem, unsigned int *csum,
                                                      int nchunks, int *theta, int *need, int *candlen,
                                                      int *needsort, int *binoff, unsigned int *coltot,
                                                      int *type_cnt, const long long *__restrict__ anchor,
                                                      long long *__restrict__ anchor_next,
                                                      long long *__restrict__ gcut_next, int guess,
-                                                     const long long *__restrict__ gcut) {
-    thresholds_body(zcs, zn, T, dem, csum, nchunks, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next, guess, gcut, blockIdx.x, gridDim.x);
+                                                     const long long *__restrict__ gcut, const int *seg_cnt = nullptr,
+                                                     int nq = 0, int *jp = nullptr) {
+    if (jp != nullptr && blockIdx.x == gridDim.x - 1) {  // the launch's extra workgroup
+        seg_prefix(seg_cnt, nq, jp);
+        return;
+    }
+    thresholds_body(zcs, zn, T, dem, csum, nchunks, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor,
+                    anchor_next, gcut_next, guess, gcut, blockIdx.x, gridDim.x - (jp != nullptr ? 1 : 0));
 }
 
 // Pass 1 and the request preparation in one launch (they are independent):
@@ -2303,6 +2340,12 @@ struct ChainArgs {
     const int *lv;                   // [R][T] k_rank's level rows (T <= 8), else nullptr
     const unsigned char *rtype;      // [R] type index of the candidate at each global rank (with lv)
     unsigned long long *stamps;      // [nseg][8] s_memrealtime per phase (diagnostic build of the run), or nullptr
+    // k_rank_chain0 (k_rank's blocks in the chain's launch): their arrival counter (monotone) and the
+    // value it reaches once this launch's rank blocks are done; nullptr when k_rank ran as a launch
+    const unsigned long long *rdone;
+    unsigned long long rtarget;
+    const int *needsort;             // [T] (k_thresholds): a list k_rank sorts
+    const int *jpref;                // [R/64 + 1] exclusive prefix of seg_cnt (k_thresholds), or nullptr: summed here
 };
 
 // diagnostic phase stamps (100 MHz constant clock), lane 0 of a segment
@@ -2997,6 +3040,9 @@ __device__ void park_tail(const DonorCtx &c, int donors, const int *__restrict__
     for (int q = w0; q < w1; q++) {
         unsigned long long b = q - w0 < MAXW ? bits[q - w0]
                                              : __hip_atomic_load(pmask + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // read for the last time: zero again for the next batch (its waves write only non-zero words)
+        if (b) __hip_atomic_store(const_cast<unsigned long long *>(pmask) + q, 0ull, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
         for (; b; b &= b - 1) {
             const int jj = q * 64 + __ffsll((long long)b) - 1;
             const int *rq = reqs + (long long)ADLBQ_RESERVE_INTS * jj;
@@ -3218,10 +3264,12 @@ __device__ __forceinline__ void finalize_body(FinArgs f, const int bid_, const i
     if (j < f.R) {
         const bool parks = !failed && rk.y && tm < 0 && um < 0;
         const unsigned long long pb = __ballot(parks);
-        if ((threadIdx.x & 63) == 0) {
-            // published for the last workgroup's park (write-through, drained before the arrival below)
+        if ((threadIdx.x & 63) == 0 && pb) {
+            // published for the last workgroup's park (write-through, drained before the arrival below);
+            // a wave with nothing parked writes nothing: park_tail zeroes the words it read, so every word
+            // is zero at the start of a batch
             __hip_atomic_store(f.pmask + (j >> 6), pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (pb) atomicAdd(&s_parked, __popcll(pb));
+            atomicAdd(&s_parked, __popcll(pb));
             __builtin_amdgcn_s_waitcnt(0);  // this wave's store has landed before the block arrives
         }
     }
@@ -3385,7 +3433,7 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
         a.umatch[0] = um;
         const int2 rk = f.rh[0];
         const bool parks = !bad && rk.y && um < 0;
-        __hip_atomic_store(f.pmask, parks ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (parks) __hip_atomic_store(f.pmask, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // zero otherwise
         fin_request(f, 0, bad, rk, -1, um);
         s_last = (parks ? 1 : 0) | (bad ? 2 : 0);
     }
@@ -3424,8 +3472,32 @@ __device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefi
     }
     // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
     const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
+    // J from the prefix k_thresholds left, unless k_rank changed seg_cnt since (a type with no candidate)
+    const int jpv = a.jpref != nullptr ? a.jpref[jb >> 6] : 0;
+    const bool use_jp = a.jpref != nullptr && __ballot(lane < T && my_len == 0) == 0ull;
+    if (a.rdone != nullptr) {
+        // k_rank's blocks ride in this launch (k_rank_chain0).  They write what the chain reads (ranks, level
+        // rows, seg_cnt) only when k_select_open did not rank the candidates, a list needs sorting or a type
+        // has no candidate at all -- the conditions of rank_body's own early return; then wait for every
+        // rank block's arrival (release there, acquire here: MI355X_MICROARCH.md, inter-workgroup visibility)
+        const int ns = lane < T ? a.needsort[lane] : 0;
+        const bool slow = ld_sc1(&a.ctr->rank_fast) == 0 || __ballot(ns == 1 && my_len > 1) != 0ull ||
+                          __ballot(lane < T && my_len == 0) != 0ull;
+        if (slow) {
+            if (lane == 0) {
+                while (__hip_atomic_load(a.rdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.rtarget)
+                    __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_wave_barrier();
+            __syncthreads();
+        }
+    }
     int J = 0;  // requests before jb that take an untargeted unit
-    {
+    if (use_jp) {
+        J = jpv;
+    } else {
         const int nq = jb >> 6;
         int cv[16];
 #pragma unroll
@@ -3433,9 +3505,9 @@ __device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefi
 #pragma unroll
         for (int u = 0; u < 16; u++) J += cv[u];
         for (int q = 1024 + lane; q < nq; q += 64) J += a.seg_cnt[q];  // batches above 65,536 Reserves
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
+        for (int o = 32; o > 0; o >>= 1) J += __shfl_xor(J, o, 64);
+    }
     int guess;
     if (a.lv != nullptr) {  // T <= 8: the level state at J is k_rank's row J (every head at one level)
         const int G = __builtin_amdgcn_readlane(my_off, T);
@@ -3507,6 +3579,29 @@ __device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefi
 template <int TB>
 __global__ __launch_bounds__(64) void k_chain0(ChainArgs a, ChainPass cp, int prefix_next, int final) {
     chain0_body<TB>(a, cp, prefix_next, final, blockIdx.x, gridDim.x);
+}
+
+// k_rank and round 0 of the chain as one launch (T <= 8): blocks [0, rg) are
+// k_rank's (64 threads each), the rest the chain's segments.  In the usual case
+// (k_select_open ranked the candidates) the rank blocks have nothing the chain
+// reads and the segments never wait; otherwise each segment waits for every
+// rank block's arrival.  The segments cannot hold back a rank block: each CU
+// has room for a rank block beside a segment, whatever the dispatch order.
+template <int TB>
+__global__ __launch_bounds__(64) void k_rank_chain0(RankArgs ra, int rg, ChainArgs a, ChainPass cp, int prefix_next,
+                                                    int final) {
+    if ((int)blockIdx.x < rg) {
+        rank_body<64>(ra, blockIdx.x, rg);
+        __syncthreads();
+        if (threadIdx.x == 0) {  // one wave: its stores drained, written back, then the arrival
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            atomicAdd(const_cast<unsigned long long *>(a.rdone), 1ull);
+        }
+        return;
+    }
+    chain0_body<TB>(a, cp, prefix_next, final, (int)blockIdx.x - rg, (int)gridDim.x - rg);
 }
 
 // ---------------------------------------------------------------- one launch per kernel for a group of handles
@@ -3638,10 +3733,11 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipStreamSynchronize(h->stream));
     void *ps[] = {h->d_mask, h->d_tmatch, h->d_umatch, h->d_mslot, h->d_rh, h->d_reqbuf, h->d_respbuf,
                   h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_cht,
-                  h->d_chcnt, h->d_chE, h->d_chflag, h->d_pmask, h->d_lv, h->d_rtype};
+                  h->d_chcnt, h->d_chE, h->d_chflag, h->d_pmask, h->d_lv, h->d_rtype, h->d_jpref};
     for (void *p : ps)
         if (p) AQ_HIP(hipFree(p));
     AQ_HIP(hipMalloc((void **)&h->d_mask, sizeof(unsigned long long) * nc));
+    AQ_HIP(hipMalloc((void **)&h->d_jpref, sizeof(int) * ((nc + 63) / 64 + 1)));
     AQ_HIP(hipMalloc((void **)&h->d_tmatch, sizeof(int) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_umatch, sizeof(int) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_mslot, sizeof(int) * nc));
@@ -3652,6 +3748,7 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
     AQ_HIP(hipMalloc((void **)&h->d_seg_cnt, sizeof(int) * ((nc + 63) / 64)));
     AQ_HIP(hipMalloc((void **)&h->d_pmask, sizeof(unsigned long long) * ((nc + 63) / 64)));
+    AQ_HIP(hipMemsetAsync(h->d_pmask, 0, sizeof(unsigned long long) * ((nc + 63) / 64), h->stream));  // see k_finalize
     AQ_HIP(hipMalloc((void **)&h->d_chS, sizeof(int) * 2 * nseg * T1));  // two buffers: launch parity
     AQ_HIP(hipMalloc((void **)&h->d_chD, sizeof(int) * 2 * nseg * T1));
     AQ_HIP(hipMalloc((void **)&h->d_chLP, sizeof(int) * nseg * T1));
@@ -3664,9 +3761,10 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_chclean, sizeof(int) * 2));  // [1]: the fused finalize's epoch flag
     AQ_HIP(hipMemsetAsync(h->d_chclean, 0, sizeof(int) * 2, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_cht, (size_t)nc));
-    AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * (CH_GROUPS + 1)));
+    AQ_HIP(hipMalloc((void **)&h->d_chcnt, sizeof(unsigned long long) * (CH_GROUPS + 2)));  // + k_rank_chain0's
     // the last arriver of every chain launch re-zeroes them
-    AQ_HIP(hipMemsetAsync(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 1), h->stream));
+    AQ_HIP(hipMemsetAsync(h->d_chcnt, 0, sizeof(unsigned long long) * (CH_GROUPS + 2), h->stream));
+    h->rank_arrivals = 0;  // k_rank_chain0's counter starts again
     AQ_HIP(hipMalloc((void **)&h->d_lv, sizeof(int) * 8 * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_rtype, (size_t)nc + 64));
     h->cap_req = nc;
@@ -3751,6 +3849,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     HistArgs ha{h->d_open_pages, np, h->open.tail_fill, h->d_prio, h->d_meta, T, h->d_anchor, h->d_gh, csum,
                 h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide, zcs, h->csum_used[par ^ 1], pg0};
     ha.kst = kst_for(h, np, 0);
+    ha.all_narrow = h->open_all_narrow ? 1 : 0;
     if (scan) {  // this scan's buffer; the other one is clean once pass 1 has run
         const int nch = (np + CHUNK - 1) / CHUNK;
         h->csum_used[par] = (long long)(nch + th_tiles(nch)) * C;  // the chunk sums and the tile area
@@ -3787,10 +3886,13 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                                 h->d_gcut_next, nprep > 0 ? 1 : 0, th_tiles(nchunks) * T, h->d_gcut};
         } else {
             stage_begin(h, "thresholds", &ev);
-            k_thresholds<<<th_tiles(nchunks) * T, TH_THREADS, 0, s>>>(zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need,
-                                                  h->d_candlen, h->d_needsort, h->d_binoff, h->d_coltot,
-                                                  h->d_type_cnt, h->d_anchor, h->d_anchor_next, h->d_gcut_next,
-                                                  nprep > 0 ? 1 : 0, h->d_gcut);
+            // plus one workgroup: the prefix of seg_cnt for the chain (prep_block wrote it in this batch)
+            const bool jp = nprep > 0 && T <= 8;
+            k_thresholds<<<th_tiles(nchunks) * T + (jp ? 1 : 0), TH_THREADS, 0, s>>>(
+                zcs, ha.zn, T, h->d_dem, csum, nchunks, h->d_theta, h->d_need, h->d_candlen, h->d_needsort,
+                h->d_binoff, h->d_coltot, h->d_type_cnt, h->d_anchor, h->d_anchor_next, h->d_gcut_next,
+                nprep > 0 ? 1 : 0, h->d_gcut, h->d_seg_cnt, (R + 63) / 64, jp ? h->d_jpref : nullptr);
+            h->jpref_ok = jp;
             stage_end(h, "thresholds", ev);
         }
         stage_begin(h, "select", &ev);
@@ -5082,6 +5184,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     }
     hsec("sort", st0);
     RankArgs rka{};
+    // k_rank rides in the chain's launch (k_rank_chain0) for T <= 8 outside a group
+    const bool fuse_rc = np > 0 && T > 0 && T <= 8 && !h->grec && h->fuse_rank_chain;
+    int rg_fused = 0;
     if (np > 0 && T > 0) {
         if (++h->rank_epoch == 0) h->rank_epoch = 1;
         const RankSort rs{h->d_needsort, h->d_ckey2, h->d_cslot, h->d_cslot2, h->d_rank_sync, h->rank_epoch,
@@ -5105,6 +5210,10 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             if (h->grec) {
                 h->grec->kinds |= GK_RANK;
                 h->grec->rank = GRank{rka, rgrid};
+            } else if (fuse_rc) {
+                // 64-thread blocks: as many threads as rgrid blocks of RANK_TILE (16 on a rank hint: its
+                // blocks then only check, the chain does not wait for them)
+                rg_fused = h->rank_grid ? h->rank_grid : rank_hint(h) ? 16 : rgrid * (RANK_TILE / 64);
             } else {
                 k_rank<<<rgrid, RANK_TILE, 0, s>>>(rka);
             }
@@ -5135,7 +5244,14 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         ChainArgs ca{h->d_mask, h->d_tmatch, R, T, nseg, warm, gs, h->d_candoff, h->d_candlen, h->d_crank,
                      h->d_umatch, h->d_cht, h->d_seg_cnt, h->d_chS, h->d_chD, h->d_chS + nsT, h->d_chD + nsT,
                      h->d_chLP, h->d_chGT, h->d_chGO, h->d_chclean, h->d_chcnt, h->d_ctr,
-                     (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr};
+                     (T <= 8 && np > 0) ? h->d_lv : nullptr, h->d_rtype, nullptr, nullptr, 0ull, h->d_needsort,
+                     // the prefix of seg_cnt holds unless the targeted phase changed seg_cnt after k_thresholds
+                     (h->jpref_ok && !targeted) ? h->d_jpref : nullptr};
+        h->jpref_ok = false;
+        if (rg_fused > 0) {
+            ca.rdone = h->d_chcnt + CH_GROUPS + 1;
+            ca.rtarget = (h->rank_arrivals += (unsigned long long)rg_fused);
+        }
         if (h->chain_stamps) {
             if (nseg > h->cap_stamps) {
                 AQ_HIP(hipStreamSynchronize(s));
@@ -5164,6 +5280,9 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             h->grec->kinds |= GK_CHAIN;
             h->grec->chain = GChain{ca, cp, mode_of(1), K == 0 ? 1 : 0, nseg};
             h->grec->lds_chain = lds;
+        } else if (rg_fused > 0) {
+            auto krc = T <= 4 ? k_rank_chain0<4> : k_rank_chain0<8>;
+            krc<<<rg_fused + nseg, 64, lds, s>>>(rka, rg_fused, ca, cp, mode_of(1), K == 0);
         } else if (T <= 4) k_chain0<4><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
         else if (T <= 8) k_chain0<8><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);
         else k_chain0<64><<<nseg, 64, lds, s>>>(ca, cp, mode_of(1), K == 0);

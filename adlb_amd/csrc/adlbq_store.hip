@@ -515,6 +515,9 @@ int sync_tables(adlbq_server *h) {
             std::memcpy(t + o_pb, h->page_base.data(), sizeof(int) * npg);
             std::memcpy(t + o_pw, h->page_wide.data(), sizeof(int) * npg);
         }
+        bool narrow = true;  // pass 1 skips the per-page wide flag when no open page is wide
+        for (size_t i = 0; i < op.size() && narrow; i++) narrow = h->page_wide[(size_t)op[i]] == 0;
+        h->open_all_narrow = narrow;
         AQ_HIP(hipMemcpyAsync(h->d_tab, t, sizeof(int) * total, hipMemcpyHostToDevice, h->stream));
         AQ_HIP(hipEventRecord(h->tab_ev[sl], h->stream));
         int *d = h->d_tab;
@@ -670,18 +673,19 @@ __global__ void k_put_match(const PutRec *__restrict__ r, int n, const int *__re
         }
         if (lane == 0) {
             int *o = out3 + 3 * i;
-            o[0] = u.seq;
-            o[1] = -1;
-            o[2] = -1;
+            int o1 = -1, o2 = -1;
             if (found >= 0) {
                 int rk = rq_rank[found];
                 st_agent(rq_live + found, 0);
-                o[1] = rk;
-                o[2] = rq_seq[found];
+                o1 = rk;
+                o2 = rq_seq[found];
                 bytes_add(ctr, -BYTES_RQ);  // rq_delete (adlb.c:1040)
                 pin[u.slot] = rk;
                 if (rk >= 0) meta[u.slot] = (uint32_t)u.meta | M_PINNED;
             }
+            o[0] = u.seq;  // every result word written once
+            o[1] = o1;
+            o[2] = o2;
         }
         if (found >= 0) {
             live--;
@@ -919,20 +923,22 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
             const long long wb = BYTES_WQ + u[q].len;  // pmalloc + wq_node_create
             pk = max(pk, acc + wb);
             acc += wb;
-            o[0] = u[q].seq;
-            o[1] = -1;
-            o[2] = -1;
             const int e = res[q];
+            int o1 = -1, o2 = -1;
             if (e >= 0) {
                 const int k = s_k[e], rk = rq_rank[k];
                 rq_live[k] = 0;
-                o[1] = rk;
-                o[2] = rq_seq[k];
+                o1 = rk;
+                o2 = rq_seq[k];
                 pin[u[q].slot] = rk;
                 if (rk >= 0) meta[u[q].slot] = (uint32_t)u[q].meta | M_PINNED;
                 acc -= BYTES_RQ;  // rq_delete (adlb.c:1040)
                 nmatch++;
             }
+            // every result word written once (a reader of mapped memory may poll them)
+            o[0] = u[q].seq;
+            o[1] = o1;
+            o[2] = o2;
         }
         // block exclusive scan of acc in Put order, the peak, the chunk total
         long long x = acc;
@@ -1633,7 +1639,7 @@ int adlbq_destroy(adlbq_server *h) {
                     h->d_dkeys, h->d_dkeys2, h->d_dvals, h->d_dvals2, h->d_dstart, h->d_dend,
                     h->d_mslot, h->d_rh, h->d_wk0, h->d_wk1, h->d_wekey, h->d_wv0, h->d_wv1,
                     h->d_wflag, h->d_wrstart, h->d_whead, h->d_wrkey, h->d_wreq, h->d_wcnt, h->d_wpages, h->d_wtmp, h->d_kr,
-                    h->d_onepart, h->d_utsorted};
+                    h->d_onepart, h->d_utsorted, h->d_jpref};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (h->h_result) hipHostFree(h->h_result);
@@ -2610,6 +2616,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     }
     if (n == "recycle_pages") {
         h->recycle_pages = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
+    if (n == "fuse_rank_chain") {
+        h->fuse_rank_chain = value ? 1 : 0;
         return ADLBQ_OK;
     }
     if (n == "bound_inject") {

@@ -157,11 +157,15 @@ def replay_many(servers, traces, cap_factor: int = 8):
     return [o[: nout[j]].copy() for j, o in enumerate(outs)], [ncall[j] for j in range(n)]
 
 
-def replay_rounds(servers, traces, k: int, rqcap: int, steal_cap: int = 1 << 22):
+def replay_rounds(servers, traces, k: int, rqcap: int, steal_cap: int = 1 << 22, closed: bool = False,
+                  stats: dict | None = None):
     """Config 5 at its SURVEY shape (adlb_replay.cpp, adlbsrv_replay_rounds): the
     shards' traces with steal rounds (event 23 in every trace), device-side
     batches between the rounds from one host thread per shard, one steal-group
     round (export depth k, rqcap parked Reserves per shard) at each marker.
+    closed: a Get is issued only once the reply it depends on has landed, with
+    the wqseqno from that reply (adlbsrv_replay_rounds2); stats then receives
+    {get_calls_waited, wait_s, wqseqno_mismatch}.
     Returns (outputs per shard, steals (n, 15), seconds, calls per shard)."""
     import ctypes
 
@@ -181,8 +185,11 @@ def replay_rounds(servers, traces, k: int, rqcap: int, steal_cap: int = 1 << 22)
     nout, ncall = LA(), LA()
     nst = ctypes.c_longlong()
     sec = ctypes.c_double()
-    rc = lib.adlbsrv_replay_rounds(hs, n, servers[0].T, tp, lens, k, rqcap, op, caps, nout, steals.ctypes.data,
-                                   steal_cap, ctypes.byref(nst), ctypes.byref(sec), ncall)
+    cl = (ctypes.c_double * 3)()
+    rc = lib.adlbsrv_replay_rounds2(hs, n, servers[0].T, tp, lens, k, rqcap, op, caps, nout, steals.ctypes.data,
+                                    steal_cap, ctypes.byref(nst), ctypes.byref(sec), ncall, 1 if closed else 0, cl)
+    if stats is not None:
+        stats.update(get_calls_waited=int(cl[0]), wait_s=round(cl[1], 4), wqseqno_mismatch=int(cl[2]))
     if rc:
         raise RuntimeError(f"adlbsrv_replay_rounds: {lib.adlbsrv_replay_error().decode(errors='replace')}")
     return ([o[: nout[j]].copy() for j, o in enumerate(outs)], steals[: nst.value].copy(), sec.value,

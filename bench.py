@@ -583,14 +583,15 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
     warm = oracle.gen_config5(n_events=min(args.c5_events, 100_000), seed=args.seed + 7 + 101 * rank, **kw)
     c5_stats = {}
 
-    def run(dd):
+    def run(dd, closed=False, cl_stats=None):
         srvs = [Server(dd["user_types"], A, S, s_, max_units=1 << 16, device=local) for s_ in range(S)]
         try:
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
             w0 = time.perf_counter()
-            got, steals, sec, calls = replay.replay_rounds(srvs, dd["traces"], k=args.c5_k, rqcap=A)
+            got, steals, sec, calls = replay.replay_rounds(srvs, dd["traces"], k=args.c5_k, rqcap=A, closed=closed,
+                                                           stats=cl_stats)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -616,15 +617,37 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
 
     run(warm)  # kernels loaded, pools sized
     got, steals, sec, calls, wall = run(d)
-    same = all(np.array_equal(g, e) for g, e in zip(got, d["outputs"]))
     st_key = lambda a: np.sort(np.ascontiguousarray(a).view([("", a.dtype)] * 15), axis=0)
-    same_steals = steals.shape == d["steals"].shape and np.array_equal(st_key(steals), st_key(d["steals"]))
+
+    def parity(got_, steals_):
+        same_ = all(np.array_equal(g, e) for g, e in zip(got_, d["outputs"]))
+        same_st = steals_.shape == d["steals"].shape and np.array_equal(st_key(steals_), st_key(d["steals"]))
+        return bool(same_), bool(same_st)
+
+    same, same_steals = parity(got, steals)
     ok = bool(same and same_steals)
     total = int(d["events"])
     el = sec
+    # closed loop: every Get waits for the reply it depends on and takes its wqseqno from it
+    cl = {}
+    run(warm, closed=True)
+    got_c, steals_c, sec_c, _, _ = run(d, closed=True, cl_stats=cl)
+    same_c, same_steals_c = parity(got_c, steals_c)
+    ok_c = same_c and same_steals_c and cl.get("wqseqno_mismatch", 1) == 0
+    el_c = sec_c
     if world > 1:
+        el_c, _ = shards.reduce_step_timing(el_c, total)
+        ok_c = all_ranks_true(ok_c)
         el, total = shards.reduce_step_timing(el, total)
         ok = all_ranks_true(ok)
+    closed_loop = {"value": total / el_c if ok_c else None, "unit": "events/s", "seconds": round(el_c, 4),
+                   "parity": bool(ok_c), **cl,
+                   "note": "each Get issued only after the TA_RESERVE_RESP (or put-side match, or steal answer) it "
+                           "depends on has landed in mapped host memory, its wqseqno taken from that reply "
+                           "(tsp.c:157-162); Puts and Reserves as in the open-loop run"}
+    cpu_sh = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu_sh = cpu_baseline_c5(d, A, S)
     return {"workload": f"config5: {S} server shards x tsp-style streams ({A} app ranks, {int(d['events'])} events, "
                         f"a qmstat exchange + steal round every {args.c5_round_every} events: {int(d['rounds'])} rounds, "
                         f"{d['steals'].shape[0]} steals, {int(d['stopped'])} stopped at export depth {args.c5_k}) "
@@ -635,10 +658,44 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
             "host_seconds": replay.last_rounds_prof(),
             "engine": dict(c5_stats),
             "parity": ok, "parity_outputs": bool(same), "parity_steals": bool(same_steals),
-            "cpu_oracle_events_per_s": int(d["events"]) / gen_s, "cpu_cores": 1,
-            "cpu_note": "the oracle (oracle/be_own.c) serving all shards' streams and steal rounds on one core, "
-                        "with the stream generator in the loop (gen_c5.c)",
+            "closed_loop": closed_loop,
+            "cpu_baseline": cpu_sh,
+            "cpu_generator_events_per_s": int(d["events"]) / gen_s,
+            "cpu_generator_note": "the stream generator (gen_c5.c) with the oracle serving every shard, one core: "
+                                  "generation cost included, not a server baseline",
             "scaling": "weak"}
+
+
+def cpu_baseline_c5(d, A, S) -> dict:
+    """Config 5's CPU baseline in the ADLB-natural layout: S server processes,
+    one per shard, each replaying its own shard's stream with its part of every
+    steal round inlined (oracle/gen_c5.c xtrace: its SS_RFR answers as donor,
+    its rq deletions as requester) through this repo's restatement of xq.c /
+    adlb.c's handlers (oracle/liboracle.so), in parallel.  value = the stream's
+    events / the slowest process's seconds.  No MPI messaging is charged, so
+    this favours the CPU."""
+    import multiprocessing as mp
+    import tempfile
+    from oracle.baseline import c5_shard
+    tmp = tempfile.mkdtemp(prefix="c5cpu_")
+    try:
+        jobs = []
+        for s_ in range(S):
+            path = os.path.join(tmp, f"x{s_}.npy")
+            np.save(path, d["xtraces"][s_])
+            jobs.append((path, d["user_types"], A, S, s_))
+        ctx = mp.get_context("spawn")  # this process holds the GPU: no fork
+        with ctx.Pool(S) as pool:
+            res = pool.map_async(c5_shard, jobs).get(1200)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    slowest = max(r[1] for r in res)
+    return {"value": int(d["events"]) / slowest, "unit": "events/s", "cores": S, "kind": "port",
+            "seconds_slowest": round(slowest, 4), "seconds_per_process": [round(r[1], 4) for r in res],
+            "host_cpus": {"affinity": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count()},
+            "sample": f"the whole config-5 stream ({int(d['events'])} events): {S} server processes, one per shard, "
+                      f"each replaying its shard's events and its part of every steal round through "
+                      f"oracle/liboracle.so (this repo's restatement of xq.c / adlb.c's handlers); no MPI cost"}
 
 
 def bench_wide(args, torch, dev):

@@ -216,7 +216,7 @@ def gen_config5(n_shards: int = 8, n_ranks: int = 4096, n_events: int = 10_000_0
     lib.c5_seconds.restype = ctypes.c_double
     lib.c5_seconds.argtypes = [ctypes.c_void_p]
     pp = ctypes.POINTER(ctypes.POINTER(ctypes.c_int))
-    for f in ("c5_trace", "c5_out"):
+    for f in ("c5_trace", "c5_out", "c5_xtrace"):
         getattr(lib, f).restype = ctypes.c_long
         getattr(lib, f).argtypes = [ctypes.c_void_p, ctypes.c_int, pp]
     for f in ("c5_steals", "c5_round_nsteal"):
@@ -236,6 +236,9 @@ def gen_config5(n_shards: int = 8, n_ranks: int = 4096, n_events: int = 10_000_0
 
         return {"traces": [arr(lib.c5_trace, s).ravel() for s in range(n_shards)],
                 "outputs": [arr(lib.c5_out, s).ravel() for s in range(n_shards)],
+                # each shard's trace with its part of every steal round inlined (ORC_OP_RFR as donor,
+                # ORC_OP_RQDEL as requester): one server process's whole work, replayed alone
+                "xtraces": [arr(lib.c5_xtrace, s).ravel() for s in range(n_shards)],
                 "steals": arr(lib.c5_steals, cols=15), "round_nsteal": arr(lib.c5_round_nsteal).ravel(),
                 "events": lib.c5_events(g), "rounds": lib.c5_rounds(g), "stopped": lib.c5_stopped(g),
                 "seconds": lib.c5_seconds(g), "n_shards": n_shards, "n_ranks": n_ranks, "k": k,

@@ -48,3 +48,27 @@ def _time(oracle, synth, kind, w, budget, num_servers=1, idx=0):
         o.replay(synth.reserve_events(w.r_rank[done:done + k], w.r_types[done:done + k], w.r_hang[done:done + k]))
         done += k
     return done, time.perf_counter() - t0, w.n_units
+
+
+def c5_shard(job):
+    """One server process of the config-5 CPU baseline: shard s's expanded
+    trace (oracle/gen_c5.c xtrace: its events plus its part of every steal
+    round) replayed alone through the oracle, as one ADLB server process
+    serves its own queue.  job = (path of the .npy trace, user_types,
+    num_app_ranks, num_servers, s).  Returns (events, seconds)."""
+    import numpy as np
+
+    import oracle
+    path, ut, A, S, s = job
+    tr = np.load(path, mmap_mode="r")
+    tr = np.ascontiguousarray(tr, dtype=np.int32)
+    o = oracle.Oracle("own")
+    o.init(ut, A, S, s)
+    cap = oracle.output_bound(tr, o.ntypes)
+    out = np.empty(cap, dtype=np.int32)
+    t0 = time.perf_counter()
+    n = o.lib.orc_replay(tr.ctypes.data, tr.size, out.ctypes.data, cap)
+    sec = time.perf_counter() - t0
+    if n < 0:
+        raise ValueError(f"oracle: shard {s} trace rejected (rc={n})")
+    return int(tr.size), sec

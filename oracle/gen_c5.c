@@ -72,6 +72,8 @@ typedef struct {
     void *(*wq_next)(void *);
     void (*wq_view)(void *, be_unit_view *);
     Vec tr, out;  /* the shard's trace and the oracle's outputs */
+    Vec xtr;      /* the trace plus this shard's part of every steal round (its SS_RFR answers as donor, its
+                     rq deletions as requester): what one server process replays alone (bench cpu baseline) */
     Vec pend;     /* Puts addressed to this shard, not yet issued */
     long live;    /* units held (model bookkeeping for the queue level) */
 } Shard;
@@ -122,6 +124,7 @@ static int *issue(C5 *g, int s, const int *ev, long nint, long *nout) {
         return NULL;
     }
     vpush(&h->tr, ev, nint);
+    vpush(&h->xtr, ev, nint);
     long o0 = h->out.n;
     vpush(&h->out, ob, n);
     *nout = n;
@@ -309,8 +312,10 @@ static int steal_round(C5 *g) {
                 snprintf(g->err, sizeof g->err, "a donor chosen on a fresh table had no unit (shard %d)", donor);
                 return -1;
             }
+            vpush(&g->sh[donor].xtr, ev, 3 + ORC_REQ_TYPES);
             ev[0] = ORC_OP_RQDEL;
             ev[1] = rqs;
+            vpush(&g->sh[i].xtr, ev, 2);
             int dd[16];
             if (query(g, i, ev, 2, dd, 16) < 0 || dd[1] != 1) {
                 snprintf(g->err, sizeof g->err, "steal of an rq entry that is gone (shard %d)", i);
@@ -491,6 +496,7 @@ long c5_stopped(C5 *g) { return g->stopped; }
 double c5_seconds(C5 *g) { return g->seconds; }
 long c5_trace(C5 *g, int s, const int **p) { *p = g->sh[s].tr.p; return g->sh[s].tr.n; }
 long c5_out(C5 *g, int s, const int **p) { *p = g->sh[s].out.p; return g->sh[s].out.n; }
+long c5_xtrace(C5 *g, int s, const int **p) { *p = g->sh[s].xtr.p; return g->sh[s].xtr.n; }
 long c5_steals(C5 *g, const int **p) { *p = g->steals.p; return g->steals.n / 15; }
 long c5_round_nsteal(C5 *g, const int **p) { *p = g->round_nsteal.p; return g->round_nsteal.n; }
 
@@ -499,6 +505,7 @@ void c5_free(C5 *g) {
     for (int s = 0; s < g->S; s++) {
         free(g->sh[s].tr.p);
         free(g->sh[s].out.p);
+        free(g->sh[s].xtr.p);
         free(g->sh[s].pend.p);
         if (g->sh[s].dl) dlclose(g->sh[s].dl);
     }

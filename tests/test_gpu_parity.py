@@ -226,6 +226,9 @@ VARIANTS = {
     "rank_in_k_rank": {"rank_in_select": 0},  # k_rank ranks every candidate (k_select_open does not)
     "split_prep": {"split_prep": 1},          # request preparation and pass 1 as two launches
     "select_four_waves": {"select_wave": 0},  # pass 2 with four waves per page (k_select_open) for T <= 8
+    "rank_launch": {"fuse_rank_chain": 0},    # k_rank as a launch of its own, not in the chain's (T <= 8)
+    # k_rank's blocks in the chain's launch doing the ranking (k_select_open does not rank): the segments wait
+    "fused_rank_ranks": {"rank_in_select": 0, "fuse_rank_chain": 1},
 }
 
 
