@@ -134,6 +134,14 @@ const char *adlbsrv_replay_error(void);
 int adlbsrv_replay_rounds(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
                           int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
                           int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls);
+/* The same; closed != 0: a shard issues each Get only once the reply it depends on (its Reserve's
+ * TA_RESERVE_RESP, the put-side match of its parked Reserve, or the steal round's answer) has landed in
+ * mapped host memory, with the wqseqno from that reply (tsp.c:157-162).  cl_stats[3] (may be NULL):
+ * Get calls that waited, seconds waited, replies whose wqseqno differs from the recorded Get's. */
+int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *const *traces, const long long *lens,
+                           int k, int rqcap, int *const *outs, const long long *caps, long long *nouts,
+                           int *steals, long long steal_cap, long long *nsteals, double *seconds, long long *ncalls,
+                           int closed, double *cl_stats);
 void adlbsrv_replay_prof(double *out8);
 
 /* state for the driver */
