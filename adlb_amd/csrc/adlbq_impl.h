@@ -330,6 +330,10 @@ struct adlbq_server {
     unsigned long long *d_kb = nullptr;  // [2 * ADLBQ_MAX_TYPES] per-list key OR / AND (k_keybits)
     int rank_grid = 0;                 // test hook ("rank_grid"): k_rank's grid (0: 4 on a rank hint, else 1280)
     int fuse_rank_chain = 1;           // "fuse_rank_chain": k_rank's blocks in the chain's launch (T <= 8)
+    int fin_snap_diag = 0;             // "fin_snap_diag" (timing diagnostic): the finalize snapshot undrained
+    int targeted_scan = -1;            // "targeted_scan": 1 = the pre-targeted match scans the rank buckets
+                                       //   (k_targeted), 0 = the sorted index (k_targeted_idx), -1 = by size
+    long long tscan_batches = 0;       // batches whose targeted phase scanned the buckets (stat "tscan_batches")
     unsigned long long rank_arrivals = 0;  // rank blocks launched in k_rank_chain0 so far (their counter's target)
     int *d_jpref = nullptr;            // [cap_req / 64 + 1] exclusive prefix of seg_cnt (k_thresholds' extra workgroup)
     bool jpref_ok = false;             // this batch's k_thresholds wrote d_jpref

@@ -1520,11 +1520,12 @@ __global__ __launch_bounds__(256) void k_targeted(const int *__restrict__ bucket
                             ((long long)rpages[p0 + (L >> PAGE_SHIFT)] << PAGE_SHIFT) + (L & (PAGE - 1));
                         tmatch[jj] = (int)slot;
                         atomicSub(&seg_cnt[jj >> 6], 1);
-                        // taken for this rank's later Reserves (this block owns the bucket)
+                        // taken for this rank's later Reserves (this block owns the bucket): a write-through
+                        // store, drained before the barrier; the block's scans read meta with sc1 loads
                         st_agent(reinterpret_cast<int *>(meta + slot), (int)(meta[slot] | M_PINNED));
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                 }
-                __threadfence();
                 __syncthreads();
             }
             if (threadIdx.x == 0) nlist = 0;
@@ -3117,6 +3118,8 @@ struct FinArgs {
     int *mslot;  // [R] out: the slot request j was given, or -1 (adlbq_unreserve_resp_device reads it back)
     const int2 *rh;  // [R] (rank, hang) as prep_block copied them: 8 B per request instead of a 72 B record stride
     int flat;        // grids up to this size arrive at one counter ("fin_flat"), larger ones by 8 groups
+    int snap_diag;   // diagnostic ("fin_snap_diag"): the snapshot's host stores not drained before the tag
+    int resp16;      // resp is 16-byte aligned (every row then is: 48 B each)
 };
 
 // k_rank gave up waiting for an in-launch candidate sort: the lists may be
@@ -3167,6 +3170,14 @@ __device__ __forceinline__ void fin_request(const FinArgs &f, int j, bool failed
     }
     const bool parks = slot < 0 && hang;
     int *out = f.resp + (long long)ADLBQ_RESP_INTS * j;
+    if (f.resp16) {  // 16-byte aligned rows: three (or two and a half) vector stores instead of twelve
+        int4 *o4 = reinterpret_cast<int4 *>(out);
+        o4[0] = make_int4(o[0], o[1], o[2], o[3]);
+        o4[1] = make_int4(o[4], o[5], o[6], o[7]);
+        if (!parks) o4[2] = make_int4(o[8], o[9], -1, -1);
+        else *reinterpret_cast<int2 *>(out + 8) = make_int2(o[8], o[9]);  // [10], [11]: the park tail
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 10; i++) out[i] = o[i];
     if (!parks) {
@@ -3236,6 +3247,10 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
         const int *src = reinterpret_cast<const int *>(f.ctr);
         int *dst = reinterpret_cast<int *>(f.snap);
         for (int i = threadIdx.x; i < (int)(sizeof(DevCounters) / 4); i += 64) dst[i] = ld_sc1(src + i);
+        if (f.snap_diag) {  // timing diagnostic only: no drain, no release (a torn snapshot may land)
+            if (threadIdx.x == 0) __hip_atomic_store(&f.snap->snap_tag, f.snap_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // the tag's system-scope release store orders the wave's drained snapshot stores before it
         if (threadIdx.x == 0)
@@ -4692,7 +4707,8 @@ static FinArgs fin_args(adlbq_server *h, int R, const int *d_reqs, int *d_resp, 
                    h->d_ctr, donor_ctx(h), (h->S > 1 || !h->tq.empty()) ? 1 : 0, h->d_rq_rank, h->d_rq_types,
                    h->d_rq_live, h->d_rq_req, h->d_rq_seq, h->d_dem, h->T, snap, h->snap_tag[h->snap_next],
                    h->d_anchor, h->d_anchor_next, h->d_pmask, h->d_gcut, h->d_gcut_next, h->d_rrec, h->d_needsort,
-                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_mslot, h->d_rh, h->fin_flat};
+                   h->d_rank_sync + ADLBQ_MAX_TYPES + 1, h->d_mslot, h->d_rh, h->fin_flat, h->fin_snap_diag,
+                   ((uintptr_t)d_resp & 15) == 0 ? 1 : 0};
 }
 
 // the host side of a batch in flight: its snapshot slot, counts, upper bounds
@@ -5037,7 +5053,14 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
                 nullptr, 0, nullptr, nullptr, 0, h->export_extra, h->d_rh};
     const int nb = (int)h->bucket_ranks.size();
     const bool targeted = h->live_targeted > 0 && nb > 0;
-    if (targeted && nb < (1 << 20)) {  // per-bucket Reserve lists for k_targeted_idx
+    // small rank buckets and few Reserves per bucket (config 5's bound updates): each bucket's Reserves
+    // scan its pages (k_targeted) -- no sorted index to keep up to date after every targeted Put
+    bool tscan = targeted && nb < (1 << 20) && h->targeted_scan != 0;
+    if (tscan && h->targeted_scan < 0) {
+        tscan = (long long)R <= 4ll * nb;
+        for (int k = 0; k < nb && tscan; k++) tscan = (int)h->rankb[k].pages.size() <= 1;
+    }
+    if (targeted && nb < (1 << 20) && !tscan) {  // per-bucket Reserve lists for k_targeted_idx
         const int tcap = std::min(TGT_REQ, std::max(64, 2 * ((R + nb - 1) / nb) + 64));
         if ((long long)nb > h->cap_tcnt || (long long)nb * tcap > h->cap_tlist) {
             AQ_HIP(hipStreamSynchronize(s));
@@ -5094,12 +5117,20 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     if (targeted) {
         if ((rc = leave_group())) return rc;
         const auto ti_t0 = std::chrono::steady_clock::now();
-        if (nb < (1 << 20) && (rc = ensure_tindex(h))) return rc;
+        if (tscan) {  // the index is not kept meanwhile: the next indexed batch rebuilds it in full
+            h->tnew_keys.clear();
+            h->tnew_vals.clear();
+            h->tidx_valid = false;
+            h->tindex_dirty = true;
+            h->tscan_batches++;
+        } else if (nb < (1 << 20) && (rc = ensure_tindex(h))) {
+            return rc;
+        }
         host_stage_add(h, "tindex", ti_t0);
         auto tt = ti_t0;
         hsec("tindex", tt);
         stage_begin(h, "targeted", &ev);
-        if (nb < (1 << 20))
+        if (nb < (1 << 20) && !tscan)
             k_targeted_idx<<<nb, 256, 0, s>>>(h->d_bucket_ranks, h->d_rank_pstart, h->d_rank_pages, h->d_tkeys,
                                               h->d_tvals, h->d_tstart, h->d_tend,
                                               TDelta{h->d_dkeys, h->d_dvals, h->d_dstart, h->d_dend, (int)h->tdel_n},

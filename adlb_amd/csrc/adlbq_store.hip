@@ -2618,6 +2618,15 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->recycle_pages = value ? 1 : 0;
         return ADLBQ_OK;
     }
+    if (n == "targeted_scan") {
+        if (value < -1 || value > 1) return fail(ADLBQ_ERR_ARG, "targeted_scan must be -1, 0 or 1");
+        h->targeted_scan = (int)value;
+        return ADLBQ_OK;
+    }
+    if (n == "fin_snap_diag") {
+        h->fin_snap_diag = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "fuse_rank_chain") {
         h->fuse_rank_chain = value ? 1 : 0;
         return ADLBQ_OK;
@@ -2796,6 +2805,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         return h->ctr.plan_missed;
     }
     if (n == "bound_faults") return h->ctr.bound_faults;
+    if (n == "tscan_batches") return h->tscan_batches;
     if (n == "sort_timeouts" || n == "batch_failed") {  // batches answered ADLB_ERROR because k_rank's wait
         refresh_counters(h);                                // for an in-launch sort gave up (0 unless broken)
         return h->ctr.batch_failed;

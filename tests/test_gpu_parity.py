@@ -105,6 +105,7 @@ def test_small_queue_vs_oracle(gpu_available, name, engine):
             s.set_param(k, v)
         got = replay.replay(s, tr)
         used = s.stat("small_batches") + s.stat("one_batches")  # (a one-Reserve batch takes k_reserve_one)
+        assert s.stat("bound_faults") == 0  # no choice outside the page list (DESIGN.md §9, round-5 fault)
     assert_same(got, run_oracle(w.user_types, cfg, tr))
     assert (used > 0) == (engine == "default"), used
 
@@ -229,6 +230,9 @@ VARIANTS = {
     "rank_launch": {"fuse_rank_chain": 0},    # k_rank as a launch of its own, not in the chain's (T <= 8)
     # k_rank's blocks in the chain's launch doing the ranking (k_select_open does not rank): the segments wait
     "fused_rank_ranks": {"rank_in_select": 0, "fuse_rank_chain": 1},
+    # the pre-targeted match over the rank buckets' pages (k_targeted) / always the sorted index
+    "targeted_scan": {"targeted_scan": 1},
+    "targeted_index": {"targeted_scan": 0},
 }
 
 
@@ -794,3 +798,19 @@ def test_one_and_pipeline_batches_interleaved_vs_oracle(gpu_available, T):
         got = replay.replay(s, np.concatenate(trace))
         assert s.stat("one_batches") > 0
     assert_same(got, np.concatenate(exp))
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+@pytest.mark.parametrize("name", ["s_c4_targeted", "s_c4_t8_tied", "s_c4_r256"])
+def test_targeted_scan_vs_index_small(gpu_available, name, mode):
+    """Small queues with targeted units: the pre-targeted match (xq.c:219-247) by
+    scanning each rank bucket (k_targeted, "targeted_scan" 1) and by the sorted
+    index (k_targeted_idx, 0), each with the one-workgroup choice after it."""
+    w = SMALL[name]()
+    tr = synth.workload_trace(w)
+    cfg = (w.num_app_ranks, 1, 0)
+    with Server(w.user_types, *cfg, max_units=w.n_units) as s:
+        s.set_param("targeted_scan", mode)
+        got = replay.replay(s, tr)
+        assert (s.stat("tscan_batches") > 0) == (mode == 1)
+    assert_same(got, run_oracle(w.user_types, cfg, tr))

@@ -277,3 +277,15 @@ def test_mix_many_types_every_unit_once(np_, ns, nt):
                                   env_extra={"ADLB_STEAL_REPORT": "1"})
     assert got == exp, out[-2000:]
     assert _steal_report(err) == [], err[-2000:]
+
+
+@pytest.mark.gpu
+def test_mix_steal_transport_default_shared_gpu():
+    """The steal group's transport at its default: the servers' PCI bus ids are
+    all-gathered; two servers sharing the box's one GPU keep MPI_Allgather
+    (RCCL is chosen only when every server owns a GPU), and every unit is
+    consumed once."""
+    out, got, exp, err = _run_mix(6, ["-nservers", "2", "-n", "150"],
+                                  env_extra={"ADLB_STEAL_GROUP": "1", "ADLB_STEAL_REPORT": "1"})
+    assert got == exp, out[-2000:]
+    assert "steal transport: mpi (servers share a GPU)" in err, err[-2000:]

@@ -44,6 +44,16 @@ fixed)
 metric)
   timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 $M "$@" > $O/metric.json 2> $O/metric.err || { echo bench failed; tail -20 $O/metric.err; exit 1; }
   tail -1 $O/metric.json | cut -c1-2500 ;;
+ab)
+  # A/B of metric-leg variants: each argument is one variant's extra bench arguments (quoted), run twice
+  i=0
+  for v in "$@"; do
+    for rep in 1 2; do
+      timeout -k 10 300 python3 bench.py --steps 100 --warmup 5 $M --chain-stamps $v > $O/ab_$i_$rep.json 2> $O/ab.err || { echo bench failed; tail -5 $O/ab.err; exit 1; }
+      python3 -c "import json; d=json.loads(open('$O/ab_$i_$rep.json').read().strip().splitlines()[-1]); print('$v', round(d['ms_per_step'],4), {k: v['ms'] for k, v in d['kernels_ms'].items()}, d.get('chain_phases_ns'))"
+    done
+    i=$((i+1))
+  done ;;
 prof)
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/metric_prof -o metric -- python3 $R/bench.py --steps 20 --warmup 5 $M > $O/metric_prof.json 2> $O/metric_prof.err || { echo metric prof failed; tail -5 $O/metric_prof.err; exit 1; }
