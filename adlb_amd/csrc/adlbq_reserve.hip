@@ -1096,7 +1096,7 @@ __device__ __forceinline__ void select_open_body(
 #define ADLBQ_SELW_GATE 1  // k_select_wave reads a column's page prefix only at or below its threshold
 #endif
 template <int TB>
-__global__ __launch_bounds__(64) void k_select_wave(
+__device__ __forceinline__ void select_wave_body(
     const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
     const uint32_t *__restrict__ meta, int T, const long long *__restrict__ anchor,
     const int *__restrict__ theta, const int *__restrict__ need,
@@ -1106,7 +1106,7 @@ __global__ __launch_bounds__(64) void k_select_wave(
     const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
     const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
     unsigned char *__restrict__ rtype, int R,
-    unsigned long long *kst) {
+    unsigned long long *kst, const int p) {
     static_assert(TB <= 8 && TB <= RANK_FAST_T, "one wave per page: T <= 8");
     constexpr int RT = TB;
     constexpr int CPL = TB * NB / 64;  // columns per lane
@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(64) void k_select_wave(
     __shared__ long long sanc[TB], scut[TB];
     __shared__ int sth[TB], sneed[TB], soff[TB], slen[TB], slb[TB];
     __shared__ int sbo[TB * NB];
-    const int C = T * NB, lane = threadIdx.x, p = blockIdx.x;
+    const int C = T * NB, lane = threadIdx.x;
     kstamp(kst, p, 0);
     unsigned int *run = lds;
     unsigned int *list = lds + C;
@@ -1346,6 +1346,23 @@ __global__ __launch_bounds__(64) void k_select_wave(
     if (p == 0 && lane == 0) ctr->rank_fast = fast ? 1 : 0;
     const bool empty = __ballot(tl && len_l <= 0) != 0ull;
     if (crank != nullptr && p == 0 && lane == 0) ctr->rank_covered = (fast && !empty) ? 1 : 0;
+}
+
+template <int TB>
+__global__ __launch_bounds__(64) void k_select_wave(
+    const int *__restrict__ pages, int npages, int tail_fill, const int *__restrict__ prio,
+    const uint32_t *__restrict__ meta, int T, const long long *__restrict__ anchor,
+    const int *__restrict__ theta, const int *__restrict__ need,
+    const int *__restrict__ binoff, const unsigned int *__restrict__ csum, const unsigned short *__restrict__ gh,
+    const int *__restrict__ candlen, int *__restrict__ candoff_out,
+    unsigned long long *__restrict__ ckey, int *__restrict__ cslot, const long long *__restrict__ gcut,
+    const unsigned int *__restrict__ spec, const int *__restrict__ specn, const int *__restrict__ pbase,
+    const int *__restrict__ pwide, DevCounters *ctr, unsigned int *__restrict__ crank, int *__restrict__ lv,
+    unsigned char *__restrict__ rtype, int R,
+    unsigned long long *kst) {
+    select_wave_body<TB>(pages, npages, tail_fill, prio, meta, T, anchor, theta, need, binoff, csum, gh, candlen,
+                         candoff_out, ckey, cslot, gcut, spec, specn, pbase, pwide, ctr, crank, lv, rtype, R, kst,
+                         blockIdx.x);
 }
 
 template <int TB>  // TB >= T; the candidates are ranked here only for TB <= RT
@@ -3648,6 +3665,8 @@ struct GroupRec {
     int tb = 0;     // the TB of the templated kernels (4 or 8)
     GPrep prep; GThr thr; GSel sel; GRank rank; GChain chain; GFin fin;
     size_t lds_prep = 0, lds_sel = 0, lds_chain = 0;
+    bool selw = false;  // pass 2 with one wave per page (k_select_wave), else four (k_select_open)
+    size_t lds_sel_open = 0;  // k_select_open's LDS for this handle (a group of mixed shapes takes it)
 };
 
 template <int TB>
@@ -3669,6 +3688,15 @@ __global__ __launch_bounds__(256) void k_select_open_g(const GSel *__restrict__ 
     select_open_body<TB>(g.pages, g.npages, g.tail_fill, g.prio, g.meta, g.seqa, g.T, g.anchor, g.theta, g.need,
                          g.binoff, g.csum, g.gh, g.candlen, g.candoff_out, g.ckey, g.cslot, g.gcut, g.spec, g.specn,
                          g.pbase, g.pwide, g.ctr, g.crank, g.lv, g.rtype, g.R, blockIdx.x, g.grid);
+}
+// the group twin of k_select_wave (T <= 8): one wave per page, blockIdx.y = shard
+template <int TB>
+__global__ __launch_bounds__(64) void k_select_wave_g(const GSel *__restrict__ t) {
+    const GSel &g = t[blockIdx.y];
+    if ((int)blockIdx.x >= g.npages) return;  // whole workgroups return together
+    select_wave_body<TB>(g.pages, g.npages, g.tail_fill, g.prio, g.meta, g.T, g.anchor, g.theta, g.need, g.binoff,
+                         g.csum, g.gh, g.candlen, g.candoff_out, g.ckey, g.cslot, g.gcut, g.spec, g.specn, g.pbase,
+                         g.pwide, g.ctr, g.crank, g.lv, g.rtype, g.R, nullptr, blockIdx.x);
 }
 __global__ __launch_bounds__(RANK_TILE) void k_rank_g(const GRank *__restrict__ t) {
     const GRank &g = t[blockIdx.y];
@@ -3919,7 +3947,9 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                                 h->d_ckey, h->d_cslot, h->d_gcut, h->d_spec, h->d_specn, h->d_pbase, h->d_pwide,
                                 h->d_ctr, (sort || !h->rank_in_select) ? nullptr : h->d_crank,
                                 (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R, np};
-            h->grec->lds_sel = sizeof(unsigned int) * (4 * C + 4 * 1024);
+            h->grec->selw = T <= 8 && h->select_wave;
+            h->grec->lds_sel_open = sizeof(unsigned int) * (4 * C + 4 * 1024);
+            h->grec->lds_sel = h->grec->selw ? sizeof(unsigned int) * (C + 1024) : sizeof(unsigned int) * (4 * C + 4 * 1024);
         } else if (T <= 8 && h->select_wave) {
             auto selw = T <= 4 ? k_select_wave<4> : k_select_wave<8>;
             selw<<<np, 64, sizeof(unsigned int) * (C + 1024), s>>>(
@@ -5001,7 +5031,14 @@ static int launch_recorded(adlbq_server *h, GroupRec &r) {
                                                    g.candlen, g.needsort, g.binoff, g.coltot, g.type_cnt, g.anchor,
                                                    g.anchor_next, g.gcut_next, g.guess, g.gcut);
     }
-    if (r.kinds & GK_SEL) {
+    if ((r.kinds & GK_SEL) && r.selw) {
+        const GSel &g = r.sel;
+        auto selw = t4 ? k_select_wave<4> : k_select_wave<8>;
+        selw<<<g.grid, 64, r.lds_sel, s>>>(g.pages, g.npages, g.tail_fill, g.prio, g.meta, g.T, g.anchor, g.theta,
+                                            g.need, g.binoff, g.csum, g.gh, g.candlen, g.candoff_out, g.ckey, g.cslot,
+                                            g.gcut, g.spec, g.specn, g.pbase, g.pwide, g.ctr, g.crank, g.lv, g.rtype,
+                                            g.R, nullptr);
+    } else if (r.kinds & GK_SEL) {
         const GSel &g = r.sel;
         auto sel = t4 ? k_select_open<4> : k_select_open<8>;
         sel<<<g.grid, 256, r.lds_sel, s>>>(g.pages, g.npages, g.tail_fill, g.prio, g.meta, g.seqa, g.T, g.anchor,
@@ -5509,7 +5546,8 @@ static int run_group(adlbq_server *const *hs, std::vector<GroupRec> &rec, const 
     auto *tc = reinterpret_cast<GChain *>(hb + o_chain);
     auto *tf = reinterpret_cast<GFin *>(hb + o_fin);
     int gp = 0, gt = 0, gs = 0, gr = 0, gc = 0, gf = 0;
-    size_t lp = 0, lsel = 0, lc = 0;
+    bool all_selw = true;  // every member's pass 2 is one wave per page: k_select_wave_g
+    size_t lp = 0, lsel = 0, lc = 0, lsel_o = 0;
     for (int j = 0; j < k; j++) {
         const GroupRec &r = rec[(size_t)m[(size_t)j]];
         tp[j] = r.prep;
@@ -5532,6 +5570,8 @@ static int run_group(adlbq_server *const *hs, std::vector<GroupRec> &rec, const 
         gf = std::max(gf, tf[j].grid);
         lp = std::max(lp, r.lds_prep);
         lsel = std::max(lsel, r.lds_sel);
+        if ((r.kinds & GK_SEL) && !r.selw) all_selw = false;
+        lsel_o = std::max(lsel_o, r.lds_sel_open);
         lc = std::max(lc, r.lds_chain);
     }
     char *d = L->d_gtab;
@@ -5540,7 +5580,11 @@ static int run_group(adlbq_server *const *hs, std::vector<GroupRec> &rec, const 
     const bool t4 = rec[(size_t)m[0]].tb == 4;
     if (gp) (t4 ? k_prep_hist_g<4> : k_prep_hist_g<8>)<<<dim3(gp, k), 256, lp, ls>>>(reinterpret_cast<const GPrep *>(d));
     if (gt) k_thresholds_g<<<dim3(gt, k), TH_THREADS, 0, ls>>>(reinterpret_cast<const GThr *>(d + o_thr));
-    if (gs) (t4 ? k_select_open_g<4> : k_select_open_g<8>)<<<dim3(gs, k), 256, lsel, ls>>>(reinterpret_cast<const GSel *>(d + o_sel));
+    if (gs && all_selw)
+        (t4 ? k_select_wave_g<4> : k_select_wave_g<8>)<<<dim3(gs, k), 64, lsel, ls>>>(reinterpret_cast<const GSel *>(d + o_sel));
+    else if (gs)
+        (t4 ? k_select_open_g<4> : k_select_open_g<8>)<<<dim3(gs, k), 256, lsel_o, ls>>>(
+            reinterpret_cast<const GSel *>(d + o_sel));
     if (gr) k_rank_g<<<dim3(gr, k), RANK_TILE, 0, ls>>>(reinterpret_cast<const GRank *>(d + o_rank));
     if (gc) (t4 ? k_chain0_g<4> : k_chain0_g<8>)<<<dim3(gc, k), 64, lc, ls>>>(reinterpret_cast<const GChain *>(d + o_chain));
     if (gf) k_finalize_g<<<dim3(gf, k), 256, 0, ls>>>(reinterpret_cast<const GFin *>(d + o_fin));
