@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--c3-param", action="append", default=[], metavar="NAME=V",
                     help="config 3: adlbq_set_param on every shard (repeatable)")
     ap.add_argument("--no-config4", action="store_true", help="skip the config-4 measurement")
+    ap.add_argument("--no-config2", action="store_true", help="skip the config-2 (1M-unit) leg")
+    ap.add_argument("--c2-units", type=int, default=1_000_000, help="config 2: units")
+    ap.add_argument("--c2-steps", type=int, default=20, help="config 2: timed steps")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 stream measurement")
     ap.add_argument("--no-wide", action="store_true", help="skip the more-than-64-types leg")
     ap.add_argument("--diag-same-batch", action="store_true",
@@ -698,6 +701,70 @@ def cpu_baseline_c5(d, A, S) -> dict:
                       f"oracle/liboracle.so (this repo's restatement of xq.c / adlb.c's handlers); no MPI cost"}
 
 
+def bench_config2(args, torch, dist, world, rank, local, dev):
+    """BASELINE config 2 at its own size: a 1,000,000-unit queue (4 types, prio
+    U[0,1024), all untargeted) against 65,536 hanging Reserves per step; a step
+    = the Reserve batch + the SS_UNRESERVE of its matches (as the metric leg),
+    inputs resident in HBM, args.c2_steps timed steps after args.warmup.  The
+    last timed batch is checked against the sequential result."""
+    from adlb_amd import shards, synth
+    from adlb_amd.server import Server
+    R, N = args.reserves, args.c2_units
+    w = synth.config2(n_units=N, n_types=args.types, n_reserves=R, seed=shards.shard_seed(args.seed + 20, rank))
+    srv = Server(w.user_types, w.num_app_ranks, world, rank, max_units=N, device=local)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    srv.set_stream(stream.cuda_stream)
+    try:
+        units = np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(N, -1), np.zeros(N),
+                          np.full(N, -1), np.full(N, -1)], axis=1).astype(np.int32)
+        srv.put_batch(units)
+        del units
+        W2, K2 = max(args.warmup, 1), args.c2_steps
+        nb = W2 + K2
+        rng = np.random.default_rng(args.seed + 27 + rank)
+        reqs = np.empty((nb, R, 18), np.int32)
+        for b in range(nb):
+            reqs[b, :, 0] = np.arange(R, dtype=np.int32)
+            reqs[b, :, 1] = 1
+            reqs[b, :, 2:] = synth.type_vectors(rng, w.user_types, R) if b else w.r_types
+        d_reqs = torch.from_numpy(reqs).to(dev)
+        d_resp = torch.empty((nb, R, 12), dtype=torch.int32, device=dev)
+        p_req = [d_reqs[b].data_ptr() for b in range(nb)]
+        p_resp = [d_resp[b].data_ptr() for b in range(nb)]
+
+        def step(b):
+            srv.reserve_batch_device(R, p_req[b], p_resp[b])
+            srv.unreserve_resp_device(R, p_req[b], p_resp[b])
+
+        for b in range(W2):
+            step(b)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for b in range(W2, nb):
+            step(b)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        matched = int((d_resp[W2:, :, 0] == 1).sum().item())
+        if world > 1:
+            el, matched = shards.reduce_step_timing(el, matched)
+        ec = _exact_check()
+        par = parity_of(lambda: check_units(ec, w, np.arange(1, N + 1, dtype=np.int64), np.ones(N, bool),
+                                            reqs[nb - 1], d_resp[nb - 1].cpu().numpy(), w.num_app_ranks + rank))
+        if world > 1:
+            par["parity"] = all_ranks_true(par["parity"])
+        return {"workload": f"config2: {N} units/shard, {args.types} types, prio U[0,1024), {R} hanging Reserves/step "
+                            f"(70/20/10 single/pair/wildcard), step = reserve batch + unreserve of matched units",
+                "value": matched / el if par["parity"] else None, "unit": "assignments/s", "steps": K2,
+                "warmup": W2, "ms_per_step": el * 1e3 / K2, **par, "scaling": "weak"}
+    finally:
+        srv.close()
+
+
 def bench_wide(args, torch, dev):
     """More than 64 work types (the sorted-runs Reserve path, adlbq_wide.hip):
     a config-2-shaped queue with args.wide_types types; a step = one Reserve
@@ -1203,6 +1270,11 @@ def main():
         res["chain_per_batch"] = {"fields": ["passes", "recomputed", "fallback", "timeouts"], "batches": chain_batches}
     srv.close()
     del d_reqs, d_resp
+    if not args.no_config2:
+        try:
+            res["config2"] = bench_config2(args, torch, dist, world, rank, local, dev)
+        except Exception as e:  # reported, not fatal: the metric line above stands
+            res["config2"] = {"error": f"{type(e).__name__}: {e}"}
     if not args.no_config3:
         try:
             res["config3"] = bench_config3(args, torch, dist, world, rank, local, dev)

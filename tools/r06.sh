@@ -17,7 +17,7 @@ trap "kill $HB" EXIT
 python -c "import torch" > /dev/null 2>&1
 PART=${1:-all}
 shift
-M="--no-cpu --no-pmc --no-host-path --no-config3 --no-config4 --no-config5 --no-wide"
+M="--no-cpu --no-pmc --no-host-path --no-config2 --no-config3 --no-config4 --no-config5 --no-wide"
 case "$PART" in
 sel)
   timeout -k 10 900 python -u -m pytest "$@" -m gpu -v -x --timeout 200 --timeout-method thread > $O/sel.log 2>&1
