@@ -232,7 +232,7 @@ struct adlbq_server {
     int cap_req = 0;
     unsigned long long *d_mask = nullptr;
     int *d_tmatch = nullptr, *d_umatch = nullptr;
-    int *d_mslot = nullptr;            // [cap_req] the slot the last reserve batch gave request j (-1: none)
+    int2 *d_mslot = nullptr;           // [cap_req] (slot, wqseqno) the last reserve batch gave request j (-1: none)
     int2 *d_rh = nullptr;              // [cap_req] (rank, hang) of the last batch's requests (k_finalize)
     int *d_reqbuf = nullptr, *d_respbuf = nullptr;  // host-API staging
     int *d_dem = nullptr;              // [T]
@@ -334,6 +334,9 @@ struct adlbq_server {
     int targeted_scan = -1;            // "targeted_scan": 1 = the pre-targeted match scans the rank buckets
                                        //   (k_targeted), 0 = the sorted index (k_targeted_idx), -1 = by size
     long long tscan_batches = 0;       // batches whose targeted phase scanned the buckets (stat "tscan_batches")
+    int unres_trust = 1;               // "unres_trust": the unreserve of the last batch's own responses, nothing
+                                       //   changed since, from its (slot, wqseqno) records alone
+    long long unres_trusted_calls = 0; // such unreserves (stat "unres_trusted")
     unsigned long long rank_arrivals = 0;  // rank blocks launched in k_rank_chain0 so far (their counter's target)
     int *d_jpref = nullptr;            // [cap_req / 64 + 1] exclusive prefix of seg_cnt (k_thresholds' extra workgroup)
     bool jpref_ok = false;             // this batch's k_thresholds wrote d_jpref
@@ -368,6 +371,10 @@ struct adlbq_server {
     int group_launch = 1;              // "group_launch": 0 = adlbq_reserve_group_device launches this handle alone
     const int *last_reqs = nullptr;    // the last batch's request array and size (its d_rh rows describe it)
     int last_R = 0;
+    // mut_epoch: bumped by every queue change (wq_changed) and reserve launch; mslot_epoch: its value when
+    // the last batch that wrote d_mslot was launched (the unreserve of that batch's own responses is then
+    // exact from d_mslot alone: adlbq_unreserve_resp_device)
+    unsigned long long mut_epoch = 0, mslot_epoch = ~0ull;
     int fin_flat = 512;                // "fin_flat": k_finalize grids up to this size arrive at one counter
     ::GroupRec *grec = nullptr;        // non-null: launch_reserve records its launches (adlbq_reserve_group_device)
     // the group launch's argument tables (kept by the group's first handle): pinned staging x 2, device copy
@@ -442,7 +449,10 @@ void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
 bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi = nullptr);
-inline void wq_changed(adlbq_server *h) { h->batch_export_k = 0; }  // the last batch's lists no longer describe the wq  // newest landed batch's candidate sort plan
+inline void wq_changed(adlbq_server *h) {
+    h->batch_export_k = 0;
+    h->mut_epoch++;
+}  // the last batch's lists no longer describe the wq  // newest landed batch's candidate sort plan
 bool sort_hint(adlbq_server *h);  // parked Reserves alive, upper bound (no sync)  // newest landed batch snapshot -> rq_n_upper
 int ensure_rq_capacity(adlbq_server *h, int extra);
 void stage_begin(adlbq_server *h, const char *name, hipEvent_t *ev);
@@ -454,7 +464,7 @@ int sync_batch_counters(adlbq_server *h);  // synchronise; h->ctr from the last 
 int wide_choose(adlbq_server *h, int R, const int *d_reqs);
 int launch_keyrank(adlbq_server *h, int R);  // 8 < T <= 64: lists sorted and ranked (k_kr_*)
 bool keyrank_hint(adlbq_server *h);         // no failed keyrank landed recently  // T > ADLBQ_MAX_TYPES: the batch's choices
-int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12);  // k_unreserve_resp
+int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12, int trusted);  // k_unreserve_resp
 int group_join(adlbq_server *const *hs, const std::vector<int> &m);     // hs[m[0]]'s stream waits for the members'
 int group_release(adlbq_server *const *hs, const std::vector<int> &m);  // the members' streams wait for hs[m[0]]'s
 int launch_export(adlbq_server *h, int k, int *d_out, long long *d_navail);
@@ -483,9 +493,25 @@ int launch_export_after_group(const ExportAfterGroup &g, int n, int k, int Tmax,
 __device__ __forceinline__ void unreserve_resp_body(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
                                                     const long long *__restrict__ seq2slot, long long nseq,
                                                     uint32_t *meta, int *pin, const int4 *__restrict__ rrec,
-                                                    long long *anchor, const int *__restrict__ mslot, int ntypes,
-                                                    int bid, const int2 *__restrict__ rh = nullptr) {
+                                                    long long *anchor, const int2 *__restrict__ mslot, int ntypes,
+                                                    int bid, const int2 *__restrict__ rh, bool trusted) {
     int i = bid * blockDim.x + threadIdx.x;
+    if (trusted) {
+        // nothing changed the queue since the batch that wrote mslot (these requests'): its record is the
+        // unit's slot and wqseqno, the unit is still live and pinned to the request's rank, and its
+        // priority is at most the anchor (that batch's k_thresholds bound every unit its scan saw, the
+        // chosen ones included; small / one-Reserve batches leave the anchor as it was) -- no gather of
+        // meta / pin / record and no anchor update
+        if (i < n) {
+            const int rc = resp[(long long)ADLBQ_RESP_INTS * i], seq = resp[(long long)ADLBQ_RESP_INTS * i + 5];
+            const int2 ms = mslot[i];
+            if (rc == 1 && ms.x >= 0 && ms.y == seq) {
+                pin[ms.x] = -1;
+                __hip_atomic_fetch_and(meta + ms.x, ~(uint32_t)M_PINNED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        return;
+    }
     int t = -1, up = INT_MIN;
     // lane u holds anchor[u] (T <= 64), loaded with the responses: only a unit above it needs an
     // atomic max (one per type of the wave; every wave adding to one word would serialise them)
@@ -495,7 +521,7 @@ __device__ __forceinline__ void unreserve_resp_body(const int *__restrict__ reqs
         const int rc = resp[(long long)ADLBQ_RESP_INTS * i], seq = resp[(long long)ADLBQ_RESP_INTS * i + 5];
         // the last batch's own requests: (rank, hang) compacted by its prep (8 B instead of a 72 B stride)
         const int rank = rh != nullptr ? rh[i].x : reqs[(long long)ADLBQ_RESERVE_INTS * i];
-        const int ms = mslot != nullptr ? mslot[i] : -1;
+        const int ms = mslot != nullptr ? mslot[i].x : -1;
         if (rc == 1 && seq > 0 && seq < nseq) {
             long long slot = ms;
             uint32_t m = 0;

@@ -3132,7 +3132,7 @@ struct FinArgs {
     const int4 *rrec;
     const int *needsort;
     int *sortfail;
-    int *mslot;  // [R] out: the slot request j was given, or -1 (adlbq_unreserve_resp_device reads it back)
+    int2 *mslot;  // [R] out: (slot, wqseqno) request j was given, or -1 (adlbq_unreserve_resp_device reads it back)
     const int2 *rh;  // [R] (rank, hang) as prep_block copied them: 8 B per request instead of a 72 B record stride
     int flat;        // grids up to this size arrive at one counter ("fin_flat"), larger ones by 8 groups
     int snap_diag;   // diagnostic ("fin_snap_diag"): the snapshot's host stores not drained before the tag
@@ -3164,7 +3164,6 @@ __device__ __forceinline__ bool pos_in_list(unsigned int pos, int npages, DevCou
 __device__ __forceinline__ void fin_request(const FinArgs &f, int j, bool failed, int2 rk, int tm, int um) {
     const int rank = rk.x, hang = failed ? 0 : rk.y;
     const int slot = failed ? -1 : tm >= 0 ? tm : (um >= 0 ? f.cslot[um] : -1);
-    f.mslot[j] = slot;
     int o[ADLBQ_RESP_INTS] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1, -1};
     if (failed) {
         o[0] = -1;  // ADLB_ERROR
@@ -3185,6 +3184,7 @@ __device__ __forceinline__ void fin_request(const FinArgs &f, int j, bool failed
     } else if (!hang) {
         o[0] = -2;  // NO_CURR_WORK
     }
+    f.mslot[j] = make_int2(slot, o[5]);
     const bool parks = slot < 0 && hang;
     int *out = f.resp + (long long)ADLBQ_RESP_INTS * j;
     if (f.resp16) {  // 16-byte aligned rows: three (or two and a half) vector stores instead of twelve
@@ -3783,9 +3783,9 @@ int ensure_req_capacity(adlbq_server *h, int n) {
     AQ_HIP(hipMalloc((void **)&h->d_jpref, sizeof(int) * ((nc + 63) / 64 + 1)));
     AQ_HIP(hipMalloc((void **)&h->d_tmatch, sizeof(int) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_umatch, sizeof(int) * nc));
-    AQ_HIP(hipMalloc((void **)&h->d_mslot, sizeof(int) * nc));
+    AQ_HIP(hipMalloc((void **)&h->d_mslot, sizeof(int2) * nc));
     AQ_HIP(hipMalloc((void **)&h->d_rh, sizeof(int2) * nc));
-    AQ_HIP(hipMemsetAsync(h->d_mslot, 0xff, sizeof(int) * nc, h->stream));
+    AQ_HIP(hipMemsetAsync(h->d_mslot, 0xff, sizeof(int2) * nc, h->stream));
     AQ_HIP(hipMalloc((void **)&h->d_reqbuf, sizeof(int) * ADLBQ_RESERVE_INTS * (size_t)nc));
     AQ_HIP(hipMalloc((void **)&h->d_respbuf, sizeof(int) * ADLBQ_RESP_INTS * (size_t)nc));
     const size_t nseg = (size_t)(nc + SEG - 1) / SEG, T1 = (size_t)std::max(h->T, 1);
@@ -4745,6 +4745,9 @@ static FinArgs fin_args(adlbq_server *h, int R, const int *d_reqs, int *d_resp, 
 static void batch_launched(adlbq_server *h, int R, int export_k, const int *d_reqs) {
     h->last_reqs = d_reqs;  // its d_rh rows describe these requests (adlbq_unreserve_resp_device)
     h->last_R = R;
+    // its k_finalize (fin_request) writes d_mslot; a batch with targeted units in the queue is not trusted
+    // (k_thresholds' anchor bound covers the open bucket's units only)
+    h->mslot_epoch = h->live_targeted == 0 ? h->mut_epoch : ~0ull;
     h->batch_export_k = export_k;
     h->batch_export_R = R;
     h->launched_reserves += R;
@@ -5060,6 +5063,7 @@ static int launch_recorded(adlbq_server *h, GroupRec &r) {
 int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
     int rc;
     const auto host_t0 = std::chrono::steady_clock::now();
+    h->mut_epoch++;   // pins units (and may fail before writing d_mslot)
     h->hint_stamp++;  // landed-snapshot hints are looked up once for this launch
     h->reserve_batches++;
     using hclk = std::chrono::steady_clock;

@@ -1221,15 +1221,22 @@ __global__ __launch_bounds__(256) void k_info_fused(const int *__restrict__ page
 
 __global__ void k_unreserve_resp(const int *__restrict__ reqs, const int *__restrict__ resp, int n,
                                  const long long *__restrict__ seq2slot, long long nseq, uint32_t *meta, int *pin,
-                                 const int4 *__restrict__ rrec, long long *anchor, const int *__restrict__ mslot,
-                                 int ntypes, const int2 *__restrict__ rh) {
-    unreserve_resp_body(reqs, resp, n, seq2slot, nseq, meta, pin, rrec, anchor, mslot, ntypes, blockIdx.x, rh);
+                                 const int4 *__restrict__ rrec, long long *anchor, const int2 *__restrict__ mslot,
+                                 int ntypes, const int2 *__restrict__ rh, int trusted) {
+    unreserve_resp_body(reqs, resp, n, seq2slot, nseq, meta, pin, rrec, anchor, mslot, ntypes, blockIdx.x, rh,
+                        trusted != 0);
 }
 
 // The last batch's compacted (rank, hang) rows when the unreserve is of that batch's own requests
 // (k_finalize read the same rows), else none (the ranks come from the request records).
 static const int2 *unres_rh(const adlbq_server *h, const int *d_reqs18, int n) {
     return (h->d_rh && d_reqs18 == h->last_reqs && n == h->last_R) ? h->d_rh : nullptr;
+}
+// ... and nothing has changed the queue since that batch launched (read before this call's wq_changed):
+// k_unreserve_resp's exact path from the batch's (slot, wqseqno) records alone
+static int unres_trusted(const adlbq_server *h, const int *d_reqs18, int n) {
+    return (unres_rh(h, d_reqs18, n) != nullptr && h->d_mslot && n <= h->cap_req && h->unres_trust &&
+            h->mslot_epoch == h->mut_epoch) ? 1 : 0;
 }
 
 // adlbq_unreserve_resp_group_device: up to UNRES_GROUP shards per launch, blockIdx.y = shard, the
@@ -1244,9 +1251,10 @@ struct UnresArgs {
     int *pin;
     const int4 *rrec;
     long long *anchor;
-    const int *mslot;
+    const int2 *mslot;
     int ntypes;
     const int2 *rh;
+    int trusted;
 };
 struct UnresGroup {
     UnresArgs a[UNRES_GROUP];
@@ -1255,7 +1263,7 @@ __global__ __launch_bounds__(256) void k_unreserve_resp_g(const UnresGroup g) {
     const UnresArgs &a = g.a[blockIdx.y];
     if ((int)blockIdx.x * 256 >= a.n) return;  // whole workgroups return together
     unreserve_resp_body(a.reqs, a.resp, a.n, a.seq2slot, a.nseq, a.meta, a.pin, a.rrec, a.anchor, a.mslot, a.ntypes,
-                        blockIdx.x, a.rh);
+                        blockIdx.x, a.rh, a.trusted != 0);
 }
 
 // Several handles' work as one launch on the first handle's stream (hs[m[0]]):
@@ -1996,11 +2004,12 @@ int adlbq_unreserve(adlbq_server *h, int rank, int wqseqno, int new_pin_rank, in
 
 }  // extern "C"
 namespace adlbq {
-int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12) {
+int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12, int trusted) {
+    if (trusted) h->unres_trusted_calls++;
     k_unreserve_resp<<<(n + 255) / 256, 256, 0, h->stream>>>(d_reqs18, d_resp12, n, h->d_seq2slot, h->next_wqseqno,
                                                              h->d_meta, h->d_pin, h->d_rrec, h->d_anchor,
                                                              (h->d_mslot && n <= h->cap_req) ? h->d_mslot : nullptr,
-                                                             std::min(h->T, 64), unres_rh(h, d_reqs18, n));
+                                                             std::min(h->T, 64), unres_rh(h, d_reqs18, n), trusted);
     AQ_HIP(hipGetLastError());
     return ADLBQ_OK;
 }
@@ -2008,25 +2017,27 @@ int launch_unreserve_resp(adlbq_server *h, int n, const int *d_reqs18, const int
 extern "C" {
 
 int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12) {
+    const int trusted = (h && ok_handle(h) && n > 0) ? unres_trusted(h, d_reqs18, n) : 0;
     if (h) wq_changed(h);
     if (!ok_handle(h) || n < 0 || (n && (!d_reqs18 || !d_resp12)))
         return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_device");
     if (!n) return ADLBQ_OK;
     hipSetDevice(h->device);
-    return launch_unreserve_resp(h, n, d_reqs18, d_resp12);
+    return launch_unreserve_resp(h, n, d_reqs18, d_resp12, trusted);
 }
 
 int adlbq_unreserve_resp_group_device(adlbq_server *const *hs, int n, const int *const *d_reqs18,
                                       const int *const *d_resp12, const int *counts) {
     if (n < 0 || (n && (!hs || !d_reqs18 || !d_resp12 || !counts)))
         return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_group_device");
-    std::vector<int> m;
+    std::vector<int> m, trust(n > 0 ? n : 0);
     for (int i = 0; i < n; i++) {
         if (!ok_handle(hs[i]) || counts[i] < 0 || (counts[i] && (!d_reqs18[i] || !d_resp12[i])) ||
             hs[i]->device != hs[0]->device)
             return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_group_device: bad handle, count or pointer, or mixed devices");
         for (int j = 0; j < i; j++)
             if (hs[j] == hs[i]) return fail(ADLBQ_ERR_ARG, "adlbq_unreserve_resp_group_device: a handle appears twice");
+        trust[i] = counts[i] > 0 ? unres_trusted(hs[i], d_reqs18[i], counts[i]) : 0;
         wq_changed(hs[i]);
         if (counts[i] > 0) m.push_back(i);
     }
@@ -2042,7 +2053,7 @@ int adlbq_unreserve_resp_group_device(adlbq_server *const *hs, int n, const int 
             const int c = counts[mm[j]];
             g.a[j] = UnresArgs{d_reqs18[mm[j]], d_resp12[mm[j]], c, h->d_seq2slot, h->next_wqseqno, h->d_meta, h->d_pin,
                                h->d_rrec, h->d_anchor, (h->d_mslot && c <= h->cap_req) ? h->d_mslot : nullptr,
-                               std::min(h->T, 64), unres_rh(h, d_reqs18[mm[j]], c)};
+                               std::min(h->T, 64), unres_rh(h, d_reqs18[mm[j]], c), trust[mm[j]]};
             nb = std::max(nb, (c + 255) / 256);
         }
         adlbq_server *L = hs[mm[0]];
@@ -2627,6 +2638,10 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->fin_snap_diag = value ? 1 : 0;
         return ADLBQ_OK;
     }
+    if (n == "unres_trust") {
+        h->unres_trust = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
     if (n == "fuse_rank_chain") {
         h->fuse_rank_chain = value ? 1 : 0;
         return ADLBQ_OK;
@@ -2806,6 +2821,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     }
     if (n == "bound_faults") return h->ctr.bound_faults;
     if (n == "tscan_batches") return h->tscan_batches;
+    if (n == "unres_trusted") return h->unres_trusted_calls;
     if (n == "sort_timeouts" || n == "batch_failed") {  // batches answered ADLB_ERROR because k_rank's wait
         refresh_counters(h);                                // for an in-launch sort gave up (0 unless broken)
         return h->ctr.batch_failed;

@@ -461,6 +461,11 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
                                          for k in HACC if k not in HACC_MS},
         "scaling": "weak",
     }
+    out["rq_per_shard"] = {"cap": [srv.stat("rq_cap") for srv in srvs],
+                           "slots": [srv.stat("rq_slots") for srv in srvs],
+                           "device_reclaims": [srv.stat("rq_reclaims") for srv in srvs],
+                           "sync_reclaims": [srv.stat("hacc:rq_reclaims") for srv in srvs],
+                           "waits": [srv.stat("hacc:rq_waits") for srv in srvs]}
     bg, bd = group.check()
     out["steal_check"] = {"bad_grants": bg, "bad_deletes": bd}
     par = parity_of(lambda: config3_parity(_exact_check(), wks, h_reqs, d_resp, nb - 1, group, last_round,

@@ -516,10 +516,13 @@ def test_repeated_batches_vs_oracle(gpu_available, name):
         assert st["spec_lists"] == 1 or -100000 < st["spec_lists"] < 0, ("spec_lists", st["spec_lists"])
 
 
-def test_unreserve_resp_restores_queue(gpu_available):
+@pytest.mark.parametrize("trust", [1, 0])
+def test_unreserve_resp_restores_queue(gpu_available, trust):
     """adlbq_unreserve_resp_device (SS_UNRESERVE of every unit a batch matched,
     read from the batch's own responses) leaves the queue as it was: the same
-    batch then gets the same answers, which equal the oracle's."""
+    batch then gets the same answers, which equal the oracle's.  trust=1: the
+    unreserve straight after the batch takes the exact path from the batch's
+    (slot, wqseqno) records ("unres_trust"); 0: the checked path."""
     import torch
     w = synth.config2(n_units=100_000, n_reserves=8192, seed=231)
     reqs = np.concatenate([w.r_rank[:, None], w.r_hang[:, None].astype(np.int32), w.r_types],
@@ -532,6 +535,7 @@ def test_unreserve_resp_restores_queue(gpu_available):
                           np.zeros(w.n_units), np.full(w.n_units, -1), np.full(w.n_units, -1)],
                          axis=1).astype(np.int32)
         s.put_batch(units)
+        s.set_param("unres_trust", trust)
         d_req = torch.from_numpy(reqs).cuda()
         d_resp = torch.empty((len(reqs), 12), dtype=torch.int32, device="cuda")
         outs = []
@@ -542,10 +546,73 @@ def test_unreserve_resp_restores_queue(gpu_available):
             outs.append(d_resp.cpu().numpy().copy())
             s.unreserve_resp_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
             s.sync()
+        assert s.stat("unres_trusted") == (3 if trust else 0)
+        # a second unreserve of the same responses finds nothing pinned (the checked path: the first changed
+        # the queue), and the queue still answers the same
+        s.unreserve_resp_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
+        s.reserve_batch_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
+        s.sync()
+        outs.append(d_resp.cpu().numpy().copy())
+        assert s.stat("unres_trusted") == (3 if trust else 0)
         assert (outs[0][:, 0] == 1).all()
         for o in outs[1:]:
             assert np.array_equal(o, outs[0])
         assert np.array_equal(outs[0][:, :10], np.asarray(exp)[:, :10])
+
+
+@pytest.mark.parametrize("between", ["none", "put", "get"])
+def test_unreserve_resp_partial_vs_oracle(gpu_available, between):
+    """Unreserve of a batch where some Reserves match and others do not (more
+    Reserves than units), with nothing, a Put above every unit or a Get in
+    between (those two take the checked path), then batches that deplete the
+    queue: every answer equals the oracle's, stepped through the same events."""
+    import torch
+    w = synth.config2(n_units=3000, n_reserves=4096, seed=233)
+    cfg = (w.num_app_ranks, 1, 0)
+    hang = np.zeros(len(w.r_rank), np.int32)
+    reqs = np.concatenate([w.r_rank[:, None], hang[:, None], w.r_types], axis=1).astype(np.int32)
+    units = np.stack([w.u_type, w.u_prio, w.u_answer, w.u_target, w.u_len, np.full(w.n_units, -1),
+                      np.zeros(w.n_units), np.full(w.n_units, -1), np.full(w.n_units, -1)],
+                     axis=1).astype(np.int32)
+    o = oracle.Oracle("own")
+    o.init(w.user_types, *cfg)
+
+    def step(ev):
+        return synth.split_outputs(o.replay(np.asarray(ev, dtype=np.int32).ravel()))
+
+    step(synth.put_events(w))
+    with Server(w.user_types, w.num_app_ranks, max_units=w.n_units + 16) as s:
+        s.set_param("small_pages", 0)  # the batch pipeline (a 3000-unit bucket would take k_reserve_small)
+        s.put_batch(units)
+        d_req = torch.from_numpy(reqs).cuda()
+        d_resp = torch.empty((len(reqs), 12), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        s.reserve_batch_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
+        s.sync()
+        first = d_resp.cpu().numpy().copy()
+        exp = np.asarray(step(synth.reserve_events(w.r_rank, w.r_types, hang)))
+        assert np.array_equal(first[:, :10], exp[:, :10])
+        m = first[:, 0] == 1
+        assert 0 < m.sum() < len(reqs)
+        back = [(int(r), int(x[5])) for r, x in zip(w.r_rank, first) if x[0] == 1]
+        if between == "put":
+            extra = units[:1].copy()
+            extra[0, 1] = 10 ** 6  # above every unit: the anchor must follow it
+            s.put_batch(extra)
+            step(np.concatenate([[synth.OP_PUT], extra[0, :5], [-1, 0, -1, -1]]))
+        elif between == "get":
+            r, q = back.pop(0)  # fetched, so the oracle does not unreserve it
+            s.get_reserved(r, q)
+            step([synth.OP_GET, r, q])
+        s.unreserve_resp_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
+        step([[synth.OP_UNRESERVE, r, q, -1] for r, q in back])
+        assert s.stat("unres_trusted") == (1 if between == "none" else 0)
+        for b in range(3):
+            s.reserve_batch_device(len(reqs), d_req.data_ptr(), d_resp.data_ptr())
+            s.sync()
+            got = d_resp.cpu().numpy()
+            exp = np.asarray(step(synth.reserve_events(w.r_rank, w.r_types, hang)))
+            assert np.array_equal(got[:, :10], exp[:, :10]), f"batch {b} after the unreserve"
 
 
 @pytest.mark.parametrize("seed", [62, 63])
