@@ -105,9 +105,17 @@ __device__ __forceinline__ void prep_block(const PrepArgs &a, const int blk) {
     int ur[TB <= 8 ? TB : 1];
     bool uok[TB <= 8 ? TB : 1];
     if constexpr (TB <= 8) {
+        // every load unconditional (a clamped index) under one uniform branch: a load per "t < T"
+        // branch waited for the one before
+        if (T > 0) {
+#pragma unroll
+            for (int t = 0; t < TB; t++) ur[t] = utypes[t < T ? t : T - 1];
+        } else {
+#pragma unroll
+            for (int t = 0; t < TB; t++) ur[t] = 0;
+        }
 #pragma unroll
         for (int t = 0; t < TB; t++) {
-            ur[t] = t < T ? utypes[t] : 0;
             uok[t] = t < T;
 #pragma unroll
             for (int t2 = 0; t2 < t; t2++) uok[t] = uok[t] && ur[t2] != ur[t];
@@ -233,16 +241,27 @@ __device__ __forceinline__ void load_quarter(const int *__restrict__ prio, const
     const int4 *P4 = reinterpret_cast<const int4 *>(prio + base);
     const uint4 *M4 = reinterpret_cast<const uint4 *>(meta + base);
     const int wide = pwide[pg], pb = pbase[pg];  // in flight with the meta loads
+    // unconditional loads (slot 0 past the fill, masked after; the masks opaque to the optimiser):
+    // loads under a per-lane branch were issued one at a time
+    unsigned int km[4];
+    int ic[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int idx = (w * 4 + k) * 64 + lane;
-        mv[k] = idx * 4 < fill ? M4[idx] : make_uint4(0, 0, 0, 0);
+        km[k] = idx * 4 < fill ? ~0u : 0u;
+        ic[k] = idx * 4 < fill ? idx : 0;
+        mv[k] = M4[ic[k]];
     }
+    asm volatile("" : "+v"(km[0]), "+v"(km[1]), "+v"(km[2]), "+v"(km[3]));
+#pragma unroll
+    for (int k = 0; k < 4; k++) mv[k] = make_uint4(mv[k].x & km[k], mv[k].y & km[k], mv[k].z & km[k], mv[k].w & km[k]);
     if (wide) {
 #pragma unroll
+        for (int k = 0; k < 4; k++) pv[k] = P4[ic[k]];
+#pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int idx = (w * 4 + k) * 64 + lane;
-            pv[k] = idx * 4 < fill ? P4[idx] : make_int4(0, 0, 0, 0);
+            const int m = (int)km[k];
+            pv[k] = make_int4(pv[k].x & m, pv[k].y & m, pv[k].z & m, pv[k].w & m);
         }
     } else {
 #pragma unroll
@@ -742,10 +761,23 @@ __device__ __forceinline__ void seg_prefix(const int *__restrict__ seg_cnt, int 
     __shared__ int wtot[TH_THREADS / 64];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     int base = 0;
-    for (int q0 = 0; q0 < nq; q0 += TH_THREADS) {
-        const int q = q0 + tid;
-        const int v = q < nq ? seg_cnt[q] : 0;
-        int x = v;  // inclusive scan over the wave
+    constexpr int PER = 4;  // consecutive entries per thread, their loads in flight together
+    for (int q0 = 0; q0 < nq; q0 += TH_THREADS * PER) {
+        const int qa = q0 + tid * PER;
+        int v[PER], sum = 0;
+        unsigned int okm = 0u;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            okm |= (qa + k < nq ? 1u : 0u) << k;
+            v[k] = seg_cnt[qa + k < nq ? qa + k : 0];
+        }
+        asm volatile("" : "+v"(okm));  // masks opaque to the optimiser (no load sunk into a branch)
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            v[k] &= 0 - (int)((okm >> k) & 1u);
+            sum += v[k];
+        }
+        int x = sum;  // inclusive scan over the wave
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(x, o, 64);
@@ -755,7 +787,12 @@ __device__ __forceinline__ void seg_prefix(const int *__restrict__ seg_cnt, int 
         __syncthreads();
         int pre = base;
         for (int k = 0; k < w; k++) pre += wtot[k];
-        if (q < nq) jp[q] = pre + x - v;
+        pre += x - sum;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            if (qa + k < nq) jp[qa + k] = pre;
+            pre += v[k];
+        }
         int tot = 0;
         for (int k = 0; k < TH_THREADS / 64; k++) tot += wtot[k];
         base += tot;
@@ -1145,20 +1182,27 @@ __device__ __forceinline__ void select_wave_body(
     const int p0 = (p / CHUNK) * CHUNK;
 #pragma unroll
     for (int r = 0; r < CPL; r++) {
+        // every lane loads (a column past the threshold or the list reads column 0 of the same rows: one
+        // line, no traffic to speak of) and masks after: loads under a branch were issued one column
+        // group at a time
         const int c = lane + r * 64;
-        ppv[r] = 0;
         const int thc = __shfl(th_l, (c / NB) & 63, 64);
         const bool use = c < C && (c % NB) <= thc;
-        if (ADLBQ_SELW_GATE ? use : c < C) {  // ungated: the loads need not wait for theta
-            const int nch = (npages + CHUNK - 1) / CHUNK;  // the tile prefixes follow the chunk sums
-            unsigned int v = csum[(long long)(p / CHUNK) * C + c] + csum[(long long)(nch + p / CHUNK / TH_ROWS) * C + c];
-            unsigned short g[CHUNK - 1];
+        const int cc = (ADLBQ_SELW_GATE ? use : c < C) ? c : 0;  // ungated: the loads need not wait for theta
+        const int nch = (npages + CHUNK - 1) / CHUNK;  // the tile prefixes follow the chunk sums
+        const unsigned int v0 = csum[(long long)(p / CHUNK) * C + cc],
+                           v1 = csum[(long long)(nch + p / CHUNK / TH_ROWS) * C + cc];
+        unsigned int g[CHUNK - 1];
 #pragma unroll
-            for (int q = 0; q < CHUNK - 1; q++) g[q] = p0 + q < p ? gh[(long long)(p0 + q) * C + c] : (unsigned short)0;
+        for (int q = 0; q < CHUNK - 1; q++) g[q] = gh[(long long)(p0 + q < p ? p0 + q : p0) * C + cc];
+        unsigned int km = use ? ~0u : 0u, gm = 0u;  // opaque to the optimiser (no select sunk into a branch)
 #pragma unroll
-            for (int q = 0; q < CHUNK - 1; q++) v += g[q];
-            ppv[r] = use ? v : 0u;
-        }
+        for (int q = 0; q < CHUNK - 1; q++) gm |= (p0 + q < p ? 1u : 0u) << q;
+        asm volatile("" : "+v"(km), "+v"(gm));
+        unsigned int v = v0 + v1;
+#pragma unroll
+        for (int q = 0; q < CHUNK - 1; q++) v += g[q] & (0u - ((gm >> q) & 1u));
+        ppv[r] = v & km;
     }
     // the lists' further entries: read when the list is that long (rarely; a list is
     // typically a few dozen entries at the metric size)
@@ -1688,6 +1732,8 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
     __shared__ int cslot[TGT_CACHE], cex[TGT_CACHE + 1];
     __shared__ int dem[64], coff[65], cmid[64], gbase[64], gend[64], dbase[64], dend[64], ccnt[64];
     __shared__ int gnext[64], dnext[64], amain[64];
+    __shared__ int4 s_st[64];                    // the block serve: per type {hd, cached, offset, more}
+    __shared__ unsigned long long s_ball[64];    // ... and the lanes choosing it
     __shared__ unsigned long long cut[64];
     __shared__ int nlist, wcnt[4], wsum[4], s_over;
     const int b = blockIdx.x, r = bucket_ranks[b], p0 = pstart[b];
@@ -1925,9 +1971,24 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
             int hd = 0;                                      // cached heads consumed
             int gn = tl ? gbase[lane] + gnext[lane] : 0;     // main and delta positions past the cache
             int dn = tl ? dbase[lane] + dnext[lane] : 0;
-            unsigned long long hk = ~0ull, nk = ~0ull;  // head key and the next cached one
-            unsigned long long lastk = 0ull;            // key of the type's last unit taken (0: none)
-            int hs = -1, ns = -1;
+            // head key / slot and the next three cached entries in registers: a Reserve's advance is
+            // register moves (an LDS read per advance made every Reserve wait for the one before);
+            // the ring is refilled from the cache after each block of 64, or when it runs dry
+            unsigned long long hk = ~0ull, k1 = ~0ull, k2 = ~0ull, k3 = ~0ull;
+            unsigned long long lastk = 0ull;  // key of the type's last unit taken (0: none)
+            int hs = -1, s1 = -1, s2 = -1, s3 = -1;
+            auto fill = [&]() {  // type lane, cached heads left: the head and the ring from entry hd on
+                if (!tl || hd >= cn) return;
+                const int b = co + hd;
+                hk = ckey[b];
+                hs = cslot[b];
+                k1 = hd + 1 < cn ? ckey[b + 1] : ~0ull;
+                s1 = hd + 1 < cn ? cslot[b + 1] : -1;
+                k2 = hd + 2 < cn ? ckey[b + 2] : ~0ull;
+                s2 = hd + 2 < cn ? cslot[b + 2] : -1;
+                k3 = hd + 3 < cn ? ckey[b + 3] : ~0ull;
+                s3 = hd + 3 < cn ? cslot[b + 3] : -1;
+            };
             auto walk = [&](unsigned long long &k, int &sl) {  // next available unit past the cache (slow path)
                 k = ~0ull;
                 sl = -1;
@@ -1953,15 +2014,92 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                     }
                 }
             };
-            if (tl) {
-                if (cn > 0) { hk = ckey[co]; hs = cslot[co]; }
-                if (cn > 1) { nk = ckey[co + 1]; ns = cslot[co + 1]; }
-            }
+            fill();
             for (int k0 = 0; k0 < n; k0 += 64) {
                 const unsigned long long mv = k0 + lane < n ? smk[k0 + lane] : 0ull;
                 const int jv = k0 + lane < n ? sreq[k0 + lane] : 0;
                 const int kn = min(64, n - k0);
-                for (int kk = 0; kk < kn; kk++) {
+                int myslot = -1;  // lane kk: the unit Reserve k0 + kk takes (written after the block)
+                bool solved = false;
+                if (!(tdiag & 8)) {
+                    // ---- the block in parallel (lane i = Reserve k0 + i), Jacobi rounds on the choice
+                    // types: lane i's candidate of type t is cached entry hd_t + #{earlier lanes choosing
+                    // t}; lane k is exact by round k + 1, and the fixed point is the serial answer unless
+                    // some lane needs an entry past a type's cache with more units behind it (a walk):
+                    // then the block goes one by one below.  Per round: one ballot per wanted type
+                    // (into LDS), then each lane's types' state, counts and keys in two LDS rounds.
+                    s_st[lane] = make_int4(tl ? hd : 0, tl ? cn : 0, tl ? co : 0,
+                                           (tl && (gn < ge || dn < de || (hd >= cn && hk != ~0ull))) ? 1 : 0);
+                    unsigned long long want = mv;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) want |= __shfl_xor(want, o, 64);
+                    want = readlane64(want, 0);
+                    int tt[4];  // this lane's first four types (-1: none); the rest in `rest`
+                    unsigned long long rest = mv;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        tt[q] = rest ? __ffsll((long long)rest) - 1 : -1;
+                        rest &= rest - 1;
+                    }
+                    const unsigned long long lt = lanemask_lt();
+                    int ch = -1;
+                    bool unc = false;
+                    for (int round = 0; round <= kn; round++) {
+                        for (unsigned long long wm = want; wm; wm &= wm - 1) {
+                            const int t = __ffsll((long long)wm) - 1;
+                            const unsigned long long b = __ballot(ch == t);
+                            if (lane == 0) s_ball[t] = b;
+                        }
+                        __builtin_amdgcn_wave_barrier();  // one wave's LDS operations stay in order
+                        unsigned long long best = ~0ull;
+                        int nc = -1;
+                        unc = false;
+                        auto look = [&](int t, const int4 st, unsigned long long b) {
+                            const int idx = st.x + (int)__popcll(b & lt);
+                            if (idx < st.y) {
+                                const unsigned long long kt = ckey[st.z + idx];
+                                if (kt < best) best = kt, nc = t;
+                            } else if (st.w) {
+                                unc = true;
+                            }
+                        };
+                        int4 st4[4];
+                        unsigned long long b4[4];
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            st4[q] = s_st[tt[q] >= 0 ? tt[q] : 0];
+                            b4[q] = s_ball[tt[q] >= 0 ? tt[q] : 0];
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; q++)
+                            if (tt[q] >= 0) look(tt[q], st4[q], b4[q]);
+                        for (unsigned long long mm = rest; mm; mm &= mm - 1) {
+                            const int t = __ffsll((long long)mm) - 1;
+                            look(t, s_st[t], s_ball[t]);
+                        }
+                        const bool changed = nc != ch;
+                        ch = nc;
+                        __builtin_amdgcn_wave_barrier();  // the reads above before the next round's writes
+                        if (!__ballot(changed)) break;
+                    }
+                    if (!__ballot(unc)) {
+                        solved = true;
+                        // s_ball holds the final choices' ballots (the last round changed nothing)
+                        if (ch >= 0) {
+                            const int4 st = s_st[ch];
+                            myslot = cslot[st.z + st.x + (int)__popcll(s_ball[ch] & lt)];
+                        }
+                        const int took = (tl && ((want >> lane) & 1ull)) ? (int)__popcll(s_ball[lane]) : 0;
+                        if (took > 0) {
+                            hd += took;
+                            lastk = ckey[co + hd - 1];
+                            hk = ~0ull;  // fill() below reloads the head and the ring (or leaves none)
+                            hs = -1;
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+                for (int kk = 0; kk < kn && !solved; kk++) {
                     const unsigned long long m = readlane64(mv, kk);
                     // a type whose cache ran dry walks before it competes (uniform loop over such types)
                     const unsigned long long dry = __ballot(tl && hk == ~0ull && hd >= cn && (gn < ge || dn < de)) & m;
@@ -1977,23 +2115,21 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                         }
                     }
                     if (bt < 0 || best == ~0ull) continue;
-                    if (lane == 0) {
-                        const int j = __builtin_amdgcn_readlane(jv, kk);
-                        tmatch[j] = __builtin_amdgcn_readlane(hs, bt);
-                        atomicSub(&seg_cnt[j >> 6], 1);
-                    }
+                    // no global store in the loop: a walk's loads make the compiler wait for every
+                    // outstanding memory operation at the loop's join (vmcnt counts stores and atomics)
+                    const int sl = __builtin_amdgcn_readlane(hs, bt);
+                    if (lane == kk) myslot = sl;
                     if (lane == bt) {  // advance: the next cached head, else the walk later
                         lastk = hk;
                         if (hd < cn) hd++;
-                        if (hd < cn) {
-                            hk = nk;
-                            hs = ns;
-                            if (hd + 1 < cn) { nk = ckey[co + hd + 1]; ns = cslot[co + hd + 1]; }
-                        } else {
-                            hk = ~0ull;
-                            hs = -1;
-                        }
+                        hk = k1, hs = s1, k1 = k2, s1 = s2, k2 = k3, s2 = s3, k3 = ~0ull, s3 = -1;
+                        if (hk == ~0ull) fill();  // the ring ran dry (the cache may hold more)
                     }
+                }
+                fill();
+                if (lane < kn && myslot >= 0) {  // the block's choices, one lane each
+                    tmatch[jv] = myslot;
+                    atomicSub(&seg_cnt[jv >> 6], 1);
                 }
             }
             // overflow only: the next Reserves of the rank resume after the last unit taken of each type
@@ -2208,12 +2344,17 @@ __device__ __forceinline__ void rank_body(const RankArgs &ra, const int bid, con
             for (int g0 = bid * (NT / 64) + w; g0 * 64 < R; g0 += waves * DU) {
                 unsigned long long m[DU];
                 int tmv[DU];
+                unsigned int okm = 0u;  // unconditional loads, masked after (opaque masks)
 #pragma unroll
                 for (int i = 0; i < DU; i++) {
                     const int j = (g0 + i * waves) * 64 + lane;
-                    m[i] = j < R ? mask[j] : 0ull;
-                    tmv[i] = j < R ? tmatch[j] : 0;
+                    okm |= (j < R ? 1u : 0u) << i;
+                    m[i] = mask[j < R ? j : 0];
+                    tmv[i] = tmatch[j < R ? j : 0];
                 }
+                asm volatile("" : "+v"(okm));
+#pragma unroll
+                for (int i = 0; i < DU; i++) m[i] &= 0ull - (unsigned long long)((okm >> i) & 1u);
 #pragma unroll
                 for (int i = 0; i < DU; i++) {
                     const int g = g0 + i * waves;
@@ -2393,27 +2534,42 @@ __device__ __forceinline__ int level_guess(const ChainArgs a, int J) {
     const unsigned int key = (unsigned int)J << 6;
     int my = 0;
     for (int g = 0; g < a.T; g += TB) {
+        // every load unconditional (clamped index, masked after; masks opaque to the optimiser): a load
+        // per type under its own condition was issued only after the one before had returned
         int lo[TB], hi[TB], off[TB];
 #pragma unroll
         for (int q = 0; q < TB; q++) {
-            const int t = g + q;
-            off[q] = t < a.T ? a.candoff[t] : 0;
+            const int t = min(g + q, a.T - 1);
+            off[q] = a.candoff[t];
+            hi[q] = a.candlen[t];
+        }
+        unsigned int tm = 0u;
+#pragma unroll
+        for (int q = 0; q < TB; q++) tm |= (g + q < a.T && J > 0 ? 1u : 0u) << q;
+        asm volatile("" : "+v"(tm));
+#pragma unroll
+        for (int q = 0; q < TB; q++) {
             lo[q] = 0;
-            hi[q] = (t < a.T && J > 0) ? a.candlen[t] : 0;
+            hi[q] &= 0 - (int)((tm >> q) & 1u);
         }
         while (true) {
             bool open = false;
 #pragma unroll
             for (int q = 0; q < TB; q++) open |= hi[q] > lo[q];
             if (!open) break;
-            unsigned int v[TB];
+            unsigned int v[TB], pm = 0u;
             int step[TB];
 #pragma unroll
             for (int q = 0; q < TB; q++) {
                 step[q] = (hi[q] - lo[q] + 63) >> 6;
                 const int idx = lo[q] + lane * step[q];
-                v[q] = (hi[q] > lo[q] && idx < hi[q]) ? a.crank[off[q] + idx] : ~0u;
+                const bool ok = hi[q] > lo[q] && idx < hi[q];
+                pm |= (ok ? 1u : 0u) << q;
+                v[q] = a.crank[ok ? off[q] + idx : 0];
             }
+            asm volatile("" : "+v"(pm));
+#pragma unroll
+            for (int q = 0; q < TB; q++) v[q] |= ((pm >> q) & 1u) - 1u;  // ~0u where not probed
 #pragma unroll
             for (int q = 0; q < TB; q++) {
                 if (hi[q] <= lo[q]) continue;
@@ -2471,13 +2627,28 @@ __device__ __forceinline__ int seg_solve_small(const ChainArgs a, int s, int jb,
     int tm[SEG_BLOCKS];
     unsigned char sd[SEG_BLOCKS];
     if (load) {  // a re-solve of one segment (jb == j0): its masks, results of the targeted phase, seeds
+        unsigned int okm = 0u;  // unconditional loads, masked after (as in the chain's prologue)
 #pragma unroll
         for (int i = 0; i < SEG_BLOCKS; i++) {
             const int j = jb + i * 64 + lane;
-            const bool ok = j < j1;
-            mk[i] = ok ? a.mask[j] : 0ull;
-            tm[i] = ok ? a.tmatch[j] : 0;
-            sd[i] = (seeded && ok) ? a.cht[j] : CHT_NONE;
+            okm |= (j < j1 ? 1u : 0u) << i;
+            mk[i] = a.mask[j < j1 ? j : 0];
+            tm[i] = a.tmatch[j < j1 ? j : 0];
+        }
+        if (seeded) {
+#pragma unroll
+            for (int i = 0; i < SEG_BLOCKS; i++) {
+                const int j = jb + i * 64 + lane;
+                sd[i] = a.cht[j < j1 ? j : 0];
+            }
+        }
+        asm volatile("" : "+v"(okm));
+#pragma unroll
+        for (int i = 0; i < SEG_BLOCKS; i++) {
+            const unsigned int b = (okm >> i) & 1u;
+            mk[i] &= 0ull - (unsigned long long)b;
+            tm[i] &= 0 - (int)b;
+            sd[i] = (seeded && b) ? sd[i] : CHT_NONE;
         }
     }
 #pragma unroll
@@ -2614,11 +2785,30 @@ __device__ __forceinline__ int seg_solve_wide(const ChainArgs a, int s, int my_s
     }
     unsigned long long mk[SEG_BLOCKS];
     unsigned char sd[SEG_BLOCKS];
+    {
+        unsigned int okm = 0u;  // unconditional loads, masked after (as in the chain's prologue)
+        int tmv[SEG_BLOCKS];
 #pragma unroll
-    for (int i = 0; i < SEG_BLOCKS; i++) {
-        const int j = j0 + i * 64 + lane;
-        mk[i] = (j < j1 && a.tmatch[j] < 0) ? a.mask[j] : 0ull;
-        sd[i] = (seeded && j < j1) ? a.cht[j] : CHT_NONE;
+        for (int i = 0; i < SEG_BLOCKS; i++) {
+            const int j = j0 + i * 64 + lane;
+            okm |= (j < j1 ? 1u : 0u) << i;
+            tmv[i] = a.tmatch[j < j1 ? j : 0];
+            mk[i] = a.mask[j < j1 ? j : 0];
+        }
+        if (seeded) {
+#pragma unroll
+            for (int i = 0; i < SEG_BLOCKS; i++) {
+                const int j = j0 + i * 64 + lane;
+                sd[i] = a.cht[j < j1 ? j : 0];
+            }
+        }
+        asm volatile("" : "+v"(okm));
+#pragma unroll
+        for (int i = 0; i < SEG_BLOCKS; i++) {
+            const bool ok = ((okm >> i) & 1u) && tmv[i] < 0;
+            mk[i] = ok ? mk[i] : 0ull;
+            sd[i] = (seeded && ((okm >> i) & 1u)) ? sd[i] : CHT_NONE;
+        }
     }
     // one wave owns win and rec: its LDS ops complete in order, only the compiler must not reorder
     __builtin_amdgcn_wave_barrier();
@@ -3239,10 +3429,12 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
             f.gcut_next[threadIdx.x] = LLONG_MIN;
         }
     }
+    int nsl = 0;  // every type's sort flag at once (one thread's loop waited for each load in turn)
+    for (int t = threadIdx.x; t < T; t += blockDim.x) nsl |= f.needsort[t];
     if (total > 0)
         park_tail(f.dc, f.donors, f.reqs, f.R, f.pmask, f.rq_rank, f.rq_types, f.rq_live, f.rq_req, f.rq_seq, f.ctr,
                   f.resp);
-    __syncthreads();
+    const int ns = __syncthreads_or(nsl != 0);
     if (threadIdx.x == 0) {
         DevCounters *ctr = f.ctr;
         if (failed) {
@@ -3250,9 +3442,7 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
             __hip_atomic_store(f.sortfail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // per batch
         }
         if (total == 0) ctr->n_parked_last = 0;
-        int ns = 0;
-        for (int t = 0; t < T; t++) ns |= f.needsort[t];
-        ctr->needsort_last = ns;  // the host launches the segmented sort while this holds
+        ctr->needsort_last = ns ? 1 : 0;  // the host launches the segmented sort while this holds
         for (int g = 0; g < 8; g++) ctr->fin_group[g] = 0;
         ctr->fin_top = 0;
     }
@@ -3263,7 +3453,13 @@ __device__ __forceinline__ void fin_tail(const FinArgs &f, int total, bool faile
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int *src = reinterpret_cast<const int *>(f.ctr);
         int *dst = reinterpret_cast<int *>(f.snap);
-        for (int i = threadIdx.x; i < (int)(sizeof(DevCounters) / 4); i += 64) dst[i] = ld_sc1(src + i);
+        constexpr int NW = (int)(sizeof(DevCounters) / 4), NR = (NW + 63) / 64;
+        int v[NR];  // every load in flight before the first store
+#pragma unroll
+        for (int q = 0; q < NR; q++) v[q] = threadIdx.x + 64 * q < NW ? ld_sc1(src + threadIdx.x + 64 * q) : 0;
+#pragma unroll
+        for (int q = 0; q < NR; q++)
+            if (threadIdx.x + 64 * q < NW) dst[threadIdx.x + 64 * q] = v[q];
         if (f.snap_diag) {  // timing diagnostic only: no drain, no release (a torn snapshot may land)
             if (threadIdx.x == 0) __hip_atomic_store(&f.snap->snap_tag, f.snap_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
@@ -3364,10 +3560,17 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
         for (int i = 0; i < 8; i++) {
             const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
             const int fill = p == a.npages - 1 ? a.tail_fill : PAGE;
-            const bool ok = pg[h] >= 0 && gi * 4 < fill;
+            const bool ok = pg[h] >= 0 && gi * 4 < fill, okp = ok && wide[h];
             const long long base = (long long)(ok ? pg[h] : 0) << PAGE_SHIFT;
-            mv[i] = ok ? reinterpret_cast<const uint4 *>(a.meta + base)[gi] : make_uint4(0, 0, 0, 0);
-            pv[i] = ok && wide[h] ? reinterpret_cast<const int4 *>(a.prio + base)[gi] : make_int4(0, 0, 0, 0);
+            // unconditional loads (an address select, slot 0 when out of range): a load inside a
+            // branch made the compiler wait for each pair before issuing the next
+            const uint4 m4 = reinterpret_cast<const uint4 *>(a.meta + base)[ok ? gi : 0];
+            const int4 p4 = reinterpret_cast<const int4 *>(a.prio + (okp ? base : 0))[okp ? gi : 0];
+            // masks opaque to the optimiser: a select would be sunk into a branch around the load
+            unsigned int km = ok ? ~0u : 0u, kp = okp ? ~0u : 0u;
+            asm volatile("" : "+v"(km), "+v"(kp));
+            mv[i] = make_uint4(m4.x & km, m4.y & km, m4.z & km, m4.w & km);
+            pv[i] = make_int4(p4.x & (int)kp, p4.y & (int)kp, p4.z & (int)kp, p4.w & (int)kp);
         }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
@@ -3494,16 +3697,30 @@ __device__ __forceinline__ void chain0_body(ChainArgs a, ChainPass cp, int prefi
     int tm[NRB];
     const int j1 = min(a.R, s * SEG + SEG);
     if constexpr (TB <= 8) {
+        // unconditional loads (clamped index, masked after with masks opaque to the optimiser): a load
+        // under a per-lane condition was issued only after the one before had returned
+        unsigned int okm = 0u;
 #pragma unroll
         for (int i = 0; i < NRB; i++) {
             const int j = jb + i * 64 + lane;
-            const bool ok = j < j1;
-            mk[i] = ok ? a.mask[j] : 0ull;
-            tm[i] = ok ? a.tmatch[j] : 0;
+            okm |= (j < j1 ? 1u : 0u) << i;
+            mk[i] = a.mask[j < j1 ? j : 0];
+            tm[i] = a.tmatch[j < j1 ? j : 0];
+        }
+        asm volatile("" : "+v"(okm));
+#pragma unroll
+        for (int i = 0; i < NRB; i++) {
+            const unsigned int b = (okm >> i) & 1u;
+            mk[i] &= 0ull - (unsigned long long)b;
+            tm[i] &= 0 - (int)b;
         }
     }
     // lane t: type t's list offset and length (lane T: the total), all loads of the prologue in flight together
-    const int my_off = lane <= T ? a.candoff[lane] : 0, my_len = lane < T ? a.candlen[lane] : 0;
+    unsigned int lm = (lane <= T ? 1u : 0u) | (lane < T ? 2u : 0u);
+    int my_off = a.candoff[lane <= T ? lane : 0], my_len = a.candlen[lane < T ? lane : 0];
+    asm volatile("" : "+v"(lm));
+    my_off &= 0 - (int)(lm & 1u);
+    my_len &= 0 - (int)((lm >> 1) & 1u);
     // J from the prefix k_thresholds left, unless k_rank changed seg_cnt since (a type with no candidate)
     const int jpv = a.jpref != nullptr ? a.jpref[jb >> 6] : 0;
     const bool use_jp = a.jpref != nullptr && __ballot(lane < T && my_len == 0) == 0ull;
@@ -3883,6 +4100,12 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
     hipStream_t s = h->stream;
     hipEvent_t ev;
     const bool scan = np > 0 && T > 0;
+    auto lt0 = std::chrono::steady_clock::now();
+    auto lsec = [&](const char *name) {  // host time per launch of the scan ("hacc:ls_*")
+        const auto now = std::chrono::steady_clock::now();
+        h->hacc[name] += std::chrono::duration_cast<std::chrono::nanoseconds>(now - lt0).count();
+        lt0 = now;
+    };
     // the open bucket's pages in one run of ids (one bulk Put): pass 1 computes the page id
     int pg0 = np > 0 ? h->open.pages[0] : -1;
     for (int i = 1; i < np && pg0 >= 0; i++)
@@ -3916,9 +4139,11 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             h->grec->prep = GPrep{pa, nprep, ha, grid};
             h->grec->lds_prep = (size_t)lds;
         } else {
+            lsec("ls_pre");
             kph<<<grid, 256, lds, s>>>(pa, nprep, ha);
         }
         stage_end(h, "hist", ev);
+        lsec("ls_hist");
     }
     if (scan) {
         const int nchunks = (np + CHUNK - 1) / CHUNK;
@@ -3937,6 +4162,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
                 nprep > 0 ? 1 : 0, h->d_gcut, h->d_seg_cnt, (R + 63) / 64, jp ? h->d_jpref : nullptr);
             h->jpref_ok = jp;
             stage_end(h, "thresholds", ev);
+            lsec("ls_thr");
         }
         stage_begin(h, "select", &ev);
         auto sel = T <= 4 ? k_select_open<4> : T <= 8 ? k_select_open<8> : k_select_open<64>;
@@ -3965,6 +4191,7 @@ static int launch_scan(adlbq_server *h, const PrepArgs &pa, int nprep, bool sort
             (sort || !h->rank_in_select) ? nullptr : h->d_crank, (!sort && T <= 8) ? h->d_lv : nullptr, h->d_rtype, R,
             kst_for(h, np, 1));
         stage_end(h, "select", ev);
+        lsec("ls_sel");
         if (sort) {  // a reserve batch sorts inside k_rank
             stage_begin(h, "sort", &ev);
             k_sort_types<<<T, 1024, 0, s>>>(h->d_needsort, h->d_candoff, h->d_candlen, h->d_ckey, h->d_cslot,
@@ -4818,14 +5045,26 @@ __global__ __launch_bounds__(SMALL_THREADS) void k_reserve_small(SmallArgs a) {
     uint32_t gm[GPT];
     int gp[GPT];
 #pragma unroll
-    for (int g = 0; g < GPT; g++) {
-        const int i = g * SMALL_THREADS + tid;
-        gm[g] = 0u;
-        gp[g] = LOWEST;
-        if (i < nslots) {
-            const long long slot = ((long long)a.pages[i >> PAGE_SHIFT] << PAGE_SHIFT) | (i & (PAGE - 1));
-            gm[g] = a.meta[slot];
-            gp[g] = a.prio[slot];
+    for (int g = 0; g < GPT; g++) gm[g] = 0u, gp[g] = LOWEST;
+    if (nslots > 0) {
+        // unconditional loads (slot 0 of page 0 past the end, masked after): loads inside a branch were
+        // issued one unit at a time.  Two rounds: the page ids, then every unit's meta and prio.
+        int pgs[GPT];
+#pragma unroll
+        for (int g = 0; g < GPT; g++) {
+            const int i = g * SMALL_THREADS + tid;
+            pgs[g] = a.pages[(i < nslots ? i : 0) >> PAGE_SHIFT];
+        }
+#pragma unroll
+        for (int g = 0; g < GPT; g++) {
+            const int i = g * SMALL_THREADS + tid;
+            const long long slot = ((long long)pgs[g] << PAGE_SHIFT) | (i < nslots ? (i & (PAGE - 1)) : 0);
+            const uint32_t m = a.meta[slot];
+            const int pr = a.prio[slot];
+            unsigned int km = i < nslots ? ~0u : 0u;  // opaque: a select would be sunk into a branch
+            asm volatile("" : "+v"(km));
+            gm[g] = m & km;  // 0: not LIVE
+            gp[g] = pr;
         }
     }
     unsigned long long gk[GPT];  // this thread's units' keys, ~0 when not available

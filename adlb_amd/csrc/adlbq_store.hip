@@ -228,8 +228,13 @@ void maybe_compact_rq(adlbq_server *h) {
     // a compaction launched earlier that this view does not show yet: its effect is unknown, wait for it
     if (v->rq_reclaims < h->rq_reclaims_launched) return;
     const long long span = (long long)v->rq_n - v->rq_head;
-    if (span <= 2ll * v->rq_live + 4096 && span * 2 <= h->rq_cap) return;
-    if (span <= v->rq_live + 256) return;  // nothing much to reclaim
+    // mostly dead slots between head and tail, or the append index past half the slots: a steal round
+    // deletes every Reserve it settles and the head follows, so the span stays short while rq_n still
+    // climbs to the capacity check (which then reclaimed synchronously: config 3, every fifth step)
+    const bool thin = span > 2ll * v->rq_live + 4096 || span * 2 > h->rq_cap;
+    const bool high = 2ll * v->rq_n > h->rq_cap;
+    if (!thin && !high) return;
+    if (!high && span <= v->rq_live + 256) return;  // nothing much to reclaim
     h->rq_compact_calls = 0;
     h->rq_compactions++;
     h->rq_reclaims_launched++;
@@ -253,6 +258,21 @@ int ensure_rq_capacity(adlbq_server *h, int extra) {
         need = h->rq_n_upper + extra;
         if (need <= h->rq_cap) return ADLBQ_OK;
         h->hacc["rq_waits"] += 1;
+        {  // what the bound was made of (stats "hacc:rqw_*": the last wait)
+            const int N = adlbq_server::NSNAP;
+            int li = -1, nl = 0;
+            for (int k = 1; k <= N; k++) {
+                const int i = (h->snap_next - k + N) % N;
+                if (!h->snap_at[i]) continue;
+                if (snap_landed(h, i)) { if (li < 0) li = i; nl++; }
+            }
+            h->hacc["rqw_need"] = need;
+            h->hacc["rqw_cap"] = h->rq_cap;
+            h->hacc["rqw_landed"] = nl;
+            h->hacc["rqw_snap_rq_n"] = li >= 0 ? h->h_snap[li].rq_n : -1;
+            h->hacc["rqw_since"] = li >= 0 ? h->launched_reserves - h->snap_at[li] : -1;
+            h->hacc["rqw_stale"] = h->ctr_stale ? 1 : 0;
+        }
         // the oldest batches in flight first, one at a time (a stream synchronisation would
         // drain the queue and leave the GPU idle while the host issues the next batch)
         while (!h->rq_wait_sync && wait_oldest_snapshot(h)) {
@@ -751,7 +771,15 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
         for (int q = 0; q < w; q++) pre += s_cnt[q];
         const int pos = pre + __popcll(b & lanemask_lt());
         if (live && pos < PM_CAP) {
-            const int *tv = rq_types + (long long)k * NREQ;
+            // the entry's 16 types in four vector loads, all in flight before the lookups (a load per
+            // type inside the lookup loop waited for each in turn)
+            const int4 *tv4 = reinterpret_cast<const int4 *>(rq_types + (long long)k * NREQ);
+            int tv[NREQ];
+#pragma unroll
+            for (int q = 0; q < NREQ / 4; q++) {
+                const int4 x = tv4[q];
+                tv[4 * q] = x.x, tv[4 * q + 1] = x.y, tv[4 * q + 2] = x.z, tv[4 * q + 3] = x.w;
+            }
             unsigned long long m = 0;
             bool wild = false;
 #pragma unroll

@@ -128,6 +128,8 @@ def parse():
     ap.add_argument("--c4-param", action="append", default=[], metavar="NAME=V",
                     help="config-4 leg: any adlbq_set_param (diagnostics), repeatable")
     ap.add_argument("--kernel-stamps", action="store_true", help="diagnostic: phase stamps of passes 1 and 2 (us)")
+    ap.add_argument("--diag-first", action="store_true",
+                    help="diagnostic (never a reported number): host sections of the first timed step")
     ap.add_argument("--param", action="append", default=[], metavar="NAME=V",
                     help="metric leg: any adlbq_set_param (diagnostics), repeatable")
     ap.add_argument("--c4-chain-stats", action="store_true",
@@ -465,7 +467,9 @@ def bench_config3(args, torch, dist, world, rank, local, dev):
                            "slots": [srv.stat("rq_slots") for srv in srvs],
                            "device_reclaims": [srv.stat("rq_reclaims") for srv in srvs],
                            "sync_reclaims": [srv.stat("hacc:rq_reclaims") for srv in srvs],
-                           "waits": [srv.stat("hacc:rq_waits") for srv in srvs]}
+                           "waits": [srv.stat("hacc:rq_waits") for srv in srvs],
+                           "last_wait": [{k: srv.stat("hacc:rqw_" + k) for k in ("need", "cap", "landed", "snap_rq_n",
+                                                                                "since", "stale")} for srv in srvs[:2]]}
     bg, bd = group.check()
     out["steal_check"] = {"bad_grants": bg, "bad_deletes": bd}
     par = parity_of(lambda: config3_parity(_exact_check(), wks, h_reqs, d_resp, nb - 1, group, last_round,
@@ -1117,10 +1121,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     HACC_M = ("req_cap", "tables", "rq_cap", "scan_cap", "l_scan", "sort", "l_rank", "l_chain", "l_fin", "total")
-    hacc0 = {k: srv.stat("hacc:" + k) for k in HACC_M}
+    HACC_D = ("ls_pre", "ls_hist", "ls_thr", "ls_sel")  # diagnostic only (--diag-first)
+    hacc0 = {k: srv.stat("hacc:" + k) for k in HACC_M + HACC_D}
     t_enq = []
     t0 = time.perf_counter()
+    first_sections = None
     for b in range(args.warmup, nb):
+        if args.diag_first and b == args.warmup + 1:  # diagnostic only: host sections of the first timed step
+            first_sections = {k: round((srv.stat("hacc:" + k) - hacc0[k]) / 1e3, 1) for k in HACC_M + HACC_D}
         step(b)
         t_enq.append(time.perf_counter())
     t_submit = time.perf_counter() - t0  # host time to enqueue the K steps
@@ -1248,6 +1256,7 @@ def main():
         "ms_per_step": el * 1e3 / args.steps,
         "host_submit_ms_per_step": round(t_submit * 1e3 / args.steps, 4),
         "timed_region_host_ms": enqueue_ms,
+        **({"diag_first_step_host_us": first_sections} if first_sections else {}),
         "reserve_host_sections_ms_per_step": host_sections,
         "host_buffer_path": host_path,
         "higher_is_better": True,

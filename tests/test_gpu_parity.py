@@ -867,17 +867,29 @@ def test_one_and_pipeline_batches_interleaved_vs_oracle(gpu_available, T):
     assert_same(got, np.concatenate(exp))
 
 
-@pytest.mark.parametrize("mode", [1, 0])
+@pytest.mark.parametrize("mode", [1, 0, 8])
 @pytest.mark.parametrize("name", ["s_c4_targeted", "s_c4_t8_tied", "s_c4_r256"])
 def test_targeted_scan_vs_index_small(gpu_available, name, mode):
     """Small queues with targeted units: the pre-targeted match (xq.c:219-247) by
     scanning each rank bucket (k_targeted, "targeted_scan" 1) and by the sorted
-    index (k_targeted_idx, 0), each with the one-workgroup choice after it."""
+    index (k_targeted_idx, 0: 64 Reserves of a bucket at a time in parallel;
+    8: one by one), each with the one-workgroup choice after it."""
     w = SMALL[name]()
     tr = synth.workload_trace(w)
     cfg = (w.num_app_ranks, 1, 0)
     with Server(w.user_types, *cfg, max_units=w.n_units) as s:
-        s.set_param("targeted_scan", mode)
+        s.set_param("targeted_scan", 1 if mode == 1 else 0)
+        if mode == 8:
+            s.set_param("targeted_diag", 8)
         got = replay.replay(s, tr)
         assert (s.stat("tscan_batches") > 0) == (mode == 1)
     assert_same(got, run_oracle(w.user_types, cfg, tr))
+
+
+def test_config4_2m_targeted_one_by_one_exact(gpu_available):
+    """The pre-targeted match served one Reserve at a time ("targeted_diag" 8)
+    instead of 64-Reserve blocks in parallel (the default): the same exact answers."""
+    w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
+    stats = {}
+    _exact_full(w, batches=3, stats=stats, params=[("targeted_diag", 8)])
+    assert stats["sort_timeouts"] == 0, stats
