@@ -391,7 +391,7 @@ struct adlbq_server {
     long long n_keyrank = 0, kr_fail_seen = 0, kr_skip_until = 0;
     int rq_wait_sync = 1;              // "rq_wait_sync": rq backpressure by stream sync (0: spin on the oldest snapshot, measured slower)
     int targeted_diag = 0;             // diagnostic ("targeted_diag"): parts of k_targeted_idx skipped (1, 2, 4: wrong
-                                       //   results); 8: every Reserve served one by one (A/B, exact)
+                                       //   results); 8: 64 Reserves of a bucket at a time by Jacobi rounds (A/B, exact)
     int kr_par = 0;                    // parity of keyrank's chunk-count rows
     // ---- steal round (adlbq_steal.hip): device export + pinned host mirror
     int *d_export = nullptr; long long cap_export = 0;   // [T*k*8 recs | T nrec]

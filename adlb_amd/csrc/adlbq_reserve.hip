@@ -2021,7 +2021,7 @@ __global__ __launch_bounds__(256) void k_targeted_idx(const int *__restrict__ bu
                 const int kn = min(64, n - k0);
                 int myslot = -1;  // lane kk: the unit Reserve k0 + kk takes (written after the block)
                 bool solved = false;
-                if (!(tdiag & 8)) {
+                if (tdiag & 8) {  // A/B ("targeted_diag" 8): measured slower than the serve below (config 4)
                     // ---- the block in parallel (lane i = Reserve k0 + i), Jacobi rounds on the choice
                     // types: lane i's candidate of type t is cached entry hd_t + #{earlier lanes choosing
                     // t}; lane k is exact by round k + 1, and the fixed point is the serial answer unless
@@ -3396,6 +3396,28 @@ __device__ __forceinline__ void fin_request(const FinArgs &f, int j, bool failed
 // Two-level arrival of workgroup bid of nb (8 groups, then one top counter)
 // keeps every counter's atomics to about nb / 8; a count rides in the high
 // half.  One thread; returns (parked in the batch << 32) | 1 for the last.
+// fin_arrive in two halves: the first atomic (issue), then what its result decides (finish)
+__device__ __forceinline__ unsigned long long fin_arrive_issue(const FinArgs &f, int parked, unsigned int nb,
+                                                               unsigned int bid) {
+    // an index the compiler must treat as per-lane: its wave-level atomic optimisation (one lane's
+    // atomic, the result broadcast with readfirstlane) would wait for the result right here
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    unsigned long long *c = nb <= (unsigned int)f.flat ? &f.ctr->fin_top : &f.ctr->fin_group[bid & 7u];
+    return atomicAdd(c + z, ((unsigned long long)parked << 32) | 1ull);
+}
+__device__ __forceinline__ unsigned long long fin_arrive_finish(const FinArgs &f, int parked, unsigned int nb,
+                                                                unsigned int bid, unsigned long long v) {
+    if (nb <= (unsigned int)f.flat)
+        return (unsigned int)v == nb - 1u ? ((((v >> 32) + (unsigned long long)parked) << 32) | 1ull) : 0ull;
+    const unsigned int g = bid & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
+    if ((unsigned int)v == ng - 1u) {
+        const unsigned long long tg = (v >> 32) + (unsigned long long)parked;
+        const unsigned long long top = atomicAdd(&f.ctr->fin_top, (tg << 32) | 1ull);
+        if ((unsigned int)top == ngroups - 1u) return (((top >> 32) + tg) << 32) | 1ull;
+    }
+    return 0ull;
+}
 __device__ __forceinline__ unsigned long long fin_arrive(const FinArgs &f, int parked, unsigned int nb,
                                                          unsigned int bid) {
     if (nb <= (unsigned int)f.flat) {  // a small grid: one counter, one returning atomic per workgroup
@@ -3480,14 +3502,15 @@ __device__ __forceinline__ void finalize_body(FinArgs f, const int bid_, const i
     __shared__ unsigned long long s_ticket;
     const int j = bid_ * blockDim.x + threadIdx.x;
     if (threadIdx.x == 0) s_parked = 0;
+    // the request's rows first (unconditional, clamped; the past-the-end lanes' values replaced after),
+    // then the batch's failure flag: loaded first, it was waited for before these were issued
+    const int jc = j < f.R ? j : 0;
+    int2 rk = f.rh[jc];
+    int tm = f.tmatch[jc], um = f.umatch[jc];
     const bool failed = fin_failed(f);
-    int2 rk = make_int2(-1, 0);
-    int tm = -1, um = -1;
-    if (j < f.R) {
-        rk = f.rh[j];
-        tm = f.tmatch[j];
-        um = f.umatch[j];
-    }
+    unsigned int in = j < f.R ? 1u : 0u;
+    asm volatile("" : "+v"(in));  // opaque to the optimiser (no select sunk into a branch around the loads)
+    if (!in) rk = make_int2(-1, 0), tm = -1, um = -1;
     __syncthreads();
     if (j < f.R) {
         const bool parks = !failed && rk.y && tm < 0 && um < 0;
@@ -3502,8 +3525,13 @@ __device__ __forceinline__ void finalize_body(FinArgs f, const int bid_, const i
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) s_ticket = fin_arrive(f, s_parked, nbk_, bid_);
+    // the arrival's first atomic goes out, the request's loads and stores follow, and its result is
+    // looked at only after them (the two used to run one after the other in wave 0)
+    unsigned long long v;  // read by thread 0 only (no value on the other lanes: nothing to merge at the join)
+    const int parked = s_parked;
+    if (threadIdx.x == 0) v = fin_arrive_issue(f, parked, nbk_, bid_);
     if (j < f.R) fin_request(f, j, failed, rk, tm, um);
+    if (threadIdx.x == 0) s_ticket = fin_arrive_finish(f, parked, nbk_, bid_, v);
     __syncthreads();
     if (!(s_ticket & 1ull)) return;
     fin_tail(f, (int)(s_ticket >> 32), failed);
@@ -3556,22 +3584,35 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
             pb[h] = pg[h] >= 0 ? a.pbase[pg[h]] : 0;
             wide[h] = pg[h] >= 0 ? a.pwide[pg[h]] : 0;
         }
+        // unconditional meta loads (slot 0 when out of range, masked after with a mask opaque to the
+        // optimiser: a load inside a per-lane branch made the compiler wait for each before the next);
+        // the prio column only on a wide page (h = i / 4 is uniform: one branch per page)
+        unsigned int km[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
             const int fill = p == a.npages - 1 ? a.tail_fill : PAGE;
-            const bool ok = pg[h] >= 0 && gi * 4 < fill, okp = ok && wide[h];
+            const bool ok = pg[h] >= 0 && gi * 4 < fill;
             const long long base = (long long)(ok ? pg[h] : 0) << PAGE_SHIFT;
-            // unconditional loads (an address select, slot 0 when out of range): a load inside a
-            // branch made the compiler wait for each pair before issuing the next
-            const uint4 m4 = reinterpret_cast<const uint4 *>(a.meta + base)[ok ? gi : 0];
-            const int4 p4 = reinterpret_cast<const int4 *>(a.prio + (okp ? base : 0))[okp ? gi : 0];
-            // masks opaque to the optimiser: a select would be sunk into a branch around the load
-            unsigned int km = ok ? ~0u : 0u, kp = okp ? ~0u : 0u;
-            asm volatile("" : "+v"(km), "+v"(kp));
-            mv[i] = make_uint4(m4.x & km, m4.y & km, m4.z & km, m4.w & km);
-            pv[i] = make_int4(p4.x & (int)kp, p4.y & (int)kp, p4.z & (int)kp, p4.w & (int)kp);
+            mv[i] = reinterpret_cast<const uint4 *>(a.meta + base)[ok ? gi : 0];
+            km[i] = ok ? ~0u : 0u;
+            pv[i] = make_int4(0, 0, 0, 0);
         }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (pg[h] >= 0 && wide[h]) {
+                const long long base = (long long)pg[h] << PAGE_SHIFT;
+#pragma unroll
+                for (int i = 4 * h; i < 4 * h + 4; i++) {
+                    const int gi = (tid + 256 * i) & 1023;
+                    pv[i] = reinterpret_cast<const int4 *>(a.prio + base)[gi];  // masked through mv below
+                }
+            }
+        }
+        asm volatile("" : "+v"(km[0]), "+v"(km[1]), "+v"(km[2]), "+v"(km[3]), "+v"(km[4]), "+v"(km[5]),
+                     "+v"(km[6]), "+v"(km[7]));
+#pragma unroll
+        for (int i = 0; i < 8; i++) mv[i] = make_uint4(mv[i].x & km[i], mv[i].y & km[i], mv[i].z & km[i], mv[i].w & km[i]);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;

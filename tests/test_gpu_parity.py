@@ -872,8 +872,8 @@ def test_one_and_pipeline_batches_interleaved_vs_oracle(gpu_available, T):
 def test_targeted_scan_vs_index_small(gpu_available, name, mode):
     """Small queues with targeted units: the pre-targeted match (xq.c:219-247) by
     scanning each rank bucket (k_targeted, "targeted_scan" 1) and by the sorted
-    index (k_targeted_idx, 0: 64 Reserves of a bucket at a time in parallel;
-    8: one by one), each with the one-workgroup choice after it."""
+    index (k_targeted_idx, 0: one Reserve at a time; 8: 64 Reserves of a bucket
+    at a time by Jacobi rounds), each with the one-workgroup choice after it."""
     w = SMALL[name]()
     tr = synth.workload_trace(w)
     cfg = (w.num_app_ranks, 1, 0)
@@ -886,9 +886,9 @@ def test_targeted_scan_vs_index_small(gpu_available, name, mode):
     assert_same(got, run_oracle(w.user_types, cfg, tr))
 
 
-def test_config4_2m_targeted_one_by_one_exact(gpu_available):
-    """The pre-targeted match served one Reserve at a time ("targeted_diag" 8)
-    instead of 64-Reserve blocks in parallel (the default): the same exact answers."""
+def test_config4_2m_targeted_blocks_exact(gpu_available):
+    """The pre-targeted match served 64 Reserves of a bucket at a time by Jacobi
+    rounds ("targeted_diag" 8) instead of one by one: the same exact answers."""
     w = synth.config4(n_units=2_000_000, n_reserves=65_536, n_ranks=1024, seed=9)
     stats = {}
     _exact_full(w, batches=3, stats=stats, params=[("targeted_diag", 8)])
