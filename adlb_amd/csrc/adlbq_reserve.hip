@@ -3562,9 +3562,10 @@ struct OneArgs {
     int *umatch, *cslot;
     FinArgs f;
     int inject;  // test only: the choice is told a position past the page list
+    const uint32_t *zero;  // 16 KB of zeros: the meta read for a group past the open pages
 };
 template <int TB>
-__global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
+__global__ __launch_bounds__(256, 5) void k_reserve_one(OneArgs a) {  // five waves per SIMD: every workgroup of the 10M queue resident at once
     static_assert(TB <= 8, "T <= 8");
     __shared__ unsigned long long smin[4][8];
     __shared__ int s_last;
@@ -3584,18 +3585,17 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
             pb[h] = pg[h] >= 0 ? a.pbase[pg[h]] : 0;
             wide[h] = pg[h] >= 0 ? a.pwide[pg[h]] : 0;
         }
-        // unconditional meta loads (slot 0 when out of range, masked after with a mask opaque to the
-        // optimiser: a load inside a per-lane branch made the compiler wait for each before the next);
-        // the prio column only on a wide page (h = i / 4 is uniform: one branch per page)
-        unsigned int km[8];
+        // unconditional meta loads, a group past the open pages reading zeros (nothing LIVE): a load
+        // inside a per-lane branch made the compiler wait for each before the next, and a mask per
+        // group cost the registers of a fifth wave per SIMD; the prio column only on a wide page
+        // (h = i / 4 is uniform: one branch per page)
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
             const int fill = p == a.npages - 1 ? a.tail_fill : PAGE;
             const bool ok = pg[h] >= 0 && gi * 4 < fill;
-            const long long base = (long long)(ok ? pg[h] : 0) << PAGE_SHIFT;
-            mv[i] = reinterpret_cast<const uint4 *>(a.meta + base)[ok ? gi : 0];
-            km[i] = ok ? ~0u : 0u;
+            const uint32_t *src = ok ? a.meta + ((long long)pg[h] << PAGE_SHIFT) : a.zero;
+            mv[i] = reinterpret_cast<const uint4 *>(src)[gi];
             pv[i] = make_int4(0, 0, 0, 0);
         }
 #pragma unroll
@@ -3609,10 +3609,7 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
                 }
             }
         }
-        asm volatile("" : "+v"(km[0]), "+v"(km[1]), "+v"(km[2]), "+v"(km[3]), "+v"(km[4]), "+v"(km[5]),
-                     "+v"(km[6]), "+v"(km[7]));
-#pragma unroll
-        for (int i = 0; i < 8; i++) mv[i] = make_uint4(mv[i].x & km[i], mv[i].y & km[i], mv[i].z & km[i], mv[i].w & km[i]);
+
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
@@ -3671,11 +3668,24 @@ __global__ __launch_bounds__(256) void k_reserve_one(OneArgs a) {
     unsigned long long gm[TB];
 #pragma unroll
     for (int u = 0; u < TB; u++) gm[u] = ~0ull;
-    for (int b = tid; b < (int)gridDim.x; b += 256)
+    // every workgroup's minima, RW rows per thread in flight at once (clamped rows re-read row 0:
+    // a minimum is idempotent); a loop of one row per step waited for each
+    constexpr int RW = TB <= 4 ? 8 : 4;  // rows per thread per step (registers: RW x TB minima)
+    for (int b0 = 0; b0 < (int)gridDim.x; b0 += RW * 256) {
+        unsigned long long x[RW][TB];
 #pragma unroll
-        for (int u = 0; u < TB; u++)
-            gm[u] = min(gm[u], (unsigned long long)__hip_atomic_load(
-                                   (long long *)(a.part + (long long)b * 8 + u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        for (int k = 0; k < RW; k++) {
+            const int b = b0 + tid + 256 * k, bc = b < (int)gridDim.x ? b : 0;
+#pragma unroll
+            for (int u = 0; u < TB; u++)
+                x[k][u] = (unsigned long long)__hip_atomic_load((long long *)(a.part + (long long)bc * 8 + u),
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int k = 0; k < RW; k++)
+#pragma unroll
+            for (int u = 0; u < TB; u++) gm[u] = min(gm[u], x[k][u]);
+    }
 #pragma unroll
     for (int u = 0; u < TB; u++) {
 #pragma unroll
@@ -5469,9 +5479,12 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             AQ_HIP(hipStreamSynchronize(s));
             if (h->d_onepart) AQ_HIP(hipFree(h->d_onepart));
             h->cap_onepart = std::max(grid, 2 * h->cap_onepart);
-            // [16] arrival counters (ints), then [grid][8] per-type minima
-            AQ_HIP(hipMalloc((void **)&h->d_onepart, sizeof(unsigned long long) * 8 * (h->cap_onepart + 2)));
+            // [16] arrival counters (ints), then [grid][8] per-type minima, then 16 KB of zeros (the
+            // meta k_reserve_one reads past the open pages: nothing LIVE, no mask register needed)
+            const size_t zoff = (size_t)8 * (h->cap_onepart + 2);
+            AQ_HIP(hipMalloc((void **)&h->d_onepart, sizeof(unsigned long long) * (zoff + 2048)));
             AQ_HIP(hipMemsetAsync(h->d_onepart, 0, sizeof(unsigned long long) * 16, s));
+            AQ_HIP(hipMemsetAsync(h->d_onepart + zoff, 0, sizeof(unsigned long long) * 2048, s));
         }
         DevCounters *const snap = h->d_snap + h->snap_next;
         h->snap_tag[h->snap_next] = ++h->snap_tags;
@@ -5481,7 +5494,8 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             if (h->open.pages[(size_t)i] != pg0 + i) pg0 = -1;
         const OneArgs oa{pa, h->d_open_pages, np, h->open.tail_fill, pg0, h->d_prio, h->d_meta, h->d_pbase, h->d_pwide, T,
                          h->d_onepart + 16, reinterpret_cast<int *>(h->d_onepart), h->d_umatch, h->d_cslot,
-                         fin_args(h, R, d_reqs, d_resp, snap), h->bound_inject};
+                         fin_args(h, R, d_reqs, d_resp, snap), h->bound_inject,
+                         reinterpret_cast<const uint32_t *>(h->d_onepart + (size_t)8 * (h->cap_onepart + 2))};
         h->bound_inject = 0;
         stage_begin(h, "one", &ev);
         if (T <= 4) k_reserve_one<4><<<grid, 256, 0, s>>>(oa);
