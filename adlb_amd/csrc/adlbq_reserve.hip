@@ -3647,18 +3647,19 @@ __global__ __launch_bounds__(256, 5) void k_reserve_one(OneArgs a) {  // five wa
     }
     __syncthreads();
     if (tid == 0) {  // two-level arrival: eight group counters, then the top one (a.arrive[8])
-        // release: this workgroup's minima (and, through the group counter, its group's) are visible
-        // to whoever observes the arrival; the last workgroup acquires below before reading a.part
+        // The minima go out as sc1 (agent-scope) stores drained by vmcnt(0) before the arrival, and the
+        // last workgroup reads them with sc1 (agent-scope atomic) loads: MI355X_MICROARCH.md's valid
+        // hand-off form without a release / acquire pair.  An acq_rel arrival cost every workgroup an
+        // L2 write-back and invalidate (~10 us on the one-Reserve latency, measured).
         const unsigned int nb = gridDim.x, g = blockIdx.x & 7u, ng = (nb - g + 7u) / 8u, ngroups = min(nb, 8u);
         int last = 0;
-        if ((unsigned int)__hip_atomic_fetch_add(a.arrive + g, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ng - 1u)
-            last = (unsigned int)__hip_atomic_fetch_add(a.arrive + 8, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+        if ((unsigned int)__hip_atomic_fetch_add(a.arrive + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1u)
+            last = (unsigned int)__hip_atomic_fetch_add(a.arrive + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                    ngroups - 1u;
         s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every workgroup's minima before they are read
     if (tid <= 8) a.arrive[tid] = 0;  // for the next launch (kernel boundary in between)
 #ifdef ADLBQ_ONE_DIAG  // timing diagnostic only (wrong results): the scan and the arrival alone
     return;
@@ -3891,12 +3892,20 @@ template <int TB>
 __global__ __launch_bounds__(64) void k_rank_chain0(RankArgs ra, int rg, ChainArgs a, ChainPass cp, int prefix_next,
                                                     int final) {
     if ((int)blockIdx.x < rg) {
+        // whether the chain will wait for these blocks (its own test, read before rank_body changes any
+        // flag: k_select_open did not rank the candidates, or a type has none): only then is there
+        // anything to write back before the arrival (the release fence writes back the XCD's L2)
+        const int lane = threadIdx.x;
+        const int len = ra.candlen[lane < ra.T ? lane : 0];
+        const bool slow = ld_sc1(&ra.ctr->rank_fast) == 0 || __ballot(lane < ra.T && len == 0) != 0ull;
         rank_body<64>(ra, blockIdx.x, rg);
         __syncthreads();
         if (threadIdx.x == 0) {  // one wave: its stores drained, written back, then the arrival
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (slow) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             atomicAdd(const_cast<unsigned long long *>(a.rdone), 1ull);
         }
         return;
