@@ -3544,20 +3544,25 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
 // ---------------------------------------------------------------- one Reserve against a large open bucket
 // A batch of one Reserve (T <= 8, no targeted units, an open bucket too large
 // for k_reserve_small) in one launch instead of the seven of the pipeline.
-// Every workgroup takes two pages (256 threads, 32 units each, all loads in
-// flight) and finds each type's best available unit by (prio desc, bucket
-// position asc) -- wq_find_hi_prio's order (xq.c:190-217), the pipeline's key;
-// the per-type minima go out write-through and the workgroup arrives.  The
-// last workgroup prepares the request (prep_block), takes the best head among
-// its types, and finalizes it as k_finalize would (pin, response, park,
-// counters, snapshot).
+// At most 512 workgroups step through the bucket's page pairs in bucket order
+// (256 threads, 32 units each per pair, all loads in flight) and find each
+// type's best available unit by (prio desc, bucket position asc) --
+// wq_find_hi_prio's order (xq.c:190-217), the pipeline's key -- folding each
+// pair's minima into per-type global ones (agent-scope atomic min).  A
+// workgroup stops once every type the Reserve names has its best unit so far
+// at the type's anchor (the upper bound of its available priorities) before
+// its next pair: nothing later can come first.  On a queue whose top
+// priority is common that is within the first round of pairs; with a stale
+// anchor the whole bucket is read, as before.  The last workgroup to arrive
+// prepares the request (prep_block), takes the best head among its types, and
+// finalizes it as k_finalize would (pin, response, park, counters, snapshot).
 struct OneArgs {
     PrepArgs pa;
     const int *pages; int npages, tail_fill;
     int pg0;                   // >= 0: the open pages are pg0, pg0 + 1, ... (no page-table read before the loads)
     const int *prio; const uint32_t *meta; const int *pbase, *pwide;
     int T;
-    unsigned long long *part;  // [grid][8] per-type minima
+    unsigned long long *part;  // [8] per-type best key over the workgroups (atomic min; ~0 between launches)
     int *arrive;               // [9] arrival counters: eight groups, then the top (the last workgroup resets them)
     int *umatch, *cslot;
     FinArgs f;
@@ -3565,87 +3570,127 @@ struct OneArgs {
     const uint32_t *zero;  // 16 KB of zeros: the meta read for a group past the open pages
 };
 template <int TB>
-__global__ __launch_bounds__(256, 5) void k_reserve_one(OneArgs a) {  // five waves per SIMD: every workgroup of the 10M queue resident at once
+__global__ __launch_bounds__(256, 2) void k_reserve_one(OneArgs a) {  // at most 512 workgroups: two per CU
     static_assert(TB <= 8, "T <= 8");
     __shared__ unsigned long long smin[4][8];
-    __shared__ int s_last;
+    __shared__ unsigned long long s_want;
+    __shared__ long long s_anc[8];
+    __shared__ int s_last, s_skip;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    unsigned long long kmin[TB];
+    const int npairs = (a.npages + 1) / 2;
+    unsigned long long *const gbest = a.part;  // [8] per-type best key over the workgroups (atomic min)
+    // wave 0: the Reserve's types (a superset of prep_block's mask: every type whose value a slot
+    // names, every type for a -1) and the anchors (upper bounds of the available priorities)
+    if (w == 0) {
+        const int v = a.pa.reqs[2 + (lane < NREQ ? lane : 0)];
+        const int ut = a.pa.utypes[lane < a.T ? lane : 0];
+        const long long an = a.f.anchor[lane < a.T ? lane : 0];
+        const bool wild = __ballot(lane < NREQ && v == -1) != 0ull;
+        unsigned long long want = 0ull;
 #pragma unroll
-    for (int u = 0; u < TB; u++) kmin[u] = ~0ull;
-    {
-        // groups of 4 units: this workgroup's two pages hold 2 x 1024; thread tid takes g = tid + 256 i
-        uint4 mv[8];
-        int4 pv[8];
-        int pb[2], wide[2], pg[2];
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int p = 2 * blockIdx.x + h;
-            pg[h] = p >= a.npages ? -1 : a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
-            pb[h] = pg[h] >= 0 ? a.pbase[pg[h]] : 0;
-            wide[h] = pg[h] >= 0 ? a.pwide[pg[h]] : 0;
+        for (int q = 0; q < NREQ; q++) want |= __ballot(lane < a.T && ut == __shfl(v, q, 64));
+        if (wild) want = (1ull << a.T) - 1;
+        if (lane == 0) s_want = want;
+        if (lane < 8) s_anc[lane] = lane < a.T ? an : LLONG_MAX;
+    }
+    __syncthreads();
+    const unsigned long long want = s_want;
+    // Page pairs in bucket order, gridDim.x workgroups at a time.  A pair is skipped (and so every later
+    // one of this workgroup) once each wanted type's best unit so far sits at its anchor's priority
+    // before the pair: no unit of the pair can come first (prio desc, then bucket position asc).
+    for (int pair = blockIdx.x; pair < npairs; pair += gridDim.x) {
+        if (w == 0) {
+            bool open_t = false;
+            if (lane < TB && ((want >> lane) & 1ull)) {
+                const unsigned long long gb = (unsigned long long)__hip_atomic_load(
+                    (long long *)(gbest + lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const long long an = s_anc[lane];
+                const bool at_anchor = an >= (long long)INT_MIN && an <= (long long)INT_MAX &&
+                                       (unsigned int)(gb >> 32) == ~((unsigned int)(int)an ^ 0x80000000u);
+                open_t = !(gb != ~0ull && at_anchor && (unsigned int)gb < ((unsigned int)(2 * pair) << PAGE_SHIFT));
+            }
+            const unsigned long long ob = __ballot(open_t);
+            if (lane == 0) s_skip = ob == 0ull;
         }
-        // unconditional meta loads, a group past the open pages reading zeros (nothing LIVE): a load
-        // inside a per-lane branch made the compiler wait for each before the next, and a mask per
-        // group cost the registers of a fifth wave per SIMD; the prio column only on a wide page
-        // (h = i / 4 is uniform: one branch per page)
+        __syncthreads();
+        if (s_skip) break;
+        unsigned long long kmin[TB];
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
-            const int fill = p == a.npages - 1 ? a.tail_fill : PAGE;
-            const bool ok = pg[h] >= 0 && gi * 4 < fill;
-            const uint32_t *src = ok ? a.meta + ((long long)pg[h] << PAGE_SHIFT) : a.zero;
-            mv[i] = reinterpret_cast<const uint4 *>(src)[gi];
-            pv[i] = make_int4(0, 0, 0, 0);
-        }
+        for (int u = 0; u < TB; u++) kmin[u] = ~0ull;
+        {
+            // groups of 4 units: the pair's two pages hold 2 x 1024; thread tid takes g = tid + 256 i
+            uint4 mv[8];
+            int4 pv[8];
+            int pb[2], wide[2], pg[2];
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            if (pg[h] >= 0 && wide[h]) {
-                const long long base = (long long)pg[h] << PAGE_SHIFT;
+            for (int h = 0; h < 2; h++) {
+                const int p = 2 * pair + h;
+                pg[h] = p >= a.npages ? -1 : a.pg0 >= 0 ? a.pg0 + p : a.pages[p];
+                pb[h] = pg[h] >= 0 ? a.pbase[pg[h]] : 0;
+                wide[h] = pg[h] >= 0 ? a.pwide[pg[h]] : 0;
+            }
+            // unconditional meta loads, a group past the open pages reading zeros (nothing LIVE): a load
+            // inside a per-lane branch made the compiler wait for each before the next, and a mask per
+            // group cost the registers of a fifth wave per SIMD; the prio column only on a wide page
+            // (h = i / 4 is uniform: one branch per page)
 #pragma unroll
-                for (int i = 4 * h; i < 4 * h + 4; i++) {
-                    const int gi = (tid + 256 * i) & 1023;
-                    pv[i] = reinterpret_cast<const int4 *>(a.prio + base)[gi];  // masked through mv below
+            for (int i = 0; i < 8; i++) {
+                const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * pair + h;
+                const int fill = p == a.npages - 1 ? a.tail_fill : PAGE;
+                const bool ok = pg[h] >= 0 && gi * 4 < fill;
+                const uint32_t *src = ok ? a.meta + ((long long)pg[h] << PAGE_SHIFT) : a.zero;
+                mv[i] = reinterpret_cast<const uint4 *>(src)[gi];
+                pv[i] = make_int4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                if (pg[h] >= 0 && wide[h]) {
+                    const long long base = (long long)pg[h] << PAGE_SHIFT;
+#pragma unroll
+                    for (int i = 4 * h; i < 4 * h + 4; i++) {
+                        const int gi = (tid + 256 * i) & 1023;
+                        pv[i] = reinterpret_cast<const int4 *>(a.prio + base)[gi];  // masked through mv below
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * pair + h;
+                const uint32_t mm[4] = {mv[i].x, mv[i].y, mv[i].z, mv[i].w};
+                const int pw[4] = {pv[i].x, pv[i].y, pv[i].z, pv[i].w};
+#ifdef ADLBQ_ONE_MEMONLY  // timing diagnostic only (wrong results): the loads without the comparisons
+                kmin[0] ^= (unsigned long long)(mm[0] ^ mm[1] ^ mm[2] ^ mm[3] ^ pw[0]);
+                continue;
+#endif
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int pr = wide[h] ? pw[q] : pb[h] + (int)(mm[q] >> M_OFF_SHIFT);
+                    if ((mm[q] & (M_LIVE | M_PINNED)) != M_LIVE || pr <= LOWEST) continue;
+                    const int t = (int)(mm[q] & M_TYPE);
+                    const unsigned long long key = ((unsigned long long)(~((unsigned int)pr ^ 0x80000000u)) << 32) |
+                                                   ((unsigned long long)(unsigned int)p << PAGE_SHIFT) |
+                                                   (unsigned long long)(gi * 4 + q);
+#pragma unroll
+                    for (int u = 0; u < TB; u++)  // only the types the Reserve names (a uniform test)
+                        if (((want >> u) & 1ull) && t == u) kmin[u] = min(kmin[u], key);
                 }
             }
         }
-
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const int g = tid + 256 * i, h = g >> 10, gi = g & 1023, p = 2 * blockIdx.x + h;
-            const uint32_t mm[4] = {mv[i].x, mv[i].y, mv[i].z, mv[i].w};
-            const int pw[4] = {pv[i].x, pv[i].y, pv[i].z, pv[i].w};
-#ifdef ADLBQ_ONE_MEMONLY  // timing diagnostic only (wrong results): the loads without the comparisons
-            kmin[0] ^= (unsigned long long)(mm[0] ^ mm[1] ^ mm[2] ^ mm[3] ^ pw[0]);
-            continue;
-#endif
+        for (int u = 0; u < TB; u++) {
+            if (!((want >> u) & 1ull)) continue;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int pr = wide[h] ? pw[q] : pb[h] + (int)(mm[q] >> M_OFF_SHIFT);
-                if ((mm[q] & (M_LIVE | M_PINNED)) != M_LIVE || pr <= LOWEST) continue;
-                const int t = (int)(mm[q] & M_TYPE);
-                const unsigned long long key = ((unsigned long long)(~((unsigned int)pr ^ 0x80000000u)) << 32) |
-                                               ((unsigned long long)(unsigned int)p << PAGE_SHIFT) |
-                                               (unsigned long long)(gi * 4 + q);
-#pragma unroll
-                for (int u = 0; u < TB; u++)
-                    if (t == u) kmin[u] = min(kmin[u], key);
-            }
+            for (int o = 32; o > 0; o >>= 1) kmin[u] = min(kmin[u], (unsigned long long)__shfl_xor((long long)kmin[u], o, 64));
+            if (lane == 0) smin[w][u] = kmin[u];
         }
+        __syncthreads();
+        if (tid < TB && ((want >> tid) & 1ull)) {  // the pair's minima into the per-type global ones (agent scope)
+            const unsigned long long m = min(min(smin[0][tid], smin[1][tid]), min(smin[2][tid], smin[3][tid]));
+            if (m != ~0ull) __hip_atomic_fetch_min(gbest + tid, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
     }
-#pragma unroll
-    for (int u = 0; u < TB; u++) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) kmin[u] = min(kmin[u], (unsigned long long)__shfl_xor((long long)kmin[u], o, 64));
-        if (lane == 0) smin[w][u] = kmin[u];
-    }
-    __syncthreads();
-    if (tid < TB) {
-        const unsigned long long m = min(min(smin[0][tid], smin[1][tid]), min(smin[2][tid], smin[3][tid]));
-        __hip_atomic_store(a.part + (long long)blockIdx.x * 8 + tid, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
     if (tid == 0) {  // two-level arrival: eight group counters, then the top one (a.arrive[8])
         // The minima go out as sc1 (agent-scope) stores drained by vmcnt(0) before the arrival, and the
         // last workgroup reads them with sc1 (agent-scope atomic) loads: MI355X_MICROARCH.md's valid
@@ -3666,36 +3711,32 @@ __global__ __launch_bounds__(256, 5) void k_reserve_one(OneArgs a) {  // five wa
 #endif
     // ---- the last workgroup: the request, every workgroup's minima, the choice, its finalize
     prep_block<TB>(a.pa, 0);
-    unsigned long long gm[TB];
-#pragma unroll
-    for (int u = 0; u < TB; u++) gm[u] = ~0ull;
-    // every workgroup's minima, RW rows per thread in flight at once (clamped rows re-read row 0:
-    // a minimum is idempotent); a loop of one row per step waited for each
-    constexpr int RW = TB <= 4 ? 8 : 4;  // rows per thread per step (registers: RW x TB minima)
-    for (int b0 = 0; b0 < (int)gridDim.x; b0 += RW * 256) {
-        unsigned long long x[RW][TB];
-#pragma unroll
-        for (int k = 0; k < RW; k++) {
-            const int b = b0 + tid + 256 * k, bc = b < (int)gridDim.x ? b : 0;
-#pragma unroll
-            for (int u = 0; u < TB; u++)
-                x[k][u] = (unsigned long long)__hip_atomic_load((long long *)(a.part + (long long)bc * 8 + u),
-                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the per-type minima every workgroup folded in (agent-scope atomic loads; every workgroup has
+    // arrived), then reset for the next launch
+    unsigned long long gm = ~0ull;
+    if (tid < TB) {
+        gm = (unsigned long long)__hip_atomic_load((long long *)(gbest + tid), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gbest + tid, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // a wanted type's best unit is its highest available priority: the anchor comes down to it (after
+        // an early stop it is the anchor already), so the next one-Reserve batch can stop early again
+        // instead of reading the whole bucket behind a stale anchor
+        if (((want >> tid) & 1ull) && gm != ~0ull) {
+            const long long pr = (long long)(int)(~(unsigned int)(gm >> 32) ^ 0x80000000u);
+            if (pr < a.f.anchor[tid]) a.f.anchor[tid] = pr;
         }
-#pragma unroll
-        for (int k = 0; k < RW; k++)
-#pragma unroll
-            for (int u = 0; u < TB; u++) gm[u] = min(gm[u], x[k][u]);
     }
-#pragma unroll
-    for (int u = 0; u < TB; u++) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) gm[u] = min(gm[u], (unsigned long long)__shfl_xor((long long)gm[u], o, 64));
+    if (w == 0) {  // every wanted type's best unit at its anchor: the host sizes the next grid for an early stop
+        bool hit = true;
+        if (lane < TB && ((want >> lane) & 1ull)) {
+            const long long an = s_anc[lane];
+            hit = gm != ~0ull && (long long)(int)(~(unsigned int)(gm >> 32) ^ 0x80000000u) == an;
+        }
+        const bool all = __ballot(!hit) == 0ull;
+        if (lane == 0) __hip_atomic_store(&a.f.ctr->one_hit, all ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();  // prep_block's outputs, and smin free again
-    if (lane == 0)
-#pragma unroll
-        for (int u = 0; u < TB; u++) smin[w][u] = gm[u];
+    if (tid < TB) smin[0][tid] = gm, smin[1][tid] = ~0ull, smin[2][tid] = ~0ull, smin[3][tid] = ~0ull;
     __syncthreads();
     const FinArgs &f = a.f;
     if (tid == 0) {
@@ -5483,7 +5524,13 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_end(h, "targeted", ev);
     }
     if (one) {
-        const int grid = (np + 1) / 2;
+        // page pairs, at most 512 workgroups at a time (they step through the pairs in bucket order and
+        // stop once every wanted type's best unit is known: k_reserve_one)
+        int gmax = h->one_grid;
+        if (gmax <= 0) {  // few workgroups when the last one-Reserve batch could stop early, else many
+            gmax = one_hit_hint(h) ? 128 : 512;
+        }
+        const int grid = std::min((np + 1) / 2, gmax);
         if (grid > h->cap_onepart) {
             AQ_HIP(hipStreamSynchronize(s));
             if (h->d_onepart) AQ_HIP(hipFree(h->d_onepart));
@@ -5493,6 +5540,7 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
             const size_t zoff = (size_t)8 * (h->cap_onepart + 2);
             AQ_HIP(hipMalloc((void **)&h->d_onepart, sizeof(unsigned long long) * (zoff + 2048)));
             AQ_HIP(hipMemsetAsync(h->d_onepart, 0, sizeof(unsigned long long) * 16, s));
+            AQ_HIP(hipMemsetAsync(h->d_onepart + 16, 0xff, sizeof(unsigned long long) * 8, s));  // per-type best: none
             AQ_HIP(hipMemsetAsync(h->d_onepart + zoff, 0, sizeof(unsigned long long) * 2048, s));
         }
         DevCounters *const snap = h->d_snap + h->snap_next;

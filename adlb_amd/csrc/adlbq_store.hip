@@ -121,6 +121,11 @@ long long rq_live_upper(adlbq_server *h) {
 }
 
 // Whether the newest landed reserve batch needed a multi-prio-bin sort.
+bool one_hit_hint(adlbq_server *h) {  // the newest landed batch was a one-Reserve batch that could stop early
+    const int i = newest_landed(h);
+    return i >= 0 && h->h_snap[i].one_hit != 0;
+}
+
 bool rank_hint(adlbq_server *h) {  // the newest landed batch ranked its candidates in k_select_open
     const int i = newest_landed(h);
     return i >= 0 && h->h_snap[i].rank_fast != 0;
@@ -2664,6 +2669,11 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
     }
     if (n == "fin_snap_diag") {
         h->fin_snap_diag = value ? 1 : 0;
+        return ADLBQ_OK;
+    }
+    if (n == "one_grid") {
+        if (value < 0 || value > (1 << 20)) return fail(ADLBQ_ERR_ARG, "one_grid must be in [0, 2^20]");
+        h->one_grid = (int)value;
         return ADLBQ_OK;
     }
     if (n == "unres_trust") {

@@ -779,6 +779,38 @@ ONE = {
 }
 
 
+def _one_big(prio_hi, missing):
+    """More page pairs than k_reserve_one's 512 workgroups (4.3M units, 1,050 pages).  prio_hi 2^20: a
+    priority is rare, so once the best unit is taken the anchor is stale and no workgroup may stop
+    early; missing: no unit of the last type (its Reserves never resolve early either)."""
+    w = synth.config2(n_units=4_300_000, n_reserves=60, seed=707 + prio_hi % 97, prio_hi=prio_hi)
+    if missing:
+        w.u_type[w.u_type == w.user_types[-1]] = w.user_types[0]
+    return w
+
+
+ONE_BIG = {"one_big_dense": lambda: _one_big(1024, False), "one_big_sparse": lambda: _one_big(1 << 20, False),
+           "one_big_missing": lambda: _one_big(1024, True)}
+
+
+@pytest.mark.parametrize("name", sorted(ONE_BIG))
+def test_single_reserve_large_bucket_vs_oracle(gpu_available, name):
+    """k_reserve_one stepping its 512 workgroups through 1,050 pages in bucket order, stopping once every
+    wanted type's best unit sits at its anchor's priority before the next pair: single Reserves, nothing
+    returned in between (pins accumulate), equal to the oracle Reserve after Reserve."""
+    w = ONE_BIG[name]()
+    parts = [synth.put_events(w)]
+    for j in range(w.r_rank.size):
+        parts.append(synth.reserve_events(w.r_rank[j:j + 1], w.r_types[j:j + 1], w.r_hang[j:j + 1]))
+        parts.append(synth.simple_events(synth.OP_INFO))
+    tr = np.concatenate(parts)
+    cfg = (w.num_app_ranks, 1, 0)
+    with Server(w.user_types, *cfg, max_units=w.n_units) as s:
+        got = replay.replay(s, tr)
+        assert s.stat("one_batches") == w.r_rank.size
+    assert_same(got, run_oracle(w.user_types, cfg, tr))
+
+
 @pytest.mark.parametrize("engine", ["one", "pipeline"])
 @pytest.mark.parametrize("name", sorted(ONE))
 def test_single_reserve_batches_vs_oracle(gpu_available, name, engine):
