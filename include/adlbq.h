@@ -123,7 +123,12 @@ int adlbq_unreserve_batch_device(adlbq_server *h, int n, const int *d_triples);
 
 /* SS_UNRESERVE (src/adlb.c:2051-2070) of every unit a reserve batch handed
  * out, taken straight from that batch's device-resident reqs18 / resp12 (rows
- * with rc 1): pin_rank = -1, pinned = 0.  Enqueued on the handle's stream. */
+ * with rc 1): pin_rank = -1, pinned = 0.  Enqueued on the handle's stream.
+ * When d_reqs18 / n are the last reserve batch's own and no call has changed
+ * the queue since, each row is checked against that batch's record of what it
+ * gave (slot, wqseqno) and the unit is released without a lookup; the request
+ * rows must then still hold what the batch read (the caller's buffer is not
+ * rewritten in between). */
 int adlbq_unreserve_resp_device(adlbq_server *h, int n, const int *d_reqs18, const int *d_resp12);
 
 /* adlbq_unreserve_resp_device for several handles of one process (distinct,
