@@ -94,7 +94,6 @@ struct DevCounters {
                            // is answered ADLB_ERROR, never indexed past the list)
     int rq_next;           // rqseqnos handed out (next_rqseqno - 1, adlb.c:1244)
     int rq_reclaims;       // k_rq_reclaim compactions (cumulative)
-    int one_hit;           // the last one-Reserve batch found every wanted type's best unit at its anchor
     // the reference's curr_bytes_dmalloced / hwm_bytes_dmalloced (adlb.c:3419-3474) over the
     // structures this handle replaces, plus what the caller adds (adlbq_bytes_adjust)
     long long bytes, bytes_hwm;
@@ -350,8 +349,7 @@ struct adlbq_server {
     int recycle_pages = 1;             // "recycle_pages": 0 = keep every page (the old behaviour)
     int reserve_one = 1;               // "reserve_one": a one-Reserve batch on a large open bucket in one launch
     unsigned long long *d_onepart = nullptr; int cap_onepart = 0; long long one_batches = 0;
-    int one_grid = 0;                  // "one_grid": k_reserve_one's workgroups (0: 128 after a batch that found
-                                       //   its types' best units at their anchors, else 512)
+    int one_grid = 0;                  // "one_grid": k_reserve_one's workgroups at most (0: 256)
     int select_wave = 1;               // "select_wave": pass 2 with one wave per page (T <= 8); 0 = four
     int rq_compact_calls = 0; long long rq_compactions = 0;  // background rq compaction (maybe_compact_rq)
     long long rq_reclaims_launched = 0;  // k_rq_reclaim launches (DevCounters::rq_reclaims counts the landed ones)
@@ -451,7 +449,6 @@ int refresh_counters(adlbq_server *h);     // d_ctr -> ctr (synchronises)
 bool wait_last_snapshot(adlbq_server *h);  // spin until the last batch's snapshot lands (no HIP call)
 void tighten_rq_bound(adlbq_server *h, bool wait_oldest);
 long long rq_live_upper(adlbq_server *h);
-bool one_hit_hint(adlbq_server *h);  // newest landed batch: a one-Reserve batch that could stop early (no sync)
 bool rank_hint(adlbq_server *h);  // newest landed batch ranked in k_select_open (no sync)
 bool plan_hint(adlbq_server *h, int *g, int *lo, int *phi = nullptr);
 inline void wq_changed(adlbq_server *h) {

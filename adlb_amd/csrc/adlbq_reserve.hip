@@ -618,17 +618,17 @@ __device__ __forceinline__ long long cut_of(int th, long long an) {
 // Type t's threshold, by wave 0 of the workgroup whose column of type t
 // arrived last (lane b = bin b): the bin where the demand is reached and how
 // many units of it are needed; the next anchor and guessed cut.
-__device__ void type_threshold(const int t, const int *__restrict__ dem, int *theta, int *need, int *candlen,
-                               int *needsort, int *binoff, const unsigned int *coltot, int *type_cnt,
+// d: the type's demand (prep's atomics), x: lane b's column total (bin b), both from the caller: the
+// totals are the caller's own sums, and the demand was loaded with the tile totals (no second round)
+__device__ void type_threshold(const int t, const int d, const long long x, int *theta, int *need, int *candlen,
+                               int *needsort, int *binoff, int *type_cnt,
                                const long long *__restrict__ anchor, long long *__restrict__ anchor_next,
                                long long *__restrict__ gcut_next, int guess, const long long *__restrict__ gcut,
                                int T) {
     const int lane = threadIdx.x & 63;
-    // the last column of type t: wave 0, lane b = bin b (NB == 64), all totals loaded at once
+    // the last column of type t: wave 0, lane b = bin b (NB == 64)
     static_assert(NB == 64, "one lane per bin");
     if (lane == 0) type_cnt[t] = 0;  // for the next batch
-    const int d = __hip_atomic_load(dem + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // prep's atomics
-    const long long x = __hip_atomic_load(coltot + t * NB + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     long long incl = x;  // inclusive prefix over bins
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -735,6 +735,7 @@ __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn,
     }
     __syncthreads();
     if (!s_last || threadIdx.x >= 64) return;
+    const int d = __hip_atomic_load(dem + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // with the tile totals
     unsigned int tot = 0;
     for (int r0 = 0; r0 < nrt; r0 += 8) {  // eight tiles' loads in flight at a time
         unsigned int y[8];
@@ -749,9 +750,9 @@ __device__ __forceinline__ void thresholds_body(unsigned int *zcs, long long zn,
             tot += y[i];
         }
     }
-    __hip_atomic_store(coltot + c, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    type_threshold(t, dem, theta, need, candlen, needsort, binoff, coltot, type_cnt, anchor, anchor_next, gcut_next,
-                   guess, gcut, T);
+    __hip_atomic_store(coltot + c, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for pass 2 and the export
+    type_threshold(t, d, (long long)tot, theta, need, candlen, needsort, binoff, type_cnt, anchor, anchor_next,
+                   gcut_next, guess, gcut, T);
 }
 
 // The exclusive prefix of seg_cnt per 64 requests (jp[q] = requests before 64 q that may take an
@@ -3544,7 +3545,7 @@ __global__ __launch_bounds__(256) void k_finalize(FinArgs f) {
 // ---------------------------------------------------------------- one Reserve against a large open bucket
 // A batch of one Reserve (T <= 8, no targeted units, an open bucket too large
 // for k_reserve_small) in one launch instead of the seven of the pipeline.
-// At most 512 workgroups step through the bucket's page pairs in bucket order
+// At most 256 workgroups step through the bucket's page pairs in bucket order
 // (256 threads, 32 units each per pair, all loads in flight) and find each
 // type's best available unit by (prio desc, bucket position asc) --
 // wq_find_hi_prio's order (xq.c:190-217), the pipeline's key -- folding each
@@ -3570,7 +3571,7 @@ struct OneArgs {
     const uint32_t *zero;  // 16 KB of zeros: the meta read for a group past the open pages
 };
 template <int TB>
-__global__ __launch_bounds__(256, 2) void k_reserve_one(OneArgs a) {  // at most 512 workgroups: two per CU
+__global__ __launch_bounds__(256, 2) void k_reserve_one(OneArgs a) {  // at most 256 workgroups (one_grid)
     static_assert(TB <= 8, "T <= 8");
     __shared__ unsigned long long smin[4][8];
     __shared__ unsigned long long s_want;
@@ -3725,15 +3726,6 @@ __global__ __launch_bounds__(256, 2) void k_reserve_one(OneArgs a) {  // at most
             const long long pr = (long long)(int)(~(unsigned int)(gm >> 32) ^ 0x80000000u);
             if (pr < a.f.anchor[tid]) a.f.anchor[tid] = pr;
         }
-    }
-    if (w == 0) {  // every wanted type's best unit at its anchor: the host sizes the next grid for an early stop
-        bool hit = true;
-        if (lane < TB && ((want >> lane) & 1ull)) {
-            const long long an = s_anc[lane];
-            hit = gm != ~0ull && (long long)(int)(~(unsigned int)(gm >> 32) ^ 0x80000000u) == an;
-        }
-        const bool all = __ballot(!hit) == 0ull;
-        if (lane == 0) __hip_atomic_store(&a.f.ctr->one_hit, all ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();  // prep_block's outputs, and smin free again
     if (tid < TB) smin[0][tid] = gm, smin[1][tid] = ~0ull, smin[2][tid] = ~0ull, smin[3][tid] = ~0ull;
@@ -5524,13 +5516,10 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         stage_end(h, "targeted", ev);
     }
     if (one) {
-        // page pairs, at most 512 workgroups at a time (they step through the pairs in bucket order and
-        // stop once every wanted type's best unit is known: k_reserve_one)
-        int gmax = h->one_grid;
-        if (gmax <= 0) {  // few workgroups when the last one-Reserve batch could stop early, else many
-            gmax = one_hit_hint(h) ? 128 : 512;
-        }
-        const int grid = std::min((np + 1) / 2, gmax);
+        // page pairs, at most 256 workgroups at a time (they step through the pairs in bucket order and
+        // stop once every wanted type's best unit is known: k_reserve_one); fewer stop sooner on a queue
+        // whose best units sit at the anchors, more read a whole bucket faster (profiles/r06_variants.txt)
+        const int grid = std::min((np + 1) / 2, h->one_grid > 0 ? h->one_grid : 256);
         if (grid > h->cap_onepart) {
             AQ_HIP(hipStreamSynchronize(s));
             if (h->d_onepart) AQ_HIP(hipFree(h->d_onepart));

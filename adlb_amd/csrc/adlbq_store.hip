@@ -121,11 +121,6 @@ long long rq_live_upper(adlbq_server *h) {
 }
 
 // Whether the newest landed reserve batch needed a multi-prio-bin sort.
-bool one_hit_hint(adlbq_server *h) {  // the newest landed batch was a one-Reserve batch that could stop early
-    const int i = newest_landed(h);
-    return i >= 0 && h->h_snap[i].one_hit != 0;
-}
-
 bool rank_hint(adlbq_server *h) {  // the newest landed batch ranked its candidates in k_select_open
     const int i = newest_landed(h);
     return i >= 0 && h->h_snap[i].rank_fast != 0;

@@ -780,7 +780,7 @@ ONE = {
 
 
 def _one_big(prio_hi, missing):
-    """More page pairs than k_reserve_one's 512 workgroups (4.3M units, 1,050 pages).  prio_hi 2^20: a
+    """More page pairs than k_reserve_one's 256 workgroups (4.3M units, 1,050 pages).  prio_hi 2^20: a
     priority is rare, so once the best unit is taken the anchor is stale and no workgroup may stop
     early; missing: no unit of the last type (its Reserves never resolve early either)."""
     w = synth.config2(n_units=4_300_000, n_reserves=60, seed=707 + prio_hi % 97, prio_hi=prio_hi)
@@ -795,7 +795,7 @@ ONE_BIG = {"one_big_dense": lambda: _one_big(1024, False), "one_big_sparse": lam
 
 @pytest.mark.parametrize("name", sorted(ONE_BIG))
 def test_single_reserve_large_bucket_vs_oracle(gpu_available, name):
-    """k_reserve_one stepping its 512 workgroups through 1,050 pages in bucket order, stopping once every
+    """k_reserve_one stepping its 256 workgroups through 1,050 pages in bucket order, stopping once every
     wanted type's best unit sits at its anchor's priority before the next pair: single Reserves, nothing
     returned in between (pins accumulate), equal to the oracle Reserve after Reserve."""
     w = ONE_BIG[name]()
