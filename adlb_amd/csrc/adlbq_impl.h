@@ -350,10 +350,6 @@ struct adlbq_server {
     int reserve_one = 1;               // "reserve_one": a one-Reserve batch on a large open bucket in one launch
     unsigned long long *d_onepart = nullptr; int cap_onepart = 0; long long one_batches = 0;
     int one_grid = 0;                  // "one_grid": k_reserve_one's workgroups at most (0: 256)
-    // the host copy of a one-Reserve batch's request (adlbq_reserve_batch, zero-copy) while it launches:
-    // k_reserve_one then takes the row from its kernel arguments instead of reading mapped host memory
-    const int *one_req_host = nullptr;
-    int one_kernarg = 1;               // "one_kernarg": 0 = k_reserve_one reads the request row from reqs
     int select_wave = 1;               // "select_wave": pass 2 with one wave per page (T <= 8); 0 = four
     int rq_compact_calls = 0; long long rq_compactions = 0;  // background rq compaction (maybe_compact_rq)
     long long rq_reclaims_launched = 0;  // k_rq_reclaim launches (DevCounters::rq_reclaims counts the landed ones)

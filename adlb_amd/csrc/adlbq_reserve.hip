@@ -3569,10 +3569,6 @@ struct OneArgs {
     FinArgs f;
     int inject;  // test only: the choice is told a position past the page list
     const uint32_t *zero;  // 16 KB of zeros: the meta read for a group past the open pages
-    // the request row itself when the host has it (a host-buffer call): no workgroup waits for a read of
-    // mapped host memory before its scan, nor the last one before its prep
-    int has_req;
-    int req[ADLBQ_RESERVE_INTS];
 };
 template <int TB>
 __global__ __launch_bounds__(256, 2) void k_reserve_one(OneArgs a) {  // at most 256 workgroups (one_grid)
@@ -3587,14 +3583,7 @@ __global__ __launch_bounds__(256, 2) void k_reserve_one(OneArgs a) {  // at most
     // wave 0: the Reserve's types (a superset of prep_block's mask: every type whose value a slot
     // names, every type for a -1) and the anchors (upper bounds of the available priorities)
     if (w == 0) {
-        int v = 0;
-        if (a.has_req) {  // uniform: scalar reads of the kernel arguments
-#pragma unroll
-            for (int q = 0; q < NREQ; q++)
-                if (lane == q) v = a.req[2 + q];
-        } else {
-            v = a.pa.reqs[2 + (lane < NREQ ? lane : 0)];
-        }
+        const int v = a.pa.reqs[2 + (lane < NREQ ? lane : 0)];
         const int ut = a.pa.utypes[lane < a.T ? lane : 0];
         const long long an = a.f.anchor[lane < a.T ? lane : 0];
         const bool wild = __ballot(lane < NREQ && v == -1) != 0ull;
@@ -3722,11 +3711,7 @@ __global__ __launch_bounds__(256, 2) void k_reserve_one(OneArgs a) {  // at most
     return;
 #endif
     // ---- the last workgroup: the request, every workgroup's minima, the choice, its finalize
-    {
-        PrepArgs pa = a.pa;
-        if (a.has_req) pa.reqs = a.req;  // the row in the kernel arguments (device memory)
-        prep_block<TB>(pa, 0);
-    }
+    prep_block<TB>(a.pa, 0);
     // the per-type minima every workgroup folded in (agent-scope atomic loads; every workgroup has
     // arrived), then reset for the next launch
     unsigned long long gm = ~0ull;
@@ -5553,14 +5538,10 @@ int launch_reserve(adlbq_server *h, int R, const int *d_reqs, int *d_resp) {
         int pg0 = h->open.pages[0];
         for (int i = 1; i < np && pg0 >= 0; i++)
             if (h->open.pages[(size_t)i] != pg0 + i) pg0 = -1;
-        OneArgs oa{pa, h->d_open_pages, np, h->open.tail_fill, pg0, h->d_prio, h->d_meta, h->d_pbase, h->d_pwide, T,
-                   h->d_onepart + 16, reinterpret_cast<int *>(h->d_onepart), h->d_umatch, h->d_cslot,
-                   fin_args(h, R, d_reqs, d_resp, snap), h->bound_inject,
-                   reinterpret_cast<const uint32_t *>(h->d_onepart + (size_t)8 * (h->cap_onepart + 2)), 0, {}};
-        if (h->one_req_host && h->one_kernarg) {  // adlbq_reserve_batch: the same row it copied to d_reqs
-            oa.has_req = 1;
-            std::memcpy(oa.req, h->one_req_host, sizeof(oa.req));
-        }
+        const OneArgs oa{pa, h->d_open_pages, np, h->open.tail_fill, pg0, h->d_prio, h->d_meta, h->d_pbase, h->d_pwide, T,
+                         h->d_onepart + 16, reinterpret_cast<int *>(h->d_onepart), h->d_umatch, h->d_cslot,
+                         fin_args(h, R, d_reqs, d_resp, snap), h->bound_inject,
+                         reinterpret_cast<const uint32_t *>(h->d_onepart + (size_t)8 * (h->cap_onepart + 2))};
         h->bound_inject = 0;
         stage_begin(h, "one", &ev);
         if (T <= 4) k_reserve_one<4><<<grid, 256, 0, s>>>(oa);
@@ -6009,10 +5990,7 @@ int adlbq_reserve_batch(adlbq_server *h, int n, const int *reqs18, int *resp12) 
         if ((rc = ensure_zc(h, (long long)(ni + no)))) return rc;
         std::memcpy(h->h_zc, reqs18, sizeof(int) * ni);
         const long long one0 = h->one_batches;
-        h->one_req_host = n == 1 ? reqs18 : nullptr;
-        rc = launch_reserve(h, n, h->d_zc, h->d_zc + ni);
-        h->one_req_host = nullptr;
-        if (rc) return rc;
+        if ((rc = launch_reserve(h, n, h->d_zc, h->d_zc + ni))) return rc;
         // k_reserve_one: its one finishing wave stores the response, then the snapshot and last its
         // tag (system-scope release): the landed tag is the batch's end, no stream synchronisation
         if (h->one_batches == one0 || !wait_last_snapshot(h)) {

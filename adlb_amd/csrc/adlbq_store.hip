@@ -2671,10 +2671,6 @@ int adlbq_set_param(adlbq_server *h, const char *name, long long value) {
         h->one_grid = (int)value;
         return ADLBQ_OK;
     }
-    if (n == "one_kernarg") {
-        h->one_kernarg = value ? 1 : 0;
-        return ADLBQ_OK;
-    }
     if (n == "unres_trust") {
         h->unres_trust = value ? 1 : 0;
         return ADLBQ_OK;

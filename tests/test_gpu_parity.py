@@ -811,14 +811,12 @@ def test_single_reserve_large_bucket_vs_oracle(gpu_available, name):
     assert_same(got, run_oracle(w.user_types, cfg, tr))
 
 
-@pytest.mark.parametrize("engine", ["one", "one_rows", "pipeline"])
+@pytest.mark.parametrize("engine", ["one", "pipeline"])
 @pytest.mark.parametrize("name", sorted(ONE))
 def test_single_reserve_batches_vs_oracle(gpu_available, name, engine):
     """Batches of one Reserve on an open bucket larger than the one-workgroup
-    path takes: k_reserve_one (one launch; the request row in its kernel
-    arguments, or with "one_rows" read from the mapped request buffer) and the
-    pipeline all give the oracle's result, Reserve after Reserve (an INFO ends
-    every batch)."""
+    path takes: k_reserve_one (one launch) and the pipeline both give the
+    oracle's result, Reserve after Reserve (an INFO ends every batch)."""
     w = ONE[name]()
     parts = [synth.put_events(w)]
     for j in range(w.r_rank.size):
@@ -829,12 +827,10 @@ def test_single_reserve_batches_vs_oracle(gpu_available, name, engine):
     with Server(w.user_types, *cfg, max_units=w.n_units) as s:
         if engine == "pipeline":
             s.set_param("reserve_one", 0)
-        if engine == "one_rows":
-            s.set_param("one_kernarg", 0)
         got = replay.replay(s, tr)
         used = s.stat("one_batches")
     assert_same(got, run_oracle(w.user_types, cfg, tr))
-    assert (used == w.r_rank.size) == (engine != "pipeline"), used
+    assert (used == w.r_rank.size) == (engine == "one"), used
 
 
 def test_single_reserve_exhaustion_parks_vs_oracle(gpu_available):
