@@ -840,42 +840,46 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
             // Lane t keeps a lower bound for type t: the entries before it holding type t are all
             // taken, so an untargeted Put of type t starts there and moves it past its match.
             if (w == 0 && m <= PM_REG * 64) {
-                // at most 256 entries: lane l holds entries l, l + 64, ... in registers, their taken
-                // bits in four uniform words; a Put is PM_REG ballots, no memory access
+                // at most 256 entries: lane l holds entries l, l + 64, ... in registers and a bit per
+                // entry still free; a Put is PM_REG ballots without a branch (the short-circuit test
+                // and the early exit per ballot had made each Put a chain of exec-mask branches)
                 int erk[PM_REG];
-                unsigned long long emk[PM_REG], taken[PM_REG];
+                unsigned long long emk[PM_REG];
+                unsigned int fr = 0u;  // bit q: entry q * 64 + lane exists and is free
 #pragma unroll
                 for (int q = 0; q < PM_REG; q++) {
                     const int e = q * 64 + lane;
                     erk[q] = e < m ? s_rank[e] : INT_MIN;
                     emk[q] = e < m ? s_mask[e] : 0ull;
-                    taken[q] = __ballot(e < m && erk[q] == INT_MIN);  // taken by an earlier chunk
+                    fr |= (e < m && erk[q] != INT_MIN ? 1u : 0u) << q;  // INT_MIN: taken by an earlier chunk
                 }
                 int pty = 0, ptg = -1, res_l = -1;  // lane l: Put i0 + l's type, target, result
                 int i = 0;
                 for (; i < nc && mlive > 0; i++) {
-                    if ((i & 63) == 0) {
-                        const int il = i + lane;
-                        pty = il < nc ? (r[c0 + il].meta & (int)M_TYPE) : 0;
-                        ptg = il < nc ? r[c0 + il].target : -1;
+                    if ((i & 63) == 0) {  // unconditional loads (clamped), masked after
+                        const int il = i + lane, ilc = il < nc ? il : nc - 1;
+                        const int mt = r[c0 + ilc].meta, tt = r[c0 + ilc].target;
+                        unsigned int in = il < nc ? 1u : 0u;
+                        asm volatile("" : "+v"(in));
+                        pty = in ? (mt & (int)M_TYPE) : 0;
+                        ptg = in ? tt : -1;
                         res_l = -1;
                     }
                     const int t = __builtin_amdgcn_readlane(pty, i & 63);
                     const int tg = __builtin_amdgcn_readlane(ptg, i & 63);
+                    unsigned int cand = 0u;
+#pragma unroll
+                    for (int q = 0; q < PM_REG; q++)
+                        cand |= ((unsigned int)(emk[q] >> t) & (unsigned int)((tg == -1) | (tg == erk[q]))) << q;
+                    cand &= fr;
                     int found = -1;
 #pragma unroll
-                    for (int q = 0; q < PM_REG; q++) {
-                        if (found >= 0) break;
-                        const bool hit = ((emk[q] >> t) & 1ull) && (tg == -1 || tg == erk[q]) &&
-                                         !((taken[q] >> lane) & 1ull) && erk[q] != INT_MIN;
-                        const unsigned long long hb = __ballot(hit);
-                        if (hb) {
-                            const int b = __ffsll((long long)hb) - 1;
-                            found = q * 64 + b;
-                            taken[q] |= 1ull << b;
-                        }
+                    for (int q = PM_REG - 1; q >= 0; q--) {  // the first entry in FIFO order: lowest q, then lane
+                        const unsigned long long hb = __ballot((cand >> q) & 1u);
+                        found = hb ? q * 64 + __ffsll((long long)hb) - 1 : found;
                     }
-                    if (found >= 0) mlive--;
+                    fr &= ~((found >= 0 && lane == (found & 63)) ? (1u << (found >> 6)) : 0u);
+                    mlive -= found >= 0 ? 1 : 0;
                     if ((i & 63) == lane) res_l = found;
                     if ((i & 63) == 63 || i == nc - 1 || mlive == 0) {  // this block of 64 Puts' results
                         const int il = (i & ~63) + lane;
@@ -886,7 +890,7 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
 #pragma unroll
                 for (int q = 0; q < PM_REG; q++) {  // the taken entries, for the later chunks
                     const int e = q * 64 + lane;
-                    if (e < m && ((taken[q] >> lane) & 1ull)) s_rank[e] = INT_MIN;
+                    if (e < m && !((fr >> q) & 1u)) s_rank[e] = INT_MIN;
                 }
             } else if (w == 0) {
                 int tptr = 0;
