@@ -896,10 +896,13 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                 int tptr = 0;
                 int pty = 0, ptg = -1;  // lane l: Put c0 + i0 + l's type and target (64 Puts per load)
                 for (int i = 0; i < nc; i++) {
-                    if ((i & 63) == 0) {
-                        const int il = i + lane;
-                        pty = il < nc ? (r[c0 + il].meta & (int)M_TYPE) : 0;
-                        ptg = il < nc ? r[c0 + il].target : -1;
+                    if ((i & 63) == 0) {  // unconditional loads (clamped), masked after
+                        const int il = i + lane, ilc = il < nc ? il : nc - 1;
+                        const int mt = r[c0 + ilc].meta, tt = r[c0 + ilc].target;
+                        unsigned int in = il < nc ? 1u : 0u;
+                        asm volatile("" : "+v"(in));
+                        pty = in ? (mt & (int)M_TYPE) : 0;
+                        ptg = in ? tt : -1;
                     }
                     int found = -1;
                     if (mlive > 0) {
@@ -910,12 +913,12 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
                         // a targeted Put whose rank has no parked entry: no scan
                         const bool none = tg >= 0 && !s_rbig && (tg >= PM_RBITS || !((s_rbits[tg >> 5] >> (tg & 31)) & 1u));
                         for (int base = none ? m : e0; base < m; base += 64) {
-                            const int e = base + lane;
-                            bool hit = false;
-                            if (e < m) {
-                                const int rk = s_rank[e];
-                                hit = rk != INT_MIN && (s_mask[e] & pb) && (tg == -1 || tg == rk);
-                            }
+                            // both LDS reads unconditional (a clamped entry) and the test without
+                            // short-circuits: no exec-mask branch inside the step
+                            const int e = base + lane, ec = e < m ? e : m - 1;
+                            const int rk = s_rank[ec];
+                            const unsigned long long mk = s_mask[ec];
+                            const bool hit = (e < m) & (rk != INT_MIN) & ((mk & pb) != 0ull) & ((tg == -1) | (tg == rk));
                             const unsigned long long hb = __ballot(hit);
                             if (hb) {
                                 found = base + __ffsll((long long)hb) - 1;
