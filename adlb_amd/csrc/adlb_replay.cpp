@@ -445,10 +445,16 @@ int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *cons
             }
         }
     }
-    // closed loop: the reply each rank holds (its wqseqno; 0: none), written by the thread of the
-    // shard that answered (or the round, under its barrier), read by the thread whose shard holds the unit
-    std::vector<std::atomic<int>> held((size_t)std::max(A, 1));
+    // closed loop: the reply each rank holds (its wqseqno; 0: none) per shard holding the unit, written by
+    // that shard's thread (its Reserve replies and put-side matches) or by the round under its barrier
+    // (a steal: the donor shard), read by the same shard's thread at the Get.  One slot per rank for all
+    // shards let a shard's thread that ran ahead deliver the rank's next reply over the one another
+    // shard's thread had delivered and not yet consumed (the threads meet only at rounds): that Get then
+    // found no reply ("a Get whose reply never arrived")
+    const int AH = std::max(A, 1);
+    std::vector<std::atomic<int>> held((size_t)S * AH);
     for (auto &x : held) x.store(0, std::memory_order_relaxed);
+    const int master = S > 0 ? (int)adlbq_stat(hs[0], "master") : 0;  // world rank of shard 0
     adlbq_steal_group *g = nullptr;
     if (adlbq_steal_group_create(&g, hs, S, k, rqcap)) {
         g_rerr = std::string("adlbq_steal_group_create: ") + adlbq_last_error();
@@ -484,8 +490,9 @@ int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *cons
                         for (int q = 0; q < cnt && ns < steal_cap; q++, ns++) {
                             std::memcpy(steals + 15 * ns, resp.data() + 15 * q, sizeof(int) * 15);
                             const int *row = resp.data() + 15 * q;  // {shard, rqseqno, rank, resp[12]}
-                            if (closed && row[3] == 1 && row[2] >= 0 && row[2] < A)
-                                held[(size_t)row[2]].store(row[3 + 5], std::memory_order_relaxed);
+                            const int donor = row[3 + 6] - master;  // the shard that holds the granted unit
+                            if (closed && row[3] == 1 && row[2] >= 0 && row[2] < A && donor >= 0 && donor < S)
+                                held[(size_t)donor * AH + row[2]].store(row[3 + 5], std::memory_order_relaxed);
                         }
                         if (cnt && ns >= steal_cap) {
                             gerr = "steal output full";
@@ -507,6 +514,7 @@ int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *cons
     auto work = [&](int j) {
         RShard &r = sh[(size_t)j];
         adlbq_server *h = r.h;
+        std::atomic<int> *const held_j = held.data() + (size_t)j * AH;  // the replies for units this shard holds
         bool ok = true;
         double prof[8] = {0};
         using clk = std::chrono::steady_clock;
@@ -528,14 +536,14 @@ int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *cons
                 const auto w0 = clk::now();
                 for (int e = 0; e < c.n && ok; e++) {
                     const int rank = c.x[3 * e], want = c.x[3 * e + 1];  // the recorded {op, rank, wqseqno}
-                    while (held[(size_t)rank].load(std::memory_order_relaxed) == 0 && r.cursor < ci) {
+                    while (held_j[rank].load(std::memory_order_relaxed) == 0 && r.cursor < ci) {
                         const RCall &d = r.calls[r.cursor++];
                         if (d.op == OP_RESERVE) {
                             for (int q = 0; q < d.n; q++) {
                                 const int *o = r.hout + d.dout + (long long)q * ADLBQ_RESP_INTS;
                                 if (__atomic_load_n(o, __ATOMIC_ACQUIRE) == INT_MIN) waited = true;
                                 if (landed(o) == 1)  // TA_RESERVE_RESP success: the rank holds [5]
-                                    held[(size_t)r.hin[(size_t)(d.in + (long long)q * ADLBQ_RESERVE_INTS)]].store(
+                                    held_j[r.hin[(size_t)(d.in + (long long)q * ADLBQ_RESERVE_INTS)]].store(
                                         landed(o + 5), std::memory_order_relaxed);
                             }
                         } else if (d.op == OP_PUT) {
@@ -543,11 +551,11 @@ int adlbsrv_replay_rounds2(adlbq_server **hs, int S, int ntypes, const int *cons
                                 const int *o = r.hout + d.dout + 3ll * q;
                                 if (__atomic_load_n(o + 1, __ATOMIC_ACQUIRE) == INT_MIN) waited = true;
                                 const int mr = landed(o + 1);  // a parked Reserve matched: its rank holds [0]
-                                if (mr >= 0 && mr < A) held[(size_t)mr].store(landed(o), std::memory_order_relaxed);
+                                if (mr >= 0 && mr < A) held_j[mr].store(landed(o), std::memory_order_relaxed);
                             }
                         }
                     }
-                    const int got = held[(size_t)rank].exchange(0, std::memory_order_relaxed);
+                    const int got = held_j[rank].exchange(0, std::memory_order_relaxed);
                     if (got == 0) {
                         r.err = "closed loop: a Get whose reply never arrived (rank " + std::to_string(rank) + ")";
                         ok = false;

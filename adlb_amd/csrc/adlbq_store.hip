@@ -760,6 +760,18 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
     for (int q = tid; q < PM_RBITS / 32; q += PM_THREADS) s_rbits[q] = 0u;
     if (tid == 0) s_tot = 0, s_rbig = 0;
     __syncthreads();
+    // T <= 8: the user types in registers, a type equal to an earlier one never matching (get_type_idx
+    // returns the first declared match): a slot's lookup is eight compares instead of a walk over LDS
+    int ur[8];
+    bool uok[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) ur[t] = s_ut[t < T ? t : 0];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        uok[t] = t < T;
+#pragma unroll
+        for (int t2 = 0; t2 < t; t2++) uok[t] = uok[t] && ur[t2] != ur[t];
+    }
     // stage the live entries in FIFO order (compaction in chunks of 1024)
     for (int c0 = head; c0 < nrq; c0 += PM_THREADS) {
         const int k = c0 + tid;
@@ -782,15 +794,25 @@ __global__ __launch_bounds__(PM_THREADS) void k_put_match_blk(const PutRec *__re
             }
             unsigned long long m = 0;
             bool wild = false;
+            if (T <= 8) {
 #pragma unroll
-            for (int q = 0; q < NREQ; q++) {
-                const int v = tv[q];
-                wild |= v == -1;
-                for (int t = 0; t < T; t++)
-                    if (s_ut[t] == v) {  // get_type_idx: first declared match
-                        m |= 1ull << t;
-                        break;
-                    }
+                for (int q = 0; q < NREQ; q++) {
+                    const int v = tv[q];
+                    wild |= v == -1;
+#pragma unroll
+                    for (int t = 0; t < 8; t++) m |= (uok[t] && v == ur[t]) ? (1ull << t) : 0ull;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < NREQ; q++) {
+                    const int v = tv[q];
+                    wild |= v == -1;
+                    for (int t = 0; t < T; t++)
+                        if (s_ut[t] == v) {  // get_type_idx: first declared match
+                            m |= 1ull << t;
+                            break;
+                        }
+                }
             }
             const int rk = rq_rank[k];
             s_rank[pos] = rk;
@@ -2713,7 +2735,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
     hipSetDevice(h->device);
     std::string n(name);
     // host-side section timers need no device counters: no launch, no synchronisation
-    const bool host_only = n.rfind("hacc:", 0) == 0 || n.rfind("host_ns:", 0) == 0;
+    const bool host_only = n.rfind("hacc:", 0) == 0 || n.rfind("host_ns:", 0) == 0 || n == "master";
     if (!host_only && refresh_counters(h)) return -1;
     if (n.rfind("kst_", 0) == 0 && h->d_kst && h->n_kst > 0) {
         // diagnostic: "kst_{hist,sel}_{1,2,3}" = median over workgroups of (stamp K - stamp 0) in ns,
@@ -2810,6 +2832,7 @@ long long adlbq_stat(adlbq_server *h, const char *name) {
         std::sort(d.begin(), d.end());
         return mx ? d.back() : d[d.size() / 2];
     }
+    if (n == "master") return h->master;  // world rank of the first server (adlb.c:256)
     if (n == "parked") return h->ctr.n_parked_last;
     if (n == "one_batches") return h->one_batches;  // one-Reserve batches through k_reserve_one
     if (n == "rq_cap") return h->rq_cap;  // rq slots allocated

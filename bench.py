@@ -642,11 +642,15 @@ def bench_config5(args, torch, dist, world, rank, local, dev):
     el = sec
     # closed loop: every Get waits for the reply it depends on and takes its wqseqno from it
     cl = {}
-    run(warm, closed=True)
-    got_c, steals_c, sec_c, _, _ = run(d, closed=True, cl_stats=cl)
-    same_c, same_steals_c = parity(got_c, steals_c)
-    ok_c = same_c and same_steals_c and cl.get("wqseqno_mismatch", 1) == 0
-    el_c = sec_c
+    try:
+        run(warm, closed=True)
+        got_c, steals_c, sec_c, _, _ = run(d, closed=True, cl_stats=cl)
+        same_c, same_steals_c = parity(got_c, steals_c)
+        ok_c = same_c and same_steals_c and cl.get("wqseqno_mismatch", 1) == 0
+        el_c = sec_c
+    except RuntimeError as e:  # reported in the line (value null, parity false), not a lost bench line
+        cl["error"] = str(e)
+        ok_c, el_c = False, 0.0
     if world > 1:
         el_c, _ = shards.reduce_step_timing(el_c, total)
         ok_c = all_ranks_true(ok_c)

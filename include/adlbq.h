@@ -373,7 +373,8 @@ long long adlbq_last_scan_units(adlbq_server *h);
  * passes that gave up, cumulative; they cost time only), "parked" (Reserves parked), "candidates",
  * "sort_timeouts" (waits of the rank pass for an in-launch sort that gave up,
  * cumulative; 0 unless something is broken), "device_sorted_lists" (candidate
- * lists long enough for a device-wide radix sort of their own, cumulative).
+ * lists long enough for a device-wide radix sort of their own, cumulative),
+ * "master" (the world rank of the first server, adlb.c:256; no device access).
  * -1 if unknown. */
 long long adlbq_stat(adlbq_server *h, const char *name);
 /* Tuning: "chain_passes" = passes of the ordered choice's first launch (1..8;
